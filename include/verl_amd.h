@@ -1,0 +1,216 @@
+/*
+ * verl_amd.h — C-ABI of the MI355X-native PPO/GRPO actor-update hot path.
+ *
+ * One shared library (verl_amd/lib/libverl_amd.so, built for gfx950 by hipcc) exports the
+ * functions below. Signatures use plain pointers, sizes and a hipStream_t passed as void*;
+ * no torch types cross this boundary. Every entry point:
+ *   - borrows caller-owned device buffers (row-major, contiguous along the last dim unless a
+ *     stride argument says otherwise);
+ *   - launches asynchronously on `stream` and never synchronises the host;
+ *   - performs no allocation (scratch space is a caller-provided `workspace`; its byte size is
+ *     given by the matching *_workspace_bytes() query), so it is safe under hipGraph capture;
+ *   - returns 0 on success, or a negative VA_E* code with a message readable through
+ *     va_last_error() (thread-local).
+ *
+ * Which reference interface each entry point replaces is cited as file:line of rfahrn/verl
+ * (verl 0.4.1.dev). The Python mirror of that interface lives in verl_amd/ (same module
+ * names, function names, argument meaning and error texts) and binds this header via ctypes
+ * (verl_amd/_lib.py); INTEGRATION.md shows the binding a maintainer of the reference adds.
+ */
+#ifndef VERL_AMD_H
+#define VERL_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VA_ABI_VERSION 1
+
+/* error codes */
+#define VA_OK 0
+#define VA_E_ARG -1    /* invalid size / pointer / enum */
+#define VA_E_ALIGN -2  /* a pointer does not meet the stated alignment */
+#define VA_E_LAUNCH -3 /* hipLaunch / hip runtime error */
+
+/* element dtype codes (logits) */
+#define VA_F32 0
+#define VA_BF16 1
+#define VA_F16 2
+
+/* mask dtype codes (response_mask / attention_mask slices) */
+#define VA_MASK_F32 0
+#define VA_MASK_I64 1
+#define VA_MASK_I32 2
+#define VA_MASK_U8 3 /* torch.bool */
+
+/* loss_agg_mode (core_algos.py:686-719) */
+#define VA_AGG_TOKEN_MEAN 0
+#define VA_AGG_SEQ_MEAN_TOKEN_SUM 1
+#define VA_AGG_SEQ_MEAN_TOKEN_MEAN 2
+#define VA_AGG_SEQ_MEAN_TOKEN_SUM_NORM 3
+
+/* kl_penalty type (core_algos.py:1034-1069); "full" has no code: NotImplementedError on host */
+#define VA_KL_NONE (-1)
+#define VA_KL_K1 0  /* "kl", "k1" */
+#define VA_KL_ABS 1 /* "abs" */
+#define VA_KL_K2 2  /* "mse", "k2" */
+#define VA_KL_K3 3  /* "low_var_kl", "k3" */
+
+/* outcome-advantage estimators sharing the per-group kernel (core_algos.py:245-476) */
+#define VA_ADV_GRPO 0      /* (s - mean) / (std + eps)              core_algos.py:246-308 */
+#define VA_ADV_GRPO_NOSTD 1 /* s - mean (Dr.GRPO)                   core_algos.py:304-305 */
+#define VA_ADV_RLOO 2      /* s*n/(n-1) - mean*n/(n-1)              core_algos.py:428-476 */
+#define VA_ADV_MEAN_ONLY 3 /* s - mean, first half of RF++-baseline core_algos.py:376-424 */
+
+/* scalar slots of the fused policy-loss output vector out[VA_LOSS_NOUT] */
+#define VA_LOSS_PG 0            /* pg_loss                 core_algos.py:791-792 */
+#define VA_LOSS_CLIPFRAC 1      /* pg_clipfrac             core_algos.py:783 */
+#define VA_LOSS_PPO_KL 2        /* ppo_kl                  core_algos.py:770 */
+#define VA_LOSS_CLIPFRAC_LOWER 3 /* pg_clipfrac_lower      core_algos.py:787-789 */
+#define VA_LOSS_KL 4            /* agg_loss(kl_penalty)    dp_actor.py:456-459 */
+#define VA_LOSS_ENTROPY 5       /* agg_loss(entropy)       dp_actor.py:446 */
+#define VA_LOSS_NTOKENS 6       /* sum(response_mask)      (diagnostic) */
+#define VA_LOSS_NROWS 7         /* batch rows              (diagnostic) */
+#define VA_LOSS_NOUT 8
+
+int va_abi_version(void);
+const char *va_last_error(void);
+/* number of compute units / name of the device the library is bound to (diagnostics). */
+int va_device_info(int *num_cu, int *arch_major, int *arch_minor);
+
+/* ---------------------------------------------------------------------------------------
+ * Per-token log-prob + entropy over the vocab, fused in one HBM pass.
+ * Replaces: verl/utils/torch_functional.py:64-100 (logprobs_from_logits, flash-attn
+ * cross_entropy_loss path), :116-133 (logprobs_from_logits_v2), :145-149
+ * (entropy_from_logits), and the temperature division dp_actor.py:182 (logits.div_(T)),
+ * applied on load with the reference's rounding (bf16 -> bf16(x / T)).
+ *   logits  [n_rows, row_stride] of `dtype`, first `vocab` columns used
+ *   labels  [n_rows] int64; label == -100 gives logp = 0 (flash-attn ignore_index);
+ *           any other label outside [0, vocab) gives NaN
+ *   logp, lse [n_rows] fp32 (required); entropy [n_rows] fp32 (may be NULL)
+ * ------------------------------------------------------------------------------------ */
+int va_logprob_entropy_fwd(const void *logits, int dtype, int64_t n_rows, int64_t vocab,
+                           int64_t row_stride, const int64_t *labels, float temperature,
+                           float *logp, float *entropy, float *lse, void *stream);
+
+/* Backward of the above w.r.t. the raw (pre-temperature) logits:
+ *   dz = g_logp*(onehot - p) - g_entropy*p*(log p + H);   dlogits = dz / T
+ * (experimental/torch_functional.py:55-67; flash-attn in-place CE backward).
+ * g_logp / g_entropy may be NULL (zero). dlogits may alias logits (in-place backward,
+ * torch_functional.py:64 inplace_backward=True); it has `dtype` and its own row stride. */
+int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const void *logits,
+                           int dtype, int64_t n_rows, int64_t vocab, int64_t row_stride,
+                           const int64_t *labels, const float *lse, const float *entropy,
+                           float temperature, void *dlogits, int64_t dlogits_row_stride,
+                           void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Fused vanilla PPO clipped policy loss + optional KL-loss + optional entropy term, with
+ * loss aggregation and the three metrics, over one [B, R] micro-batch.
+ * Replaces: core_algos.py:722-794 (compute_policy_loss), :686-719 (agg_loss),
+ * :1034-1069 (kl_penalty) as called at dp_actor.py:421-461.
+ *   old_lp, lp, adv [B,R] fp32; mask [B,R] of `mask_dtype`;
+ *   ref_lp [B,R] fp32 or NULL (kl_type must then be VA_KL_NONE);
+ *   entropy [B,R] fp32 or NULL.
+ *   clip_lo = 1 - clip_ratio_low, clip_hi = 1 + clip_ratio_high (rounded to fp32 on host, as
+ *   torch.clamp casts its scalar bounds), clip_c = clip_ratio_c (> 1, asserted on host).
+ *   out[VA_LOSS_NOUT] fp32 (device). workspace: va_ppo_loss_workspace_bytes(B).
+ * The workspace holds per-row partial sums that the backward reads: keep it alive between
+ * the forward and the backward of the same micro-batch. */
+int64_t va_ppo_loss_workspace_bytes(int64_t B);
+int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float *adv, const void *mask,
+                    int mask_dtype, const float *ref_lp, const float *entropy, int64_t B,
+                    int64_t R, float clip_lo, float clip_hi, float clip_c, int agg_mode,
+                    int kl_type, float *out, void *workspace, void *stream);
+
+/* Backward: g_out[VA_LOSS_NOUT] is d(loss)/d(out) as a device vector (only slots PG, KL,
+ * ENTROPY are read; may be NULL = zeros). Writes d_lp [B,R] and, if non-NULL, d_entropy.
+ * Tie and boundary gradients follow torch autograd of the reference expression:
+ * maximum/minimum split ties 1/2-1/2, clamp passes inclusive of its bounds. */
+int va_ppo_loss_bwd(const float *g_out, const float *old_lp, const float *lp, const float *adv,
+                    const void *mask, int mask_dtype, const float *ref_lp, int64_t B, int64_t R,
+                    float clip_lo, float clip_hi, float clip_c, int agg_mode, int kl_type,
+                    const void *workspace, float *d_lp, float *d_entropy, void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Elementwise KL estimators (core_algos.py:1034-1069), n elements.
+ *   fwd: kld = f(lp, ref).  bwd: d_lp = g * df/dlp, d_ref = g * df/dref (either may be NULL).
+ * ------------------------------------------------------------------------------------ */
+int va_kl_penalty_fwd(const float *lp, const float *ref, int64_t n, int kl_type, float *kld,
+                      void *stream);
+int va_kl_penalty_bwd(const float *g, const float *lp, const float *ref, int64_t n, int kl_type,
+                      float *d_lp, float *d_ref, void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Masked aggregation of a [B, R] fp32 matrix (agg_loss core_algos.py:686-719; masked_mean /
+ * masked_sum torch_functional.py:163-185).
+ *   mode = VA_AGG_*, or VA_REDUCE_MASKED_SUM (4): sum(where(m, x, 0) * m),
+ *   or VA_REDUCE_ROW_MASKED_MEAN (5): out[b] = masked_mean over row b (axis=-1).
+ *   out: 1 float (modes 0-4) or B floats (mode 5).  workspace: va_agg_workspace_bytes(B).
+ * Backward: dx[b,t] = g * weight(b,t), read from the same workspace. */
+#define VA_REDUCE_MASKED_SUM 4
+#define VA_REDUCE_ROW_MASKED_MEAN 5
+int64_t va_agg_workspace_bytes(int64_t B);
+int va_masked_agg_fwd(const float *x, const void *mask, int mask_dtype, int64_t B, int64_t R,
+                      int mode, float *out, void *workspace, void *stream);
+int va_masked_agg_bwd(const float *g, const void *mask, int mask_dtype, int64_t B, int64_t R,
+                      int mode, const void *workspace, float *dx, void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Outcome advantages over prompt groups (GRPO and relatives), one launch.
+ * Replaces: core_algos.py:246-308 (compute_grpo_outcome_advantage) and the group-mean part of
+ * :376-476 (RF++-baseline, RLOO). Groups are given in CSR form built on host from the uid
+ * array (np.unique(return_inverse) + stable argsort; the host-side grouping of
+ * core_algos.py:290-291): rows of group g are order[offsets[g] .. offsets[g+1]).
+ *   score[b] = sum_t rewards[b,t] (unmasked, core_algos.py:282)
+ *   adv[b,t] = a(b) * mask[b,t]; also writes scores[B] fp32 if non-NULL.
+ * Singleton group: mean 0, std 1 (core_algos.py:293-295). ------------------------------ */
+int va_outcome_advantage(const float *rewards, const void *mask, int mask_dtype, int64_t B,
+                         int64_t R, const int32_t *order, const int32_t *offsets,
+                         int64_t n_groups, int64_t max_group_size, float epsilon, int estimator,
+                         float *adv, float *scores, void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * GAE (core_algos.py:193-241): masked reverse recurrence per row as an LDS-staged chunked
+ * affine scan, then the batch-global masked whitening (torch_functional.py:188-223).
+ *   rewards, values [B,R] fp32, mask [B,R] -> adv [B,R] (whitened), ret [B,R] (= raw + values)
+ *   row_stats: workspace (va_gae_workspace_bytes(B)).
+ *   stats_out[4] fp32 (device): {mean, rsqrt(var + 1e-8), mask_sum, error_flag}
+ *   error_flag = 1 when mask_sum == 0, 2 when mask_sum == 1 (the ValueErrors of
+ *   torch_functional.py:195-200, raised by the host wrapper).
+ * For data-parallel whitening the three phases are exported separately:
+ *   va_gae_scan        -> adv_raw, ret, row partials (n, sum, M2) in fp64
+ *   va_whiten_finalize -> merges K partial triples in index order (Chan), emits the merged
+ *                         fp64 triple and the fp32 stats (call it again on all-gathered triples)
+ *   va_whiten_apply    -> x = (x - mean) * rstd [* mask] in place.
+ * ------------------------------------------------------------------------------------ */
+int64_t va_gae_workspace_bytes(int64_t B);
+int va_gae_scan(const float *rewards, const float *values, const void *mask, int mask_dtype,
+                int64_t B, int64_t R, float gamma, float lam, float *adv_raw, float *ret,
+                double *row_partials, void *stream);
+int va_masked_row_partials(const float *x, const void *mask, int mask_dtype, int64_t B,
+                           int64_t R, double *row_partials, void *stream);
+int va_whiten_finalize(const double *partials, int64_t K, double *merged, float *stats_out,
+                       void *stream);
+int va_whiten_apply(float *x, const float *stats, const void *mask, int mask_dtype, int64_t B,
+                    int64_t R, int post_multiply_mask, void *stream);
+int va_gae_advantage_return(const float *rewards, const float *values, const void *mask,
+                            int mask_dtype, int64_t B, int64_t R, float gamma, float lam,
+                            float *adv, float *ret, float *stats_out, void *workspace,
+                            void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * In-reward KL penalty (ray_trainer.py:153-193 apply_kl_penalty):
+ *   kld = kl_penalty(old, ref) * mask; rewards = scores - beta * kld;
+ *   row_kl[b] = masked_mean(kld[b], mask[b]) (the per-sequence current_kl before the batch mean)
+ * ------------------------------------------------------------------------------------ */
+int va_apply_kl_penalty(const float *scores, const float *old_lp, const float *ref_lp,
+                        const void *mask, int mask_dtype, int64_t B, int64_t R, int kl_type,
+                        float beta, float *rewards, float *row_kl, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VERL_AMD_H */

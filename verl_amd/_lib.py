@@ -1,0 +1,114 @@
+"""ctypes binding of the C-ABI in ``include/verl_amd.h`` (libverl_amd.so).
+
+This is the only place that loads the native library. The product path has no CPU fallback:
+if the library is missing or a tensor is not on a HIP device, the call raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from ctypes import POINTER, c_double, c_float, c_int, c_int64, c_void_p
+from pathlib import Path
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("VERL_AMD_LIB", _PKG / "lib" / "libverl_amd.so"))
+HEADER_PATH = _PKG.parent / "include" / "verl_amd.h"
+
+# constants mirrored from include/verl_amd.h
+VA_F32, VA_BF16, VA_F16 = 0, 1, 2
+VA_MASK_F32, VA_MASK_I64, VA_MASK_I32, VA_MASK_U8 = 0, 1, 2, 3
+VA_AGG_TOKEN_MEAN, VA_AGG_SEQ_MEAN_TOKEN_SUM, VA_AGG_SEQ_MEAN_TOKEN_MEAN, VA_AGG_SEQ_MEAN_TOKEN_SUM_NORM = 0, 1, 2, 3
+VA_REDUCE_MASKED_SUM, VA_REDUCE_ROW_MASKED_MEAN = 4, 5
+VA_KL_NONE, VA_KL_K1, VA_KL_ABS, VA_KL_K2, VA_KL_K3 = -1, 0, 1, 2, 3
+VA_ADV_GRPO, VA_ADV_GRPO_NOSTD, VA_ADV_RLOO, VA_ADV_MEAN_ONLY = 0, 1, 2, 3
+VA_LOSS_PG, VA_LOSS_CLIPFRAC, VA_LOSS_PPO_KL, VA_LOSS_CLIPFRAC_LOWER = 0, 1, 2, 3
+VA_LOSS_KL, VA_LOSS_ENTROPY, VA_LOSS_NTOKENS, VA_LOSS_NROWS, VA_LOSS_NOUT = 4, 5, 6, 7, 8
+
+_P = c_void_p
+_SIGNATURES: dict[str, tuple] = {
+    "va_abi_version": (c_int, []),
+    "va_last_error": (ctypes.c_char_p, []),
+    "va_device_info": (c_int, [POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
+    "va_logprob_entropy_fwd": (c_int, [_P, c_int, c_int64, c_int64, c_int64, _P, c_float, _P, _P, _P, _P]),
+    "va_logprob_entropy_bwd": (
+        c_int,
+        [_P, _P, _P, c_int, c_int64, c_int64, c_int64, _P, _P, _P, c_float, _P, c_int64, _P],
+    ),
+    "va_ppo_loss_workspace_bytes": (c_int64, [c_int64]),
+    "va_ppo_loss_fwd": (
+        c_int,
+        [_P, _P, _P, _P, c_int, _P, _P, c_int64, c_int64, c_float, c_float, c_float, c_int, c_int, _P, _P, _P],
+    ),
+    "va_ppo_loss_bwd": (
+        c_int,
+        [_P, _P, _P, _P, _P, c_int, _P, c_int64, c_int64, c_float, c_float, c_float, c_int, c_int, _P, _P, _P, _P],
+    ),
+    "va_kl_penalty_fwd": (c_int, [_P, _P, c_int64, c_int, _P, _P]),
+    "va_kl_penalty_bwd": (c_int, [_P, _P, _P, c_int64, c_int, _P, _P, _P]),
+    "va_agg_workspace_bytes": (c_int64, [c_int64]),
+    "va_masked_agg_fwd": (c_int, [_P, _P, c_int, c_int64, c_int64, c_int, _P, _P, _P]),
+    "va_masked_agg_bwd": (c_int, [_P, _P, c_int, c_int64, c_int64, c_int, _P, _P, _P]),
+    "va_outcome_advantage": (
+        c_int,
+        [_P, _P, c_int, c_int64, c_int64, _P, _P, c_int64, c_int64, c_float, c_int, _P, _P, _P],
+    ),
+    "va_gae_workspace_bytes": (c_int64, [c_int64]),
+    "va_gae_scan": (c_int, [_P, _P, _P, c_int, c_int64, c_int64, c_float, c_float, _P, _P, _P, _P]),
+    "va_masked_row_partials": (c_int, [_P, _P, c_int, c_int64, c_int64, _P, _P]),
+    "va_whiten_finalize": (c_int, [_P, c_int64, _P, _P, _P]),
+    "va_whiten_apply": (c_int, [_P, _P, _P, c_int, c_int64, c_int64, c_int, _P]),
+    "va_gae_advantage_return": (
+        c_int,
+        [_P, _P, _P, c_int, c_int64, c_int64, c_float, c_float, _P, _P, _P, _P, _P],
+    ),
+    "va_apply_kl_penalty": (c_int, [_P, _P, _P, _P, c_int, c_int64, c_int64, c_int, c_float, _P, _P, _P]),
+}
+
+_lib = None
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def header_symbols() -> list[str]:
+    """Every function the public header declares (used by the ABI tests)."""
+    text = HEADER_PATH.read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char \*)\s*(va_\w+)\s*\(", text, re.M)))
+
+
+def load():
+    """Load libverl_amd.so once and attach the argument types. Raises when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise NativeLibraryError(
+            f"{LIB_PATH} is missing: build the MI355X kernels first "
+            "(python -m verl_amd.build, or __graft_entry__.build())"
+        )
+    lib = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.va_abi_version() != 1:
+        raise NativeLibraryError(f"ABI version mismatch: {lib.va_abi_version()} != 1")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = _lib.va_last_error().decode(errors="replace") if _lib is not None else "?"
+        raise RuntimeError(f"verl_amd native call {what} failed ({rc}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    lib = load()
+    check(getattr(lib, name)(*args), name)
+
+
+__all__ = ["load", "call", "check", "header_symbols", "LIB_PATH", "NativeLibraryError", "c_double"]

@@ -1,0 +1,484 @@
+// Advantage estimation kernels: per-group outcome advantages (GRPO family) and GAE with the
+// batch-global masked whitening.
+//
+// Reference semantics (rfahrn/verl):
+//   core_algos.py:246-308  compute_grpo_outcome_advantage (unmasked row-sum score, per-uid
+//                          mean / unbiased std, singleton -> (0, 1), broadcast * mask)
+//   core_algos.py:428-476  RLOO;  :376-424 RF++-baseline (mean-only half)
+//   core_algos.py:193-241  compute_gae_advantage_return (masked reverse recurrence)
+//   torch_functional.py:188-223 masked_var (unbiased; ValueError at mask sum 0/1),
+//                          masked_whiten: (x - mean) * rsqrt(var + 1e-8)
+//
+// GRPO: one workgroup per prompt group. Its 4 waves reduce the group's rewards rows (one
+// wave per row, 16-byte loads) into scores held in LDS, wave 0 forms mean / unbiased std in
+// fp64 in member order, and the waves write the advantage rows (a * mask). One launch, the
+// rewards are read once.
+//
+// GAE: one wave per response row, a 256-thread workgroup carries 4 rows. The row's rewards,
+// values and mask are staged into LDS (coalesced), each lane owns a contiguous chunk of
+// L = ceil(R / 64) steps and composes the chunk's affine map on the state (g, nextvalue);
+// a wave-level reverse scan of the 64 maps gives each chunk its incoming state; the lane then
+// re-runs its chunk in the reference's exact op order, writing g (raw advantage) and returns.
+// The same pass emits per-row (count, sum, M2) in fp64 for the whitening, merged afterwards
+// in fixed row order (Chan), so results do not depend on scheduling.
+
+#include <math.h>
+
+#include "va_common.h"
+
+namespace va {
+namespace {
+
+constexpr int kPartStride = 3;  // (n, sum, M2) per row, fp64
+
+// ---------------------------------------------------------------- outcome advantages
+template <int MT, int EST>
+__global__ __launch_bounds__(256) void outcome_adv_kernel(
+    const float *__restrict__ rewards, const void *__restrict__ mask, int64_t R,
+    const int32_t *__restrict__ order, const int32_t *__restrict__ offsets, float eps,
+    float *__restrict__ adv, float *__restrict__ scores_out) {
+  extern __shared__ float s_score[];  // [group size] + 2 floats of broadcast stats
+  const int g = blockIdx.x;
+  const int beg = offsets[g];
+  const int n = offsets[g + 1] - beg;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  float *s_stat = s_score + n;
+
+  // 1) scores: unmasked row sums (core_algos.py:282), fp32 like the reference
+  const bool vec = (R % 4 == 0);
+  for (int k = wave; k < n; k += nw) {
+    const int64_t row = order[beg + k];
+    const float *r = rewards + row * R;
+    float acc = 0.f;
+    if (vec) {
+      const float4 *r4 = reinterpret_cast<const float4 *>(r);
+      for (int64_t j = lane; j < R / 4; j += kWave) {
+        const float4 q = r4[j];
+        acc += (q.x + q.y) + (q.z + q.w);
+      }
+    } else {
+      for (int64_t j = lane; j < R; j += kWave) acc += r[j];
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) {
+      s_score[k] = acc;
+      if (scores_out) scores_out[row] = acc;
+    }
+  }
+  __syncthreads();
+
+  // 2) group statistics in member order, fp64, rounded to fp32 as torch.mean / torch.std
+  if (threadIdx.x == 0) {
+    float mean32, std32;
+    if (n == 1) {
+      mean32 = 0.f;  // core_algos.py:293-295
+      std32 = 1.f;
+    } else {
+      double sum = 0.0;
+      for (int k = 0; k < n; ++k) sum += s_score[k];
+      const double mean = sum / n;
+      double m2 = 0.0;
+      for (int k = 0; k < n; ++k) {
+        const double d = s_score[k] - mean;
+        m2 += d * d;
+      }
+      mean32 = static_cast<float>(mean);
+      std32 = static_cast<float>(sqrt(m2 / (n - 1)));
+    }
+    s_stat[0] = mean32;
+    s_stat[1] = std32;
+  }
+  __syncthreads();
+  const float mean = s_stat[0], stdv = s_stat[1];
+
+  // 3) advantage rows: a * mask (core_algos.py:302-306)
+  for (int k = wave; k < n; k += nw) {
+    const int64_t row = order[beg + k];
+    const float s = s_score[k];
+    float a;
+    if constexpr (EST == VA_ADV_GRPO) {
+      a = (s - mean) / (stdv + eps);
+    } else if constexpr (EST == VA_ADV_GRPO_NOSTD || EST == VA_ADV_MEAN_ONLY) {
+      a = s - mean;
+    } else {  // RLOO, core_algos.py:469-473
+      if (n > 1) {
+        const float nn = static_cast<float>(n), nm1 = static_cast<float>(n - 1);
+        a = (s * nn) / nm1 - (mean * nn) / nm1;
+      } else {
+        a = s;
+      }
+    }
+    float *o = adv + row * R;
+    for (int64_t j = lane; j < R; j += kWave) o[j] = a * load_mask<MT>(mask, row * R + j);
+  }
+}
+
+// ---------------------------------------------------------------- GAE chunked scan
+// Affine map on (g, nv):  g' = a*g + c*nv + b1 ;  nv' = e*nv + b2   (lower-left entry 0)
+struct Aff {
+  float a, c, e, b1, b2;
+};
+// compose: apply `second` after `first`
+__device__ __forceinline__ Aff compose(const Aff &second, const Aff &first) {
+  Aff r;
+  r.a = second.a * first.a;
+  r.c = second.a * first.c + second.c * first.e;
+  r.e = second.e * first.e;
+  r.b1 = second.a * first.b1 + second.c * first.b2 + second.b1;
+  r.b2 = second.e * first.b2 + second.b2;
+  return r;
+}
+
+template <int MT, bool LDS>
+__global__ __launch_bounds__(256) void gae_scan_kernel(
+    const float *__restrict__ rew, const float *__restrict__ val, const void *__restrict__ mask,
+    int64_t B, int64_t R, int L, float gamma, float gl, float *__restrict__ adv_raw,
+    float *__restrict__ ret, double *__restrict__ part) {
+  extern __shared__ float lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + wave;
+  if (row >= B) return;  // waves are independent: no workgroup barrier below
+  const int64_t base = row * R;
+  // padded LDS image: step t lives at (t / L) * (L + 1) + t % L  (lane-chunk reads conflict-free)
+  const int P = 64 * (L + 1);
+  float *sr = lds + static_cast<int64_t>(wave) * 3 * P;
+  float *sv = sr + P;
+  float *sm = sv + P;
+  auto pidx = [L](int64_t t) -> int { return static_cast<int>((t / L) * (L + 1) + t % L); };
+
+  if constexpr (LDS) {
+    for (int64_t t = lane; t < R; t += kWave) {
+      const int p = pidx(t);
+      sr[p] = rew[base + t];
+      sv[p] = val[base + t];
+      sm[p] = load_mask<MT>(mask, base + t);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  auto R_ = [&](int64_t t) -> float { return LDS ? sr[pidx(t)] : rew[base + t]; };
+  auto V_ = [&](int64_t t) -> float { return LDS ? sv[pidx(t)] : val[base + t]; };
+  auto M_ = [&](int64_t t) -> float { return LDS ? sm[pidx(t)] : load_mask<MT>(mask, base + t); };
+
+  const int64_t t0 = static_cast<int64_t>(lane) * L;
+  const int64_t t1 = (t0 + L < R) ? t0 + L : R;
+
+  // 1) compose the chunk's map, processing steps from t1-1 down to t0
+  Aff F{1.f, 0.f, 1.f, 0.f, 0.f};
+  for (int64_t t = t1 - 1; t >= t0; --t) {
+    const float m = M_(t), r = R_(t), v = V_(t);
+    Aff s;
+    s.a = m * gl + (1.f - m);
+    s.c = m * gamma;
+    s.e = 1.f - m;
+    s.b1 = m * (r - v);
+    s.b2 = m * v;
+    F = compose(s, F);
+  }
+  // 2) reverse inclusive scan over lanes: lane k holds G_k o G_{k+1} o ... o G_63
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    Aff nb;
+    nb.a = __shfl_down(F.a, o, kWave);
+    nb.c = __shfl_down(F.c, o, kWave);
+    nb.e = __shfl_down(F.e, o, kWave);
+    nb.b1 = __shfl_down(F.b1, o, kWave);
+    nb.b2 = __shfl_down(F.b2, o, kWave);
+    if (lane + o < 64) F = compose(F, nb);
+  }
+  // incoming state of chunk k = state after chunks 63..k+1 applied to (0, 0)
+  float g = __shfl_down(F.b1, 1, kWave);
+  float nv = __shfl_down(F.b2, 1, kWave);
+  if (lane == 63) {
+    g = 0.f;
+    nv = 0.f;
+  }
+  // 3) re-run the chunk in the reference op order (core_algos.py:229-236)
+  for (int64_t t = t1 - 1; t >= t0; --t) {
+    const float m = M_(t), r = R_(t), v = V_(t);
+    const float delta = (r + gamma * nv) - v;
+    const float gnew = delta + gl * g;
+    nv = v * m + (1.f - m) * nv;
+    g = gnew * m + (1.f - m) * g;
+    if constexpr (LDS) {
+      sr[pidx(t)] = g;  // reuse the rewards slot for g
+    } else {
+      adv_raw[base + t] = g;
+      ret[base + t] = g + v;
+    }
+  }
+  if constexpr (LDS) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // 4) coalesced stores + row partials (n, sum, M2) of g over the mask
+  double n = 0.0, s = 0.0;
+  for (int64_t t = lane; t < R; t += kWave) {
+    float gv, m, v;
+    if constexpr (LDS) {
+      const int p = pidx(t);
+      gv = sr[p];
+      v = sv[p];
+      m = sm[p];
+      adv_raw[base + t] = gv;
+      ret[base + t] = gv + v;
+    } else {
+      gv = adv_raw[base + t];
+      m = load_mask<MT>(mask, base + t);
+    }
+    n += m;
+    s += static_cast<double>((m != 0.f ? gv : 0.f) * m);
+  }
+  n = wave_sum(n);
+  s = wave_sum(s);
+  const double mu = n > 0.0 ? s / n : 0.0;
+  double m2 = 0.0;
+  for (int64_t t = lane; t < R; t += kWave) {
+    float gv, m;
+    if constexpr (LDS) {
+      const int p = pidx(t);
+      gv = sr[p];
+      m = sm[p];
+    } else {
+      gv = adv_raw[base + t];
+      m = load_mask<MT>(mask, base + t);
+    }
+    if (m != 0.f) {
+      const double d = static_cast<double>(gv) - mu;
+      m2 += static_cast<double>(m) * d * d;
+    }
+  }
+  m2 = wave_sum(m2);
+  if (lane == 0) {
+    part[row * kPartStride + 0] = n;
+    part[row * kPartStride + 1] = s;
+    part[row * kPartStride + 2] = m2;
+  }
+}
+
+// Per-row (n, sum, M2) of an arbitrary [B, R] matrix (masked_whiten on non-GAE inputs).
+template <int MT>
+__global__ __launch_bounds__(256) void row_partials_kernel(const float *__restrict__ x,
+                                                           const void *__restrict__ mask,
+                                                           int64_t B, int64_t R,
+                                                           double *__restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const int64_t base = row * R;
+  double n = 0.0, s = 0.0;
+  for (int64_t t = lane; t < R; t += kWave) {
+    const float m = load_mask<MT>(mask, base + t);
+    n += m;
+    s += static_cast<double>((m != 0.f ? x[base + t] : 0.f) * m);
+  }
+  n = wave_sum(n);
+  s = wave_sum(s);
+  const double mu = n > 0.0 ? s / n : 0.0;
+  double m2 = 0.0;
+  for (int64_t t = lane; t < R; t += kWave) {
+    const float m = load_mask<MT>(mask, base + t);
+    if (m != 0.f) {
+      const double d = static_cast<double>(x[base + t]) - mu;
+      m2 += static_cast<double>(m) * d * d;
+    }
+  }
+  m2 = wave_sum(m2);
+  if (lane == 0) {
+    part[row * kPartStride + 0] = n;
+    part[row * kPartStride + 1] = s;
+    part[row * kPartStride + 2] = m2;
+  }
+}
+
+// Merge K (n, sum, M2) triples in index order; emit the merged triple and the fp32 whitening
+// stats {mean, rsqrt(var + 1e-8), n, error_flag} with the reference's formulas.
+__global__ __launch_bounds__(256) void whiten_finalize_kernel(const double *__restrict__ part,
+                                                              int64_t K, double *__restrict__ merged,
+                                                              float *__restrict__ stats) {
+  __shared__ double sh[256 * 3];
+  Moments acc{0.0, 0.0, 0.0};
+  // contiguous slice per thread keeps the merge order a fixed function of K
+  const int64_t per = (K + blockDim.x - 1) / blockDim.x;
+  const int64_t lo = threadIdx.x * per, hi = (lo + per < K) ? lo + per : K;
+  for (int64_t k = lo; k < hi; ++k) {
+    const double n = part[k * kPartStride + 0];
+    Moments mk{n, n > 0.0 ? part[k * kPartStride + 1] / n : 0.0, part[k * kPartStride + 2]};
+    acc = merge_moments(acc, mk);
+  }
+  sh[threadIdx.x * 3 + 0] = acc.n;
+  sh[threadIdx.x * 3 + 1] = acc.mean;
+  sh[threadIdx.x * 3 + 2] = acc.m2;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Moments tot{0.0, 0.0, 0.0};
+    for (unsigned j = 0; j < blockDim.x; ++j)
+      tot = merge_moments(tot, Moments{sh[j * 3], sh[j * 3 + 1], sh[j * 3 + 2]});
+    const double n = tot.n;
+    merged[0] = n;
+    merged[1] = tot.mean * n;
+    merged[2] = tot.m2;
+    // torch_functional.py:171-185, 188-223
+    const double mean = (tot.mean * n) / (n + 1e-8);
+    const double dm = tot.mean - mean;
+    const double var_b = (tot.m2 + n * dm * dm) / (n + 1e-8);
+    float flag = 0.f;
+    double var = var_b;
+    if (n == 0.0) flag = 1.f;
+    else if (n == 1.0) flag = 2.f;
+    else var = var_b * (n / (n - 1.0));
+    const float var32 = static_cast<float>(var);
+    stats[0] = static_cast<float>(mean);
+    stats[1] = 1.0f / sqrtf(var32 + 1e-8f);
+    stats[2] = static_cast<float>(n);
+    stats[3] = flag;
+  }
+}
+
+template <int MT, bool POSTMASK>
+__global__ __launch_bounds__(256) void whiten_apply_kernel(float *__restrict__ x,
+                                                           const float *__restrict__ stats,
+                                                           const void *__restrict__ mask,
+                                                           int64_t n) {
+  const float mean = stats[0], rstd = stats[1];
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    float v = (x[i] - mean) * rstd;
+    if constexpr (POSTMASK) v = v * load_mask<MT>(mask, i);
+    x[i] = v;
+  }
+}
+
+int gae_lds_bytes(int L, int waves) { return waves * 3 * 64 * (L + 1) * 4; }
+
+}  // namespace
+}  // namespace va
+
+using namespace va;
+
+extern "C" int va_outcome_advantage(const float *rewards, const void *mask, int mask_dtype,
+                                    int64_t B, int64_t R, const int32_t *order,
+                                    const int32_t *offsets, int64_t n_groups,
+                                    int64_t max_group_size, float epsilon, int estimator,
+                                    float *adv, float *scores, void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0 && n_groups > 0 && n_groups <= B, "bad shape (B=%lld G=%lld)",
+               (long long)B, (long long)n_groups);
+  VA_CHECK_ARG(max_group_size > 0 && max_group_size <= 32768, "group size %lld out of range",
+               (long long)max_group_size);
+  VA_CHECK_ARG(rewards && mask && order && offsets && adv, "null pointer argument");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t shm = static_cast<size_t>(max_group_size + 2) * sizeof(float);
+#define VA_LAUNCH_ADV(E)                                                                     \
+  VA_DISPATCH_MASK(mask_dtype, {                                                             \
+    hipLaunchKernelGGL((outcome_adv_kernel<MT, E>), dim3(n_groups), dim3(256), shm, s,        \
+                       rewards, mask, R, order, offsets, epsilon, adv, scores);              \
+  })
+  switch (estimator) {
+    case VA_ADV_GRPO: VA_LAUNCH_ADV(VA_ADV_GRPO); break;
+    case VA_ADV_GRPO_NOSTD: VA_LAUNCH_ADV(VA_ADV_GRPO_NOSTD); break;
+    case VA_ADV_RLOO: VA_LAUNCH_ADV(VA_ADV_RLOO); break;
+    case VA_ADV_MEAN_ONLY: VA_LAUNCH_ADV(VA_ADV_MEAN_ONLY); break;
+    default: set_error("unknown estimator %d", estimator); return VA_E_ARG;
+  }
+#undef VA_LAUNCH_ADV
+  return check_launch("outcome_advantage");
+}
+
+extern "C" int64_t va_gae_workspace_bytes(int64_t B) {
+  return static_cast<int64_t>(sizeof(double)) * (B * kPartStride + 4);
+}
+
+extern "C" int va_gae_scan(const float *rewards, const float *values, const void *mask,
+                           int mask_dtype, int64_t B, int64_t R, float gamma, float lam,
+                           float *adv_raw, float *ret, double *row_partials, void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0, "empty batch");
+  VA_CHECK_ARG(rewards && values && mask && adv_raw && ret && row_partials,
+               "null pointer argument");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int L = static_cast<int>((R + 63) / 64);
+  // gamma * lam is a Python-float product in the reference, applied as an fp32 scalar
+  const float gl = static_cast<float>(static_cast<double>(gamma) * static_cast<double>(lam));
+  int waves = 4;
+  while (waves > 1 && gae_lds_bytes(L, waves) > 160 * 1024) waves >>= 1;
+  const bool use_lds = gae_lds_bytes(L, waves) <= 160 * 1024;
+  const dim3 block(64 * waves);
+  const dim3 grid(static_cast<unsigned>((B + waves - 1) / waves));
+  if (use_lds) {
+    const size_t shm = static_cast<size_t>(gae_lds_bytes(L, waves));
+    VA_DISPATCH_MASK(mask_dtype, {
+      if (hipFuncSetAttribute(reinterpret_cast<const void *>(&gae_scan_kernel<MT, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(shm)) != hipSuccess) {
+        set_error("gae_scan: cannot reserve %zu bytes of LDS", shm);
+        return VA_E_LAUNCH;
+      }
+      hipLaunchKernelGGL((gae_scan_kernel<MT, true>), grid, block, shm, s, rewards, values, mask,
+                         B, R, L, gamma, gl, adv_raw, ret, row_partials);
+    });
+  } else {
+    VA_DISPATCH_MASK(mask_dtype, {
+      hipLaunchKernelGGL((gae_scan_kernel<MT, false>), grid, block, 0, s, rewards, values, mask,
+                         B, R, L, gamma, gl, adv_raw, ret, row_partials);
+    });
+  }
+  return check_launch("gae_scan");
+}
+
+extern "C" int va_masked_row_partials(const float *x, const void *mask, int mask_dtype,
+                                      int64_t B, int64_t R, double *row_partials, void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0, "empty input");
+  VA_CHECK_ARG(x && mask && row_partials, "null pointer argument");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  VA_DISPATCH_MASK(mask_dtype, {
+    hipLaunchKernelGGL((row_partials_kernel<MT>), dim3((B + 3) / 4), dim3(256), 0, s, x, mask,
+                       B, R, row_partials);
+  });
+  return check_launch("masked_row_partials");
+}
+
+extern "C" int va_whiten_finalize(const double *partials, int64_t K, double *merged,
+                                  float *stats_out, void *stream) {
+  VA_CHECK_ARG(K > 0, "K must be > 0");
+  VA_CHECK_ARG(partials && merged && stats_out, "null pointer argument");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(whiten_finalize_kernel, dim3(1), dim3(256), 0, s, partials, K, merged,
+                     stats_out);
+  return check_launch("whiten_finalize");
+}
+
+extern "C" int va_whiten_apply(float *x, const float *stats, const void *mask, int mask_dtype,
+                               int64_t B, int64_t R, int post_multiply_mask, void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0, "empty input");
+  VA_CHECK_ARG(x && stats, "null pointer argument");
+  VA_CHECK_ARG(!post_multiply_mask || mask != nullptr, "mask required for post multiply");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n = B * R;
+  int64_t grid = (n + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  if (post_multiply_mask) {
+    VA_DISPATCH_MASK(mask_dtype, {
+      hipLaunchKernelGGL((whiten_apply_kernel<MT, true>), dim3(grid), dim3(256), 0, s, x, stats,
+                         mask, n);
+    });
+  } else {
+    hipLaunchKernelGGL((whiten_apply_kernel<VA_MASK_F32, false>), dim3(grid), dim3(256), 0, s, x,
+                       stats, nullptr, n);
+  }
+  return check_launch("whiten_apply");
+}
+
+extern "C" int va_gae_advantage_return(const float *rewards, const float *values,
+                                       const void *mask, int mask_dtype, int64_t B, int64_t R,
+                                       float gamma, float lam, float *adv, float *ret,
+                                       float *stats_out, void *workspace, void *stream) {
+  VA_CHECK_ARG(workspace && stats_out, "null pointer argument");
+  double *part = static_cast<double *>(workspace);
+  int e = va_gae_scan(rewards, values, mask, mask_dtype, B, R, gamma, lam, adv, ret, part,
+                      stream);
+  if (e) return e;
+  e = va_whiten_finalize(part, B, part + B * kPartStride, stats_out, stream);
+  if (e) return e;
+  return va_whiten_apply(adv, stats_out, mask, mask_dtype, B, R, 0, stream);
+}

@@ -1,0 +1,536 @@
+// Fused PPO clipped policy loss + KL loss + entropy aggregation, and masked aggregation.
+//
+// Reference semantics (rfahrn/verl):
+//   core_algos.py:722-794  compute_policy_loss (dual-clip PPO), the three metrics
+//   core_algos.py:686-719  agg_loss (token-mean / seq-mean-token-sum / -token-mean / -sum-norm)
+//   core_algos.py:1034-1069 kl_penalty (k1, abs, k2/mse, k3/low_var_kl)
+//   torch_functional.py:163-185 masked_sum / masked_mean
+//   dp_actor.py:421-470   how the actor combines them (pg - c_H*H_loss + c_kl*kl_loss)
+//
+// Forward = two launches per micro-batch: a row kernel (one 256-thread workgroup per response
+// row) that emits per-row partial sums in fp64, and a one-workgroup finalize that applies the
+// aggregation mode and writes the 8-slot output vector. Backward = one elementwise launch
+// that reads the row partials and the upstream gradient scalars from device memory (no host
+// sync anywhere). Tie / boundary gradients follow torch autograd of the reference expression:
+// maximum/minimum give 1/2 to each side on ties, clamp passes gradient inclusive of bounds.
+// Bound: launch latency at micro-batch size (8 x 1024), HBM at large B*R.
+
+#include <math.h>
+
+#include "va_common.h"
+
+namespace va {
+namespace {
+
+constexpr int kNQ = 8;        // fp64 partial slots per row
+constexpr int kTotals = 8;    // fp64 totals slots after the rows
+
+// NaN-propagating maximum / minimum (torch.maximum / torch.minimum semantics).
+__device__ __forceinline__ float tmax(float a, float b) {
+  return (a != a || b != b) ? __builtin_nanf("") : (a > b ? a : b);
+}
+__device__ __forceinline__ float tmin(float a, float b) {
+  return (a != a || b != b) ? __builtin_nanf("") : (a < b ? a : b);
+}
+// torch.clamp(x, lo, hi) forward; NaN passes through
+__device__ __forceinline__ float tclamp(float x, float lo, float hi) {
+  return x != x ? x : (x < lo ? lo : (x > hi ? hi : x));
+}
+__device__ __forceinline__ float pass_incl(float x, float lo, float hi) {
+  return (x >= lo && x <= hi) ? 1.f : 0.f;
+}
+// gradient share of `a` in maximum(a, b)
+__device__ __forceinline__ float gmax_share(float a, float b) {
+  return a > b ? 1.f : (a == b ? 0.5f : 0.f);
+}
+
+// kl_penalty forward, core_algos.py:1046-1063
+template <int KL>
+__device__ __forceinline__ float kl_fwd(float lp, float ref) {
+  if constexpr (KL == VA_KL_K1) {
+    return lp - ref;
+  } else if constexpr (KL == VA_KL_ABS) {
+    return fabsf(lp - ref);
+  } else if constexpr (KL == VA_KL_K2) {
+    const float d = lp - ref;
+    return 0.5f * (d * d);
+  } else if constexpr (KL == VA_KL_K3) {
+    const float kc = tclamp(ref - lp, -20.f, 20.f);
+    const float ratio = expf(kc);
+    const float kld = (ratio - kc) - 1.f;
+    return tclamp(kld, -10.f, 10.f);
+  } else {
+    return 0.f;
+  }
+}
+// d kl / d lp (d kl / d ref is its negative for every estimator)
+template <int KL>
+__device__ __forceinline__ float kl_dlp(float lp, float ref) {
+  if constexpr (KL == VA_KL_K1) {
+    return 1.f;
+  } else if constexpr (KL == VA_KL_ABS) {
+    const float d = lp - ref;
+    return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);  // sgn, torch abs backward
+  } else if constexpr (KL == VA_KL_K2) {
+    return lp - ref;
+  } else if constexpr (KL == VA_KL_K3) {
+    const float k = ref - lp;
+    const float kc = tclamp(k, -20.f, 20.f);
+    const float ratio = expf(kc);
+    const float kld = (ratio - kc) - 1.f;
+    // out = clamp(ratio - kc - 1); d/dkc = ratio - 1; dkc/dk = pass; dk/dlp = -1
+    return -(pass_incl(kld, -10.f, 10.f) * (ratio - 1.f) * pass_incl(k, -20.f, 20.f));
+  } else {
+    return 0.f;
+  }
+}
+
+struct PolicyElem {
+  float pg, clip, negkl, lower;
+};
+
+// compute_policy_loss elementwise part, core_algos.py:766-791 (same op order)
+__device__ __forceinline__ PolicyElem policy_elem(float old, float lp, float A, float lo,
+                                                  float hi, float c) {
+  PolicyElem e;
+  const float dc = tclamp(lp - old, -20.f, 20.f);
+  const float r = expf(dc);
+  const float nA = -A;
+  const float l1 = nA * r;
+  const float l2 = nA * tclamp(r, lo, hi);
+  const float c1 = tmax(l1, l2);
+  const float l3 = nA * c;
+  const float c2 = tmin(l3, c1);
+  e.pg = (A < 0.f) ? c2 : c1;
+  e.clip = (l2 > l1) ? 1.f : 0.f;
+  e.negkl = -dc;
+  e.lower = ((c1 > l3) ? 1.f : 0.f) * ((A < 0.f) ? 1.f : 0.f);
+  return e;
+}
+
+// d pg / d lp for a given upstream gradient w on pg (autograd chain order of the reference)
+__device__ __forceinline__ float policy_dlp(float w, float old, float lp, float A, float lo,
+                                           float hi, float c) {
+  const float d = lp - old;
+  const float dc = tclamp(d, -20.f, 20.f);
+  const float r = expf(dc);
+  const float nA = -A;
+  const float l1 = nA * r;
+  const float l2 = nA * tclamp(r, lo, hi);
+  const float c1 = tmax(l1, l2);
+  const float l3 = nA * c;
+  float g_c1;
+  if (A < 0.f) {
+    // c2 = minimum(l3, c1): share of c1
+    const float share = c1 < l3 ? 1.f : (c1 == l3 ? 0.5f : 0.f);
+    g_c1 = share == 0.5f ? w / 2.f : w * share;
+  } else {
+    g_c1 = w;
+  }
+  const float s1 = gmax_share(l1, l2), s2 = gmax_share(l2, l1);
+  const float g_l1 = s1 == 0.5f ? g_c1 / 2.f : g_c1 * s1;
+  const float g_l2 = s2 == 0.5f ? g_c1 / 2.f : g_c1 * s2;
+  const float g_r = g_l1 * nA + (g_l2 * nA) * pass_incl(r, lo, hi);
+  return (g_r * r) * pass_incl(d, -20.f, 20.f);
+}
+
+// upstream-gradient weight of one element under an aggregation mode (see agg_loss)
+__device__ __forceinline__ float agg_weight(int agg, float g, float m, double n_b, double n_tot,
+                                            int64_t B, int64_t R) {
+  switch (agg) {
+    case VA_AGG_TOKEN_MEAN:
+      return (g / static_cast<float>(n_tot + 1e-8)) * m;
+    case VA_AGG_SEQ_MEAN_TOKEN_SUM:
+      return (g / static_cast<float>(B)) * m;
+    case VA_AGG_SEQ_MEAN_TOKEN_MEAN:
+      return ((g / static_cast<float>(B)) / static_cast<float>(n_b)) * m;
+    default:  // VA_AGG_SEQ_MEAN_TOKEN_SUM_NORM
+      return (g / static_cast<float>(R)) * m;
+  }
+}
+
+// value of an aggregated loss from the row partials in slot q
+__device__ double agg_value(int agg, const double *part, int q, int64_t B, int64_t R,
+                            double n_tot, double *scratch) {
+  double acc[1] = {0.0};
+  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
+    const double s = part[b * kNQ + q];
+    if (agg == VA_AGG_SEQ_MEAN_TOKEN_MEAN) acc[0] += s / part[b * kNQ + 0];
+    else acc[0] += s;
+  }
+  block_sum<1>(acc, scratch);
+  switch (agg) {
+    case VA_AGG_TOKEN_MEAN: return acc[0] / (n_tot + 1e-8);
+    case VA_AGG_SEQ_MEAN_TOKEN_SUM: return acc[0] / static_cast<double>(B);
+    case VA_AGG_SEQ_MEAN_TOKEN_MEAN: return acc[0] / static_cast<double>(B);
+    default: return acc[0] / static_cast<double>(R);
+  }
+}
+
+// ------------------------------------------------------------------ policy loss forward
+template <int MT, int KL>
+__global__ __launch_bounds__(256) void ppo_loss_rows_kernel(
+    const float *__restrict__ old_lp, const float *__restrict__ lp, const float *__restrict__ adv,
+    const void *__restrict__ mask, const float *__restrict__ ref, const float *__restrict__ ent,
+    int64_t R, float lo, float hi, float c, int agg, double *__restrict__ part) {
+  __shared__ double scratch[4 * 7];
+  const int64_t b = blockIdx.x;
+  const int64_t base = b * R;
+  const bool tok = (agg == VA_AGG_TOKEN_MEAN);
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};
+  for (int64_t t = threadIdx.x; t < R; t += blockDim.x) {
+    const int64_t i = base + t;
+    const float m = load_mask<MT>(mask, i);
+    const bool mb = (m != 0.f);
+    const PolicyElem e = policy_elem(old_lp[i], lp[i], adv[i], lo, hi, c);
+    v[0] += m;
+    // masked_sum: where(mask.bool(), x, 0) * mask ; seq modes: x * mask
+    v[1] += tok ? (mb ? e.pg : 0.f) * m : e.pg * m;
+    v[2] += (mb ? e.clip : 0.f) * m;
+    v[3] += (mb ? e.negkl : 0.f) * m;
+    v[4] += (mb ? e.lower : 0.f) * m;
+    if constexpr (KL != VA_KL_NONE) {
+      const float k = kl_fwd<KL>(lp[i], ref[i]);
+      v[5] += tok ? (mb ? k : 0.f) * m : k * m;
+    }
+    if (ent != nullptr) {
+      const float h = ent[i];
+      v[6] += tok ? (mb ? h : 0.f) * m : h * m;
+    }
+  }
+  block_sum<7>(v, scratch);
+  if (threadIdx.x < 7) part[b * kNQ + threadIdx.x] = v[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void ppo_loss_finalize_kernel(const double *__restrict__ part,
+                                                                int64_t B, int64_t R, int agg,
+                                                                int has_kl, int has_ent,
+                                                                double *__restrict__ totals,
+                                                                float *__restrict__ out) {
+  __shared__ double scratch[4 * 5];
+  double v[5] = {0, 0, 0, 0, 0};  // n, clip, negkl, lower, (unused)
+  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
+    v[0] += part[b * kNQ + 0];
+    v[1] += part[b * kNQ + 2];
+    v[2] += part[b * kNQ + 3];
+    v[3] += part[b * kNQ + 4];
+  }
+  block_sum<5>(v, scratch);
+  const double n = v[0];
+  const double pg = agg_value(agg, part, 1, B, R, n, scratch);
+  const double kl = has_kl ? agg_value(agg, part, 5, B, R, n, scratch) : 0.0;
+  const double en = has_ent ? agg_value(agg, part, 6, B, R, n, scratch) : 0.0;
+  if (threadIdx.x == 0) {
+    const double den = n + 1e-8;
+    out[VA_LOSS_PG] = static_cast<float>(pg);
+    out[VA_LOSS_CLIPFRAC] = static_cast<float>(v[1] / den);
+    out[VA_LOSS_PPO_KL] = static_cast<float>(v[2] / den);
+    out[VA_LOSS_CLIPFRAC_LOWER] = static_cast<float>(v[3] / den);
+    out[VA_LOSS_KL] = static_cast<float>(kl);
+    out[VA_LOSS_ENTROPY] = static_cast<float>(en);
+    out[VA_LOSS_NTOKENS] = static_cast<float>(n);
+    out[VA_LOSS_NROWS] = static_cast<float>(B);
+    totals[0] = n;
+  }
+}
+
+// ------------------------------------------------------------------ policy loss backward
+template <int MT, int KL>
+__global__ __launch_bounds__(256) void ppo_loss_bwd_kernel(
+    const float *__restrict__ g_out, const float *__restrict__ old_lp,
+    const float *__restrict__ lp, const float *__restrict__ adv, const void *__restrict__ mask,
+    const float *__restrict__ ref, int64_t B, int64_t R, float lo, float hi, float c, int agg,
+    const double *__restrict__ part, float *__restrict__ d_lp, float *__restrict__ d_ent) {
+  const int64_t b = blockIdx.y;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= R) return;
+  const int64_t i = b * R + t;
+  const float g_pg = g_out ? g_out[VA_LOSS_PG] : 0.f;
+  const float g_kl = g_out ? g_out[VA_LOSS_KL] : 0.f;
+  const float g_en = g_out ? g_out[VA_LOSS_ENTROPY] : 0.f;
+  const double n_b = part[b * kNQ + 0];
+  const double n_tot = part[B * kNQ + 0];
+  const float m = load_mask<MT>(mask, i);
+  const bool mb = (m != 0.f);
+  const bool tok = (agg == VA_AGG_TOKEN_MEAN);
+  // token-mean routes through where(mask.bool(), x, 0): zero where mask == 0
+  const float keep = (!tok || mb) ? 1.f : 0.f;
+  const float w_pg = agg_weight(agg, g_pg, m, n_b, n_tot, B, R) * keep;
+  const float x_lp = lp[i];
+  float g = policy_dlp(w_pg, old_lp[i], x_lp, adv[i], lo, hi, c);
+  if constexpr (KL != VA_KL_NONE) {
+    const float w_kl = agg_weight(agg, g_kl, m, n_b, n_tot, B, R) * keep;
+    g += w_kl * kl_dlp<KL>(x_lp, ref[i]);
+  }
+  d_lp[i] = g;
+  if (d_ent != nullptr) d_ent[i] = agg_weight(agg, g_en, m, n_b, n_tot, B, R) * keep;
+}
+
+// ------------------------------------------------------------------ masked aggregation
+template <int MT>
+__global__ __launch_bounds__(256) void masked_rows_kernel(const float *__restrict__ x,
+                                                          const void *__restrict__ mask,
+                                                          int64_t R, int agg,
+                                                          double *__restrict__ part) {
+  __shared__ double scratch[4 * 3];
+  const int64_t b = blockIdx.x;
+  double v[3] = {0, 0, 0};  // n, where-sum, mul-sum
+  for (int64_t t = threadIdx.x; t < R; t += blockDim.x) {
+    const int64_t i = b * R + t;
+    const float m = load_mask<MT>(mask, i);
+    const float xv = x[i];
+    v[0] += m;
+    v[1] += (m != 0.f ? xv : 0.f) * m;
+    v[2] += xv * m;
+  }
+  block_sum<3>(v, scratch);
+  if (threadIdx.x == 0) {
+    part[b * kNQ + 0] = v[0];
+    // slot 1 carries the sum the mode aggregates: where-form for token-mean/masked_sum/row mean
+    const bool where_form = (agg == VA_AGG_TOKEN_MEAN || agg == VA_REDUCE_MASKED_SUM ||
+                             agg == VA_REDUCE_ROW_MASKED_MEAN);
+    part[b * kNQ + 1] = where_form ? v[1] : v[2];
+  }
+}
+
+__global__ __launch_bounds__(256) void masked_agg_finalize_kernel(const double *__restrict__ part,
+                                                                  int64_t B, int64_t R, int agg,
+                                                                  double *__restrict__ totals,
+                                                                  float *__restrict__ out) {
+  __shared__ double scratch[4 * 2];
+  if (agg == VA_REDUCE_ROW_MASKED_MEAN) {
+    for (int64_t b = threadIdx.x; b < B; b += blockDim.x)
+      out[b] = static_cast<float>(part[b * kNQ + 1] / (part[b * kNQ + 0] + 1e-8));
+    return;
+  }
+  double v[2] = {0, 0};
+  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
+    v[0] += part[b * kNQ + 0];
+    v[1] += part[b * kNQ + 1];
+  }
+  block_sum<2>(v, scratch);
+  double r;
+  if (agg == VA_REDUCE_MASKED_SUM) r = v[1];
+  else r = agg_value(agg, part, 1, B, R, v[0], scratch);
+  if (threadIdx.x == 0) {
+    out[0] = static_cast<float>(r);
+    totals[0] = v[0];
+  }
+}
+
+template <int MT>
+__global__ __launch_bounds__(256) void masked_agg_bwd_kernel(const float *__restrict__ g,
+                                                             const void *__restrict__ mask,
+                                                             int64_t B, int64_t R, int agg,
+                                                             const double *__restrict__ part,
+                                                             float *__restrict__ dx) {
+  const int64_t b = blockIdx.y;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= R) return;
+  const int64_t i = b * R + t;
+  const float m = load_mask<MT>(mask, i);
+  const bool mb = (m != 0.f);
+  float d;
+  if (agg == VA_REDUCE_ROW_MASKED_MEAN) {
+    d = (g[b] / static_cast<float>(part[b * kNQ + 0] + 1e-8)) * m * (mb ? 1.f : 0.f);
+  } else if (agg == VA_REDUCE_MASKED_SUM) {
+    d = g[0] * m * (mb ? 1.f : 0.f);
+  } else {
+    const float keep = (agg != VA_AGG_TOKEN_MEAN || mb) ? 1.f : 0.f;
+    d = agg_weight(agg, g[0], m, part[b * kNQ + 0], part[B * kNQ + 0], B, R) * keep;
+  }
+  dx[i] = d;
+}
+
+// ------------------------------------------------------------------ elementwise KL
+template <int KL>
+__global__ __launch_bounds__(256) void kl_fwd_kernel(const float *__restrict__ lp,
+                                                     const float *__restrict__ ref, int64_t n,
+                                                     float *__restrict__ out) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    out[i] = kl_fwd<KL>(lp[i], ref[i]);
+}
+template <int KL>
+__global__ __launch_bounds__(256) void kl_bwd_kernel(const float *__restrict__ g,
+                                                     const float *__restrict__ lp,
+                                                     const float *__restrict__ ref, int64_t n,
+                                                     float *__restrict__ d_lp,
+                                                     float *__restrict__ d_ref) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const float d = g[i] * kl_dlp<KL>(lp[i], ref[i]);
+    if (d_lp) d_lp[i] = d;
+    if (d_ref) d_ref[i] = -d;
+  }
+}
+
+template <int KL, int MT>
+__global__ __launch_bounds__(256) void apply_kl_penalty_kernel(
+    const float *__restrict__ scores, const float *__restrict__ old_lp,
+    const float *__restrict__ ref, const void *__restrict__ mask, int64_t R, float beta,
+    float *__restrict__ rewards, float *__restrict__ row_kl) {
+  __shared__ double scratch[4 * 2];
+  const int64_t b = blockIdx.x;
+  double v[2] = {0, 0};
+  for (int64_t t = threadIdx.x; t < R; t += blockDim.x) {
+    const int64_t i = b * R + t;
+    const float m = load_mask<MT>(mask, i);
+    const float kld = kl_fwd<KL>(old_lp[i], ref[i]) * m;  // ray_trainer.py:174-177
+    rewards[i] = scores[i] - beta * kld;                  // :180
+    v[0] += m;
+    v[1] += (m != 0.f ? kld : 0.f) * m;  // masked_mean(kld, mask, axis=-1) :182
+  }
+  block_sum<2>(v, scratch);
+  if (threadIdx.x == 0) row_kl[b] = static_cast<float>(v[1] / (v[0] + 1e-8));
+}
+
+int64_t grid_1d(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  return g > 8192 ? 8192 : (g < 1 ? 1 : g);
+}
+
+}  // namespace
+}  // namespace va
+
+using namespace va;
+
+#define VA_DISPATCH_KL(kt, ...)                                                  \
+  switch (kt) {                                                                  \
+    case VA_KL_NONE: { constexpr int KL = VA_KL_NONE; __VA_ARGS__; break; }       \
+    case VA_KL_K1: { constexpr int KL = VA_KL_K1; __VA_ARGS__; break; }           \
+    case VA_KL_ABS: { constexpr int KL = VA_KL_ABS; __VA_ARGS__; break; }         \
+    case VA_KL_K2: { constexpr int KL = VA_KL_K2; __VA_ARGS__; break; }           \
+    case VA_KL_K3: { constexpr int KL = VA_KL_K3; __VA_ARGS__; break; }           \
+    default: set_error("unknown kl type %d", (int)(kt)); return VA_E_ARG;         \
+  }
+
+extern "C" int64_t va_ppo_loss_workspace_bytes(int64_t B) {
+  return static_cast<int64_t>(sizeof(double)) * (B * kNQ + kTotals);
+}
+extern "C" int64_t va_agg_workspace_bytes(int64_t B) { return va_ppo_loss_workspace_bytes(B); }
+
+static int check_agg(int agg, bool allow_reduce) {
+  const int hi = allow_reduce ? VA_REDUCE_ROW_MASKED_MEAN : VA_AGG_SEQ_MEAN_TOKEN_SUM_NORM;
+  VA_CHECK_ARG(agg >= 0 && agg <= hi, "Invalid loss_agg_mode code: %d", agg);
+  return VA_OK;
+}
+
+extern "C" int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float *adv,
+                               const void *mask, int mask_dtype, const float *ref_lp,
+                               const float *entropy, int64_t B, int64_t R, float clip_lo,
+                               float clip_hi, float clip_c, int agg_mode, int kl_type,
+                               float *out, void *workspace, void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0, "empty batch (B=%lld, R=%lld)", (long long)B, (long long)R);
+  VA_CHECK_ARG(B < (1ll << 31), "B too large");
+  VA_CHECK_ARG(old_lp && lp && adv && mask && out && workspace, "null pointer argument");
+  VA_CHECK_ARG(kl_type == VA_KL_NONE || ref_lp != nullptr, "ref_lp required for kl_type %d",
+               kl_type);
+  if (int e = check_agg(agg_mode, false)) return e;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  double *part = static_cast<double *>(workspace);
+  VA_DISPATCH_MASK(mask_dtype, VA_DISPATCH_KL(kl_type, {
+    hipLaunchKernelGGL((ppo_loss_rows_kernel<MT, KL>), dim3(B), dim3(256), 0, s, old_lp, lp,
+                       adv, mask, ref_lp, entropy, R, clip_lo, clip_hi, clip_c, agg_mode, part);
+  }));
+  hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, B, R, agg_mode,
+                     kl_type != VA_KL_NONE ? 1 : 0, entropy != nullptr ? 1 : 0, part + B * kNQ,
+                     out);
+  return check_launch("ppo_loss_fwd");
+}
+
+extern "C" int va_ppo_loss_bwd(const float *g_out, const float *old_lp, const float *lp,
+                               const float *adv, const void *mask, int mask_dtype,
+                               const float *ref_lp, int64_t B, int64_t R, float clip_lo,
+                               float clip_hi, float clip_c, int agg_mode, int kl_type,
+                               const void *workspace, float *d_lp, float *d_entropy,
+                               void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0, "empty batch");
+  VA_CHECK_ARG(B < 65536, "B must be < 65536 for the 2-D backward grid");
+  VA_CHECK_ARG(old_lp && lp && adv && mask && workspace && d_lp, "null pointer argument");
+  VA_CHECK_ARG(kl_type == VA_KL_NONE || ref_lp != nullptr, "ref_lp required");
+  if (int e = check_agg(agg_mode, false)) return e;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const double *part = static_cast<const double *>(workspace);
+  const dim3 grid(static_cast<unsigned>((R + 255) / 256), static_cast<unsigned>(B));
+  VA_DISPATCH_MASK(mask_dtype, VA_DISPATCH_KL(kl_type, {
+    hipLaunchKernelGGL((ppo_loss_bwd_kernel<MT, KL>), grid, dim3(256), 0, s, g_out, old_lp, lp,
+                       adv, mask, ref_lp, B, R, clip_lo, clip_hi, clip_c, agg_mode, part, d_lp,
+                       d_entropy);
+  }));
+  return check_launch("ppo_loss_bwd");
+}
+
+extern "C" int va_masked_agg_fwd(const float *x, const void *mask, int mask_dtype, int64_t B,
+                                 int64_t R, int mode, float *out, void *workspace,
+                                 void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0, "empty input");
+  VA_CHECK_ARG(x && mask && out && workspace, "null pointer argument");
+  if (int e = check_agg(mode, true)) return e;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  double *part = static_cast<double *>(workspace);
+  VA_DISPATCH_MASK(mask_dtype, {
+    hipLaunchKernelGGL((masked_rows_kernel<MT>), dim3(B), dim3(256), 0, s, x, mask, R, mode,
+                       part);
+  });
+  hipLaunchKernelGGL(masked_agg_finalize_kernel, dim3(1), dim3(256), 0, s, part, B, R, mode,
+                     part + B * kNQ, out);
+  return check_launch("masked_agg_fwd");
+}
+
+extern "C" int va_masked_agg_bwd(const float *g, const void *mask, int mask_dtype, int64_t B,
+                                 int64_t R, int mode, const void *workspace, float *dx,
+                                 void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0 && B < 65536, "bad shape");
+  VA_CHECK_ARG(g && mask && workspace && dx, "null pointer argument");
+  if (int e = check_agg(mode, true)) return e;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<unsigned>((R + 255) / 256), static_cast<unsigned>(B));
+  VA_DISPATCH_MASK(mask_dtype, {
+    hipLaunchKernelGGL((masked_agg_bwd_kernel<MT>), grid, dim3(256), 0, s, g, mask, B, R, mode,
+                       static_cast<const double *>(workspace), dx);
+  });
+  return check_launch("masked_agg_bwd");
+}
+
+extern "C" int va_kl_penalty_fwd(const float *lp, const float *ref, int64_t n, int kl_type,
+                                 float *kld, void *stream) {
+  VA_CHECK_ARG(n >= 0, "n < 0");
+  if (n == 0) return VA_OK;
+  VA_CHECK_ARG(lp && ref && kld, "null pointer argument");
+  VA_CHECK_ARG(kl_type != VA_KL_NONE, "kl_type NONE has no forward");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  VA_DISPATCH_KL(kl_type, {
+    hipLaunchKernelGGL((kl_fwd_kernel<KL>), dim3(grid_1d(n)), dim3(256), 0, s, lp, ref, n, kld);
+  });
+  return check_launch("kl_penalty_fwd");
+}
+
+extern "C" int va_kl_penalty_bwd(const float *g, const float *lp, const float *ref, int64_t n,
+                                 int kl_type, float *d_lp, float *d_ref, void *stream) {
+  VA_CHECK_ARG(n >= 0, "n < 0");
+  if (n == 0) return VA_OK;
+  VA_CHECK_ARG(g && lp && ref, "null pointer argument");
+  VA_CHECK_ARG(kl_type != VA_KL_NONE, "kl_type NONE has no backward");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  VA_DISPATCH_KL(kl_type, {
+    hipLaunchKernelGGL((kl_bwd_kernel<KL>), dim3(grid_1d(n)), dim3(256), 0, s, g, lp, ref, n,
+                       d_lp, d_ref);
+  });
+  return check_launch("kl_penalty_bwd");
+}
+
+extern "C" int va_apply_kl_penalty(const float *scores, const float *old_lp, const float *ref_lp,
+                                   const void *mask, int mask_dtype, int64_t B, int64_t R,
+                                   int kl_type, float beta, float *rewards, float *row_kl,
+                                   void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0, "empty batch");
+  VA_CHECK_ARG(scores && old_lp && ref_lp && mask && rewards && row_kl, "null pointer argument");
+  VA_CHECK_ARG(kl_type != VA_KL_NONE, "kl_type NONE");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  VA_DISPATCH_MASK(mask_dtype, VA_DISPATCH_KL(kl_type, {
+    hipLaunchKernelGGL((apply_kl_penalty_kernel<KL, MT>), dim3(B), dim3(256), 0, s, scores,
+                       old_lp, ref_lp, mask, R, beta, rewards, row_kl);
+  }));
+  return check_launch("apply_kl_penalty");
+}

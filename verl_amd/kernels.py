@@ -1,0 +1,385 @@
+"""Tensor-level wrappers (and autograd) around the gfx950 kernels of libverl_amd.
+
+Device memory, streams and autograd come from PyTorch-ROCm; the arithmetic runs in the HIP
+kernels behind the C-ABI of include/verl_amd.h. Every wrapper:
+  * requires HIP-resident tensors (no CPU fallback: a CPU tensor raises);
+  * launches on torch's current stream of the tensor's device, without host syncs;
+  * allocates outputs / workspaces through the torch caching allocator.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+_vp = ctypes.c_void_p
+
+_MASK_CODES = {
+    torch.float32: L.VA_MASK_F32,
+    torch.int64: L.VA_MASK_I64,
+    torch.int32: L.VA_MASK_I32,
+    torch.bool: L.VA_MASK_U8,
+    torch.uint8: L.VA_MASK_U8,
+}
+_DTYPE_CODES = {torch.float32: L.VA_F32, torch.bfloat16: L.VA_BF16, torch.float16: L.VA_F16}
+
+AGG_MODES = {
+    "token-mean": L.VA_AGG_TOKEN_MEAN,
+    "seq-mean-token-sum": L.VA_AGG_SEQ_MEAN_TOKEN_SUM,
+    "seq-mean-token-mean": L.VA_AGG_SEQ_MEAN_TOKEN_MEAN,
+    "seq-mean-token-sum-norm": L.VA_AGG_SEQ_MEAN_TOKEN_SUM_NORM,
+}
+KL_TYPES = {
+    "kl": L.VA_KL_K1,
+    "k1": L.VA_KL_K1,
+    "abs": L.VA_KL_ABS,
+    "mse": L.VA_KL_K2,
+    "k2": L.VA_KL_K2,
+    "low_var_kl": L.VA_KL_K3,
+    "k3": L.VA_KL_K3,
+}
+
+
+def _p(t: torch.Tensor | None):
+    return None if t is None else _vp(t.data_ptr())
+
+
+def _stream(t: torch.Tensor):
+    return _vp(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _require_device(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(
+                "verl_amd kernels run on MI355X (HIP) tensors only; got a tensor on "
+                f"{t.device}. There is no CPU fallback in the product path."
+            )
+
+
+def _f32(t: torch.Tensor | None) -> torch.Tensor | None:
+    if t is None:
+        return None
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def _mask(mask: torch.Tensor) -> tuple[torch.Tensor, int]:
+    if mask.dtype not in _MASK_CODES:
+        mask = mask.float()
+    mask = mask.contiguous()
+    return mask, _MASK_CODES[mask.dtype]
+
+
+def _as_2d(t: torch.Tensor) -> tuple[int, int]:
+    if t.dim() == 1:
+        return 1, t.shape[0]
+    R = t.shape[-1]
+    return t.numel() // max(R, 1), R
+
+
+# =============================================================================== log-prob
+class _LogprobEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, temperature, inplace_backward):
+        V = logits.shape[-1]
+        x = logits.reshape(-1, V)
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        n = x.shape[0]
+        lab = labels.reshape(-1)
+        if lab.dtype != torch.int64:
+            lab = lab.long()
+        lab = lab.contiguous()
+        if lab.shape[0] != n:
+            raise ValueError(f"labels ({lab.shape[0]}) do not match logits rows ({n})")
+        if x.dtype not in _DTYPE_CODES:
+            raise TypeError(f"unsupported logits dtype {x.dtype}")
+        logp = torch.empty(n, dtype=torch.float32, device=x.device)
+        ent = torch.empty(n, dtype=torch.float32, device=x.device)
+        lse = torch.empty(n, dtype=torch.float32, device=x.device)
+        L.call(
+            "va_logprob_entropy_fwd", _p(x), _DTYPE_CODES[x.dtype], n, V, x.stride(0), _p(lab),
+            float(temperature), _p(logp), _p(ent), _p(lse), _stream(x),
+        )
+        ctx.save_for_backward(x, lab, lse, ent)
+        ctx.temperature = float(temperature)
+        ctx.inplace = bool(inplace_backward)
+        ctx.in_shape = logits.shape
+        out_shape = logits.shape[:-1]
+        return logp.view(out_shape), ent.view(out_shape)
+
+    @staticmethod
+    def backward(ctx, g_logp, g_ent):
+        x, lab, lse, ent = ctx.saved_tensors
+        n, V = x.shape
+        g1 = None if g_logp is None else _f32(g_logp.reshape(-1))
+        g2 = None if g_ent is None else _f32(g_ent.reshape(-1))
+        dx = x if ctx.inplace else torch.empty_like(x)
+        L.call(
+            "va_logprob_entropy_bwd", _p(g1), _p(g2), _p(x), _DTYPE_CODES[x.dtype], n, V, x.stride(0),
+            _p(lab), _p(lse), _p(ent), ctx.temperature, _p(dx), dx.stride(0), _stream(x),
+        )
+        return dx.view(ctx.in_shape), None, None, None
+
+
+def logprob_entropy(logits, labels, temperature: float = 1.0, inplace_backward: bool = False):
+    """(log p[label], entropy) per row of ``logits[..., V]`` after the reference's
+    ``logits.div_(temperature)``; one fused HBM pass forward, one backward."""
+    _require_device(logits, labels)
+    return _LogprobEntropy.apply(logits, labels, temperature, inplace_backward)
+
+
+# =============================================================================== policy loss
+class _PolicyLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, old_lp, lp, adv, mask, ref_lp, entropy, clip_lo, clip_hi, clip_c, agg, kl_type):
+        B, R = _as_2d(lp)
+        old_c, lp_c, adv_c = _f32(old_lp), _f32(lp), _f32(adv)
+        ref_c, ent_c = _f32(ref_lp), _f32(entropy)
+        m, mcode = _mask(mask)
+        out = torch.empty(L.VA_LOSS_NOUT, dtype=torch.float32, device=lp.device)
+        nbytes = L.load().va_ppo_loss_workspace_bytes(B)
+        ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=lp.device)
+        L.call(
+            "va_ppo_loss_fwd", _p(old_c), _p(lp_c), _p(adv_c), _p(m), mcode, _p(ref_c), _p(ent_c), B, R,
+            clip_lo, clip_hi, clip_c, agg, kl_type, _p(out), _p(ws), _stream(lp),
+        )
+        ctx.save_for_backward(old_c, lp_c, adv_c, m, ref_c, ws)
+        ctx.cfg = (B, R, mcode, clip_lo, clip_hi, clip_c, agg, kl_type, entropy is not None)
+        ctx.lp_shape = lp.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        old_c, lp_c, adv_c, m, ref_c, ws = ctx.saved_tensors
+        B, R, mcode, clip_lo, clip_hi, clip_c, agg, kl_type, has_ent = ctx.cfg
+        g = _f32(g_out)
+        d_lp = torch.empty_like(lp_c)
+        d_ent = torch.empty_like(lp_c) if has_ent and ctx.needs_input_grad[5] else None
+        L.call(
+            "va_ppo_loss_bwd", _p(g), _p(old_c), _p(lp_c), _p(adv_c), _p(m), mcode, _p(ref_c), B, R,
+            clip_lo, clip_hi, clip_c, agg, kl_type, _p(ws), _p(d_lp), _p(d_ent), _stream(lp_c),
+        )
+        d_lp = d_lp.view(ctx.lp_shape) if ctx.needs_input_grad[1] else None
+        if d_ent is not None:
+            d_ent = d_ent.view(ctx.lp_shape)
+        return None, d_lp, None, None, None, d_ent, None, None, None, None, None
+
+
+def fused_policy_loss(
+    old_log_prob,
+    log_prob,
+    advantages,
+    response_mask,
+    clip_ratio_low: float,
+    clip_ratio_high: float,
+    clip_ratio_c: float = 3.0,
+    loss_agg_mode: str = "token-mean",
+    ref_log_prob=None,
+    kl_loss_type: str | None = None,
+    entropy=None,
+) -> torch.Tensor:
+    """Fused compute_policy_loss + agg_loss(kl_penalty) + agg_loss(entropy) (dp_actor.py:421-459).
+
+    Returns the 8-slot vector (see VA_LOSS_* in include/verl_amd.h) whose slots are the scalars
+    the reference returns; gradients flow from slots PG, KL and ENTROPY to log_prob / entropy.
+    """
+    _require_device(old_log_prob, log_prob, advantages, response_mask, ref_log_prob, entropy)
+    assert clip_ratio_c > 1.0, (
+        "The lower bound of the clip_ratio_c for dual-clip PPO should be greater than 1.0,"
+        + f" but get the value: {clip_ratio_c}."
+    )
+    if loss_agg_mode not in AGG_MODES:
+        raise ValueError(f"Invalid loss_agg_mode: {loss_agg_mode}")
+    kl_type = L.VA_KL_NONE
+    if ref_log_prob is not None:
+        if kl_loss_type == "full" or kl_loss_type not in KL_TYPES:
+            raise NotImplementedError
+        kl_type = KL_TYPES[kl_loss_type]
+    # torch.clamp casts its python-float bounds to the tensor dtype (fp32)
+    clip_lo = float(np.float32(1 - clip_ratio_low))
+    clip_hi = float(np.float32(1 + clip_ratio_high))
+    clip_c = float(np.float32(clip_ratio_c))
+    return _PolicyLoss.apply(
+        old_log_prob, log_prob, advantages, response_mask, ref_log_prob, entropy, clip_lo, clip_hi, clip_c,
+        AGG_MODES[loss_agg_mode], kl_type,
+    )
+
+
+# =============================================================================== kl penalty
+class _KLPenalty(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, lp, ref, kl_type):
+        a, b = _f32(lp), _f32(ref)
+        out = torch.empty_like(a)
+        L.call("va_kl_penalty_fwd", _p(a), _p(b), a.numel(), kl_type, _p(out), _stream(a))
+        ctx.save_for_backward(a, b)
+        ctx.kl_type = kl_type
+        return out.view(lp.shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = _f32(g)
+        d_lp = torch.empty_like(a) if ctx.needs_input_grad[0] else None
+        d_ref = torch.empty_like(a) if ctx.needs_input_grad[1] else None
+        L.call("va_kl_penalty_bwd", _p(g), _p(a), _p(b), a.numel(), ctx.kl_type, _p(d_lp), _p(d_ref), _stream(a))
+        return d_lp, d_ref, None
+
+
+def kl_penalty(logprob, ref_logprob, kl_type: str):
+    _require_device(logprob, ref_logprob)
+    if kl_type not in KL_TYPES:
+        raise NotImplementedError
+    return _KLPenalty.apply(logprob, ref_logprob, KL_TYPES[kl_type])
+
+
+# =============================================================================== masked aggregation
+class _MaskedAgg(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mask, mode, B, R):
+        xc = _f32(x)
+        m, mcode = _mask(mask)
+        nout = B if mode == L.VA_REDUCE_ROW_MASKED_MEAN else 1
+        out = torch.empty(nout, dtype=torch.float32, device=x.device)
+        nbytes = L.load().va_agg_workspace_bytes(B)
+        ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=x.device)
+        L.call("va_masked_agg_fwd", _p(xc), _p(m), mcode, B, R, mode, _p(out), _p(ws), _stream(xc))
+        ctx.save_for_backward(m, ws)
+        ctx.cfg = (mcode, B, R, mode, x.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        m, ws = ctx.saved_tensors
+        mcode, B, R, mode, shape = ctx.cfg
+        g = _f32(g)
+        dx = torch.empty(B * R, dtype=torch.float32, device=m.device)
+        L.call("va_masked_agg_bwd", _p(g), _p(m), mcode, B, R, mode, _p(ws), _p(dx), _stream(m))
+        return dx.view(shape), None, None, None, None
+
+
+def masked_aggregate(x, mask, mode: int):
+    """Aggregate a [..., R] matrix over the mask; mode is a VA_AGG_* / VA_REDUCE_* code."""
+    _require_device(x, mask)
+    if x.shape != mask.shape:
+        mask = mask.expand_as(x)
+    B, R = _as_2d(x)
+    out = _MaskedAgg.apply(x, mask, mode, B, R)
+    if mode == L.VA_REDUCE_ROW_MASKED_MEAN:
+        return out.view(x.shape[:-1])
+    return out.view(())
+
+
+# =============================================================================== advantages
+def group_csr(index, device) -> tuple[torch.Tensor, torch.Tensor, int, int]:
+    """Host-side uid grouping (core_algos.py:290-291) into CSR: (order, offsets, G, max_size).
+
+    Groups keep row order inside (stable sort), which is the reference's append order.
+    """
+    idx = np.asarray(index)
+    if idx.dtype == object:
+        _, inverse = np.unique(idx.astype(str) if all(isinstance(u, str) for u in idx) else idx, return_inverse=True)
+    else:
+        _, inverse = np.unique(idx, return_inverse=True)
+    inverse = inverse.reshape(-1).astype(np.int64)
+    order = np.argsort(inverse, kind="stable").astype(np.int32)
+    counts = np.bincount(inverse)
+    offsets = np.zeros(len(counts) + 1, dtype=np.int32)
+    np.cumsum(counts, out=offsets[1:])
+    order_t = torch.from_numpy(order).to(device)
+    offs_t = torch.from_numpy(offsets).to(device)
+    return order_t, offs_t, int(len(counts)), int(counts.max())
+
+
+def outcome_advantage(token_level_rewards, response_mask, index, epsilon: float, estimator: int):
+    _require_device(token_level_rewards, response_mask)
+    r = _f32(token_level_rewards)
+    B, R = r.shape
+    m, mcode = _mask(response_mask)
+    order, offsets, G, gmax = group_csr(index, r.device)
+    adv = torch.empty_like(r)
+    L.call(
+        "va_outcome_advantage", _p(r), _p(m), mcode, B, R, _p(order), _p(offsets), G, gmax, float(epsilon),
+        estimator, _p(adv), None, _stream(r),
+    )
+    return adv
+
+
+_WHITEN_ERRORS = {
+    1: "At least one element in the mask has to be 1.",
+    2: "The sum of the mask is one, which can cause a division by zero.",
+}
+
+
+def _raise_whiten_flag(stats: torch.Tensor) -> None:
+    flag = int(stats[3].item())  # the reference syncs here too (torch_functional.py:195-200)
+    if flag:
+        raise ValueError(_WHITEN_ERRORS[flag])
+
+
+def gae_advantage_return(rewards, values, mask, gamma: float, lam: float, check: bool = True):
+    _require_device(rewards, values, mask)
+    r, v = _f32(rewards), _f32(values)
+    B, R = r.shape
+    m, mcode = _mask(mask)
+    adv = torch.empty_like(r)
+    ret = torch.empty_like(r)
+    stats = torch.empty(4, dtype=torch.float32, device=r.device)
+    nbytes = L.load().va_gae_workspace_bytes(B)
+    ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=r.device)
+    L.call(
+        "va_gae_advantage_return", _p(r), _p(v), _p(m), mcode, B, R, float(gamma), float(lam), _p(adv), _p(ret),
+        _p(stats), _p(ws), _stream(r),
+    )
+    if check:
+        _raise_whiten_flag(stats)
+    return adv, ret
+
+
+def whiten_stats(values, mask) -> tuple[torch.Tensor, torch.Tensor]:
+    """(stats fp32[4] = {mean, rstd, n, flag}, merged fp64[3] = {n, sum, M2}) of a masked matrix."""
+    _require_device(values, mask)
+    x = _f32(values)
+    if mask.shape != x.shape:
+        mask = mask.expand_as(x)
+    B, R = _as_2d(x)
+    m, mcode = _mask(mask)
+    part = torch.empty(B * 3 + 3, dtype=torch.float64, device=x.device)
+    stats = torch.empty(4, dtype=torch.float32, device=x.device)
+    s = _stream(x)
+    L.call("va_masked_row_partials", _p(x), _p(m), mcode, B, R, _p(part), s)
+    merged = part[B * 3:]
+    L.call("va_whiten_finalize", _p(part), B, _p(merged), _p(stats), s)
+    return stats, merged
+
+
+def whiten_apply(values, mask, stats, post_multiply_mask: bool = False, out=None):
+    x = _f32(values)
+    y = x.clone() if out is None else out.copy_(x)
+    B, R = _as_2d(y)
+    m, mcode = _mask(mask.expand_as(x)) if post_multiply_mask else (None, 0)
+    L.call("va_whiten_apply", _p(y), _p(stats), _p(m), mcode, B, R, 1 if post_multiply_mask else 0, _stream(y))
+    return y
+
+
+def apply_kl_penalty(token_level_scores, old_log_prob, ref_log_prob, response_mask, beta: float, kl_type: str):
+    _require_device(token_level_scores, old_log_prob, ref_log_prob, response_mask)
+    if kl_type not in KL_TYPES:
+        raise NotImplementedError
+    s, o, r = _f32(token_level_scores), _f32(old_log_prob), _f32(ref_log_prob)
+    B, R = s.shape
+    m, mcode = _mask(response_mask)
+    rewards = torch.empty_like(s)
+    row_kl = torch.empty(B, dtype=torch.float32, device=s.device)
+    L.call(
+        "va_apply_kl_penalty", _p(s), _p(o), _p(r), _p(m), mcode, B, R, KL_TYPES[kl_type], float(beta),
+        _p(rewards), _p(row_kl), _stream(s),
+    )
+    return rewards, row_kl
