@@ -1,0 +1,244 @@
+"""GRPO actor-update benchmark on MI355X (BASELINE.json metric).
+
+One step = the actor-update hot path on this rank's shard: old-logp forward (compute_log_prob),
+GRPO advantages, then update_policy (forward, fused clipped loss + k3 KL loss, backward,
+bucketed RCCL gradient all-reduce, grad clip, AdamW). Workload per rank: Qwen2.5-0.5B
+architecture (random init), 64 prompts x n=8 = 512 responses x 1024 tokens, prompts left-padded
+to 256, vocab 151,936 — configs[1] of BASELINE.json; weak scaling (every rank does that work).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+  N > 1 is launched by torch.distributed.run (one process per GPU, RCCL).
+Rank 0 prints ONE JSON line (see the driver contract in the task statement).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--prompts", type=int, default=64)
+    ap.add_argument("--n", type=int, default=8)
+    ap.add_argument("--prompt-len", type=int, default=256)
+    ap.add_argument("--response-len", type=int, default=1024)
+    ap.add_argument("--micro", type=int, default=8, help="ppo_micro_batch_size_per_gpu (responses)")
+    ap.add_argument("--logprob-micro", type=int, default=16, help="log_prob_micro_batch_size_per_gpu")
+    ap.add_argument("--model", default="0.5b")
+    ap.add_argument("--no-rmpad", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--cpu-sample-rows", type=int, default=2048)
+    ap.add_argument("--out", default=None, help="also write the JSON line here")
+    return ap.parse_args()
+
+
+def _barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def cpu_baseline(args, rank) -> dict | None:
+    """Oracle (eager PyTorch CPU restatement of the reference) on the box's host cores, bounded
+    sample: log-prob + entropy of ``cpu_sample_rows`` response tokens over the full vocab (fp32
+    row loop, torch_functional.py:116-133, 145-149) and GRPO + clipped loss + k3 KL over the
+    full 512 x 1024 batch (core_algos.py). Reported as hot-path tokens/s (not the whole update:
+    the model GEMMs are outside the oracle)."""
+    if rank != 0:
+        return None
+    from oracle import reference_ops as ref
+
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    V, rows = 151936, args.cpu_sample_rows
+    g = torch.Generator().manual_seed(0)
+    logits = torch.randn(rows, V, generator=g) * 2
+    labels = torch.randint(0, V, (rows,), generator=g)
+    t0 = time.perf_counter()
+    lp = ref.logprobs_from_logits(logits, labels)
+    ent = ref.entropy_from_logits(logits)
+    t_lp = time.perf_counter() - t0
+    del logits, lp, ent
+    B, R, n = args.prompts * args.n, args.response_len, args.n
+    rewards = torch.zeros(B, R)
+    rewards[:, -1] = torch.randint(0, 2, (B,), generator=g).float()
+    mask = torch.ones(B, R, dtype=torch.int64)
+    index = np.array([f"p{i // n}" for i in range(B)], dtype=object)
+    new = -torch.rand(B, R, generator=g)
+    old = new + 0.05 * torch.randn(B, R, generator=g)
+    refl = new + 0.1 * torch.randn(B, R, generator=g)
+    t0 = time.perf_counter()
+    adv, _ = ref.compute_grpo_outcome_advantage(rewards, mask, index)
+    newr = new.clone().requires_grad_(True)
+    loss, _ = ref.actor_loss(old, newr, adv, mask, ref_log_prob=refl, kl_loss_type="low_var_kl")
+    loss.backward()
+    t_algo = time.perf_counter() - t0
+    per_token = t_lp / rows + t_algo / (B * R)
+    return {
+        "value": round(1.0 / per_token, 1),
+        "unit": "tokens/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": (f"oracle log-prob+entropy fwd of {rows} tokens x V={V} fp32 ({t_lp:.2f}s) + GRPO adv + "
+                   f"clipped loss + k3 KL fwd/bwd on {B}x{R} ({t_algo:.2f}s); model GEMMs excluded"),
+    }
+
+
+def main():
+    args = parse()
+    from verl_amd import kernels as K
+    from verl_amd.trainer.ppo.core_algos import AdvantageEstimator
+    from verl_amd.trainer.ppo.ray_trainer import compute_advantage
+    from verl_amd.utils.config import AttrDict, actor_config
+    from verl_amd.utils.model import build_qwen2
+    from verl_amd.utils.synthetic import make_grpo_batch
+    from verl_amd.workers.dp_workers import ActorWorker, init_distributed
+
+    rank, world = init_distributed()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+
+    B = args.prompts * args.n
+    R = args.response_len
+    cfg = AttrDict(
+        actor=actor_config(
+            ppo_mini_batch_size=args.prompts,  # prompts; x n / world in ActorWorker -> one optimizer step
+            ppo_micro_batch_size_per_gpu=args.micro,
+            use_kl_loss=True, kl_loss_coef=0.001, kl_loss_type="low_var_kl",
+            clip_ratio=0.2, clip_ratio_c=3.0, loss_agg_mode="token-mean", entropy_coeff=0,
+            use_remove_padding=not args.no_rmpad,
+        ),
+        rollout=AttrDict(log_prob_micro_batch_size_per_gpu=args.logprob_micro, temperature=1.0),
+    )
+    # weak scaling: every rank owns a full 512-response shard; normalise against world=1
+    worker = ActorWorker(cfg, rollout_n=args.n * world)
+    model = build_qwen2(args.model, device=dev, seed=0)
+    worker.init_model(model)
+    batch = make_grpo_batch(args.prompts, args.n, args.prompt_len, R, seed=1234 + rank, device=dev)
+    # reference-policy log-probs are an input of the step (ref = new + N(0, 0.1^2))
+    with torch.no_grad():
+        lp0 = worker.compute_log_prob(batch).batch["old_log_probs"]
+        gen = torch.Generator(device=dev).manual_seed(99 + rank)
+        batch.batch["ref_log_prob"] = lp0 + 0.1 * torch.randn(lp0.shape, device=dev, generator=gen)
+    del lp0
+
+    def step():
+        out = worker.compute_log_prob(batch)
+        batch.batch["old_log_probs"] = out.batch["old_log_probs"]
+        compute_advantage(batch, AdvantageEstimator.GRPO, norm_adv_by_std_in_grpo=True)
+        return worker.update_actor(batch)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not args.no_kernel_timing:
+        K.TIMER = K.KernelTimer()
+    _barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    metrics = None
+    for _ in range(args.steps):
+        metrics = step()
+    torch.cuda.synchronize()
+    _barrier(world)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ksum = K.TIMER.summary() if K.TIMER is not None else {}
+    K.TIMER = None
+
+    resp_tokens = int(batch.batch["response_mask"].sum().item())
+    total_tokens = torch.tensor([resp_tokens, sum(batch.meta_info["global_token_num"])], dtype=torch.float64,
+                                device=dev)
+    if world > 1:
+        dist.all_reduce(total_tokens)
+    tok_s = float(total_tokens[0].item()) * args.steps / elapsed
+    perf_throughput = float(total_tokens[1].item()) * args.steps / elapsed / world  # metric_utils.py:249-257
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, rank)
+
+    if rank == 0:
+        roof = None
+        if ksum:
+            dom = max(ksum.items(), key=lambda kv: kv[1]["time_ms_total"])
+            name, d = dom
+            roof = {
+                "kernel": name,
+                "bound": "hbm",
+                "achieved": round(d["gbps"], 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(d["gbps"] / HBM_PEAK_GBPS, 4),
+                "traffic": None,
+                "algo_bytes_per_launch": d["avg_bytes"],
+                "avg_launch_us": round(d["avg_us"], 2),
+                "launches": d["launches"],
+            }
+        line = {
+            "metric": "GRPO actor-update tokens/sec (512x1024)",
+            "value": round(tok_s, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random token ids, Bernoulli outcome rewards; random-init weights)",
+            "config": {
+                "workload": "GRPO actor update: old-logp fwd + GRPO adv + fwd/fused clipped loss+k3 KL/bwd + "
+                            "RCCL grad all-reduce + clip + AdamW",
+                "model": "Qwen2.5-0.5B architecture",
+                "global_batch": B * world,
+                "responses_per_gpu": B,
+                "seq_len": args.prompt_len + R,
+                "response_len": R,
+                "vocab": 151936,
+                "micro_batch": args.micro,
+                "logprob_micro_batch": args.logprob_micro,
+                "parallelism": f"dp{world}",
+                "remove_padding": not args.no_rmpad,
+            },
+            "perf_throughput": round(perf_throughput, 1),
+            "roofline": roof,
+            "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                        for k, v in ksum.items()},
+            "cpu_baseline": cpu,
+            "final_metrics": {k: v[-1] for k, v in (metrics.meta_info["metrics"].items() if metrics else [])},
+        }
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(s + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

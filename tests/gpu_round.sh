@@ -1,0 +1,17 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, then the benchmark. Every GPU step has its own time
+# limit and a fault (rc >= 2 from pytest, or any signal exit) stops the script.
+set -u
+mkdir -p gpurun_out
+STAGE=${1:-all}
+run() { local name=$1 limit=$2; shift 2; timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "rc=$rc" >> "gpurun_out/$name.log"; echo "[$name] rc=$rc"; return $rc; }
+if [[ $STAGE == all || $STAGE == tests ]]; then
+  run tests 900 python -m pytest tests -m gpu -q -rf -p no:cacheprovider; rc=$?
+  if [ $rc -ge 2 ]; then exit $rc; fi
+  run smoke 300 python __graft_entry__.py smoke || exit $?
+fi
+if [[ $STAGE == all || $STAGE == bench ]]; then
+  run bench_small 400 python bench.py --prompts 8 --steps 2 --warmup 1 --no-cpu-baseline || exit $?
+  run bench 900 python bench.py --steps 3 --warmup 1 --out gpurun_out/bench.json || exit $?
+fi
+exit 0

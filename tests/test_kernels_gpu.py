@@ -86,7 +86,9 @@ def test_logprob_entropy_bwd(K, dtype, temperature, with_entropy_grad):
     g_h = torch.randn(n) if with_entropy_grad else None
     # oracle gradient: autograd through the fp32 restatement of div_(T) -> logp / entropy
     x = base.double().requires_grad_(True)
-    z = x / temperature
+    # value: the reference's in-dtype div_ (bf16 rounding); gradient: d(x/T)/dx = 1/T
+    z_val = ref.apply_temperature(base, temperature).double()
+    z = z_val + (x / temperature - (x / temperature).detach())
     lp_ref = ref.logprobs_from_logits(z, labels)
     loss = (lp_ref * g_lp.double()).sum()
     if g_h is not None:

@@ -44,6 +44,41 @@ KL_TYPES = {
 }
 
 
+class KernelTimer:
+    """Opt-in HIP-event timing of kernel launches (bench.py): events are recorded on the same
+    stream the kernel is launched on, around that launch only."""
+
+    def __init__(self):
+        self.records: list[tuple[str, float, object, object]] = []
+
+    def start(self, stream):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        return ev
+
+    def stop(self, name: str, algo_bytes: float, stream, ev0):
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record(stream)
+        self.records.append((name, algo_bytes, ev0, ev1))
+
+    def summary(self) -> dict:
+        """{name: {launches, algo_bytes_total, time_ms_total, avg_us, gbps}} (after a sync)."""
+        out: dict[str, dict] = {}
+        for name, nb, e0, e1 in self.records:
+            d = out.setdefault(name, {"launches": 0, "algo_bytes_total": 0.0, "time_ms_total": 0.0})
+            d["launches"] += 1
+            d["algo_bytes_total"] += nb
+            d["time_ms_total"] += e0.elapsed_time(e1)
+        for d in out.values():
+            d["avg_us"] = 1e3 * d["time_ms_total"] / d["launches"]
+            d["avg_bytes"] = d["algo_bytes_total"] / d["launches"]
+            d["gbps"] = d["algo_bytes_total"] / (d["time_ms_total"] * 1e-3) / 1e9
+        return out
+
+
+TIMER: KernelTimer | None = None
+
+
 def _p(t: torch.Tensor | None):
     return None if t is None else _vp(t.data_ptr())
 
@@ -103,10 +138,14 @@ class _LogprobEntropy(torch.autograd.Function):
         logp = torch.empty(n, dtype=torch.float32, device=x.device)
         ent = torch.empty(n, dtype=torch.float32, device=x.device)
         lse = torch.empty(n, dtype=torch.float32, device=x.device)
+        st = _stream(x)
+        ev = TIMER.start(torch.cuda.current_stream(x.device)) if TIMER is not None else None
         L.call(
             "va_logprob_entropy_fwd", _p(x), _DTYPE_CODES[x.dtype], n, V, x.stride(0), _p(lab),
-            float(temperature), _p(logp), _p(ent), _p(lse), _stream(x),
+            float(temperature), _p(logp), _p(ent), _p(lse), st,
         )
+        if ev is not None:  # algorithmic bytes: s*V logits + 8 label + 12 outputs per row
+            TIMER.stop("logprob_entropy_fwd", n * (x.element_size() * V + 20), torch.cuda.current_stream(x.device), ev)
         ctx.save_for_backward(x, lab, lse, ent)
         ctx.temperature = float(temperature)
         ctx.inplace = bool(inplace_backward)
@@ -121,10 +160,13 @@ class _LogprobEntropy(torch.autograd.Function):
         g1 = None if g_logp is None else _f32(g_logp.reshape(-1))
         g2 = None if g_ent is None else _f32(g_ent.reshape(-1))
         dx = x if ctx.inplace else torch.empty_like(x)
+        ev = TIMER.start(torch.cuda.current_stream(x.device)) if TIMER is not None else None
         L.call(
             "va_logprob_entropy_bwd", _p(g1), _p(g2), _p(x), _DTYPE_CODES[x.dtype], n, V, x.stride(0),
             _p(lab), _p(lse), _p(ent), ctx.temperature, _p(dx), dx.stride(0), _stream(x),
         )
+        if ev is not None:  # read + write logits, 28 B of row scalars
+            TIMER.stop("logprob_entropy_bwd", n * (2 * x.element_size() * V + 28), torch.cuda.current_stream(x.device), ev)
         return dx.view(ctx.in_shape), None, None, None
 
 

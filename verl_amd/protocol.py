@@ -1,0 +1,553 @@
+"""DataProto — the batch type that crosses every boundary of the actor-update path.
+
+Mirror of verl/protocol.py:207-964 (DataProto, DataProtoItem, pad/unpad, union, chunk, split,
+concat, repeat, reorder, select, pop, rename, padding), without tensordict or ray:
+``batch`` is a :class:`TensorBatch` — an ordered dict of tensors sharing dim 0 —, and
+``non_tensor_batch`` holds numpy object arrays of the same length. ``meta_info`` is a plain
+dict. The pickled form is a dict of tensors written by ``torch.save`` (loaded back with
+``weights_only=True``), numpy arrays and meta_info.
+"""
+
+from __future__ import annotations
+
+import copy
+import io
+import logging
+import pickle
+from collections.abc import Iterator
+from dataclasses import dataclass, field
+from typing import Any, Optional
+
+import numpy as np
+import torch
+
+__all__ = ["DataProto", "DataProtoItem", "TensorBatch", "union_tensor_dict", "pad_dataproto_to_divisor",
+           "unpad_dataproto", "DataProtoConfig", "collate_fn"]
+
+
+class _DataProtoConfigMeta(type):
+    _config: dict = {}
+    auto_padding_key = "_verl_auto_padding"
+
+    @property
+    def auto_padding(cls):
+        return cls._config.get(cls.auto_padding_key, False)
+
+    @auto_padding.setter
+    def auto_padding(cls, enabled: bool):
+        assert isinstance(enabled, bool), f"enabled must be a boolean, got {enabled} as {type(enabled)}"
+        cls._config[cls.auto_padding_key] = enabled
+
+
+class DataProtoConfig(metaclass=_DataProtoConfigMeta):
+    """Global switch for auto-padding in chunk() (protocol.py:47-63)."""
+
+
+class TensorBatch(dict):
+    """Ordered mapping of tensors with a common leading batch dimension (TensorDict stand-in)."""
+
+    def __init__(self, source: Optional[dict] = None, batch_size=None):
+        super().__init__()
+        source = source or {}
+        for k, v in source.items():
+            if not isinstance(v, torch.Tensor):
+                raise TypeError(f"TensorBatch values must be tensors, got {type(v)} for {k}")
+            dict.__setitem__(self, k, v)
+        if batch_size is None:
+            batch_size = (next(iter(source.values())).shape[0],) if source else (0,)
+        if isinstance(batch_size, int):
+            batch_size = (batch_size,)
+        self.batch_size = torch.Size(batch_size)
+        for k, v in self.items():
+            if tuple(v.shape[: len(self.batch_size)]) != tuple(self.batch_size):
+                raise ValueError(f"key {k} has shape {tuple(v.shape)}, batch size is {tuple(self.batch_size)}")
+
+    def __setitem__(self, key, value):
+        if not isinstance(value, torch.Tensor):
+            raise TypeError("TensorBatch values must be tensors")
+        if tuple(value.shape[: len(self.batch_size)]) != tuple(self.batch_size):
+            raise ValueError(f"key {key}: shape {tuple(value.shape)} does not match batch size {tuple(self.batch_size)}")
+        dict.__setitem__(self, key, value)
+
+    def __getitem__(self, item):
+        if isinstance(item, str):
+            return dict.__getitem__(self, item)
+        sel = {k: v[item] for k, v in self.items()}
+        n = next(iter(sel.values())).shape[0] if sel else _index_len(item, self.batch_size[0])
+        return TensorBatch(sel, batch_size=(n,))
+
+    @property
+    def device(self):
+        devs = {v.device for v in self.values()}
+        return devs.pop() if len(devs) == 1 else None
+
+    def to(self, device) -> "TensorBatch":
+        return TensorBatch({k: v.to(device) for k, v in self.items()}, batch_size=self.batch_size)
+
+    def select(self, *keys) -> "TensorBatch":
+        return TensorBatch({k: dict.__getitem__(self, k) for k in keys}, batch_size=self.batch_size)
+
+    def pop(self, key, *default):
+        return dict.pop(self, key, *default)
+
+    def rename_key_(self, old_keys, new_keys):
+        for o, n in zip(old_keys, new_keys, strict=True):
+            dict.__setitem__(self, n, dict.pop(self, o))
+        return self
+
+    def contiguous(self) -> "TensorBatch":
+        return TensorBatch({k: v.contiguous() for k, v in self.items()}, batch_size=self.batch_size)
+
+    def chunk(self, chunks: int, dim: int = 0) -> list["TensorBatch"]:
+        assert dim == 0
+        parts = {k: torch.chunk(v, chunks, dim=0) for k, v in self.items()}
+        n = len(next(iter(parts.values()))) if parts else 0
+        return [TensorBatch({k: p[i] for k, p in parts.items()}) for i in range(n)]
+
+    def clone(self) -> "TensorBatch":
+        return TensorBatch({k: v.clone() for k, v in self.items()}, batch_size=self.batch_size)
+
+    @property
+    def sorted_keys(self):
+        return sorted(self.keys())
+
+    def __repr__(self):
+        body = ", ".join(f"{k}: {tuple(v.shape)} {v.dtype}" for k, v in self.items())
+        return f"TensorBatch(batch_size={tuple(self.batch_size)}, {{{body}}})"
+
+
+def _index_len(item, n):
+    if isinstance(item, slice):
+        return len(range(*item.indices(n)))
+    return len(item)
+
+
+def _cat_batches(batches: list[TensorBatch]) -> TensorBatch:
+    keys = list(batches[0].keys())
+    return TensorBatch({k: torch.cat([b[k] for b in batches], dim=0) for k in keys})
+
+
+def union_tensor_dict(tensor_dict1: TensorBatch, tensor_dict2: TensorBatch) -> TensorBatch:
+    """protocol.py:105-118: merge; conflicting keys must hold equal tensors."""
+    assert tensor_dict1.batch_size == tensor_dict2.batch_size, (
+        f"Two tensor dict must have identical batch size. Got {tensor_dict1.batch_size} and {tensor_dict2.batch_size}"
+    )
+    for key in tensor_dict2.keys():
+        if key not in tensor_dict1.keys():
+            tensor_dict1[key] = tensor_dict2[key]
+        else:
+            assert tensor_dict1[key].equal(tensor_dict2[key]), (
+                f"{key} in tensor_dict1 and tensor_dict2 are not the same object"
+            )
+    return tensor_dict1
+
+
+def _arrays_equal(a: np.ndarray, b: np.ndarray) -> bool:
+    if a.shape != b.shape:
+        return False
+    for x, y in zip(a.reshape(-1), b.reshape(-1), strict=True):
+        both_nan = isinstance(x, float) and isinstance(y, float) and np.isnan(x) and np.isnan(y)
+        if not both_nan and not np.array_equal(np.asarray(x, dtype=object), np.asarray(y, dtype=object)):
+            return False
+    return True
+
+
+def union_numpy_dict(d1: dict, d2: dict) -> dict:
+    """protocol.py:121-132."""
+    for key, val in d2.items():
+        if key in d1:
+            assert isinstance(val, np.ndarray) and isinstance(d1[key], np.ndarray)
+            assert _arrays_equal(val, d1[key]), f"{key} in tensor_dict1 and tensor_dict2 are not the same object"
+        d1[key] = val
+    return d1
+
+
+def union_two_dict(dict1: dict, dict2: dict) -> dict:
+    for key, val in dict2.items():
+        if key in dict1:
+            assert dict1[key] == val, f"{key} in meta_dict1 and meta_dict2 are not the same object"
+        dict1[key] = val
+    return dict1
+
+
+def list_of_dict_to_dict_of_list(list_of_dict: list[dict]) -> dict:
+    if not list_of_dict:
+        return {}
+    out = {k: [] for k in list_of_dict[0]}
+    for d in list_of_dict:
+        for k, v in d.items():
+            assert k in out
+            out[k].append(v)
+    return out
+
+
+@dataclass
+class DataProtoItem:
+    batch: Optional[TensorBatch] = None
+    non_tensor_batch: dict = field(default_factory=dict)
+    meta_info: dict = field(default_factory=dict)
+
+
+def collate_fn(x: list[DataProtoItem]) -> "DataProto":
+    batch = TensorBatch({k: torch.stack([it.batch[k] for it in x]) for k in x[0].batch.keys()})
+    non_tensor = {k: np.array([it.non_tensor_batch[k] for it in x], dtype=object) for k in x[0].non_tensor_batch}
+    return DataProto(batch=batch, non_tensor_batch=non_tensor, meta_info=x[0].meta_info)
+
+
+@dataclass
+class DataProto:
+    """Batch protocol (protocol.py:207). ``batch``: TensorBatch; ``non_tensor_batch``: dict of
+    numpy object arrays; ``meta_info``: dict."""
+
+    batch: Optional[TensorBatch] = None
+    non_tensor_batch: dict = field(default_factory=dict)
+    meta_info: dict = field(default_factory=dict)
+
+    def __post_init__(self):
+        if self.batch is not None and not isinstance(self.batch, TensorBatch):
+            self.batch = TensorBatch(dict(self.batch))
+        self.check_consistency()
+
+    # ------------------------------------------------------------------ basics
+    def __len__(self):
+        if self.batch is not None:
+            return self.batch.batch_size[0]
+        if self.non_tensor_batch:
+            return next(iter(self.non_tensor_batch.values())).shape[0]
+        return 0
+
+    def __getitem__(self, item):
+        if isinstance(item, slice):
+            return self.slice(item.start, item.stop, item.step)
+        if isinstance(item, list | np.ndarray | torch.Tensor):
+            return self.select_idxs(item)
+        if isinstance(item, int | np.integer):
+            tensor_data = TensorBatch({k: v[item] for k, v in self.batch.items()}, batch_size=()) if self.batch is not None else None
+            non_tensor = {k: v[item] for k, v in self.non_tensor_batch.items()}
+            return DataProtoItem(batch=tensor_data, non_tensor_batch=non_tensor, meta_info=self.meta_info)
+        raise TypeError(f"Indexing with {type(item)} is not supported")
+
+    def __getstate__(self):
+        buf = io.BytesIO()
+        tensors = None if self.batch is None else {k: v.contiguous() for k, v in self.batch.items()}
+        torch.save(tensors, buf)
+        return buf.getvalue(), self.non_tensor_batch, self.meta_info
+
+    def __setstate__(self, data):
+        raw, non_tensor_batch, meta_info = data
+        tensors = torch.load(io.BytesIO(raw), weights_only=True, map_location="cpu")
+        self.batch = None if tensors is None else TensorBatch(tensors)
+        self.non_tensor_batch = non_tensor_batch
+        self.meta_info = meta_info
+
+    def save_to_disk(self, filepath):
+        with open(filepath, "wb") as f:
+            pickle.dump(self, f)
+
+    @staticmethod
+    def load_from_disk(filepath) -> "DataProto":
+        """Loads a file written by save_to_disk of THIS package (it unpickles: trusted files only)."""
+        with open(filepath, "rb") as f:
+            return pickle.load(f)
+
+    def print_size(self, prefix=""):
+        t = sum(v.element_size() * v.numel() for v in self.batch.values()) if self.batch is not None else 0
+        a = sum(v.nbytes for v in self.non_tensor_batch.values())
+        msg = f"Size of tensordict: {t / 1024**3} GB, size of non_tensor_batch: {a / 1024**3} GB"
+        print(f"{prefix}, {msg}" if prefix else msg)
+
+    def check_consistency(self):
+        if self.batch is not None:
+            assert len(self.batch.batch_size) == 1, "only support num_batch_dims=1"
+        if self.non_tensor_batch is not None:
+            for key, val in self.non_tensor_batch.items():
+                assert isinstance(val, np.ndarray), (
+                    f"data in the non_tensor_batch must be a numpy.array with dtype=object, but for {key=}, got {type(val)=}"
+                )
+        if self.batch is not None and self.non_tensor_batch:
+            bs = self.batch.batch_size[0]
+            for key, val in self.non_tensor_batch.items():
+                assert val.shape[0] == bs, f"key {key} length {len(val)} is not equal to batch size {bs}"
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def from_single_dict(cls, data: dict, meta_info=None, auto_padding=False):
+        tensors, non_tensors = {}, {}
+        for key, val in data.items():
+            if isinstance(val, torch.Tensor):
+                tensors[key] = val
+            elif isinstance(val, np.ndarray):
+                non_tensors[key] = val
+            else:
+                raise ValueError(f"Unsupported type in data {type(val)}")
+        return cls.from_dict(tensors=tensors, non_tensors=non_tensors, meta_info=meta_info, auto_padding=auto_padding)
+
+    @classmethod
+    def from_dict(cls, tensors=None, non_tensors=None, meta_info=None, num_batch_dims=1, auto_padding=False):
+        assert num_batch_dims > 0, "num_batch_dims must be greater than zero"
+        if non_tensors is not None:
+            assert num_batch_dims == 1, "only support num_batch_dims=1 when non_tensors is not None."
+        tensors = tensors or {}
+        meta_info = meta_info if meta_info is not None else {}
+        non_tensors = non_tensors if non_tensors is not None else {}
+        assert isinstance(non_tensors, dict)
+        batch_size, pivot = None, None
+        for key, t in tensors.items():
+            if batch_size is None:
+                batch_size, pivot = t.shape[:num_batch_dims], key
+            else:
+                assert batch_size == t.shape[:num_batch_dims], (
+                    f"Not all the tensor in tensors have the same batch size with batch_dims={num_batch_dims}. "
+                    f"Got {pivot} has {batch_size}, {key} has {t.shape[:num_batch_dims]}"
+                )
+        for key, val in non_tensors.items():
+            if not isinstance(val, np.ndarray):
+                non_tensors[key] = np.array(val, dtype=object)
+        batch = TensorBatch(tensors, batch_size=batch_size) if tensors else None
+        if auto_padding:
+            meta_info[DataProtoConfig.auto_padding_key] = True
+        return cls(batch=batch, non_tensor_batch=non_tensors, meta_info=meta_info)
+
+    # ------------------------------------------------------------------ moves and views
+    def to(self, device, non_blocking: bool = False) -> "DataProto":
+        if self.batch is not None:
+            self.batch = TensorBatch({k: v.to(device, non_blocking=non_blocking) for k, v in self.batch.items()},
+                                     batch_size=self.batch.batch_size)
+        return self
+
+    def select(self, batch_keys=None, non_tensor_batch_keys=None, meta_info_keys=None, deepcopy=False) -> "DataProto":
+        sub_batch = self.batch.select(*tuple(batch_keys)) if batch_keys is not None else self.batch
+        if non_tensor_batch_keys is not None:
+            non_tensor = {k: v for k, v in self.non_tensor_batch.items() if k in non_tensor_batch_keys}
+        else:
+            non_tensor = self.non_tensor_batch
+        if deepcopy:
+            non_tensor = copy.deepcopy(non_tensor)
+        if meta_info_keys is not None:
+            meta = {k: v for k, v in self.meta_info.items() if k in meta_info_keys}
+        else:
+            meta = self.meta_info
+        if deepcopy:
+            meta = copy.deepcopy(meta)
+        return type(self)(batch=sub_batch, non_tensor_batch=non_tensor, meta_info=meta)
+
+    def select_idxs(self, idxs) -> "DataProto":
+        if isinstance(idxs, list):
+            idxs = torch.tensor(idxs)
+            if idxs.dtype != torch.bool:
+                idxs = idxs.type(torch.int32)
+        if isinstance(idxs, np.ndarray):
+            idxs_np, idxs_t = idxs, torch.from_numpy(idxs)
+        else:
+            idxs_t, idxs_np = idxs, idxs.detach().cpu().numpy()
+        n = int(idxs_np.sum()) if idxs_np.dtype == bool else idxs_np.shape[0]
+        batch = None
+        if self.batch is not None:
+            dev = self.batch.device
+            it = idxs_t.to(dev) if dev is not None else idxs_t
+            batch = TensorBatch({k: v[it] for k, v in self.batch.items()}, batch_size=(n,))
+        non_tensor = {k: v[idxs_np] for k, v in self.non_tensor_batch.items()}
+        return type(self)(batch=batch, non_tensor_batch=non_tensor, meta_info=self.meta_info)
+
+    def slice(self, start=None, end=None, step=None) -> "DataProto":
+        s = slice(start, end, step)
+        batch = self.batch[s] if self.batch is not None else None
+        non_tensor = {k: v[s] for k, v in self.non_tensor_batch.items()}
+        return type(self)(batch=batch, non_tensor_batch=non_tensor, meta_info=self.meta_info)
+
+    def pop(self, batch_keys=None, non_tensor_batch_keys=None, meta_info_keys=None) -> "DataProto":
+        tensors = {}
+        for key in batch_keys or []:
+            assert key in self.batch.keys()
+            tensors[key] = self.batch.pop(key)
+        non_tensors = {}
+        for key in non_tensor_batch_keys or []:
+            assert key in self.non_tensor_batch.keys()
+            non_tensors[key] = self.non_tensor_batch.pop(key)
+        meta = {}
+        for key in meta_info_keys or []:
+            assert key in self.meta_info.keys()
+            meta[key] = self.meta_info.pop(key)
+        return DataProto.from_dict(tensors=tensors, non_tensors=non_tensors, meta_info=meta)
+
+    def rename(self, old_keys=None, new_keys=None) -> "DataProto":
+        def norm(keys):
+            if keys is None:
+                return keys
+            if isinstance(keys, str):
+                return [keys]
+            if isinstance(keys, list):
+                return keys
+            raise TypeError(f"keys must be a list or a string, but got {type(keys)}")
+
+        old_keys, new_keys = norm(old_keys), norm(new_keys)
+        if len(new_keys) != len(old_keys):
+            raise ValueError(
+                f"new_keys and old_keys must have the same length, but got {len(new_keys)} and {len(old_keys)}"
+            )
+        self.batch.rename_key_(tuple(old_keys), tuple(new_keys))
+        return self
+
+    def union(self, other: "DataProto") -> "DataProto":
+        if self.batch is None:
+            self.batch = other.batch
+        elif other.batch is not None:
+            self.batch = union_tensor_dict(self.batch, other.batch)
+        self.non_tensor_batch = union_numpy_dict(self.non_tensor_batch, other.non_tensor_batch)
+        self.meta_info = union_two_dict(self.meta_info, other.meta_info)
+        return self
+
+    def make_iterator(self, mini_batch_size, epochs, seed=None, dataloader_kwargs=None) -> Iterator["DataProto"]:
+        """protocol.py:625-663 — mini-batch iterator; shuffles when dataloader_kwargs['shuffle']."""
+        assert len(self) % mini_batch_size == 0, f"{len(self)} % {mini_batch_size} != 0"
+        kw = dataloader_kwargs or {}
+        gen = torch.Generator()
+        if seed is not None:
+            gen.manual_seed(seed)
+
+        def gen_data():
+            for _ in range(epochs):
+                order = torch.randperm(len(self), generator=gen) if kw.get("shuffle", False) else torch.arange(len(self))
+                for s in range(0, len(self), mini_batch_size):
+                    d = self.select_idxs(order[s : s + mini_batch_size])
+                    d.meta_info = self.meta_info
+                    yield d
+
+        return iter(gen_data())
+
+    # ------------------------------------------------------------------ padding / chunking
+    def is_padding_enabled(self) -> bool:
+        return self.meta_info.get(DataProtoConfig.auto_padding_key, False) or DataProtoConfig.auto_padding
+
+    def padding(self, padding_size, padding_candidate=""):
+        if padding_size == 0:
+            return
+        cand = self.select_idxs([0 if padding_candidate == "first" else len(self) - 1])
+        padded = DataProto.concat([self, cand.repeat(padding_size)])
+        self.batch = padded.batch
+        self.non_tensor_batch = padded.non_tensor_batch
+
+    def chunk(self, chunks: int) -> list["DataProto"]:
+        """protocol.py:689-728 — equal chunks along dim 0 (DP_COMPUTE_PROTO dispatch)."""
+        if not self.is_padding_enabled():
+            assert len(self) % chunks == 0, f"only support equal chunk. Got size of DataProto {len(self)} and chunk {chunks}."
+        if self.batch is not None:
+            batch_lst = self.batch.chunk(chunks=chunks, dim=0)
+            sizes = np.array([b.batch_size[0] for b in batch_lst])
+            cuts = np.cumsum(sizes)[:-1]
+        else:
+            batch_lst = [None] * chunks
+            sizes, cuts = None, None
+        non_tensor_lst = [{} for _ in range(chunks)]
+        for key, val in self.non_tensor_batch.items():
+            parts = np.array_split(val, cuts.tolist()) if sizes is not None else np.array_split(val, chunks)
+            assert len(parts) == chunks
+            for i in range(chunks):
+                non_tensor_lst[i][key] = parts[i]
+        return [type(self)(batch=batch_lst[i], non_tensor_batch=non_tensor_lst[i], meta_info=self.meta_info)
+                for i in range(chunks)]
+
+    def split(self, split_size: int) -> list["DataProto"]:
+        return [self[i : i + split_size] for i in range(0, len(self), split_size)]
+
+    @staticmethod
+    def concat(data: list["DataProto"]) -> "DataProto":
+        new_batch = _cat_batches([d.batch for d in data]) if data[0].batch is not None else None
+        non_tensor = list_of_dict_to_dict_of_list([d.non_tensor_batch for d in data])
+        for key, val in non_tensor.items():
+            non_tensor[key] = np.concatenate(val, axis=0)
+        cls = type(data[0]) if data else DataProto
+        return cls(batch=new_batch, non_tensor_batch=non_tensor, meta_info=data[0].meta_info)
+
+    def reorder(self, indices):
+        idx_np = indices.detach().cpu().numpy()
+        self.batch = self.batch[indices.to(self.batch.device) if self.batch.device is not None else indices]
+        self.non_tensor_batch = {k: v[idx_np] for k, v in self.non_tensor_batch.items()}
+
+    def repeat(self, repeat_times=2, interleave=True) -> "DataProto":
+        """protocol.py:772-814 — interleave=True keeps each prompt's n samples contiguous."""
+        batch = None
+        if self.batch is not None:
+            if interleave:
+                rep = {k: v.repeat_interleave(repeat_times, dim=0) for k, v in self.batch.items()}
+            else:
+                rep = {k: v.unsqueeze(0).expand(repeat_times, *v.shape).reshape(-1, *v.shape[1:])
+                       for k, v in self.batch.items()}
+            batch = TensorBatch(rep, batch_size=(self.batch.batch_size[0] * repeat_times,))
+        non_tensor = {}
+        for key, val in self.non_tensor_batch.items():
+            non_tensor[key] = np.repeat(val, repeat_times, axis=0) if interleave else np.tile(
+                val, (repeat_times,) + (1,) * (val.ndim - 1))
+        return type(self)(batch=batch, non_tensor_batch=non_tensor, meta_info=self.meta_info)
+
+    def sample_level_repeat(self, repeat_times) -> "DataProto":
+        """protocol.py:855-901 — per-sample repeat counts."""
+        if isinstance(repeat_times, tuple):
+            repeat_times = list(repeat_times)
+        elif isinstance(repeat_times, torch.Tensor):
+            assert repeat_times.dim() == 1
+            repeat_times = repeat_times.tolist()
+        elif isinstance(repeat_times, np.ndarray):
+            assert repeat_times.ndim == 1
+            repeat_times = repeat_times.tolist()
+        else:
+            assert isinstance(repeat_times, list), (
+                f"repeat_times type must be in [list, torch.Tensor, np.ndarray, tuple], got {type(repeat_times)}"
+            )
+        reps = torch.tensor(repeat_times)
+        batch = None
+        if self.batch is not None:
+            rep = {k: v.repeat_interleave(reps.to(v.device), dim=0) for k, v in self.batch.items()}
+            batch = TensorBatch(rep, batch_size=(int(reps.sum()),))
+        non_tensor = {k: np.repeat(v, repeat_times, axis=0) for k, v in self.non_tensor_batch.items()}
+        return type(self)(batch=batch, non_tensor_batch=non_tensor, meta_info=self.meta_info)
+
+
+def pad_dataproto_to_divisor(data: DataProto, size_divisor: int):
+    """protocol.py:70-95 — pad by re-using leading rows; returns (padded, pad_size)."""
+    assert isinstance(data, DataProto), "data must be a DataProto"
+    if len(data) % size_divisor != 0:
+        pad_size = size_divisor - len(data) % size_divisor
+        parts, remaining = [], pad_size
+        while remaining > 0:
+            take = min(remaining, len(data))
+            parts.append(data[:take])
+            remaining -= take
+        return DataProto.concat([data] + parts), pad_size
+    if len(data) == 0:
+        logging.warning("padding a DataProto with no item, no changed made")
+    return data, 0
+
+
+def unpad_dataproto(data: DataProto, pad_size):
+    return data[:-pad_size] if pad_size != 0 else data
+
+
+def fold_batch_dim(data: DataProto, new_batch_size):
+    """protocol.py:147-164."""
+    bs = data.batch.batch_size[0]
+    assert bs % new_batch_size == 0
+    tensors = {k: v.view(new_batch_size, -1, *v.shape[1:]) for k, v in data.batch.items()}
+    non_tensor = {k: np.reshape(v, (new_batch_size, -1, *v.shape[1:])) for k, v in data.non_tensor_batch.items()}
+    out = DataProto(batch=None, non_tensor_batch={}, meta_info=data.meta_info)
+    out.batch = TensorBatch(tensors, batch_size=(new_batch_size,))
+    out.non_tensor_batch = non_tensor
+    return out
+
+
+def all_gather_data_proto(data: DataProto, process_group) -> None:
+    """protocol.py:953-964 — in-place all-gather of every batch key and non-tensor array."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group=process_group)
+    if data.batch is not None:
+        gathered = {}
+        for k in sorted(data.batch.keys()):
+            v = data.batch[k].contiguous()
+            out = [torch.empty_like(v) for _ in range(world)]
+            dist.all_gather(out, v, group=process_group)
+            gathered[k] = torch.cat(out, dim=0)
+        data.batch = TensorBatch(gathered)
+    objs: list[Any] = [None] * world
+    dist.all_gather_object(objs, data.non_tensor_batch, group=process_group)
+    data.non_tensor_batch = {k: np.concatenate([o[k] for o in objs]) for k in data.non_tensor_batch}

@@ -1,0 +1,93 @@
+"""Driver-side hot-path functions of verl/trainer/ppo/ray_trainer.py, without Ray.
+
+compute_response_mask (ray_trainer.py:196-211), apply_kl_penalty (:153-193) and
+compute_advantage (:214-291) keep their reference signatures and dispatch GAE / GRPO by module
+attribute of core_algos, as the reference does (:247, :266), so a replacement of those module
+functions is picked up here too. The tensors stay on the device they arrive on: with the
+batch already on the MI355X, advantage estimation runs in the gfx950 kernels instead of the
+driver CPU.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ... import kernels as K
+from ...protocol import DataProto
+from . import core_algos
+from .core_algos import AdvantageEstimator
+
+
+def apply_kl_penalty(data: DataProto, kl_ctrl, kl_penalty="kl"):
+    """ray_trainer.py:153-193: token_level_rewards = scores - beta * kl * mask; adaptive beta update."""
+    response_mask = data.batch["response_mask"]
+    scores = data.batch["token_level_scores"]
+    batch_size = data.batch.batch_size[0]
+    beta = kl_ctrl.value
+    rewards, row_kl = K.apply_kl_penalty(
+        scores, data.batch["old_log_probs"], data.batch["ref_log_prob"], response_mask, float(beta), kl_penalty
+    )
+    current_kl = torch.mean(row_kl, dim=0).item()
+    kl_ctrl.update(current_kl=current_kl, n_steps=batch_size)
+    data.batch["token_level_rewards"] = rewards
+    return data, {"actor/reward_kl_penalty": current_kl, "actor/reward_kl_penalty_coeff": beta}
+
+
+def compute_response_mask(data: DataProto):
+    """ray_trainer.py:196-211."""
+    R = data.batch["responses"].size(1)
+    return data.batch["attention_mask"][:, -R:]
+
+
+def compute_advantage(
+    data: DataProto,
+    adv_estimator: AdvantageEstimator,
+    gamma: float = 1.0,
+    lam: float = 1.0,
+    num_repeat: int = 1,
+    norm_adv_by_std_in_grpo: bool = True,
+    config: Optional[dict] = None,
+) -> DataProto:
+    """ray_trainer.py:214-291."""
+    if "response_mask" not in data.batch.keys():
+        data.batch["response_mask"] = compute_response_mask(data)
+    if adv_estimator == AdvantageEstimator.GAE:
+        adv, ret = core_algos.compute_gae_advantage_return(
+            token_level_rewards=data.batch["token_level_rewards"],
+            values=data.batch["values"],
+            response_mask=data.batch["response_mask"],
+            gamma=gamma,
+            lam=lam,
+        )
+        data.batch["advantages"] = adv
+        data.batch["returns"] = ret
+        if config is not None and config.get("use_pf_ppo", False):
+            data = core_algos.compute_pf_ppo_reweight_data(
+                data, config.pf_ppo.reweight_method, config.pf_ppo.weight_pow
+            )
+    elif adv_estimator == AdvantageEstimator.GRPO:
+        adv, ret = core_algos.compute_grpo_outcome_advantage(
+            token_level_rewards=data.batch["token_level_rewards"],
+            response_mask=data.batch["response_mask"],
+            index=data.non_tensor_batch["uid"],
+            norm_adv_by_std_in_grpo=norm_adv_by_std_in_grpo,
+        )
+        data.batch["advantages"] = adv
+        data.batch["returns"] = ret
+    else:
+        fn = core_algos.get_adv_estimator_fn(adv_estimator)
+        kwargs = {
+            "token_level_rewards": data.batch["token_level_rewards"],
+            "response_mask": data.batch["response_mask"],
+            "config": config,
+        }
+        if "uid" in data.non_tensor_batch:
+            kwargs["index"] = data.non_tensor_batch["uid"]
+        if "reward_baselines" in data.batch:
+            kwargs["reward_baselines"] = data.batch["reward_baselines"]
+        adv, ret = fn(**kwargs)
+        data.batch["advantages"] = adv
+        data.batch["returns"] = ret
+    return data

@@ -1,0 +1,38 @@
+"""Model builders for the actor-update benchmark and tests.
+
+No checkpoints or network exist on the boxes, so models are HF architectures instantiated from
+locally written configs with random init. Qwen2.5-0.5B: hidden 896 and vocab 151,936 are
+confirmed by the reference (tests/utils/test_linear_cross_entropy.py:121-125); the remaining
+values (24 layers, 14 query heads, 2 KV heads, FFN 4864, tied embeddings, rope theta 1e6) are
+the public model card's and are recorded as assumptions in DESIGN.md.
+"""
+
+from __future__ import annotations
+
+import torch
+
+
+def qwen2_config(size: str = "0.5b", **overrides):
+    from transformers import Qwen2Config
+
+    presets = {
+        "0.5b": dict(hidden_size=896, intermediate_size=4864, num_hidden_layers=24, num_attention_heads=14,
+                     num_key_value_heads=2, vocab_size=151936, tie_word_embeddings=True),
+        "tiny": dict(hidden_size=128, intermediate_size=352, num_hidden_layers=2, num_attention_heads=4,
+                     num_key_value_heads=2, vocab_size=4096, tie_word_embeddings=True),
+    }
+    kw = dict(presets[size])
+    kw.update(max_position_embeddings=32768, rope_theta=1000000.0, rms_norm_eps=1e-6, use_sliding_window=False,
+              hidden_act="silu", attention_dropout=0.0, torch_dtype="float32")
+    kw.update(overrides)
+    return Qwen2Config(**kw)
+
+
+def build_qwen2(size: str = "0.5b", device="cuda", dtype=torch.float32, seed: int = 0, **overrides):
+    from transformers import Qwen2ForCausalLM
+
+    torch.manual_seed(seed)
+    cfg = qwen2_config(size, **overrides)
+    with torch.device(device):
+        model = Qwen2ForCausalLM(cfg)
+    return model.to(dtype)

@@ -1,0 +1,172 @@
+"""Drop-in mirror of verl/utils/torch_functional.py for the actor-update hot path.
+
+Same function names, argument meaning and error texts as the reference; the arithmetic runs
+in the gfx950 kernels (verl_amd.kernels). Inputs must live on the HIP device.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.distributed
+
+from .. import _lib as L
+from .. import kernels as K
+
+__all__ = [
+    "gather_from_labels", "logprobs_from_logits", "logprobs_from_logits_v2", "logprobs_and_entropy_from_logits",
+    "entropy_from_logits", "entropy_from_logits_with_chunking", "masked_sum", "masked_mean", "masked_var",
+    "masked_whiten", "clip_by_value", "get_response_mask", "distributed_mean_max_min_std",
+    "distributed_masked_mean", "allgather_dict_tensors", "broadcast_dict_tensor",
+]
+
+
+def gather_from_labels(data, label):
+    """torch_functional.py:49-61."""
+    return torch.gather(data, -1, label.unsqueeze(-1)).squeeze(-1)
+
+
+def logprobs_from_logits(logits, labels, inplace_backward=True):
+    """torch_functional.py:64-92: log p(label) over the last dim, fp32 result.
+
+    One fused HBM pass (va_logprob_entropy_fwd); the backward is a second pass that writes
+    dlogits — into the logits buffer when ``inplace_backward`` (flash-attn semantics).
+    """
+    logp, _ = K.logprob_entropy(logits, labels, 1.0, inplace_backward)
+    return logp
+
+
+def logprobs_from_logits_v2(logits, labels):
+    """torch_functional.py:116-133 (memory-efficient variant): same result, one pass."""
+    return logprobs_from_logits(logits, labels, inplace_backward=False)
+
+
+def logprobs_and_entropy_from_logits(logits, labels, temperature: float = 1.0, inplace_backward: bool = False):
+    """Fused dp_actor.py:182-201: ``logits.div_(T)`` + logprobs_from_logits + entropy_from_logits
+    in one read of the logits (the reference reads them twice or three times)."""
+    return K.logprob_entropy(logits, labels, temperature, inplace_backward)
+
+
+def _entropy(logits):
+    V = logits.shape[-1]
+    dummy = torch.zeros(logits.shape[:-1], dtype=torch.int64, device=logits.device)
+    _, ent = K.logprob_entropy(logits, dummy, 1.0, False)
+    del V
+    return ent
+
+
+def entropy_from_logits(logits: torch.Tensor):
+    """torch_functional.py:145-149: logsumexp(x) - sum(softmax(x) * x), fp32 math."""
+    return _entropy(logits)
+
+
+def entropy_from_logits_with_chunking(logits: torch.Tensor, chunk_size: int = 2048):
+    """torch_functional.py:152-160 (fp32 upcast per chunk): the kernel streams rows anyway."""
+    return _entropy(logits)
+
+
+def clip_by_value(x, tensor_min, tensor_max):
+    """torch_functional.py:136-142."""
+    return torch.max(torch.min(x, tensor_max), tensor_min)
+
+
+def masked_sum(values, mask, axis=None):
+    """torch_functional.py:163-168."""
+    if axis is None:
+        return K.masked_aggregate(values, mask, L.VA_REDUCE_MASKED_SUM)
+    return (torch.where(mask.bool(), values, 0.0) * mask).sum(axis=axis)
+
+
+def masked_mean(values, mask, axis=None):
+    """torch_functional.py:171-185: sum(where(m, x, 0) * m) / (sum(m) + 1e-8)."""
+    if axis is None:
+        return K.masked_aggregate(values, mask, L.VA_AGG_TOKEN_MEAN)
+    nd = values.dim()
+    ax = axis if isinstance(axis, int) else None
+    if ax is not None and ax % nd == nd - 1:
+        return K.masked_aggregate(values, mask.expand_as(values), L.VA_REDUCE_ROW_MASKED_MEAN)
+    if ax is not None:
+        v = values.movedim(ax, -1).contiguous()
+        m = mask.expand_as(values).movedim(ax, -1).contiguous()
+        return K.masked_aggregate(v, m, L.VA_REDUCE_ROW_MASKED_MEAN)
+    s = (torch.where(mask.bool(), values, 0.0) * mask).sum(axis=axis)
+    return s / (mask.sum(axis=axis) + 1e-8)
+
+
+def _merged_var(merged: torch.Tensor, unbiased: bool) -> torch.Tensor:
+    n, s, m2 = merged[0], merged[1], merged[2]
+    mean = s / (n + 1e-8)
+    mu = torch.where(n > 0, s / n.clamp(min=1e-300), torch.zeros_like(n))
+    var = (m2 + n * (mu - mean) ** 2) / (n + 1e-8)
+    if unbiased:
+        nv = float(n.item())
+        if nv == 0:
+            raise ValueError("At least one element in the mask has to be 1.")
+        if nv == 1:
+            raise ValueError("The sum of the mask is one, which can cause a division by zero.")
+        var = var * (n / (n - 1))
+    return var.float()
+
+
+def masked_var(values, mask, unbiased=True):
+    """torch_functional.py:188-203 (ValueError when the mask sums to 0 or 1 and unbiased)."""
+    _, merged = K.whiten_stats(values, mask)
+    return _merged_var(merged, unbiased)
+
+
+def masked_whiten(values, mask, shift_mean=True):
+    """torch_functional.py:206-223: (x - mean) * rsqrt(var + 1e-8), stats over the mask."""
+    stats, _ = K.whiten_stats(values, mask)
+    K._raise_whiten_flag(stats)
+    out = K.whiten_apply(values, mask, stats)
+    if not shift_mean:
+        out += stats[0]
+    return out
+
+
+def get_response_mask(response_id: torch.Tensor, eos_token=2, dtype=torch.int64):
+    """torch_functional.py:226-246: 1 up to and including the first EOS, 0 after."""
+    eos = torch.isin(response_id, torch.tensor(eos_token, device=response_id.device)).int()
+    return (eos.cumsum(dim=1) - eos).eq(0).to(dtype)
+
+
+def distributed_mean_max_min_std(local_tensor, compute_max=True, compute_min=True, compute_std=True):
+    """torch_functional.py:709-749: global stats with one SUM all-reduce of (sum, count)."""
+    dev = local_tensor.device
+    packed = torch.stack([local_tensor.sum().float(), torch.tensor(float(local_tensor.numel()), device=dev)])
+    torch.distributed.all_reduce(packed, op=torch.distributed.ReduceOp.SUM)
+    mean = packed[0] / packed[1]
+    gmax = gmin = gstd = None
+    if compute_max:
+        gmax = local_tensor.max().clone()
+        torch.distributed.all_reduce(gmax, op=torch.distributed.ReduceOp.MAX)
+    if compute_min:
+        gmin = local_tensor.min().clone()
+        torch.distributed.all_reduce(gmin, op=torch.distributed.ReduceOp.MIN)
+    if compute_std:
+        sq = torch.sum((local_tensor - mean) ** 2)
+        torch.distributed.all_reduce(sq, op=torch.distributed.ReduceOp.SUM)
+        gstd = torch.sqrt(sq / (packed[1] - 1))
+    return mean, gmax, gmin, gstd
+
+
+def distributed_masked_mean(local_tensor, local_mask):
+    """torch_functional.py:752-771: one all-reduce of (sum(x*m), sum(m))."""
+    packed = torch.stack([(local_tensor * local_mask).sum().float(), local_mask.sum().float()])
+    torch.distributed.all_reduce(packed, op=torch.distributed.ReduceOp.SUM)
+    return packed[0] / packed[1]
+
+
+def broadcast_dict_tensor(tensors, src, group):
+    for key in sorted(tensors.keys()):
+        torch.distributed.broadcast(tensors[key], src=src, group=group, async_op=False)
+
+
+def allgather_dict_tensors(tensors, size, group, dim=0):
+    """torch_functional.py:266-297 (dict form)."""
+    out = {}
+    for key in sorted(tensors.keys()):
+        val = tensors[key].contiguous()
+        parts = [torch.empty_like(val) for _ in range(size)]
+        torch.distributed.all_gather(parts, val, group=group, async_op=False)
+        out[key] = torch.cat(parts, dim=dim)
+    return out

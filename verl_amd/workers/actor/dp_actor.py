@@ -1,0 +1,316 @@
+"""DataParallelPPOActor — mirror of verl/workers/actor/dp_actor.py:51-486 on MI355X.
+
+Same constructor, config keys, micro/mini-batch loops, loss scaling and metric keys as the
+reference. What changes is how the hot path maps onto the GPU:
+
+  * padding removal is computed once per call on the host from the attention mask (one D2H
+    copy), so the micro-batch loop has no host syncs;
+  * the backbone runs on packed tokens with PyTorch-ROCm flash varlen attention
+    (attention.py) and only the hidden states that predict response tokens go through the
+    lm_head (the reference materialises logits for prompt tokens too and slices afterwards,
+    dp_actor.py:219-237); log-probs at masked-out positions are 0 here;
+  * temperature, log-softmax, label gather and entropy are ONE fused gfx950 kernel pass over
+    the logits (va_logprob_entropy_fwd); its backward writes dlogits in place;
+  * the clipped policy loss, KL loss, entropy aggregation and metrics are one fused kernel
+    (va_ppo_loss_fwd/bwd); metrics stay on device and are read once per update;
+  * gradients are averaged across DP ranks by a bucketed RCCL all-reduce overlapped with the
+    last micro-batch's backward (grad_sync.py), then clipped and stepped (AdamW).
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+from torch import nn
+
+from ... import _lib as L
+from ...protocol import DataProto
+from ...trainer.ppo import core_algos
+from ...trainer.ppo.core_algos import agg_loss, get_policy_loss_fn, kl_penalty
+from ...utils import torch_functional as verl_F
+from . import attention
+from .base import BasePPOActor
+
+__all__ = ["DataParallelPPOActor"]
+
+logger = logging.getLogger(__file__)
+logger.setLevel(os.getenv("VERL_LOGGING_LEVEL", "WARN"))
+
+_NO_MASK = {"full_attention": None, "sliding_attention": None}
+
+
+def append_to_dict(data: dict, new_data: dict):
+    for k, v in new_data.items():
+        data.setdefault(k, []).append(v)
+
+
+@dataclass
+class _Packing:
+    """Host-computed padding removal of one micro-batch (flash_attn.bert_padding.unpad_input)."""
+
+    token_idx: torch.Tensor  # [nnz] flat indices of real tokens in [B*S]
+    cu_seqlens: torch.Tensor  # [B+1] int32
+    max_seqlen: int
+    sel_hidden: torch.Tensor  # [n_sel] rows of the packed hidden states that predict a response token
+    sel_out: torch.Tensor  # [n_sel] flat index into [B*R]
+
+
+def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device) -> _Packing:
+    B, S = attn_mask_cpu.shape
+    flat = attn_mask_cpu.reshape(-1).astype(bool)
+    token_idx = np.flatnonzero(flat)
+    seqlens = attn_mask_cpu.astype(bool).sum(axis=1)
+    cu = np.zeros(B + 1, dtype=np.int32)
+    np.cumsum(seqlens, out=cu[1:])
+    # packed index of every padded position (valid only where the mask is 1)
+    packed_of = np.cumsum(flat) - 1
+    # position p = S - R - 1 + t predicts response token t (dp_actor.py:236-237)
+    t = np.arange(R)
+    p = (S - R - 1) + t
+    pos = (np.arange(B)[:, None] * S + p[None, :]).reshape(-1)
+    nxt = pos + 1
+    valid = flat[pos] & flat[nxt]
+    sel_out = np.flatnonzero(valid)
+    sel_hidden = packed_of[pos[valid]]
+
+    def dev(a, dt):
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(device, non_blocking=True)
+
+    return _Packing(
+        token_idx=dev(token_idx, np.int64),
+        cu_seqlens=dev(cu, np.int32),
+        max_seqlen=int(seqlens.max()) if B else 0,
+        sel_hidden=dev(sel_hidden, np.int64),
+        sel_out=dev(sel_out, np.int64),
+    )
+
+
+class DataParallelPPOActor(BasePPOActor):
+    def __init__(self, config, actor_module: nn.Module, actor_optimizer: torch.optim.Optimizer = None,
+                 grad_reducer=None):
+        """When actor_optimizer is None this is a reference policy (dp_actor.py:52-53)."""
+        super().__init__(config)
+        self.actor_module = actor_module
+        self.actor_optimizer = actor_optimizer
+        self.grad_reducer = grad_reducer
+        self.use_remove_padding = self.config.get("use_remove_padding", True)
+        self.ulysses_sequence_parallel_size = self.config.get("ulysses_sequence_parallel_size", 1)
+        if self.ulysses_sequence_parallel_size != 1:
+            raise NotImplementedError("Ulysses sequence parallelism is out of scope for the DP actor-update path")
+        base_prefix = getattr(actor_module, "base_model_prefix", "model")
+        self._backbone = getattr(actor_module, base_prefix)
+        self._lm_head = actor_module.get_output_embeddings()
+        if self.use_remove_padding:
+            name = attention.register()
+            if hasattr(actor_module, "set_attn_implementation"):
+                actor_module.set_attn_implementation(name)
+            else:
+                actor_module.config._attn_implementation = name
+        self.device_name = "cuda"
+        # bf16 autocast as the reference (dp_actor.py:100); None runs the model in its own dtype
+        self.autocast_dtype = self.config.get("autocast_dtype", torch.bfloat16)
+
+    # ------------------------------------------------------------------ forward
+    def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False, packing: _Packing = None):
+        """Returns (entropy or None, log_probs), both [bs, response_len] fp32."""
+        responses = micro_batch["responses"]
+        R = responses.size(-1)
+        input_ids = micro_batch["input_ids"]
+        B, S = input_ids.shape
+        ac = self.autocast_dtype
+        with torch.autocast(device_type=self.device_name, dtype=ac or torch.bfloat16, enabled=ac is not None):
+            if self.use_remove_padding:
+                if packing is None:
+                    packing = _plan_packing(micro_batch["attention_mask"].cpu().numpy(), R, input_ids.device)
+                ids = input_ids.reshape(-1).index_select(0, packing.token_idx).unsqueeze(0)
+                pos_ids = micro_batch["position_ids"]
+                if pos_ids.dim() == 3:
+                    raise NotImplementedError("mrope position ids (VLM) are out of scope")
+                pos = pos_ids.reshape(-1).index_select(0, packing.token_idx).unsqueeze(0)
+                out = self._backbone(
+                    input_ids=ids, position_ids=pos, attention_mask=_NO_MASK, use_cache=False,
+                    cu_seq_lens_q=packing.cu_seqlens, cu_seq_lens_k=packing.cu_seqlens,
+                    max_length_q=packing.max_seqlen, max_length_k=packing.max_seqlen,
+                )
+                hidden = out.last_hidden_state[0]
+                h_sel = hidden.index_select(0, packing.sel_hidden)
+                logits = self._lm_head(h_sel)
+                labels = responses.reshape(-1).index_select(0, packing.sel_out)
+                lp_sel, ent_sel = verl_F.logprobs_and_entropy_from_logits(
+                    logits, labels, temperature, inplace_backward=True)
+                log_probs = lp_sel.new_zeros(B * R).index_copy(0, packing.sel_out, lp_sel).view(B, R)
+                entropy = None
+                if calculate_entropy:
+                    entropy = ent_sel.new_zeros(B * R).index_copy(0, packing.sel_out, ent_sel).view(B, R)
+            else:
+                out = self._backbone(
+                    input_ids=input_ids, attention_mask=micro_batch["attention_mask"],
+                    position_ids=micro_batch["position_ids"], use_cache=False,
+                )
+                hidden = out.last_hidden_state[:, -R - 1 : -1]
+                logits = self._lm_head(hidden)
+                log_probs, ent = verl_F.logprobs_and_entropy_from_logits(
+                    logits, responses, temperature, inplace_backward=True)
+                entropy = ent if calculate_entropy else None
+        return entropy, log_probs
+
+    def _plans(self, data: DataProto, sizes: list[int]) -> list:
+        if not self.use_remove_padding:
+            return [None] * len(sizes)
+        am = data.batch["attention_mask"].cpu().numpy()  # one D2H for the whole call
+        R = data.batch["responses"].size(-1)
+        dev = data.batch["input_ids"].device
+        plans, s = [], 0
+        for n in sizes:
+            plans.append(_plan_packing(am[s : s + n], R, dev))
+            s += n
+        return plans
+
+    # ------------------------------------------------------------------ optimizer
+    def _zero_grad(self):
+        if self.grad_reducer is not None:
+            self.grad_reducer.zero_grad()
+        else:
+            self.actor_optimizer.zero_grad()
+
+    def _optimizer_step(self):
+        assert self.config.grad_clip is not None
+        if self.grad_reducer is not None:
+            self.grad_reducer.finish_sync()
+        grad_norm = torch.nn.utils.clip_grad_norm_(
+            self.actor_module.parameters(), max_norm=self.config.grad_clip, foreach=True)
+        if not torch.isfinite(grad_norm):
+            rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+            print(f"WARN: rank {rank} grad_norm is not finite: {grad_norm}")
+            self._zero_grad()
+        else:
+            self.actor_optimizer.step()
+        return grad_norm
+
+    # ------------------------------------------------------------------ API
+    @torch.no_grad()
+    def compute_log_prob(self, data: DataProto, calculate_entropy=False):
+        """dp_actor.py:290-349 — old-logp (and entropy) over micro-batches, no grad."""
+        self.actor_module.eval()
+        micro_batch_size = data.meta_info["micro_batch_size"]
+        temperature = data.meta_info["temperature"]
+        use_dynamic_bsz = data.meta_info["use_dynamic_bsz"]
+        if use_dynamic_bsz:
+            raise NotImplementedError("dynamic token-budget micro-batching (seqlen_balancing) is not yet ported")
+        data = data.select(batch_keys=["responses", "input_ids", "attention_mask", "position_ids"])
+        micro_batches = data.split(micro_batch_size)
+        plans = self._plans(data, [len(m) for m in micro_batches])
+        lps, ents = [], []
+        for mb, plan in zip(micro_batches, plans, strict=True):
+            ent, lp = self._forward_micro_batch(mb.batch, temperature, calculate_entropy, plan)
+            lps.append(lp)
+            if calculate_entropy:
+                ents.append(ent)
+        log_probs = torch.concat(lps, dim=0)
+        entropys = torch.concat(ents, dim=0) if calculate_entropy else None
+        return log_probs, entropys
+
+    def update_policy(self, data: DataProto):
+        """dp_actor.py:351-486 — PPO epochs x mini-batches x micro-batches; one optimizer step per
+        mini-batch; returns {metric: [values]}."""
+        self.actor_module.train()
+        temperature = data.meta_info["temperature"]
+        cfg = self.config
+        keys = ["responses", "response_mask", "input_ids", "attention_mask", "position_ids", "old_log_probs",
+                "advantages"]
+        if cfg.use_kl_loss:
+            keys.append("ref_log_prob")
+        data = data.select(batch_keys=keys)
+        if cfg.use_dynamic_bsz:
+            raise NotImplementedError("dynamic token-budget micro-batching (seqlen_balancing) is not yet ported")
+        mini_batches = data.split(cfg.ppo_mini_batch_size)
+        self.gradient_accumulation = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
+        clip_ratio = cfg.clip_ratio
+        clip_low = cfg.clip_ratio_low if cfg.get("clip_ratio_low") is not None else clip_ratio
+        clip_high = cfg.clip_ratio_high if cfg.get("clip_ratio_high") is not None else clip_ratio
+        clip_c = cfg.get("clip_ratio_c", 3.0)
+        entropy_coeff = cfg.entropy_coeff
+        agg_mode = cfg.loss_agg_mode
+        loss_mode = cfg.policy_loss.get("loss_mode", "vanilla")
+
+        dev_metrics: dict[str, list] = {}
+        for _ in range(cfg.ppo_epochs):
+            for mini in mini_batches:
+                micro_batches = mini.split(cfg.ppo_micro_batch_size_per_gpu)
+                plans = self._plans(mini, [len(m) for m in micro_batches])
+                self._zero_grad()
+                for i, (mb, plan) in enumerate(zip(micro_batches, plans, strict=True)):
+                    b = mb.batch
+                    response_mask = b["response_mask"]
+                    calc_ent = entropy_coeff != 0
+                    entropy, log_prob = self._forward_micro_batch(b, temperature, calc_ent, plan)
+                    m = {}
+                    if loss_mode == "vanilla":
+                        out = core_algos.compute_actor_loss(
+                            b["old_log_probs"], log_prob, b["advantages"], response_mask, clip_low, clip_high,
+                            clip_c, agg_mode, entropy=entropy if calc_ent else None,
+                            ref_log_prob=b["ref_log_prob"] if cfg.use_kl_loss else None,
+                            kl_loss_type=cfg.kl_loss_type if cfg.use_kl_loss else None,
+                        )
+                        pg_loss, pg_clipfrac = out[L.VA_LOSS_PG], out[L.VA_LOSS_CLIPFRAC]
+                        ppo_kl, pg_clipfrac_lower = out[L.VA_LOSS_PPO_KL], out[L.VA_LOSS_CLIPFRAC_LOWER]
+                        policy_loss = pg_loss
+                        if calc_ent:
+                            policy_loss = pg_loss - out[L.VA_LOSS_ENTROPY] * entropy_coeff
+                        if cfg.use_kl_loss:
+                            kl_loss = out[L.VA_LOSS_KL]
+                            policy_loss = policy_loss + kl_loss * cfg.kl_loss_coef
+                            m["actor/kl_loss"] = kl_loss.detach()
+                            m["actor/kl_coef"] = cfg.kl_loss_coef
+                    else:
+                        fn = get_policy_loss_fn(loss_mode)
+                        pg_loss, pg_clipfrac, ppo_kl, pg_clipfrac_lower = fn(
+                            old_log_prob=b["old_log_probs"], log_prob=log_prob, advantages=b["advantages"],
+                            response_mask=response_mask, loss_agg_mode=agg_mode, config=cfg)
+                        policy_loss = pg_loss
+                        if calc_ent:
+                            policy_loss = pg_loss - agg_loss(entropy, response_mask, agg_mode) * entropy_coeff
+                        if cfg.use_kl_loss:
+                            kld = kl_penalty(log_prob, b["ref_log_prob"], cfg.kl_loss_type)
+                            kl_loss = agg_loss(kld, response_mask, agg_mode)
+                            policy_loss = policy_loss + kl_loss * cfg.kl_loss_coef
+                            m["actor/kl_loss"] = kl_loss.detach()
+                            m["actor/kl_coef"] = cfg.kl_loss_coef
+                    loss = policy_loss / self.gradient_accumulation
+                    last = i == len(micro_batches) - 1
+                    if last and self.grad_reducer is not None:
+                        self.grad_reducer.begin_sync()
+                    loss.backward()
+                    m.update({
+                        "actor/pg_loss": pg_loss.detach(),
+                        "actor/pg_clipfrac": pg_clipfrac.detach(),
+                        "actor/ppo_kl": ppo_kl.detach(),
+                        "actor/pg_clipfrac_lower": pg_clipfrac_lower.detach(),
+                    })
+                    append_to_dict(dev_metrics, m)
+                grad_norm = self._optimizer_step()
+                append_to_dict(dev_metrics, {"actor/grad_norm": grad_norm.detach()})
+        self._zero_grad()
+        return _to_host(dev_metrics)
+
+
+def _to_host(dev_metrics: dict) -> dict:
+    """One device->host transfer for every metric of the update (the reference calls .item()
+    per micro-batch, dp_actor.py:462-483)."""
+    keys, vals = [], []
+    for k, lst in dev_metrics.items():
+        for v in lst:
+            keys.append(k)
+            vals.append(v.float().reshape(()) if isinstance(v, torch.Tensor) else torch.tensor(float(v)))
+    if not vals:
+        return {}
+    dev = next((v.device for v in vals if v.is_cuda), torch.device("cpu"))
+    flat = torch.stack([v.to(dev) for v in vals]).cpu().tolist()
+    out: dict[str, list] = {}
+    for k, v in zip(keys, flat, strict=True):
+        out.setdefault(k, []).append(v)
+    return out

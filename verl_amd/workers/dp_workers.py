@@ -1,0 +1,93 @@
+"""Per-GPU actor worker — the update_actor / compute_log_prob surface of
+verl/workers/fsdp_workers.py:105-916 (ActorRolloutRefWorker) without Ray or FSDP.
+
+One process per GPU (launched by torch.distributed.run or by the caller), torch.distributed
+over RCCL for device tensors. Every rank holds full fp32 parameters; gradients are averaged
+with the bucketed all-reduce of grad_sync.py. The DP_COMPUTE_PROTO contract of the reference
+(decorator.py:375-408: chunk the batch by DP rank, run, concat) is available as
+dispatch_dp_compute_data_proto / collect_dp_compute_data_proto for a caller holding the full
+batch; an SPMD caller passes each rank its own shard directly.
+"""
+
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+from ..protocol import DataProto
+from .actor import DataParallelPPOActor
+from .grad_sync import GradBucketReducer
+
+
+def init_distributed(backend: str | None = None) -> tuple[int, int]:
+    """fsdp_workers.py:118-126: init the process group from the torchrun env (127.0.0.1)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local) if backend == "nccl" else None)
+    return rank, world
+
+
+def dispatch_dp_compute_data_proto(data: DataProto, world_size: int) -> list[DataProto]:
+    """decorator.py:375-385: equal chunks, one per DP rank."""
+    return data.chunk(chunks=world_size)
+
+
+def collect_dp_compute_data_proto(outputs: list[DataProto]) -> DataProto:
+    """decorator.py:399-408."""
+    return DataProto.concat(outputs)
+
+
+class ActorWorker:
+    """update_actor / compute_log_prob of the actor role, one per GPU."""
+
+    def __init__(self, config, rollout_n: int = 1):
+        self.config = config
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.world_size = dist.get_world_size() if dist.is_initialized() else 1
+        actor = config.actor
+        # batch-size normalisation, fsdp_workers.py:174-196 (sp = 1)
+        actor.ppo_mini_batch_size = actor.ppo_mini_batch_size * rollout_n // self.world_size
+        assert actor.ppo_mini_batch_size > 0, "ppo_mini_batch_size must be > 0 after normalisation"
+        if actor.get("ppo_micro_batch_size_per_gpu") is None and actor.get("ppo_micro_batch_size") is not None:
+            actor.ppo_micro_batch_size_per_gpu = actor.ppo_micro_batch_size // self.world_size
+        assert actor.ppo_mini_batch_size % actor.ppo_micro_batch_size_per_gpu == 0, (
+            f"normalized ppo_mini_batch_size {actor.ppo_mini_batch_size} should be divisible by "
+            f"ppo_micro_batch_size_per_gpu {actor.ppo_micro_batch_size_per_gpu}"
+        )
+        self.actor = None
+        self.module = None
+
+    def init_model(self, module: torch.nn.Module, bucket_mb: int = 256):
+        """fsdp_workers.py:562-670 (model already built by the caller; AdamW with the actor's optim
+        config, fsdp_workers.py:418-423)."""
+        self.module = module
+        optim = self.config.actor.optim
+        fused = next(module.parameters()).is_cuda
+        opt = torch.optim.AdamW(module.parameters(), lr=optim.lr, betas=tuple(optim.get("betas", (0.9, 0.999))),
+                                weight_decay=optim.get("weight_decay", 0.01), fused=fused)
+        reducer = GradBucketReducer(module.parameters(), bucket_bytes=bucket_mb << 20)
+        self.actor = DataParallelPPOActor(self.config.actor, module, opt, grad_reducer=reducer)
+        return self
+
+    def compute_log_prob(self, data: DataProto) -> DataProto:
+        """fsdp_workers.py:758-800: old_log_probs (+ entropys) for this rank's shard."""
+        data.meta_info.setdefault("micro_batch_size", self.config.rollout.log_prob_micro_batch_size_per_gpu)
+        data.meta_info.setdefault("temperature", self.config.rollout.temperature)
+        data.meta_info.setdefault("use_dynamic_bsz", self.config.rollout.get("log_prob_use_dynamic_bsz", False))
+        lp, ent = self.actor.compute_log_prob(data, calculate_entropy=True)
+        return DataProto.from_dict(tensors={"old_log_probs": lp, "entropys": ent},
+                                   meta_info={"temperature": data.meta_info["temperature"]})
+
+    def update_actor(self, data: DataProto) -> DataProto:
+        """fsdp_workers.py:672-716: one PPO update; metrics in meta_info."""
+        metrics = self.actor.update_policy(data)
+        return DataProto(meta_info={"metrics": metrics})
