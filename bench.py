@@ -49,6 +49,14 @@ def parse():
     return ap.parse_args()
 
 
+_T0 = time.perf_counter()
+
+
+def log(rank, msg):
+    if rank == 0:
+        print(f"[bench +{time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def _barrier(world):
     if world > 1:
         dist.barrier()
@@ -64,7 +72,8 @@ def cpu_baseline(args, rank) -> dict | None:
         return None
     from oracle import reference_ops as ref
 
-    cores = len(os.sched_getaffinity(0))
+    # the box grants a CPU share (OMP_NUM_THREADS=16 there) although affinity lists every host CPU
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(len(os.sched_getaffinity(0)), 16)
     torch.set_num_threads(cores)
     V, rows = 151936, args.cpu_sample_rows
     g = torch.Generator().manual_seed(0)
@@ -133,6 +142,7 @@ def main():
     worker = ActorWorker(cfg, rollout_n=args.n * world)
     model = build_qwen2(args.model, device=dev, seed=0)
     worker.init_model(model)
+    log(rank, f"model ready ({sum(p.numel() for p in model.parameters()) / 1e6:.1f}M params), world={world}")
     batch = make_grpo_batch(args.prompts, args.n, args.prompt_len, R, seed=1234 + rank, device=dev)
     # reference-policy log-probs are an input of the step (ref = new + N(0, 0.1^2))
     with torch.no_grad():
@@ -147,8 +157,11 @@ def main():
         compute_advantage(batch, AdvantageEstimator.GRPO, norm_adv_by_std_in_grpo=True)
         return worker.update_actor(batch)
 
-    for _ in range(args.warmup):
+    log(rank, "batch + reference log-probs ready")
+    for i in range(args.warmup):
         step()
+        torch.cuda.synchronize()
+        log(rank, f"warmup step {i} done")
     torch.cuda.synchronize()
     if not args.no_kernel_timing:
         K.TIMER = K.KernelTimer()
@@ -156,8 +169,9 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     metrics = None
-    for _ in range(args.steps):
+    for i in range(args.steps):
         metrics = step()
+        log(rank, f"timed step {i} issued")
     torch.cuda.synchronize()
     _barrier(world)
     elapsed = time.perf_counter() - t0
@@ -176,9 +190,11 @@ def main():
     tok_s = float(total_tokens[0].item()) * args.steps / elapsed
     perf_throughput = float(total_tokens[1].item()) * args.steps / elapsed / world  # metric_utils.py:249-257
 
+    log(rank, f"timed region: {elapsed:.2f}s for {args.steps} steps")
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, rank)
+        log(rank, f"cpu baseline: {cpu['value']} tokens/s on {cpu['cores']} threads")
 
     if rank == 0:
         roof = None
@@ -229,7 +245,7 @@ def main():
             "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in ksum.items()},
             "cpu_baseline": cpu,
-            "final_metrics": {k: v[-1] for k, v in (metrics.meta_info["metrics"].items() if metrics else [])},
+            "final_metrics": {k: v[-1] for k, v in (metrics.meta_info["metrics"].items() if metrics is not None else [])},
         }
         s = json.dumps(line)
         print(s, flush=True)

@@ -14,4 +14,9 @@ if [[ $STAGE == all || $STAGE == bench ]]; then
   run bench_small 400 python bench.py --prompts 8 --steps 2 --warmup 1 --no-cpu-baseline || exit $?
   run bench 900 python bench.py --steps 3 --warmup 1 --out gpurun_out/bench.json || exit $?
 fi
+
+if [[ $STAGE == prof ]]; then
+  export TMPDIR=/tmp
+  run prof_small 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_small -o run -- python bench.py --prompts 8 --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing || exit $?
+fi
 exit 0

@@ -31,9 +31,14 @@ def varlen_attention_forward(module, query, key, value, attention_mask, scaling=
     if cu is None:
         raise RuntimeError("verl_amd_varlen attention needs cu_seq_lens_q / max_length_q kwargs")
     assert query.shape[0] == 1, "packed varlen attention expects batch 1"
-    q = query[0].transpose(0, 1).contiguous()
-    k = key[0].transpose(0, 1).contiguous()
-    v = value[0].transpose(0, 1).contiguous()
+    # RoPE's fp32 cos/sin promote q/k to fp32 under autocast; flash runs in the autocast dtype
+    if torch.is_autocast_enabled("cuda"):
+        dt = torch.get_autocast_dtype("cuda")
+    else:
+        dt = value.dtype if value.dtype in (torch.float16, torch.bfloat16) else torch.bfloat16
+    q = query[0].transpose(0, 1).to(dt).contiguous()
+    k = key[0].transpose(0, 1).to(dt).contiguous()
+    v = value[0].transpose(0, 1).to(dt).contiguous()
     if scaling is not None and abs(scaling - q.shape[-1] ** -0.5) > 1e-12:
         q = q * (scaling / q.shape[-1] ** -0.5)
     hq, hk = q.shape[1], k.shape[1]
