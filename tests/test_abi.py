@@ -1,0 +1,69 @@
+"""The C-ABI library loads, exports every symbol include/verl_amd.h declares, and the product path
+refuses CPU tensors (no CPU fallback). No compute calls: this runs without a GPU."""
+
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from verl_amd import _lib as L
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not L.LIB_PATH.exists():
+        from verl_amd import build
+
+        build.build()
+    return L.load()
+
+
+def test_header_declares_the_expected_entry_points():
+    syms = L.header_symbols()
+    for s in ["va_logprob_entropy_fwd", "va_logprob_entropy_bwd", "va_ppo_loss_fwd", "va_ppo_loss_bwd",
+              "va_outcome_advantage", "va_gae_advantage_return", "va_whiten_finalize", "va_kl_penalty_fwd"]:
+        assert s in syms
+    assert len(syms) == len(L._SIGNATURES)
+
+
+def test_library_exports_every_header_symbol(lib):
+    raw = ctypes.CDLL(str(L.LIB_PATH))
+    missing = [s for s in L.header_symbols() if not hasattr(raw, s)]
+    assert not missing, missing
+    assert set(L.header_symbols()) == set(L._SIGNATURES)
+
+
+def test_abi_version_and_workspace_queries(lib):
+    assert lib.va_abi_version() == 1
+    assert lib.va_ppo_loss_workspace_bytes(10) == 8 * (10 * 8 + 8)
+    assert lib.va_gae_workspace_bytes(7) == 8 * (7 * 3 + 4)
+
+
+def test_argument_validation_without_device(lib):
+    # invalid shapes are rejected before any HIP call
+    rc = lib.va_logprob_entropy_fwd(None, 1, 4, 0, 0, None, 1.0, None, None, None, None)
+    assert rc == -1 and b"vocab" in lib.va_last_error()
+    rc = lib.va_ppo_loss_fwd(None, None, None, None, 0, None, None, 0, 5, 0.8, 1.2, 3.0, 0, -1, None, None, None)
+    assert rc == -1 and b"empty batch" in lib.va_last_error()
+    assert lib.va_logprob_entropy_fwd(None, 1, 0, 10, 10, None, 1.0, None, None, None, None) == 0  # n_rows 0: no-op
+
+
+def test_product_path_rejects_cpu_tensors():
+    from verl_amd import kernels as K
+    from verl_amd.trainer.ppo import core_algos
+
+    x = torch.randn(2, 5)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        K.logprob_entropy(x, torch.zeros(2, dtype=torch.long))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        core_algos.compute_policy_loss(x, x, x, torch.ones(2, 5), cliprange=0.2)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        core_algos.compute_grpo_outcome_advantage(x, torch.ones(2, 5), np.array([0, 0]))
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(L, "_lib", None)
+    monkeypatch.setattr(L, "LIB_PATH", tmp_path / "nope.so")
+    with pytest.raises(L.NativeLibraryError, match="missing"):
+        L.load()

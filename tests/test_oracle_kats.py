@@ -1,0 +1,151 @@
+"""Pin the oracle (CPU restatement) to the reference's own known-answer tests and properties,
+plus KATs hand-derived from the reference source. CPU only."""
+
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import reference_ops as ref
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "golden_config1.npz")
+
+
+# --- tests/utils/test_torch_functional.py:55-66 -------------------------------------------------
+@pytest.mark.parametrize(
+    "value,mask,gt",
+    [
+        ([1.0, 2.0, 3.0, 4.0], [1, 0, 0, 1], 2.5),
+        ([1.0, 2.0, float("nan"), 4.0], [1, 0, 0, 1], 2.5),
+        ([1.0, 2.0, float("nan"), 4.0], [1, 0, 1, 0], float("nan")),
+    ],
+)
+def test_masked_mean_reference_kat(value, mask, gt):
+    res = ref.masked_mean(torch.tensor(value), torch.tensor(mask))
+    gt = torch.tensor(gt)
+    assert torch.allclose(res, gt) or (torch.isnan(res) and torch.isnan(gt))
+
+
+# --- tests/trainer/ppo/test_core_algos_on_cpu.py:134-188 ---------------------------------------
+def test_gae_multi_turn_property():
+    gamma, lam = random.uniform(0.0, 1.0), random.uniform(0.0, 1.0)
+    rewards = torch.tensor([[0.0, 0.0, 0.1, 0.1, 0.1, 0.0, 0.0, 0.1, 1.0, 0.0, 0.0]])
+    v1 = torch.tensor([[random.uniform(-100, 100), random.random(), 4.0, 5.0, 6.0, random.uniform(-100, 0),
+                        random.random(), 7.0, 9.0, 0.0, 0.0]])
+    v2 = torch.tensor([[random.random(), random.uniform(-100, 100), 4.0, 5.0, 6.0, random.random(),
+                        random.uniform(0, 100), 7.0, 9.0, 0.0, 0.0]])
+    mask = torch.tensor([[0, 0, 1, 1, 1, 0, 0, 1, 1, 0, 0]], dtype=torch.float)
+    a1, r1 = ref.compute_gae_advantage_return(rewards, v1, mask, gamma, lam)
+    a2, r2 = ref.compute_gae_advantage_return(rewards, v2, mask, gamma, lam)
+    assert torch.equal(a1, a2)
+    assert torch.equal(r1 * mask, r2 * mask)
+
+
+# --- tests/trainer/config/test_algo_config_on_cpu.py:190-192 (hand-derived answer) ----------------
+def test_grpo_algo_config_input_kat():
+    rewards = torch.tensor([[1.0, 0.5, 0.0], [2.0, 1.0, 0.0], [0.5, 0.2, 0.0], [1.5, 0.8, 0.0]])
+    adv, ret = ref.compute_grpo_outcome_advantage(rewards, torch.ones(4, 3), np.array([0, 0, 1, 1]))
+    s = [1.5, 3.0, 0.7, 2.3]
+    for g in (0, 1):
+        a, b = s[2 * g], s[2 * g + 1]
+        sd = abs(a - b) / np.sqrt(2)
+        want = (a - (a + b) / 2) / (sd + 1e-6)
+        assert abs(adv[2 * g, 0].item() - want) < 1e-6
+        assert abs(adv[2 * g + 1, 2].item() + want) < 1e-6
+    assert abs(adv[0, 0].item() + 0.70710611) < 1e-7
+    assert abs(adv[2, 0].item() + 0.70710616) < 1e-7
+    assert torch.equal(adv, ret)
+
+
+# --- hand-derived KATs from the source semantics ------------------------------------
+def test_grpo_singleton_equal_and_unmasked_sum():
+    rewards = torch.zeros(5, 4)
+    rewards[0, 3] = 2.0  # singleton group: A = s / (1 + 1e-6)
+    rewards[1:3, 1] = 0.7  # group of two equal scores: A = 0
+    rewards[3, 0], rewards[3, 3] = 1.0, 1.0  # reward outside the mask still counts (unmasked sum)
+    rewards[4, 0] = 0.0
+    mask = torch.tensor([[1, 1, 1, 1], [1, 1, 0, 0], [1, 1, 1, 1], [1, 1, 0, 0], [1, 1, 1, 1]])
+    adv, _ = ref.compute_grpo_outcome_advantage(rewards, mask, np.array(["a", "b", "b", "c", "c"]))
+    assert abs(adv[0, 0].item() - 2.0 / (1 + 1e-6)) < 1e-6
+    assert torch.all(adv[1:3] == 0)
+    sd = np.sqrt(2.0) * 1.0  # scores 2 and 0: std = sqrt(2)
+    assert abs(adv[3, 0].item() - 1.0 / (sd + 1e-6)) < 1e-6
+    assert adv[3, 2].item() == 0.0  # broadcast times the mask
+
+
+def test_gae_closed_form_gamma_lambda_one():
+    torch.manual_seed(0)
+    r = torch.randn(3, 9, dtype=torch.float64)
+    v = torch.randn(3, 9, dtype=torch.float64)
+    m = torch.ones(3, 9, dtype=torch.float64)
+    m[1, 6:] = 0  # positions right of the last valid token keep g = 0 before whitening
+    raw = torch.zeros_like(r)
+    for b in range(3):
+        n = int(m[b].sum())
+        for t in range(n):
+            raw[b, t] = r[b, t:n].sum() - v[b, t]
+    adv, ret = ref.compute_gae_advantage_return(r, v, m, 1.0, 1.0)
+    assert torch.allclose(ret, raw + v)
+    mu = (raw * m).sum() / m.sum()
+    var = ((raw - mu) ** 2 * m).sum() / m.sum() * m.sum() / (m.sum() - 1)
+    assert torch.allclose(adv, (raw - mu) / torch.sqrt(var + 1e-8))
+    assert torch.allclose(adv[1, 7], -mu / torch.sqrt(var + 1e-8))  # after whitening: -mean*rstd, not 0
+
+
+def test_kl_and_policy_identities():
+    lp = torch.randn(4, 8)
+    for kt in ["kl", "abs", "mse", "low_var_kl"]:
+        assert torch.all(ref.kl_penalty(lp, lp, kt) == 0)
+    with pytest.raises(NotImplementedError):
+        ref.kl_penalty(lp, lp, "full")
+    adv = torch.randn(4, 8)
+    m = torch.ones(4, 8)
+    pg, cf, kl, cfl = ref.compute_policy_loss(lp, lp, adv, m, cliprange=0.2)
+    assert cf.item() == 0 and kl.item() == 0 and cfl.item() == 0
+    assert torch.allclose(pg, -adv.mean())
+    with pytest.raises(AssertionError):
+        ref.compute_policy_loss(lp, lp, adv, m, cliprange=0.2, clip_ratio_c=1.0)
+    with pytest.raises(ValueError, match="Invalid loss_agg_mode"):
+        ref.agg_loss(lp, m, "bogus")
+
+
+def test_masked_var_errors():
+    x = torch.randn(2, 3)
+    with pytest.raises(ValueError, match="At least one element"):
+        ref.masked_var(x, torch.zeros(2, 3))
+    m = torch.zeros(2, 3)
+    m[0, 0] = 1
+    with pytest.raises(ValueError, match="sum of the mask is one"):
+        ref.masked_var(x, m)
+
+
+def test_torch_autograd_tie_semantics():
+    """The backward of the reference expression relies on these torch rules (parity of the
+    fused kernel's tie handling is checked against them in the GPU tests)."""
+    a = torch.tensor([1.0, 2.0], requires_grad=True)
+    b = torch.tensor([1.0, 1.0], requires_grad=True)
+    torch.maximum(a, b).sum().backward()
+    assert a.grad.tolist() == [0.5, 1.0] and b.grad.tolist() == [0.5, 0.0]
+    a.grad = b.grad = None
+    torch.min(a, b).sum().backward()
+    assert a.grad.tolist() == [0.5, 0.0] and b.grad.tolist() == [0.5, 1.0]
+    x = torch.tensor([0.8, 1.2, 0.5], requires_grad=True)
+    torch.clamp(x, 0.8, 1.2).sum().backward()
+    assert x.grad.tolist() == [1.0, 1.0, 0.0]
+
+
+# --- golden fixtures: the oracle reproduces its frozen outputs ----------------------------------
+def test_oracle_reproduces_golden_fixtures():
+    from tests.golden import make_golden
+
+    want = np.load(GOLDEN, allow_pickle=False)
+    got = make_golden.build()
+    assert set(want.files) == set(got.keys())
+    for k in want.files:
+        a, b = want[k], got[k]
+        if a.dtype.kind in "fc":
+            assert np.array_equal(a, b, equal_nan=True), k
+        else:
+            assert np.array_equal(a, b), k

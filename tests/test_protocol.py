@@ -1,0 +1,183 @@
+"""DataProto semantics (mirror of the reference's tests/test_protocol_on_cpu.py behaviours). CPU only."""
+
+import pickle
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from verl_amd.protocol import (
+    DataProto,
+    DataProtoConfig,
+    TensorBatch,
+    fold_batch_dim,
+    pad_dataproto_to_divisor,
+    union_numpy_dict,
+    union_tensor_dict,
+    unfold_batch_dim,
+    unpad_dataproto,
+)
+
+
+def _dp():
+    return DataProto.from_dict(tensors={"obs": torch.tensor([[1, 2], [3, 4], [5, 6]])}, non_tensors={"labels": ["a", "b", "c"]},
+                               meta_info={"info": "test_info"})
+
+
+def test_union():
+    obs = torch.randn(10, 3)
+    d1 = TensorBatch({"obs": obs, "act": torch.randn(10, 2)})
+    d2 = TensorBatch({"obs": obs, "rew": torch.randn(10)})
+    d = union_tensor_dict(d1, d2)
+    assert set(d.keys()) == {"obs", "act", "rew"}
+    with pytest.raises(AssertionError):
+        union_tensor_dict(d1, TensorBatch({"obs": obs + 1}))
+    a = np.random.random(5)
+    b = np.array([float("nan")] * 4 + ["nan"], dtype=object)
+    x = {"a": a, "b": b, "c": np.tile(b, (2, 1))}
+    union_numpy_dict(x, {"a": a, "b": b.copy(), "c": np.tile(b, (2, 1))})
+    with pytest.raises(AssertionError):
+        union_numpy_dict(x, {"a": np.random.random(5)})
+
+
+def test_constructor_batch_dims():
+    d = DataProto.from_dict(tensors={"obs": torch.randn(100, 10), "act": torch.randn(100, 10, 3)})
+    assert d.batch.batch_size == torch.Size([100])
+    with pytest.raises(AssertionError):
+        DataProto.from_dict(tensors={"obs": torch.randn(100, 10), "act": torch.randn(100, 10, 3)}, num_batch_dims=2)
+    with pytest.raises(AssertionError):
+        DataProto.from_dict(tensors={"obs": torch.randn(5, 2), "act": torch.randn(6, 2)})
+
+
+def test_make_iterator_deterministic():
+    ds = DataProto.from_dict(tensors={"obs": torch.randn(100, 10)},
+                             non_tensors={"labels": [random.choice(["x", "y"]) for _ in range(100)]})
+    a = list(ds.make_iterator(mini_batch_size=10, epochs=2, seed=1, dataloader_kwargs={"shuffle": True}))
+    b = list(ds.make_iterator(mini_batch_size=10, epochs=2, seed=1, dataloader_kwargs={"shuffle": True}))
+    assert len(a) == 20
+    for x, y in zip(a, b, strict=True):
+        assert torch.equal(x.batch["obs"], y.batch["obs"])
+        assert np.array_equal(x.non_tensor_batch["labels"], y.non_tensor_batch["labels"])
+
+
+def test_reorder_chunk_concat():
+    d = DataProto.from_dict(tensors={"obs": torch.tensor([1, 2, 3, 4, 5, 6])}, non_tensors={"labels": list("abcdef")},
+                            meta_info={"name": "x"})
+    d.reorder(torch.tensor([3, 4, 2, 0, 1, 5]))
+    assert d.batch["obs"].tolist() == [4, 5, 3, 1, 2, 6]
+    assert list(d.non_tensor_batch["labels"]) == list("decabf")
+    with pytest.raises(AssertionError):
+        d.chunk(5)
+    parts = d.chunk(2)
+    assert parts[0].batch["obs"].tolist() == [4, 5, 3] and parts[0].meta_info == {"name": "x"}
+    back = DataProto.concat(parts)
+    assert back.batch["obs"].tolist() == [4, 5, 3, 1, 2, 6]
+    assert list(back.non_tensor_batch["labels"]) == list("decabf")
+
+
+def test_chunk_auto_padding():
+    d = DataProto.from_dict(tensors={"obs": torch.arange(7)}, non_tensors={"l": list("abcdefg")})
+    DataProtoConfig.auto_padding = True
+    try:
+        parts = d.chunk(3)
+    finally:
+        DataProtoConfig.auto_padding = False
+    assert [len(p) for p in parts] == [3, 3, 1]
+    assert [len(p.non_tensor_batch["l"]) for p in parts] == [3, 3, 1]
+
+
+def test_pop_select_rename():
+    d = DataProto.from_dict(tensors={"a": torch.zeros(4), "b": torch.ones(4)}, non_tensors={"n": list("wxyz")},
+                            meta_info={"m": 1, "k": 2})
+    p = d.pop(batch_keys=["a"], meta_info_keys=["m"])
+    assert list(p.batch.keys()) == ["a"] and p.meta_info == {"m": 1}
+    assert list(d.batch.keys()) == ["b"] and d.meta_info == {"k": 2}
+    s = d.select(batch_keys=["b"], non_tensor_batch_keys=[])
+    assert s.non_tensor_batch == {}
+    d.rename("b", "c")
+    assert "c" in d.batch.keys()
+    with pytest.raises(ValueError):
+        d.rename(["c"], ["x", "y"])
+
+
+def test_repeat_and_sample_level_repeat():
+    d = _dp()
+    r = d.repeat(2, interleave=True)
+    assert r.batch["obs"].tolist() == [[1, 2], [1, 2], [3, 4], [3, 4], [5, 6], [5, 6]]
+    assert list(r.non_tensor_batch["labels"]) == ["a", "a", "b", "b", "c", "c"]
+    r = d.repeat(2, interleave=False)
+    assert r.batch["obs"].tolist() == [[1, 2], [3, 4], [5, 6], [1, 2], [3, 4], [5, 6]]
+    s = d.sample_level_repeat([3, 1, 2])
+    assert list(s.non_tensor_batch["labels"]) == ["a", "a", "a", "b", "c", "c"]
+    s = d.sample_level_repeat(torch.tensor([1, 2, 3]))
+    assert s.batch["obs"].tolist() == [[1, 2], [3, 4], [3, 4], [5, 6], [5, 6], [5, 6]]
+
+
+@pytest.mark.parametrize("div,pad,obs", [(2, 1, [[1, 2], [3, 4], [5, 6], [1, 2]]), (3, 0, [[1, 2], [3, 4], [5, 6]]),
+                                         (7, 4, [[1, 2], [3, 4], [5, 6], [1, 2], [3, 4], [5, 6], [1, 2]])])
+def test_pad_unpad(div, pad, obs):
+    d = _dp()
+    p, ps = pad_dataproto_to_divisor(d, div)
+    assert ps == pad and p.batch["obs"].tolist() == obs and p.meta_info == {"info": "test_info"}
+    u = unpad_dataproto(p, ps)
+    assert torch.equal(u.batch["obs"], d.batch["obs"])
+    assert list(u.non_tensor_batch["labels"]) == ["a", "b", "c"]
+
+
+def test_fold_unfold():
+    d = _dp().repeat(2, interleave=True)
+    f = fold_batch_dim(d, new_batch_size=3)
+    assert f.batch["obs"].tolist() == [[[1, 2], [1, 2]], [[3, 4], [3, 4]], [[5, 6], [5, 6]]]
+    f.reorder(torch.tensor([1, 2, 0]))
+    u = unfold_batch_dim(f, batch_dims=2)
+    assert u.batch["obs"].tolist() == [[3, 4], [3, 4], [5, 6], [5, 6], [1, 2], [1, 2]]
+    assert list(u.non_tensor_batch["labels"]) == ["b", "b", "c", "c", "a", "a"]
+
+
+def test_pickle_roundtrip_and_disk(tmp_path):
+    d = _dp()
+    e = pickle.loads(pickle.dumps(d))
+    assert torch.equal(e.batch["obs"], d.batch["obs"]) and e.meta_info == d.meta_info
+    path = tmp_path / "d.pkl"
+    d.save_to_disk(str(path))
+    f = DataProto.load_from_disk(str(path))
+    assert list(f.non_tensor_batch["labels"]) == ["a", "b", "c"]
+
+
+@pytest.mark.parametrize("kind", ["np_int", "torch_int", "list_int", "np_bool", "torch_bool", "list_bool"])
+def test_index_forms(kind):
+    n = 20
+    obs = torch.randn(n, 3)
+    labels = np.array([f"l{i}" for i in range(n)], dtype=object)
+    d = DataProto.from_dict(tensors={"obs": obs}, non_tensors={"labels": labels})
+    rng = np.random.RandomState(0)
+    idx = {
+        "np_int": rng.randint(0, n, 6),
+        "torch_int": torch.from_numpy(rng.randint(0, n, 6)),
+        "list_int": [int(x) for x in rng.randint(0, n, 6)],
+        "np_bool": rng.randint(0, 2, n).astype(bool),
+        "torch_bool": torch.from_numpy(rng.randint(0, 2, n).astype(bool)),
+        "list_bool": [bool(x) for x in rng.randint(0, 2, n)],
+    }[kind]
+    s = d[idx]
+    ref_idx = np.asarray(idx.numpy() if isinstance(idx, torch.Tensor) else idx)
+    assert torch.equal(s.batch["obs"], obs[torch.as_tensor(ref_idx)])
+    assert np.array_equal(s.non_tensor_batch["labels"], labels[ref_idx])
+    assert isinstance(s.batch.batch_size, torch.Size) and all(isinstance(v, int) for v in s.batch.batch_size)
+
+
+def test_slice_int_len_and_no_batch():
+    d = _dp()
+    assert len(d) == 3 and len(d[1:]) == 2 and len(d[::2]) == 2
+    item = d[1]
+    assert item.batch["obs"].tolist() == [3, 4] and item.non_tensor_batch["labels"] == "b"
+    nb = DataProto.from_dict(non_tensors={"labels": ["a", "b", "c"]}, meta_info={"info": 1})
+    assert len(nb) == 3
+    p = nb.pop(non_tensor_batch_keys=["labels"])
+    assert list(p.non_tensor_batch["labels"]) == ["a", "b", "c"] and nb.non_tensor_batch == {}
+
+
+def test_split_matches_reference_micro_batching():
+    d = DataProto.from_dict(tensors={"x": torch.arange(10)})
+    assert [m.batch["x"].tolist() for m in d.split(4)] == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9]]

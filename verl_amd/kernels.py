@@ -232,7 +232,6 @@ def fused_policy_loss(
     Returns the 8-slot vector (see VA_LOSS_* in include/verl_amd.h) whose slots are the scalars
     the reference returns; gradients flow from slots PG, KL and ENTROPY to log_prob / entropy.
     """
-    _require_device(old_log_prob, log_prob, advantages, response_mask, ref_log_prob, entropy)
     assert clip_ratio_c > 1.0, (
         "The lower bound of the clip_ratio_c for dual-clip PPO should be greater than 1.0,"
         + f" but get the value: {clip_ratio_c}."
@@ -244,6 +243,7 @@ def fused_policy_loss(
         if kl_loss_type == "full" or kl_loss_type not in KL_TYPES:
             raise NotImplementedError
         kl_type = KL_TYPES[kl_loss_type]
+    _require_device(old_log_prob, log_prob, advantages, response_mask, ref_log_prob, entropy)
     # torch.clamp casts its python-float bounds to the tensor dtype (fp32)
     clip_lo = float(np.float32(1 - clip_ratio_low))
     clip_hi = float(np.float32(1 + clip_ratio_high))

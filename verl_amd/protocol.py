@@ -535,6 +535,16 @@ def fold_batch_dim(data: DataProto, new_batch_size):
     return out
 
 
+def unfold_batch_dim(data: DataProto, batch_dims=2):
+    """protocol.py:167-183 — inverse of fold_batch_dim: merge the leading ``batch_dims`` dims."""
+    tensors = {k: v.reshape(-1, *v.shape[batch_dims:]) for k, v in data.batch.items()}
+    non_tensor = {k: np.reshape(v, (-1, *v.shape[batch_dims:])) for k, v in data.non_tensor_batch.items()}
+    out = DataProto(batch=None, non_tensor_batch={}, meta_info=data.meta_info)
+    out.batch = TensorBatch(tensors) if tensors else None
+    out.non_tensor_batch = non_tensor
+    return out
+
+
 def all_gather_data_proto(data: DataProto, process_group) -> None:
     """protocol.py:953-964 — in-place all-gather of every batch key and non-tensor array."""
     import torch.distributed as dist
