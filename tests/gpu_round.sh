@@ -19,4 +19,15 @@ if [[ $STAGE == prof ]]; then
   export TMPDIR=/tmp
   run prof_small 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_small -o run -- python bench.py --prompts 8 --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing || exit $?
 fi
+if [[ $STAGE == kbench ]]; then
+  export TMPDIR=/tmp
+  run kbench 600 python tools/kernel_bench.py || exit $?
+  run kb_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kb_trace -o run -- python tools/kernel_bench.py --only logprob --iters 10 || exit $?
+  run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python tools/kernel_bench.py --only logprob --iters 5 || exit $?
+  run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python tools/kernel_bench.py --only logprob --iters 5 || exit $?
+fi
+if [[ $STAGE == dp ]]; then
+  run tests_dp 600 python -m pytest tests/test_dp_gpu.py -q -rf -p no:cacheprovider; rc=$?
+  if [ $rc -ge 2 ]; then exit $rc; fi
+fi
 exit 0
