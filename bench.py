@@ -29,6 +29,23 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+def pmc_traffic(kernel: str, algo_bytes_per_launch: float, vocab: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
+    MI355X_MICROARCH.md §HBM corrections) of the same kernel, scaled to this launch's rows."""
+    import glob
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_logprob.json")))
+    if not paths:
+        return None, None
+    d = json.load(open(paths[-1]))
+    k = d["kernels"].get(kernel)
+    if k is None or d.get("vocab") != vocab:
+        return None, None
+    per_row_algo = k["algo_bytes"] / d["rows_per_launch"]
+    rows = algo_bytes_per_launch / per_row_algo
+    return k["traffic_bytes_per_row"] * rows, os.path.relpath(paths[-1], ROOT)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -201,6 +218,7 @@ def main():
         if ksum:
             dom = max(ksum.items(), key=lambda kv: kv[1]["time_ms_total"])
             name, d = dom
+            traffic, src = pmc_traffic(name, d["avg_bytes"], 151936)
             roof = {
                 "kernel": name,
                 "bound": "hbm",
@@ -208,7 +226,8 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(d["gbps"] / HBM_PEAK_GBPS, 4),
-                "traffic": None,
+                "traffic": round(traffic) if traffic else None,
+                "traffic_source": src,
                 "algo_bytes_per_launch": d["avg_bytes"],
                 "avg_launch_us": round(d["avg_us"], 2),
                 "launches": d["launches"],
