@@ -59,6 +59,7 @@ def parse():
     ap.add_argument("--logprob-micro", type=int, default=16, help="log_prob_micro_batch_size_per_gpu")
     ap.add_argument("--model", default="0.5b")
     ap.add_argument("--no-rmpad", action="store_true")
+    ap.add_argument("--no-mixed-precision", action="store_true", help="fp32 weights + autocast instead of bf16/fp32-master")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=2048)
@@ -158,7 +159,7 @@ def main():
     # weak scaling: every rank owns a full 512-response shard; normalise against world=1
     worker = ActorWorker(cfg, rollout_n=args.n * world)
     model = build_qwen2(args.model, device=dev, seed=0)
-    worker.init_model(model)
+    worker.init_model(model, mixed_precision=not args.no_mixed_precision)
     log(rank, f"model ready ({sum(p.numel() for p in model.parameters()) / 1e6:.1f}M params), world={world}")
     batch = make_grpo_batch(args.prompts, args.n, args.prompt_len, R, seed=1234 + rank, device=dev)
     # reference-policy log-probs are an input of the step (ref = new + N(0, 0.1^2))
@@ -258,6 +259,8 @@ def main():
                 "logprob_micro_batch": args.logprob_micro,
                 "parallelism": f"dp{world}",
                 "remove_padding": not args.no_rmpad,
+                "mixed_precision": "bf16 weights / fp32 master+grads+reduce" if not args.no_mixed_precision
+                else "fp32 weights + bf16 autocast",
             },
             "perf_throughput": round(perf_throughput, 1),
             "roofline": roof,

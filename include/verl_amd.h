@@ -106,6 +106,14 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
                            float temperature, void *dlogits, int64_t dlogits_row_stride,
                            void *stream);
 
+/* Launch-shape knobs of the log-prob kernels (results are identical for every setting):
+ *   VA_TUNE_FWD/BWD_WAVES_PER_ROW: 0 = auto, 1 / 2 / 4 waves stream one row together;
+ *   VA_TUNE_NONTEMPORAL: 1 = non-temporal (streaming) loads/stores of the logits. */
+#define VA_TUNE_FWD_WAVES_PER_ROW 1
+#define VA_TUNE_BWD_WAVES_PER_ROW 2
+#define VA_TUNE_NONTEMPORAL 3
+int va_set_tuning(int key, int value);
+
 /* ---------------------------------------------------------------------------------------
  * Fused vanilla PPO clipped policy loss + optional KL-loss + optional entropy term, with
  * loss aggregation and the three metrics, over one [B, R] micro-batch.

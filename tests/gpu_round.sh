@@ -30,4 +30,10 @@ if [[ $STAGE == dp ]]; then
   run tests_dp 600 python -m pytest tests/test_dp_gpu.py -q -rf -p no:cacheprovider; rc=$?
   if [ $rc -ge 2 ]; then exit $rc; fi
 fi
+if [[ $STAGE == sweep ]]; then
+  export TMPDIR=/tmp
+  run sweep8k 600 python tools/kernel_bench.py --sweep --rows 8192 || exit $?
+  run sweep16k 600 python tools/kernel_bench.py --sweep --rows 16384 || exit $?
+  run small_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/small_trace -o run -- python tools/kernel_bench.py --only small --iters 10 || exit $?
+fi
 exit 0

@@ -71,6 +71,48 @@ def test_grad_bucket_reducer_matches_single_process_mean():
     _run(_reducer_worker)
 
 
+def _mp_worker(rank, world, port):
+    _init(rank, world, port)
+    from verl_amd.workers.grad_sync import MixedPrecisionParams
+
+    model = _model()
+    ref = _model()
+    mp_ = MixedPrecisionParams(model, bucket_bytes=256)
+    assert all(p.dtype == torch.bfloat16 for p in model.parameters())
+    opt = torch.optim.AdamW(mp_.optimizer_params(), lr=1e-2)
+    g = torch.Generator().manual_seed(5)
+    xs = [torch.randn(4, 6, generator=g) for _ in range(world * 2)]
+    mp_.zero_grad()
+    for i, x in enumerate(xs[rank * 2 : rank * 2 + 2]):
+        if i == 1:
+            mp_.begin_sync()
+        (model(x.bfloat16()).float().square().mean() / 2).backward()
+    mp_.finish_sync()
+    # fp32 gradient buckets hold the rank-mean of bf16 gradients (accumulated in fp32)
+    refp = {n: p for n, p in ref.named_parameters()}
+    bf = _model()
+    for p in bf.parameters():
+        p.data = p.data.bfloat16()
+    for x in xs:
+        (bf(x.bfloat16()).float().square().mean() / (2 * world)).backward()
+    for (n, p), m in zip(bf.named_parameters(), mp_.optimizer_params(), strict=True):
+        assert torch.allclose(m.grad, p.grad.float(), atol=2e-2, rtol=2e-2), n
+        assert torch.equal(m.data, refp[n].data)  # masters start as the fp32 init
+    opt.step()
+    mp_.after_step()
+    for p, m in zip(model.parameters(), mp_.optimizer_params(), strict=True):
+        assert torch.equal(p.data, m.data.bfloat16())
+    flat = torch.cat([m.detach().reshape(-1) for m in mp_.optimizer_params()])
+    other = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(other, flat)
+    assert torch.equal(other[0], other[1])
+    dist.destroy_process_group()
+
+
+def test_mixed_precision_params_dp():
+    _run(_mp_worker)
+
+
 # ------------------------------------------------------------------ distributed stats
 def _stats_worker(rank, world, port):
     _init(rank, world, port)

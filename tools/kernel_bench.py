@@ -52,12 +52,54 @@ def report(name, nbytes, med_ms, min_ms, copy_gbps, extra=None):
     return d
 
 
+def sweep(args, src, copy_gbps):
+    """Interleaved A/B of waves-per-row x non-temporal for fwd and bwd (guide rule 24)."""
+    dev = src.device
+    x = src.view(args.rows, args.vocab)
+    labels = torch.randint(0, args.vocab, (args.rows,), device=dev)
+    lp, ent, lse = (torch.empty(args.rows, device=dev) for _ in range(3))
+    g1 = torch.randn(args.rows, device=dev)
+    dx = torch.empty_like(x)
+    lib = L.load()
+    st = K._stream(x)
+
+    def fwd():
+        L.call("va_logprob_entropy_fwd", K._p(x), L.VA_BF16, args.rows, args.vocab, args.vocab, K._p(labels), 1.0,
+               K._p(lp), K._p(ent), K._p(lse), st)
+
+    def bwd():
+        L.call("va_logprob_entropy_bwd", K._p(g1), None, K._p(x), L.VA_BF16, args.rows, args.vocab, args.vocab,
+               K._p(labels), K._p(lse), K._p(ent), 1.0, K._p(dx), args.vocab, st)
+
+    fwd()
+    variants = [(w, nt) for w in (1, 2, 4) for nt in (0, 1)]
+    times = {("fwd",) + v: [] for v in variants}
+    times.update({("bwd",) + v: [] for v in variants})
+    for _ in range(5):
+        for w, nt in variants:
+            lib.va_set_tuning(L.VA_TUNE_FWD_WAVES_PER_ROW, w)
+            lib.va_set_tuning(L.VA_TUNE_BWD_WAVES_PER_ROW, w)
+            lib.va_set_tuning(L.VA_TUNE_NONTEMPORAL, nt)
+            times[("fwd", w, nt)].append(timeit(fwd, 5, warmup=1)[0])
+            times[("bwd", w, nt)].append(timeit(bwd, 5, warmup=1)[0])
+    fb = args.rows * (2 * args.vocab + 20)
+    bb = args.rows * (4 * args.vocab + 28)
+    for k, ts in times.items():
+        nb = fb if k[0] == "fwd" else bb
+        med = float(np.median(ts))
+        print(json.dumps(dict(kernel=f"{k[0]}_wpr{k[1]}_nt{k[2]}", median_us=round(med * 1e3, 1),
+                              min_us=round(min(ts) * 1e3, 1), gbps=round(nb / (med * 1e-3) / 1e9, 1))), flush=True)
+    for key in (L.VA_TUNE_FWD_WAVES_PER_ROW, L.VA_TUNE_BWD_WAVES_PER_ROW, L.VA_TUNE_NONTEMPORAL):
+        lib.va_set_tuning(key, 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=8192)
     ap.add_argument("--vocab", type=int, default=151936)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="all")
+    ap.add_argument("--sweep", action="store_true", help="A/B the log-prob launch shapes (interleaved rounds)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -71,6 +113,10 @@ def main():
     copy_gbps = 2 * n_el * 2 / (med * 1e-3) / 1e9
     print(json.dumps(dict(kernel="device_copy_bf16", avg_us=round(med * 1e3, 1), gbps=round(copy_gbps, 1))), flush=True)
     del dst
+
+    if args.sweep:
+        sweep(args, src, copy_gbps)
+        return
 
     if args.only in ("all", "logprob"):
         logits = (src.view(args.rows, args.vocab) * 2.0)

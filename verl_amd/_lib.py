@@ -25,12 +25,14 @@ VA_KL_NONE, VA_KL_K1, VA_KL_ABS, VA_KL_K2, VA_KL_K3 = -1, 0, 1, 2, 3
 VA_ADV_GRPO, VA_ADV_GRPO_NOSTD, VA_ADV_RLOO, VA_ADV_MEAN_ONLY = 0, 1, 2, 3
 VA_LOSS_PG, VA_LOSS_CLIPFRAC, VA_LOSS_PPO_KL, VA_LOSS_CLIPFRAC_LOWER = 0, 1, 2, 3
 VA_LOSS_KL, VA_LOSS_ENTROPY, VA_LOSS_NTOKENS, VA_LOSS_NROWS, VA_LOSS_NOUT = 4, 5, 6, 7, 8
+VA_TUNE_FWD_WAVES_PER_ROW, VA_TUNE_BWD_WAVES_PER_ROW, VA_TUNE_NONTEMPORAL = 1, 2, 3
 
 _P = c_void_p
 _SIGNATURES: dict[str, tuple] = {
     "va_abi_version": (c_int, []),
     "va_last_error": (ctypes.c_char_p, []),
     "va_device_info": (c_int, [POINTER(c_int), POINTER(c_int), POINTER(c_int)]),
+    "va_set_tuning": (c_int, [c_int, c_int]),
     "va_logprob_entropy_fwd": (c_int, [_P, c_int, c_int64, c_int64, c_int64, _P, c_float, _P, _P, _P, _P]),
     "va_logprob_entropy_bwd": (
         c_int,

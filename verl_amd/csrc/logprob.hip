@@ -154,70 +154,152 @@ __device__ __forceinline__ void acc_merge(Acc &a, float om, float os, float ot) 
   a.m = nm;
 }
 
+// ---- 16-byte vector access ------------------------------------------------------------
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ u32x4 vload(const u32x4 *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void vstore(u32x4 *p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// element k of a 16-byte vector, as fp32
+template <typename T>
+__device__ __forceinline__ float elem(const u32x4 &r, int k);
+template <>
+__device__ __forceinline__ float elem<float>(const u32x4 &r, int k) { return __uint_as_float(r[k]); }
+template <>
+__device__ __forceinline__ float elem<bf16_t>(const u32x4 &r, int k) {
+  return (k & 1) ? bf16_hi(r[k >> 1]) : bf16_lo(r[k >> 1]);
+}
+template <>
+__device__ __forceinline__ float elem<f16_t>(const u32x4 &r, int k) {
+  const uint32_t w = r[k >> 1];
+  return f16_to_f32(static_cast<uint16_t>((k & 1) ? (w >> 16) : (w & 0xffffu)));
+}
+template <typename T>
+__device__ __forceinline__ u32x4 pack_vec(const float *x) {
+  const uint4 q = Elem<T>::pack(x);
+  u32x4 r = {q.x, q.y, q.z, q.w};
+  return r;
+}
+
+// Online-softmax update with U raw vectors. Without temperature the fp32 values are re-derived
+// from the raw registers in each pass (one VALU op each) instead of being kept live, which keeps
+// the kernel at <= 64 VGPRs (8 waves per SIMD).
+template <typename T, int U, bool SCALE>
+__device__ __forceinline__ void acc_raw(Acc &a, const u32x4 *raw, float temperature) {
+  constexpr int VEC = Elem<T>::kVec;
+  if constexpr (SCALE) {
+    float x[U * VEC];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) x[u * VEC + k] = Elem<T>::scale(elem<T>(raw[u], k), temperature);
+    acc_chunk<U * VEC>(a, x);
+  } else {
+    float cm = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) cm = fmaxf(cm, elem<T>(raw[u], k));
+    const float nm = fmaxf(a.m, cm);
+    const float nb = base_of(nm);
+    const float alpha = __builtin_amdgcn_exp2f(base_of(a.m) - nb);
+    float s0 = 0.f, s1 = 0.f, t0 = 0.f, t1 = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < VEC; k += 2) {
+        const float x0 = elem<T>(raw[u], k), x1 = elem<T>(raw[u], k + 1);
+        const float e0 = __builtin_amdgcn_exp2f(fmaf(x0, kLog2e, -nb));
+        const float e1 = __builtin_amdgcn_exp2f(fmaf(x1, kLog2e, -nb));
+        s0 += e0;
+        s1 += e1;
+        t0 = fmaf(e0, x0, t0);
+        t1 = fmaf(e1, x1, t1);
+      }
+    a.s = fmaf(a.s, alpha, s0 + s1);
+    a.t = fmaf(a.t, alpha, t0 + t1);
+    a.m = nm;
+  }
+}
+
 // ---- forward ---------------------------------------------------------------------------
-template <typename T, bool SCALE, bool VECTOR>
-__global__ __launch_bounds__(256) void logprob_entropy_fwd_kernel(
+// A 256-thread workgroup = 4 waves = 4/WPR rows; the WPR waves of a row interleave 1 KiB
+// segments of it and merge their accumulators through LDS.
+template <typename T, bool SCALE, bool VECTOR, int WPR, bool NT>
+__global__ __launch_bounds__(256, 8) void logprob_entropy_fwd_kernel(
     const T *__restrict__ logits, int64_t n_rows, int64_t V, int64_t stride,
     const int64_t *__restrict__ labels, float temperature, float *__restrict__ logp,
     float *__restrict__ entropy, float *__restrict__ lse_out) {
   using E = Elem<T>;
   constexpr int VEC = E::kVec;
-  const int lane = threadIdx.x & 63;
-  const int64_t row = static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= n_rows) return;  // wave-uniform
-  const T *xr = logits + row * stride;
-
+  constexpr int RPB = 4 / WPR;
+  constexpr int STEP = kWave * WPR;
+  __shared__ float sh[4][3];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int part = wave % WPR;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * RPB + wave / WPR;
+  const bool active = row < n_rows;
   Acc a{-INFINITY, 0.f, 0.f};
-  int64_t tail_begin = 0;
-  if constexpr (VECTOR) {
-    const uint4 *xv = reinterpret_cast<const uint4 *>(xr);
-    const int64_t nvec = V / VEC;
-    int64_t i = lane;
-    for (; i + (kUnroll - 1) * kWave < nvec; i += kUnroll * kWave) {
-      uint4 raw[kUnroll];
+  if (active) {
+    const T *xr = logits + row * stride;
+    int64_t tail_begin = 0;
+    if constexpr (VECTOR) {
+      const u32x4 *xv = reinterpret_cast<const u32x4 *>(xr);
+      const int64_t nvec = V / VEC;
+      int64_t i = static_cast<int64_t>(part) * kWave + lane;
+      for (; i + (kUnroll - 1) * STEP < nvec; i += kUnroll * STEP) {
+        u32x4 raw[kUnroll];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) raw[u] = xv[i + u * kWave];
-      float x[kUnroll * VEC];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) E::unpack(raw[u], x + u * VEC);
-      if constexpr (SCALE) {
-#pragma unroll
-        for (int k = 0; k < kUnroll * VEC; ++k) x[k] = E::scale(x[k], temperature);
+        for (int u = 0; u < kUnroll; ++u) raw[u] = vload<NT>(xv + i + u * STEP);
+        acc_raw<T, kUnroll, SCALE>(a, raw, temperature);
       }
-      acc_chunk<kUnroll * VEC>(a, x);
-    }
-    for (; i < nvec; i += kWave) {
-      float x[VEC];
-      E::unpack(xv[i], x);
-      if constexpr (SCALE) {
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) x[k] = E::scale(x[k], temperature);
+      for (; i < nvec; i += STEP) {
+        const u32x4 r = vload<NT>(xv + i);
+        acc_raw<T, 1, SCALE>(a, &r, temperature);
       }
-      acc_chunk<VEC>(a, x);
+      tail_begin = nvec * VEC;
     }
-    tail_begin = nvec * VEC;
-  }
-  for (int64_t j = tail_begin + lane; j < V; j += kWave) {
-    float x = E::load1(xr + j);
-    if constexpr (SCALE) x = E::scale(x, temperature);
-    acc_chunk<1>(a, &x);
-  }
-
+    for (int64_t j = tail_begin + static_cast<int64_t>(part) * kWave + lane; j < V; j += STEP) {
+      float x = E::load1(xr + j);
+      if constexpr (SCALE) x = E::scale(x, temperature);
+      acc_chunk<1>(a, &x);
+    }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float om = __shfl_xor(a.m, o, kWave);
-    const float os = __shfl_xor(a.s, o, kWave);
-    const float ot = __shfl_xor(a.t, o, kWave);
-    acc_merge(a, om, os, ot);
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(a.m, o, kWave);
+      const float os = __shfl_xor(a.s, o, kWave);
+      const float ot = __shfl_xor(a.t, o, kWave);
+      acc_merge(a, om, os, ot);
+    }
   }
-
-  if (lane == 0) {
+  if constexpr (WPR > 1) {
+    if (lane == 0) {
+      sh[wave][0] = a.m;
+      sh[wave][1] = a.s;
+      sh[wave][2] = a.t;
+    }
+    __syncthreads();
+    if (part == 0 && lane == 0 && active) {
+#pragma unroll
+      for (int w = 1; w < WPR; ++w) acc_merge(a, sh[wave + w][0], sh[wave + w][1], sh[wave + w][2]);
+    }
+  }
+  if (part == 0 && lane == 0 && active) {
+    const T *xr = logits + row * stride;
     // lse = m + ln(s) + ln 2 * (B(m) - m L): keeps the max exact and corrects fl(m L)
     float lse;
     if (a.m == -INFINITY) {
       lse = -INFINITY;
     } else {
-      const float corr = -fmaf(a.m, kLog2e, -base_of(a.m));  // B(m) - m*L, |corr| <= ulp/2
+      const float corr = -fmaf(a.m, kLog2e, -base_of(a.m));
       lse = a.m + kLn2 * (__builtin_amdgcn_logf(a.s) + corr);
     }
     lse_out[row] = lse;
@@ -238,17 +320,20 @@ __global__ __launch_bounds__(256) void logprob_entropy_fwd_kernel(
 }
 
 // ---- backward --------------------------------------------------------------------------
-template <typename T, bool SCALE, bool VECTOR>
-__global__ __launch_bounds__(256) void logprob_entropy_bwd_kernel(
+template <typename T, bool SCALE, bool VECTOR, int WPR, bool NT>
+__global__ __launch_bounds__(256, 8) void logprob_entropy_bwd_kernel(
     const float *__restrict__ g_logp, const float *__restrict__ g_ent, const T *logits,
     int64_t n_rows, int64_t V, int64_t stride, const int64_t *__restrict__ labels,
     const float *__restrict__ lse_in, const float *__restrict__ ent_in, float temperature,
     T *dlogits, int64_t dstride) {
   using E = Elem<T>;
   constexpr int VEC = E::kVec;
-  const int lane = threadIdx.x & 63;
-  const int64_t row = static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= n_rows) return;
+  constexpr int RPB = 4 / WPR;
+  constexpr int STEP = kWave * WPR;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int part = wave % WPR;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * RPB + wave / WPR;
+  if (row >= n_rows) return;  // no barrier below
   const T *xr = logits + row * stride;
   T *dr = dlogits + row * dstride;
 
@@ -258,62 +343,90 @@ __global__ __launch_bounds__(256) void logprob_entropy_bwd_kernel(
   const float gh = (g_ent != nullptr) ? g_ent[row] : 0.f;
   const float lse = lse_in[row];
   const float h = (g_ent != nullptr) ? ent_in[row] : 0.f;
-  const float inv_out = SCALE ? 1.f / temperature : 1.f;
 
-  // dz_j = -p_j * (glp + gh * (log p_j + H)) + glp * [j == label]
-  auto grad = [&](float z, int64_t j) -> float {
+  // dz_j = -p_j * (glp + gh * (log p_j + H)) + glp * [j == label];  dx = dz / T
+  auto grad = [&](float z, bool is_lab) -> float {
     const float lp = z - lse;
     const float p = __builtin_amdgcn_exp2f(lp * kLog2e);
     float d = -p * fmaf(gh, lp + h, glp);
-    if (j == lab) d += glp;
+    if (is_lab) d += glp;
     if constexpr (SCALE) d = d / temperature;
     return d;
   };
-  (void)inv_out;
 
   int64_t tail_begin = 0;
   if constexpr (VECTOR) {
-    const uint4 *xv = reinterpret_cast<const uint4 *>(xr);
-    uint4 *dv = reinterpret_cast<uint4 *>(dr);
+    const u32x4 *xv = reinterpret_cast<const u32x4 *>(xr);
+    u32x4 *dv = reinterpret_cast<u32x4 *>(dr);
     const int64_t nvec = V / VEC;
-    int64_t i = lane;
-    for (; i + (kUnroll - 1) * kWave < nvec; i += kUnroll * kWave) {
-      uint4 raw[kUnroll];
+    const int64_t lab_vec = has_lab ? lab / VEC : -1;
+    const int lab_k = has_lab ? static_cast<int>(lab % VEC) : -1;
+    int64_t i = static_cast<int64_t>(part) * kWave + lane;
+    for (; i + (kUnroll - 1) * STEP < nvec; i += kUnroll * STEP) {
+      u32x4 raw[kUnroll];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) raw[u] = xv[i + u * kWave];
+      for (int u = 0; u < kUnroll; ++u) raw[u] = vload<NT>(xv + i + u * STEP);
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
+        const int hit = (i + u * STEP == lab_vec) ? lab_k : -1;
         float x[VEC];
-        E::unpack(raw[u], x);
-        const int64_t j0 = (i + u * kWave) * VEC;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-          float z = x[k];
+          float z = elem<T>(raw[u], k);
           if constexpr (SCALE) z = E::scale(z, temperature);
-          x[k] = grad(z, j0 + k);
+          x[k] = grad(z, k == hit);
         }
-        dv[i + u * kWave] = E::pack(x);
+        vstore<NT>(dv + i + u * STEP, pack_vec<T>(x));
       }
     }
-    for (; i < nvec; i += kWave) {
+    for (; i < nvec; i += STEP) {
+      const u32x4 r = vload<NT>(xv + i);
+      const int hit = (i == lab_vec) ? lab_k : -1;
       float x[VEC];
-      E::unpack(xv[i], x);
-      const int64_t j0 = i * VEC;
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
-        float z = x[k];
+        float z = elem<T>(r, k);
         if constexpr (SCALE) z = E::scale(z, temperature);
-        x[k] = grad(z, j0 + k);
+        x[k] = grad(z, k == hit);
       }
-      dv[i] = E::pack(x);
+      vstore<NT>(dv + i, pack_vec<T>(x));
     }
     tail_begin = nvec * VEC;
   }
-  for (int64_t j = tail_begin + lane; j < V; j += kWave) {
+  for (int64_t j = tail_begin + static_cast<int64_t>(part) * kWave + lane; j < V; j += STEP) {
     float z = E::load1(xr + j);
     if constexpr (SCALE) z = E::scale(z, temperature);
-    E::store1(dr + j, grad(z, j));
+    E::store1(dr + j, grad(z, j == lab));
   }
+}
+
+// ---- tuning (va_set_tuning) ---------------------------------------------------------------
+int g_fwd_wpr = 0;  // 0 = auto
+int g_bwd_wpr = 0;
+int g_nt = 0;
+
+int auto_wpr(int64_t n_rows, int64_t V, int override_wpr) {
+  if (override_wpr == 1 || override_wpr == 2 || override_wpr == 4) return override_wpr;
+  // split long rows over several waves so that a launch is many waves deep per CU slot
+  // (avoids the partial last round of 1-wave-per-row at a few thousand rows)
+  if (V >= 16384) return 4;
+  if (V >= 4096) return 2;
+  (void)n_rows;
+  return 1;
+}
+
+template <typename T, bool S, bool VV, int W>
+void launch_fwd_w(const T *x, int64_t n_rows, int64_t V, int64_t stride, const int64_t *labels,
+                  float temperature, float *logp, float *entropy, float *lse, hipStream_t stream,
+                  bool nt) {
+  const dim3 block(256);
+  const dim3 grid(static_cast<unsigned>((n_rows + (4 / W) - 1) / (4 / W)));
+  if (nt)
+    hipLaunchKernelGGL((logprob_entropy_fwd_kernel<T, S, VV, W, true>), grid, block, 0, stream, x,
+                       n_rows, V, stride, labels, temperature, logp, entropy, lse);
+  else
+    hipLaunchKernelGGL((logprob_entropy_fwd_kernel<T, S, VV, W, false>), grid, block, 0, stream, x,
+                       n_rows, V, stride, labels, temperature, logp, entropy, lse);
 }
 
 template <typename T>
@@ -324,18 +437,37 @@ int launch_fwd(const void *logits, int64_t n_rows, int64_t V, int64_t stride,
   const bool vec = (reinterpret_cast<uintptr_t>(logits) % 16 == 0) &&
                    ((stride * static_cast<int64_t>(sizeof(T))) % 16 == 0);
   const bool scale = (temperature != 1.0f);
-  const dim3 block(256);
-  const dim3 grid(static_cast<unsigned>((n_rows + 3) / 4));
-#define VA_LAUNCH_FWD(S, VV)                                                                 \
-  hipLaunchKernelGGL((logprob_entropy_fwd_kernel<T, S, VV>), grid, block, 0, stream, x, n_rows, \
-                     V, stride, labels, temperature, logp, entropy, lse)
+  const int w = auto_wpr(n_rows, V, g_fwd_wpr);
+  const bool nt = g_nt != 0;
+#define VA_FWD(S, VV)                                                                        \
+  do {                                                                                       \
+    if (w == 4) launch_fwd_w<T, S, VV, 4>(x, n_rows, V, stride, labels, temperature, logp, entropy, lse, stream, nt); \
+    else if (w == 2) launch_fwd_w<T, S, VV, 2>(x, n_rows, V, stride, labels, temperature, logp, entropy, lse, stream, nt); \
+    else launch_fwd_w<T, S, VV, 1>(x, n_rows, V, stride, labels, temperature, logp, entropy, lse, stream, nt); \
+  } while (0)
   if (scale) {
-    if (vec) VA_LAUNCH_FWD(true, true); else VA_LAUNCH_FWD(true, false);
+    if (vec) VA_FWD(true, true); else VA_FWD(true, false);
   } else {
-    if (vec) VA_LAUNCH_FWD(false, true); else VA_LAUNCH_FWD(false, false);
+    if (vec) VA_FWD(false, true); else VA_FWD(false, false);
   }
-#undef VA_LAUNCH_FWD
+#undef VA_FWD
   return check_launch("logprob_entropy_fwd");
+}
+
+template <typename T, bool S, bool VV, int W>
+void launch_bwd_w(const float *g_logp, const float *g_ent, const T *x, int64_t n_rows, int64_t V,
+                  int64_t stride, const int64_t *labels, const float *lse, const float *ent,
+                  float temperature, T *d, int64_t dstride, hipStream_t stream, bool nt) {
+  const dim3 block(256);
+  const dim3 grid(static_cast<unsigned>((n_rows + (4 / W) - 1) / (4 / W)));
+  if (nt)
+    hipLaunchKernelGGL((logprob_entropy_bwd_kernel<T, S, VV, W, true>), grid, block, 0, stream,
+                       g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d,
+                       dstride);
+  else
+    hipLaunchKernelGGL((logprob_entropy_bwd_kernel<T, S, VV, W, false>), grid, block, 0, stream,
+                       g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d,
+                       dstride);
 }
 
 template <typename T>
@@ -350,17 +482,20 @@ int launch_bwd(const float *g_logp, const float *g_ent, const void *logits, int6
                    ((stride * static_cast<int64_t>(sizeof(T))) % 16 == 0) &&
                    ((dstride * static_cast<int64_t>(sizeof(T))) % 16 == 0);
   const bool scale = (temperature != 1.0f);
-  const dim3 block(256);
-  const dim3 grid(static_cast<unsigned>((n_rows + 3) / 4));
-#define VA_LAUNCH_BWD(S, VV)                                                                  \
-  hipLaunchKernelGGL((logprob_entropy_bwd_kernel<T, S, VV>), grid, block, 0, stream, g_logp,    \
-                     g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d, dstride)
+  const int w = auto_wpr(n_rows, V, g_bwd_wpr);
+  const bool nt = g_nt != 0;
+#define VA_BWD(S, VV)                                                                        \
+  do {                                                                                       \
+    if (w == 4) launch_bwd_w<T, S, VV, 4>(g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d, dstride, stream, nt); \
+    else if (w == 2) launch_bwd_w<T, S, VV, 2>(g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d, dstride, stream, nt); \
+    else launch_bwd_w<T, S, VV, 1>(g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d, dstride, stream, nt); \
+  } while (0)
   if (scale) {
-    if (vec) VA_LAUNCH_BWD(true, true); else VA_LAUNCH_BWD(true, false);
+    if (vec) VA_BWD(true, true); else VA_BWD(true, false);
   } else {
-    if (vec) VA_LAUNCH_BWD(false, true); else VA_LAUNCH_BWD(false, false);
+    if (vec) VA_BWD(false, true); else VA_BWD(false, false);
   }
-#undef VA_LAUNCH_BWD
+#undef VA_BWD
   return check_launch("logprob_entropy_bwd");
 }
 
@@ -424,5 +559,14 @@ extern "C" int va_logprob_entropy_bwd(const float *g_logp, const float *g_entrop
     default:
       va::set_error("unsupported logits dtype %d", dtype);
       return VA_E_ARG;
+  }
+}
+
+extern "C" int va_set_tuning(int key, int value) {
+  switch (key) {
+    case VA_TUNE_FWD_WAVES_PER_ROW: va::g_fwd_wpr = value; return VA_OK;
+    case VA_TUNE_BWD_WAVES_PER_ROW: va::g_bwd_wpr = value; return VA_OK;
+    case VA_TUNE_NONTEMPORAL: va::g_nt = value; return VA_OK;
+    default: va::set_error("unknown tuning key %d", key); return VA_E_ARG;
   }
 }

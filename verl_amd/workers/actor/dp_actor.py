@@ -181,14 +181,17 @@ class DataParallelPPOActor(BasePPOActor):
         assert self.config.grad_clip is not None
         if self.grad_reducer is not None:
             self.grad_reducer.finish_sync()
-        grad_norm = torch.nn.utils.clip_grad_norm_(
-            self.actor_module.parameters(), max_norm=self.config.grad_clip, foreach=True)
+        params = (self.grad_reducer.optimizer_params() if self.grad_reducer is not None
+                  else list(self.actor_module.parameters()))
+        grad_norm = torch.nn.utils.clip_grad_norm_(params, max_norm=self.config.grad_clip, foreach=True)
         if not torch.isfinite(grad_norm):
             rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
             print(f"WARN: rank {rank} grad_norm is not finite: {grad_norm}")
             self._zero_grad()
         else:
             self.actor_optimizer.step()
+            if self.grad_reducer is not None:
+                self.grad_reducer.after_step()
         return grad_norm
 
     # ------------------------------------------------------------------ API

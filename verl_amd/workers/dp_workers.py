@@ -18,7 +18,7 @@ import torch.distributed as dist
 
 from ..protocol import DataProto
 from .actor import DataParallelPPOActor
-from .grad_sync import GradBucketReducer
+from .grad_sync import GradBucketReducer, MixedPrecisionParams
 
 
 def init_distributed(backend: str | None = None) -> tuple[int, int]:
@@ -66,16 +66,21 @@ class ActorWorker:
         self.actor = None
         self.module = None
 
-    def init_model(self, module: torch.nn.Module, bucket_mb: int = 256):
+    def init_model(self, module: torch.nn.Module, bucket_mb: int = 256, mixed_precision: bool = True):
         """fsdp_workers.py:562-670 (model already built by the caller; AdamW with the actor's optim
-        config, fsdp_workers.py:418-423)."""
+        config, fsdp_workers.py:418-423). mixed_precision=True is the FSDP MixedPrecision of the
+        reference (bf16 compute weights, fp32 master weights / grads / reduction, :337-347)."""
         self.module = module
         optim = self.config.actor.optim
         fused = next(module.parameters()).is_cuda
-        opt = torch.optim.AdamW(module.parameters(), lr=optim.lr, betas=tuple(optim.get("betas", (0.9, 0.999))),
+        if mixed_precision:
+            manager = MixedPrecisionParams(module, bucket_bytes=bucket_mb << 20)
+        else:
+            manager = GradBucketReducer(module.parameters(), bucket_bytes=bucket_mb << 20)
+        opt = torch.optim.AdamW(manager.optimizer_params(), lr=optim.lr,
+                                betas=tuple(optim.get("betas", (0.9, 0.999))),
                                 weight_decay=optim.get("weight_decay", 0.01), fused=fused)
-        reducer = GradBucketReducer(module.parameters(), bucket_bytes=bucket_mb << 20)
-        self.actor = DataParallelPPOActor(self.config.actor, module, opt, grad_reducer=reducer)
+        self.actor = DataParallelPPOActor(self.config.actor, module, opt, grad_reducer=manager)
         return self
 
     def compute_log_prob(self, data: DataProto) -> DataProto:

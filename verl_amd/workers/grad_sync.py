@@ -105,6 +105,127 @@ class GradBucketReducer:
             b.handle = None
         self.sync_enabled = False
 
+    def optimizer_params(self):
+        return self.params
+
+    def after_step(self):
+        pass
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks.clear()
+
+
+class MixedPrecisionParams:
+    """bf16 compute weights + fp32 master weights + fp32 gradient buckets.
+
+    The MI355X equivalent of the reference's FSDP MixedPrecision(param_dtype=bf16,
+    reduce_dtype=fp32, buffer_dtype=fp32) (fsdp_workers.py:337-347), without sharding:
+
+      * the module's parameters are converted in place to bf16 (buffers such as RoPE's
+        inv_freq stay fp32), so forward/backward run on bf16 weights with no per-op casts;
+      * each parameter has an fp32 master copy living in a flat bucket; the optimizer (fused
+        AdamW) and grad-norm clipping act on the masters;
+      * after each parameter's bf16 gradient is produced, a post-accumulate-grad hook adds it
+        into the fp32 bucket (accumulation over micro-batches in fp32) and frees it; on the last
+        micro-batch the hook launches the bucket's RCCL all-reduce as soon as the bucket is full,
+        overlapping communication with the rest of the backward;
+      * after the optimizer step the masters are copied back to the bf16 weights (foreach copy).
+    """
+
+    def __init__(self, module: torch.nn.Module, bucket_bytes: int = 256 << 20, process_group=None,
+                 compute_dtype=torch.bfloat16):
+        self.group = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.compute_dtype = compute_dtype
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        self.sync_enabled = False
+        ordered = list(reversed(self.params))
+        groups, cur, cur_bytes = [], [], 0
+        for p in ordered:
+            nb = p.numel() * 4
+            if cur and cur_bytes + nb > bucket_bytes:
+                groups.append(cur)
+                cur, cur_bytes = [], 0
+            cur.append(p)
+            cur_bytes += nb
+        if cur:
+            groups.append(cur)
+        self.buckets: list[_Bucket] = []
+        self.masters: list[torch.nn.Parameter] = []
+        self._master_of = {}
+        self._gview = {}
+        self._bucket_of = {}
+        for g in groups:
+            n = sum(p.numel() for p in g)
+            dev = g[0].device
+            mbuf = torch.empty(n, dtype=torch.float32, device=dev)
+            gbuf = torch.zeros(n, dtype=torch.float32, device=dev)
+            off = 0
+            for p in g:
+                k = p.numel()
+                mv = mbuf[off : off + k].view_as(p)
+                mv.copy_(p.detach().float())
+                master = torch.nn.Parameter(mv, requires_grad=True)
+                master.grad = gbuf[off : off + k].view_as(p)
+                self._master_of[id(p)] = master
+                self._gview[id(p)] = master.grad
+                off += k
+            b = _Bucket(gbuf, g)
+            self.buckets.append(b)
+            for p in g:
+                self._bucket_of[id(p)] = b
+        # masters in module order (optimizer state order == parameter order)
+        self.masters = [self._master_of[id(p)] for p in self.params]
+        for p in self.params:
+            p.data = p.data.to(compute_dtype)
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    def _on_grad(self, p):
+        self._gview[id(p)].add_(p.grad)
+        p.grad = None
+        if not self.sync_enabled:
+            return
+        b = self._bucket_of[id(p)]
+        b.pending -= 1
+        if b.pending == 0:
+            b.handle = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    # same interface as GradBucketReducer
+    def zero_grad(self):
+        for b in self.buckets:
+            b.buf.zero_()
+        for p in self.params:
+            p.grad = None
+
+    def begin_sync(self):
+        self.sync_enabled = self.world > 1
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.handle = None
+
+    def finish_sync(self):
+        if self.world <= 1:
+            self.sync_enabled = False
+            return
+        for b in self.buckets:
+            if b.handle is None:
+                b.handle = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        for b in self.buckets:
+            b.handle.wait()
+            b.buf.mul_(1.0 / self.world)
+            b.handle = None
+        self.sync_enabled = False
+
+    def optimizer_params(self):
+        return self.masters
+
+    @torch.no_grad()
+    def after_step(self):
+        """Refresh the bf16 compute weights from the fp32 masters."""
+        torch._foreach_copy_([p.data for p in self.params], [m.data for m in self.masters])
+
     def remove(self):
         for h in self._hooks:
             h.remove()
