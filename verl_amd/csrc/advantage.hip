@@ -293,14 +293,15 @@ __global__ __launch_bounds__(256) void row_partials_kernel(const float *__restri
   }
 }
 
-// Merge K (n, sum, M2) triples in index order; emit the merged triple and the fp32 whitening
-// stats {mean, rsqrt(var + 1e-8), n, error_flag} with the reference's formulas.
+// Merge K (n, sum, M2) triples; emit the merged triple and the fp32 whitening stats
+// {mean, rsqrt(var + 1e-8), n, error_flag} with the reference's formulas. Each thread merges a
+// contiguous slice, then a fixed binary tree in LDS: the merge order depends only on K, so the
+// result is deterministic run to run.
 __global__ __launch_bounds__(256) void whiten_finalize_kernel(const double *__restrict__ part,
                                                               int64_t K, double *__restrict__ merged,
                                                               float *__restrict__ stats) {
   __shared__ double sh[256 * 3];
   Moments acc{0.0, 0.0, 0.0};
-  // contiguous slice per thread keeps the merge order a fixed function of K
   const int64_t per = (K + blockDim.x - 1) / blockDim.x;
   const int64_t lo = threadIdx.x * per, hi = (lo + per < K) ? lo + per : K;
   for (int64_t k = lo; k < hi; ++k) {
@@ -312,10 +313,19 @@ __global__ __launch_bounds__(256) void whiten_finalize_kernel(const double *__re
   sh[threadIdx.x * 3 + 1] = acc.mean;
   sh[threadIdx.x * 3 + 2] = acc.m2;
   __syncthreads();
+  for (unsigned s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      const unsigned a = threadIdx.x, b = threadIdx.x + s;
+      const Moments m = merge_moments(Moments{sh[a * 3], sh[a * 3 + 1], sh[a * 3 + 2]},
+                                      Moments{sh[b * 3], sh[b * 3 + 1], sh[b * 3 + 2]});
+      sh[a * 3] = m.n;
+      sh[a * 3 + 1] = m.mean;
+      sh[a * 3 + 2] = m.m2;
+    }
+    __syncthreads();
+  }
   if (threadIdx.x == 0) {
-    Moments tot{0.0, 0.0, 0.0};
-    for (unsigned j = 0; j < blockDim.x; ++j)
-      tot = merge_moments(tot, Moments{sh[j * 3], sh[j * 3 + 1], sh[j * 3 + 2]});
+    const Moments tot{sh[0], sh[1], sh[2]};
     const double n = tot.n;
     merged[0] = n;
     merged[1] = tot.mean * n;
