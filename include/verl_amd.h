@@ -108,10 +108,12 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 
 /* Launch-shape knobs of the log-prob kernels (results are identical for every setting):
  *   VA_TUNE_FWD/BWD_WAVES_PER_ROW: 0 = auto, 1 / 2 / 4 waves stream one row together;
- *   VA_TUNE_NONTEMPORAL: 1 = non-temporal (streaming) loads/stores of the logits. */
+ *   VA_TUNE_NONTEMPORAL: 1 = non-temporal (streaming) loads/stores of the logits (default),
+ *   0 = default cache policy. */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3
+#define VA_TUNE_PIPELINE 4 /* 0: 4 vectors/lane; 1: 2+2 software-pipelined; 2: 4+4 pipelined */
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------
@@ -217,6 +219,15 @@ int va_gae_advantage_return(const float *rewards, const float *values, const voi
 int va_apply_kl_penalty(const float *scores, const float *old_lp, const float *ref_lp,
                         const void *mask, int mask_dtype, int64_t B, int64_t R, int kl_type,
                         float beta, float *rewards, float *row_kl, void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Mixed-precision gradient accumulation (the fp32 gradient side of the reference's FSDP
+ * MixedPrecision, fsdp_workers.py:337-347): dst[i][:] += scale * src[i][:] for n_tensors
+ * tensors in one or a few launches. src: device pointers of `src_dtype` (VA_BF16 / VA_F16 /
+ * VA_F32), dst: device fp32 pointers; the pointer / size arrays themselves live on the host.
+ * ------------------------------------------------------------------------------------ */
+int va_accumulate_grads(int n_tensors, const void *const *src, const int64_t *numel,
+                        int src_dtype, float *const *dst, float scale, void *stream);
 
 #ifdef __cplusplus
 }

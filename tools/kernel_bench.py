@@ -72,25 +72,27 @@ def sweep(args, src, copy_gbps):
                K._p(labels), K._p(lse), K._p(ent), 1.0, K._p(dx), args.vocab, st)
 
     fwd()
-    variants = [(w, nt) for w in (1, 2, 4) for nt in (0, 1)]
+    variants = [(4, 1, 0), (4, 1, 1), (4, 1, 2), (2, 1, 1), (1, 1, 1), (4, 0, 1), (2, 1, 0)]
     times = {("fwd",) + v: [] for v in variants}
     times.update({("bwd",) + v: [] for v in variants})
     for _ in range(5):
-        for w, nt in variants:
+        for w, nt, pipe in variants:
             lib.va_set_tuning(L.VA_TUNE_FWD_WAVES_PER_ROW, w)
             lib.va_set_tuning(L.VA_TUNE_BWD_WAVES_PER_ROW, w)
             lib.va_set_tuning(L.VA_TUNE_NONTEMPORAL, nt)
-            times[("fwd", w, nt)].append(timeit(fwd, 5, warmup=1)[0])
-            times[("bwd", w, nt)].append(timeit(bwd, 5, warmup=1)[0])
+            lib.va_set_tuning(L.VA_TUNE_PIPELINE, pipe)
+            times[("fwd", w, nt, pipe)].append(timeit(fwd, 5, warmup=1)[0])
+            times[("bwd", w, nt, pipe)].append(timeit(bwd, 5, warmup=1)[0])
     fb = args.rows * (2 * args.vocab + 20)
     bb = args.rows * (4 * args.vocab + 28)
     for k, ts in times.items():
         nb = fb if k[0] == "fwd" else bb
         med = float(np.median(ts))
-        print(json.dumps(dict(kernel=f"{k[0]}_wpr{k[1]}_nt{k[2]}", median_us=round(med * 1e3, 1),
+        print(json.dumps(dict(kernel=f"{k[0]}_wpr{k[1]}_nt{k[2]}_pipe{k[3]}", median_us=round(med * 1e3, 1),
                               min_us=round(min(ts) * 1e3, 1), gbps=round(nb / (med * 1e-3) / 1e9, 1))), flush=True)
-    for key in (L.VA_TUNE_FWD_WAVES_PER_ROW, L.VA_TUNE_BWD_WAVES_PER_ROW, L.VA_TUNE_NONTEMPORAL):
-        lib.va_set_tuning(key, 0)
+    for key, default in ((L.VA_TUNE_FWD_WAVES_PER_ROW, 0), (L.VA_TUNE_BWD_WAVES_PER_ROW, 0),
+                         (L.VA_TUNE_NONTEMPORAL, -1), (L.VA_TUNE_PIPELINE, 0)):
+        lib.va_set_tuning(key, default)
 
 
 def main():

@@ -25,7 +25,6 @@ namespace {
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.69314718055994531f;
-constexpr int kUnroll = 4;  // 16-byte vectors in flight per lane
 
 typedef float float2v __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
@@ -233,7 +232,7 @@ __device__ __forceinline__ void acc_raw(Acc &a, const u32x4 *raw, float temperat
 // ---- forward ---------------------------------------------------------------------------
 // A 256-thread workgroup = 4 waves = 4/WPR rows; the WPR waves of a row interleave 1 KiB
 // segments of it and merge their accumulators through LDS.
-template <typename T, bool SCALE, bool VECTOR, int WPR, bool NT>
+template <typename T, bool SCALE, bool VECTOR, int WPR, bool NT, int U, bool PIPE>
 __global__ __launch_bounds__(256, 8) void logprob_entropy_fwd_kernel(
     const T *__restrict__ logits, int64_t n_rows, int64_t V, int64_t stride,
     const int64_t *__restrict__ labels, float temperature, float *__restrict__ logp,
@@ -255,11 +254,34 @@ __global__ __launch_bounds__(256, 8) void logprob_entropy_fwd_kernel(
       const u32x4 *xv = reinterpret_cast<const u32x4 *>(xr);
       const int64_t nvec = V / VEC;
       int64_t i = static_cast<int64_t>(part) * kWave + lane;
-      for (; i + (kUnroll - 1) * STEP < nvec; i += kUnroll * STEP) {
-        u32x4 raw[kUnroll];
+      if constexpr (PIPE) {
+        // software pipeline: the next U vectors are in flight while the current U are reduced
+        if (i + (U - 1) * STEP < nvec) {
+          u32x4 cur[U];
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) raw[u] = vload<NT>(xv + i + u * STEP);
-        acc_raw<T, kUnroll, SCALE>(a, raw, temperature);
+          for (int u = 0; u < U; ++u) cur[u] = vload<NT>(xv + i + u * STEP);
+          while (true) {
+            const int64_t nx = i + U * STEP;
+            const bool more = nx + (U - 1) * STEP < nvec;
+            u32x4 nxt[U];
+            if (more) {
+#pragma unroll
+              for (int u = 0; u < U; ++u) nxt[u] = vload<NT>(xv + nx + u * STEP);
+            }
+            acc_raw<T, U, SCALE>(a, cur, temperature);
+            i = nx;
+            if (!more) break;
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+          }
+        }
+      } else {
+        for (; i + (U - 1) * STEP < nvec; i += U * STEP) {
+          u32x4 raw[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) raw[u] = vload<NT>(xv + i + u * STEP);
+          acc_raw<T, U, SCALE>(a, raw, temperature);
+        }
       }
       for (; i < nvec; i += STEP) {
         const u32x4 r = vload<NT>(xv + i);
@@ -320,7 +342,7 @@ __global__ __launch_bounds__(256, 8) void logprob_entropy_fwd_kernel(
 }
 
 // ---- backward --------------------------------------------------------------------------
-template <typename T, bool SCALE, bool VECTOR, int WPR, bool NT>
+template <typename T, bool SCALE, bool VECTOR, int WPR, bool NT, int U, bool PIPE>
 __global__ __launch_bounds__(256, 8) void logprob_entropy_bwd_kernel(
     const float *__restrict__ g_logp, const float *__restrict__ g_ent, const T *logits,
     int64_t n_rows, int64_t V, int64_t stride, const int64_t *__restrict__ labels,
@@ -362,13 +384,10 @@ __global__ __launch_bounds__(256, 8) void logprob_entropy_bwd_kernel(
     const int64_t lab_vec = has_lab ? lab / VEC : -1;
     const int lab_k = has_lab ? static_cast<int>(lab % VEC) : -1;
     int64_t i = static_cast<int64_t>(part) * kWave + lane;
-    for (; i + (kUnroll - 1) * STEP < nvec; i += kUnroll * STEP) {
-      u32x4 raw[kUnroll];
+    auto emit = [&](const u32x4 *raw, int64_t at) {
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) raw[u] = vload<NT>(xv + i + u * STEP);
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int hit = (i + u * STEP == lab_vec) ? lab_k : -1;
+      for (int u = 0; u < U; ++u) {
+        const int hit = (at + u * STEP == lab_vec) ? lab_k : -1;
         float x[VEC];
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
@@ -376,7 +395,37 @@ __global__ __launch_bounds__(256, 8) void logprob_entropy_bwd_kernel(
           if constexpr (SCALE) z = E::scale(z, temperature);
           x[k] = grad(z, k == hit);
         }
-        vstore<NT>(dv + i + u * STEP, pack_vec<T>(x));
+        vstore<NT>(dv + at + u * STEP, pack_vec<T>(x));
+      }
+    };
+    if constexpr (PIPE) {
+      // loads of the next U vectors are issued before the stores of the current U (they never
+      // touch the same addresses, also in place), so the wave does not stall on each load
+      if (i + (U - 1) * STEP < nvec) {
+        u32x4 cur[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = vload<NT>(xv + i + u * STEP);
+        while (true) {
+          const int64_t nx = i + U * STEP;
+          const bool more = nx + (U - 1) * STEP < nvec;
+          u32x4 nxt[U];
+          if (more) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) nxt[u] = vload<NT>(xv + nx + u * STEP);
+          }
+          emit(cur, i);
+          i = nx;
+          if (!more) break;
+#pragma unroll
+          for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        }
+      }
+    } else {
+      for (; i + (U - 1) * STEP < nvec; i += U * STEP) {
+        u32x4 raw[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) raw[u] = vload<NT>(xv + i + u * STEP);
+        emit(raw, i);
       }
     }
     for (; i < nvec; i += STEP) {
@@ -403,7 +452,8 @@ __global__ __launch_bounds__(256, 8) void logprob_entropy_bwd_kernel(
 // ---- tuning (va_set_tuning) ---------------------------------------------------------------
 int g_fwd_wpr = 0;  // 0 = auto
 int g_bwd_wpr = 0;
-int g_nt = -1;  // -1 = auto (non-temporal on: +10-12% fwd, +1-2% bwd measured)
+int g_nt = -1;
+int g_pipe = 0;  // 0: 4 vectors per lane, no pipeline; 1: 2+2 pipelined; 2: 4+4 pipelined  // -1 = auto (non-temporal on: +10-12% fwd, +1-2% bwd measured)
 
 int auto_wpr(int64_t n_rows, int64_t V, int override_wpr) {
   if (override_wpr == 1 || override_wpr == 2 || override_wpr == 4) return override_wpr;
@@ -421,12 +471,16 @@ void launch_fwd_w(const T *x, int64_t n_rows, int64_t V, int64_t stride, const i
                   bool nt) {
   const dim3 block(256);
   const dim3 grid(static_cast<unsigned>((n_rows + (4 / W) - 1) / (4 / W)));
-  if (nt)
-    hipLaunchKernelGGL((logprob_entropy_fwd_kernel<T, S, VV, W, true>), grid, block, 0, stream, x,
-                       n_rows, V, stride, labels, temperature, logp, entropy, lse);
-  else
-    hipLaunchKernelGGL((logprob_entropy_fwd_kernel<T, S, VV, W, false>), grid, block, 0, stream, x,
-                       n_rows, V, stride, labels, temperature, logp, entropy, lse);
+#define VA_K(NTV, UU, PP)                                                                         \
+  hipLaunchKernelGGL((logprob_entropy_fwd_kernel<T, S, VV, W, NTV, UU, PP>), grid, block, 0, stream, x, \
+                     n_rows, V, stride, labels, temperature, logp, entropy, lse)
+  const int pipe = VV ? g_pipe : 0;
+  if (nt) {
+    if (pipe == 1) VA_K(true, 2, true); else if (pipe == 2) VA_K(true, 4, true); else VA_K(true, 4, false);
+  } else {
+    if (pipe == 1) VA_K(false, 2, true); else if (pipe == 2) VA_K(false, 4, true); else VA_K(false, 4, false);
+  }
+#undef VA_K
 }
 
 template <typename T>
@@ -460,14 +514,16 @@ void launch_bwd_w(const float *g_logp, const float *g_ent, const T *x, int64_t n
                   float temperature, T *d, int64_t dstride, hipStream_t stream, bool nt) {
   const dim3 block(256);
   const dim3 grid(static_cast<unsigned>((n_rows + (4 / W) - 1) / (4 / W)));
-  if (nt)
-    hipLaunchKernelGGL((logprob_entropy_bwd_kernel<T, S, VV, W, true>), grid, block, 0, stream,
-                       g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d,
-                       dstride);
-  else
-    hipLaunchKernelGGL((logprob_entropy_bwd_kernel<T, S, VV, W, false>), grid, block, 0, stream,
-                       g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d,
-                       dstride);
+#define VA_K(NTV, UU, PP)                                                                      \
+  hipLaunchKernelGGL((logprob_entropy_bwd_kernel<T, S, VV, W, NTV, UU, PP>), grid, block, 0, stream, \
+                     g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d, dstride)
+  const int pipe = VV ? g_pipe : 0;
+  if (nt) {
+    if (pipe == 1) VA_K(true, 2, true); else if (pipe == 2) VA_K(true, 4, true); else VA_K(true, 4, false);
+  } else {
+    if (pipe == 1) VA_K(false, 2, true); else if (pipe == 2) VA_K(false, 4, true); else VA_K(false, 4, false);
+  }
+#undef VA_K
 }
 
 template <typename T>
@@ -567,6 +623,7 @@ extern "C" int va_set_tuning(int key, int value) {
     case VA_TUNE_FWD_WAVES_PER_ROW: va::g_fwd_wpr = value; return VA_OK;
     case VA_TUNE_BWD_WAVES_PER_ROW: va::g_bwd_wpr = value; return VA_OK;
     case VA_TUNE_NONTEMPORAL: va::g_nt = value; return VA_OK;
+    case VA_TUNE_PIPELINE: va::g_pipe = value; return VA_OK;
     default: va::set_error("unknown tuning key %d", key); return VA_E_ARG;
   }
 }

@@ -425,3 +425,17 @@ def apply_kl_penalty(token_level_scores, old_log_prob, ref_log_prob, response_ma
         _p(rewards), _p(row_kl), _stream(s),
     )
     return rewards, row_kl
+
+
+# =============================================================================== grad accumulation
+def accumulate_grads(srcs: list, dsts: list, scale: float = 1.0) -> None:
+    """dst[i] += scale * src[i] (fp32 dst, bf16/fp16/fp32 src) in one multi-tensor launch."""
+    if not srcs:
+        return
+    dt = srcs[0].dtype
+    n = len(srcs)
+    src_arr = (ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs])
+    dst_arr = (ctypes.c_void_p * n)(*[t.data_ptr() for t in dsts])
+    num_arr = (ctypes.c_int64 * n)(*[t.numel() for t in srcs])
+    L.call("va_accumulate_grads", n, ctypes.cast(src_arr, ctypes.c_void_p), ctypes.cast(num_arr, ctypes.c_void_p),
+           _DTYPE_CODES[dt], ctypes.cast(dst_arr, ctypes.c_void_p), float(scale), _stream(dsts[0]))

@@ -288,6 +288,8 @@ class DataParallelPPOActor(BasePPOActor):
                     if last and self.grad_reducer is not None:
                         self.grad_reducer.begin_sync()
                     loss.backward()
+                    if self.grad_reducer is not None:
+                        self.grad_reducer.after_backward()
                     m.update({
                         "actor/pg_loss": pg_loss.detach(),
                         "actor/pg_clipfrac": pg_clipfrac.detach(),

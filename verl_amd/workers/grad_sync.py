@@ -108,6 +108,9 @@ class GradBucketReducer:
     def optimizer_params(self):
         return self.params
 
+    def after_backward(self):
+        pass
+
     def after_step(self):
         pass
 
@@ -180,17 +183,37 @@ class MixedPrecisionParams:
         self.masters = [self._master_of[id(p)] for p in self.params]
         for p in self.params:
             p.data = p.data.to(compute_dtype)
+        self._ready: dict = {}
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
 
     def _on_grad(self, p):
-        self._gview[id(p)].add_(p.grad)
-        p.grad = None
-        if not self.sync_enabled:
-            return
         b = self._bucket_of[id(p)]
-        b.pending -= 1
-        if b.pending == 0:
+        self._ready.setdefault(id(b), []).append(p)
+        if len(self._ready[id(b)]) == len(b.params):
+            self._flush(b)
+
+    def _flush(self, b):
+        """Accumulate the bucket's ready bf16 gradients into its fp32 buffer (one multi-tensor
+        launch) and, on a syncing micro-batch, start the bucket's all-reduce."""
+        ready = self._ready.pop(id(b), [])
+        if ready:
+            if ready[0].is_cuda:
+                from .. import kernels as K
+
+                K.accumulate_grads([q.grad for q in ready], [self._gview[id(q)] for q in ready])
+            else:
+                for q in ready:
+                    self._gview[id(q)].add_(q.grad)
+            for q in ready:
+                q.grad = None
+        if self.sync_enabled and b.handle is None and not self._ready.get(id(b)):
             b.handle = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def after_backward(self):
+        """Flush buckets that did not complete (parameters without a gradient this pass)."""
+        for b in self.buckets:
+            if self._ready.get(id(b)):
+                self._flush(b)
 
     # same interface as GradBucketReducer
     def zero_grad(self):
@@ -198,6 +221,7 @@ class MixedPrecisionParams:
             b.buf.zero_()
         for p in self.params:
             p.grad = None
+        self._ready = {}
 
     def begin_sync(self):
         self.sync_enabled = self.world > 1
@@ -206,6 +230,7 @@ class MixedPrecisionParams:
             b.handle = None
 
     def finish_sync(self):
+        self.after_backward()
         if self.world <= 1:
             self.sync_enabled = False
             return
