@@ -1,0 +1,136 @@
+"""GPU kernels vs the committed golden fixtures (tests/golden/golden_config1.npz, BASELINE config 1),
+and headline-size (512 x 1024, V = 151,936) parity: the full core-algos batch against the oracle,
+the log-prob kernel on sampled rows of a full micro-batch plus size-independent invariants."""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import reference_ops as ref
+from tests.golden.make_golden import LOGIT_CASES, logits_case
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+G = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_config1.npz"), allow_pickle=False)
+
+
+def t(name, dtype=None):
+    x = torch.from_numpy(G[name])
+    return (x if dtype is None else x.to(dtype)).to(DEV)
+
+
+def close(a, b, atol, rtol, what):
+    a = a.detach().double().cpu().numpy()
+    b = np.asarray(b, dtype=np.float64)
+    assert np.allclose(a, b, atol=atol, rtol=rtol, equal_nan=True), f"{what}: max err {np.nanmax(np.abs(a - b)):.3e}"
+
+
+def test_golden_grpo_and_gae():
+    from verl_amd.trainer.ppo import core_algos
+
+    uid = G["uid"]
+    adv, ret = core_algos.compute_grpo_outcome_advantage(t("rewards"), t("mask"), uid)
+    close(adv, G["grpo_adv"], 1e-5, 1e-5, "grpo")
+    assert torch.equal(adv, ret)
+    adv, _ = core_algos.compute_grpo_outcome_advantage(t("rewards"), t("mask"), uid, norm_adv_by_std_in_grpo=False)
+    close(adv, G["grpo_nostd_adv"], 1e-6, 1e-6, "dr.grpo")
+    for tag, (g, lam) in {"g1": (1.0, 1.0), "g099": (0.99, 0.95)}.items():
+        a, r = core_algos.compute_gae_advantage_return(t("rewards"), t("values"), t("mask"), g, lam)
+        close(r, G[f"gae_{tag}_ret"], 1e-4, 1e-4, f"gae {tag} returns")
+        close(a, G[f"gae_{tag}_adv"], 1e-4, 1e-4, f"gae {tag} advantages")
+
+
+@pytest.mark.parametrize("agg", ["token-mean", "seq-mean-token-sum", "seq-mean-token-mean", "seq-mean-token-sum-norm"])
+def test_golden_policy_loss(agg):
+    from verl_amd import kernels as K
+
+    lp = t("new").requires_grad_(True)
+    out = K.fused_policy_loss(t("old"), lp, t("grpo_adv"), t("mask"), 0.2, 0.28, 3.0, agg, ref_log_prob=t("ref"),
+                              kl_loss_type="low_var_kl")
+    (out[0] + 0.001 * out[4]).backward()
+    key = agg.replace("-", "_")
+    want = G[f"loss_{key}_scalars"]
+    close(out[[0, 1, 2, 3, 4]], want, 1e-5, 1e-4, f"{agg} scalars")
+    g = G[f"loss_{key}_dlp"]
+    close(lp.grad, g, 1e-6 * np.abs(g).max() + 1e-12, 1e-4, f"{agg} dlp")
+
+
+def test_golden_kl():
+    from verl_amd.trainer.ppo import core_algos
+
+    for kt in ["kl", "abs", "mse", "low_var_kl"]:
+        close(core_algos.kl_penalty(t("new"), t("ref"), kt), G[f"kl_{kt}"], 1e-6, 1e-5, kt)
+
+
+@pytest.mark.parametrize("case", LOGIT_CASES, ids=[c[0] for c in LOGIT_CASES])
+def test_golden_logprob(case):
+    from verl_amd.utils import torch_functional as vF
+
+    name, seed, rows, V, dt, T = case
+    logits, labels = logits_case(seed, rows, V)
+    logits = logits.to(getattr(torch, dt)).to(DEV)
+    assert np.array_equal(labels.numpy(), G[f"lp_{name}_labels"])
+    lp, ent = vF.logprobs_and_entropy_from_logits(logits, labels.to(DEV), T)
+    close(lp, G[f"lp_{name}_logp"], 1e-4, 1e-4, f"{name} logp")
+    close(ent, G[f"lp_{name}_entropy"], 1e-4, 1e-4, f"{name} entropy")
+
+
+# ------------------------------------------------------------------ headline sizes
+def test_headline_core_algos_512x1024():
+    """GRPO, GAE and the fused loss at the headline batch against the oracle (full batch)."""
+    from verl_amd import kernels as K
+    from verl_amd.trainer.ppo import core_algos
+
+    g = torch.Generator().manual_seed(42)
+    B, R = 512, 1024
+    lens = torch.randint(128, R + 1, (B,), generator=g)
+    mask = (torch.arange(R)[None, :] < lens[:, None]).long()
+    rewards = torch.zeros(B, R)
+    rewards[torch.arange(B), lens - 1] = torch.bernoulli(torch.full((B,), 0.5), generator=g)
+    uid = np.array([f"p{i // 8}" for i in range(B)], dtype=object)[torch.randperm(B, generator=g).numpy()]
+    want, _ = ref.compute_grpo_outcome_advantage(rewards.clone(), mask, uid)
+    got, _ = core_algos.compute_grpo_outcome_advantage(rewards.to(DEV), mask.to(DEV), uid)
+    close(got, want.numpy(), 1e-5, 1e-5, "grpo 512x1024")
+    values = torch.randn(B, R, generator=g)
+    wa, wr = ref.compute_gae_advantage_return(rewards.double(), values.double(), mask.double(), 1.0, 1.0)
+    a, r = core_algos.compute_gae_advantage_return(rewards.to(DEV), values.to(DEV), mask.to(DEV), 1.0, 1.0)
+    close(r, wr.numpy(), 4e-4, 1e-4, "gae returns 512x1024 (vs fp64 twin)")
+    close(a, wa.numpy(), 4e-4, 1e-4, "gae adv 512x1024 (vs fp64 twin)")
+    new = -torch.rand(B, R, generator=g) * 3
+    old = new + 0.05 * torch.randn(B, R, generator=g)
+    refl = new + 0.1 * torch.randn(B, R, generator=g)
+    newr = new.clone().requires_grad_(True)
+    loss, met = ref.actor_loss(old, newr, want, mask, ref_log_prob=refl, kl_loss_type="low_var_kl")
+    loss.backward()
+    nd = new.to(DEV).requires_grad_(True)
+    out = K.fused_policy_loss(old.to(DEV), nd, got, mask.to(DEV), 0.2, 0.2, 3.0, "token-mean", ref_log_prob=refl.to(DEV),
+                              kl_loss_type="low_var_kl")
+    (out[0] + 0.001 * out[4]).backward()
+    close(out[0], met["pg_loss"].item(), 1e-5, 1e-4, "pg_loss")
+    close(out[4], met["kl_loss"].item(), 1e-6, 1e-4, "kl_loss")
+    gm = newr.grad.abs().max().item()
+    close(nd.grad, newr.grad.numpy(), 1e-6 * gm, 1e-4, "dlp 512x1024")
+
+
+def test_headline_logprob_micro_batch_8x1024x151936():
+    """A full update micro-batch of logits (8 x 1024 rows x 151,936 bf16 = 2.5 GB): oracle on 64
+    sampled rows; on all rows the size-independent invariants logp <= 0, 0 <= H <= log V, and
+    fwd/bwd consistency: sum_j dlogits[i, j] = 0 for the log-prob gradient (softmax rows sum to 1)."""
+    from verl_amd import kernels as K
+
+    n, V = 8 * 1024, 151936
+    torch.manual_seed(0)
+    logits = (torch.randn(n, V, device=DEV) * 2).to(torch.bfloat16)
+    labels = torch.randint(0, V, (n,), device=DEV)
+    x = logits.clone().requires_grad_(True)
+    lp, ent = K.logprob_entropy(x, labels)
+    assert torch.all(lp <= 0) and torch.all(ent >= 0) and torch.all(ent <= np.log(V) + 1e-4)
+    rows = torch.randperm(n)[:64]
+    sub = logits[rows.to(DEV)].cpu()
+    close(lp[rows.to(DEV)], ref.logprobs_fp32_math(sub, labels[rows.to(DEV)].cpu()).numpy(), 1e-4, 1e-4, "logp rows")
+    close(ent[rows.to(DEV)], ref.entropy_from_logits(sub.float()).numpy(), 1e-4, 1e-4, "entropy rows")
+    lp.sum().backward()
+    rowsum = x.grad.float().sum(dim=-1)
+    assert rowsum.abs().max().item() < 5e-2  # bf16-rounded gradients of onehot - softmax
