@@ -229,6 +229,26 @@ int va_apply_kl_penalty(const float *scores, const float *old_lp, const float *r
 int va_accumulate_grads(int n_tensors, const void *const *src, const int64_t *numel,
                         int src_dtype, float *const *dst, float scale, void *stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Fused bf16 model ops for the actor backbone (not the reference's hot path: they replace the
+ * HF Qwen2 RMSNorm / SwiGLU / rotary PyTorch op chains, see verl_amd/workers/actor/qwen2_fused.py).
+ *   rmsnorm: x, y [T, H], w [H], rstd [T] fp32; bwd writes dx [T, H] and dw [H] (bf16) using a
+ *            fp32 workspace of va_rmsnorm_workspace_bytes(T, H).
+ *   swiglu:  y = silu(g) * u over n elements; bwd writes dg, du.
+ *   rope:    q [T, Hq, D], k [T, Hk, D], cos / sin [T, D] (rotate_half convention); backward=1
+ *            applies the transposed rotation to the incoming gradients.
+ * ------------------------------------------------------------------------------------ */
+int64_t va_rmsnorm_workspace_bytes(int64_t T, int64_t H);
+int va_rmsnorm_fwd(const void *x, const void *w, int dtype, int64_t T, int64_t H, float eps, void *y,
+                   float *rstd, void *stream);
+int va_rmsnorm_bwd(const void *dy, const void *x, const void *w, const float *rstd, int dtype, int64_t T,
+                   int64_t H, void *dx, void *dw, float *workspace, void *stream);
+int va_swiglu_fwd(const void *g, const void *u, int dtype, int64_t n, void *y, void *stream);
+int va_swiglu_bwd(const void *dy, const void *g, const void *u, int dtype, int64_t n, void *dg, void *du,
+                  void *stream);
+int va_rope(const void *q, const void *k, const void *cos, const void *sin, int dtype, int64_t T, int64_t Hq,
+            int64_t Hk, int64_t D, int backward, void *qo, void *ko, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -439,3 +439,101 @@ def accumulate_grads(srcs: list, dsts: list, scale: float = 1.0) -> None:
     num_arr = (ctypes.c_int64 * n)(*[t.numel() for t in srcs])
     L.call("va_accumulate_grads", n, ctypes.cast(src_arr, ctypes.c_void_p), ctypes.cast(num_arr, ctypes.c_void_p),
            _DTYPE_CODES[dt], ctypes.cast(dst_arr, ctypes.c_void_p), float(scale), _stream(dsts[0]))
+
+
+# =============================================================================== fused model ops (bf16)
+def _bf16_only(*ts):
+    for t in ts:
+        if t.dtype != torch.bfloat16:
+            raise TypeError(f"fused model ops are bf16-only, got {t.dtype}")
+
+
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        H = x.shape[-1]
+        x2 = x.reshape(-1, H).contiguous()
+        y = torch.empty_like(x2)
+        rstd = torch.empty(x2.shape[0], dtype=torch.float32, device=x.device)
+        L.call("va_rmsnorm_fwd", _p(x2), _p(w), L.VA_BF16, x2.shape[0], H, float(eps), _p(y), _p(rstd), _stream(x2))
+        ctx.save_for_backward(x2, w, rstd)
+        ctx.shape = x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, rstd = ctx.saved_tensors
+        T, H = x2.shape
+        dy2 = dy.reshape(T, H).contiguous()
+        dx = torch.empty_like(x2)
+        dw = torch.empty_like(w)
+        nb = L.load().va_rmsnorm_workspace_bytes(T, H)
+        ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=x2.device)
+        L.call("va_rmsnorm_bwd", _p(dy2), _p(x2), _p(w), _p(rstd), L.VA_BF16, T, H, _p(dx), _p(dw), _p(ws), _stream(x2))
+        return dx.view(ctx.shape), dw, None
+
+
+def rmsnorm(x, weight, eps: float):
+    """Qwen2RMSNorm forward in one kernel (bf16)."""
+    _require_device(x, weight)
+    _bf16_only(x, weight)
+    return _RMSNorm.apply(x, weight, eps)
+
+
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, g, u):
+        g2, u2 = g.contiguous(), u.contiguous()
+        y = torch.empty_like(g2)
+        L.call("va_swiglu_fwd", _p(g2), _p(u2), L.VA_BF16, g2.numel(), _p(y), _stream(g2))
+        ctx.save_for_backward(g2, u2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        g2, u2 = ctx.saved_tensors
+        dy2 = dy.contiguous()
+        dg = torch.empty_like(g2)
+        du = torch.empty_like(u2)
+        L.call("va_swiglu_bwd", _p(dy2), _p(g2), _p(u2), L.VA_BF16, g2.numel(), _p(dg), _p(du), _stream(g2))
+        return dg, du
+
+
+def swiglu(gate, up):
+    """silu(gate) * up in one kernel (bf16), Qwen2MLP's activation."""
+    _require_device(gate, up)
+    _bf16_only(gate, up)
+    return _SwiGLU.apply(gate, up)
+
+
+class _RoPE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, cos, sin):
+        T, Hq, D = q.shape
+        Hk = k.shape[1]
+        q2, k2 = q.contiguous(), k.contiguous()
+        c, s = cos.reshape(T, D).contiguous(), sin.reshape(T, D).contiguous()
+        qo, ko = torch.empty_like(q2), torch.empty_like(k2)
+        L.call("va_rope", _p(q2), _p(k2), _p(c), _p(s), L.VA_BF16, T, Hq, Hk, D, 0, _p(qo), _p(ko), _stream(q2))
+        ctx.save_for_backward(c, s)
+        return qo, ko
+
+    @staticmethod
+    def backward(ctx, dqo, dko):
+        c, s = ctx.saved_tensors
+        T, D = c.shape
+        dqo = dqo.contiguous()
+        dko = torch.zeros(0) if dko is None else dko.contiguous()
+        Hq = dqo.shape[1]
+        Hk = dko.shape[1] if dko.dim() == 3 else 0
+        dq, dk = torch.empty_like(dqo), (torch.empty_like(dko) if Hk else None)
+        L.call("va_rope", _p(dqo), _p(dko) if Hk else None, _p(c), _p(s), L.VA_BF16, T, Hq, Hk, D, 1, _p(dq),
+               _p(dk), _stream(dqo))
+        return dq, dk, None, None
+
+
+def rope(q, k, cos, sin):
+    """apply_rotary_pos_emb (rotate_half form) on [T, H, D] q and k, one kernel (bf16)."""
+    _require_device(q, k, cos, sin)
+    _bf16_only(q, k, cos, sin)
+    return _RoPE.apply(q, k, cos, sin)

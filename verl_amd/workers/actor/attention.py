@@ -23,9 +23,29 @@ def _varlen(q, k, v, cu, mx):
     return varlen_attn(q, k, v, cu, cu, mx, mx, is_causal=True)
 
 
-def varlen_attention_forward(module, query, key, value, attention_mask, scaling=None, dropout=0.0, **kwargs):
-    """query [1, Hq, nnz, D], key/value [1, Hkv, nnz, D] -> ([1, nnz, Hq, D], None)."""
+def packed_attention(q, k, v, cu, mx, scaling=None):
+    """Causal flash varlen attention on packed [T, H, D] tensors (GQA: Hk divides Hq)."""
     global _gqa_native
+    if scaling is not None and abs(scaling - q.shape[-1] ** -0.5) > 1e-12:
+        q = q * (scaling / q.shape[-1] ** -0.5)
+    hq, hk = q.shape[1], k.shape[1]
+    if hq != hk:
+        if _gqa_native is None:
+            try:
+                out = _varlen(q, k, v, cu, mx)
+                _gqa_native = True
+                return out
+            except Exception:
+                _gqa_native = False
+        if not _gqa_native:
+            k = k.repeat_interleave(hq // hk, dim=1)
+            v = v.repeat_interleave(hq // hk, dim=1)
+    return _varlen(q, k, v, cu, mx)
+
+
+def varlen_attention_forward(module, query, key, value, attention_mask, scaling=None, dropout=0.0, **kwargs):
+    """AttentionInterface entry: query [1, Hq, nnz, D], key/value [1, Hkv, nnz, D] ->
+    ([1, nnz, Hq, D], None)."""
     cu = kwargs.get("cu_seq_lens_q")
     mx = kwargs.get("max_length_q")
     if cu is None:
@@ -39,21 +59,7 @@ def varlen_attention_forward(module, query, key, value, attention_mask, scaling=
     q = query[0].transpose(0, 1).to(dt).contiguous()
     k = key[0].transpose(0, 1).to(dt).contiguous()
     v = value[0].transpose(0, 1).to(dt).contiguous()
-    if scaling is not None and abs(scaling - q.shape[-1] ** -0.5) > 1e-12:
-        q = q * (scaling / q.shape[-1] ** -0.5)
-    hq, hk = q.shape[1], k.shape[1]
-    if hq != hk:
-        if _gqa_native is None:
-            try:
-                out = _varlen(q, k, v, cu, mx)
-                _gqa_native = True
-                return out.unsqueeze(0), None
-            except Exception:
-                _gqa_native = False
-        if not _gqa_native:
-            k = k.repeat_interleave(hq // hk, dim=1)
-            v = v.repeat_interleave(hq // hk, dim=1)
-    out = _varlen(q, k, v, cu, mx)
+    out = packed_attention(q, k, v, cu, mx, scaling)
     return out.unsqueeze(0), None
 
 

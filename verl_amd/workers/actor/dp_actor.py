@@ -113,6 +113,9 @@ class DataParallelPPOActor(BasePPOActor):
         self.device_name = "cuda"
         # bf16 autocast as the reference (dp_actor.py:100); None runs the model in its own dtype
         self.autocast_dtype = self.config.get("autocast_dtype", torch.bfloat16)
+        # fused RMSNorm / SwiGLU / RoPE kernels on the packed path (bf16 weights only)
+        self.fused_model_ops = self.use_remove_padding and self.config.get("fused_model_ops", True)
+        self._patched = False
 
     # ------------------------------------------------------------------ forward
     def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False, packing: _Packing = None):
@@ -124,6 +127,11 @@ class DataParallelPPOActor(BasePPOActor):
         ac = self.autocast_dtype
         with torch.autocast(device_type=self.device_name, dtype=ac or torch.bfloat16, enabled=ac is not None):
             if self.use_remove_padding:
+                if self.fused_model_ops and not self._patched:
+                    from .qwen2_fused import patch_qwen2
+
+                    patch_qwen2(self.actor_module)
+                    self._patched = True
                 if packing is None:
                     packing = _plan_packing(micro_batch["attention_mask"].cpu().numpy(), R, input_ids.device)
                 ids = input_ids.reshape(-1).index_select(0, packing.token_idx).unsqueeze(0)
