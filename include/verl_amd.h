@@ -230,24 +230,30 @@ int va_accumulate_grads(int n_tensors, const void *const *src, const int64_t *nu
                         int src_dtype, float *const *dst, float scale, void *stream);
 
 /* ---------------------------------------------------------------------------------------
- * Fused bf16 model ops for the actor backbone (not the reference's hot path: they replace the
- * HF Qwen2 RMSNorm / SwiGLU / rotary PyTorch op chains, see verl_amd/workers/actor/qwen2_fused.py).
- *   rmsnorm: x, y [T, H], w [H], rstd [T] fp32; bwd writes dx [T, H] and dw [H] (bf16) using a
- *            fp32 workspace of va_rmsnorm_workspace_bytes(T, H).
- *   swiglu:  y = silu(g) * u over n elements; bwd writes dg, du.
- *   rope:    q [T, Hq, D], k [T, Hk, D], cos / sin [T, D] (rotate_half convention); backward=1
- *            applies the transposed rotation to the incoming gradients.
+ * Fused bf16 model ops for the actor backbone. Not the reference's hot path: they replace the
+ * HF Qwen2 residual-add / RMSNorm / SwiGLU / rotary PyTorch op chains on the packed actor path
+ * (verl_amd/workers/actor/qwen2_fused.py). All buffers 16-byte aligned, H % 8 == 0, H <= 4096.
+ *   rmsnorm_fwd: h = x + residual (skipped when residual is NULL: h is x), y = RMSNorm(h) * w,
+ *                rstd [T] fp32. x, residual, h_out, y [T, H]; w [H].
+ *   rmsnorm_bwd: dx = d/dh of y given dy, plus dres (the gradient reaching h through the residual
+ *                stream; NULL = none); dw [H] bf16; workspace of va_rmsnorm_workspace_bytes(T, H).
+ *   swiglu:      y = silu(g) * u over n elements; bwd writes dg, du.
+ *   rope_qkv:    qkv [T, ld] holds q | k | v ([Hq | Hk | Hk] x D per row); fwd writes rotated
+ *                q [T, Hq, D], k [T, Hk, D] and v [T, Hk, D] (rotate_half convention, cos / sin
+ *                [T, D]); bwd applies the transposed rotation and writes dqkv [T, ld]. D % 16 == 0.
  * ------------------------------------------------------------------------------------ */
 int64_t va_rmsnorm_workspace_bytes(int64_t T, int64_t H);
-int va_rmsnorm_fwd(const void *x, const void *w, int dtype, int64_t T, int64_t H, float eps, void *y,
-                   float *rstd, void *stream);
-int va_rmsnorm_bwd(const void *dy, const void *x, const void *w, const float *rstd, int dtype, int64_t T,
-                   int64_t H, void *dx, void *dw, float *workspace, void *stream);
+int va_rmsnorm_fwd(const void *x, const void *residual, const void *w, int dtype, int64_t T, int64_t H, float eps,
+                   void *h_out, void *y, float *rstd, void *stream);
+int va_rmsnorm_bwd(const void *dy, const void *h, const void *w, const float *rstd, const void *dres, int dtype,
+                   int64_t T, int64_t H, void *dx, void *dw, float *workspace, void *stream);
 int va_swiglu_fwd(const void *g, const void *u, int dtype, int64_t n, void *y, void *stream);
 int va_swiglu_bwd(const void *dy, const void *g, const void *u, int dtype, int64_t n, void *dg, void *du,
                   void *stream);
-int va_rope(const void *q, const void *k, const void *cos, const void *sin, int dtype, int64_t T, int64_t Hq,
-            int64_t Hk, int64_t D, int backward, void *qo, void *ko, void *stream);
+int va_rope_qkv_fwd(const void *qkv, int64_t ld, const void *cos, const void *sin, int dtype, int64_t T,
+                    int64_t Hq, int64_t Hk, int64_t D, void *q, void *k, void *v, void *stream);
+int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *cos, const void *sin, int dtype,
+                    int64_t T, int64_t Hq, int64_t Hk, int64_t D, void *dqkv, int64_t ld, void *stream);
 
 #ifdef __cplusplus
 }

@@ -67,34 +67,85 @@ def test_swiglu_matches_hf():
     _grad_close(ub.grad, ua.grad, "swiglu du")
 
 
-def test_rope_matches_hf():
+def test_add_rmsnorm_matches_hf():
+    """Residual add + RMSNorm (Qwen2DecoderLayer: h = residual + x; norm(h)); both outputs and the
+    gradient that reaches x / residual through h and through the norm."""
+    from transformers.models.qwen2.modeling_qwen2 import Qwen2RMSNorm
+
+    from verl_amd import kernels as K
+
+    torch.manual_seed(5)
+    T, H = 1531, 896
+    m = Qwen2RMSNorm(H, eps=1e-6).to(DEV).to(torch.bfloat16)
+    with torch.no_grad():
+        m.weight.copy_(1 + 0.1 * torch.randn(H, device=DEV))
+    x = (torch.randn(T, H, device=DEV) * 2).to(torch.bfloat16)
+    r = (torch.randn(T, H, device=DEV) * 4).to(torch.bfloat16)
+    xa, ra = x.clone().requires_grad_(True), r.clone().requires_grad_(True)
+    ha = ra + xa
+    ya = m(ha)
+    w2 = m.weight.detach().clone().requires_grad_(True)
+    xb, rb = x.clone().requires_grad_(True), r.clone().requires_grad_(True)
+    hb, yb = K.add_rmsnorm(xb, rb, w2, 1e-6)
+    assert torch.equal(hb, ha)
+    _ulp_close(yb, ya, what="add_rmsnorm fwd")
+    gh, gy = torch.randn_like(ha), torch.randn_like(ya)
+    torch.autograd.backward([ha, ya], [gh, gy])
+    torch.autograd.backward([hb, yb], [gh, gy])
+    _grad_close(xb.grad, xa.grad, "add_rmsnorm dx")
+    _grad_close(rb.grad, ra.grad, "add_rmsnorm dres")
+    _grad_close(w2.grad, m.weight.grad, "add_rmsnorm dw")
+
+
+@pytest.mark.parametrize("H", [64, 896, 1536, 3584])
+def test_rmsnorm_widths(H):
+    """Every register-tile width (NV = 1, 2, 4, 8 vectors per lane) against the HF module."""
+    from transformers.models.qwen2.modeling_qwen2 import Qwen2RMSNorm
+
+    from verl_amd import kernels as K
+
+    torch.manual_seed(H)
+    T = 333
+    m = Qwen2RMSNorm(H, eps=1e-6).to(DEV).to(torch.bfloat16)
+    x = torch.randn(T, H, device=DEV).to(torch.bfloat16)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    w2 = m.weight.detach().clone().requires_grad_(True)
+    ya, yb = m(xa), K.rmsnorm(xb, w2, 1e-6)
+    _ulp_close(yb, ya, what=f"rmsnorm H={H}")
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    _grad_close(xb.grad, xa.grad, f"rmsnorm dx H={H}")
+    _grad_close(w2.grad, m.weight.grad, f"rmsnorm dw H={H}")
+
+
+def test_rope_qkv_matches_hf():
     from transformers.models.qwen2.modeling_qwen2 import apply_rotary_pos_emb
 
     from verl_amd import kernels as K
 
     torch.manual_seed(2)
     T, Hq, Hk, D = 777, 14, 2, 64
-    q = torch.randn(T, Hq, D, device=DEV).to(torch.bfloat16)
-    k = torch.randn(T, Hk, D, device=DEV).to(torch.bfloat16)
+    qkv = torch.randn(T, (Hq + 2 * Hk) * D, device=DEV).to(torch.bfloat16)
     pos = torch.arange(T, device=DEV).float()
     inv = 1.0 / (1e6 ** (torch.arange(0, D, 2, device=DEV).float() / D))
     freqs = pos[:, None] * inv[None, :]
     emb = torch.cat([freqs, freqs], dim=-1)
     cos, sin = emb.cos().to(torch.bfloat16)[None], emb.sin().to(torch.bfloat16)[None]
-    qa, ka = q.clone().requires_grad_(True), k.clone().requires_grad_(True)
+    qa_in = qkv.clone().requires_grad_(True)
+    q = qa_in[:, : Hq * D].view(T, Hq, D)
+    k = qa_in[:, Hq * D : (Hq + Hk) * D].view(T, Hk, D)
+    v = qa_in[:, (Hq + Hk) * D :].view(T, Hk, D)
     # HF layout [1, H, T, D]
-    qe, ke = apply_rotary_pos_emb(qa.transpose(0, 1)[None], ka.transpose(0, 1)[None], cos, sin)
+    qe, ke = apply_rotary_pos_emb(q.transpose(0, 1)[None], k.transpose(0, 1)[None], cos, sin)
     qe, ke = qe[0].transpose(0, 1), ke[0].transpose(0, 1)
-    qb, kb = q.clone().requires_grad_(True), k.clone().requires_grad_(True)
-    qf, kf = K.rope(qb, kb, cos, sin)
-    assert torch.equal(qf, qe) and torch.equal(kf, ke)  # same bf16 rounding points: bitwise
-    dq, dk = torch.randn_like(qe), torch.randn_like(ke)
-    (qe * dq).sum().backward(retain_graph=True)
-    (ke * dk).sum().backward()
-    (qf * dq).sum().backward(retain_graph=True)
-    (kf * dk).sum().backward()
-    _grad_close(qb.grad, qa.grad, "rope dq", rtol=1e-2)
-    _grad_close(kb.grad, ka.grad, "rope dk", rtol=1e-2)
+    qb_in = qkv.clone().requires_grad_(True)
+    qf, kf, vf = K.rope_qkv(qb_in, cos, sin, Hq, Hk, D)
+    assert torch.equal(qf, qe) and torch.equal(kf, ke) and torch.equal(vf, v)  # same rounding: bitwise
+    dq, dk, dv = torch.randn_like(qe), torch.randn_like(ke), torch.randn_like(v)
+    torch.autograd.backward([qe, ke, v], [dq, dk, dv])
+    torch.autograd.backward([qf, kf, vf], [dq, dk, dv])
+    _grad_close(qb_in.grad, qa_in.grad, "rope dqkv", rtol=1e-2)
 
 
 def test_patched_actor_matches_unpatched():
@@ -120,6 +171,7 @@ def test_patched_actor_matches_unpatched():
         b = data.batch
         e, lp2 = a._forward_micro_batch(b, 1.0, calculate_entropy=False)
         (lp2 * b["response_mask"]).sum().backward()
+        assert a._fused_backbone is fused, "fused packed backbone not taken"
         out[fused] = (lp, ent, {n: p.grad.clone() for n, p in m.named_parameters()})
     msk = data.batch["response_mask"].bool()
     assert torch.allclose(out[True][0][msk], out[False][0][msk], atol=5e-2, rtol=2e-2)

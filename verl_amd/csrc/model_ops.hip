@@ -1,14 +1,24 @@
 // Fused elementwise / normalisation kernels for the actor's Qwen2 backbone on MI355X (bf16).
 //
-// These are not part of the reference's hot path; they replace the ~20 small PyTorch kernels
-// per layer that HF Qwen2 issues for RMSNorm, SwiGLU and rotary embedding (plus the layout
-// copies around varlen attention), which made the actor step launch-bound (GPU ~80% busy).
+// These are not part of the reference's hot path; they replace the PyTorch op chains HF Qwen2
+// issues per decoder layer (RMSNorm ~8 ops, residual add, SwiGLU 2-3 ops, rotary ~10 ops plus
+// the layout copies around varlen attention), so that the packed actor step is GEMM/attention
+// bound rather than bound by small HBM round trips.
 // Forward numerics follow the HF modules' bf16 rounding points:
-//   RMSNorm  y = bf16(w * bf16(x * rsqrt(mean(x^2) + eps)))           (modeling_qwen2 Qwen2RMSNorm)
-//   SwiGLU   y = bf16(bf16(silu(g)) * u)                               (Qwen2MLP)
-//   RoPE     q' = bf16(bf16(q * cos) + bf16(rotate_half(q) * sin))    (apply_rotary_pos_emb)
+//   residual  h = bf16(x + r)                                           (Qwen2DecoderLayer)
+//   RMSNorm   y = bf16(w * bf16(h * rsqrt(mean(h^2) + eps)))           (Qwen2RMSNorm)
+//   SwiGLU    y = bf16(bf16(silu(g)) * u)                               (Qwen2MLP)
+//   RoPE      q' = bf16(bf16(q * cos) + bf16(rotate_half(q) * sin))    (apply_rotary_pos_emb)
 // Backwards compute in fp32 and round once (autograd of the HF graph rounds at every op).
-// All kernels are HBM-bound streaming (16-byte vectors where aligned).
+//
+// Layout / mapping (all HBM-bound streaming, 16-byte accesses):
+//   * RMSNorm: one wave64 per row, the row held in registers as NV 16-byte vectors per lane
+//     (NV = ceil(H / 512)); fwd writes h (when a residual is added), y and rstd.  bwd keeps the
+//     per-lane dw partial for its columns in registers across the rows of a workgroup, reduces
+//     the 4 waves through LDS into a [n_blocks, H] fp32 partial, then a column-sum kernel
+//     produces dw (fixed order: deterministic).
+//   * RoPE reads the merged q|k|v projection [T, (Hq+2Hk)*D] once and writes q, k (rotated) and
+//     v in flash varlen's [T, H, D] layout; its backward writes the merged gradient directly.
 
 #include <math.h>
 
@@ -21,75 +31,154 @@ __device__ __forceinline__ float bf(uint16_t b) { return bf16_to_f32(b); }
 __device__ __forceinline__ uint16_t to_bf(float f) { return static_cast<uint16_t>(f32_to_bf16_bits(f)); }
 __device__ __forceinline__ float rbf(float f) { return bf(to_bf(f)); }  // round through bf16
 
-// ------------------------------------------------------------------ RMSNorm
-// one wave per row; 4 rows per 256-thread workgroup
-__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(const uint16_t *__restrict__ x,
-                                                          const uint16_t *__restrict__ w, int64_t T,
-                                                          int H, float eps, uint16_t *__restrict__ y,
-                                                          float *__restrict__ rstd) {
+// 8 bf16 <-> 8 floats
+__device__ __forceinline__ void unpack8(const uint4 v, float (&f)[8]) {
+  f[0] = bf16_lo(v.x); f[1] = bf16_hi(v.x); f[2] = bf16_lo(v.y); f[3] = bf16_hi(v.y);
+  f[4] = bf16_lo(v.z); f[5] = bf16_hi(v.z); f[6] = bf16_lo(v.w); f[7] = bf16_hi(v.w);
+}
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  uint4 v;
+  v.x = f32_to_bf16_bits(f[0]) | (f32_to_bf16_bits(f[1]) << 16);
+  v.y = f32_to_bf16_bits(f[2]) | (f32_to_bf16_bits(f[3]) << 16);
+  v.z = f32_to_bf16_bits(f[4]) | (f32_to_bf16_bits(f[5]) << 16);
+  v.w = f32_to_bf16_bits(f[6]) | (f32_to_bf16_bits(f[7]) << 16);
+  return v;
+}
+__device__ __forceinline__ uint4 ld16(const uint16_t *p) { return *reinterpret_cast<const uint4 *>(p); }
+__device__ __forceinline__ void st16(uint16_t *p, uint4 v) { *reinterpret_cast<uint4 *>(p) = v; }
+
+// ------------------------------------------------------------------ RMSNorm (+ residual add)
+template <int NV>
+__global__ __launch_bounds__(256) void add_rmsnorm_fwd_kernel(
+    const uint16_t *__restrict__ x, const uint16_t *__restrict__ res, const uint16_t *__restrict__ w,
+    int64_t T, int H, float eps, uint16_t *__restrict__ hout, uint16_t *__restrict__ y,
+    float *__restrict__ rstd) {
   const int lane = threadIdx.x & 63;
   const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= T) return;
+  const int nvec = H >> 3;
   const uint16_t *xr = x + row * H;
+  float v[NV][8];
   float ss = 0.f;
-  for (int h = lane; h < H; h += kWave) {
-    const float v = bf(xr[h]);
-    ss = fmaf(v, v, ss);
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = lane + k * kWave;
+    if (i < nvec) {
+      unpack8(ld16(xr + i * 8), v[k]);
+      if (res != nullptr) {
+        float r8[8];
+        unpack8(ld16(res + row * H + i * 8), r8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[k][e] = rbf(v[k][e] + r8[e]);
+        st16(hout + row * H + i * 8, pack8(v[k]));
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss = fmaf(v[k][e], v[k][e], ss);
+    }
   }
   ss = wave_sum(ss);
   const float r = 1.0f / sqrtf(ss / static_cast<float>(H) + eps);
   if (lane == 0) rstd[row] = r;
-  uint16_t *yr = y + row * H;
-  for (int h = lane; h < H; h += kWave) {
-    const float xh = rbf(bf(xr[h]) * r);
-    yr[h] = to_bf(bf(w[h]) * xh);
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = lane + k * kWave;
+    if (i < nvec) {
+      float w8[8], o[8];
+      unpack8(ld16(w + i * 8), w8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = w8[e] * rbf(v[k][e] * r);
+      st16(y + row * H + i * 8, pack8(o));
+    }
   }
 }
 
-// dx = r * (g - xh * mean(g * xh)),  g = dy * w,  xh = x * r;  dw partials over row blocks
-constexpr int kRowsPerBlock = 64;
-
-__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
-    const uint16_t *__restrict__ dy, const uint16_t *__restrict__ x, const uint16_t *__restrict__ w,
-    const float *__restrict__ rstd, int64_t T, int H, uint16_t *__restrict__ dx,
-    float *__restrict__ dw_part) {
+// dh = r * (g - xh * mean(g * xh)) (+ dres),  g = dy * w,  xh = h * r;  dw += dy * bf16(xh)
+template <int NV>
+__global__ __launch_bounds__(256) void add_rmsnorm_bwd_kernel(
+    const uint16_t *__restrict__ dy, const uint16_t *__restrict__ h, const uint16_t *__restrict__ w,
+    const float *__restrict__ rstd, const uint16_t *__restrict__ dres, int64_t T, int H,
+    int rows_per_block, uint16_t *__restrict__ dx, float *__restrict__ dw_part) {
   extern __shared__ float sdw[];  // [4][H]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int h = threadIdx.x; h < 4 * H; h += 256) sdw[h] = 0.f;
-  __syncthreads();
-  float *mine = sdw + wave * H;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kRowsPerBlock;
-  for (int64_t row = r0 + wave; row < r0 + kRowsPerBlock && row < T; row += 4) {
-    const uint16_t *xr = x + row * H;
-    const uint16_t *dyr = dy + row * H;
+  const int nvec = H >> 3;
+  float acc[NV][8];
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  int64_t r1 = r0 + rows_per_block;
+  if (r1 > T) r1 = T;
+  for (int64_t row = r0 + wave; row < r1; row += 4) {
     const float r = rstd[row];
+    float hv[NV][8], g[NV][8];
     float dot = 0.f;
-    for (int h = lane; h < H; h += kWave) {
-      const float xu = bf(xr[h]) * r;
-      const float g = bf(dyr[h]) * bf(w[h]);
-      dot = fmaf(g, xu, dot);
-      mine[h] += bf(dyr[h]) * rbf(xu);  // dw sees the bf16-rounded x_hat; lanes own columns
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int i = lane + k * kWave;
+      if (i < nvec) {
+        float d8[8], w8[8];
+        unpack8(ld16(h + row * H + i * 8), hv[k]);
+        unpack8(ld16(dy + row * H + i * 8), d8);
+        unpack8(ld16(w + i * 8), w8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xh = hv[k][e] * r;
+          g[k][e] = d8[e] * w8[e];
+          dot = fmaf(g[k][e], xh, dot);
+          acc[k][e] = fmaf(d8[e], rbf(xh), acc[k][e]);
+        }
+      }
     }
-    dot = wave_sum(dot) / static_cast<float>(H);
-    uint16_t *dxr = dx + row * H;
-    for (int h = lane; h < H; h += kWave) {
-      const float xh = bf(xr[h]) * r;
-      const float g = bf(dyr[h]) * bf(w[h]);
-      dxr[h] = to_bf(r * (g - xh * dot));
+    const float mean = wave_sum(dot) / static_cast<float>(H);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int i = lane + k * kWave;
+      if (i < nvec) {
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = r * (g[k][e] - hv[k][e] * r * mean);
+        if (dres != nullptr) {
+          float a8[8];
+          unpack8(ld16(dres + row * H + i * 8), a8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] += a8[e];
+        }
+        st16(dx + row * H + i * 8, pack8(o));
+      }
+    }
+  }
+  // 4 waves -> one [H] partial per workgroup (lanes own disjoint columns: no conflicts)
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = lane + k * kWave;
+    if (i < nvec) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sdw[wave * H + i * 8 + e] = acc[k][e];
     }
   }
   __syncthreads();
-  for (int h = threadIdx.x; h < H; h += 256)
-    dw_part[static_cast<int64_t>(blockIdx.x) * H + h] = sdw[h] + sdw[H + h] + sdw[2 * H + h] + sdw[3 * H + h];
+  for (int c = threadIdx.x; c < H; c += 256)
+    dw_part[static_cast<int64_t>(blockIdx.x) * H + c] = (sdw[c] + sdw[H + c]) + (sdw[2 * H + c] + sdw[3 * H + c]);
 }
 
-__global__ __launch_bounds__(256) void colsum_to_bf16_kernel(const float *__restrict__ part, int nblk,
-                                                             int H, uint16_t *__restrict__ out) {
-  const int h = blockIdx.x * 256 + threadIdx.x;
-  if (h >= H) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[static_cast<int64_t>(b) * H + h];
-  out[h] = to_bf(s);
+// dw[c] = bf16(sum_b part[b, c]); 64 columns x 16 row groups per workgroup, fixed-order merge
+__global__ __launch_bounds__(1024) void colsum_to_bf16_kernel(const float *__restrict__ part, int nblk,
+                                                              int H, uint16_t *__restrict__ out) {
+  __shared__ float s[16][65];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float acc = 0.f;
+  if (c < H)
+    for (int b = g; b < nblk; b += 16) acc += part[static_cast<int64_t>(b) * H + c];
+  s[g][cl] = acc;
+  __syncthreads();
+  if (g == 0 && c < H) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += s[k][cl];
+    out[c] = to_bf(t);
+  }
 }
 
 // ------------------------------------------------------------------ SwiGLU
@@ -101,16 +190,12 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const uint16_t *__restr
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 256 * 8;
   for (int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 8; i < n; i += stride) {
     if (i + 8 <= n) {
-      const uint4 gv = *reinterpret_cast<const uint4 *>(g + i);
-      const uint4 uv = *reinterpret_cast<const uint4 *>(u + i);
-      const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w}, uw[4] = {uv.x, uv.y, uv.z, uv.w};
-      uint32_t o[4];
+      float g8[8], u8[8], o[8];
+      unpack8(ld16(g + i), g8);
+      unpack8(ld16(u + i), u8);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float a0 = rbf(silu(bf16_lo(gw[k]))), a1 = rbf(silu(bf16_hi(gw[k])));
-        o[k] = (f32_to_bf16_bits(a0 * bf16_lo(uw[k]))) | (f32_to_bf16_bits(a1 * bf16_hi(uw[k])) << 16);
-      }
-      *reinterpret_cast<uint4 *>(y + i) = make_uint4(o[0], o[1], o[2], o[3]);
+      for (int e = 0; e < 8; ++e) o[e] = rbf(silu(g8[e])) * u8[e];
+      st16(y + i, pack8(o));
     } else {
       for (int64_t j = i; j < n; ++j) y[j] = to_bf(rbf(silu(bf(g[j]))) * bf(u[j]));
     }
@@ -124,34 +209,21 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const uint16_t *__restr
                                                          uint16_t *__restrict__ du) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 256 * 8;
   for (int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 8; i < n; i += stride) {
-    const int64_t e = (i + 8 <= n) ? i + 8 : n;
-    if (e - i == 8) {
-      const uint4 dv = *reinterpret_cast<const uint4 *>(dy + i);
-      const uint4 gv = *reinterpret_cast<const uint4 *>(g + i);
-      const uint4 uv = *reinterpret_cast<const uint4 *>(u + i);
-      const uint32_t dw_[4] = {dv.x, dv.y, dv.z, dv.w}, gw[4] = {gv.x, gv.y, gv.z, gv.w},
-                     uw[4] = {uv.x, uv.y, uv.z, uv.w};
-      uint32_t og[4], ou[4];
+    if (i + 8 <= n) {
+      float d8[8], g8[8], u8[8], rg[8], ru[8];
+      unpack8(ld16(dy + i), d8);
+      unpack8(ld16(g + i), g8);
+      unpack8(ld16(u + i), u8);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float r_g[2], r_u[2];
-#pragma unroll
-        for (int hlf = 0; hlf < 2; ++hlf) {
-          const float d = hlf ? bf16_hi(dw_[k]) : bf16_lo(dw_[k]);
-          const float gg = hlf ? bf16_hi(gw[k]) : bf16_lo(gw[k]);
-          const float uu = hlf ? bf16_hi(uw[k]) : bf16_lo(uw[k]);
-          const float s = 1.f / (1.f + __expf(-gg));
-          const float a = rbf(gg * s);
-          r_u[hlf] = d * a;
-          r_g[hlf] = d * uu * (s * (1.f + gg * (1.f - s)));
-        }
-        og[k] = f32_to_bf16_bits(r_g[0]) | (f32_to_bf16_bits(r_g[1]) << 16);
-        ou[k] = f32_to_bf16_bits(r_u[0]) | (f32_to_bf16_bits(r_u[1]) << 16);
+      for (int e = 0; e < 8; ++e) {
+        const float s = 1.f / (1.f + __expf(-g8[e]));
+        ru[e] = d8[e] * rbf(g8[e] * s);
+        rg[e] = d8[e] * u8[e] * (s * (1.f + g8[e] * (1.f - s)));
       }
-      *reinterpret_cast<uint4 *>(dg + i) = make_uint4(og[0], og[1], og[2], og[3]);
-      *reinterpret_cast<uint4 *>(du + i) = make_uint4(ou[0], ou[1], ou[2], ou[3]);
+      st16(dg + i, pack8(rg));
+      st16(du + i, pack8(ru));
     } else {
-      for (int64_t j = i; j < e; ++j) {
+      for (int64_t j = i; j < n; ++j) {
         const float d = bf(dy[j]), gg = bf(g[j]), uu = bf(u[j]);
         const float s = 1.f / (1.f + __expf(-gg));
         du[j] = to_bf(d * rbf(gg * s));
@@ -161,44 +233,82 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const uint16_t *__restr
   }
 }
 
-// ------------------------------------------------------------------ RoPE (rotate_half form)
-// q [T, Hq, D], k [T, Hk, D], cos / sin [T, D] -> same layouts; one thread per (t, head, j < D/2)
-__global__ __launch_bounds__(256) void rope_kernel(const uint16_t *__restrict__ q,
-                                                   const uint16_t *__restrict__ k,
-                                                   const uint16_t *__restrict__ cs,
-                                                   const uint16_t *__restrict__ sn, int64_t T, int Hq,
-                                                   int Hk, int D, int backward,
-                                                   uint16_t *__restrict__ qo,
-                                                   uint16_t *__restrict__ ko) {
-  const int half = D / 2;
-  const int64_t per_t = static_cast<int64_t>(Hq + Hk) * half;
+// ------------------------------------------------------------------ RoPE on the merged q|k|v
+// thread = (token t, head in [0, Hq + 2 Hk), chunk c of 8 elements in the first half of D)
+__global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(
+    const uint16_t *__restrict__ qkv, int64_t ld, const uint16_t *__restrict__ cs,
+    const uint16_t *__restrict__ sn, int64_t T, int Hq, int Hk, int D, uint16_t *__restrict__ q,
+    uint16_t *__restrict__ k, uint16_t *__restrict__ v) {
+  const int half = D >> 1, cph = half >> 3, nh = Hq + 2 * Hk;
+  const int64_t per_t = static_cast<int64_t>(nh) * cph;
   const int64_t total = T * per_t;
   for (int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; idx < total;
        idx += static_cast<int64_t>(gridDim.x) * 256) {
     const int64_t t = idx / per_t;
     const int rem = static_cast<int>(idx - t * per_t);
-    const int head = rem / half, j = rem - head * half;
-    const uint16_t *src;
-    uint16_t *dst;
-    if (head < Hq) {
-      src = q + (t * Hq + head) * D;
-      dst = qo + (t * Hq + head) * D;
-    } else {
-      src = k + (t * Hk + (head - Hq)) * D;
-      dst = ko + (t * Hk + (head - Hq)) * D;
+    const int head = rem / cph, j = (rem - head * cph) * 8;
+    const uint16_t *src = qkv + t * ld + static_cast<int64_t>(head) * D;
+    const uint4 a = ld16(src + j), b = ld16(src + j + half);
+    if (head >= Hq + Hk) {  // v: layout change only
+      uint16_t *dst = v + (t * Hk + (head - Hq - Hk)) * D;
+      st16(dst + j, a);
+      st16(dst + j + half, b);
+      continue;
     }
-    const float x1 = bf(src[j]), x2 = bf(src[j + half]);
-    const float c1 = bf(cs[t * D + j]), c2 = bf(cs[t * D + j + half]);
-    const float s1 = bf(sn[t * D + j]), s2 = bf(sn[t * D + j + half]);
-    if (!backward) {
+    uint16_t *dst = head < Hq ? q + (t * Hq + head) * D : k + (t * Hk + (head - Hq)) * D;
+    float x1[8], x2[8], c1[8], c2[8], s1[8], s2[8], o1[8], o2[8];
+    unpack8(a, x1);
+    unpack8(b, x2);
+    unpack8(ld16(cs + t * D + j), c1);
+    unpack8(ld16(cs + t * D + j + half), c2);
+    unpack8(ld16(sn + t * D + j), s1);
+    unpack8(ld16(sn + t * D + j + half), s2);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
       // out[j] = x1*c1 + (-x2)*s1 ; out[j+half] = x2*c2 + x1*s2  (bf16 after each op)
-      dst[j] = to_bf(rbf(x1 * c1) + rbf(-x2 * s1));
-      dst[j + half] = to_bf(rbf(x2 * c2) + rbf(x1 * s2));
-    } else {
-      // d x1 = g1*c1 + g2*s2 ; d x2 = g2*c2 - g1*s1
-      dst[j] = to_bf(x1 * c1 + x2 * s2);
-      dst[j + half] = to_bf(x2 * c2 - x1 * s1);
+      o1[e] = rbf(x1[e] * c1[e]) + rbf(-x2[e] * s1[e]);
+      o2[e] = rbf(x2[e] * c2[e]) + rbf(x1[e] * s2[e]);
     }
+    st16(dst + j, pack8(o1));
+    st16(dst + j + half, pack8(o2));
+  }
+}
+
+__global__ __launch_bounds__(256) void rope_qkv_bwd_kernel(
+    const uint16_t *__restrict__ dq, const uint16_t *__restrict__ dk, const uint16_t *__restrict__ dv,
+    const uint16_t *__restrict__ cs, const uint16_t *__restrict__ sn, int64_t T, int Hq, int Hk, int D,
+    uint16_t *__restrict__ dqkv, int64_t ld) {
+  const int half = D >> 1, cph = half >> 3, nh = Hq + 2 * Hk;
+  const int64_t per_t = static_cast<int64_t>(nh) * cph;
+  const int64_t total = T * per_t;
+  for (int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; idx < total;
+       idx += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t t = idx / per_t;
+    const int rem = static_cast<int>(idx - t * per_t);
+    const int head = rem / cph, j = (rem - head * cph) * 8;
+    uint16_t *dst = dqkv + t * ld + static_cast<int64_t>(head) * D;
+    if (head >= Hq + Hk) {
+      const uint16_t *src = dv + (t * Hk + (head - Hq - Hk)) * D;
+      st16(dst + j, ld16(src + j));
+      st16(dst + j + half, ld16(src + j + half));
+      continue;
+    }
+    const uint16_t *src = head < Hq ? dq + (t * Hq + head) * D : dk + (t * Hk + (head - Hq)) * D;
+    float g1[8], g2[8], c1[8], c2[8], s1[8], s2[8], o1[8], o2[8];
+    unpack8(ld16(src + j), g1);
+    unpack8(ld16(src + j + half), g2);
+    unpack8(ld16(cs + t * D + j), c1);
+    unpack8(ld16(cs + t * D + j + half), c2);
+    unpack8(ld16(sn + t * D + j), s1);
+    unpack8(ld16(sn + t * D + j + half), s2);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      // d x1 = g1*c1 + g2*s2 ; d x2 = g2*c2 - g1*s1
+      o1[e] = g1[e] * c1[e] + g2[e] * s2[e];
+      o2[e] = g2[e] * c2[e] - g1[e] * s1[e];
+    }
+    st16(dst + j, pack8(o1));
+    st16(dst + j + half, pack8(o2));
   }
 }
 
@@ -207,47 +317,89 @@ int64_t grid_for(int64_t n, int per_thread) {
   return g < 1 ? 1 : (g > 65536 ? 65536 : g);
 }
 
+bool aligned16(const void *p) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+
+int nv_for(int64_t H) { return static_cast<int>((H / 8 + kWave - 1) / kWave); }
+
+// rows per bwd workgroup: >= 16, and at most ~1024 workgroups (partials stay small)
+int64_t bwd_rows_per_block(int64_t T) {
+  int64_t r = (T + 1023) / 1024;
+  if (r < 16) r = 16;
+  return (r + 3) / 4 * 4;
+}
+
 }  // namespace
 }  // namespace va
 
 using namespace va;
 
+#define VA_NV_DISPATCH(nv, CALL)                   \
+  switch (nv) {                                    \
+    case 1: { constexpr int NV = 1; CALL; break; } \
+    case 2: { constexpr int NV = 2; CALL; break; } \
+    case 3:                                        \
+    case 4: { constexpr int NV = 4; CALL; break; } \
+    default: { constexpr int NV = 8; CALL; break; } \
+  }
+
 extern "C" int64_t va_rmsnorm_workspace_bytes(int64_t T, int64_t H) {
-  return static_cast<int64_t>(sizeof(float)) * ((T + kRowsPerBlock - 1) / kRowsPerBlock) * H;
+  const int64_t nblk = (T + bwd_rows_per_block(T) - 1) / bwd_rows_per_block(T);
+  return static_cast<int64_t>(sizeof(float)) * (nblk > 0 ? nblk : 1) * H;
 }
 
-extern "C" int va_rmsnorm_fwd(const void *x, const void *w, int dtype, int64_t T, int64_t H, float eps,
-                              void *y, float *rstd, void *stream) {
+extern "C" int va_rmsnorm_fwd(const void *x, const void *residual, const void *w, int dtype, int64_t T,
+                              int64_t H, float eps, void *h_out, void *y, float *rstd, void *stream) {
   VA_CHECK_ARG(dtype == VA_BF16, "rmsnorm: only bf16 is implemented");
-  VA_CHECK_ARG(T >= 0 && H > 0 && H <= 16384, "rmsnorm: bad shape");
+  VA_CHECK_ARG(T >= 0 && H > 0 && H % 8 == 0 && H <= 4096, "rmsnorm: need 0 < H <= 4096, H %% 8 == 0 (H=%lld)",
+               static_cast<long long>(H));
   if (T == 0) return VA_OK;
-  VA_CHECK_ARG(x && w && y && rstd, "null pointer argument");
-  hipLaunchKernelGGL(rmsnorm_fwd_kernel, dim3((T + 3) / 4), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const uint16_t *>(x), static_cast<const uint16_t *>(w), T, static_cast<int>(H),
-                     eps, static_cast<uint16_t *>(y), rstd);
+  VA_CHECK_ARG(x && w && y && rstd && (residual == nullptr || h_out != nullptr), "null pointer argument");
+  if (!(aligned16(x) && aligned16(residual) && aligned16(w) && aligned16(h_out) && aligned16(y))) {
+    set_error("rmsnorm: 16-byte aligned buffers required");
+    return VA_E_ALIGN;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const auto *xp = static_cast<const uint16_t *>(x);
+  const auto *rp = static_cast<const uint16_t *>(residual);
+  const auto *wp = static_cast<const uint16_t *>(w);
+  VA_NV_DISPATCH(nv_for(H), hipLaunchKernelGGL(add_rmsnorm_fwd_kernel<NV>, dim3((T + 3) / 4), dim3(256), 0, s, xp,
+                                               rp, wp, T, static_cast<int>(H), eps,
+                                               static_cast<uint16_t *>(h_out), static_cast<uint16_t *>(y), rstd));
   return check_launch("rmsnorm_fwd");
 }
 
-extern "C" int va_rmsnorm_bwd(const void *dy, const void *x, const void *w, const float *rstd, int dtype,
-                              int64_t T, int64_t H, void *dx, void *dw, float *workspace, void *stream) {
+extern "C" int va_rmsnorm_bwd(const void *dy, const void *h, const void *w, const float *rstd, const void *dres,
+                              int dtype, int64_t T, int64_t H, void *dx, void *dw, float *workspace,
+                              void *stream) {
   VA_CHECK_ARG(dtype == VA_BF16, "rmsnorm: only bf16 is implemented");
-  VA_CHECK_ARG(T >= 0 && H > 0 && H <= 8192, "rmsnorm: bad shape");
-  VA_CHECK_ARG(dy && x && w && rstd && dx && dw && workspace, "null pointer argument");
+  VA_CHECK_ARG(T >= 0 && H > 0 && H % 8 == 0 && H <= 4096, "rmsnorm: need 0 < H <= 4096, H %% 8 == 0");
+  VA_CHECK_ARG(dy && h && w && rstd && dx && dw && workspace, "null pointer argument");
+  if (!(aligned16(dy) && aligned16(h) && aligned16(w) && aligned16(dres) && aligned16(dx))) {
+    set_error("rmsnorm: 16-byte aligned buffers required");
+    return VA_E_ALIGN;
+  }
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t nblk = (T + kRowsPerBlock - 1) / kRowsPerBlock;
+  const int64_t rpb = bwd_rows_per_block(T);
+  const int64_t nblk = (T + rpb - 1) / rpb;
   if (nblk > 0) {
     const size_t shm = static_cast<size_t>(4 * H) * sizeof(float);
-    if (shm > 64 * 1024 &&
-        hipFuncSetAttribute(reinterpret_cast<const void *>(&rmsnorm_bwd_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)) != hipSuccess) {
-      set_error("rmsnorm_bwd: cannot reserve %zu bytes of LDS", shm);
-      return VA_E_LAUNCH;
-    }
-    hipLaunchKernelGGL(rmsnorm_bwd_kernel, dim3(nblk), dim3(256), shm, s, static_cast<const uint16_t *>(dy),
-                       static_cast<const uint16_t *>(x), static_cast<const uint16_t *>(w), rstd, T,
-                       static_cast<int>(H), static_cast<uint16_t *>(dx), workspace);
+    const auto *dyp = static_cast<const uint16_t *>(dy);
+    const auto *hp = static_cast<const uint16_t *>(h);
+    const auto *wp = static_cast<const uint16_t *>(w);
+    const auto *dr = static_cast<const uint16_t *>(dres);
+    auto *dxp = static_cast<uint16_t *>(dx);
+    VA_NV_DISPATCH(nv_for(H), {
+      if (shm > 64 * 1024 &&
+          hipFuncSetAttribute(reinterpret_cast<const void *>(&add_rmsnorm_bwd_kernel<NV>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)) != hipSuccess) {
+        set_error("rmsnorm_bwd: cannot reserve %zu bytes of LDS", shm);
+        return VA_E_LAUNCH;
+      }
+      hipLaunchKernelGGL(add_rmsnorm_bwd_kernel<NV>, dim3(nblk), dim3(256), shm, s, dyp, hp, wp, rstd, dr, T,
+                         static_cast<int>(H), static_cast<int>(rpb), dxp, workspace);
+    });
   }
-  hipLaunchKernelGGL(colsum_to_bf16_kernel, dim3((H + 255) / 256), dim3(256), 0, s, workspace,
+  hipLaunchKernelGGL(colsum_to_bf16_kernel, dim3((H + 63) / 64), dim3(1024), 0, s, workspace,
                      static_cast<int>(nblk), static_cast<int>(H), static_cast<uint16_t *>(dw));
   return check_launch("rmsnorm_bwd");
 }
@@ -256,8 +408,10 @@ extern "C" int va_swiglu_fwd(const void *g, const void *u, int dtype, int64_t n,
   VA_CHECK_ARG(dtype == VA_BF16, "swiglu: only bf16 is implemented");
   if (n == 0) return VA_OK;
   VA_CHECK_ARG(g && u && y && n > 0, "bad arguments");
-  VA_CHECK_ARG(reinterpret_cast<uintptr_t>(g) % 16 == 0 && reinterpret_cast<uintptr_t>(u) % 16 == 0 &&
-                   reinterpret_cast<uintptr_t>(y) % 16 == 0, "swiglu: 16-byte aligned buffers required");
+  if (!(aligned16(g) && aligned16(u) && aligned16(y))) {
+    set_error("swiglu: 16-byte aligned buffers required");
+    return VA_E_ALIGN;
+  }
   hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(n, 8)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      static_cast<const uint16_t *>(g), static_cast<const uint16_t *>(u), n,
                      static_cast<uint16_t *>(y));
@@ -269,9 +423,10 @@ extern "C" int va_swiglu_bwd(const void *dy, const void *g, const void *u, int d
   VA_CHECK_ARG(dtype == VA_BF16, "swiglu: only bf16 is implemented");
   if (n == 0) return VA_OK;
   VA_CHECK_ARG(dy && g && u && dg && du && n > 0, "bad arguments");
-  VA_CHECK_ARG(reinterpret_cast<uintptr_t>(dy) % 16 == 0 && reinterpret_cast<uintptr_t>(g) % 16 == 0 &&
-                   reinterpret_cast<uintptr_t>(u) % 16 == 0 && reinterpret_cast<uintptr_t>(dg) % 16 == 0 &&
-                   reinterpret_cast<uintptr_t>(du) % 16 == 0, "swiglu: 16-byte aligned buffers required");
+  if (!(aligned16(dy) && aligned16(g) && aligned16(u) && aligned16(dg) && aligned16(du))) {
+    set_error("swiglu: 16-byte aligned buffers required");
+    return VA_E_ALIGN;
+  }
   hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(n, 8)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      static_cast<const uint16_t *>(dy), static_cast<const uint16_t *>(g),
                      static_cast<const uint16_t *>(u), n, static_cast<uint16_t *>(dg),
@@ -279,17 +434,50 @@ extern "C" int va_swiglu_bwd(const void *dy, const void *g, const void *u, int d
   return check_launch("swiglu_bwd");
 }
 
-extern "C" int va_rope(const void *q, const void *k, const void *cos, const void *sin, int dtype, int64_t T,
-                       int64_t Hq, int64_t Hk, int64_t D, int backward, void *qo, void *ko, void *stream) {
+static int rope_checks(int dtype, int64_t T, int64_t Hq, int64_t Hk, int64_t D, int64_t ld) {
   VA_CHECK_ARG(dtype == VA_BF16, "rope: only bf16 is implemented");
-  VA_CHECK_ARG(T >= 0 && Hq > 0 && Hk >= 0 && D > 0 && D % 2 == 0, "rope: bad shape");
+  VA_CHECK_ARG(T >= 0 && Hq > 0 && Hk > 0 && D > 0 && D % 16 == 0, "rope: need D %% 16 == 0 and Hq, Hk > 0");
+  VA_CHECK_ARG(ld >= (Hq + 2 * Hk) * D && ld % 8 == 0, "rope: merged row stride %lld too small or unaligned",
+               static_cast<long long>(ld));
+  return VA_OK;
+}
+
+extern "C" int va_rope_qkv_fwd(const void *qkv, int64_t ld, const void *cos, const void *sin, int dtype,
+                               int64_t T, int64_t Hq, int64_t Hk, int64_t D, void *q, void *k, void *v,
+                               void *stream) {
+  const int rc = rope_checks(dtype, T, Hq, Hk, D, ld);
+  if (rc != VA_OK) return rc;
   if (T == 0) return VA_OK;
-  VA_CHECK_ARG(q && cos && sin && qo && (Hk == 0 || (k && ko)), "null pointer argument");
-  const int64_t total = T * (Hq + Hk) * (D / 2);
-  hipLaunchKernelGGL(rope_kernel, dim3(grid_for(total, 4)), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(k),
-                     static_cast<const uint16_t *>(cos), static_cast<const uint16_t *>(sin), T,
-                     static_cast<int>(Hq), static_cast<int>(Hk), static_cast<int>(D), backward,
-                     static_cast<uint16_t *>(qo), static_cast<uint16_t *>(ko));
-  return check_launch("rope");
+  VA_CHECK_ARG(qkv && cos && sin && q && k && v, "null pointer argument");
+  if (!(aligned16(qkv) && aligned16(cos) && aligned16(sin) && aligned16(q) && aligned16(k) && aligned16(v))) {
+    set_error("rope: 16-byte aligned buffers required");
+    return VA_E_ALIGN;
+  }
+  const int64_t total = T * (Hq + 2 * Hk) * (D / 16);
+  hipLaunchKernelGGL(rope_qkv_fwd_kernel, dim3(grid_for(total, 1)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint16_t *>(qkv), ld, static_cast<const uint16_t *>(cos),
+                     static_cast<const uint16_t *>(sin), T, static_cast<int>(Hq), static_cast<int>(Hk),
+                     static_cast<int>(D), static_cast<uint16_t *>(q), static_cast<uint16_t *>(k),
+                     static_cast<uint16_t *>(v));
+  return check_launch("rope_qkv_fwd");
+}
+
+extern "C" int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *cos, const void *sin,
+                               int dtype, int64_t T, int64_t Hq, int64_t Hk, int64_t D, void *dqkv, int64_t ld,
+                               void *stream) {
+  const int rc = rope_checks(dtype, T, Hq, Hk, D, ld);
+  if (rc != VA_OK) return rc;
+  if (T == 0) return VA_OK;
+  VA_CHECK_ARG(dq && dk && dv && cos && sin && dqkv, "null pointer argument");
+  if (!(aligned16(dq) && aligned16(dk) && aligned16(dv) && aligned16(cos) && aligned16(sin) && aligned16(dqkv))) {
+    set_error("rope: 16-byte aligned buffers required");
+    return VA_E_ALIGN;
+  }
+  const int64_t total = T * (Hq + 2 * Hk) * (D / 16);
+  hipLaunchKernelGGL(rope_qkv_bwd_kernel, dim3(grid_for(total, 1)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint16_t *>(dq), static_cast<const uint16_t *>(dk),
+                     static_cast<const uint16_t *>(dv), static_cast<const uint16_t *>(cos),
+                     static_cast<const uint16_t *>(sin), T, static_cast<int>(Hq), static_cast<int>(Hk),
+                     static_cast<int>(D), static_cast<uint16_t *>(dqkv), ld);
+  return check_launch("rope_qkv_bwd");
 }

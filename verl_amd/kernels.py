@@ -444,40 +444,67 @@ def accumulate_grads(srcs: list, dsts: list, scale: float = 1.0) -> None:
 # =============================================================================== fused model ops (bf16)
 def _bf16_only(*ts):
     for t in ts:
-        if t.dtype != torch.bfloat16:
+        if t is not None and t.dtype != torch.bfloat16:
             raise TypeError(f"fused model ops are bf16-only, got {t.dtype}")
 
 
-class _RMSNorm(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, w, eps):
-        H = x.shape[-1]
-        x2 = x.reshape(-1, H).contiguous()
-        y = torch.empty_like(x2)
-        rstd = torch.empty(x2.shape[0], dtype=torch.float32, device=x.device)
-        L.call("va_rmsnorm_fwd", _p(x2), _p(w), L.VA_BF16, x2.shape[0], H, float(eps), _p(y), _p(rstd), _stream(x2))
-        ctx.save_for_backward(x2, w, rstd)
-        ctx.shape = x.shape
-        return y.view(x.shape)
+class _AddRMSNorm(torch.autograd.Function):
+    """(x, residual | None, w) -> (h = x + residual, y = RMSNorm(h) * w); without a residual only y."""
 
     @staticmethod
-    def backward(ctx, dy):
-        x2, w, rstd = ctx.saved_tensors
-        T, H = x2.shape
+    def forward(ctx, x, res, w, eps):
+        H = x.shape[-1]
+        x2 = x.reshape(-1, H).contiguous()
+        T = x2.shape[0]
+        y = torch.empty_like(x2)
+        rstd = torch.empty(T, dtype=torch.float32, device=x.device)
+        if res is not None:
+            r2 = res.reshape(T, H).contiguous()
+            h = torch.empty_like(x2)
+        else:
+            r2, h = None, x2
+        L.call("va_rmsnorm_fwd", _p(x2), _p(r2), _p(w), L.VA_BF16, T, H, float(eps), _p(h if res is not None else None),
+               _p(y), _p(rstd), _stream(x2))
+        ctx.save_for_backward(h, w, rstd)
+        ctx.shape = x.shape
+        ctx.has_res = res is not None
+        if res is None:
+            return y.view(x.shape)
+        return h.view(x.shape), y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        h, w, rstd = ctx.saved_tensors
+        T, H = h.shape
+        if ctx.has_res:
+            dh, dy = grads
+        else:
+            dh, dy = None, grads[0]
         dy2 = dy.reshape(T, H).contiguous()
-        dx = torch.empty_like(x2)
+        dh2 = dh.reshape(T, H).contiguous() if dh is not None else None
+        dx = torch.empty_like(h)
         dw = torch.empty_like(w)
         nb = L.load().va_rmsnorm_workspace_bytes(T, H)
-        ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=x2.device)
-        L.call("va_rmsnorm_bwd", _p(dy2), _p(x2), _p(w), _p(rstd), L.VA_BF16, T, H, _p(dx), _p(dw), _p(ws), _stream(x2))
-        return dx.view(ctx.shape), dw, None
+        ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=h.device)
+        L.call("va_rmsnorm_bwd", _p(dy2), _p(h), _p(w), _p(rstd), _p(dh2), L.VA_BF16, T, H, _p(dx), _p(dw), _p(ws),
+               _stream(h))
+        dx = dx.view(ctx.shape)
+        return dx, (dx if ctx.has_res else None), dw, None
 
 
 def rmsnorm(x, weight, eps: float):
     """Qwen2RMSNorm forward in one kernel (bf16)."""
     _require_device(x, weight)
     _bf16_only(x, weight)
-    return _RMSNorm.apply(x, weight, eps)
+    return _AddRMSNorm.apply(x, None, weight, eps)
+
+
+def add_rmsnorm(x, residual, weight, eps: float):
+    """h = residual + x (bf16) and RMSNorm(h) in one kernel: returns (h, y). The residual
+    stream's gradient and the norm's gradient are summed inside the backward kernel."""
+    _require_device(x, residual, weight)
+    _bf16_only(x, residual, weight)
+    return _AddRMSNorm.apply(x, residual, weight, eps)
 
 
 class _SwiGLU(torch.autograd.Function):
@@ -506,34 +533,42 @@ def swiglu(gate, up):
     return _SwiGLU.apply(gate, up)
 
 
-class _RoPE(torch.autograd.Function):
+class _RoPEQKV(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, cos, sin):
-        T, Hq, D = q.shape
-        Hk = k.shape[1]
-        q2, k2 = q.contiguous(), k.contiguous()
-        c, s = cos.reshape(T, D).contiguous(), sin.reshape(T, D).contiguous()
-        qo, ko = torch.empty_like(q2), torch.empty_like(k2)
-        L.call("va_rope", _p(q2), _p(k2), _p(c), _p(s), L.VA_BF16, T, Hq, Hk, D, 0, _p(qo), _p(ko), _stream(q2))
+    def forward(ctx, qkv, cos, sin, hq, hk, d):
+        T = qkv.shape[0]
+        if qkv.stride(-1) != 1:
+            qkv = qkv.contiguous()
+        ld = qkv.stride(0)
+        c, s = cos.reshape(T, d).contiguous(), sin.reshape(T, d).contiguous()
+        q = torch.empty(T, hq, d, dtype=qkv.dtype, device=qkv.device)
+        k = torch.empty(T, hk, d, dtype=qkv.dtype, device=qkv.device)
+        v = torch.empty(T, hk, d, dtype=qkv.dtype, device=qkv.device)
+        L.call("va_rope_qkv_fwd", _p(qkv), ld, _p(c), _p(s), L.VA_BF16, T, hq, hk, d, _p(q), _p(k), _p(v), _stream(qkv))
         ctx.save_for_backward(c, s)
-        return qo, ko
+        ctx.dims = (hq, hk, d, qkv.shape[1])
+        return q, k, v
 
     @staticmethod
-    def backward(ctx, dqo, dko):
+    def backward(ctx, dq, dk, dv):
         c, s = ctx.saved_tensors
-        T, D = c.shape
-        dqo = dqo.contiguous()
-        dko = torch.zeros(0) if dko is None else dko.contiguous()
-        Hq = dqo.shape[1]
-        Hk = dko.shape[1] if dko.dim() == 3 else 0
-        dq, dk = torch.empty_like(dqo), (torch.empty_like(dko) if Hk else None)
-        L.call("va_rope", _p(dqo), _p(dko) if Hk else None, _p(c), _p(s), L.VA_BF16, T, Hq, Hk, D, 1, _p(dq),
-               _p(dk), _stream(dqo))
-        return dq, dk, None, None
+        hq, hk, d, width = ctx.dims
+        T = c.shape[0]
+        dq = dq.contiguous() if dq is not None else torch.zeros(T, hq, d, dtype=c.dtype, device=c.device)
+        dk = dk.contiguous() if dk is not None else torch.zeros(T, hk, d, dtype=c.dtype, device=c.device)
+        dv = dv.contiguous() if dv is not None else torch.zeros(T, hk, d, dtype=c.dtype, device=c.device)
+        dqkv = torch.empty(T, width, dtype=dq.dtype, device=dq.device)
+        L.call("va_rope_qkv_bwd", _p(dq), _p(dk), _p(dv), _p(c), _p(s), L.VA_BF16, T, hq, hk, d, _p(dqkv), width,
+               _stream(dqkv))
+        return dqkv, None, None, None, None, None
 
 
-def rope(q, k, cos, sin):
-    """apply_rotary_pos_emb (rotate_half form) on [T, H, D] q and k, one kernel (bf16)."""
-    _require_device(q, k, cos, sin)
-    _bf16_only(q, k, cos, sin)
-    return _RoPE.apply(q, k, cos, sin)
+def rope_qkv(qkv, cos, sin, num_q_heads: int, num_kv_heads: int, head_dim: int):
+    """Split the merged q|k|v projection [T, (Hq+2Hk)*D] into flash varlen's [T, H, D] tensors and
+    apply apply_rotary_pos_emb (rotate_half form) to q and k, in one kernel (bf16)."""
+    _require_device(qkv, cos, sin)
+    _bf16_only(qkv, cos, sin)
+    if qkv.dim() != 2 or qkv.shape[1] != (num_q_heads + 2 * num_kv_heads) * head_dim:
+        raise ValueError(f"rope_qkv: qkv {tuple(qkv.shape)} does not hold {num_q_heads}+2x{num_kv_heads} heads of "
+                         f"{head_dim}")
+    return _RoPEQKV.apply(qkv, cos, sin, num_q_heads, num_kv_heads, head_dim)

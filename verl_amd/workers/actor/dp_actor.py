@@ -113,9 +113,10 @@ class DataParallelPPOActor(BasePPOActor):
         self.device_name = "cuda"
         # bf16 autocast as the reference (dp_actor.py:100); None runs the model in its own dtype
         self.autocast_dtype = self.config.get("autocast_dtype", torch.bfloat16)
-        # fused RMSNorm / SwiGLU / RoPE kernels on the packed path (bf16 weights only)
+        # packed Qwen2 backbone with the fused add+RMSNorm / q|k|v+RoPE / SwiGLU kernels
+        # (qwen2_fused.py; bf16 weights only, decided on first use)
         self.fused_model_ops = self.use_remove_padding and self.config.get("fused_model_ops", True)
-        self._patched = False
+        self._fused_backbone = None
 
     # ------------------------------------------------------------------ forward
     def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False, packing: _Packing = None):
@@ -127,11 +128,6 @@ class DataParallelPPOActor(BasePPOActor):
         ac = self.autocast_dtype
         with torch.autocast(device_type=self.device_name, dtype=ac or torch.bfloat16, enabled=ac is not None):
             if self.use_remove_padding:
-                if self.fused_model_ops and not self._patched:
-                    from .qwen2_fused import patch_qwen2
-
-                    patch_qwen2(self.actor_module)
-                    self._patched = True
                 if packing is None:
                     packing = _plan_packing(micro_batch["attention_mask"].cpu().numpy(), R, input_ids.device)
                 ids = input_ids.reshape(-1).index_select(0, packing.token_idx).unsqueeze(0)
@@ -139,12 +135,21 @@ class DataParallelPPOActor(BasePPOActor):
                 if pos_ids.dim() == 3:
                     raise NotImplementedError("mrope position ids (VLM) are out of scope")
                 pos = pos_ids.reshape(-1).index_select(0, packing.token_idx).unsqueeze(0)
-                out = self._backbone(
-                    input_ids=ids, position_ids=pos, attention_mask=_NO_MASK, use_cache=False,
-                    cu_seq_lens_q=packing.cu_seqlens, cu_seq_lens_k=packing.cu_seqlens,
-                    max_length_q=packing.max_seqlen, max_length_k=packing.max_seqlen,
-                )
-                hidden = out.last_hidden_state[0]
+                if self._fused_backbone is None:
+                    from . import qwen2_fused
+
+                    self._fused_backbone = self.fused_model_ops and qwen2_fused.supports(self._backbone)
+                if self._fused_backbone:
+                    from .qwen2_fused import packed_forward
+
+                    hidden = packed_forward(self._backbone, ids[0], pos[0], packing.cu_seqlens, packing.max_seqlen)
+                else:
+                    out = self._backbone(
+                        input_ids=ids, position_ids=pos, attention_mask=_NO_MASK, use_cache=False,
+                        cu_seq_lens_q=packing.cu_seqlens, cu_seq_lens_k=packing.cu_seqlens,
+                        max_length_q=packing.max_seqlen, max_length_k=packing.max_seqlen,
+                    )
+                    hidden = out.last_hidden_state[0]
                 h_sel = hidden.index_select(0, packing.sel_hidden)
                 logits = self._lm_head(h_sel)
                 labels = responses.reshape(-1).index_select(0, packing.sel_out)

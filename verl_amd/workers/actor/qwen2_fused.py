@@ -1,72 +1,97 @@
-"""Per-instance patch of an HF Qwen2 backbone for the packed (remove-padding) actor path.
+"""Packed (remove-padding) Qwen2 backbone forward for the actor on MI355X.
 
-The reference patches HF attention for flash-attn varlen + Ulysses (verl/models/transformers/
-monkey_patch.py:50-192). Here the patch serves MI355X launch efficiency: for bf16 weights it
-replaces, module instance by module instance,
+The reference runs the HF model on packed tokens with flash-attn varlen patched into HF attention
+(verl/models/transformers/monkey_patch.py:50-192, dp_actor.py:104-180). Here the same math runs
+through one function that owns the layer loop, so that per decoder layer the work is
 
-  Qwen2RMSNorm.forward  -> one fused kernel fwd, one bwd (+ column-sum for dw)   (~8+10 ops before)
-  Qwen2MLP.forward      -> gate/up GEMMs + one fused SwiGLU kernel + down GEMM    (2+3 ops before)
-  Qwen2Attention.forward-> q/k/v GEMMs written as [T, H, D] views, one fused RoPE kernel that also
-                           produces flash varlen's layout (no transposes / contiguous copies),
-                           varlen attention, o GEMM                                (~16 ops before)
+  add_rmsnorm (residual add + input_layernorm, one kernel; its bwd also sums the residual grad)
+  q|k|v projection as ONE GEMM (weights concatenated per call: 2 MB at H=896)
+  rope_qkv   (split q/k/v into flash varlen's [T, H, D] layout + rotary, one kernel)
+  flash varlen attention, o_proj GEMM
+  add_rmsnorm (residual add + post_attention_layernorm)
+  gate / up GEMMs, swiglu (one kernel), down GEMM
 
-Forward numerics keep HF's bf16 rounding points (see verl_amd/csrc/model_ops.hip). Other
-architectures are left untouched.
+instead of the ~45 PyTorch kernels HF issues (norm chains, adds, transposes, rotary, bias
+reductions x3). Forward numerics keep HF's bf16 rounding points (see csrc/model_ops.hip), so
+the result matches the HF module graph to bf16 rounding (tests/test_model_ops_gpu.py).
+
+Only bf16 Qwen2-family backbones (RMSNorm + SwiGLU MLP + rotate_half RoPE + GQA with q/k/v bias)
+take this path; anything else keeps the HF forward.
 """
 
 from __future__ import annotations
 
-import types
-
 import torch
+import torch.nn.functional as F
 
 from ... import kernels as K
 from . import attention
 
 
-def _norm_forward(self, hidden_states):
-    return K.rmsnorm(hidden_states, self.weight, self.variance_epsilon)
-
-
-def _mlp_forward(self, x):
-    return self.down_proj(K.swiglu(self.gate_proj(x), self.up_proj(x)))
-
-
-def _attn_forward(self, hidden_states, position_embeddings, attention_mask=None, past_key_values=None, **kwargs):
-    cu = kwargs.get("cu_seq_lens_q")
-    mx = kwargs.get("max_length_q")
-    if cu is None or hidden_states.shape[0] != 1:
-        raise RuntimeError("fused Qwen2 attention serves the packed varlen path (batch 1 + cu_seq_lens_q)")
-    x = hidden_states[0]
-    T = x.shape[0]
-    D = self.head_dim
-    q = self.q_proj(x).view(T, -1, D)
-    k = self.k_proj(x).view(T, -1, D)
-    v = self.v_proj(x).view(T, -1, D)
-    cos, sin = position_embeddings
-    q, k = K.rope(q, k, cos, sin)
-    out = attention.packed_attention(q, k, v, cu, mx, scaling=self.scaling)
-    out = self.o_proj(out.reshape(T, -1))
-    return out.unsqueeze(0), None
-
-
-def patch_qwen2(model: torch.nn.Module) -> int:
-    """Patch every Qwen2 RMSNorm / MLP / Attention instance in ``model`` whose weights are bf16.
-    Returns the number of patched modules (0 for other architectures)."""
+def supports(backbone: torch.nn.Module) -> bool:
     try:
         from transformers.models.qwen2 import modeling_qwen2 as m
     except ImportError:  # pragma: no cover
-        return 0
-    n = 0
-    for mod in model.modules():
-        if isinstance(mod, m.Qwen2RMSNorm) and mod.weight.dtype == torch.bfloat16:
-            mod.forward = types.MethodType(_norm_forward, mod)
-            n += 1
-        elif isinstance(mod, m.Qwen2MLP) and mod.gate_proj.weight.dtype == torch.bfloat16 \
-                and mod.config.hidden_act == "silu":
-            mod.forward = types.MethodType(_mlp_forward, mod)
-            n += 1
-        elif isinstance(mod, m.Qwen2Attention) and mod.q_proj.weight.dtype == torch.bfloat16:
-            mod.forward = types.MethodType(_attn_forward, mod)
-            n += 1
-    return n
+        return False
+    if not isinstance(backbone, m.Qwen2Model):
+        return False
+    cfg = backbone.config
+    if getattr(cfg, "hidden_act", "silu") != "silu" or getattr(cfg, "use_sliding_window", False):
+        return False
+    if getattr(cfg, "rope_scaling", None) not in (None, {}) and \
+            (cfg.rope_scaling or {}).get("rope_type", "default") != "default":
+        return False
+    h = cfg.hidden_size
+    if h % 8 or h > 4096:
+        return False
+    d = getattr(cfg, "head_dim", None) or h // cfg.num_attention_heads
+    if d % 16:
+        return False
+    return all(p.dtype == torch.bfloat16 for p in backbone.parameters())
+
+
+def _qkv_weight(attn):
+    w = torch.cat([attn.q_proj.weight, attn.k_proj.weight, attn.v_proj.weight], dim=0)
+    if attn.q_proj.bias is None:
+        return w, None
+    return w, torch.cat([attn.q_proj.bias, attn.k_proj.bias, attn.v_proj.bias], dim=0)
+
+
+def _attention(attn, y, cos, sin, cu, max_len, hq, hk, d):
+    T = y.shape[0]
+    w, b = _qkv_weight(attn)
+    qkv = F.linear(y, w, b)
+    q, k, v = K.rope_qkv(qkv, cos, sin, hq, hk, d)
+    out = attention.packed_attention(q, k, v, cu, max_len, scaling=attn.scaling)
+    return attn.o_proj(out.reshape(T, hq * d))
+
+
+def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor, cu_seqlens: torch.Tensor,
+                   max_seqlen: int) -> torch.Tensor:
+    """input_ids / position_ids [T] (packed), cu_seqlens [B+1] int32 -> last hidden state [T, H] bf16
+    (after the final norm), i.e. Qwen2Model(...).last_hidden_state[0] on the same packing."""
+    cfg = backbone.config
+    hq = cfg.num_attention_heads
+    hk = cfg.num_key_value_heads
+    d = getattr(cfg, "head_dim", None) or cfg.hidden_size // hq
+    x = backbone.embed_tokens(input_ids)  # [T, H]
+    cos, sin = backbone.rotary_emb(x.unsqueeze(0), position_ids.unsqueeze(0))  # [1, T, D] bf16
+    residual = x
+    layers = backbone.layers[: cfg.num_hidden_layers]
+    h = None
+    for i, layer in enumerate(layers):
+        ln = layer.input_layernorm
+        if i == 0:
+            y = K.rmsnorm(residual, ln.weight, ln.variance_epsilon)
+        else:
+            residual, y = K.add_rmsnorm(h, residual, ln.weight, ln.variance_epsilon)
+        a = _attention(layer.self_attn, y, cos, sin, cu_seqlens, max_seqlen, hq, hk, d)
+        ln = layer.post_attention_layernorm
+        residual, y = K.add_rmsnorm(a, residual, ln.weight, ln.variance_epsilon)
+        mlp = layer.mlp
+        h = mlp.down_proj(K.swiglu(mlp.gate_proj(y), mlp.up_proj(y)))
+    norm = backbone.norm
+    if h is None:
+        return K.rmsnorm(residual, norm.weight, norm.variance_epsilon)
+    _, y = K.add_rmsnorm(h, residual, norm.weight, norm.variance_epsilon)
+    return y
