@@ -237,7 +237,9 @@ int va_accumulate_grads(int n_tensors, const void *const *src, const int64_t *nu
  *                rstd [T] fp32. x, residual, h_out, y [T, H]; w [H].
  *   rmsnorm_bwd: dx = d/dh of y given dy, plus dres (the gradient reaching h through the residual
  *                stream; NULL = none); dw [H] bf16; workspace of va_rmsnorm_workspace_bytes(T, H).
- *   swiglu:      y = silu(g) * u over n elements; bwd writes dg, du.
+ *   swiglu:      y [T, F] = silu(g) * u where g / u are rows of gu [T, ldgu] (u at column offset uoff;
+ *                the merged gate|up projection has ldgu = 2F, uoff = F); bwd writes dg / du into dgu
+ *                [T, lddgu] at column offsets 0 / duoff. F, strides and offsets multiples of 8.
  *   rope_qkv:    qkv [T, ld] holds q | k | v ([Hq | Hk | Hk] x D per row); fwd writes rotated
  *                q [T, Hq, D], k [T, Hk, D] and v [T, Hk, D] (rotate_half convention, cos / sin
  *                [T, D]); bwd applies the transposed rotation and writes dqkv [T, ld]. D % 16 == 0.
@@ -247,9 +249,10 @@ int va_rmsnorm_fwd(const void *x, const void *residual, const void *w, int dtype
                    void *h_out, void *y, float *rstd, void *stream);
 int va_rmsnorm_bwd(const void *dy, const void *h, const void *w, const float *rstd, const void *dres, int dtype,
                    int64_t T, int64_t H, void *dx, void *dw, float *workspace, void *stream);
-int va_swiglu_fwd(const void *g, const void *u, int dtype, int64_t n, void *y, void *stream);
-int va_swiglu_bwd(const void *dy, const void *g, const void *u, int dtype, int64_t n, void *dg, void *du,
+int va_swiglu_fwd(const void *gu, int64_t ldgu, int64_t uoff, int dtype, int64_t T, int64_t F, void *y,
                   void *stream);
+int va_swiglu_bwd(const void *dy, const void *gu, int64_t ldgu, int64_t uoff, int dtype, int64_t T, int64_t F,
+                  void *dgu, int64_t lddgu, int64_t duoff, void *stream);
 int va_rope_qkv_fwd(const void *qkv, int64_t ld, const void *cos, const void *sin, int dtype, int64_t T,
                     int64_t Hq, int64_t Hk, int64_t D, void *q, void *k, void *v, void *stream);
 int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *cos, const void *sin, int dtype,

@@ -70,8 +70,8 @@ _SIGNATURES: dict[str, tuple] = {
     "va_rmsnorm_workspace_bytes": (c_int64, [c_int64, c_int64]),
     "va_rmsnorm_fwd": (c_int, [_P, _P, _P, c_int, c_int64, c_int64, c_float, _P, _P, _P, _P]),
     "va_rmsnorm_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, _P, _P, _P, _P]),
-    "va_swiglu_fwd": (c_int, [_P, _P, c_int, c_int64, _P, _P]),
-    "va_swiglu_bwd": (c_int, [_P, _P, _P, c_int, c_int64, _P, _P, _P]),
+    "va_swiglu_fwd": (c_int, [_P, c_int64, c_int64, c_int, c_int64, c_int64, _P, _P]),
+    "va_swiglu_bwd": (c_int, [_P, _P, c_int64, c_int64, c_int, c_int64, c_int64, _P, c_int64, c_int64, _P]),
     "va_rope_qkv_fwd": (c_int, [_P, c_int64, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, _P, _P, _P]),
     "va_rope_qkv_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, c_int64, _P]),
 }

@@ -182,54 +182,55 @@ __global__ __launch_bounds__(1024) void colsum_to_bf16_kernel(const float *__res
 }
 
 // ------------------------------------------------------------------ SwiGLU
+// gate / up are rows of a merged [T, ldgu] projection output (u at column offset `uoff`, so the
+// plain two-tensor case is ldgu = F, uoff = u - g); y is [T, F].  Backward writes dg / du into the
+// same merged layout (the gradient of the merged gate|up GEMM).
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
-__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const uint16_t *__restrict__ g,
-                                                         const uint16_t *__restrict__ u, int64_t n,
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const uint16_t *__restrict__ gu, int64_t ldgu,
+                                                         int64_t uoff, int64_t T, int F,
                                                          uint16_t *__restrict__ y) {
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256 * 8;
-  for (int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 8; i < n; i += stride) {
-    if (i + 8 <= n) {
-      float g8[8], u8[8], o[8];
-      unpack8(ld16(g + i), g8);
-      unpack8(ld16(u + i), u8);
+  const int vpr = F >> 3;
+  const int64_t total = T * vpr;
+  for (int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; idx < total;
+       idx += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t t = idx / vpr;
+    const int c = static_cast<int>(idx - t * vpr) * 8;
+    const uint16_t *gr = gu + t * ldgu + c;
+    float g8[8], u8[8], o[8];
+    unpack8(ld16(gr), g8);
+    unpack8(ld16(gr + uoff), u8);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = rbf(silu(g8[e])) * u8[e];
-      st16(y + i, pack8(o));
-    } else {
-      for (int64_t j = i; j < n; ++j) y[j] = to_bf(rbf(silu(bf(g[j]))) * bf(u[j]));
-    }
+    for (int e = 0; e < 8; ++e) o[e] = rbf(silu(g8[e])) * u8[e];
+    st16(y + t * F + c, pack8(o));
   }
 }
 
 __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const uint16_t *__restrict__ dy,
-                                                         const uint16_t *__restrict__ g,
-                                                         const uint16_t *__restrict__ u, int64_t n,
-                                                         uint16_t *__restrict__ dg,
-                                                         uint16_t *__restrict__ du) {
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256 * 8;
-  for (int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 8; i < n; i += stride) {
-    if (i + 8 <= n) {
-      float d8[8], g8[8], u8[8], rg[8], ru[8];
-      unpack8(ld16(dy + i), d8);
-      unpack8(ld16(g + i), g8);
-      unpack8(ld16(u + i), u8);
+                                                         const uint16_t *__restrict__ gu, int64_t ldgu,
+                                                         int64_t uoff, int64_t T, int F,
+                                                         uint16_t *__restrict__ dgu, int64_t lddgu,
+                                                         int64_t duoff) {
+  const int vpr = F >> 3;
+  const int64_t total = T * vpr;
+  for (int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; idx < total;
+       idx += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t t = idx / vpr;
+    const int c = static_cast<int>(idx - t * vpr) * 8;
+    const uint16_t *gr = gu + t * ldgu + c;
+    float d8[8], g8[8], u8[8], rg[8], ru[8];
+    unpack8(ld16(dy + t * F + c), d8);
+    unpack8(ld16(gr), g8);
+    unpack8(ld16(gr + uoff), u8);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float s = 1.f / (1.f + __expf(-g8[e]));
-        ru[e] = d8[e] * rbf(g8[e] * s);
-        rg[e] = d8[e] * u8[e] * (s * (1.f + g8[e] * (1.f - s)));
-      }
-      st16(dg + i, pack8(rg));
-      st16(du + i, pack8(ru));
-    } else {
-      for (int64_t j = i; j < n; ++j) {
-        const float d = bf(dy[j]), gg = bf(g[j]), uu = bf(u[j]);
-        const float s = 1.f / (1.f + __expf(-gg));
-        du[j] = to_bf(d * rbf(gg * s));
-        dg[j] = to_bf(d * uu * (s * (1.f + gg * (1.f - s))));
-      }
+    for (int e = 0; e < 8; ++e) {
+      const float s = 1.f / (1.f + __expf(-g8[e]));
+      ru[e] = d8[e] * rbf(g8[e] * s);
+      rg[e] = d8[e] * u8[e] * (s * (1.f + g8[e] * (1.f - s)));
     }
+    uint16_t *dr = dgu + t * lddgu + c;
+    st16(dr, pack8(rg));
+    st16(dr + duoff, pack8(ru));
   }
 }
 
@@ -404,33 +405,39 @@ extern "C" int va_rmsnorm_bwd(const void *dy, const void *h, const void *w, cons
   return check_launch("rmsnorm_bwd");
 }
 
-extern "C" int va_swiglu_fwd(const void *g, const void *u, int dtype, int64_t n, void *y, void *stream) {
+extern "C" int va_swiglu_fwd(const void *gu, int64_t ldgu, int64_t uoff, int dtype, int64_t T, int64_t F, void *y,
+                             void *stream) {
   VA_CHECK_ARG(dtype == VA_BF16, "swiglu: only bf16 is implemented");
-  if (n == 0) return VA_OK;
-  VA_CHECK_ARG(g && u && y && n > 0, "bad arguments");
-  if (!(aligned16(g) && aligned16(u) && aligned16(y))) {
+  VA_CHECK_ARG(T >= 0 && F > 0 && F % 8 == 0 && ldgu % 8 == 0 && uoff % 8 == 0 && ldgu >= F,
+               "swiglu: need F %% 8 == 0 and 8-element aligned strides");
+  if (T == 0) return VA_OK;
+  VA_CHECK_ARG(gu && y, "null pointer argument");
+  if (!(aligned16(gu) && aligned16(y))) {
     set_error("swiglu: 16-byte aligned buffers required");
     return VA_E_ALIGN;
   }
-  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(n, 8)), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const uint16_t *>(g), static_cast<const uint16_t *>(u), n,
-                     static_cast<uint16_t *>(y));
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(T * (F / 8), 1)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint16_t *>(gu), ldgu, uoff, T,
+                     static_cast<int>(F), static_cast<uint16_t *>(y));
   return check_launch("swiglu_fwd");
 }
 
-extern "C" int va_swiglu_bwd(const void *dy, const void *g, const void *u, int dtype, int64_t n, void *dg,
-                             void *du, void *stream) {
+extern "C" int va_swiglu_bwd(const void *dy, const void *gu, int64_t ldgu, int64_t uoff, int dtype, int64_t T,
+                             int64_t F, void *dgu, int64_t lddgu, int64_t duoff, void *stream) {
   VA_CHECK_ARG(dtype == VA_BF16, "swiglu: only bf16 is implemented");
-  if (n == 0) return VA_OK;
-  VA_CHECK_ARG(dy && g && u && dg && du && n > 0, "bad arguments");
-  if (!(aligned16(dy) && aligned16(g) && aligned16(u) && aligned16(dg) && aligned16(du))) {
+  VA_CHECK_ARG(T >= 0 && F > 0 && F % 8 == 0 && ldgu % 8 == 0 && uoff % 8 == 0 && lddgu % 8 == 0 &&
+                   duoff % 8 == 0 && ldgu >= F && lddgu >= F,
+               "swiglu: need F %% 8 == 0 and 8-element aligned strides");
+  if (T == 0) return VA_OK;
+  VA_CHECK_ARG(dy && gu && dgu, "null pointer argument");
+  if (!(aligned16(dy) && aligned16(gu) && aligned16(dgu))) {
     set_error("swiglu: 16-byte aligned buffers required");
     return VA_E_ALIGN;
   }
-  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(n, 8)), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const uint16_t *>(dy), static_cast<const uint16_t *>(g),
-                     static_cast<const uint16_t *>(u), n, static_cast<uint16_t *>(dg),
-                     static_cast<uint16_t *>(du));
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(T * (F / 8), 1)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint16_t *>(dy),
+                     static_cast<const uint16_t *>(gu), ldgu, uoff, T, static_cast<int>(F),
+                     static_cast<uint16_t *>(dgu), lddgu, duoff);
   return check_launch("swiglu_bwd");
 }
 

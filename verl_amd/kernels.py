@@ -509,28 +509,79 @@ def add_rmsnorm(x, residual, weight, eps: float):
 
 class _SwiGLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, g, u):
-        g2, u2 = g.contiguous(), u.contiguous()
-        y = torch.empty_like(g2)
-        L.call("va_swiglu_fwd", _p(g2), _p(u2), L.VA_BF16, g2.numel(), _p(y), _stream(g2))
-        ctx.save_for_backward(g2, u2)
+    def forward(ctx, gu, F):
+        if gu.stride(-1) != 1 or gu.stride(0) % 8:
+            gu = gu.contiguous()
+        T = gu.shape[0]
+        y = torch.empty(T, F, dtype=gu.dtype, device=gu.device)
+        L.call("va_swiglu_fwd", _p(gu), gu.stride(0), F, L.VA_BF16, T, F, _p(y), _stream(gu))
+        ctx.save_for_backward(gu)
+        ctx.F = F
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        g2, u2 = ctx.saved_tensors
+        (gu,) = ctx.saved_tensors
+        F = ctx.F
+        T = gu.shape[0]
         dy2 = dy.contiguous()
-        dg = torch.empty_like(g2)
-        du = torch.empty_like(u2)
-        L.call("va_swiglu_bwd", _p(dy2), _p(g2), _p(u2), L.VA_BF16, g2.numel(), _p(dg), _p(du), _stream(g2))
-        return dg, du
+        dgu = torch.empty(T, 2 * F, dtype=gu.dtype, device=gu.device)
+        L.call("va_swiglu_bwd", _p(dy2), _p(gu), gu.stride(0), F, L.VA_BF16, T, F, _p(dgu), 2 * F, F, _stream(gu))
+        return dgu, None
+
+
+def swiglu_merged(gu):
+    """silu(g) * u for the merged gate|up projection output gu [T, 2F] (g = gu[:, :F], u = gu[:, F:])
+    in one kernel (bf16), Qwen2MLP's activation; the backward writes the merged gradient."""
+    _require_device(gu)
+    _bf16_only(gu)
+    if gu.dim() != 2 or gu.shape[1] % 16:
+        raise ValueError(f"swiglu_merged expects [T, 2F] with F % 8 == 0, got {tuple(gu.shape)}")
+    return _SwiGLU.apply(gu, gu.shape[1] // 2)
 
 
 def swiglu(gate, up):
-    """silu(gate) * up in one kernel (bf16), Qwen2MLP's activation."""
+    """silu(gate) * up for separate gate / up tensors of the same shape (bf16)."""
     _require_device(gate, up)
     _bf16_only(gate, up)
-    return _SwiGLU.apply(gate, up)
+    shape = gate.shape
+    F = shape[-1]
+    y = swiglu_merged(torch.cat([gate.reshape(-1, F), up.reshape(-1, F)], dim=1))
+    return y.view(shape)
+
+
+class _MergedLinear(torch.autograd.Function):
+    """y = x @ W^T (+ b) where W is ONE buffer whose row blocks are the weights of several
+    parameters (views into it), e.g. q|k|v or gate|up. One GEMM forward, one dgrad and one wgrad
+    GEMM backward; the gradients are returned as views of the merged gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w_all, b_all, n_w, *params):
+        ctx.save_for_backward(x, w_all)
+        ctx.n_w = n_w
+        ctx.w_rows = [p.shape[0] for p in params[:n_w]]
+        ctx.has_b = b_all is not None
+        return torch.nn.functional.linear(x, w_all, b_all)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w_all = ctx.saved_tensors
+        dx = dy @ w_all
+        x2 = x.reshape(-1, x.shape[-1])
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dw = dy2.t() @ x2
+        grads = list(torch.split(dw, ctx.w_rows, dim=0))
+        if ctx.has_b:
+            db = dy2.sum(0)
+            grads += list(torch.split(db, ctx.w_rows, dim=0))
+        return (dx, None, None, None, *grads)
+
+
+def merged_linear(x, w_all, b_all, weights: list, biases: list | None = None):
+    """F.linear over a merged weight buffer ``w_all`` (rows = cat of ``weights``, which must be
+    views into it) with gradients routed to the individual parameters."""
+    params = list(weights) + (list(biases) if biases else [])
+    return _MergedLinear.apply(x, w_all, b_all, len(weights), *params)
 
 
 class _RoPEQKV(torch.autograd.Function):

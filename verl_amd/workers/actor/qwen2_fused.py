@@ -5,15 +5,20 @@ The reference runs the HF model on packed tokens with flash-attn varlen patched 
 through one function that owns the layer loop, so that per decoder layer the work is
 
   add_rmsnorm (residual add + input_layernorm, one kernel; its bwd also sums the residual grad)
-  q|k|v projection as ONE GEMM (weights concatenated per call: 2 MB at H=896)
+  q|k|v projection as ONE GEMM (+ one wgrad GEMM and one bias reduction in backward)
   rope_qkv   (split q/k/v into flash varlen's [T, H, D] layout + rotary, one kernel)
   flash varlen attention, o_proj GEMM
   add_rmsnorm (residual add + post_attention_layernorm)
-  gate / up GEMMs, swiglu (one kernel), down GEMM
+  gate|up as ONE GEMM, swiglu on the merged output (one kernel), down GEMM
 
 instead of the ~45 PyTorch kernels HF issues (norm chains, adds, transposes, rotary, bias
 reductions x3). Forward numerics keep HF's bf16 rounding points (see csrc/model_ops.hip), so
 the result matches the HF module graph to bf16 rounding (tests/test_model_ops_gpu.py).
+
+Merging is done in memory, not in the module tree: on first use the q/k/v (and gate/up) weight
+and bias Parameters of each layer are re-pointed (``param.data``) to row blocks of one buffer, so
+the GEMM reads the merged matrix with no per-call concatenation while optimizers, state dicts and
+the fp32-master copy-back keep addressing the original Parameters.
 
 Only bf16 Qwen2-family backbones (RMSNorm + SwiGLU MLP + rotate_half RoPE + GQA with q/k/v bias)
 take this path; anything else keeps the HF forward.
@@ -22,7 +27,6 @@ take this path; anything else keeps the HF forward.
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 
 from ... import kernels as K
 from . import attention
@@ -50,17 +54,40 @@ def supports(backbone: torch.nn.Module) -> bool:
     return all(p.dtype == torch.bfloat16 for p in backbone.parameters())
 
 
-def _qkv_weight(attn):
-    w = torch.cat([attn.q_proj.weight, attn.k_proj.weight, attn.v_proj.weight], dim=0)
-    if attn.q_proj.bias is None:
-        return w, None
-    return w, torch.cat([attn.q_proj.bias, attn.k_proj.bias, attn.v_proj.bias], dim=0)
+def _merged(module, key: str, params: list):
+    """Row-concatenated buffer whose row blocks are ``params`` (re-pointing them on first use or
+    whenever one of them was re-allocated, e.g. by a dtype change)."""
+    cache = module.__dict__.setdefault("_va_merged", {})
+    ent = cache.get(key)
+    if ent is not None:
+        buf, ptrs = ent
+        if all(p.data_ptr() == q for p, q in zip(params, ptrs)) and buf.dtype == params[0].dtype:
+            return buf
+    with torch.no_grad():
+        buf = torch.cat([p.data.reshape(p.shape[0], -1) for p in params], dim=0)
+        if params[0].dim() == 1:
+            buf = buf.reshape(-1)
+        off = 0
+        for p in params:
+            p.data = buf[off : off + p.shape[0]].view(p.shape)
+            off += p.shape[0]
+    cache[key] = (buf, [p.data_ptr() for p in params])
+    return buf
+
+
+def _merged_linear(module, key: str, x, linears: list):
+    ws = [lin.weight for lin in linears]
+    w_all = _merged(module, key + ".w", ws)
+    if linears[0].bias is None:
+        return K.merged_linear(x, w_all, None, ws)
+    bs = [lin.bias for lin in linears]
+    b_all = _merged(module, key + ".b", bs)
+    return K.merged_linear(x, w_all, b_all, ws, bs)
 
 
 def _attention(attn, y, cos, sin, cu, max_len, hq, hk, d):
     T = y.shape[0]
-    w, b = _qkv_weight(attn)
-    qkv = F.linear(y, w, b)
+    qkv = _merged_linear(attn, "qkv", y, [attn.q_proj, attn.k_proj, attn.v_proj])
     q, k, v = K.rope_qkv(qkv, cos, sin, hq, hk, d)
     out = attention.packed_attention(q, k, v, cu, max_len, scaling=attn.scaling)
     return attn.o_proj(out.reshape(T, hq * d))
@@ -89,7 +116,8 @@ def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor
         ln = layer.post_attention_layernorm
         residual, y = K.add_rmsnorm(a, residual, ln.weight, ln.variance_epsilon)
         mlp = layer.mlp
-        h = mlp.down_proj(K.swiglu(mlp.gate_proj(y), mlp.up_proj(y)))
+        gu = _merged_linear(mlp, "gate_up", y, [mlp.gate_proj, mlp.up_proj])
+        h = mlp.down_proj(K.swiglu_merged(gu))
     norm = backbone.norm
     if h is None:
         return K.rmsnorm(residual, norm.weight, norm.variance_epsilon)
