@@ -258,6 +258,15 @@ int va_rope_qkv_fwd(const void *qkv, int64_t ld, const void *cos, const void *si
 int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *cos, const void *sin, int dtype,
                     int64_t T, int64_t Hq, int64_t Hk, int64_t D, void *dqkv, int64_t ld, void *stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Host-side (no GPU) sequence-length balancing. Replaces verl/utils/seqlen_balancing.py:26-127
+ * `karmarkar_karp(seqlen_list, k_partitions, equal_size)` with identical partitions.
+ *   seqlens [n]; order [n] receives the item indices of partition 0, then 1, ... in the
+ *   reference's item order; offsets [k + 1] the partition boundaries. equal_size requires n % k == 0.
+ * ------------------------------------------------------------------------------------ */
+int va_karmarkar_karp(const int64_t *seqlens, int64_t n, int64_t k, int equal_size, int64_t *order,
+                      int64_t *offsets);
+
 #ifdef __cplusplus
 }
 #endif

@@ -159,3 +159,59 @@ def test_worker_step_runs_and_learns():
     # first update: lp == old -> ratio 1, no clipping, kl 0
     assert max(met["actor/pg_clipfrac"]) == 0.0
     assert abs(met["actor/ppo_kl"][0]) < 1e-3
+
+
+def test_dynamic_bsz_log_prob_and_update_match_reference():
+    """use_dynamic_bsz (dp_actor.py:321-347, 382-384, 465-467): token-budget micro-batches give the
+    same log-probs as fixed micro-batches, and update_policy's gradient is the reference's sum of
+    per-micro-batch losses scaled by rows / ppo_mini_batch_size."""
+    from verl_amd.utils.model import build_qwen2
+    from verl_amd.utils.seqlen_balancing import prepare_dynamic_batch
+
+    torch.manual_seed(0)
+    model = build_qwen2("tiny", device=DEV, attn_implementation="sdpa")
+    model_ref = copy.deepcopy(model)
+    data = _batch(B=8, seed=6)
+    b = data.batch
+    R = b["responses"].shape[1]
+    S = b["input_ids"].shape[1]
+    budget = 2 * S  # several micro-batches of uneven row counts
+    actor = _actor(model, use_remove_padding=False, autocast_dtype=None, ppo_mini_batch_size=8,
+                   ppo_micro_batch_size_per_gpu=None, use_dynamic_bsz=True, ppo_max_token_len_per_gpu=budget,
+                   use_kl_loss=False, entropy_coeff=0.0, clip_ratio=0.2, grad_clip=1e9)
+    data.meta_info.update(micro_batch_size=None, temperature=1.0, use_dynamic_bsz=True, max_token_len=budget)
+    lp_dyn, ent_dyn = actor.compute_log_prob(data, calculate_entropy=True)
+    with torch.no_grad():
+        want_lp, want_ent = _ref_logprobs(model_ref, data, 1.0)
+    m = b["response_mask"].bool()
+    assert torch.allclose(lp_dyn[m], want_lp[m], atol=1e-4, rtol=1e-4)
+    assert torch.allclose(ent_dyn[m], want_ent[m], atol=1e-4, rtol=1e-4)
+
+    g = torch.Generator(device=DEV).manual_seed(2)
+    b["old_log_probs"] = want_lp + 0.05 * torch.randn(want_lp.shape, device=DEV, generator=g)
+    b["advantages"] = torch.randn(8, R, device=DEV, generator=g) * b["response_mask"]
+    grads = {}
+
+    def capture():
+        for n, p in model.named_parameters():
+            grads[n] = p.grad.detach().clone()
+        return torch.tensor(0.0, device=DEV)
+
+    actor._optimizer_step = capture
+    actor.update_policy(data)
+    sel = data.select(batch_keys=["responses", "response_mask", "input_ids", "attention_mask", "position_ids",
+                                  "old_log_probs", "advantages"])
+    micro, idx_lists = prepare_dynamic_batch(sel, max_token_len=budget)
+    assert len(micro) > 1 and len({len(ix) for ix in idx_lists}) >= 1
+    model_ref.zero_grad()
+    for mbp in micro:
+        mb = mbp.batch
+        out = model_ref(input_ids=mb["input_ids"], attention_mask=mb["attention_mask"],
+                        position_ids=mb["position_ids"], use_cache=False).logits[:, -R - 1 : -1, :]
+        lp = torch.stack([ref.logprobs_from_logits(r, lab) for r, lab in zip(out, mb["responses"], strict=True)])
+        loss, _ = ref.actor_loss(mb["old_log_probs"], lp, mb["advantages"], mb["response_mask"], clip_ratio=0.2,
+                                 loss_agg_mode="token-mean", grad_scale=len(mbp) / 8)
+        loss.backward()
+    for n, p in model_ref.named_parameters():
+        scale = p.grad.abs().max().item() + 1e-12
+        assert torch.allclose(grads[n], p.grad, atol=1e-4 * scale, rtol=1e-3), n

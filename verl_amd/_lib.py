@@ -73,6 +73,7 @@ _SIGNATURES: dict[str, tuple] = {
     "va_swiglu_fwd": (c_int, [_P, c_int64, c_int64, c_int, c_int64, c_int64, _P, _P]),
     "va_swiglu_bwd": (c_int, [_P, _P, c_int64, c_int64, c_int, c_int64, c_int64, _P, c_int64, c_int64, _P]),
     "va_rope_qkv_fwd": (c_int, [_P, c_int64, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, _P, _P, _P]),
+    "va_karmarkar_karp": (c_int, [_P, c_int64, c_int64, c_int, _P, _P]),
     "va_rope_qkv_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, c_int64, _P]),
 }
 

@@ -43,8 +43,15 @@ def _stale(target: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
+# host-only C++ (no device code) is compiled by the system C++ compiler
+CXXFLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall"]
+
+
 def _compile(hipcc: str, src: Path, obj: Path) -> None:
-    cmd = [hipcc, *CFLAGS, "-c", str(src), "-o", str(obj)]
+    if src.suffix == ".cpp":
+        cmd = [shutil.which("g++") or "c++", *CXXFLAGS, "-c", str(src), "-o", str(obj)]
+    else:
+        cmd = [hipcc, *CFLAGS, "-c", str(src), "-o", str(obj)]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed on {src.name}:\n{res.stdout}\n{res.stderr}")
@@ -53,11 +60,11 @@ def _compile(hipcc: str, src: Path, obj: Path) -> None:
 def build(force: bool = False, verbose: bool = False) -> Path:
     hipcc = _hipcc()
     BUILD_DIR.mkdir(parents=True, exist_ok=True)
-    sources = sorted(CSRC.glob("*.hip"))
+    sources = sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp"))
     jobs = []
     objs = []
     for src in sources:
-        obj = BUILD_DIR / (src.stem + ".o")
+        obj = BUILD_DIR / (src.stem + (".o" if src.suffix == ".hip" else ".host.o"))
         objs.append(obj)
         if force or _stale(obj, [src, *HEADERS]):
             jobs.append((src, obj))

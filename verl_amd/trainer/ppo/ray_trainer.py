@@ -91,3 +91,37 @@ def compute_advantage(
         data.batch["advantages"] = adv
         data.batch["returns"] = ret
     return data
+
+
+def balance_batch(batch: DataProto, world_size: int, metrics: dict, logging_prefix: str = "global_seqlen"):
+    """RayPPOTrainer._balance_batch (ray_trainer.py:1064-1079) without Ray: reorder ``batch`` in
+    place so the equal ``chunk(world_size)`` of DP_COMPUTE_PROTO gives every rank a similar total
+    token count (Karmarkar-Karp, equal partition sizes); balance statistics go into ``metrics``."""
+    from ...utils.seqlen_balancing import get_seqlen_balanced_partitions, log_seqlen_unbalance
+
+    am = batch.batch["attention_mask"]
+    seqlens = am.view(am.shape[0], -1).sum(-1).tolist()
+    parts = get_seqlen_balanced_partitions(seqlens, k_partitions=world_size, equal_size=True)
+    batch.reorder(torch.tensor([j for p in parts for j in p]))
+    metrics.update(log_seqlen_unbalance(seqlen_list=seqlens, partitions=parts, prefix=logging_prefix))
+
+
+def filter_groups(batch: DataProto, metric: str = "acc"):
+    """DAPO dynamic sampling filter (recipe/dapo/dapo_ray_trainer.py:199-237): keep the responses
+    of every prompt (uid) whose ``metric`` has a non-zero population std across its responses,
+    plus singleton groups. ``metric`` is a non-tensor key, or "seq_final_reward" /
+    "seq_reward" (row sums of token_level_rewards / token_level_scores, computed here as the
+    reference does). Returns (kept batch, number of kept prompts)."""
+    import numpy as np
+
+    if metric == "seq_final_reward":
+        batch.non_tensor_batch["seq_final_reward"] = batch.batch["token_level_rewards"].sum(dim=-1).cpu().numpy()
+    elif metric == "seq_reward":
+        batch.non_tensor_batch["seq_reward"] = batch.batch["token_level_scores"].sum(dim=-1).cpu().numpy()
+    uids = batch.non_tensor_batch["uid"]
+    vals: dict = {}
+    for uid, v in zip(uids, batch.non_tensor_batch[metric], strict=True):
+        vals.setdefault(uid, []).append(v)
+    kept = {uid for uid, vs in vals.items() if np.std(vs) > 0 or len(vs) == 1}
+    idx = [i for i, uid in enumerate(uids) if uid in kept]
+    return batch[idx], len(kept)

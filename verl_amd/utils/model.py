@@ -36,3 +36,25 @@ def build_qwen2(size: str = "0.5b", device="cuda", dtype=torch.float32, seed: in
     with torch.device(device):
         model = Qwen2ForCausalLM(cfg)
     return model.to(dtype)
+
+
+def create_random_mask(input_ids: torch.Tensor, max_ratio_of_valid_token: float, max_ratio_of_left_padding: float,
+                       min_ratio_of_valid_token: float = 0):
+    """verl/utils/model.py:176-216 — a random left-padded / right-padded 0/1 mask (numpy RNG)."""
+    import numpy as np
+
+    assert 0 < max_ratio_of_valid_token <= 1.0
+    assert 0 <= max_ratio_of_left_padding < 1.0
+    assert min_ratio_of_valid_token <= max_ratio_of_valid_token
+    bs, seq = input_ids.shape
+    max_valid = int(seq * max_ratio_of_valid_token)
+    min_valid = max(1, int(seq * min_ratio_of_valid_token))
+    max_left = int(seq * max_ratio_of_left_padding)
+    assert max_valid + max_left <= seq
+    masks = torch.ones_like(input_ids, dtype=torch.int64)
+    for i in range(bs):
+        left = int(np.random.randint(low=0, high=max_left + 1, dtype=np.int64))
+        valid = int(np.random.randint(low=min_valid, high=max_valid + 1, dtype=np.int64))
+        masks[i, :left] = 0
+        masks[i, left + valid :] = 0
+    return masks

@@ -32,6 +32,7 @@ from ...protocol import DataProto
 from ...trainer.ppo import core_algos
 from ...trainer.ppo.core_algos import agg_loss, get_policy_loss_fn, kl_penalty
 from ...utils import torch_functional as verl_F
+from ...utils.seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
 from . import attention
 from .base import BasePPOActor
 
@@ -171,12 +172,17 @@ class DataParallelPPOActor(BasePPOActor):
                 entropy = ent if calculate_entropy else None
         return entropy, log_probs
 
-    def _plans(self, data: DataProto, sizes: list[int]) -> list:
+    def _plans(self, data: DataProto, sizes: list[int] = None, idx_lists: list[list[int]] = None) -> list:
+        """Packing plans of consecutive micro-batches of ``sizes`` rows, or of the dynamic
+        micro-batches' row index lists, from one D2H copy of the attention mask."""
+        n_mb = len(sizes) if idx_lists is None else len(idx_lists)
         if not self.use_remove_padding:
-            return [None] * len(sizes)
-        am = data.batch["attention_mask"].cpu().numpy()  # one D2H for the whole call
+            return [None] * n_mb
+        am = data.batch["attention_mask"].cpu().numpy()
         R = data.batch["responses"].size(-1)
         dev = data.batch["input_ids"].device
+        if idx_lists is not None:
+            return [_plan_packing(am[np.asarray(ix, dtype=np.int64)], R, dev) for ix in idx_lists]
         plans, s = [], 0
         for n in sizes:
             plans.append(_plan_packing(am[s : s + n], R, dev))
@@ -215,11 +221,15 @@ class DataParallelPPOActor(BasePPOActor):
         micro_batch_size = data.meta_info["micro_batch_size"]
         temperature = data.meta_info["temperature"]
         use_dynamic_bsz = data.meta_info["use_dynamic_bsz"]
-        if use_dynamic_bsz:
-            raise NotImplementedError("dynamic token-budget micro-batching (seqlen_balancing) is not yet ported")
         data = data.select(batch_keys=["responses", "input_ids", "attention_mask", "position_ids"])
-        micro_batches = data.split(micro_batch_size)
-        plans = self._plans(data, [len(m) for m in micro_batches])
+        if use_dynamic_bsz:
+            # dp_actor.py:321-323: micro-batches cut by a token budget, restored afterwards
+            max_token_len = data.meta_info["max_token_len"] * self.ulysses_sequence_parallel_size
+            micro_batches, batch_idx_list = prepare_dynamic_batch(data, max_token_len=max_token_len)
+            plans = self._plans(data, idx_lists=batch_idx_list)
+        else:
+            micro_batches = data.split(micro_batch_size)
+            plans = self._plans(data, [len(m) for m in micro_batches])
         lps, ents = [], []
         for mb, plan in zip(micro_batches, plans, strict=True):
             ent, lp = self._forward_micro_batch(mb.batch, temperature, calculate_entropy, plan)
@@ -228,6 +238,10 @@ class DataParallelPPOActor(BasePPOActor):
                 ents.append(ent)
         log_probs = torch.concat(lps, dim=0)
         entropys = torch.concat(ents, dim=0) if calculate_entropy else None
+        if use_dynamic_bsz:
+            log_probs = restore_dynamic_batch(log_probs, batch_idx_list)
+            if entropys is not None:
+                entropys = restore_dynamic_batch(entropys, batch_idx_list)
         return log_probs, entropys
 
     def update_policy(self, data: DataProto):
@@ -241,10 +255,9 @@ class DataParallelPPOActor(BasePPOActor):
         if cfg.use_kl_loss:
             keys.append("ref_log_prob")
         data = data.select(batch_keys=keys)
-        if cfg.use_dynamic_bsz:
-            raise NotImplementedError("dynamic token-budget micro-batching (seqlen_balancing) is not yet ported")
         mini_batches = data.split(cfg.ppo_mini_batch_size)
-        self.gradient_accumulation = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
+        if not cfg.use_dynamic_bsz:
+            self.gradient_accumulation = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
         clip_ratio = cfg.clip_ratio
         clip_low = cfg.clip_ratio_low if cfg.get("clip_ratio_low") is not None else clip_ratio
         clip_high = cfg.clip_ratio_high if cfg.get("clip_ratio_high") is not None else clip_ratio
@@ -256,8 +269,14 @@ class DataParallelPPOActor(BasePPOActor):
         dev_metrics: dict[str, list] = {}
         for _ in range(cfg.ppo_epochs):
             for mini in mini_batches:
-                micro_batches = mini.split(cfg.ppo_micro_batch_size_per_gpu)
-                plans = self._plans(mini, [len(m) for m in micro_batches])
+                if cfg.use_dynamic_bsz:
+                    # dp_actor.py:382-384
+                    max_token_len = cfg.ppo_max_token_len_per_gpu * self.ulysses_sequence_parallel_size
+                    micro_batches, idx_lists = prepare_dynamic_batch(mini, max_token_len=max_token_len)
+                    plans = self._plans(mini, idx_lists=idx_lists)
+                else:
+                    micro_batches = mini.split(cfg.ppo_micro_batch_size_per_gpu)
+                    plans = self._plans(mini, [len(m) for m in micro_batches])
                 self._zero_grad()
                 for i, (mb, plan) in enumerate(zip(micro_batches, plans, strict=True)):
                     b = mb.batch
@@ -296,7 +315,11 @@ class DataParallelPPOActor(BasePPOActor):
                             policy_loss = policy_loss + kl_loss * cfg.kl_loss_coef
                             m["actor/kl_loss"] = kl_loss.detach()
                             m["actor/kl_coef"] = cfg.kl_loss_coef
-                    loss = policy_loss / self.gradient_accumulation
+                    if cfg.use_dynamic_bsz:
+                        # relative to the dynamic bsz (dp_actor.py:465-467)
+                        loss = policy_loss * (response_mask.shape[0] / cfg.ppo_mini_batch_size)
+                    else:
+                        loss = policy_loss / self.gradient_accumulation
                     last = i == len(micro_batches) - 1
                     if last and self.grad_reducer is not None:
                         self.grad_reducer.begin_sync()

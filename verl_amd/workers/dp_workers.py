@@ -59,10 +59,13 @@ class ActorWorker:
         assert actor.ppo_mini_batch_size > 0, "ppo_mini_batch_size must be > 0 after normalisation"
         if actor.get("ppo_micro_batch_size_per_gpu") is None and actor.get("ppo_micro_batch_size") is not None:
             actor.ppo_micro_batch_size_per_gpu = actor.ppo_micro_batch_size // self.world_size
-        assert actor.ppo_mini_batch_size % actor.ppo_micro_batch_size_per_gpu == 0, (
-            f"normalized ppo_mini_batch_size {actor.ppo_mini_batch_size} should be divisible by "
-            f"ppo_micro_batch_size_per_gpu {actor.ppo_micro_batch_size_per_gpu}"
-        )
+        if actor.get("ppo_micro_batch_size_per_gpu") is not None:
+            assert actor.ppo_mini_batch_size % actor.ppo_micro_batch_size_per_gpu == 0, (
+                f"normalized ppo_mini_batch_size {actor.ppo_mini_batch_size} should be divisible by "
+                f"ppo_micro_batch_size_per_gpu {actor.ppo_micro_batch_size_per_gpu}"
+            )
+        elif not actor.get("use_dynamic_bsz", False):
+            raise ValueError("ppo_micro_batch_size_per_gpu is required unless use_dynamic_bsz is set")
         self.actor = None
         self.module = None
 
@@ -85,9 +88,11 @@ class ActorWorker:
 
     def compute_log_prob(self, data: DataProto) -> DataProto:
         """fsdp_workers.py:758-800: old_log_probs (+ entropys) for this rank's shard."""
-        data.meta_info.setdefault("micro_batch_size", self.config.rollout.log_prob_micro_batch_size_per_gpu)
-        data.meta_info.setdefault("temperature", self.config.rollout.temperature)
-        data.meta_info.setdefault("use_dynamic_bsz", self.config.rollout.get("log_prob_use_dynamic_bsz", False))
+        ro = self.config.rollout
+        data.meta_info.setdefault("micro_batch_size", ro.get("log_prob_micro_batch_size_per_gpu"))
+        data.meta_info.setdefault("temperature", ro.temperature)
+        data.meta_info.setdefault("use_dynamic_bsz", ro.get("log_prob_use_dynamic_bsz", False))
+        data.meta_info.setdefault("max_token_len", ro.get("log_prob_max_token_len_per_gpu", 16384))
         lp, ent = self.actor.compute_log_prob(data, calculate_entropy=True)
         return DataProto.from_dict(tensors={"old_log_probs": lp, "entropys": ent},
                                    meta_info={"temperature": data.meta_info["temperature"]})
