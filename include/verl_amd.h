@@ -259,6 +259,26 @@ int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *
                     int64_t T, int64_t Hq, int64_t Hk, int64_t D, void *dqkv, int64_t ld, void *stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Critic: fused clipped value loss (core_algos.py:992-1031, clip_by_value torch_functional.py:
+ * 136-142) + the critic's vpred_mean metric (dp_critic.py:236-242).
+ *   vpreds, values, returns [B, R] fp32; mask [B, R] of mask_dtype; agg_mode = VA_AGG_*.
+ *   out[VA_VLOSS_NOUT] fp32 (device); workspace: va_ppo_loss_workspace_bytes(B).
+ * Backward: g_out[VA_VLOSS_NOUT] = d(loss)/d(out) (slots LOSS and VPRED_MEAN are read) ->
+ *   d_vpreds [B, R]. Ties follow torch.maximum / minimum autograd (gradient halves).
+ * ------------------------------------------------------------------------------------ */
+#define VA_VLOSS_LOSS 0       /* vf_loss            core_algos.py:1029 */
+#define VA_VLOSS_CLIPFRAC 1   /* vf_clipfrac        core_algos.py:1030 */
+#define VA_VLOSS_VPRED_MEAN 2 /* critic/vpred_mean  dp_critic.py:241 */
+#define VA_VLOSS_NTOKENS 3    /* sum(response_mask) (diagnostic) */
+#define VA_VLOSS_NOUT 4
+int va_value_loss_fwd(const float *vpreds, const float *values, const float *returns, const void *mask,
+                      int mask_dtype, int64_t B, int64_t R, float cliprange_value, int agg_mode, float *out,
+                      void *workspace, void *stream);
+int va_value_loss_bwd(const float *g_out, const float *vpreds, const float *values, const float *returns,
+                      const void *mask, int mask_dtype, int64_t B, int64_t R, float cliprange_value,
+                      int agg_mode, const void *workspace, float *d_vpreds, void *stream);
+
+/* ---------------------------------------------------------------------------------------
  * Host-side (no GPU) sequence-length balancing. Replaces verl/utils/seqlen_balancing.py:26-127
  * `karmarkar_karp(seqlen_list, k_partitions, equal_size)` with identical partitions.
  *   seqlens [n]; order [n] receives the item indices of partition 0, then 1, ... in the

@@ -151,6 +151,22 @@ def compute_policy_loss(
     return pg_loss, clipfrac, ppo_kl, clipfrac_lower
 
 
+def clip_by_value(x, tensor_min, tensor_max):
+    """utils/torch_functional.py:136-142."""
+    return torch.max(torch.min(x, tensor_max), tensor_min)
+
+
+def compute_value_loss(vpreds, returns, values, response_mask, cliprange_value, loss_agg_mode="token-mean"):
+    """trainer/ppo/core_algos.py:992-1031 — clipped value loss and clip fraction."""
+    vpredclipped = clip_by_value(vpreds, values - cliprange_value, values + cliprange_value)
+    vf_losses1 = (vpreds - returns) ** 2
+    vf_losses2 = (vpredclipped - returns) ** 2
+    clipped_vf_losses = torch.max(vf_losses1, vf_losses2)
+    vf_loss = 0.5 * agg_loss(clipped_vf_losses, response_mask, loss_agg_mode)
+    vf_clipfrac = masked_mean(torch.gt(vf_losses2, vf_losses1).float(), response_mask)
+    return vf_loss, vf_clipfrac
+
+
 def kl_penalty(logprob, ref_logprob, kl_penalty):
     """trainer/ppo/core_algos.py:1034-1069."""
     if kl_penalty in ("kl", "k1"):

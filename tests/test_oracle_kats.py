@@ -149,3 +149,21 @@ def test_oracle_reproduces_golden_fixtures():
             assert np.array_equal(a, b, equal_nan=True), k
         else:
             assert np.array_equal(a, b), k
+
+
+def test_value_loss_kats():
+    """core_algos.py:992-1031 by hand: values 0, cliprange 0.5, vpreds 2 -> clipped 0.5.
+    returns 0: l1 = 4, l2 = 0.25 (unclipped branch); returns 3: l1 = 1, l2 = 6.25 (clipped)."""
+    vp = torch.tensor([[2.0, 2.0]])
+    val = torch.zeros(1, 2)
+    ret = torch.tensor([[0.0, 3.0]])
+    m = torch.ones(1, 2, dtype=torch.int64)
+    loss, frac = ref.compute_value_loss(vp, ret, val, m, 0.5)
+    assert abs(loss.item() - 0.5 * (4.0 + 6.25) / 2) < 1e-6
+    assert abs(frac.item() - 0.5) < 1e-6
+    # vpreds == values: never clipped, plain half-MSE
+    vp = torch.randn(3, 5)
+    ret = torch.randn(3, 5)
+    loss, frac = ref.compute_value_loss(vp, ret, vp.clone(), torch.ones(3, 5), 0.2)
+    assert frac.item() == 0.0
+    assert torch.allclose(loss, 0.5 * ((vp - ret) ** 2).mean(), atol=1e-6)

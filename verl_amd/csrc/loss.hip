@@ -385,6 +385,111 @@ __global__ __launch_bounds__(256) void apply_kl_penalty_kernel(
   if (threadIdx.x == 0) row_kl[b] = static_cast<float>(v[1] / (v[0] + 1e-8));
 }
 
+// ------------------------------------------------------------------ clipped value loss (critic)
+// core_algos.py:992-1031 with verl_F.clip_by_value (torch_functional.py:136-142):
+//   vpc = maximum(minimum(vp, v + c), v - c); l1 = (vp - ret)^2; l2 = (vpc - ret)^2
+//   vf_loss = 0.5 * agg_loss(maximum(l1, l2)); vf_clipfrac = masked_mean(l2 > l1)
+// plus the critic's metric vpred_mean = masked_mean(vp) (dp_critic.py:236-242).
+struct ValueElem {
+  float loss, clip;
+};
+__device__ __forceinline__ ValueElem value_elem(float vp, float v, float ret, float c) {
+  const float hi = v + c, lo = v - c;
+  const float vpc = tmax(tmin(vp, hi), lo);
+  const float d1 = vp - ret, d2 = vpc - ret;
+  const float l1 = d1 * d1, l2 = d2 * d2;
+  ValueElem e;
+  e.loss = tmax(l1, l2);
+  e.clip = (l2 > l1) ? 1.f : 0.f;
+  return e;
+}
+// d loss / d vp given the upstream weight w on maximum(l1, l2) (torch autograd tie rules)
+__device__ __forceinline__ float value_dvp(float w, float vp, float v, float ret, float c) {
+  const float hi = v + c, lo = v - c;
+  const float m1 = tmin(vp, hi);
+  const float vpc = tmax(m1, lo);
+  const float d1 = vp - ret, d2 = vpc - ret;
+  const float l1 = d1 * d1, l2 = d2 * d2;
+  const float s1 = gmax_share(l1, l2), s2 = gmax_share(l2, l1);
+  const float g_l1 = s1 == 0.5f ? w / 2.f : w * s1;
+  const float g_l2 = s2 == 0.5f ? w / 2.f : w * s2;
+  const float g_vpc = g_l2 * (2.f * d2);
+  const float sa = gmax_share(m1, lo);  // vpc = maximum(m1, lo)
+  const float g_m1 = sa == 0.5f ? g_vpc / 2.f : g_vpc * sa;
+  const float sb = vp < hi ? 1.f : (vp == hi ? 0.5f : 0.f);  // m1 = minimum(vp, hi)
+  const float g_vp_clip = sb == 0.5f ? g_m1 / 2.f : g_m1 * sb;
+  return g_l1 * (2.f * d1) + g_vp_clip;
+}
+
+template <int MT>
+__global__ __launch_bounds__(256) void value_loss_rows_kernel(
+    const float *__restrict__ vp, const float *__restrict__ val, const float *__restrict__ ret,
+    const void *__restrict__ mask, int64_t R, float c, int agg, double *__restrict__ part) {
+  __shared__ double scratch[4 * 4];
+  const int64_t b = blockIdx.x;
+  const bool tok = (agg == VA_AGG_TOKEN_MEAN);
+  double v[4] = {0, 0, 0, 0};  // n, loss, clip, vpred
+  for (int64_t t = threadIdx.x; t < R; t += blockDim.x) {
+    const int64_t i = b * R + t;
+    const float m = load_mask<MT>(mask, i);
+    const bool mb = (m != 0.f);
+    const ValueElem e = value_elem(vp[i], val[i], ret[i], c);
+    v[0] += m;
+    v[1] += tok ? (mb ? e.loss : 0.f) * m : e.loss * m;
+    v[2] += (mb ? e.clip : 0.f) * m;
+    v[3] += (mb ? vp[i] : 0.f) * m;
+  }
+  block_sum<4>(v, scratch);
+  if (threadIdx.x < 4) part[b * kNQ + threadIdx.x] = v[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void value_loss_finalize_kernel(const double *__restrict__ part,
+                                                                  int64_t B, int64_t R, int agg,
+                                                                  double *__restrict__ totals,
+                                                                  float *__restrict__ out) {
+  __shared__ double scratch[4 * 3];
+  double v[3] = {0, 0, 0};
+  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
+    v[0] += part[b * kNQ + 0];
+    v[1] += part[b * kNQ + 2];
+    v[2] += part[b * kNQ + 3];
+  }
+  block_sum<3>(v, scratch);
+  const double n = v[0];
+  const double loss = agg_value(agg, part, 1, B, R, n, scratch);
+  if (threadIdx.x == 0) {
+    const double den = n + 1e-8;
+    out[VA_VLOSS_LOSS] = 0.5f * static_cast<float>(loss);
+    out[VA_VLOSS_CLIPFRAC] = static_cast<float>(v[1] / den);
+    out[VA_VLOSS_VPRED_MEAN] = static_cast<float>(v[2] / den);
+    out[VA_VLOSS_NTOKENS] = static_cast<float>(n);
+    totals[0] = n;
+  }
+}
+
+template <int MT>
+__global__ __launch_bounds__(256) void value_loss_bwd_kernel(
+    const float *__restrict__ g_out, const float *__restrict__ vp, const float *__restrict__ val,
+    const float *__restrict__ ret, const void *__restrict__ mask, int64_t B, int64_t R, float c,
+    int agg, const double *__restrict__ part, float *__restrict__ d_vp) {
+  const int64_t b = blockIdx.y;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= R) return;
+  const int64_t i = b * R + t;
+  // vf_loss = 0.5 * agg(.)  ->  d agg = 0.5 * g ;  vpred_mean = masked_mean(vp)
+  const float g_loss = g_out ? g_out[VA_VLOSS_LOSS] * 0.5f : 0.f;
+  const float g_mean = g_out ? g_out[VA_VLOSS_VPRED_MEAN] : 0.f;
+  const double n_b = part[b * kNQ + 0];
+  const double n_tot = part[B * kNQ + 0];
+  const float m = load_mask<MT>(mask, i);
+  const bool mb = (m != 0.f);
+  const float keep = (agg != VA_AGG_TOKEN_MEAN || mb) ? 1.f : 0.f;
+  const float w = agg_weight(agg, g_loss, m, n_b, n_tot, B, R) * keep;
+  float g = value_dvp(w, vp[i], val[i], ret[i], c);
+  g += (g_mean / static_cast<float>(n_tot + 1e-8)) * m * (mb ? 1.f : 0.f);
+  d_vp[i] = g;
+}
+
 int64_t grid_1d(int64_t n) {
   int64_t g = (n + 255) / 256;
   return g > 8192 ? 8192 : (g < 1 ? 1 : g);
@@ -533,4 +638,40 @@ extern "C" int va_apply_kl_penalty(const float *scores, const float *old_lp, con
                        old_lp, ref_lp, mask, R, beta, rewards, row_kl);
   }));
   return check_launch("apply_kl_penalty");
+}
+
+extern "C" int va_value_loss_fwd(const float *vpreds, const float *values, const float *returns,
+                                 const void *mask, int mask_dtype, int64_t B, int64_t R,
+                                 float cliprange_value, int agg_mode, float *out, void *workspace,
+                                 void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0, "empty batch (B=%lld, R=%lld)", (long long)B, (long long)R);
+  VA_CHECK_ARG(B < (1ll << 31), "B too large");
+  VA_CHECK_ARG(vpreds && values && returns && mask && out && workspace, "null pointer argument");
+  if (int e = check_agg(agg_mode, false)) return e;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  double *part = static_cast<double *>(workspace);
+  VA_DISPATCH_MASK(mask_dtype, {
+    hipLaunchKernelGGL((value_loss_rows_kernel<MT>), dim3(B), dim3(256), 0, s, vpreds, values,
+                       returns, mask, R, cliprange_value, agg_mode, part);
+  });
+  hipLaunchKernelGGL(value_loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, B, R, agg_mode,
+                     part + B * kNQ, out);
+  return check_launch("value_loss_fwd");
+}
+
+extern "C" int va_value_loss_bwd(const float *g_out, const float *vpreds, const float *values,
+                                 const float *returns, const void *mask, int mask_dtype, int64_t B,
+                                 int64_t R, float cliprange_value, int agg_mode,
+                                 const void *workspace, float *d_vpreds, void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0 && B < 65536, "bad shape");
+  VA_CHECK_ARG(vpreds && values && returns && mask && workspace && d_vpreds, "null pointer argument");
+  if (int e = check_agg(agg_mode, false)) return e;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<unsigned>((R + 255) / 256), static_cast<unsigned>(B));
+  VA_DISPATCH_MASK(mask_dtype, {
+    hipLaunchKernelGGL((value_loss_bwd_kernel<MT>), grid, dim3(256), 0, s, g_out, vpreds, values,
+                       returns, mask, B, R, cliprange_value, agg_mode,
+                       static_cast<const double *>(workspace), d_vpreds);
+  });
+  return check_launch("value_loss_bwd");
 }

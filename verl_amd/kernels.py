@@ -254,6 +254,46 @@ def fused_policy_loss(
     )
 
 
+# =============================================================================== value loss (critic)
+class _ValueLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, vpreds, values, returns, mask, cliprange_value, agg):
+        B, R = _as_2d(vpreds)
+        vp, v, r = _f32(vpreds), _f32(values), _f32(returns)
+        m, mcode = _mask(mask)
+        out = torch.empty(L.VA_VLOSS_NOUT, dtype=torch.float32, device=vp.device)
+        nbytes = L.load().va_ppo_loss_workspace_bytes(B)
+        ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=vp.device)
+        L.call("va_value_loss_fwd", _p(vp), _p(v), _p(r), _p(m), mcode, B, R, cliprange_value, agg, _p(out), _p(ws),
+               _stream(vp))
+        ctx.save_for_backward(vp, v, r, m, ws)
+        ctx.cfg = (B, R, mcode, cliprange_value, agg, vpreds.shape, vpreds.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        vp, v, r, m, ws = ctx.saved_tensors
+        B, R, mcode, c, agg, shape, dtype = ctx.cfg
+        g = _f32(g_out)
+        d_vp = torch.empty_like(vp)
+        L.call("va_value_loss_bwd", _p(g), _p(vp), _p(v), _p(r), _p(m), mcode, B, R, c, agg, _p(ws), _p(d_vp),
+               _stream(vp))
+        return d_vp.view(shape).to(dtype), None, None, None, None, None
+
+
+def fused_value_loss(vpreds, values, returns, response_mask, cliprange_value: float,
+                     loss_agg_mode: str = "token-mean") -> torch.Tensor:
+    """compute_value_loss (core_algos.py:992-1031) + masked_mean(vpreds) in one fused kernel pair.
+    Returns the 4-slot vector VA_VLOSS_* (vf_loss, vf_clipfrac, vpred_mean, n_tokens); gradients
+    flow from slots LOSS and VPRED_MEAN to vpreds (bf16 vpreds are upcast exactly, as the
+    reference's mixed-dtype ops promote them)."""
+    if loss_agg_mode not in AGG_MODES:
+        raise ValueError(f"Invalid loss_agg_mode: {loss_agg_mode}")
+    _require_device(vpreds, values, returns, response_mask)
+    return _ValueLoss.apply(vpreds, values, returns, response_mask, float(np.float32(cliprange_value)),
+                            AGG_MODES[loss_agg_mode])
+
+
 # =============================================================================== kl penalty
 class _KLPenalty(torch.autograd.Function):
     @staticmethod

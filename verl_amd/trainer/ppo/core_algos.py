@@ -376,13 +376,10 @@ def compute_entropy_loss(logits, response_mask, loss_agg_mode: str = "token-mean
 
 def compute_value_loss(vpreds, returns, values, response_mask, cliprange_value: float,
                        loss_agg_mode: str = "token-mean"):
-    """core_algos.py:992-1031 — clipped value loss (critic)."""
-    vclip = verl_F.clip_by_value(vpreds, values - cliprange_value, values + cliprange_value)
-    l1 = (vpreds - returns) ** 2
-    l2 = (vclip - returns) ** 2
-    vf_loss = 0.5 * agg_loss(torch.max(l1, l2), response_mask, loss_agg_mode)
-    vf_clipfrac = verl_F.masked_mean(torch.gt(l2, l1).float(), response_mask)
-    return vf_loss, vf_clipfrac
+    """core_algos.py:992-1031 — clipped value loss (critic), one fused gfx950
+    kernel pair (va_value_loss_fwd/bwd). Returns (vf_loss, vf_clipfrac) 0-d fp32 tensors."""
+    out = K.fused_value_loss(vpreds, values, returns, response_mask, cliprange_value, loss_agg_mode)
+    return out[L.VA_VLOSS_LOSS], out[L.VA_VLOSS_CLIPFRAC]
 
 
 def kl_penalty(logprob: torch.FloatTensor, ref_logprob: torch.FloatTensor, kl_penalty) -> torch.FloatTensor:

@@ -64,3 +64,31 @@ def actor_config(**overrides) -> AttrDict:
     for k, v in overrides.items():
         cfg[k] = v
     return cfg
+
+
+def critic_config(**overrides) -> AttrDict:
+    """Defaults of verl/trainer/config/critic/critic.yaml + dp_critic.yaml that the critic-update
+    path reads (mini-batch sizes are inherited from the actor there; set them explicitly here)."""
+    cfg = AttrDict(
+        strategy="fsdp",
+        rollout_n=1,
+        ppo_mini_batch_size=256,
+        ppo_micro_batch_size=None,
+        ppo_micro_batch_size_per_gpu=None,
+        forward_micro_batch_size=None,
+        forward_micro_batch_size_per_gpu=None,
+        use_dynamic_bsz=False,
+        ppo_max_token_len_per_gpu=32768,
+        forward_max_token_len_per_gpu=32768,
+        ppo_epochs=1,
+        shuffle=False,
+        cliprange_value=0.5,
+        loss_agg_mode="token-mean",
+        grad_clip=1.0,
+        ulysses_sequence_parallel_size=1,
+        model=AttrDict(use_remove_padding=False, enable_gradient_checkpointing=True),
+        optim=AttrDict(lr=1e-5, weight_decay=0.01, betas=(0.9, 0.999)),
+    )
+    for k, v in overrides.items():
+        cfg[k] = v
+    return cfg

@@ -58,3 +58,17 @@ def create_random_mask(input_ids: torch.Tensor, max_ratio_of_valid_token: float,
         masks[i, :left] = 0
         masks[i, left + valid :] = 0
     return masks
+
+
+def build_qwen2_critic(size: str = "0.5b", device="cuda", dtype=torch.float32, seed: int = 0, **overrides):
+    """The reference's critic: AutoModelForTokenClassification with num_labels = 1 and
+    classifier_dropout = 0 (fsdp_workers.py:1018-1031) on the Qwen2 architecture, random init."""
+    from transformers import Qwen2ForTokenClassification
+
+    torch.manual_seed(seed)
+    cfg = qwen2_config(size, **overrides)
+    cfg.num_labels = 1
+    cfg.classifier_dropout = 0.0
+    with torch.device(device):
+        model = Qwen2ForTokenClassification(cfg)
+    return model.to(dtype)

@@ -1,0 +1,205 @@
+"""DataParallelPPOCritic — mirror of verl/workers/critic/dp_critic.py:46-256 on MI355X
+(the critic of config 3, PPO with GAE).
+
+Same constructor, config keys, micro/mini-batch loops (fixed or token-budget dynamic), loss
+scaling and metric keys as the reference. The hot path maps onto the GPU like the actor's:
+
+  * padding removal planned once per call on the host (one D2H of the attention mask); the
+    backbone runs on packed tokens (qwen2_fused.packed_forward for bf16 Qwen2: fused
+    add+RMSNorm, merged q|k|v + RoPE, merged gate|up + SwiGLU, flash varlen attention);
+  * only the hidden states at positions that predict a response token go through the value
+    head (the reference scores every token and slices :, -R-1:-1 afterwards, dp_critic.py:123-124);
+  * the clipped value loss, vf_clipfrac and vpred_mean are ONE fused kernel pair
+    (va_value_loss_fwd/bwd); metrics stay on device until one transfer per update;
+  * gradients go through the same bucketed RCCL reducer / fp32-master manager as the actor.
+Values are returned in fp32 (the reference's bf16 autocast values, upcast exactly; GAE promotes
+them to fp32 anyway, core_algos.py:225-230).
+"""
+
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from ... import _lib as L
+from ... import kernels as K
+from ...protocol import DataProto
+from ...utils.seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
+from ..actor import attention
+from ..actor.dp_actor import _NO_MASK, _plan_packing, _to_host, append_to_dict
+from .base import BasePPOCritic
+
+__all__ = ["DataParallelPPOCritic"]
+
+
+class DataParallelPPOCritic(BasePPOCritic):
+    def __init__(self, config, critic_module: nn.Module, critic_optimizer: torch.optim.Optimizer, grad_reducer=None):
+        super().__init__(config=config)
+        self.critic_module = critic_module
+        self.critic_optimizer = critic_optimizer
+        self.grad_reducer = grad_reducer
+        model_cfg = self.config.get("model", {}) or {}
+        self.use_remove_padding = model_cfg.get("use_remove_padding", False)
+        self.ulysses_sequence_parallel_size = self.config.get("ulysses_sequence_parallel_size", 1)
+        if self.ulysses_sequence_parallel_size != 1:
+            raise NotImplementedError("Ulysses sequence parallelism is out of scope for the DP critic path")
+        self.device_name = "cuda"
+        prefix = getattr(critic_module, "base_model_prefix", "model")
+        self._backbone = getattr(critic_module, prefix)
+        self._head = getattr(critic_module, "score", None)
+        if self._head is None:
+            raise NotImplementedError("critic needs a token-classification value head (.score, num_labels=1)")
+        if self.use_remove_padding:
+            name = attention.register()
+            if hasattr(critic_module, "set_attn_implementation"):
+                critic_module.set_attn_implementation(name)
+            else:
+                critic_module.config._attn_implementation = name
+        self.fused_model_ops = self.use_remove_padding and self.config.get("fused_model_ops", True)
+        self._fused_backbone = None
+
+    # ------------------------------------------------------------------ forward
+    def _forward_micro_batch(self, micro_batch, packing=None) -> torch.Tensor:
+        """values [bs, response_len] fp32 (dp_critic.py:57-136)."""
+        R = micro_batch["responses"].size(-1)
+        input_ids = micro_batch["input_ids"]
+        B, S = input_ids.shape
+        position_ids = micro_batch["position_ids"]
+        if position_ids.dim() == 3:
+            raise NotImplementedError("mrope position ids (VLM) are out of scope")
+        with torch.autocast(device_type=self.device_name, dtype=torch.bfloat16):
+            if self.use_remove_padding:
+                if packing is None:
+                    packing = _plan_packing(micro_batch["attention_mask"].cpu().numpy(), R, input_ids.device)
+                ids = input_ids.reshape(-1).index_select(0, packing.token_idx)
+                pos = position_ids.reshape(-1).index_select(0, packing.token_idx)
+                if self._fused_backbone is None:
+                    from ..actor import qwen2_fused
+
+                    self._fused_backbone = self.fused_model_ops and qwen2_fused.supports(self._backbone)
+                if self._fused_backbone:
+                    from ..actor.qwen2_fused import packed_forward
+
+                    hidden = packed_forward(self._backbone, ids, pos, packing.cu_seqlens, packing.max_seqlen)
+                else:
+                    out = self._backbone(
+                        input_ids=ids.unsqueeze(0), position_ids=pos.unsqueeze(0), attention_mask=_NO_MASK,
+                        use_cache=False, cu_seq_lens_q=packing.cu_seqlens, cu_seq_lens_k=packing.cu_seqlens,
+                        max_length_q=packing.max_seqlen, max_length_k=packing.max_seqlen,
+                    )
+                    hidden = out.last_hidden_state[0]
+                v_sel = self._head(hidden.index_select(0, packing.sel_hidden)).squeeze(-1).float()
+                values = v_sel.new_zeros(B * R).index_copy(0, packing.sel_out, v_sel).view(B, R)
+            else:
+                out = self.critic_module(input_ids=input_ids, attention_mask=micro_batch["attention_mask"],
+                                         position_ids=position_ids, use_cache=False)
+                values = out.logits[:, -R - 1 : -1].squeeze(-1).float()
+        return values
+
+    def _plans(self, data: DataProto, sizes=None, idx_lists=None):
+        n_mb = len(sizes) if idx_lists is None else len(idx_lists)
+        if not self.use_remove_padding:
+            return [None] * n_mb
+        import numpy as np
+
+        am = data.batch["attention_mask"].cpu().numpy()
+        R = data.batch["responses"].size(-1)
+        dev = data.batch["input_ids"].device
+        if idx_lists is not None:
+            return [_plan_packing(am[np.asarray(ix, dtype=np.int64)], R, dev) for ix in idx_lists]
+        plans, s = [], 0
+        for n in sizes:
+            plans.append(_plan_packing(am[s : s + n], R, dev))
+            s += n
+        return plans
+
+    # ------------------------------------------------------------------ optimizer
+    def _zero_grad(self):
+        if self.grad_reducer is not None:
+            self.grad_reducer.zero_grad()
+        else:
+            self.critic_optimizer.zero_grad()
+
+    def _optimizer_step(self):
+        """dp_critic.py:138-154."""
+        assert self.config.grad_clip is not None
+        if self.grad_reducer is not None:
+            self.grad_reducer.finish_sync()
+        params = (self.grad_reducer.optimizer_params() if self.grad_reducer is not None
+                  else list(self.critic_module.parameters()))
+        grad_norm = torch.nn.utils.clip_grad_norm_(params, max_norm=self.config.grad_clip, foreach=True)
+        if not torch.isfinite(grad_norm):
+            print(f"WARN: grad_norm is not finite: {grad_norm}")
+            self._zero_grad()
+        else:
+            self.critic_optimizer.step()
+            if self.grad_reducer is not None:
+                self.grad_reducer.after_step()
+        return grad_norm
+
+    # ------------------------------------------------------------------ API
+    @torch.no_grad()
+    def compute_values(self, data: DataProto) -> torch.Tensor:
+        """dp_critic.py:156-191 — values over micro-batches, masked by response_mask."""
+        self.critic_module.eval()
+        micro_batch_size = data.meta_info["micro_batch_size"]
+        use_dynamic_bsz = data.meta_info["use_dynamic_bsz"]
+        data = data.select(batch_keys=["responses", "input_ids", "response_mask", "attention_mask", "position_ids"])
+        if use_dynamic_bsz:
+            max_token_len = data.meta_info["max_token_len"] * self.ulysses_sequence_parallel_size
+            micro_batches, batch_idx_list = prepare_dynamic_batch(data, max_token_len=max_token_len)
+            plans = self._plans(data, idx_lists=batch_idx_list)
+        else:
+            micro_batches = data.split(micro_batch_size)
+            plans = self._plans(data, [len(m) for m in micro_batches])
+        vals = [self._forward_micro_batch(mb.batch, plan) for mb, plan in zip(micro_batches, plans, strict=True)]
+        values = torch.concat(vals, dim=0)
+        if use_dynamic_bsz:
+            values = restore_dynamic_batch(values, batch_idx_list)
+        return values * data.batch["response_mask"]  # only action tokens have values
+
+    def update_critic(self, data: DataProto):
+        """dp_critic.py:193-256 — PPO epochs x mini-batches x micro-batches of the clipped value
+        loss; one optimizer step per mini-batch; returns {metric: [values]}."""
+        self.critic_module.train()
+        cfg = self.config
+        keys = ["input_ids", "responses", "response_mask", "attention_mask", "position_ids", "values", "returns"]
+        data = data.select(batch_keys=keys)
+        mini_batches = data.split(cfg.ppo_mini_batch_size)
+        dev_metrics: dict = {}
+        for _ in range(cfg.ppo_epochs):
+            for mini in mini_batches:
+                if cfg.use_dynamic_bsz:
+                    max_token_len = cfg.ppo_max_token_len_per_gpu * self.ulysses_sequence_parallel_size
+                    micro_batches, idx_lists = prepare_dynamic_batch(mini, max_token_len=max_token_len)
+                    plans = self._plans(mini, idx_lists=idx_lists)
+                else:
+                    self.gradient_accumulation = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
+                    micro_batches = mini.split(cfg.ppo_micro_batch_size_per_gpu)
+                    plans = self._plans(mini, [len(m) for m in micro_batches])
+                self._zero_grad()
+                for i, (mb, plan) in enumerate(zip(micro_batches, plans, strict=True)):
+                    b = mb.batch
+                    response_mask = b["response_mask"]
+                    vpreds = self._forward_micro_batch(b, plan)
+                    out = K.fused_value_loss(vpreds, b["values"], b["returns"], response_mask, cfg.cliprange_value,
+                                             cfg.loss_agg_mode)
+                    vf_loss = out[L.VA_VLOSS_LOSS]
+                    if cfg.use_dynamic_bsz:
+                        loss = vf_loss * (response_mask.shape[0] / cfg.ppo_mini_batch_size)
+                    else:
+                        loss = vf_loss / self.gradient_accumulation
+                    if i == len(micro_batches) - 1 and self.grad_reducer is not None:
+                        self.grad_reducer.begin_sync()
+                    loss.backward()
+                    if self.grad_reducer is not None:
+                        self.grad_reducer.after_backward()
+                    append_to_dict(dev_metrics, {
+                        "critic/vf_loss": vf_loss.detach(),
+                        "critic/vf_clipfrac": out[L.VA_VLOSS_CLIPFRAC].detach(),
+                        "critic/vpred_mean": out[L.VA_VLOSS_VPRED_MEAN].detach(),
+                    })
+                grad_norm = self._optimizer_step()
+                append_to_dict(dev_metrics, {"critic/grad_norm": grad_norm.detach()})
+        self._zero_grad()
+        return _to_host(dev_metrics)

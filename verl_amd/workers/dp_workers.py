@@ -101,3 +101,59 @@ class ActorWorker:
         """fsdp_workers.py:672-716: one PPO update; metrics in meta_info."""
         metrics = self.actor.update_policy(data)
         return DataProto(meta_info={"metrics": metrics})
+
+
+class CriticWorker:
+    """compute_values / update_critic of the critic role, one per GPU (fsdp_workers.py:931-1265
+    without FSDP / Ulysses / offload: plain DP over RCCL with bf16 compute + fp32 masters)."""
+
+    def __init__(self, config):
+        self.config = config
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.world_size = dist.get_world_size() if dist.is_initialized() else 1
+        c = config
+        # normalisation, fsdp_workers.py:953-975 (sp = 1)
+        c.ppo_mini_batch_size = c.ppo_mini_batch_size * c.get("rollout_n", 1) // self.world_size
+        if c.get("ppo_micro_batch_size") is not None:
+            c.ppo_micro_batch_size //= self.world_size
+            c.forward_micro_batch_size //= self.world_size
+            c.ppo_micro_batch_size_per_gpu = c.ppo_micro_batch_size
+            c.forward_micro_batch_size_per_gpu = c.forward_micro_batch_size
+        if c.get("ppo_micro_batch_size_per_gpu") is not None:
+            assert c.ppo_mini_batch_size % c.ppo_micro_batch_size_per_gpu == 0, (
+                f"normalized ppo_mini_batch_size {c.ppo_mini_batch_size} should be divisible by "
+                f"ppo_micro_batch_size_per_gpu {c.ppo_micro_batch_size_per_gpu}"
+            )
+            assert c.ppo_mini_batch_size // c.ppo_micro_batch_size_per_gpu > 0
+        if c.get("forward_micro_batch_size_per_gpu") is None:
+            c.forward_micro_batch_size_per_gpu = c.get("ppo_micro_batch_size_per_gpu")
+        self.critic = None
+
+    def init_model(self, module: torch.nn.Module, bucket_mb: int = 256, mixed_precision: bool = True):
+        from .critic import DataParallelPPOCritic
+
+        optim = self.config.optim
+        fused = next(module.parameters()).is_cuda
+        if mixed_precision:
+            manager = MixedPrecisionParams(module, bucket_bytes=bucket_mb << 20)
+        else:
+            manager = GradBucketReducer(module.parameters(), bucket_bytes=bucket_mb << 20)
+        opt = torch.optim.AdamW(manager.optimizer_params(), lr=optim.lr,
+                                betas=tuple(optim.get("betas", (0.9, 0.999))),
+                                weight_decay=optim.get("weight_decay", 0.01), fused=fused)
+        self.critic = DataParallelPPOCritic(self.config, module, opt, grad_reducer=manager)
+        return self
+
+    def compute_values(self, data: DataProto) -> DataProto:
+        """fsdp_workers.py:1207-1227."""
+        data.meta_info["micro_batch_size"] = self.config.forward_micro_batch_size_per_gpu
+        data.meta_info["max_token_len"] = self.config.forward_max_token_len_per_gpu
+        data.meta_info["use_dynamic_bsz"] = self.config.use_dynamic_bsz
+        values = self.critic.compute_values(data=data)
+        return DataProto.from_dict(tensors={"values": values})
+
+    def update_critic(self, data: DataProto) -> DataProto:
+        """fsdp_workers.py:1231-1264 (metrics + critic/lr)."""
+        metrics = self.critic.update_critic(data=data)
+        metrics["critic/lr"] = self.critic.critic_optimizer.param_groups[0]["lr"]
+        return DataProto(meta_info={"metrics": metrics})
