@@ -63,6 +63,13 @@ extern "C" {
 #define VA_ADV_GRPO_NOSTD 1 /* s - mean (Dr.GRPO)                   core_algos.py:304-305 */
 #define VA_ADV_RLOO 2      /* s*n/(n-1) - mean*n/(n-1)              core_algos.py:428-476 */
 #define VA_ADV_MEAN_ONLY 3 /* s - mean, first half of RF++-baseline core_algos.py:376-424 */
+#define VA_ADV_OPO 4       /* s - sum(len*s)/sum(len), singleton 0  core_algos.py:479-530 */
+#define VA_ADV_PASSK 5     /* best row: (r_max - r_2nd)/(std + eps)  core_algos.py:311-370 */
+#define VA_ADV_PASSK_NOSTD 6 /* best row: r_max - r_2nd             core_algos.py:363-366 */
+
+/* discounted-return modes of va_discounted_returns */
+#define VA_RET_RFPP 0      /* REINFORCE++ return with reset after EOS core_algos.py:553-560 */
+#define VA_RET_REMAX 1     /* reverse cumsum of r*m, adv = ret - b*m  core_algos.py:597-600 */
 
 /* scalar slots of the fused policy-loss output vector out[VA_LOSS_NOUT] */
 #define VA_LOSS_PG 0            /* pg_loss                 core_algos.py:791-792 */
@@ -257,6 +264,13 @@ int va_rope_qkv_fwd(const void *qkv, int64_t ld, const void *cos, const void *si
                     int64_t Hq, int64_t Hk, int64_t D, void *q, void *k, void *v, void *stream);
 int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *cos, const void *sin, int dtype,
                     int64_t T, int64_t Hq, int64_t Hk, int64_t D, void *dqkv, int64_t ld, void *stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Discounted returns for REINFORCE++ (mode VA_RET_RFPP, gamma) and ReMax (VA_RET_REMAX:
+ * baselines [B] required, adv [B, R] written). rewards / returns / adv [B, R] fp32.
+ * ------------------------------------------------------------------------------------ */
+int va_discounted_returns(const float *rewards, const void *mask, int mask_dtype, int64_t B, int64_t R, float gamma,
+                          int mode, const float *baselines, float *returns, float *adv, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Critic: fused clipped value loss (core_algos.py:992-1031, clip_by_value torch_functional.py:

@@ -296,6 +296,108 @@ def compute_reinforce_plus_plus_baseline_outcome_advantage(token_level_rewards, 
     return scores, scores
 
 
+def compute_grpo_passk_outcome_advantage(token_level_rewards, response_mask, index, epsilon=1e-6, norm=True):
+    """trainer/ppo/core_algos.py:311-370 — the group's best response gets r_max - r_second_max."""
+    scores = token_level_rewards.sum(dim=-1)
+    adv = torch.zeros_like(scores)
+    with torch.no_grad():
+        for uid, rows in _groups(index).items():
+            rewards = torch.stack([scores[i] for i in rows])
+            if rewards.numel() < 2:
+                raise ValueError(f"Pass@k requires at least 2 samples per group. Got {rewards.numel()} for group {uid}.")
+            top, top_idx = torch.topk(rewards, 2)
+            a = top[0] - top[1]
+            if norm:
+                a = a / (torch.std(rewards) + epsilon)
+            adv[rows[top_idx[0].item()]] = a
+    adv = adv.unsqueeze(-1) * response_mask
+    return adv, adv
+
+
+def compute_opo_outcome_advantage(token_level_rewards, response_mask, index, epsilon=1e-6):
+    """trainer/ppo/core_algos.py:479-530 — length-weighted baseline, 0 for singleton groups."""
+    lengths = response_mask.sum(dim=-1)
+    scores = token_level_rewards.sum(dim=-1)
+    with torch.no_grad():
+        base = {}
+        for uid, rows in _groups(index).items():
+            if len(rows) == 1:
+                base[uid] = torch.tensor(0.0)
+            else:
+                sc = torch.tensor([scores[i] for i in rows])
+                ln = torch.tensor([lengths[i] for i in rows])
+                base[uid] = (ln * sc).sum() / ln.sum()
+        for i in range(scores.shape[0]):
+            scores[i] = scores[i] - base[index[i]]
+        scores = scores.unsqueeze(-1) * response_mask
+    return scores, scores
+
+
+def compute_reinforce_plus_plus_outcome_advantage(token_level_rewards, response_mask, gamma):
+    """trainer/ppo/core_algos.py:533-569 — discounted return, reset after EOS, then whitening."""
+    with torch.no_grad():
+        returns = torch.zeros_like(token_level_rewards)
+        running = 0
+        for t in reversed(range(token_level_rewards.shape[1])):
+            running = token_level_rewards[:, t] + gamma * running
+            returns[:, t] = running
+            running = running * response_mask[:, t]
+        adv = masked_whiten(returns, response_mask) * response_mask
+    return adv, returns
+
+
+def compute_remax_outcome_advantage(token_level_rewards, reward_baselines, response_mask):
+    """trainer/ppo/core_algos.py:572-605."""
+    with torch.no_grad():
+        returns = (token_level_rewards * response_mask).flip(dims=[-1]).cumsum(dim=-1).flip(dims=[-1])
+        adv = returns - reward_baselines.unsqueeze(-1) * response_mask
+    return adv, returns
+
+
+def compute_gpg_outcome_advantage(token_level_rewards, response_mask, index, epsilon=1e-6, f_norm=1.0):
+    """trainer/ppo/core_algos.py:608-667 — alpha = B / max(#nonzero scores, 1)."""
+    scores = token_level_rewards.sum(dim=-1)
+    with torch.no_grad():
+        alpha = scores.shape[0] / torch.count_nonzero(scores).clamp(min=1)
+        means = {}
+        for uid, rows in _groups(index).items():
+            members = [scores[i] for i in rows]
+            means[uid] = torch.tensor(0.0) if len(members) == 1 else torch.mean(torch.tensor(members))
+        for i in range(scores.shape[0]):
+            scores[i] = alpha * (scores[i] - means[index[i]]) / f_norm
+        scores = scores.unsqueeze(-1) * response_mask
+    return scores, scores
+
+
+def compute_policy_loss_gpg(log_prob, advantages, response_mask, loss_agg_mode="token-mean"):
+    """trainer/ppo/core_algos.py:797-815."""
+    return agg_loss(-log_prob * advantages, response_mask, loss_agg_mode)
+
+
+def compute_policy_loss_kl_cov(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode="token-mean",
+                               kl_cov_ratio=0.0002, ppo_kl_coef=1.0):
+    """trainer/ppo/core_algos.py:908-972 — the top kl_cov_ratio covariance tokens get an |kl| penalty."""
+    nkl = log_prob - old_log_prob
+    ratio = torch.exp(nkl)
+    ppo_kl_abs = masked_mean(nkl.abs(), response_mask)
+    pg1 = -advantages * ratio
+    pgkl = -advantages * ratio + ppo_kl_coef * nkl.abs()
+    pg = pg1
+    valid = response_mask > 0
+    valid_idx = torch.nonzero(valid.reshape(-1), as_tuple=True)[0]
+    a = advantages[valid].detach().reshape(-1)
+    lp = log_prob[valid].detach().reshape(-1)
+    if min(kl_cov_ratio, len(a)) != 0:
+        cov = (a - a.mean()) * (lp - lp.mean())
+        k = max(1, int(len(cov) * kl_cov_ratio))
+        top = torch.topk(cov, k, largest=True).indices
+        if len(top):
+            flat = valid_idx[top]
+            R = advantages.shape[1]
+            pg[flat // R, flat % R] = pgkl[flat // R, flat % R]
+    return agg_loss(pg, response_mask, loss_agg_mode), ppo_kl_abs
+
+
 def compute_gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam):
     """trainer/ppo/core_algos.py:193-241 — masked reverse recurrence; observation tokens
     (mask 0) carry the value and the running advantage through unchanged."""

@@ -23,6 +23,8 @@ VA_AGG_TOKEN_MEAN, VA_AGG_SEQ_MEAN_TOKEN_SUM, VA_AGG_SEQ_MEAN_TOKEN_MEAN, VA_AGG
 VA_REDUCE_MASKED_SUM, VA_REDUCE_ROW_MASKED_MEAN = 4, 5
 VA_KL_NONE, VA_KL_K1, VA_KL_ABS, VA_KL_K2, VA_KL_K3 = -1, 0, 1, 2, 3
 VA_ADV_GRPO, VA_ADV_GRPO_NOSTD, VA_ADV_RLOO, VA_ADV_MEAN_ONLY = 0, 1, 2, 3
+VA_ADV_OPO, VA_ADV_PASSK, VA_ADV_PASSK_NOSTD = 4, 5, 6
+VA_RET_RFPP, VA_RET_REMAX = 0, 1
 VA_LOSS_PG, VA_LOSS_CLIPFRAC, VA_LOSS_PPO_KL, VA_LOSS_CLIPFRAC_LOWER = 0, 1, 2, 3
 VA_LOSS_KL, VA_LOSS_ENTROPY, VA_LOSS_NTOKENS, VA_LOSS_NROWS, VA_LOSS_NOUT = 4, 5, 6, 7, 8
 VA_VLOSS_LOSS, VA_VLOSS_CLIPFRAC, VA_VLOSS_VPRED_MEAN, VA_VLOSS_NTOKENS, VA_VLOSS_NOUT = 0, 1, 2, 3, 4
@@ -76,6 +78,7 @@ _SIGNATURES: dict[str, tuple] = {
     "va_rope_qkv_fwd": (c_int, [_P, c_int64, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, _P, _P, _P]),
     "va_value_loss_fwd": (c_int, [_P, _P, _P, _P, c_int, c_int64, c_int64, c_float, c_int, _P, _P, _P]),
     "va_value_loss_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_float, c_int, _P, _P, _P]),
+    "va_discounted_returns": (c_int, [_P, _P, c_int, c_int64, c_int64, c_float, c_int, _P, _P, _P, _P]),
     "va_karmarkar_karp": (c_int, [_P, c_int64, c_int64, c_int, _P, _P]),
     "va_rope_qkv_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, c_int64, _P]),
 }

@@ -37,12 +37,13 @@ __global__ __launch_bounds__(256) void outcome_adv_kernel(
     const float *__restrict__ rewards, const void *__restrict__ mask, int64_t R,
     const int32_t *__restrict__ order, const int32_t *__restrict__ offsets, float eps,
     float *__restrict__ adv, float *__restrict__ scores_out) {
-  extern __shared__ float s_score[];  // [group size] + 2 floats of broadcast stats
+  extern __shared__ float s_score[];  // [n] scores, [n] lengths (OPO), 4 floats of broadcast stats
   const int g = blockIdx.x;
   const int beg = offsets[g];
   const int n = offsets[g + 1] - beg;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  float *s_stat = s_score + n;
+  float *s_len = s_score + n;
+  float *s_stat = s_len + n;
 
   // 1) scores: unmasked row sums (core_algos.py:282), fp32 like the reference
   const bool vec = (R % 4 == 0);
@@ -60,6 +61,12 @@ __global__ __launch_bounds__(256) void outcome_adv_kernel(
       for (int64_t j = lane; j < R; j += kWave) acc += r[j];
     }
     acc = wave_sum(acc);
+    if constexpr (EST == VA_ADV_OPO) {  // response length = response_mask.sum(-1) (core_algos.py:505)
+      float len = 0.f;
+      for (int64_t j = lane; j < R; j += kWave) len += load_mask<MT>(mask, row * R + j);
+      len = wave_sum(len);
+      if (lane == 0) s_len[k] = len;
+    }
     if (lane == 0) {
       s_score[k] = acc;
       if (scores_out) scores_out[row] = acc;
@@ -87,6 +94,32 @@ __global__ __launch_bounds__(256) void outcome_adv_kernel(
     }
     s_stat[0] = mean32;
     s_stat[1] = std32;
+    if constexpr (EST == VA_ADV_OPO) {
+      // length-weighted group baseline, singleton -> 0 (core_algos.py:512-520)
+      float bsl = 0.f;
+      if (n > 1) {
+        double num = 0.0, den = 0.0;
+        for (int k = 0; k < n; ++k) {
+          num += static_cast<double>(static_cast<float>(s_len[k] * s_score[k]));
+          den += s_len[k];
+        }
+        bsl = static_cast<float>(num) / static_cast<float>(den);
+      }
+      s_stat[0] = bsl;
+    }
+    if constexpr (EST == VA_ADV_PASSK || EST == VA_ADV_PASSK_NOSTD) {
+      // only the best response gets r_max - r_second_max (core_algos.py:350-368); n >= 2
+      int imax = 0;
+      for (int k = 1; k < n; ++k)
+        if (s_score[k] > s_score[imax]) imax = k;
+      float second = -INFINITY;
+      for (int k = 0; k < n; ++k)
+        if (k != imax && s_score[k] > second) second = s_score[k];
+      float a = s_score[imax] - second;
+      if constexpr (EST == VA_ADV_PASSK) a = a / (std32 + eps);
+      s_stat[2] = a;
+      s_stat[3] = static_cast<float>(imax);
+    }
   }
   __syncthreads();
   const float mean = s_stat[0], stdv = s_stat[1];
@@ -98,8 +131,10 @@ __global__ __launch_bounds__(256) void outcome_adv_kernel(
     float a;
     if constexpr (EST == VA_ADV_GRPO) {
       a = (s - mean) / (stdv + eps);
-    } else if constexpr (EST == VA_ADV_GRPO_NOSTD || EST == VA_ADV_MEAN_ONLY) {
+    } else if constexpr (EST == VA_ADV_GRPO_NOSTD || EST == VA_ADV_MEAN_ONLY || EST == VA_ADV_OPO) {
       a = s - mean;
+    } else if constexpr (EST == VA_ADV_PASSK || EST == VA_ADV_PASSK_NOSTD) {
+      a = (k == static_cast<int>(s_stat[3])) ? s_stat[2] : 0.f;
     } else {  // RLOO, core_algos.py:469-473
       if (n > 1) {
         const float nn = static_cast<float>(n), nm1 = static_cast<float>(n - 1);
@@ -361,6 +396,63 @@ __global__ __launch_bounds__(256) void whiten_apply_kernel(float *__restrict__ x
   }
 }
 
+// ---------------------------------------------------------------- discounted returns (RF++ / ReMax)
+// One wave per row; lane k owns the contiguous chunk [kL, (k+1)L). The per-step state map is
+// affine, s -> A + C s:
+//   RF++  (core_algos.py:553-560): out_t = r_t + gamma * s;  s <- out_t * m_t
+//   ReMax (core_algos.py:597-599): out_t = s + r_t * m_t   (reverse cumsum of r * m);  s <- out_t
+// Chunk maps are composed per lane, a 6-step wave reverse scan gives every chunk its incoming
+// state, and each lane re-runs its chunk in the reference's op order.
+template <int MT, int MODE>
+__global__ __launch_bounds__(256) void discounted_returns_kernel(
+    const float *__restrict__ rew, const void *__restrict__ mask, int64_t B, int64_t R, int L,
+    float gamma, const float *__restrict__ baselines, float *__restrict__ ret, float *__restrict__ adv) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + wave;
+  if (row >= B) return;
+  const int64_t base = row * R;
+  const int64_t t0 = static_cast<int64_t>(lane) * L;
+  const int64_t t1 = (t0 + L < R) ? t0 + L : R;
+  float A = 0.f, C = 1.f;  // chunk map, applied to the state entering its last step
+  for (int64_t t = t1 - 1; t >= t0; --t) {
+    const float r = rew[base + t], m = load_mask<MT>(mask, base + t);
+    float a, c;
+    if constexpr (MODE == VA_RET_RFPP) {
+      a = r * m;
+      c = gamma * m;
+    } else {
+      a = r * m;
+      c = 1.f;
+    }
+    A = a + c * A;  // step o (chunk so far)
+    C = c * C;
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float nA = __shfl_down(A, o, kWave), nC = __shfl_down(C, o, kWave);
+    if (lane + o < 64) {  // (this chunk) o (chunks after it): s -> A + C (nA + nC s)
+      A = A + C * nA;
+      C = C * nC;
+    }
+  }
+  float st = __shfl_down(A, 1, kWave);  // state after chunks 63..k+1 from 0
+  if (lane == 63) st = 0.f;
+  const float b = (MODE == VA_RET_REMAX) ? baselines[row] : 0.f;
+  for (int64_t t = t1 - 1; t >= t0; --t) {
+    const float r = rew[base + t], m = load_mask<MT>(mask, base + t);
+    float out;
+    if constexpr (MODE == VA_RET_RFPP) {
+      out = r + gamma * st;
+      st = out * m;
+    } else {
+      out = st + r * m;
+      st = out;
+      adv[base + t] = out - b * m;  // core_algos.py:600
+    }
+    ret[base + t] = out;
+  }
+}
+
 int gae_lds_bytes(int L, int waves) { return waves * 3 * 64 * (L + 1) * 4; }
 
 }  // namespace
@@ -375,11 +467,11 @@ extern "C" int va_outcome_advantage(const float *rewards, const void *mask, int 
                                     float *adv, float *scores, void *stream) {
   VA_CHECK_ARG(B > 0 && R > 0 && n_groups > 0 && n_groups <= B, "bad shape (B=%lld G=%lld)",
                (long long)B, (long long)n_groups);
-  VA_CHECK_ARG(max_group_size > 0 && max_group_size <= 32768, "group size %lld out of range",
+  VA_CHECK_ARG(max_group_size > 0 && max_group_size <= 16384, "group size %lld out of range",
                (long long)max_group_size);
   VA_CHECK_ARG(rewards && mask && order && offsets && adv, "null pointer argument");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const size_t shm = static_cast<size_t>(max_group_size + 2) * sizeof(float);
+  const size_t shm = static_cast<size_t>(2 * max_group_size + 4) * sizeof(float);
 #define VA_LAUNCH_ADV(E)                                                                     \
   VA_DISPATCH_MASK(mask_dtype, {                                                             \
     hipLaunchKernelGGL((outcome_adv_kernel<MT, E>), dim3(n_groups), dim3(256), shm, s,        \
@@ -390,6 +482,9 @@ extern "C" int va_outcome_advantage(const float *rewards, const void *mask, int 
     case VA_ADV_GRPO_NOSTD: VA_LAUNCH_ADV(VA_ADV_GRPO_NOSTD); break;
     case VA_ADV_RLOO: VA_LAUNCH_ADV(VA_ADV_RLOO); break;
     case VA_ADV_MEAN_ONLY: VA_LAUNCH_ADV(VA_ADV_MEAN_ONLY); break;
+    case VA_ADV_OPO: VA_LAUNCH_ADV(VA_ADV_OPO); break;
+    case VA_ADV_PASSK: VA_LAUNCH_ADV(VA_ADV_PASSK); break;
+    case VA_ADV_PASSK_NOSTD: VA_LAUNCH_ADV(VA_ADV_PASSK_NOSTD); break;
     default: set_error("unknown estimator %d", estimator); return VA_E_ARG;
   }
 #undef VA_LAUNCH_ADV
@@ -491,4 +586,27 @@ extern "C" int va_gae_advantage_return(const float *rewards, const float *values
   e = va_whiten_finalize(part, B, part + B * kPartStride, stats_out, stream);
   if (e) return e;
   return va_whiten_apply(adv, stats_out, mask, mask_dtype, B, R, 0, stream);
+}
+
+extern "C" int va_discounted_returns(const float *rewards, const void *mask, int mask_dtype, int64_t B,
+                                     int64_t R, float gamma, int mode, const float *baselines, float *returns,
+                                     float *adv, void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0, "empty batch");
+  VA_CHECK_ARG(rewards && mask && returns, "null pointer argument");
+  VA_CHECK_ARG(mode == VA_RET_RFPP || (mode == VA_RET_REMAX && baselines && adv), "bad mode / missing ReMax outputs");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int L = static_cast<int>((R + 63) / 64);
+  const dim3 grid(static_cast<unsigned>((B + 3) / 4));
+  if (mode == VA_RET_RFPP) {
+    VA_DISPATCH_MASK(mask_dtype, {
+      hipLaunchKernelGGL((discounted_returns_kernel<MT, VA_RET_RFPP>), grid, dim3(256), 0, s, rewards, mask, B, R,
+                         L, gamma, baselines, returns, adv);
+    });
+  } else {
+    VA_DISPATCH_MASK(mask_dtype, {
+      hipLaunchKernelGGL((discounted_returns_kernel<MT, VA_RET_REMAX>), grid, dim3(256), 0, s, rewards, mask, B,
+                         R, L, gamma, baselines, returns, adv);
+    });
+  }
+  return check_launch("discounted_returns");
 }

@@ -394,6 +394,24 @@ def outcome_advantage(token_level_rewards, response_mask, index, epsilon: float,
     return adv
 
 
+def discounted_returns(token_level_rewards, response_mask, gamma: float, mode: int, baselines=None):
+    """RF++ returns (mode VA_RET_RFPP) or ReMax (VA_RET_REMAX: returns, advantages) via the chunked
+    reverse-scan kernel."""
+    _require_device(token_level_rewards, response_mask, baselines)
+    r = _f32(token_level_rewards)
+    B, R = r.shape
+    m, mcode = _mask(response_mask)
+    ret = torch.empty_like(r)
+    if mode == L.VA_RET_REMAX:
+        b = _f32(baselines).reshape(B)
+        adv = torch.empty_like(r)
+        L.call("va_discounted_returns", _p(r), _p(m), mcode, B, R, float(gamma), mode, _p(b), _p(ret), _p(adv),
+               _stream(r))
+        return ret, adv
+    L.call("va_discounted_returns", _p(r), _p(m), mcode, B, R, float(gamma), mode, None, _p(ret), None, _stream(r))
+    return ret
+
+
 _WHITEN_ERRORS = {
     1: "At least one element in the mask has to be 1.",
     2: "The sum of the mask is one, which can cause a division by zero.",

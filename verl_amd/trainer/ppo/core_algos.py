@@ -9,13 +9,17 @@ the reference (core_algos.py:33-1069). The hot-path functions run as gfx950 kern
   compute_reinforce_plus_plus_baseline_outcome_advantage -> mean-only + whiten kernels
   compute_policy_loss / agg_loss / kl_penalty / compute_entropy_loss -> fused loss kernels
 
-The remaining estimators and policy-loss variants ("next") are composed from
-device tensor ops here and are not yet dedicated kernels.
+  compute_opo_outcome_advantage / compute_grpo_passk_outcome_advantage -> va_outcome_advantage epilogues
+  compute_reinforce_plus_plus_outcome_advantage / compute_remax_outcome_advantage -> va_discounted_returns
+  compute_value_loss (critic) -> va_value_loss_fwd/bwd
+
+GPG's advantage reuses the group-mean kernel plus one device-side scale; the gpg / clip_cov /
+kl_cov policy-loss variants are device tensor ops (their top-k / random selection over the
+batch is not a streaming kernel's shape).
 """
 
 from __future__ import annotations
 
-from collections import defaultdict
 from enum import Enum
 from typing import Optional
 
@@ -152,25 +156,17 @@ def compute_grpo_outcome_advantage(
 @register_adv_est(AdvantageEstimator.GRPO_PASSK)
 def compute_grpo_passk_outcome_advantage(token_level_rewards, response_mask, index, epsilon=1e-6,
                                          norm_adv_by_std_in_grpo=True, config=None, **kwargs):
-    """core_algos.py:311-370 (device tensor ops)."""
+    """core_algos.py:311-370 — only the best response of each group gets r_max - r_second_max
+    (divided by the group's unbiased std + eps when norm_adv_by_std_in_grpo); one group kernel."""
     assert config is not None
     norm = config.get("norm_adv_by_std_in_grpo", True)
-    scores = token_level_rewards.sum(dim=-1)
-    adv = torch.zeros_like(scores)
-    groups = defaultdict(list)
-    for i, u in enumerate(index):
-        groups[u].append(i)
+    uids, counts = np.unique(np.asarray(index).astype(str), return_counts=True)
+    if len(counts) and counts.min() < 2:
+        bad = uids[int(np.argmin(counts))]
+        raise ValueError(f"Pass@k requires at least 2 samples per group. Got {int(counts.min())} for group {bad}.")
+    est = L.VA_ADV_PASSK if norm else L.VA_ADV_PASSK_NOSTD
     with torch.no_grad():
-        for u, rows in groups.items():
-            r = scores[rows]
-            if r.numel() < 2:
-                raise ValueError(f"Pass@k requires at least 2 samples per group. Got {r.numel()} for group {u}.")
-            top, top_idx = torch.topk(r, 2)
-            a = top[0] - top[1]
-            if norm:
-                a = a / (torch.std(r) + epsilon)
-            adv[rows[int(top_idx[0].item())]] = a
-    adv = adv.unsqueeze(-1) * response_mask
+        adv = K.outcome_advantage(token_level_rewards, response_mask, index, epsilon, est)
     return adv, adv
 
 
@@ -201,44 +197,35 @@ def compute_rloo_outcome_advantage(token_level_rewards, response_mask, index, ep
 
 @register_adv_est(AdvantageEstimator.OPO)
 def compute_opo_outcome_advantage(token_level_rewards, response_mask, index, epsilon=1e-6, config=None, **kwargs):
-    """core_algos.py:479-530 — length-weighted group baseline (device tensor ops)."""
-    lengths = response_mask.sum(dim=-1)
-    scores = token_level_rewards.sum(dim=-1)
-    groups = defaultdict(list)
-    for i, u in enumerate(index):
-        groups[u].append(i)
+    """core_algos.py:479-530 — length-weighted group baseline sum(len*s)/sum(len) (singleton
+    groups: baseline 0); one group kernel."""
+    _no_empty_group(index)
     with torch.no_grad():
-        base = torch.zeros_like(scores)
-        for rows in groups.values():
-            if len(rows) > 1:
-                s, ln = scores[rows], lengths[rows].to(scores.dtype)
-                base[rows] = (ln * s).sum() / ln.sum()
-        scores = (scores - base).unsqueeze(-1) * response_mask
+        scores = K.outcome_advantage(token_level_rewards, response_mask, index, epsilon, L.VA_ADV_OPO)
     return scores, scores
 
 
 @register_adv_est(AdvantageEstimator.REINFORCE_PLUS_PLUS)
 def compute_reinforce_plus_plus_outcome_advantage(token_level_rewards, response_mask, config=None, **kwargs):
-    """core_algos.py:533-569 — discounted return with reset after EOS, then whitening."""
+    """core_algos.py:533-569 — discounted return with reset after EOS (chunked scan kernel), then
+    masked whitening (whiten kernels; the reference's ValueErrors), times the mask."""
     assert config is not None
     gamma = config.gamma
     with torch.no_grad():
-        returns = torch.zeros_like(token_level_rewards)
-        running = torch.zeros_like(token_level_rewards[:, 0])
-        for t in reversed(range(token_level_rewards.shape[1])):
-            running = token_level_rewards[:, t] + gamma * running
-            returns[:, t] = running
-            running = running * response_mask[:, t]
-        adv = verl_F.masked_whiten(returns, response_mask) * response_mask
-    return adv, returns
+        returns = K.discounted_returns(token_level_rewards, response_mask, gamma, L.VA_RET_RFPP)
+        stats, _ = K.whiten_stats(returns, response_mask)
+        K._raise_whiten_flag(stats)
+        advantages = K.whiten_apply(returns, response_mask, stats, post_multiply_mask=True)
+    return advantages, returns
 
 
 @register_adv_est(AdvantageEstimator.REMAX)
 def compute_remax_outcome_advantage(token_level_rewards, reward_baselines, response_mask, config=None, **kwargs):
-    """core_algos.py:572-605."""
+    """core_algos.py:572-605 — reverse cumulative sum of r * mask (scan kernel) minus the
+    per-response baseline on valid tokens."""
     with torch.no_grad():
-        returns = (token_level_rewards * response_mask).flip(dims=[-1]).cumsum(dim=-1).flip(dims=[-1])
-        advantages = returns - reward_baselines.unsqueeze(-1) * response_mask
+        returns, advantages = K.discounted_returns(token_level_rewards, response_mask, 1.0, L.VA_RET_REMAX,
+                                                   baselines=reward_baselines)
     return advantages, returns
 
 
