@@ -266,6 +266,20 @@ int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *
                     int64_t T, int64_t Hq, int64_t Hk, int64_t D, void *dqkv, int64_t ld, void *stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Fused lm_head + log-prob + entropy forward (the reference's use_fused_kernels
+ * path, utils/kernel/kernels.py:120-663 + linear_cross_entropy.py:40-117): for hidden [N, H]
+ * (row stride ldh) and weight [V, H] (row stride ldw), both bf16 and 16-byte aligned,
+ *   logits = bf16(hidden @ weight^T), x = bf16(logits / temperature) (skipped at T == 1),
+ *   logp[i] = x[i, labels[i]] - lse_i, entropy[i] = lse_i - sum softmax(x_i) x_i, lse[i],
+ * without writing the logits. `splits` vocab ranges run in parallel and merge in fixed order.
+ * workspace: va_linear_logprob_workspace_bytes(N, splits). entropy / lse may be NULL.
+ * ------------------------------------------------------------------------------------ */
+int64_t va_linear_logprob_workspace_bytes(int64_t N, int splits);
+int va_linear_logprob_fwd(const void *hidden, int64_t ldh, const void *weight, int64_t ldw, int dtype,
+                          const int64_t *labels, int64_t N, int64_t H, int64_t V, float temperature, int splits,
+                          float *logp, float *entropy, float *lse, void *workspace, void *stream);
+
+/* ---------------------------------------------------------------------------------------
  * Discounted returns for REINFORCE++ (mode VA_RET_RFPP, gamma) and ReMax (VA_RET_REMAX:
  * baselines [B] required, adv [B, R] written). rewards / returns / adv [B, R] fp32.
  * ------------------------------------------------------------------------------------ */

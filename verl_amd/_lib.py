@@ -79,6 +79,10 @@ _SIGNATURES: dict[str, tuple] = {
     "va_value_loss_fwd": (c_int, [_P, _P, _P, _P, c_int, c_int64, c_int64, c_float, c_int, _P, _P, _P]),
     "va_value_loss_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_float, c_int, _P, _P, _P]),
     "va_discounted_returns": (c_int, [_P, _P, c_int, c_int64, c_int64, c_float, c_int, _P, _P, _P, _P]),
+    "va_linear_logprob_workspace_bytes": (c_int64, [c_int64, c_int]),
+    "va_linear_logprob_fwd": (
+        c_int, [_P, c_int64, _P, c_int64, c_int, _P, c_int64, c_int64, c_int64, c_float, c_int, _P, _P, _P, _P, _P]
+    ),
     "va_karmarkar_karp": (c_int, [_P, c_int64, c_int64, c_int, _P, _P]),
     "va_rope_qkv_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, c_int64, _P]),
 }

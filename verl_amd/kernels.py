@@ -10,6 +10,7 @@ kernels behind the C-ABI of include/verl_amd.h. Every wrapper:
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -51,6 +52,8 @@ class KernelTimer:
     def __init__(self):
         self.records: list[tuple[str, float, object, object]] = []
 
+    FLOP_KERNELS = frozenset({"linear_logprob_fwd"})
+
     def start(self, stream):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(stream)
@@ -69,10 +72,15 @@ class KernelTimer:
             d["launches"] += 1
             d["algo_bytes_total"] += nb
             d["time_ms_total"] += e0.elapsed_time(e1)
-        for d in out.values():
+        for name, d in out.items():
             d["avg_us"] = 1e3 * d["time_ms_total"] / d["launches"]
-            d["avg_bytes"] = d["algo_bytes_total"] / d["launches"]
-            d["gbps"] = d["algo_bytes_total"] / (d["time_ms_total"] * 1e-3) / 1e9
+            if name in self.FLOP_KERNELS:  # MFMA-bound: the recorded amount is algorithmic flops
+                d["algo_flops_total"] = d.pop("algo_bytes_total")
+                d["avg_flops"] = d["algo_flops_total"] / d["launches"]
+                d["tflops"] = d["algo_flops_total"] / (d["time_ms_total"] * 1e-3) / 1e12
+            else:
+                d["avg_bytes"] = d["algo_bytes_total"] / d["launches"]
+                d["gbps"] = d["algo_bytes_total"] / (d["time_ms_total"] * 1e-3) / 1e9
         return out
 
 
@@ -175,6 +183,91 @@ def logprob_entropy(logits, labels, temperature: float = 1.0, inplace_backward: 
     ``logits.div_(temperature)``; one fused HBM pass forward, one backward."""
     _require_device(logits, labels)
     return _LogprobEntropy.apply(logits, labels, temperature, inplace_backward)
+
+
+# =============================================================================== fused lm_head + log-prob
+def _linear_logprob_splits(n_rows: int) -> int:
+    """Vocab ranges per row block: enough workgroups (~4 per CU of 256) without tiny ranges."""
+    env = os.environ.get("VERL_AMD_LINEAR_LOGPROB_SPLITS")
+    if env:
+        return int(env)
+    blocks = max(1, (n_rows + 127) // 128)
+    return int(min(64, max(1, -(-1024 // blocks))))
+
+
+def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float):
+    N, H = hidden.shape
+    V = weight.shape[0]
+    splits = _linear_logprob_splits(N)
+    logp = torch.empty(N, dtype=torch.float32, device=hidden.device)
+    ent = torch.empty(N, dtype=torch.float32, device=hidden.device)
+    lse = torch.empty(N, dtype=torch.float32, device=hidden.device)
+    nbytes = L.load().va_linear_logprob_workspace_bytes(N, splits)
+    ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=hidden.device)
+    ev = TIMER.start(torch.cuda.current_stream(hidden.device)) if TIMER is not None else None
+    L.call("va_linear_logprob_fwd", _p(hidden), hidden.stride(0), _p(weight), weight.stride(0), L.VA_BF16, _p(labels),
+           N, H, V, float(temperature), splits, _p(logp), _p(ent), _p(lse), _p(ws), _stream(hidden))
+    if ev is not None:  # MFMA-bound: algorithmic flops 2 N V H
+        TIMER.stop("linear_logprob_fwd", 2 * N * V * H, torch.cuda.current_stream(hidden.device), ev)
+    return logp, ent, lse
+
+
+class _LinearLogprob(torch.autograd.Function):
+    """Forward: one fused MFMA pass (no logits in HBM). Backward: logits are recomputed per row
+    chunk with a hipBLASLt GEMM, turned into dlogits in place by va_logprob_entropy_bwd, and
+    pushed through the two GEMMs of the lm_head (the reference's fused path also recomputes)."""
+
+    CHUNK_BYTES = 2 << 30
+
+    @staticmethod
+    def forward(ctx, hidden, weight, labels, temperature):
+        logp, ent, lse = _linear_logprob_fwd_raw(hidden, weight, labels, temperature)
+        ctx.save_for_backward(hidden, weight, labels, lse, ent)
+        ctx.temperature = float(temperature)
+        return logp, ent
+
+    @staticmethod
+    def backward(ctx, g_logp, g_ent):
+        hidden, weight, labels, lse, ent = ctx.saved_tensors
+        N, H = hidden.shape
+        V = weight.shape[0]
+        g1 = None if g_logp is None else _f32(g_logp)
+        g2 = None if g_ent is None else _f32(g_ent)
+        d_hidden = torch.empty_like(hidden) if ctx.needs_input_grad[0] else None
+        d_weight = torch.zeros_like(weight, dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        rows = max(1, int(_LinearLogprob.CHUNK_BYTES // (V * hidden.element_size())))
+        for r0 in range(0, N, rows):
+            r1 = min(N, r0 + rows)
+            h = hidden[r0:r1]
+            logits = h @ weight.t()
+            L.call("va_logprob_entropy_bwd", _p(g1[r0:r1] if g1 is not None else None),
+                   _p(g2[r0:r1] if g2 is not None else None), _p(logits), L.VA_BF16, r1 - r0, V, logits.stride(0),
+                   _p(labels[r0:r1]), _p(lse[r0:r1]), _p(ent[r0:r1]), ctx.temperature, _p(logits), logits.stride(0),
+                   _stream(logits))
+            if d_hidden is not None:
+                torch.mm(logits, weight, out=d_hidden[r0:r1])
+            if d_weight is not None:
+                d_weight.add_((logits.t() @ h).float())
+        if d_weight is not None:
+            d_weight = d_weight.to(weight.dtype)
+        return d_hidden, d_weight, None, None
+
+
+def linear_logprob_entropy(hidden, weight, labels, temperature: float = 1.0):
+    """(log p[label], entropy) of ``hidden @ weight.T`` (the lm_head) after ``div_(temperature)``,
+    computed by the fused MFMA kernel without materialising the [N, V] logits. bf16 only."""
+    _require_device(hidden, weight, labels)
+    _bf16_only(hidden, weight)
+    if hidden.dim() != 2 or weight.dim() != 2 or hidden.shape[1] != weight.shape[1]:
+        raise ValueError(f"linear_logprob: hidden {tuple(hidden.shape)} vs weight {tuple(weight.shape)}")
+    if hidden.stride(-1) != 1 or hidden.stride(0) % 8 or hidden.data_ptr() % 16:
+        hidden = hidden.contiguous()
+    if weight.stride(-1) != 1 or weight.stride(0) % 8:
+        weight = weight.contiguous()
+    lab = labels.reshape(-1).long().contiguous()
+    if lab.shape[0] != hidden.shape[0]:
+        raise ValueError(f"labels ({lab.shape[0]}) do not match hidden rows ({hidden.shape[0]})")
+    return _LinearLogprob.apply(hidden, weight, lab, float(temperature))
 
 
 # =============================================================================== policy loss

@@ -58,7 +58,8 @@ def actor_config(**overrides) -> AttrDict:
         entropy_from_logits_with_chunking=False,
         entropy_checkpointing=False,
         use_remove_padding=True,
-        use_fused_kernels=True,
+        use_fused_kernels=False,
+        fused_logprob_no_grad=False,
         optim=AttrDict(lr=1e-6, weight_decay=0.01, betas=(0.9, 0.999)),
     )
     for k, v in overrides.items():

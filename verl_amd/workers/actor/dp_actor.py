@@ -28,6 +28,7 @@ import torch
 from torch import nn
 
 from ... import _lib as L
+from ... import kernels as K
 from ...protocol import DataProto
 from ...trainer.ppo import core_algos
 from ...trainer.ppo.core_algos import agg_loss, get_policy_loss_fn, kl_penalty
@@ -118,6 +119,12 @@ class DataParallelPPOActor(BasePPOActor):
         # (qwen2_fused.py; bf16 weights only, decided on first use)
         self.fused_model_ops = self.use_remove_padding and self.config.get("fused_model_ops", True)
         self._fused_backbone = None
+        # fused lm_head + log-softmax + entropy (linear_logprob.hip): the
+        # reference's use_fused_kernels flag turns it on for every pass (backward recomputes the
+        # logits per chunk, dp_actor.py:163-190); fused_logprob_no_grad uses it only where no
+        # gradient is needed (old / ref log-prob passes), where nothing has to be recomputed.
+        self.use_fused_kernels = self.config.get("use_fused_kernels", False)
+        self.fused_logprob_no_grad = self.config.get("fused_logprob_no_grad", False)
 
     # ------------------------------------------------------------------ forward
     def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False, packing: _Packing = None):
@@ -152,10 +159,16 @@ class DataParallelPPOActor(BasePPOActor):
                     )
                     hidden = out.last_hidden_state[0]
                 h_sel = hidden.index_select(0, packing.sel_hidden)
-                logits = self._lm_head(h_sel)
                 labels = responses.reshape(-1).index_select(0, packing.sel_out)
-                lp_sel, ent_sel = verl_F.logprobs_and_entropy_from_logits(
-                    logits, labels, temperature, inplace_backward=True)
+                if self._use_fused_lm_head():
+                    w = self._lm_head.weight
+                    lp_sel, ent_sel = K.linear_logprob_entropy(
+                        h_sel.to(torch.bfloat16), w if w.dtype == torch.bfloat16 else w.to(torch.bfloat16), labels,
+                        temperature)
+                else:
+                    logits = self._lm_head(h_sel)
+                    lp_sel, ent_sel = verl_F.logprobs_and_entropy_from_logits(
+                        logits, labels, temperature, inplace_backward=True)
                 log_probs = lp_sel.new_zeros(B * R).index_copy(0, packing.sel_out, lp_sel).view(B, R)
                 entropy = None
                 if calculate_entropy:
@@ -171,6 +184,12 @@ class DataParallelPPOActor(BasePPOActor):
                     logits, responses, temperature, inplace_backward=True)
                 entropy = ent if calculate_entropy else None
         return entropy, log_probs
+
+    def _use_fused_lm_head(self) -> bool:
+        head = self._lm_head
+        if not isinstance(head, nn.Linear) or head.bias is not None:
+            return False
+        return bool(self.use_fused_kernels or (self.fused_logprob_no_grad and not torch.is_grad_enabled()))
 
     def _plans(self, data: DataProto, sizes: list[int] = None, idx_lists: list[list[int]] = None) -> list:
         """Packing plans of consecutive micro-batches of ``sizes`` rows, or of the dynamic
