@@ -307,6 +307,17 @@ int va_value_loss_bwd(const float *g_out, const float *vpreds, const float *valu
                       int agg_mode, const void *workspace, float *d_vpreds, void *stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Causal varlen flash-attention forward for the actor backbone (not a §8 row). q [T, Hq, 64],
+ * k / v [T, Hk, 64] bf16 packed by cu_seqlens [B+1] int32; block_table [n_blocks][2] int32 =
+ * (sequence, first query row) of every 128-row query block (every query row of a sequence must
+ * be < max_len); o [T, Hq, 64] bf16, lse [B, Hq, max_len] fp32 = ln sum exp(scale * q.k) (the
+ * padded layout aten::_flash_attention_backward reads; rows >= a sequence's length untouched).
+ * ------------------------------------------------------------------------------------ */
+int va_flash_attn_fwd(const void *q, const void *k, const void *v, const int32_t *cu_seqlens,
+                      const int32_t *block_table, int64_t n_blocks, int64_t T, int64_t Hq, int64_t Hk,
+                      int64_t head_dim, int64_t max_len, float scale, void *o, float *lse, void *stream);
+
+/* ---------------------------------------------------------------------------------------
  * Host-side (no GPU) sequence-length balancing. Replaces verl/utils/seqlen_balancing.py:26-127
  * `karmarkar_karp(seqlen_list, k_partitions, equal_size)` with identical partitions.
  *   seqlens [n]; order [n] receives the item indices of partition 0, then 1, ... in the

@@ -1,0 +1,141 @@
+"""gfx950 causal varlen flash-attention forward (attention.hip) against PyTorch-ROCm's flash
+varlen kernel and an fp32 SDPA reference, plus the backward through aten's flash backward fed
+with this forward's O / LSE."""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _inputs(lens, hq=14, hk=2, d=64, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    T = int(sum(lens))
+    q = torch.randn(T, hq, d, generator=g).to(torch.bfloat16).to(DEV)
+    k = torch.randn(T, hk, d, generator=g).to(torch.bfloat16).to(DEV)
+    v = torch.randn(T, hk, d, generator=g).to(torch.bfloat16).to(DEV)
+    cu = np.zeros(len(lens) + 1, dtype=np.int64)
+    np.cumsum(lens, out=cu[1:])
+    return q, k, v, cu
+
+
+def _ref_fp32(q, k, v, cu, scale):
+    """Per-sequence causal SDPA in fp32 (GQA by repeat) -> O [T, Hq, D], LSE [Hq, T]."""
+    hq, hk = q.shape[1], k.shape[1]
+    outs, lses = [], []
+    for a, b in zip(cu[:-1], cu[1:]):
+        qs = q[a:b].float().transpose(0, 1)
+        ks = k[a:b].float().repeat_interleave(hq // hk, dim=1).transpose(0, 1)
+        vs = v[a:b].float().repeat_interleave(hq // hk, dim=1).transpose(0, 1)
+        s = (qs @ ks.transpose(1, 2)) * scale
+        n = b - a
+        mask = torch.ones(n, n, dtype=torch.bool, device=DEV).tril()
+        s = s.masked_fill(~mask, float("-inf"))
+        lses.append(torch.logsumexp(s, dim=-1))
+        outs.append((torch.softmax(s, dim=-1) @ vs).transpose(0, 1))
+    return torch.cat(outs, 0), torch.cat(lses, 1)
+
+
+@pytest.mark.parametrize("lens", [[1, 17, 128, 129, 300], [1184, 1100, 1280, 700], [64] * 9])
+def test_flash_forward_matches_fp32_reference(lens):
+    from verl_amd.workers.actor import attention as A
+
+    q, k, v, cu = _inputs(lens, seed=len(lens))
+    scale = 64 ** -0.5
+    cu_d = torch.tensor(cu, dtype=torch.int32, device=DEV)
+    blocks = torch.tensor(A.flash_block_table(cu), device=DEV)
+    o = A.flash_attention(q, k, v, cu_d, int(max(lens)), blocks)
+    want_o, want_lse = _ref_fp32(q, k, v, cu, scale)
+    err = (o.float() - want_o).abs()
+    assert err.max().item() < 2e-2, err.max().item()  # bf16 output + bf16 P
+    assert err.mean().item() < 2e-3
+    # LSE (aten's padded [B, Hq, max_len] layout) vs the fp32 reference
+    T, mx = q.shape[0], int(max(lens))
+    lse = torch.zeros(len(lens), 14, mx, device=DEV)
+    from verl_amd import _lib as L
+    from verl_amd import kernels as K
+
+    o2 = torch.empty_like(q)
+    L.call("va_flash_attn_fwd", K._p(q), K._p(k), K._p(v), K._p(cu_d), K._p(blocks), blocks.shape[0], T, 14, 2, 64,
+           mx, scale, K._p(o2), K._p(lse), K._stream(q))
+    assert torch.equal(o2, o)
+    for i, (a, b) in enumerate(zip(cu[:-1], cu[1:])):
+        assert (lse[i, :, : b - a] - want_lse[:, a:b]).abs().max().item() < 1e-3
+
+
+def test_flash_forward_matches_torch_flash_and_lse_convention():
+    from verl_amd.workers.actor import attention as A
+
+    lens = [200, 513, 1024, 77]
+    q, k, v, cu = _inputs(lens, seed=5)
+    cu_d = torch.tensor(cu, dtype=torch.int32, device=DEV)
+    mx = int(max(lens))
+    out_t, lse_t, *_ = torch.ops.aten._flash_attention_forward(q, k, v, cu_d, cu_d, mx, mx, 0.0, True,
+                                                              return_debug_mask=False)
+    blocks = torch.tensor(A.flash_block_table(cu), device=DEV)
+    o = A.flash_attention(q, k, v, cu_d, mx, blocks)
+    assert (o.float() - out_t.float()).abs().max().item() < 2e-2
+    from verl_amd import _lib as L
+    from verl_amd import kernels as K
+
+    lse = torch.zeros(lse_t.shape, device=DEV, dtype=torch.float32)
+    assert tuple(lse_t.shape) == (len(lens), 14, mx), lse_t.shape
+    L.call("va_flash_attn_fwd", K._p(q), K._p(k), K._p(v), K._p(cu_d), K._p(blocks), blocks.shape[0], q.shape[0], 14,
+           2, 64, mx, 64 ** -0.5, K._p(torch.empty_like(q)), K._p(lse), K._stream(q))
+    for i, n in enumerate(lens):
+        assert (lse[i, :, :n] - lse_t[i, :, :n].float()).abs().max().item() < 1e-3
+
+
+def test_flash_backward_matches_torch_varlen():
+    from torch.nn.attention.varlen import varlen_attn
+
+    from verl_amd.workers.actor import attention as A
+
+    lens = [300, 129, 1000]
+    q, k, v, cu = _inputs(lens, seed=7)
+    cu_d = torch.tensor(cu, dtype=torch.int32, device=DEV)
+    mx = int(max(lens))
+    g = torch.randn_like(q)
+    qa, ka, va = (t.clone().requires_grad_(True) for t in (q, k, v))
+    varlen_attn(qa, ka, va, cu_d, cu_d, mx, mx, is_causal=True).backward(g)
+    qb, kb, vb = (t.clone().requires_grad_(True) for t in (q, k, v))
+    blocks = torch.tensor(A.flash_block_table(cu), device=DEV)
+    A.flash_attention(qb, kb, vb, cu_d, mx, blocks).backward(g)
+    for a, b, what in ((qa.grad, qb.grad, "dq"), (ka.grad, kb.grad, "dk"), (va.grad, vb.grad, "dv")):
+        rel = (a.float() - b.float()).norm() / a.float().norm()
+        assert rel < 1e-2, f"{what}: relative L2 {rel:.3e}"
+
+
+def test_actor_with_flash_forward_matches_torch_flash():
+    import copy
+
+    from verl_amd.utils.config import actor_config
+    from verl_amd.utils.model import build_qwen2
+    from verl_amd.utils.synthetic import make_grpo_batch
+    from verl_amd.workers.actor import DataParallelPPOActor
+
+    base = build_qwen2("tiny", device=DEV, attn_implementation="sdpa", seed=3, hidden_size=256,
+                       num_attention_heads=4, num_key_value_heads=2)  # head_dim 64
+    for p in base.parameters():
+        p.data = p.data.to(torch.bfloat16)
+    data = make_grpo_batch(n_prompts=2, n=4, prompt_len=40, response_len=90, vocab=4096, min_prompt=3,
+                           dense_responses=False, min_response=5, seed=4, device=DEV)
+    data.meta_info.update(micro_batch_size=4, temperature=1.0, use_dynamic_bsz=False)
+    res = {}
+    for fa in (False, True):
+        m = copy.deepcopy(base)
+        a = DataParallelPPOActor(actor_config(use_remove_padding=True, fused_attention=fa), m,
+                                 torch.optim.SGD(m.parameters(), lr=0.0))
+        lp, ent = a.compute_log_prob(data, calculate_entropy=True)
+        b = data.batch
+        _, lp2 = a._forward_micro_batch(b, 1.0)
+        (lp2 * b["response_mask"]).sum().backward()
+        res[fa] = (lp, ent, {n: p.grad.clone() for n, p in m.named_parameters()})
+    msk = data.batch["response_mask"].bool()
+    assert torch.allclose(res[True][0][msk], res[False][0][msk], atol=5e-2, rtol=2e-2)
+    for n in res[False][2]:
+        a, b = res[True][2][n].float(), res[False][2][n].float()
+        assert ((a - b).norm() / (b.norm() + 1e-12)) < 8e-2, n

@@ -77,8 +77,46 @@ def gemm_cases(T=9472, H=896, FF=4864, QKV=1152):
     del x
 
 
+def attn_gfx950(n_seq=8, seqlen=1184, hq=14, hk=2, d=64):
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import numpy as np
+
+    from verl_amd.workers.actor import attention as A
+
+    dev = "cuda"
+    T = n_seq * seqlen
+    cu_h = np.arange(0, T + 1, seqlen)
+    cu = torch.tensor(cu_h, dtype=torch.int32, device=dev)
+    blocks = torch.tensor(A.flash_block_table(cu_h), device=dev)
+    q = torch.randn(T, hq, d, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(T, hk, d, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(T, hk, d, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    g = torch.randn_like(q)
+
+    def fwd():
+        A.flash_attention(q, k, v, cu, seqlen, blocks)
+
+    def fwdbwd():
+        o = A.flash_attention(q, k, v, cu, seqlen, blocks)
+        torch.autograd.grad(o, (q, k, v), g)
+
+    flops_fwd = 2.0 * n_seq * seqlen * seqlen * d * hq
+    tf = timeit(fwd)
+    tfb = timeit(fwdbwd)
+    print(json.dumps({"case": f"attn_gfx950_fwd_n{n_seq}", "fwd_us": round(tf, 1),
+                      "fwd_tflops": round(flops_fwd / tf / 1e6, 1), "fwdbwd_us": round(tfb, 1),
+                      "fwdbwd_tflops": round(3.5 * flops_fwd / tfb / 1e6, 1)}))
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["attn", "gemm"]
+    if "gfx950" in what:
+        attn_case("aotriton")
+        attn_gfx950()
+        attn_gfx950(n_seq=16)
     if "attn" in what:
         for b in ("aotriton", "ck"):
             try:

@@ -38,9 +38,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float base_of(float m) { return m == -INFINITY ? 0.f : m * kLog2eF; }
 
-__device__ __forceinline__ float round_bf16(float x) {
-  return __uint_as_float(f32_to_bf16_bits(x) << 16);
-}
+__device__ __forceinline__ float round_bf16(float x) { return round_to_bf16(x); }
 
 struct RowAcc {
   float m, s, t;

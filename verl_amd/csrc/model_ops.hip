@@ -28,8 +28,8 @@ namespace va {
 namespace {
 
 __device__ __forceinline__ float bf(uint16_t b) { return bf16_to_f32(b); }
-__device__ __forceinline__ uint16_t to_bf(float f) { return static_cast<uint16_t>(f32_to_bf16_bits(f)); }
-__device__ __forceinline__ float rbf(float f) { return bf(to_bf(f)); }  // round through bf16
+__device__ __forceinline__ uint16_t to_bf(float f) { return static_cast<uint16_t>(pack2_bf16(f, 0.f) & 0xffffu); }
+__device__ __forceinline__ float rbf(float f) { return round_to_bf16(f); }  // round through bf16
 
 // 8 bf16 <-> 8 floats
 __device__ __forceinline__ void unpack8(const uint4 v, float (&f)[8]) {
@@ -37,12 +37,8 @@ __device__ __forceinline__ void unpack8(const uint4 v, float (&f)[8]) {
   f[4] = bf16_lo(v.z); f[5] = bf16_hi(v.z); f[6] = bf16_lo(v.w); f[7] = bf16_hi(v.w);
 }
 __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
-  uint4 v;
-  v.x = f32_to_bf16_bits(f[0]) | (f32_to_bf16_bits(f[1]) << 16);
-  v.y = f32_to_bf16_bits(f[2]) | (f32_to_bf16_bits(f[3]) << 16);
-  v.z = f32_to_bf16_bits(f[4]) | (f32_to_bf16_bits(f[5]) << 16);
-  v.w = f32_to_bf16_bits(f[6]) | (f32_to_bf16_bits(f[7]) << 16);
-  return v;
+  return make_uint4(pack2_bf16(f[0], f[1]), pack2_bf16(f[2], f[3]), pack2_bf16(f[4], f[5]),
+                    pack2_bf16(f[6], f[7]));
 }
 __device__ __forceinline__ uint4 ld16(const uint16_t *p) { return *reinterpret_cast<const uint4 *>(p); }
 __device__ __forceinline__ void st16(uint16_t *p, uint4 v) { *reinterpret_cast<uint4 *>(p) = v; }

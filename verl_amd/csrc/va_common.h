@@ -27,6 +27,13 @@ __device__ __forceinline__ uint32_t f32_to_bf16_bits(float f) {
   uint32_t r = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
   return ((u & 0x7fffffffu) > 0x7f800000u) ? ((u >> 16) | 0x40u) : r;
 }
+// the same RNE conversion in one v_cvt_pk_bf16_f32 (2 values per instruction)
+typedef float va_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 va_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(va_f32x2{a, b}, va_bf16x2));
+}
+__device__ __forceinline__ float round_to_bf16(float x) { return __uint_as_float(pack2_bf16(x, 0.f) << 16); }
 __device__ __forceinline__ float f16_to_f32(uint16_t h) {
   return static_cast<float>(__builtin_bit_cast(_Float16, h));
 }

@@ -43,6 +43,67 @@ def packed_attention(q, k, v, cu, mx, scaling=None):
     return _varlen(q, k, v, cu, mx)
 
 
+# ------------------------------------------------------------------ gfx950 flash forward
+FLASH_QB = 128  # query rows per workgroup of va_flash_attn_fwd
+
+
+def flash_block_table(cu_host) -> "np.ndarray":
+    """(sequence, first query row) of every 128-row query block, heaviest (latest) blocks first so
+    the causal tail of long sequences does not end the launch on a few workgroups."""
+    import numpy as np
+
+    cu_host = np.asarray(cu_host, dtype=np.int64)
+    lens = np.diff(cu_host)
+    seqs = np.repeat(np.arange(len(lens)), (lens + FLASH_QB - 1) // FLASH_QB)
+    starts = np.concatenate([np.arange(0, n, FLASH_QB) for n in lens]) if len(lens) else np.zeros(0, np.int64)
+    order = np.lexsort((seqs, -starts))  # by start descending, then sequence
+    return np.stack([seqs[order], starts[order]], axis=1).astype(np.int32)
+
+
+class _FlashVarlen(torch.autograd.Function):
+    """Forward: va_flash_attn_fwd (gfx950 MFMA kernel). Backward: aten._flash_attention_backward
+    with this forward's O and LSE (the same tensors PyTorch's own varlen path hands it)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, cu, blocks, max_len, scale):
+        from ... import _lib as L
+        from ... import kernels as K
+
+        T, hq, d = q.shape
+        hk = k.shape[1]
+        o = torch.empty_like(q)
+        # aten's varlen flash LSE layout [B, Hq, max_len]; padded rows stay 0 (finite)
+        lse = torch.zeros(cu.shape[0] - 1, hq, int(max_len), dtype=torch.float32, device=q.device)
+        L.call("va_flash_attn_fwd", K._p(q), K._p(k), K._p(v), K._p(cu), K._p(blocks), blocks.shape[0], T, hq, hk, d,
+               int(max_len), float(scale), K._p(o), K._p(lse), K._stream(q))
+        ctx.save_for_backward(q, k, v, o, lse, cu)
+        ctx.max_len = int(max_len)
+        ctx.scale = float(scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, cu = ctx.saved_tensors
+        rng = torch.zeros(2, dtype=torch.uint64, device=q.device)
+        unused = torch.empty(0, device=q.device)
+        dq, dk, dv = torch.ops.aten._flash_attention_backward(
+            do.contiguous(), q, k, v, o, lse, cu, cu, ctx.max_len, ctx.max_len, 0.0, True, rng, unused,
+            scale=ctx.scale)
+        return dq, dk, dv, None, None, None, None
+
+
+def flash_attention(q, k, v, cu, max_len, blocks, scaling=None):
+    """Causal varlen attention on packed [T, H, 64] bf16 tensors with the gfx950 forward kernel.
+    ``blocks`` = device int32 [n, 2] from flash_block_table."""
+    scale = q.shape[-1] ** -0.5 if scaling is None else scaling
+    return _FlashVarlen.apply(q.contiguous(), k.contiguous(), v.contiguous(), cu, blocks, max_len, scale)
+
+
+def flash_supported(q, k) -> bool:
+    return (q.is_cuda and q.dtype == torch.bfloat16 and k.dtype == torch.bfloat16 and q.shape[-1] == 64
+            and q.shape[1] % k.shape[1] == 0)
+
+
 def varlen_attention_forward(module, query, key, value, attention_mask, scaling=None, dropout=0.0, **kwargs):
     """AttentionInterface entry: query [1, Hq, nnz, D], key/value [1, Hkv, nnz, D] ->
     ([1, nnz, Hq, D], None)."""

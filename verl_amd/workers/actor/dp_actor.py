@@ -59,6 +59,7 @@ class _Packing:
     max_seqlen: int
     sel_hidden: torch.Tensor  # [n_sel] rows of the packed hidden states that predict a response token
     sel_out: torch.Tensor  # [n_sel] flat index into [B*R]
+    attn_blocks: torch.Tensor = None  # [n, 2] int32 (sequence, first query row) for va_flash_attn_fwd
 
 
 def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device) -> _Packing:
@@ -88,6 +89,7 @@ def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device) -> _Packing:
         max_seqlen=int(seqlens.max()) if B else 0,
         sel_hidden=dev(sel_hidden, np.int64),
         sel_out=dev(sel_out, np.int64),
+        attn_blocks=dev(attention.flash_block_table(cu), np.int32),
     )
 
 
@@ -124,6 +126,8 @@ class DataParallelPPOActor(BasePPOActor):
         # logits per chunk, dp_actor.py:163-190); fused_logprob_no_grad uses it only where no
         # gradient is needed (old / ref log-prob passes), where nothing has to be recomputed.
         self.use_fused_kernels = self.config.get("use_fused_kernels", False)
+        # gfx950 flash-attention forward (attention.hip) inside the fused packed backbone
+        self.fused_attention = self.config.get("fused_attention", True)
         self.fused_logprob_no_grad = self.config.get("fused_logprob_no_grad", False)
 
     # ------------------------------------------------------------------ forward
@@ -150,7 +154,8 @@ class DataParallelPPOActor(BasePPOActor):
                 if self._fused_backbone:
                     from .qwen2_fused import packed_forward
 
-                    hidden = packed_forward(self._backbone, ids[0], pos[0], packing.cu_seqlens, packing.max_seqlen)
+                    hidden = packed_forward(self._backbone, ids[0], pos[0], packing.cu_seqlens, packing.max_seqlen,
+                                            attn_blocks=packing.attn_blocks if self.fused_attention else None)
                 else:
                     out = self._backbone(
                         input_ids=ids, position_ids=pos, attention_mask=_NO_MASK, use_cache=False,

@@ -80,7 +80,9 @@ class DataParallelPPOCritic(BasePPOCritic):
                 if self._fused_backbone:
                     from ..actor.qwen2_fused import packed_forward
 
-                    hidden = packed_forward(self._backbone, ids, pos, packing.cu_seqlens, packing.max_seqlen)
+                    blocks = packing.attn_blocks if self.config.get("fused_attention", True) else None
+                    hidden = packed_forward(self._backbone, ids, pos, packing.cu_seqlens, packing.max_seqlen,
+                                            attn_blocks=blocks)
                 else:
                     out = self._backbone(
                         input_ids=ids.unsqueeze(0), position_ids=pos.unsqueeze(0), attention_mask=_NO_MASK,
