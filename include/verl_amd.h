@@ -316,6 +316,14 @@ int va_value_loss_bwd(const float *g_out, const float *vpreds, const float *valu
 int va_flash_attn_fwd(const void *q, const void *k, const void *v, const int32_t *cu_seqlens,
                       const int32_t *block_table, int64_t n_blocks, int64_t T, int64_t Hq, int64_t Hk,
                       int64_t head_dim, int64_t max_len, float scale, void *o, float *lse, void *stream);
+/* Backward of the above (no atomics, deterministic): dq / dk / dv bf16 like q / k / v. q_blocks
+ * = the forward's block table; k_blocks = (sequence, first key) of every 128-key block; delta =
+ * fp32 workspace [B, Hq, max_len] (rowsum(dO * O), written here); partial = fp32 workspace of
+ * 2 * Hq * T * 64 (per-query-head dK / dV before the GQA group sum). */
+int va_flash_attn_bwd(const void *q, const void *k, const void *v, const void *o, const void *dout, const float *lse,
+                      const int32_t *cu_seqlens, const int32_t *q_blocks, int64_t n_q_blocks, const int32_t *k_blocks,
+                      int64_t n_k_blocks, int64_t T, int64_t Hq, int64_t Hk, int64_t head_dim, int64_t max_len,
+                      float scale, float *delta, float *partial, void *dq, void *dk, void *dv, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Host-side (no GPU) sequence-length balancing. Replaces verl/utils/seqlen_balancing.py:26-127

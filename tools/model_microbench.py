@@ -91,6 +91,7 @@ def attn_gfx950(n_seq=8, seqlen=1184, hq=14, hk=2, d=64):
     cu_h = np.arange(0, T + 1, seqlen)
     cu = torch.tensor(cu_h, dtype=torch.int32, device=dev)
     blocks = torch.tensor(A.flash_block_table(cu_h), device=dev)
+    kblocks = torch.tensor(A.flash_key_block_table(cu_h), device=dev)
     q = torch.randn(T, hq, d, device=dev, dtype=torch.bfloat16, requires_grad=True)
     k = torch.randn(T, hk, d, device=dev, dtype=torch.bfloat16, requires_grad=True)
     v = torch.randn(T, hk, d, device=dev, dtype=torch.bfloat16, requires_grad=True)
@@ -100,7 +101,7 @@ def attn_gfx950(n_seq=8, seqlen=1184, hq=14, hk=2, d=64):
         A.flash_attention(q, k, v, cu, seqlen, blocks)
 
     def fwdbwd():
-        o = A.flash_attention(q, k, v, cu, seqlen, blocks)
+        o = A.flash_attention(q, k, v, cu, seqlen, blocks, kblocks=kblocks)
         torch.autograd.grad(o, (q, k, v), g)
 
     flops_fwd = 2.0 * n_seq * seqlen * seqlen * d * hq

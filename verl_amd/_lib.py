@@ -86,6 +86,11 @@ _SIGNATURES: dict[str, tuple] = {
     "va_flash_attn_fwd": (
         c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, c_float, _P, _P, _P]
     ),
+    "va_flash_attn_bwd": (
+        c_int,
+        [_P, _P, _P, _P, _P, _P, _P, _P, c_int64, _P, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, c_float,
+         _P, _P, _P, _P, _P, _P],
+    ),
     "va_karmarkar_karp": (c_int, [_P, c_int64, c_int64, c_int, _P, _P]),
     "va_rope_qkv_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, c_int64, _P]),
 }

@@ -221,6 +221,365 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
   }
 }
 
+// =====================================================================================
+// Backward. dS = P * (dP - delta), delta = rowsum(dO * O); P recomputed from Q, K and the
+// forward's LSE. Three launches, no atomics (dQ, dK, dV are each written once: deterministic):
+//   flash_bwd_delta   delta [B, Hq, max_len] (the LSE layout)
+//   flash_bwd_dkdv    workgroup = 128 keys of one sequence x one query head; wave = 32 keys whose
+//                     K, V fragments stay in registers. It sweeps the 32-row query tiles at or
+//                     after its keys (Q, dO, LSE, delta staged in double-buffered LDS):
+//                       S = Q K^T, dP = dO V^T  with the KEY on the lane (4 MFMAs each), so
+//                       P and dS are already the B operands of
+//                       dV^T += dO^T P,  dK^T += Q^T dS  (A = transposed reads of the Q / dO images)
+//   flash_bwd_group_sum  dK, dV = fixed-order sum of the per-query-head fp32 partials over the
+//                     GQA group (1120 dK/dV workgroups instead of 160 at 8 x 1184 tokens, Hkv = 2)
+//   flash_bwd_dq      workgroup = 128 queries x one query head (the forward's block table); wave =
+//                     32 queries with Q, dO fragments in registers; per 32-key tile
+//                       S^T = K Q^T, dP^T = V dO^T (query on the lane), dQ^T += K^T dS^T
+// LDS images are [rows][64] bf16 with 16-B chunk c of row r at c ^ (r & 7): conflict-light row
+// reads (ds_read_b128) and per-lane swizzled addresses for the transposed reads.
+
+__device__ __forceinline__ int swz(int row, int d) { return row * D + ((((d >> 3) ^ (row & 7))) << 3) + (d & 7); }
+
+// A operand (32 rows of d x 16 k) from a [k][64] image by transposed reads: element j of lane
+// (d = dh*32 + lane&31, half h) = image[16 s + 8 (j >> 2) + 4 h + (j & 3) + rbase][d]
+__device__ __forceinline__ bf16x8 tr_frag(const uint16_t *img, int rbase, int s, int dh, int lane) {
+  const int h = lane >> 5, g16 = lane >> 4, li = lane & 15;
+  const int r0 = rbase + 16 * s + 4 * h + (li >> 2);
+  const int col = dh * 32 + 16 * (g16 & 1) + 4 * (li & 3);
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)(img + swz(r0, col)));
+  const v4s hi =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s *)(img + swz(r0 + 8, col)));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__device__ __forceinline__ bf16x8 pack_frag(const float *x) {
+  return __builtin_bit_cast(bf16x8, make_uint4(pk_bf16(x[0], x[1]), pk_bf16(x[2], x[3]), pk_bf16(x[4], x[5]),
+                                               pk_bf16(x[6], x[7])));
+}
+
+__global__ __launch_bounds__(128) void flash_bwd_delta_kernel(const uint16_t *__restrict__ o,
+                                                              const uint16_t *__restrict__ dout,
+                                                              const int32_t *__restrict__ cu,
+                                                              const int32_t *__restrict__ blocks, int64_t ld,
+                                                              int Hq, float *__restrict__ delta) {
+  const int seq = blocks[2 * blockIdx.x], qs = blocks[2 * blockIdx.x + 1];
+  const int head = blockIdx.y;
+  const int s0 = cu[seq], len = cu[seq + 1] - s0;
+  const int qp = qs + threadIdx.x;
+  if (qp >= len) return;
+  const int64_t base = (static_cast<int64_t>(s0 + qp) * Hq + head) * D;
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < D / 8; ++c) {
+    const uint4 a = *reinterpret_cast<const uint4 *>(o + base + 8 * c);
+    const uint4 b = *reinterpret_cast<const uint4 *>(dout + base + 8 * c);
+    acc = fmaf(bf16_lo(a.x), bf16_lo(b.x), acc); acc = fmaf(bf16_hi(a.x), bf16_hi(b.x), acc);
+    acc = fmaf(bf16_lo(a.y), bf16_lo(b.y), acc); acc = fmaf(bf16_hi(a.y), bf16_hi(b.y), acc);
+    acc = fmaf(bf16_lo(a.z), bf16_lo(b.z), acc); acc = fmaf(bf16_hi(a.z), bf16_hi(b.z), acc);
+    acc = fmaf(bf16_lo(a.w), bf16_lo(b.w), acc); acc = fmaf(bf16_hi(a.w), bf16_hi(b.w), acc);
+  }
+  delta[(static_cast<int64_t>(seq) * Hq + head) * ld + qp] = acc;
+}
+
+__global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
+    const uint16_t *__restrict__ q, const uint16_t *__restrict__ k, const uint16_t *__restrict__ v,
+    const uint16_t *__restrict__ dout, const float *__restrict__ lse, const float *__restrict__ delta,
+    const int32_t *__restrict__ cu, const int32_t *__restrict__ kblocks, int64_t ld, int64_t T, int Hq, int Hk,
+    float scale, float *__restrict__ pdk, float *__restrict__ pdv) {
+  constexpr int QT = 32;  // query rows per staged tile
+  // [buf][Q image 32x64 | dO image 32x64] bf16, then [buf][lse2 32 | delta 32] fp32
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * QT * D + 2 * 2 * QT * 2];
+  float *rowc = reinterpret_cast<float *>(lds + 2 * 2 * QT * D);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, kl = lane & 31;
+  const int seq = kblocks[2 * blockIdx.x], kb0 = kblocks[2 * blockIdx.x + 1];
+  const int hq0 = blockIdx.y, g = hq0 / (Hq / Hk);  // one query head; its partial dK / dV
+  const int s0 = cu[seq], len = cu[seq + 1] - s0;
+  const int64_t ldq = static_cast<int64_t>(Hq) * D, ldk = static_cast<int64_t>(Hk) * D;
+  const float c = scale * kLog2e_;
+  const int k0 = kb0 + wave * 32;  // this wave's first key
+  const int key = k0 + kl;         // this lane's key
+  // K^T / V^T fragments (B operands with the key on the lane): lane holds K[key][16 s + 8 h + j]
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (key < len) {
+      kf[s] = *reinterpret_cast<const bf16x8 *>(k + (s0 + key) * ldk + g * D + 16 * s + 8 * h);
+      vf[s] = *reinterpret_cast<const bf16x8 *>(v + (s0 + key) * ldk + g * D + 16 * s + 8 * h);
+    } else {
+      kf[s] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      vf[s] = kf[s];
+    }
+  }
+  f32x16 dkt[2], dvt[2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dkt[dh][r] = 0.f;
+      dvt[dh][r] = 0.f;
+    }
+  // iteration space: query tiles from the block's first key to the end of the sequence
+  const int qfirst = (kb0 / QT) * QT;
+  const int n_qt = len > qfirst ? (len - qfirst + QT - 1) / QT : 0;
+  const int n_it = n_qt;
+  // staging: one 16-B chunk of the Q tile and one of the dO tile per thread; lse2 / delta by 64 threads
+  struct StageQ {
+    uint4 q, d;
+    float rc;
+  };
+  auto load_it = [&](int it) -> StageQ {
+    StageQ st;
+    const int hq = hq0, qt0 = qfirst + it * QT;
+    const int r = tid >> 3, ch = tid & 7, qp = qt0 + r;
+    if (qp < len) {
+      const int64_t base = (s0 + qp) * ldq + hq * D + ch * 8;
+      st.q = *reinterpret_cast<const uint4 *>(q + base);
+      st.d = *reinterpret_cast<const uint4 *>(dout + base);
+    } else {
+      st.q = make_uint4(0, 0, 0, 0);
+      st.d = st.q;
+    }
+    st.rc = 0.f;
+    if (tid < 2 * QT) {
+      const int rr = tid & (QT - 1), qq = qt0 + rr;
+      const int64_t idx = (static_cast<int64_t>(seq) * Hq + hq) * ld + qq;
+      if (qq < len) st.rc = tid < QT ? lse[idx] * kLog2e_ : delta[idx];
+    }
+    return st;
+  };
+  auto store_it = [&](int buf, const StageQ &st) {
+    uint16_t *img = lds + buf * 2 * QT * D;
+    const int r = tid >> 3, ch = tid & 7;
+    *reinterpret_cast<uint4 *>(img + swz(r, ch * 8)) = st.q;
+    *reinterpret_cast<uint4 *>(img + QT * D + swz(r, ch * 8)) = st.d;
+    if (tid < 2 * QT) rowc[buf * 2 * QT + tid] = st.rc;
+  };
+  StageQ stq;
+  if (n_it > 0) {
+    stq = load_it(0);
+    store_it(0, stq);
+  }
+  __syncthreads();
+  for (int it = 0; it < n_it; ++it) {
+    if (it + 1 < n_it) stq = load_it(it + 1);
+    const int buf = it & 1;
+    const uint16_t *qi = lds + buf * 2 * QT * D;
+    const uint16_t *di = qi + QT * D;
+    const float *lse2 = rowc + buf * 2 * QT;
+    const float *dlt = lse2 + QT;
+    const int qt0 = qfirst + it * QT;
+    if (qt0 + QT - 1 >= k0 && k0 < len) {  // some query of the tile sees some key of the wave
+      // S = Q K^T and dP = dO V^T, rows = queries (registers), columns = keys (lanes)
+      f32x16 sacc, pacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sacc[r] = 0.f;
+        pacc[r] = 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 qa = *reinterpret_cast<const bf16x8 *>(qi + swz(kl, 16 * s + 8 * h));
+        const bf16x8 da = *reinterpret_cast<const bf16x8 *>(di + swz(kl, 16 * s + 8 * h));
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], pacc, 0, 0, 0);
+      }
+      const bool need_mask = (qt0 < k0 + 31) || (qt0 + QT > len) || (k0 + 32 > len);
+      float p[16], ds[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qr = crow(r, h);
+        float pv = __builtin_amdgcn_exp2f(sacc[r] * c - lse2[qr]);
+        if (need_mask) {
+          const int qp = qt0 + qr;
+          if (key > qp || qp >= len || key >= len) pv = 0.f;
+        }
+        p[r] = pv;
+        ds[r] = pv * (pacc[r] - dlt[qr]);
+      }
+      // dV^T += dO^T P, dK^T += Q^T dS  (k = queries, permuted order of the accumulator rows)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = pack_frag(p + 8 * s), db = pack_frag(ds + 8 * s);
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          dvt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(di, 0, s, dh, lane), pb, dvt[dh], 0, 0, 0);
+          dkt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(qi, 0, s, dh, lane), db, dkt[dh], 0, 0, 0);
+        }
+      }
+    }
+    if (it + 1 < n_it) store_it((it + 1) & 1, stq);
+    __syncthreads();
+  }
+  // this head's partial dK = scale * (dK^T)^T and dV = (dV^T)^T, fp32 [Hq][T][64]: lane holds
+  // column key, rows d = 32 dh + 8 gg + 4 h + i
+  if (key < len) {
+    float *dkr = pdk + (static_cast<int64_t>(hq0) * T + s0 + key) * D;
+    float *dvr = pdv + (static_cast<int64_t>(hq0) * T + s0 + key) * D;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int d0 = dh * 32 + 8 * gg + 4 * h;
+        *reinterpret_cast<float4 *>(dkr + d0) = make_float4(dkt[dh][4 * gg] * scale, dkt[dh][4 * gg + 1] * scale,
+                                                            dkt[dh][4 * gg + 2] * scale, dkt[dh][4 * gg + 3] * scale);
+        *reinterpret_cast<float4 *>(dvr + d0) =
+            make_float4(dvt[dh][4 * gg], dvt[dh][4 * gg + 1], dvt[dh][4 * gg + 2], dvt[dh][4 * gg + 3]);
+      }
+  }
+}
+
+// dK / dV [T, Hk, 64] bf16 = sum over the G query heads of a group of the partials, fixed order
+__global__ __launch_bounds__(256) void flash_bwd_group_sum_kernel(const float *__restrict__ pdk,
+                                                                  const float *__restrict__ pdv, int64_t T, int Hq,
+                                                                  int Hk, uint16_t *__restrict__ dk,
+                                                                  uint16_t *__restrict__ dv) {
+  const int G = Hq / Hk;
+  const int64_t total = T * Hk * (D / 4);  // float4 granules
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int c4 = static_cast<int>(i % (D / 4));
+    const int64_t tg = i / (D / 4);
+    const int gk = static_cast<int>(tg % Hk);
+    const int64_t t = tg / Hk;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    for (int j = 0; j < G; ++j) {
+      const int64_t off = ((static_cast<int64_t>(gk * G + j)) * T + t) * D + 4 * c4;
+      const float4 x = *reinterpret_cast<const float4 *>(pdk + off);
+      const float4 y = *reinterpret_cast<const float4 *>(pdv + off);
+      a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+      b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+    }
+    const int64_t o = (t * Hk + gk) * D + 4 * c4;
+    *reinterpret_cast<uint2 *>(dk + o) = make_uint2(pk_bf16(a.x, a.y), pk_bf16(a.z, a.w));
+    *reinterpret_cast<uint2 *>(dv + o) = make_uint2(pk_bf16(b.x, b.y), pk_bf16(b.z, b.w));
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
+    const uint16_t *__restrict__ k, const uint16_t *__restrict__ v, const uint16_t *__restrict__ q,
+    const uint16_t *__restrict__ dout, const float *__restrict__ lse, const float *__restrict__ delta,
+    const int32_t *__restrict__ cu, const int32_t *__restrict__ blocks, int64_t ld, int Hq, int Hk, float scale,
+    uint16_t *__restrict__ dq) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * KB * D];  // [buf][K | V][64 keys][64 d], swizzled
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, ql = lane & 31;
+  const int seq = blocks[2 * blockIdx.x], qs = blocks[2 * blockIdx.x + 1];
+  const int head = blockIdx.y, kvh = head / (Hq / Hk);
+  const int s0 = cu[seq], len = cu[seq + 1] - s0;
+  const int q_pos = qs + wave * 32 + ql;
+  const bool q_ok = q_pos < len;
+  const int64_t ldq = static_cast<int64_t>(Hq) * D, ldk = static_cast<int64_t>(Hk) * D;
+  const float c = scale * kLog2e_;
+  bf16x8 qf[4], df[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (q_ok) {
+      qf[s] = *reinterpret_cast<const bf16x8 *>(q + (s0 + q_pos) * ldq + head * D + 16 * s + 8 * h);
+      df[s] = *reinterpret_cast<const bf16x8 *>(dout + (s0 + q_pos) * ldq + head * D + 16 * s + 8 * h);
+    } else {
+      qf[s] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      df[s] = qf[s];
+    }
+  }
+  const int64_t ridx = (static_cast<int64_t>(seq) * Hq + head) * ld + q_pos;
+  const float lse2 = q_ok ? lse[ridx] * kLog2e_ : 0.f;
+  const float dlt = q_ok ? delta[ridx] : 0.f;
+  f32x16 dqt[2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dqt[dh][r] = 0.f;
+
+  const int kv_end = min(len, qs + QB);
+  const int nkb = (kv_end + KB - 1) / KB;
+  const int wave_last_q = qs + wave * 32 + 31;
+  uint4 sk[2], sv[2];
+  auto load_block = [&](int kb) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + u * 256, r = idx >> 3, ch = idx & 7;
+      const int kk = kb * KB + r;
+      if (kk < len) {
+        const int64_t base = (s0 + kk) * ldk + kvh * D + ch * 8;
+        sk[u] = *reinterpret_cast<const uint4 *>(k + base);
+        sv[u] = *reinterpret_cast<const uint4 *>(v + base);
+      } else {
+        sk[u] = make_uint4(0, 0, 0, 0);
+        sv[u] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto store_block = [&](int buf) {
+    uint16_t *lk = lds + buf * 2 * KB * D;
+    uint16_t *lv = lk + KB * D;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + u * 256, r = idx >> 3, ch = idx & 7;
+      *reinterpret_cast<uint4 *>(lk + swz(r, ch * 8)) = sk[u];
+      *reinterpret_cast<uint4 *>(lv + swz(r, ch * 8)) = sv[u];
+    }
+  };
+  if (nkb > 0) {
+    load_block(0);
+    store_block(0);
+  }
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    if (kb + 1 < nkb) load_block(kb + 1);
+    const uint16_t *lk = lds + (kb & 1) * 2 * KB * D;
+    const uint16_t *lv = lk + KB * D;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int key0 = kb * KB + t * 32;
+      if (key0 > wave_last_q || key0 >= len || qs + wave * 32 >= len) continue;
+      f32x16 sacc, pacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sacc[r] = 0.f;
+        pacc[r] = 0.f;
+      }
+      const int krow = t * 32 + ql;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 ka = *reinterpret_cast<const bf16x8 *>(lk + swz(krow, 16 * s + 8 * h));
+        const bf16x8 va = *reinterpret_cast<const bf16x8 *>(lv + swz(krow, 16 * s + 8 * h));
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[s], pacc, 0, 0, 0);
+      }
+      const bool need_mask = (key0 + 31 > qs + wave * 32) || (key0 + 31 >= len);
+      float ds[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float pv = __builtin_amdgcn_exp2f(sacc[r] * c - lse2);
+        if (need_mask) {
+          const int kp = key0 + crow(r, h);
+          if (kp > q_pos || kp >= len) pv = 0.f;
+        }
+        ds[r] = pv * (pacc[r] - dlt);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 db = pack_frag(ds + 8 * s);
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh)
+          dqt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(lk, t * 32, s, dh, lane), db, dqt[dh], 0, 0, 0);
+      }
+    }
+    if (kb + 1 < nkb) store_block((kb + 1) & 1);
+    __syncthreads();
+  }
+  if (q_ok) {
+    uint16_t *qr = dq + (s0 + q_pos) * ldq + head * D;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg)
+        *reinterpret_cast<uint2 *>(qr + dh * 32 + 8 * gg + 4 * h) =
+            make_uint2(pk_bf16(dqt[dh][4 * gg] * scale, dqt[dh][4 * gg + 1] * scale),
+                       pk_bf16(dqt[dh][4 * gg + 2] * scale, dqt[dh][4 * gg + 3] * scale));
+  }
+}
+
 }  // namespace
 }  // namespace va
 
@@ -242,4 +601,41 @@ extern "C" int va_flash_attn_fwd(const void *q, const void *k, const void *v, co
                      static_cast<const uint16_t *>(k), static_cast<const uint16_t *>(v), cu_seqlens, block_table,
                      max_len, static_cast<int>(Hq), static_cast<int>(Hk), scale, static_cast<uint16_t *>(o), lse);
   return check_launch("flash_attn_fwd");
+}
+
+extern "C" int va_flash_attn_bwd(const void *q, const void *k, const void *v, const void *o, const void *dout,
+                                 const float *lse, const int32_t *cu_seqlens, const int32_t *q_blocks,
+                                 int64_t n_q_blocks, const int32_t *k_blocks, int64_t n_k_blocks, int64_t T,
+                                 int64_t Hq, int64_t Hk, int64_t head_dim, int64_t max_len, float scale, float *delta,
+                                 float *partial, void *dq, void *dk, void *dv, void *stream) {
+  VA_CHECK_ARG(head_dim == D, "flash_attn_bwd: head_dim must be 64");
+  VA_CHECK_ARG(Hq > 0 && Hk > 0 && Hq % Hk == 0, "flash_attn_bwd: Hq must be a multiple of Hk");
+  VA_CHECK_ARG(T >= 0 && n_q_blocks >= 0 && n_k_blocks >= 0 && max_len >= 0, "flash_attn_bwd: bad sizes");
+  if (n_q_blocks == 0 || T == 0) return VA_OK;
+  VA_CHECK_ARG(q && k && v && o && dout && lse && cu_seqlens && q_blocks && k_blocks && delta && partial && dq && dk &&
+                   dv,
+               "null pointer argument");
+  float *pdk = partial, *pdv = partial + Hq * T * D;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(flash_bwd_delta_kernel, dim3(static_cast<unsigned>(n_q_blocks), static_cast<unsigned>(Hq)),
+                     dim3(128), 0, s, static_cast<const uint16_t *>(o), static_cast<const uint16_t *>(dout),
+                     cu_seqlens, q_blocks, max_len, static_cast<int>(Hq), delta);
+  hipLaunchKernelGGL(flash_bwd_dkdv_kernel, dim3(static_cast<unsigned>(n_k_blocks), static_cast<unsigned>(Hq)),
+                     dim3(256), 0, s, static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(k),
+                     static_cast<const uint16_t *>(v), static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens,
+                     k_blocks, max_len, T, static_cast<int>(Hq), static_cast<int>(Hk), scale, pdk, pdv);
+  {
+    const int64_t granules = T * Hk * (D / 4);
+    int64_t grid = (granules + 255) / 256;
+    if (grid > 16384) grid = 16384;
+    hipLaunchKernelGGL(flash_bwd_group_sum_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0, s, pdk, pdv, T,
+                       static_cast<int>(Hq), static_cast<int>(Hk), static_cast<uint16_t *>(dk),
+                       static_cast<uint16_t *>(dv));
+  }
+  hipLaunchKernelGGL(flash_bwd_dq_kernel, dim3(static_cast<unsigned>(n_q_blocks), static_cast<unsigned>(Hq)),
+                     dim3(256), 0, s, static_cast<const uint16_t *>(k), static_cast<const uint16_t *>(v),
+                     static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens,
+                     q_blocks, max_len, static_cast<int>(Hq), static_cast<int>(Hk), scale,
+                     static_cast<uint16_t *>(dq));
+  return check_launch("flash_attn_bwd");
 }

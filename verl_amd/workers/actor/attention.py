@@ -60,12 +60,32 @@ def flash_block_table(cu_host) -> "np.ndarray":
     return np.stack([seqs[order], starts[order]], axis=1).astype(np.int32)
 
 
+FLASH_KB = 128  # keys per workgroup of the dK / dV kernel
+
+
+def flash_key_block_table(cu_host) -> "np.ndarray":
+    """(sequence, first key) of every 128-key block, earliest (heaviest under the causal mask)
+    blocks first."""
+    import numpy as np
+
+    cu_host = np.asarray(cu_host, dtype=np.int64)
+    lens = np.diff(cu_host)
+    seqs = np.repeat(np.arange(len(lens)), (lens + FLASH_KB - 1) // FLASH_KB)
+    starts = np.concatenate([np.arange(0, n, FLASH_KB) for n in lens]) if len(lens) else np.zeros(0, np.int64)
+    order = np.lexsort((seqs, starts))
+    return np.stack([seqs[order], starts[order]], axis=1).astype(np.int32)
+
+
+# backward implementation: "gfx950" (va_flash_attn_bwd) or "aten" (AOTriton flash backward)
+FLASH_BWD = "gfx950"
+
+
 class _FlashVarlen(torch.autograd.Function):
-    """Forward: va_flash_attn_fwd (gfx950 MFMA kernel). Backward: aten._flash_attention_backward
-    with this forward's O and LSE (the same tensors PyTorch's own varlen path hands it)."""
+    """Forward: va_flash_attn_fwd (gfx950 MFMA kernel). Backward: va_flash_attn_bwd (delta, dK/dV,
+    dQ kernels), or aten._flash_attention_backward fed with this forward's O and LSE."""
 
     @staticmethod
-    def forward(ctx, q, k, v, cu, blocks, max_len, scale):
+    def forward(ctx, q, k, v, cu, blocks, max_len, scale, kblocks=None):
         from ... import _lib as L
         from ... import kernels as K
 
@@ -76,27 +96,42 @@ class _FlashVarlen(torch.autograd.Function):
         lse = torch.zeros(cu.shape[0] - 1, hq, int(max_len), dtype=torch.float32, device=q.device)
         L.call("va_flash_attn_fwd", K._p(q), K._p(k), K._p(v), K._p(cu), K._p(blocks), blocks.shape[0], T, hq, hk, d,
                int(max_len), float(scale), K._p(o), K._p(lse), K._stream(q))
-        ctx.save_for_backward(q, k, v, o, lse, cu)
+        ctx.save_for_backward(q, k, v, o, lse, cu, blocks, kblocks if kblocks is not None else blocks)
+        ctx.has_kblocks = kblocks is not None
         ctx.max_len = int(max_len)
         ctx.scale = float(scale)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, o, lse, cu = ctx.saved_tensors
+        q, k, v, o, lse, cu, blocks, kblocks = ctx.saved_tensors
+        do = do.contiguous()
+        if FLASH_BWD == "gfx950" and ctx.has_kblocks:
+            from ... import _lib as L
+            from ... import kernels as K
+
+            T, hq, d = q.shape
+            hk = k.shape[1]
+            dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+            delta = torch.zeros_like(lse)
+            partial = torch.empty(2 * hq * T * d, dtype=torch.float32, device=q.device)
+            L.call("va_flash_attn_bwd", K._p(q), K._p(k), K._p(v), K._p(o), K._p(do), K._p(lse), K._p(cu),
+                   K._p(blocks), blocks.shape[0], K._p(kblocks), kblocks.shape[0], T, hq, hk, d, ctx.max_len,
+                   ctx.scale, K._p(delta), K._p(partial), K._p(dq), K._p(dk), K._p(dv), K._stream(q))
+            return dq, dk, dv, None, None, None, None, None
         rng = torch.zeros(2, dtype=torch.uint64, device=q.device)
         unused = torch.empty(0, device=q.device)
         dq, dk, dv = torch.ops.aten._flash_attention_backward(
-            do.contiguous(), q, k, v, o, lse, cu, cu, ctx.max_len, ctx.max_len, 0.0, True, rng, unused,
-            scale=ctx.scale)
-        return dq, dk, dv, None, None, None, None
+            do, q, k, v, o, lse, cu, cu, ctx.max_len, ctx.max_len, 0.0, True, rng, unused, scale=ctx.scale)
+        return dq, dk, dv, None, None, None, None, None
 
 
-def flash_attention(q, k, v, cu, max_len, blocks, scaling=None):
-    """Causal varlen attention on packed [T, H, 64] bf16 tensors with the gfx950 forward kernel.
-    ``blocks`` = device int32 [n, 2] from flash_block_table."""
+def flash_attention(q, k, v, cu, max_len, blocks, scaling=None, kblocks=None):
+    """Causal varlen attention on packed [T, H, 64] bf16 tensors with the gfx950 kernels.
+    ``blocks`` = device int32 [n, 2] from flash_block_table; ``kblocks`` from
+    flash_key_block_table enables the gfx950 backward (else aten's)."""
     scale = q.shape[-1] ** -0.5 if scaling is None else scaling
-    return _FlashVarlen.apply(q.contiguous(), k.contiguous(), v.contiguous(), cu, blocks, max_len, scale)
+    return _FlashVarlen.apply(q.contiguous(), k.contiguous(), v.contiguous(), cu, blocks, max_len, scale, kblocks)
 
 
 def flash_supported(q, k) -> bool:

@@ -60,6 +60,7 @@ class _Packing:
     sel_hidden: torch.Tensor  # [n_sel] rows of the packed hidden states that predict a response token
     sel_out: torch.Tensor  # [n_sel] flat index into [B*R]
     attn_blocks: torch.Tensor = None  # [n, 2] int32 (sequence, first query row) for va_flash_attn_fwd
+    attn_kblocks: torch.Tensor = None  # [n, 2] int32 (sequence, first key) for va_flash_attn_bwd
 
 
 def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device) -> _Packing:
@@ -90,6 +91,7 @@ def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device) -> _Packing:
         sel_hidden=dev(sel_hidden, np.int64),
         sel_out=dev(sel_out, np.int64),
         attn_blocks=dev(attention.flash_block_table(cu), np.int32),
+        attn_kblocks=dev(attention.flash_key_block_table(cu), np.int32),
     )
 
 
@@ -154,8 +156,10 @@ class DataParallelPPOActor(BasePPOActor):
                 if self._fused_backbone:
                     from .qwen2_fused import packed_forward
 
+                    fa = self.fused_attention
                     hidden = packed_forward(self._backbone, ids[0], pos[0], packing.cu_seqlens, packing.max_seqlen,
-                                            attn_blocks=packing.attn_blocks if self.fused_attention else None)
+                                            attn_blocks=packing.attn_blocks if fa else None,
+                                            attn_kblocks=packing.attn_kblocks if fa else None)
                 else:
                     out = self._backbone(
                         input_ids=ids, position_ids=pos, attention_mask=_NO_MASK, use_cache=False,

@@ -85,19 +85,19 @@ def _merged_linear(module, key: str, x, linears: list):
     return K.merged_linear(x, w_all, b_all, ws, bs)
 
 
-def _attention(attn, y, cos, sin, cu, max_len, hq, hk, d, attn_blocks=None):
+def _attention(attn, y, cos, sin, cu, max_len, hq, hk, d, attn_blocks=None, attn_kblocks=None):
     T = y.shape[0]
     qkv = _merged_linear(attn, "qkv", y, [attn.q_proj, attn.k_proj, attn.v_proj])
     q, k, v = K.rope_qkv(qkv, cos, sin, hq, hk, d)
     if attn_blocks is not None and attention.flash_supported(q, k):
-        out = attention.flash_attention(q, k, v, cu, max_len, attn_blocks, scaling=attn.scaling)
+        out = attention.flash_attention(q, k, v, cu, max_len, attn_blocks, scaling=attn.scaling, kblocks=attn_kblocks)
     else:
         out = attention.packed_attention(q, k, v, cu, max_len, scaling=attn.scaling)
     return attn.o_proj(out.reshape(T, hq * d))
 
 
 def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor, cu_seqlens: torch.Tensor,
-                   max_seqlen: int, attn_blocks: torch.Tensor = None) -> torch.Tensor:
+                   max_seqlen: int, attn_blocks: torch.Tensor = None, attn_kblocks: torch.Tensor = None) -> torch.Tensor:
     """input_ids / position_ids [T] (packed), cu_seqlens [B+1] int32 -> last hidden state [T, H] bf16
     (after the final norm), i.e. Qwen2Model(...).last_hidden_state[0] on the same packing."""
     cfg = backbone.config
@@ -115,7 +115,7 @@ def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor
             y = K.rmsnorm(residual, ln.weight, ln.variance_epsilon)
         else:
             residual, y = K.add_rmsnorm(h, residual, ln.weight, ln.variance_epsilon)
-        a = _attention(layer.self_attn, y, cos, sin, cu_seqlens, max_seqlen, hq, hk, d, attn_blocks)
+        a = _attention(layer.self_attn, y, cos, sin, cu_seqlens, max_seqlen, hq, hk, d, attn_blocks, attn_kblocks)
         ln = layer.post_attention_layernorm
         residual, y = K.add_rmsnorm(a, residual, ln.weight, ln.variance_epsilon)
         mlp = layer.mlp

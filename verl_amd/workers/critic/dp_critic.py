@@ -80,9 +80,10 @@ class DataParallelPPOCritic(BasePPOCritic):
                 if self._fused_backbone:
                     from ..actor.qwen2_fused import packed_forward
 
-                    blocks = packing.attn_blocks if self.config.get("fused_attention", True) else None
+                    fa = self.config.get("fused_attention", True)
                     hidden = packed_forward(self._backbone, ids, pos, packing.cu_seqlens, packing.max_seqlen,
-                                            attn_blocks=blocks)
+                                            attn_blocks=packing.attn_blocks if fa else None,
+                                            attn_kblocks=packing.attn_kblocks if fa else None)
                 else:
                     out = self._backbone(
                         input_ids=ids.unsqueeze(0), position_ids=pos.unsqueeze(0), attention_mask=_NO_MASK,
