@@ -249,3 +249,19 @@ def test_fused_worker_training_tracks_master_weights():
     assert moved > 1e-3, "weights did not change: the master copy-back missed the merged buffers"
     for a, b in zip(lps[True], lps[False]):
         assert torch.allclose(a[m], b[m], atol=5e-2, rtol=2e-2), (a[m] - b[m]).abs().max().item()
+
+
+@pytest.mark.parametrize("n_out,n_in", [(1152, 896), (896, 4864)])
+def test_splitk_weight_grad(n_out, n_in):
+    """Split-K weight gradient (two K halves, fp32 batched GEMM, one rounding) vs one GEMM in fp32."""
+    from verl_amd import kernels as K
+
+    torch.manual_seed(n_out)
+    T = 8192
+    dy = torch.randn(T, n_out, device=DEV).to(torch.bfloat16)
+    x = torch.randn(T, n_in, device=DEV).to(torch.bfloat16)
+    got = K.weight_grad(dy, x)
+    want = dy.float().t() @ x.float()
+    _grad_close(got, want, "split-K dW", rtol=5e-3)
+    base = (dy.t() @ x).float()
+    assert (got.float() - want).norm() <= 1.5 * (base - want).norm() + 1e-3

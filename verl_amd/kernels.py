@@ -720,12 +720,35 @@ class _MergedLinear(torch.autograd.Function):
         dx = dy @ w_all
         x2 = x.reshape(-1, x.shape[-1])
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dw = dy2.t() @ x2
+        dw = weight_grad(dy2, x2)
         grads = list(torch.split(dw, ctx.w_rows, dim=0))
         if ctx.has_b:
             db = dy2.sum(0)
             grads += list(torch.split(db, ctx.w_rows, dim=0))
         return (dx, None, None, None, *grads)
+
+
+# weight gradients dW = dY^T X whose output has few 256 x 256 tiles (q|k|v, o, down at H = 896)
+# leave most CUs idle in one GEMM; two K-halves as a batched GEMM with fp32 output, summed in fp32
+# and rounded once, fill the chip (tools/wgrad_bench.py: 1.2-1.3x on those shapes).
+WGRAD_SPLITK_MAX_ELEMS = 6_000_000
+WGRAD_SPLITK_MIN_TOKENS = 4096
+
+
+def weight_grad(dy2, x2):
+    T, n_out = dy2.shape
+    n_in = x2.shape[1]
+    if (dy2.is_cuda and T >= WGRAD_SPLITK_MIN_TOKENS and T % 2 == 0 and n_out * n_in <= WGRAD_SPLITK_MAX_ELEMS
+            and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16):
+        h = T // 2
+        part = torch.bmm(dy2.view(2, h, n_out).transpose(1, 2), x2.reshape(2, h, n_in), out_dtype=torch.float32)
+        return (part[0] + part[1]).to(dy2.dtype)
+    return dy2.t() @ x2
+
+
+def linear(x, weight):
+    """F.linear(x, weight) (no bias) with the split-K weight gradient above."""
+    return _MergedLinear.apply(x, weight.detach(), None, 1, weight)
 
 
 def merged_linear(x, w_all, b_all, weights: list, biases: list | None = None):

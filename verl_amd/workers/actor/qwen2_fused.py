@@ -93,7 +93,10 @@ def _attention(attn, y, cos, sin, cu, max_len, hq, hk, d, attn_blocks=None, attn
         out = attention.flash_attention(q, k, v, cu, max_len, attn_blocks, scaling=attn.scaling, kblocks=attn_kblocks)
     else:
         out = attention.packed_attention(q, k, v, cu, max_len, scaling=attn.scaling)
-    return attn.o_proj(out.reshape(T, hq * d))
+    o = attn.o_proj
+    if o.bias is None:
+        return K.linear(out.reshape(T, hq * d), o.weight)
+    return o(out.reshape(T, hq * d))
 
 
 def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor, cu_seqlens: torch.Tensor,
@@ -120,7 +123,9 @@ def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor
         residual, y = K.add_rmsnorm(a, residual, ln.weight, ln.variance_epsilon)
         mlp = layer.mlp
         gu = _merged_linear(mlp, "gate_up", y, [mlp.gate_proj, mlp.up_proj])
-        h = mlp.down_proj(K.swiglu_merged(gu))
+        dp = mlp.down_proj
+        a = K.swiglu_merged(gu)
+        h = K.linear(a, dp.weight) if dp.bias is None else dp(a)
     norm = backbone.norm
     if h is None:
         return K.rmsnorm(residual, norm.weight, norm.variance_epsilon)
