@@ -32,6 +32,7 @@ constexpr int QB = 128;  // query rows per workgroup
 constexpr int KB = 64;   // keys per staged block
 constexpr float kLog2e_ = 1.4426950408889634f;
 constexpr float kLn2_ = 0.69314718055994531f;
+constexpr float kDeferLog2 = 8.f;  // forward: defer the O rescale until the max grows by 2^8
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -135,7 +136,10 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
           sacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[t], 0, 0, 0);
         }
       }
-      // ---- online softmax over the block (base 2); masks only on diagonal / sequence-end blocks
+      // ---- online softmax over the block (base 2); masks only on diagonal / sequence-end blocks.
+      // The running max m is kept on the RAW scores (c > 0), p = exp2(fma(S, c, -m c)) is one FMA
+      // + one exp per score, and O / l are rescaled only when the max grows by more than
+      // kDeferLog2 / c (p <= 2^kDeferLog2 meanwhile; l and O see the same factor: exact).
       const bool need_mask = (key0 + KB - 1 > qs + wave * 32) || (key0 + KB - 1 >= len);
       float x[32];
       float tm = -INFINITY;
@@ -143,7 +147,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float xv = sacc[t][r] * c;
+          float xv = sacc[t][r];
           if (need_mask) {
             const int kp = key0 + t * 32 + crow(r, h);
             if (kp > q_pos || kp >= len) xv = -INFINITY;
@@ -152,25 +156,27 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
           tm = fmaxf(tm, xv);
         }
       tm = fmaxf(tm, __shfl_xor(tm, 32, kWave));
-      const float mn = fmaxf(m, tm);
-      const float msafe = mn == -INFINITY ? 0.f : mn;
-      float rs = 0.f;
-#pragma unroll
-      for (int r = 0; r < 32; ++r) {
-        x[r] = __builtin_amdgcn_exp2f(x[r] - msafe);
-        rs += x[r];
-      }
-      rs += __shfl_xor(rs, 32, kWave);
-      if (mn != m) {  // rescale only rows whose max moved (all-lane uniform skip is common later on)
-        const float alpha = __builtin_amdgcn_exp2f(m - msafe);  // m = -inf -> 0
+      if (tm > m + kDeferLog2 / c) {  // per-lane; O / l rescaled only on these rows
+        const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - tm) * c);
         l *= alpha;
 #pragma unroll
         for (int dh = 0; dh < 2; ++dh)
 #pragma unroll
           for (int r = 0; r < 16; ++r) oacc[dh][r] *= alpha;
+        m = tm;
       }
+      const float nmc = m == -INFINITY ? 0.f : -m * c;
+      float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 32; r += 2) {
+        x[r] = __builtin_amdgcn_exp2f(fmaf(x[r], c, nmc));
+        x[r + 1] = __builtin_amdgcn_exp2f(fmaf(x[r + 1], c, nmc));
+        rs0 += x[r];
+        rs1 += x[r + 1];
+      }
+      float rs = rs0 + rs1;
+      rs += __shfl_xor(rs, 32, kWave);
       l += rs;
-      m = mn;
       // ---- O^T += V^T P^T over 4 k-steps of 16 keys; P^T = S^T registers 8s..8s+7 as bf16
       //      (k order permuted, guide §3); V^T fragment element j <-> key 16 s + 8 (j >> 2) + 4 h + (j & 3)
       const int g16 = lane >> 4, li = lane & 15;
@@ -217,7 +223,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
         *reinterpret_cast<uint2 *>(orow + dh * 32 + 8 * g + 4 * h) = make_uint2(w0, w1);
       }
     if (h == 0)
-      lse[(static_cast<int64_t>(seq) * Hq + head) * lse_ld + q_pos] = (m + __builtin_amdgcn_logf(l)) * kLn2_;
+      lse[(static_cast<int64_t>(seq) * Hq + head) * lse_ld + q_pos] = (m * c + __builtin_amdgcn_logf(l)) * kLn2_;
   }
 }
 
@@ -389,13 +395,13 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qr = crow(r, h);
-        float pv = __builtin_amdgcn_exp2f(sacc[r] * c - lse2[qr]);
+        float pv = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2[qr]));
         if (need_mask) {
           const int qp = qt0 + qr;
           if (key > qp || qp >= len || key >= len) pv = 0.f;
         }
         p[r] = pv;
-        ds[r] = pv * (pacc[r] - dlt[qr]);
+        ds[r] = pv * (pacc[r] - dlt[qr]);  // (dP - delta) * p
       }
       // dV^T += dO^T P, dK^T += Q^T dS  (k = queries, permuted order of the accumulator rows)
 #pragma unroll
@@ -550,7 +556,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
       float ds[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float pv = __builtin_amdgcn_exp2f(sacc[r] * c - lse2);
+        float pv = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2));
         if (need_mask) {
           const int kp = key0 + crow(r, h);
           if (kp > q_pos || kp >= len) pv = 0.f;
