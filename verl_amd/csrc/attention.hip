@@ -53,7 +53,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
     const int32_t *__restrict__ cu, const int32_t *__restrict__ blocks, int64_t lse_ld, int Hq, int Hk,
     float scale, uint16_t *__restrict__ o, float *__restrict__ lse) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * KB * D];  // [buf][K | V][64 keys][64 d]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, ql = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ql = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
   const int seq = blocks[2 * blockIdx.x], qs = blocks[2 * blockIdx.x + 1];
   const int head = blockIdx.y, kvh = head / (Hq / Hk);
   const int s0 = cu[seq], len = cu[seq + 1] - s0;
@@ -87,14 +88,12 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
     for (int u = 0; u < 2; ++u) {
       const int idx = tid + u * 256, r = idx >> 3, ch = idx & 7;
       const int key = kb * KB + r;
-      if (key < len) {
-        const int64_t base = (s0 + key) * ldk + kvh * D + ch * 8;
-        sk[u] = *reinterpret_cast<const uint4 *>(k + base);
-        sv[u] = *reinterpret_cast<const uint4 *>(v + base);
-      } else {
-        sk[u] = make_uint4(0, 0, 0, 0);
-        sv[u] = make_uint4(0, 0, 0, 0);
-      }
+      const bool ok = key < len;
+      const int64_t base = (s0 + (ok ? key : len - 1)) * ldk + kvh * D + ch * 8;  // clamped: no branch
+      const uint4 a = *reinterpret_cast<const uint4 *>(k + base);
+      const uint4 b = *reinterpret_cast<const uint4 *>(v + base);
+      sk[u] = ok ? a : make_uint4(0, 0, 0, 0);
+      sv[u] = ok ? b : make_uint4(0, 0, 0, 0);
     }
   };
   auto store_block = [&](int buf) {
@@ -142,19 +141,25 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
       // kDeferLog2 / c (p <= 2^kDeferLog2 meanwhile; l and O see the same factor: exact).
       const bool need_mask = (key0 + KB - 1 > qs + wave * 32) || (key0 + KB - 1 >= len);
       float x[32];
-      float tm = -INFINITY;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float xv = sacc[t][r];
-          if (need_mask) {
-            const int kp = key0 + t * 32 + crow(r, h);
-            if (kp > q_pos || kp >= len) xv = -INFINITY;
-          }
-          x[16 * t + r] = xv;
-          tm = fmaxf(tm, xv);
-        }
+        for (int r = 0; r < 16; ++r) x[16 * t + r] = sacc[t][r];
+      if (need_mask) {  // wave-uniform: one scalar branch; key offset vs. a per-lane limit
+        const int lim = min(q_pos, len - 1) - key0 - 4 * h;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            x[16 * t + r] = (t * 32 + crow(r, 0) > lim) ? -INFINITY : x[16 * t + r];
+      }
+      float tm0 = x[0], tm1 = x[1];  // two independent max chains
+#pragma unroll
+      for (int r = 2; r < 32; r += 2) {
+        tm0 = fmaxf(tm0, x[r]);
+        tm1 = fmaxf(tm1, x[r + 1]);
+      }
+      float tm = fmaxf(tm0, tm1);
       tm = fmaxf(tm, __shfl_xor(tm, 32, kWave));
       if (tm > m + kDeferLog2 / c) {  // per-lane; O / l rescaled only on these rows
         const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - tm) * c);
@@ -297,7 +302,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   // [buf][Q image 32x64 | dO image 32x64] bf16, then [buf][lse2 32 | delta 32] fp32
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * QT * D + 2 * 2 * QT * 2];
   float *rowc = reinterpret_cast<float *>(lds + 2 * 2 * QT * D);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, kl = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, kl = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
   const int seq = kblocks[2 * blockIdx.x], kb0 = kblocks[2 * blockIdx.x + 1];
   const int hq0 = blockIdx.y, g = hq0 / (Hq / Hk);  // one query head; its partial dK / dV
   const int s0 = cu[seq], len = cu[seq + 1] - s0;
@@ -338,13 +344,13 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
     StageQ st;
     const int hq = hq0, qt0 = qfirst + it * QT;
     const int r = tid >> 3, ch = tid & 7, qp = qt0 + r;
-    if (qp < len) {
-      const int64_t base = (s0 + qp) * ldq + hq * D + ch * 8;
-      st.q = *reinterpret_cast<const uint4 *>(q + base);
-      st.d = *reinterpret_cast<const uint4 *>(dout + base);
-    } else {
-      st.q = make_uint4(0, 0, 0, 0);
-      st.d = st.q;
+    {
+      const bool ok = qp < len;
+      const int64_t base = (s0 + (ok ? qp : len - 1)) * ldq + hq * D + ch * 8;  // clamped: no branch
+      const uint4 a = *reinterpret_cast<const uint4 *>(q + base);
+      const uint4 b = *reinterpret_cast<const uint4 *>(dout + base);
+      st.q = ok ? a : make_uint4(0, 0, 0, 0);
+      st.d = ok ? b : make_uint4(0, 0, 0, 0);
     }
     st.rc = 0.f;
     if (tid < 2 * QT) {
@@ -393,16 +399,16 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
       const bool need_mask = (qt0 < k0 + 31) || (qt0 + QT > len) || (k0 + 32 > len);
       float p[16], ds[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qr = crow(r, h);
-        float pv = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2[qr]));
-        if (need_mask) {
-          const int qp = qt0 + qr;
-          if (key > qp || qp >= len || key >= len) pv = 0.f;
-        }
-        p[r] = pv;
-        ds[r] = pv * (pacc[r] - dlt[qr]);  // (dP - delta) * p
+      for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2[crow(r, h)]));
+      if (need_mask) {  // wave-uniform branch; live rows: key <= q < len, as one unsigned range test
+        const int lo = key - qt0 - 4 * h;
+        const unsigned span = key < len ? static_cast<unsigned>(len - key) : 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          p[r] = static_cast<unsigned>(crow(r, 0) - lo) >= span ? 0.f : p[r];
       }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ds[r] = p[r] * (pacc[r] - dlt[crow(r, h)]);  // (dP - delta) * p
       // dV^T += dO^T P, dK^T += Q^T dS  (k = queries, permuted order of the accumulator rows)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -468,7 +474,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
     const int32_t *__restrict__ cu, const int32_t *__restrict__ blocks, int64_t ld, int Hq, int Hk, float scale,
     uint16_t *__restrict__ dq) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * KB * D];  // [buf][K | V][64 keys][64 d], swizzled
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, ql = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ql = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
   const int seq = blocks[2 * blockIdx.x], qs = blocks[2 * blockIdx.x + 1];
   const int head = blockIdx.y, kvh = head / (Hq / Hk);
   const int s0 = cu[seq], len = cu[seq + 1] - s0;
@@ -505,14 +512,12 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
     for (int u = 0; u < 2; ++u) {
       const int idx = tid + u * 256, r = idx >> 3, ch = idx & 7;
       const int kk = kb * KB + r;
-      if (kk < len) {
-        const int64_t base = (s0 + kk) * ldk + kvh * D + ch * 8;
-        sk[u] = *reinterpret_cast<const uint4 *>(k + base);
-        sv[u] = *reinterpret_cast<const uint4 *>(v + base);
-      } else {
-        sk[u] = make_uint4(0, 0, 0, 0);
-        sv[u] = make_uint4(0, 0, 0, 0);
-      }
+      const bool ok = kk < len;
+      const int64_t base = (s0 + (ok ? kk : len - 1)) * ldk + kvh * D + ch * 8;  // clamped: no branch
+      const uint4 a = *reinterpret_cast<const uint4 *>(k + base);
+      const uint4 b = *reinterpret_cast<const uint4 *>(v + base);
+      sk[u] = ok ? a : make_uint4(0, 0, 0, 0);
+      sv[u] = ok ? b : make_uint4(0, 0, 0, 0);
     }
   };
   auto store_block = [&](int buf) {
@@ -555,14 +560,14 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
       const bool need_mask = (key0 + 31 > qs + wave * 32) || (key0 + 31 >= len);
       float ds[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float pv = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2));
-        if (need_mask) {
-          const int kp = key0 + crow(r, h);
-          if (kp > q_pos || kp >= len) pv = 0.f;
-        }
-        ds[r] = pv * (pacc[r] - dlt);
+      for (int r = 0; r < 16; ++r) ds[r] = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2));
+      if (need_mask) {  // wave-uniform branch; key offset vs. a per-lane limit
+        const int lim = min(q_pos, len - 1) - key0 - 4 * h;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ds[r] = crow(r, 0) > lim ? 0.f : ds[r];
       }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ds[r] *= pacc[r] - dlt;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const bf16x8 db = pack_frag(ds + 8 * s);
