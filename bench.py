@@ -63,7 +63,8 @@ def parse():
     ap.add_argument("--no-mixed-precision", action="store_true", help="fp32 weights + autocast instead of bf16/fp32-master")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--cpu-sample-rows", type=int, default=2048)
+    ap.add_argument("--cpu-sample-rows", type=int, default=24576,
+                    help="response tokens of the CPU baseline's log-prob sample (~10 s on 16 cores)")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     return ap.parse_args()
 
@@ -94,15 +95,21 @@ def cpu_baseline(args, rank) -> dict | None:
     # the box grants a CPU share (OMP_NUM_THREADS=16 there) although affinity lists every host CPU
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(len(os.sched_getaffinity(0)), 16)
     torch.set_num_threads(cores)
-    V, rows = 151936, args.cpu_sample_rows
+    V = 151936
+    chunk = min(args.cpu_sample_rows, 2048)  # one 1.2 GB fp32 logits buffer, reused per chunk
+    n_chunks = max(1, args.cpu_sample_rows // chunk)
+    rows = chunk * n_chunks
     g = torch.Generator().manual_seed(0)
-    logits = torch.randn(rows, V, generator=g) * 2
-    labels = torch.randint(0, V, (rows,), generator=g)
-    t0 = time.perf_counter()
-    lp = ref.logprobs_from_logits(logits, labels)
-    ent = ref.entropy_from_logits(logits)
-    t_lp = time.perf_counter() - t0
-    del logits, lp, ent
+    logits = torch.randn(chunk, V, generator=g) * 2
+    t_lp = 0.0
+    for _ in range(n_chunks):
+        labels = torch.randint(0, V, (chunk,), generator=g)
+        t0 = time.perf_counter()
+        lp = ref.logprobs_from_logits(logits, labels)
+        ent = ref.entropy_from_logits(logits)
+        t_lp += time.perf_counter() - t0
+        del lp, ent
+    del logits
     B, R, n = args.prompts * args.n, args.response_len, args.n
     rewards = torch.zeros(B, R)
     rewards[:, -1] = torch.randint(0, 2, (B,), generator=g).float()
@@ -123,7 +130,7 @@ def cpu_baseline(args, rank) -> dict | None:
         "unit": "tokens/s",
         "cores": cores,
         "kind": "port",
-        "sample": (f"oracle log-prob+entropy fwd of {rows} tokens x V={V} fp32 ({t_lp:.2f}s) + GRPO adv + "
+        "sample": (f"oracle log-prob+entropy fwd of {rows} tokens ({n_chunks} x {chunk}) x V={V} fp32 ({t_lp:.2f}s) + GRPO adv + "
                    f"clipped loss + k3 KL fwd/bwd on {B}x{R} ({t_algo:.2f}s); model GEMMs excluded"),
     }
 

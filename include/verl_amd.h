@@ -114,13 +114,16 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
                            void *stream);
 
 /* Launch-shape knobs of the log-prob kernels (results are identical for every setting):
- *   VA_TUNE_FWD/BWD_WAVES_PER_ROW: 0 = auto, 1 / 2 / 4 waves stream one row together;
+ *   VA_TUNE_FWD_WAVES_PER_ROW: 0 = auto, 1 / 2 / 4 waves stream one row together;
+ *   VA_TUNE_BWD_WAVES_PER_ROW: accepted, no effect (the backward is a flat chunk stream);
  *   VA_TUNE_NONTEMPORAL: 1 = non-temporal (streaming) loads/stores of the logits (default),
- *   0 = default cache policy. */
+ *   0 = default cache policy;
+ *   VA_TUNE_PIPELINE: fwd 0: 4 vectors/lane, 1: 2+2 software-pipelined, 2: 4+4 pipelined;
+ *   bwd 16-B vectors per lane per workgroup chunk 0: 4, 1: 2, 2: 8. */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3
-#define VA_TUNE_PIPELINE 4 /* 0: 4 vectors/lane; 1: 2+2 software-pipelined; 2: 4+4 pipelined */
+#define VA_TUNE_PIPELINE 4
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

@@ -18,6 +18,8 @@
 
 #include <math.h>
 
+#include <type_traits>
+
 #include "va_common.h"
 
 namespace va {
@@ -342,20 +344,22 @@ __global__ __launch_bounds__(256, 8) void logprob_entropy_fwd_kernel(
 }
 
 // ---- backward --------------------------------------------------------------------------
-template <typename T, bool SCALE, bool VECTOR, int WPR, bool NT, int U, bool PIPE>
-__global__ __launch_bounds__(256, 8) void logprob_entropy_bwd_kernel(
+// The gradient is elementwise once the row's (lse, H, g_lp, g_H, label) are known, so the
+// backward is a flat stream: workgroup b = chunk b % chunks_per_row of row b / chunks_per_row,
+// 256 lanes x U x 16 B contiguous, loaded at once, written once. Workgroups in flight therefore
+// sweep a contiguous address range (as a copy does) instead of thousands of rows at once: on
+// MI355X this moves read+write from 5.2 to ~5.8 TB/s (tools/hbm_stream.hip calibration).
+template <typename T, bool SCALE, bool VECTOR, bool NT, int U>
+__global__ __launch_bounds__(256) void logprob_entropy_bwd_kernel(
     const float *__restrict__ g_logp, const float *__restrict__ g_ent, const T *logits,
-    int64_t n_rows, int64_t V, int64_t stride, const int64_t *__restrict__ labels,
-    const float *__restrict__ lse_in, const float *__restrict__ ent_in, float temperature,
-    T *dlogits, int64_t dstride) {
+    int64_t V, int64_t stride, const int64_t *__restrict__ labels, const float *__restrict__ lse_in,
+    const float *__restrict__ ent_in, float temperature, T *dlogits, int64_t dstride,
+    int chunks_per_row) {
   using E = Elem<T>;
   constexpr int VEC = E::kVec;
-  constexpr int RPB = 4 / WPR;
-  constexpr int STEP = kWave * WPR;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int part = wave % WPR;
-  const int64_t row = static_cast<int64_t>(blockIdx.x) * RPB + wave / WPR;
-  if (row >= n_rows) return;  // no barrier below
+  constexpr int CH = 256 * U * VEC;  // elements per workgroup
+  const int64_t row = blockIdx.x / chunks_per_row;
+  const int64_t e0 = static_cast<int64_t>(blockIdx.x - row * chunks_per_row) * CH;
   const T *xr = logits + row * stride;
   T *dr = dlogits + row * dstride;
 
@@ -366,86 +370,78 @@ __global__ __launch_bounds__(256, 8) void logprob_entropy_bwd_kernel(
   const float lse = lse_in[row];
   const float h = (g_ent != nullptr) ? ent_in[row] : 0.f;
 
-  // dz_j = -p_j * (glp + gh * (log p_j + H)) + glp * [j == label];  dx = dz / T
-  auto grad = [&](float z, bool is_lab) -> float {
-    const float lp = z - lse;
-    const float p = __builtin_amdgcn_exp2f(lp * kLog2e);
-    float d = -p * fmaf(gh, lp + h, glp);
+  // dz_j = -p_j * (glp + gh * (log p_j + H)) + glp * [j == label];  dx = dz / T.
+  // With log p_j = z_j - lse:  p_j = 2^(z_j L - lse L),  glp + gh (log p_j + H) = gh z_j + kk,
+  // kk = gh (H - lse) + glp: 2 FMAs + 1 exp + 1 mul per element; the label term is added by the
+  // one lane whose vector holds it.
+  const float nlb = -lse * kLog2e;
+  const float kk = fmaf(gh, h - lse, glp);
+  auto grad = [&](float z) -> float {
+    const float p = __builtin_amdgcn_exp2f(fmaf(z, kLog2e, nlb));
+    return -p * fmaf(gh, z, kk);
+  };
+  auto finish = [&](float d, bool is_lab) -> float {
     if (is_lab) d += glp;
     if constexpr (SCALE) d = d / temperature;
     return d;
   };
 
-  int64_t tail_begin = 0;
   if constexpr (VECTOR) {
     const u32x4 *xv = reinterpret_cast<const u32x4 *>(xr);
     u32x4 *dv = reinterpret_cast<u32x4 *>(dr);
     const int64_t nvec = V / VEC;
+    const int64_t i0 = e0 / VEC + threadIdx.x;
     const int64_t lab_vec = has_lab ? lab / VEC : -1;
-    const int lab_k = has_lab ? static_cast<int>(lab % VEC) : -1;
-    int64_t i = static_cast<int64_t>(part) * kWave + lane;
-    auto emit = [&](const u32x4 *raw, int64_t at) {
+    // all U loads issued before any use; the row's partial last chunk clamps its addresses
+    // (duplicate in-row reads, no stores) so no load sits behind a branch
+    auto body = [&](auto partial) {
+      u32x4 raw[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int hit = (at + u * STEP == lab_vec) ? lab_k : -1;
+        if constexpr (decltype(partial)::value) raw[u] = vload<NT>(xv + min(i0 + u * 256, nvec - 1));
+        else raw[u] = vload<NT>(xv + i0 + u * 256);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + u * 256;
+        if (decltype(partial)::value && i >= nvec) continue;
         float x[VEC];
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
           float z = elem<T>(raw[u], k);
           if constexpr (SCALE) z = E::scale(z, temperature);
-          x[k] = grad(z, k == hit);
+          x[k] = grad(z);
         }
-        vstore<NT>(dv + at + u * STEP, pack_vec<T>(x));
+        if (i == lab_vec) {  // one lane of one workgroup per row
+          const int lk = static_cast<int>(lab - i * VEC);
+#pragma unroll
+          for (int k = 0; k < VEC; ++k)
+            if (k == lk) x[k] += glp;
+        }
+        if constexpr (SCALE) {
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) x[k] = x[k] / temperature;
+        }
+        vstore<NT>(dv + i, pack_vec<T>(x));
       }
     };
-    if constexpr (PIPE) {
-      // loads of the next U vectors are issued before the stores of the current U (they never
-      // touch the same addresses, also in place), so the wave does not stall on each load
-      if (i + (U - 1) * STEP < nvec) {
-        u32x4 cur[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) cur[u] = vload<NT>(xv + i + u * STEP);
-        while (true) {
-          const int64_t nx = i + U * STEP;
-          const bool more = nx + (U - 1) * STEP < nvec;
-          u32x4 nxt[U];
-          if (more) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) nxt[u] = vload<NT>(xv + nx + u * STEP);
-          }
-          emit(cur, i);
-          i = nx;
-          if (!more) break;
-#pragma unroll
-          for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-        }
-      }
-    } else {
-      for (; i + (U - 1) * STEP < nvec; i += U * STEP) {
-        u32x4 raw[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) raw[u] = vload<NT>(xv + i + u * STEP);
-        emit(raw, i);
-      }
-    }
-    for (; i < nvec; i += STEP) {
-      const u32x4 r = vload<NT>(xv + i);
-      const int hit = (i == lab_vec) ? lab_k : -1;
-      float x[VEC];
-#pragma unroll
-      for (int k = 0; k < VEC; ++k) {
-        float z = elem<T>(r, k);
+    if (e0 + CH <= nvec * VEC) body(std::false_type{});
+    else body(std::true_type{});
+    // V % VEC trailing elements: the row's last workgroup
+    if (e0 + CH >= V) {
+      for (int64_t j = nvec * VEC + threadIdx.x; j < V; j += 256) {
+        float z = E::load1(xr + j);
         if constexpr (SCALE) z = E::scale(z, temperature);
-        x[k] = grad(z, k == hit);
+        E::store1(dr + j, finish(grad(z), j == lab));
       }
-      vstore<NT>(dv + i, pack_vec<T>(x));
     }
-    tail_begin = nvec * VEC;
-  }
-  for (int64_t j = tail_begin + static_cast<int64_t>(part) * kWave + lane; j < V; j += STEP) {
-    float z = E::load1(xr + j);
-    if constexpr (SCALE) z = E::scale(z, temperature);
-    E::store1(dr + j, grad(z, j == lab));
+  } else {
+    const int64_t end = min(V, e0 + CH);
+    for (int64_t j = e0 + threadIdx.x; j < end; j += 256) {
+      float z = E::load1(xr + j);
+      if constexpr (SCALE) z = E::scale(z, temperature);
+      E::store1(dr + j, finish(grad(z), j == lab));
+    }
   }
 }
 
@@ -508,20 +504,22 @@ int launch_fwd(const void *logits, int64_t n_rows, int64_t V, int64_t stride,
   return check_launch("logprob_entropy_fwd");
 }
 
-template <typename T, bool S, bool VV, int W>
-void launch_bwd_w(const float *g_logp, const float *g_ent, const T *x, int64_t n_rows, int64_t V,
+template <typename T, bool S, bool VV>
+void launch_bwd_u(const float *g_logp, const float *g_ent, const T *x, int64_t n_rows, int64_t V,
                   int64_t stride, const int64_t *labels, const float *lse, const float *ent,
                   float temperature, T *d, int64_t dstride, hipStream_t stream, bool nt) {
-  const dim3 block(256);
-  const dim3 grid(static_cast<unsigned>((n_rows + (4 / W) - 1) / (4 / W)));
-#define VA_K(NTV, UU, PP)                                                                      \
-  hipLaunchKernelGGL((logprob_entropy_bwd_kernel<T, S, VV, W, NTV, UU, PP>), grid, block, 0, stream, \
-                     g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d, dstride)
-  const int pipe = VV ? g_pipe : 0;
+  // vectors per lane: 4 (default), 2 (VA_TUNE_PIPELINE = 1) or 8 (= 2)
+  const int u = g_pipe == 1 ? 2 : (g_pipe == 2 ? 8 : 4);
+  const int64_t ch = 256LL * u * Elem<T>::kVec;
+  const int cpr = static_cast<int>((V + ch - 1) / ch);
+  const dim3 block(256), grid(static_cast<unsigned>(n_rows * cpr));
+#define VA_K(NTV, UU)                                                                          \
+  hipLaunchKernelGGL((logprob_entropy_bwd_kernel<T, S, VV, NTV, UU>), grid, block, 0, stream, g_logp, g_ent, x, V, \
+                     stride, labels, lse, ent, temperature, d, dstride, cpr)
   if (nt) {
-    if (pipe == 1) VA_K(true, 2, true); else if (pipe == 2) VA_K(true, 4, true); else VA_K(true, 4, false);
+    if (u == 2) VA_K(true, 2); else if (u == 8) VA_K(true, 8); else VA_K(true, 4);
   } else {
-    if (pipe == 1) VA_K(false, 2, true); else if (pipe == 2) VA_K(false, 4, true); else VA_K(false, 4, false);
+    if (u == 2) VA_K(false, 2); else if (u == 8) VA_K(false, 8); else VA_K(false, 4);
   }
 #undef VA_K
 }
@@ -538,14 +536,9 @@ int launch_bwd(const float *g_logp, const float *g_ent, const void *logits, int6
                    ((stride * static_cast<int64_t>(sizeof(T))) % 16 == 0) &&
                    ((dstride * static_cast<int64_t>(sizeof(T))) % 16 == 0);
   const bool scale = (temperature != 1.0f);
-  const int w = auto_wpr(n_rows, V, g_bwd_wpr);
   const bool nt = g_nt != 0;  // auto (-1) and 1 both select non-temporal
-#define VA_BWD(S, VV)                                                                        \
-  do {                                                                                       \
-    if (w == 4) launch_bwd_w<T, S, VV, 4>(g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d, dstride, stream, nt); \
-    else if (w == 2) launch_bwd_w<T, S, VV, 2>(g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d, dstride, stream, nt); \
-    else launch_bwd_w<T, S, VV, 1>(g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d, dstride, stream, nt); \
-  } while (0)
+#define VA_BWD(S, VV) \
+  launch_bwd_u<T, S, VV>(g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d, dstride, stream, nt)
   if (scale) {
     if (vec) VA_BWD(true, true); else VA_BWD(true, false);
   } else {
@@ -599,6 +592,7 @@ extern "C" int va_logprob_entropy_bwd(const float *g_logp, const float *g_entrop
   VA_CHECK_ARG(g_entropy == nullptr || entropy != nullptr,
                "entropy is required when g_entropy is given");
   VA_CHECK_ARG(temperature > 0.f, "temperature must be > 0");
+  VA_CHECK_ARG(n_rows * ((vocab + 2047) / 2048) < (1LL << 31), "too many rows x vocab chunks for one launch");
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (dtype) {
     case VA_F32:
