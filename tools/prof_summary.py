@@ -30,10 +30,15 @@ def main(path):
     print(f"total kernel time {tot / 1e6:.1f} ms")
     for f, (t, c) in sorted(fam.items(), key=lambda kv: -kv[1][0]):
         print(f"  {f:34s} {t / 1e6:9.1f} ms  {100 * t / tot:5.1f}%  {c:7d} launches")
+    print("top 25 kernels:")
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
+        print(f"  {r['Name'][:70]:70s} {float(r['TotalDurationNs']) / 1e6:8.1f} ms calls {r['Calls']:>6s} avg {float(r['AverageNs']) / 1e3:8.1f} us")
     print("ours:")
     for r in rows:
         if family(r["Name"]) == "verl_amd HIP kernels":
-            n = re.sub(r"\(.*", "", r["Name"])[:90]
+            n = re.sub(r"^void ", "", r["Name"]).replace("(anonymous namespace)::", "")
+            n = re.sub(r"\(.*", "", n) or n
+            n = n[:90]
             print(f"  {n:90s} calls {r['Calls']:>6s} avg {float(r['AverageNs']) / 1e3:9.1f} us")
 
 
