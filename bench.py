@@ -47,6 +47,26 @@ def pmc_traffic(kernel: str, algo_bytes_per_launch: float, vocab: int):
     return k["traffic_bytes_per_row"] * rows, os.path.relpath(paths[-1], ROOT)
 
 
+def hbm_ceiling(kernel: str):
+    """Best plain-streaming rate measured on MI355X at the same footprint (tools/hbm_stream.hip,
+    profiles/r*/hbm_stream_*rows.jsonl): read-only for the forward, read+write for the backward."""
+    import glob
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "hbm_stream_*rows.jsonl")))
+    if not paths:
+        return None, None
+    mode = "read" if kernel.endswith("fwd") else "copy"
+    rows = [json.loads(line) for line in open(paths[-1]) if line.startswith("{")]
+    best = max((r["gbps"] for r in rows if r["mode"] == mode), default=None)
+    return best, os.path.relpath(paths[-1], ROOT)
+
+
+def _gemm_table_name():
+    from verl_amd.utils import gemm_tuning
+
+    return os.path.basename(gemm_tuning._loaded) if gemm_tuning._loaded else None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -56,8 +76,14 @@ def parse():
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--response-len", type=int, default=1024)
-    ap.add_argument("--micro", type=int, default=8, help="ppo_micro_batch_size_per_gpu (responses)")
-    ap.add_argument("--logprob-micro", type=int, default=16, help="log_prob_micro_batch_size_per_gpu")
+    ap.add_argument("--micro", type=int, default=64, help="ppo_micro_batch_size_per_gpu (responses)")
+    ap.add_argument("--logprob-micro", type=int, default=64, help="log_prob_micro_batch_size_per_gpu")
+    ap.add_argument("--dynamic-bsz", type=int, default=0,
+                    help="use_dynamic_bsz with this ppo_max_token_len_per_gpu (and log-prob budget); 0 = off")
+    ap.add_argument("--pad-multiple", type=int, default=2048,
+                    help="round packed micro-batches up to a multiple of this many tokens (pack_pad_multiple)")
+    ap.add_argument("--gemm-table", default="default",
+                    help="tuned GEMM solution table (verl_amd/tuned/*.csv, 'default', or 'none')")
     ap.add_argument("--model", default="0.5b")
     ap.add_argument("--no-rmpad", action="store_true")
     ap.add_argument("--no-mixed-precision", action="store_true", help="fp32 weights + autocast instead of bf16/fp32-master")
@@ -161,8 +187,13 @@ def main():
             use_kl_loss=True, kl_loss_coef=0.001, kl_loss_type="low_var_kl",
             clip_ratio=0.2, clip_ratio_c=3.0, loss_agg_mode="token-mean", entropy_coeff=0,
             use_remove_padding=not args.no_rmpad,
+            use_dynamic_bsz=args.dynamic_bsz > 0, ppo_max_token_len_per_gpu=args.dynamic_bsz or 16384,
+            pack_pad_multiple=args.pad_multiple,
+            gemm_tuning_file=None if args.gemm_table in (None, "none") else args.gemm_table,
         ),
-        rollout=AttrDict(log_prob_micro_batch_size_per_gpu=args.logprob_micro, temperature=1.0),
+        rollout=AttrDict(log_prob_micro_batch_size_per_gpu=args.logprob_micro, temperature=1.0,
+                         log_prob_use_dynamic_bsz=args.dynamic_bsz > 0,
+                         log_prob_max_token_len_per_gpu=args.dynamic_bsz or 16384),
     )
     # weak scaling: every rank owns a full 512-response shard; normalise against world=1
     worker = ActorWorker(cfg, rollout_n=args.n * world)
@@ -242,6 +273,7 @@ def main():
                 }
             else:
                 traffic, src = pmc_traffic(name, d["avg_bytes"], 151936)
+                ceil, ceil_src = hbm_ceiling(name)
                 roof = {
                     "kernel": name,
                     "bound": "hbm",
@@ -251,6 +283,9 @@ def main():
                     "frac": round(d["gbps"] / HBM_PEAK_GBPS, 4),
                     "traffic": round(traffic) if traffic else None,
                     "traffic_source": src,
+                    "measured_stream_ceiling": ceil,
+                    "frac_of_measured_ceiling": round(d["gbps"] / ceil, 4) if ceil else None,
+                    "ceiling_source": ceil_src,
                     "algo_bytes_per_launch": d["avg_bytes"],
                     "avg_launch_us": round(d["avg_us"], 2),
                     "launches": d["launches"],
@@ -279,6 +314,10 @@ def main():
                 "vocab": 151936,
                 "micro_batch": args.micro,
                 "logprob_micro_batch": args.logprob_micro,
+                "dynamic_bsz_max_token_len": args.dynamic_bsz or None,
+                "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
+                "pack_pad_multiple": args.pad_multiple,
+                "gemm_table": _gemm_table_name(),
                 "parallelism": f"dp{world}",
                 "remove_padding": not args.no_rmpad,
                 "mixed_precision": "bf16 weights / fp32 master+grads+reduce" if not args.no_mixed_precision

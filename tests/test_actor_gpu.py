@@ -215,3 +215,43 @@ def test_dynamic_bsz_log_prob_and_update_match_reference():
     for n, p in model_ref.named_parameters():
         scale = p.grad.abs().max().item() + 1e-12
         assert torch.allclose(grads[n], p.grad, atol=1e-4 * scale, rtol=1e-3), n
+
+
+@pytest.mark.parametrize("pad", [64, 1000])
+def test_pack_pad_multiple_leaves_results_unchanged(pad):
+    """pack_pad_multiple appends one dummy sequence to every packed micro-batch (fixed GEMM
+    shapes for the tuned table): log-probs, entropies and the weight gradients of the real tokens
+    must match the unpadded run on the fused bf16 backbone."""
+    from verl_amd.utils.model import build_qwen2
+
+    torch.manual_seed(0)
+    model = build_qwen2("tiny", device=DEV, dtype=torch.bfloat16)
+    model2 = copy.deepcopy(model)
+    data = _batch(B=8, seed=11)
+    b = data.batch
+    R = b["responses"].shape[1]
+    data.meta_info.update(micro_batch_size=4, temperature=1.0, use_dynamic_bsz=False)
+    cfg = dict(ppo_mini_batch_size=8, ppo_micro_batch_size_per_gpu=4, use_kl_loss=False, grad_clip=1e9)
+    a0 = _actor(model, **cfg)
+    a1 = _actor(model2, pack_pad_multiple=pad, **cfg)
+    lp0, ent0 = a0.compute_log_prob(data, calculate_entropy=True)
+    lp1, ent1 = a1.compute_log_prob(data, calculate_entropy=True)
+    m = b["response_mask"].bool()
+    assert torch.allclose(lp1[m], lp0[m], atol=1e-2, rtol=1e-2), (lp1[m] - lp0[m]).abs().max()
+    assert torch.allclose(ent1[m], ent0[m], atol=1e-2, rtol=1e-2)
+    g = torch.Generator(device=DEV).manual_seed(2)
+    b["old_log_probs"] = lp0 + 0.05 * torch.randn(lp0.shape, device=DEV, generator=g)
+    b["advantages"] = torch.randn(8, R, device=DEV, generator=g) * b["response_mask"]
+    grads = [{}, {}]
+    for i, (a, mdl) in enumerate(((a0, model), (a1, model2))):
+        def capture(mdl=mdl, i=i):
+            for n, p in mdl.named_parameters():
+                grads[i][n] = p.grad.detach().float().clone()
+            return torch.tensor(0.0, device=DEV)
+
+        a._optimizer_step = capture
+        a.update_policy(data)
+    for n in grads[0]:
+        g0, g1 = grads[0][n], grads[1][n]
+        scale = g0.abs().max().item() + 1e-12
+        assert torch.allclose(g1, g0, atol=2e-2 * scale, rtol=2e-2), (n, (g1 - g0).abs().max().item(), scale)

@@ -251,13 +251,14 @@ def test_fused_worker_training_tracks_master_weights():
         assert torch.allclose(a[m], b[m], atol=5e-2, rtol=2e-2), (a[m] - b[m]).abs().max().item()
 
 
-@pytest.mark.parametrize("n_out,n_in", [(1152, 896), (896, 4864)])
-def test_splitk_weight_grad(n_out, n_in):
-    """Split-K weight gradient (two K halves, fp32 batched GEMM, one rounding) vs one GEMM in fp32."""
+@pytest.mark.parametrize("n_out,n_in,T", [(1152, 896, 8192), (896, 4864, 8192), (896, 896, 40000),
+                                          (9728, 896, 9473), (1152, 896, 77824)])
+def test_splitk_weight_grad(n_out, n_in, T):
+    """Split-K weight gradient (S token slices as one fp32 batched GEMM + the T % S tail, summed in
+    fp32, one rounding) vs one GEMM in fp32."""
     from verl_amd import kernels as K
 
     torch.manual_seed(n_out)
-    T = 8192
     dy = torch.randn(T, n_out, device=DEV).to(torch.bfloat16)
     x = torch.randn(T, n_in, device=DEV).to(torch.bfloat16)
     got = K.weight_grad(dy, x)

@@ -181,3 +181,34 @@ def test_slice_int_len_and_no_batch():
 def test_split_matches_reference_micro_batching():
     d = DataProto.from_dict(tensors={"x": torch.arange(10)})
     assert [m.batch["x"].tolist() for m in d.split(4)] == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9]]
+
+
+def test_plan_packing_pad_multiple_appends_one_dummy_sequence():
+    """dp_actor._plan_packing(pad_multiple): packed length rounded up by ONE extra sequence whose
+    rows are never selected; the real tokens' packing is unchanged (host logic, CPU)."""
+    import numpy as np
+    import torch
+
+    from verl_amd.workers.actor.dp_actor import _plan_packing
+
+    rs = np.random.RandomState(0)
+    B, P, R = 5, 7, 9
+    am = np.zeros((B, P + R), dtype=np.int64)
+    for i in range(B):
+        p, r = rs.randint(1, P + 1), rs.randint(1, R + 1)
+        am[i, P - p : P + r] = 1
+    base = _plan_packing(am, R, "cpu")
+    pk = _plan_packing(am, R, "cpu", pad_multiple=16)
+    nnz = int(am.sum())
+    assert pk.pad == (-nnz) % 16 and (nnz + pk.pad) % 16 == 0
+    assert torch.equal(pk.token_idx, base.token_idx)
+    assert torch.equal(pk.sel_hidden, base.sel_hidden) and torch.equal(pk.sel_out, base.sel_out)
+    assert torch.equal(pk.cu_seqlens[: B + 1], base.cu_seqlens)
+    if pk.pad:
+        assert len(pk.cu_seqlens) == B + 2 and int(pk.cu_seqlens[-1]) == nnz + pk.pad
+        ids = torch.arange(B * (P + R)).view(B, P + R) + 1
+        pos = torch.arange(P + R).repeat(B, 1)
+        gi, gp = pk.gather(ids, pos)
+        assert len(gi) == nnz + pk.pad and (gi[nnz:] == 0).all()
+        assert torch.equal(gp[nnz:], torch.arange(pk.pad))
+    assert _plan_packing(am, R, "cpu", pad_multiple=1).pad == 0

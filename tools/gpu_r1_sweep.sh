@@ -13,10 +13,16 @@ run pmc_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/p
 python3 tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write 8192 151936 gpurun_out/pmc_logprob.json
 find gpurun_out/pmc_fetch gpurun_out/pmc_write -name "*.db" -delete
 fi
-for cfg in ${SWEEP:-"16 32" "32 32" "16 64"}; do
+IFS=',' read -ra CFGS <<< "${SWEEP:-16 32 0,32 32 0}"
+for cfg in "${CFGS[@]}"; do
   set -- $cfg
-  run bench_m$1_l$2 400 python bench.py --steps 2 --warmup 1 --micro $1 --logprob-micro $2 --no-cpu-baseline; rc=$?
+  n=bench_m$1_l$2_d$3
+  run $n 400 python bench.py --steps 2 --warmup 1 --micro $1 --logprob-micro $2 --dynamic-bsz $3 --no-cpu-baseline; rc=$?
   ok $rc || exit $rc
-  grep -E "^\{" gpurun_out/bench_m$1_l$2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('micro', $1, $2, d['value'], d['ms_per_step'])" || true
+  grep -E "^\{" gpurun_out/$n.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$n', d['value'], d['ms_per_step'], d['config']['peak_hbm_gb'])" || true
 done
+if [[ -n ${TUNE_T:-} ]]; then
+  run tunableop 600 python tools/tunableop_probe.py $TUNE_T || exit $?
+  cat gpurun_out/tunableop.log
+fi
 exit 0

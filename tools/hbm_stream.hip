@@ -8,6 +8,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <stdint.h>
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -77,8 +78,10 @@ int run(const char *name, const u32x4 *src, u32x4 *dst, int64_t n, int block, in
   return 0;
 }
 
-int main() {
-  const int64_t bytes = 8192LL * 151936 * 2;  // one bf16 logits buffer of the headline micro-batch
+int main(int argc, char **argv) {
+  // one bf16 logits buffer of a micro-batch: rows x 151,936 (argv[1], default 8192 rows)
+  const int64_t rows = argc > 1 ? atoll(argv[1]) : 8192;
+  const int64_t bytes = rows * 151936 * 2;
   const int64_t n = bytes / 16;
   u32x4 *src, *dst;
   CK(hipMalloc(&src, bytes));
@@ -91,6 +94,7 @@ int main() {
       // g == 0: one U-vector chunk per thread (no grid stride)
       const int grid1 = g ? g : static_cast<int>((n + block * 4 - 1) / (block * 4));
       run<0, 4, true>("copy", src, dst, n, block, grid1);
+      run<0, 4, true>("copy_inplace", src, src, n, block, grid1);
       run<0, 4, false>("copy", src, dst, n, block, grid1);
       run<1, 4, true>("read", src, dst, n, block, grid1);
       run<2, 4, true>("write", src, dst, n, block, grid1);

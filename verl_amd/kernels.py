@@ -728,21 +728,38 @@ class _MergedLinear(torch.autograd.Function):
         return (dx, None, None, None, *grads)
 
 
-# weight gradients dW = dY^T X whose output has few 256 x 256 tiles (q|k|v, o, down at H = 896)
-# leave most CUs idle in one GEMM; two K-halves as a batched GEMM with fp32 output, summed in fp32
-# and rounded once, fill the chip (tools/wgrad_bench.py: 1.2-1.3x on those shapes).
-WGRAD_SPLITK_MAX_ELEMS = 6_000_000
-WGRAD_SPLITK_MIN_TOKENS = 4096
+# weight gradients dW = dY^T X have K = tokens (tens of thousands) and an output of only
+# ceil(n_out/256) x ceil(n_in/256) 256 x 256 tiles (20 for q|k|v, 16 for o at H = 896), which
+# leaves most of the 256 CUs idle in one GEMM. Splitting the tokens into S slices as ONE batched
+# GEMM with fp32 output (S x tiles workgroups), summed in fp32 and rounded once, fills the chip.
+# S targets >= 512 tile-workgroups (tools/wgrad_bench.py at T = 77,824 on MI355X: q|k|v 389 ->
+# 232 us with S = 16, o 362 -> 172 (16), down 866 -> 779 (8), gate|up 1790 -> 1566 (4)).
+WGRAD_SPLITK_TARGET_WGS = 512
+WGRAD_SPLITK_MAX = 16
+WGRAD_SPLITK_MIN_SLICE = 2048  # tokens per slice
+
+
+def wgrad_splits(T: int, n_out: int, n_in: int) -> int:
+    tiles = -(-n_out // 256) * -(-n_in // 256)
+    s = 1
+    while s < WGRAD_SPLITK_MAX and s * tiles < WGRAD_SPLITK_TARGET_WGS and T // (2 * s) >= WGRAD_SPLITK_MIN_SLICE:
+        s *= 2
+    return s
 
 
 def weight_grad(dy2, x2):
     T, n_out = dy2.shape
     n_in = x2.shape[1]
-    if (dy2.is_cuda and T >= WGRAD_SPLITK_MIN_TOKENS and T % 2 == 0 and n_out * n_in <= WGRAD_SPLITK_MAX_ELEMS
-            and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16):
-        h = T // 2
-        part = torch.bmm(dy2.view(2, h, n_out).transpose(1, 2), x2.reshape(2, h, n_in), out_dtype=torch.float32)
-        return (part[0] + part[1]).to(dy2.dtype)
+    s = wgrad_splits(T, n_out, n_in) if dy2.is_cuda and dy2.dtype == x2.dtype == torch.bfloat16 else 1
+    if s > 1:
+        h = T // s
+        main = s * h
+        part = torch.bmm(dy2[:main].view(s, h, n_out).transpose(1, 2), x2[:main].reshape(s, h, n_in),
+                         out_dtype=torch.float32)
+        acc = part.sum(0)
+        if main < T:  # the T % s trailing tokens
+            acc += torch.mm(dy2[main:].t(), x2[main:], out_dtype=torch.float32)
+        return acc.to(dy2.dtype)
     return dy2.t() @ x2
 
 

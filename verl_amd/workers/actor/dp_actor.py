@@ -61,14 +61,33 @@ class _Packing:
     sel_out: torch.Tensor  # [n_sel] flat index into [B*R]
     attn_blocks: torch.Tensor = None  # [n, 2] int32 (sequence, first query row) for va_flash_attn_fwd
     attn_kblocks: torch.Tensor = None  # [n, 2] int32 (sequence, first key) for va_flash_attn_bwd
+    pad: int = 0  # dummy tokens appended as one extra sequence (pad_multiple)
+    pad_pos: torch.Tensor = None  # [pad] int64 position ids of the dummy sequence
+
+    def gather(self, input_ids: torch.Tensor, position_ids: torch.Tensor):
+        """Packed (ids [T], pos [T]) of the real tokens, followed by the dummy sequence."""
+        ids = input_ids.reshape(-1).index_select(0, self.token_idx)
+        pos = position_ids.reshape(-1).index_select(0, self.token_idx)
+        if self.pad:
+            ids = torch.cat([ids, ids.new_zeros(self.pad)])
+            pos = torch.cat([pos, self.pad_pos])
+        return ids, pos
 
 
-def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device) -> _Packing:
+def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device, pad_multiple: int = 0) -> _Packing:
+    """Padding removal of one micro-batch. With ``pad_multiple`` > 0 the packed length is rounded
+    up to a multiple of it by one extra dummy sequence (token 0, positions 0..pad-1): the model
+    GEMMs then see a few fixed token counts, so a tuned GEMM table (utils/gemm_tuning.py) applies.
+    The dummy rows are never selected for the loss, so their gradients are exactly zero and they
+    attend only to themselves: the real tokens' results and every weight gradient are unchanged."""
     B, S = attn_mask_cpu.shape
     flat = attn_mask_cpu.reshape(-1).astype(bool)
     token_idx = np.flatnonzero(flat)
     seqlens = attn_mask_cpu.astype(bool).sum(axis=1)
-    cu = np.zeros(B + 1, dtype=np.int32)
+    pad = (-len(token_idx)) % pad_multiple if pad_multiple > 0 else 0
+    if pad:
+        seqlens = np.concatenate([seqlens, [pad]])
+    cu = np.zeros(len(seqlens) + 1, dtype=np.int32)
     np.cumsum(seqlens, out=cu[1:])
     # packed index of every padded position (valid only where the mask is 1)
     packed_of = np.cumsum(flat) - 1
@@ -92,6 +111,8 @@ def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device) -> _Packing:
         sel_out=dev(sel_out, np.int64),
         attn_blocks=dev(attention.flash_block_table(cu), np.int32),
         attn_kblocks=dev(attention.flash_key_block_table(cu), np.int32),
+        pad=int(pad),
+        pad_pos=dev(np.arange(pad), np.int64) if pad else None,
     )
 
 
@@ -131,6 +152,14 @@ class DataParallelPPOActor(BasePPOActor):
         # gfx950 flash-attention forward (attention.hip) inside the fused packed backbone
         self.fused_attention = self.config.get("fused_attention", True)
         self.fused_logprob_no_grad = self.config.get("fused_logprob_no_grad", False)
+        # round packed micro-batches up to a multiple of this many tokens (0 = off) and look the
+        # model GEMMs up in a tuned solution table (utils/gemm_tuning.py)
+        self.pack_pad_multiple = int(self.config.get("pack_pad_multiple", 0) or 0)
+        gemm_table = self.config.get("gemm_tuning_file", None)
+        if gemm_table:
+            from ...utils.gemm_tuning import use_tuned_gemms
+
+            use_tuned_gemms(gemm_table)
 
     # ------------------------------------------------------------------ forward
     def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False, packing: _Packing = None):
@@ -143,12 +172,13 @@ class DataParallelPPOActor(BasePPOActor):
         with torch.autocast(device_type=self.device_name, dtype=ac or torch.bfloat16, enabled=ac is not None):
             if self.use_remove_padding:
                 if packing is None:
-                    packing = _plan_packing(micro_batch["attention_mask"].cpu().numpy(), R, input_ids.device)
-                ids = input_ids.reshape(-1).index_select(0, packing.token_idx).unsqueeze(0)
+                    packing = _plan_packing(micro_batch["attention_mask"].cpu().numpy(), R, input_ids.device,
+                                            self.pack_pad_multiple)
                 pos_ids = micro_batch["position_ids"]
                 if pos_ids.dim() == 3:
                     raise NotImplementedError("mrope position ids (VLM) are out of scope")
-                pos = pos_ids.reshape(-1).index_select(0, packing.token_idx).unsqueeze(0)
+                ids, pos = packing.gather(input_ids, pos_ids)
+                ids, pos = ids.unsqueeze(0), pos.unsqueeze(0)
                 if self._fused_backbone is None:
                     from . import qwen2_fused
 
@@ -210,10 +240,11 @@ class DataParallelPPOActor(BasePPOActor):
         R = data.batch["responses"].size(-1)
         dev = data.batch["input_ids"].device
         if idx_lists is not None:
-            return [_plan_packing(am[np.asarray(ix, dtype=np.int64)], R, dev) for ix in idx_lists]
+            return [_plan_packing(am[np.asarray(ix, dtype=np.int64)], R, dev, self.pack_pad_multiple)
+                    for ix in idx_lists]
         plans, s = [], 0
         for n in sizes:
-            plans.append(_plan_packing(am[s : s + n], R, dev))
+            plans.append(_plan_packing(am[s : s + n], R, dev, self.pack_pad_multiple))
             s += n
         return plans
 

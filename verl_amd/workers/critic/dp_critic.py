@@ -57,6 +57,13 @@ class DataParallelPPOCritic(BasePPOCritic):
                 critic_module.config._attn_implementation = name
         self.fused_model_ops = self.use_remove_padding and self.config.get("fused_model_ops", True)
         self._fused_backbone = None
+        # as the actor: pad packed micro-batches to a multiple of this many tokens (0 = off) and
+        # use a tuned GEMM solution table
+        self.pack_pad_multiple = int(self.config.get("pack_pad_multiple", 0) or 0)
+        if self.config.get("gemm_tuning_file", None):
+            from ...utils.gemm_tuning import use_tuned_gemms
+
+            use_tuned_gemms(self.config.gemm_tuning_file)
 
     # ------------------------------------------------------------------ forward
     def _forward_micro_batch(self, micro_batch, packing=None) -> torch.Tensor:
@@ -70,9 +77,9 @@ class DataParallelPPOCritic(BasePPOCritic):
         with torch.autocast(device_type=self.device_name, dtype=torch.bfloat16):
             if self.use_remove_padding:
                 if packing is None:
-                    packing = _plan_packing(micro_batch["attention_mask"].cpu().numpy(), R, input_ids.device)
-                ids = input_ids.reshape(-1).index_select(0, packing.token_idx)
-                pos = position_ids.reshape(-1).index_select(0, packing.token_idx)
+                    packing = _plan_packing(micro_batch["attention_mask"].cpu().numpy(), R, input_ids.device,
+                                            self.pack_pad_multiple)
+                ids, pos = packing.gather(input_ids, position_ids)
                 if self._fused_backbone is None:
                     from ..actor import qwen2_fused
 
@@ -109,10 +116,11 @@ class DataParallelPPOCritic(BasePPOCritic):
         R = data.batch["responses"].size(-1)
         dev = data.batch["input_ids"].device
         if idx_lists is not None:
-            return [_plan_packing(am[np.asarray(ix, dtype=np.int64)], R, dev) for ix in idx_lists]
+            return [_plan_packing(am[np.asarray(ix, dtype=np.int64)], R, dev, self.pack_pad_multiple)
+                    for ix in idx_lists]
         plans, s = [], 0
         for n in sizes:
-            plans.append(_plan_packing(am[s : s + n], R, dev))
+            plans.append(_plan_packing(am[s : s + n], R, dev, self.pack_pad_multiple))
             s += n
         return plans
 
