@@ -119,11 +119,15 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   VA_TUNE_NONTEMPORAL: 1 = non-temporal (streaming) loads/stores of the logits (default),
  *   0 = default cache policy;
  *   VA_TUNE_PIPELINE: fwd 0: 4 vectors/lane, 1: 2+2 software-pipelined, 2: 4+4 pipelined;
- *   bwd 16-B vectors per lane per workgroup chunk 0: 4, 1: 2, 2: 8. */
+ *   bwd 16-B vectors per lane per workgroup chunk 0: 4, 1: 2, 2: 8;
+ *   VA_TUNE_FLASH_GROUPED_DKDV (va_flash_attn_bwd): -1 = auto, 0 = per-query-head fp32 partials +
+ *   fixed-order group sum, 1 = one workgroup per key block x KV head summing its group in registers
+ *   (results differ only in fp32 summation order). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3
 #define VA_TUNE_PIPELINE 4
+#define VA_TUNE_FLASH_GROUPED_DKDV 5
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

@@ -89,7 +89,7 @@ def test_flash_forward_matches_torch_flash_and_lse_convention():
         assert (lse[i, :, :n] - lse_t[i, :, :n].float()).abs().max().item() < 1e-3
 
 
-@pytest.mark.parametrize("bwd", ["aten", "gfx950"])
+@pytest.mark.parametrize("bwd", ["aten", "gfx950", "gfx950-grouped"])
 @pytest.mark.parametrize("lens", [[300, 129, 1000], [1, 33, 64, 65, 128, 129, 200], [1184, 1280]])
 def test_flash_backward_matches_fp32_reference(bwd, lens):
     """dQ, dK, dV of the gfx950 forward + (aten | gfx950) backward against fp32 autograd of the
@@ -110,12 +110,17 @@ def test_flash_backward_matches_fp32_reference(bwd, lens):
     qb, kb, vb = (t.clone().requires_grad_(True) for t in (q, k, v))
     blocks = torch.tensor(A.flash_block_table(cu), device=DEV)
     kblocks = torch.tensor(A.flash_key_block_table(cu), device=DEV)
+    from verl_amd import _lib as L
+
     old = A.FLASH_BWD
-    A.FLASH_BWD = bwd
+    A.FLASH_BWD = bwd.split("-")[0]
+    # grouped: one workgroup per key block x KV head (forced); plain gfx950: per-head partials
+    L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, 1 if bwd.endswith("grouped") else 0)
     try:
         A.flash_attention(qb, kb, vb, cu_d, mx, blocks, kblocks=kblocks).backward(g)
     finally:
         A.FLASH_BWD = old
+        L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, -1)
     for ref_t, tor, ours, what in ((qr.grad, qa.grad, qb.grad, "dq"), (kr.grad, ka.grad, kb.grad, "dk"),
                                    (vr.grad, va.grad, vb.grad, "dv")):
         r = ref_t.float()

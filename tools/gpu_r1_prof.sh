@@ -10,6 +10,8 @@ if [[ -n ${WGRAD_T:-} ]]; then run wgrad 300 python tools/wgrad_bench.py $WGRAD_
 run prof_$TAG 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 1 --out gpurun_out/bench_prof_$TAG.json "$@" || exit $?
 f=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
 python3 tools/prof_summary.py "$f" > gpurun_out/prof_$TAG.summary.txt && cp "$f" gpurun_out/prof_$TAG.kernel_stats.csv
+t=$(find gpurun_out/prof_$TAG -name '*kernel_trace.csv' | head -1)
+python3 tools/trace_gaps.py "$t" --window ${GAP_WINDOW:-3.0} > gpurun_out/prof_$TAG.gaps.txt || true
 find gpurun_out/prof_$TAG \( -name "*kernel_trace.csv" -o -name "*.db" \) -delete
 head -8 gpurun_out/prof_$TAG.summary.txt
 exit 0

@@ -77,14 +77,17 @@ def gemm_cases(T=9472, H=896, FF=4864, QKV=1152):
     del x
 
 
-def attn_gfx950(n_seq=8, seqlen=1184, hq=14, hk=2, d=64):
+def attn_gfx950(n_seq=8, seqlen=1184, hq=14, hk=2, d=64, grouped=-1):
     import os
     import sys
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import numpy as np
 
+    from verl_amd import _lib as L
     from verl_amd.workers.actor import attention as A
+
+    L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, grouped)
 
     dev = "cuda"
     T = n_seq * seqlen
@@ -107,7 +110,8 @@ def attn_gfx950(n_seq=8, seqlen=1184, hq=14, hk=2, d=64):
     flops_fwd = 2.0 * n_seq * seqlen * seqlen * d * hq
     tf = timeit(fwd)
     tfb = timeit(fwdbwd)
-    print(json.dumps({"case": f"attn_gfx950_fwd_n{n_seq}", "fwd_us": round(tf, 1),
+    L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, -1)
+    print(json.dumps({"case": f"attn_gfx950_fwd_n{n_seq}", "grouped_dkdv": grouped, "fwd_us": round(tf, 1),
                       "fwd_tflops": round(flops_fwd / tf / 1e6, 1), "fwdbwd_us": round(tfb, 1),
                       "fwdbwd_tflops": round(3.5 * flops_fwd / tfb / 1e6, 1)}))
 
@@ -118,6 +122,9 @@ if __name__ == "__main__":
         attn_case("aotriton")
         attn_gfx950()
         attn_gfx950(n_seq=16)
+    if "gfx950_n64" in what:
+        for gr in (0, 1):
+            attn_gfx950(n_seq=64, grouped=gr)
     if "attn" in what:
         for b in ("aotriton", "ck"):
             try:

@@ -293,11 +293,18 @@ __global__ __launch_bounds__(128) void flash_bwd_delta_kernel(const uint16_t *__
   delta[(static_cast<int64_t>(seq) * Hq + head) * ld + qp] = acc;
 }
 
+// GROUPED = false: blockIdx.y = query head, fp32 partial dK / dV per query head (summed by
+// flash_bwd_group_sum); GROUPED = true: blockIdx.y = KV head, the workgroup sweeps the query tiles of
+// all G query heads of its group in order (head-major) with dK / dV accumulated in registers, and
+// writes bf16 dK / dV directly (no partials, no group-sum launch; used when the key blocks alone fill
+// the chip).
+template <bool GROUPED>
 __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
     const uint16_t *__restrict__ q, const uint16_t *__restrict__ k, const uint16_t *__restrict__ v,
     const uint16_t *__restrict__ dout, const float *__restrict__ lse, const float *__restrict__ delta,
     const int32_t *__restrict__ cu, const int32_t *__restrict__ kblocks, int64_t ld, int64_t T, int Hq, int Hk,
-    float scale, float *__restrict__ pdk, float *__restrict__ pdv) {
+    float scale, float *__restrict__ pdk, float *__restrict__ pdv, uint16_t *__restrict__ dk_out,
+    uint16_t *__restrict__ dv_out) {
   constexpr int QT = 32;  // query rows per staged tile
   // [buf][Q image 32x64 | dO image 32x64] bf16, then [buf][lse2 32 | delta 32] fp32
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * QT * D + 2 * 2 * QT * 2];
@@ -305,7 +312,9 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, kl = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
   const int seq = kblocks[2 * blockIdx.x], kb0 = kblocks[2 * blockIdx.x + 1];
-  const int hq0 = blockIdx.y, g = hq0 / (Hq / Hk);  // one query head; its partial dK / dV
+  const int G = Hq / Hk;
+  const int hq0 = GROUPED ? blockIdx.y * G : blockIdx.y;  // (first) query head
+  const int g = GROUPED ? blockIdx.y : hq0 / G;
   const int s0 = cu[seq], len = cu[seq + 1] - s0;
   const int64_t ldq = static_cast<int64_t>(Hq) * D, ldk = static_cast<int64_t>(Hk) * D;
   const float c = scale * kLog2e_;
@@ -334,7 +343,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   // iteration space: query tiles from the block's first key to the end of the sequence
   const int qfirst = (kb0 / QT) * QT;
   const int n_qt = len > qfirst ? (len - qfirst + QT - 1) / QT : 0;
-  const int n_it = n_qt;
+  const int n_it = GROUPED ? n_qt * G : n_qt;  // grouped: head-major over the group's query heads
   // staging: one 16-B chunk of the Q tile and one of the dO tile per thread; lse2 / delta by 64 threads
   struct StageQ {
     uint4 q, d;
@@ -342,7 +351,8 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   };
   auto load_it = [&](int it) -> StageQ {
     StageQ st;
-    const int hq = hq0, qt0 = qfirst + it * QT;
+    const int hj = GROUPED ? it / n_qt : 0;
+    const int hq = hq0 + hj, qt0 = qfirst + (it - hj * n_qt) * QT;
     const int r = tid >> 3, ch = tid & 7, qp = qt0 + r;
     {
       const bool ok = qp < len;
@@ -380,7 +390,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
     const uint16_t *di = qi + QT * D;
     const float *lse2 = rowc + buf * 2 * QT;
     const float *dlt = lse2 + QT;
-    const int qt0 = qfirst + it * QT;
+    const int qt0 = qfirst + (GROUPED ? it % n_qt : it) * QT;
     if (qt0 + QT - 1 >= k0 && k0 < len) {  // some query of the tile sees some key of the wave
       // S = Q K^T and dP = dO V^T, rows = queries (registers), columns = keys (lanes)
       f32x16 sacc, pacc;
@@ -425,6 +435,25 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   }
   // this head's partial dK = scale * (dK^T)^T and dV = (dV^T)^T, fp32 [Hq][T][64]: lane holds
   // column key, rows d = 32 dh + 8 gg + 4 h + i
+  if (GROUPED) {
+    // dK = scale * (dK^T)^T, dV = (dV^T)^T summed over the group in registers: bf16 [T, Hk, 64]
+    if (key < len) {
+      uint16_t *dkr = dk_out + (static_cast<int64_t>(s0 + key) * Hk + g) * D;
+      uint16_t *dvr = dv_out + (static_cast<int64_t>(s0 + key) * Hk + g) * D;
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const int d0 = dh * 32 + 8 * gg + 4 * h;
+          *reinterpret_cast<uint2 *>(dkr + d0) =
+              make_uint2(pk_bf16(dkt[dh][4 * gg] * scale, dkt[dh][4 * gg + 1] * scale),
+                         pk_bf16(dkt[dh][4 * gg + 2] * scale, dkt[dh][4 * gg + 3] * scale));
+          *reinterpret_cast<uint2 *>(dvr + d0) =
+              make_uint2(pk_bf16(dvt[dh][4 * gg], dvt[dh][4 * gg + 1]), pk_bf16(dvt[dh][4 * gg + 2], dvt[dh][4 * gg + 3]));
+        }
+    }
+    return;
+  }
   if (key < len) {
     float *dkr = pdk + (static_cast<int64_t>(hq0) * T + s0 + key) * D;
     float *dvr = pdv + (static_cast<int64_t>(hq0) * T + s0 + key) * D;
@@ -596,6 +625,9 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
 
 using namespace va;
 
+// va_set_tuning(VA_TUNE_FLASH_GROUPED_DKDV): -1 auto, 0 per-query-head partials + group sum, 1 grouped
+int g_flash_grouped_dkdv = -1;
+
 extern "C" int va_flash_attn_fwd(const void *q, const void *k, const void *v, const int32_t *cu_seqlens,
                                  const int32_t *block_table, int64_t n_blocks, int64_t T, int64_t Hq, int64_t Hk,
                                  int64_t head_dim, int64_t max_len, float scale, void *o, float *lse, void *stream) {
@@ -631,11 +663,23 @@ extern "C" int va_flash_attn_bwd(const void *q, const void *k, const void *v, co
   hipLaunchKernelGGL(flash_bwd_delta_kernel, dim3(static_cast<unsigned>(n_q_blocks), static_cast<unsigned>(Hq)),
                      dim3(128), 0, s, static_cast<const uint16_t *>(o), static_cast<const uint16_t *>(dout),
                      cu_seqlens, q_blocks, max_len, static_cast<int>(Hq), delta);
-  hipLaunchKernelGGL(flash_bwd_dkdv_kernel, dim3(static_cast<unsigned>(n_k_blocks), static_cast<unsigned>(Hq)),
-                     dim3(256), 0, s, static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(k),
-                     static_cast<const uint16_t *>(v), static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens,
-                     k_blocks, max_len, T, static_cast<int>(Hq), static_cast<int>(Hk), scale, pdk, pdv);
-  {
+  // grouped dK / dV (one workgroup per key block x KV head, no partials) once the key blocks alone
+  // give >= 2 workgroups per CU; otherwise per query head + the fixed-order group sum
+  const bool grouped = g_flash_grouped_dkdv == 1 || (g_flash_grouped_dkdv < 0 && n_k_blocks * Hk >= 512);
+  if (grouped) {
+    hipLaunchKernelGGL(flash_bwd_dkdv_kernel<true>, dim3(static_cast<unsigned>(n_k_blocks), static_cast<unsigned>(Hk)),
+                       dim3(256), 0, s, static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(k),
+                       static_cast<const uint16_t *>(v), static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens,
+                       k_blocks, max_len, T, static_cast<int>(Hq), static_cast<int>(Hk), scale, pdk, pdv,
+                       static_cast<uint16_t *>(dk), static_cast<uint16_t *>(dv));
+  } else {
+    hipLaunchKernelGGL(flash_bwd_dkdv_kernel<false>, dim3(static_cast<unsigned>(n_k_blocks), static_cast<unsigned>(Hq)),
+                       dim3(256), 0, s, static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(k),
+                       static_cast<const uint16_t *>(v), static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens,
+                       k_blocks, max_len, T, static_cast<int>(Hq), static_cast<int>(Hk), scale, pdk, pdv,
+                       static_cast<uint16_t *>(dk), static_cast<uint16_t *>(dv));
+  }
+  if (!grouped) {
     const int64_t granules = T * Hk * (D / 4);
     int64_t grid = (granules + 255) / 256;
     if (grid > 16384) grid = 16384;

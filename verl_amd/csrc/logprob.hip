@@ -612,12 +612,15 @@ extern "C" int va_logprob_entropy_bwd(const float *g_logp, const float *g_entrop
   }
 }
 
+extern int g_flash_grouped_dkdv;  // attention.hip
+
 extern "C" int va_set_tuning(int key, int value) {
   switch (key) {
     case VA_TUNE_FWD_WAVES_PER_ROW: va::g_fwd_wpr = value; return VA_OK;
     case VA_TUNE_BWD_WAVES_PER_ROW: va::g_bwd_wpr = value; return VA_OK;
     case VA_TUNE_NONTEMPORAL: va::g_nt = value; return VA_OK;
     case VA_TUNE_PIPELINE: va::g_pipe = value; return VA_OK;
+    case VA_TUNE_FLASH_GROUPED_DKDV: g_flash_grouped_dkdv = value; return VA_OK;
     default: va::set_error("unknown tuning key %d", key); return VA_E_ARG;
   }
 }

@@ -751,6 +751,13 @@ def weight_grad(dy2, x2):
     T, n_out = dy2.shape
     n_in = x2.shape[1]
     s = wgrad_splits(T, n_out, n_in) if dy2.is_cuda and dy2.dtype == x2.dtype == torch.bfloat16 else 1
+    if s > 1 and -(-n_out // 256) * -(-n_in // 256) >= 128:
+        # >= 128 output tiles: a tuned plain GEMM (utils/gemm_tuning) beats the split (gate|up at
+        # T = 77,824: 1466 vs 1566 us); the table keys dY^T X as column-major "nt" n_in x n_out x T
+        from .utils import gemm_tuning
+
+        if gemm_tuning.has_tuned("nt", n_in, n_out, T):
+            s = 1
     if s > 1:
         h = T // s
         main = s * h

@@ -24,6 +24,7 @@ TUNED_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file_
 DEFAULT_TABLE = os.path.join(TUNED_DIR, "gemm_qwen2_0p5b_mi355x.csv")
 
 _loaded: str | None = None
+_shapes: frozenset = frozenset()  # "nt_M_N_K" problem prefixes present in the loaded table
 
 
 def resolve(path: str) -> str:
@@ -57,7 +58,16 @@ def use_tuned_gemms(path: str = "default") -> bool:
     # (concurrent ranks share it)
     tun.set_filename(os.path.join("/tmp", f"verl_amd_tunableop_{os.getpid()}.csv"), False)
     _loaded = path
+    global _shapes
+    _shapes = frozenset("_".join(line.split(",")[1].split("_")[:4]) for line in open(path)
+                        if line.startswith("Gemm"))
     return True
+
+
+def has_tuned(op: str, m: int, n: int, k: int) -> bool:
+    """Whether the loaded table holds a solution for this BLAS problem (``op`` as TunableOp writes
+    it: "nn", "nt", "tn", "tt"; column-major m, n, k)."""
+    return f"{op}_{m}_{n}_{k}" in _shapes
 
 
 def start_tuning(path: str, max_iterations: int = 10, max_duration_ms: int = 30) -> None:
