@@ -234,19 +234,21 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
 
 // =====================================================================================
 // Backward. dS = P * (dP - delta), delta = rowsum(dO * O); P recomputed from Q, K and the
-// forward's LSE. Three launches, no atomics (dQ, dK, dV are each written once: deterministic):
-//   flash_bwd_delta   delta [B, Hq, max_len] (the LSE layout)
-//   flash_bwd_dkdv    workgroup = 128 keys of one sequence x one query head; wave = 32 keys whose
-//                     K, V fragments stay in registers. It sweeps the 32-row query tiles at or
+// forward's LSE. Two or three launches, no atomics (dQ, dK, dV are each written once: deterministic):
+//   flash_bwd_dq      workgroup = 128 queries x one query head (the forward's block table); wave =
+//                     32 queries with Q, dO fragments in registers; computes its queries' delta from
+//                     O and dO first (stored in the LSE layout for the next launch), then per 32-key
+//                     tile  S^T = K Q^T, dP^T = V dO^T (query on the lane), dQ^T += K^T dS^T
+//   flash_bwd_dkdv    workgroup = 128 keys x one KV head (GROUPED: sweeps the query tiles of all the
+//                     group's query heads, dK / dV summed in registers, bf16 out) or x one query head
+//                     (fp32 partials, when key blocks alone would not fill the chip); wave = 32 keys
+//                     whose K, V fragments stay in registers. It sweeps the 32-row query tiles at or
 //                     after its keys (Q, dO, LSE, delta staged in double-buffered LDS):
 //                       S = Q K^T, dP = dO V^T  with the KEY on the lane (4 MFMAs each), so
 //                       P and dS are already the B operands of
 //                       dV^T += dO^T P,  dK^T += Q^T dS  (A = transposed reads of the Q / dO images)
-//   flash_bwd_group_sum  dK, dV = fixed-order sum of the per-query-head fp32 partials over the
-//                     GQA group (1120 dK/dV workgroups instead of 160 at 8 x 1184 tokens, Hkv = 2)
-//   flash_bwd_dq      workgroup = 128 queries x one query head (the forward's block table); wave =
-//                     32 queries with Q, dO fragments in registers; per 32-key tile
-//                       S^T = K Q^T, dP^T = V dO^T (query on the lane), dQ^T += K^T dS^T
+//   flash_bwd_group_sum  (per-query-head variant only) dK, dV = fixed-order sum of the fp32
+//                     partials over the GQA group
 // LDS images are [rows][64] bf16 with 16-B chunk c of row r at c ^ (r & 7): conflict-light row
 // reads (ds_read_b128) and per-lane swizzled addresses for the transposed reads.
 
@@ -267,30 +269,6 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint16_t *img, int rbase, int s,
 __device__ __forceinline__ bf16x8 pack_frag(const float *x) {
   return __builtin_bit_cast(bf16x8, make_uint4(pk_bf16(x[0], x[1]), pk_bf16(x[2], x[3]), pk_bf16(x[4], x[5]),
                                                pk_bf16(x[6], x[7])));
-}
-
-__global__ __launch_bounds__(128) void flash_bwd_delta_kernel(const uint16_t *__restrict__ o,
-                                                              const uint16_t *__restrict__ dout,
-                                                              const int32_t *__restrict__ cu,
-                                                              const int32_t *__restrict__ blocks, int64_t ld,
-                                                              int Hq, float *__restrict__ delta) {
-  const int seq = blocks[2 * blockIdx.x], qs = blocks[2 * blockIdx.x + 1];
-  const int head = blockIdx.y;
-  const int s0 = cu[seq], len = cu[seq + 1] - s0;
-  const int qp = qs + threadIdx.x;
-  if (qp >= len) return;
-  const int64_t base = (static_cast<int64_t>(s0 + qp) * Hq + head) * D;
-  float acc = 0.f;
-#pragma unroll
-  for (int c = 0; c < D / 8; ++c) {
-    const uint4 a = *reinterpret_cast<const uint4 *>(o + base + 8 * c);
-    const uint4 b = *reinterpret_cast<const uint4 *>(dout + base + 8 * c);
-    acc = fmaf(bf16_lo(a.x), bf16_lo(b.x), acc); acc = fmaf(bf16_hi(a.x), bf16_hi(b.x), acc);
-    acc = fmaf(bf16_lo(a.y), bf16_lo(b.y), acc); acc = fmaf(bf16_hi(a.y), bf16_hi(b.y), acc);
-    acc = fmaf(bf16_lo(a.z), bf16_lo(b.z), acc); acc = fmaf(bf16_hi(a.z), bf16_hi(b.z), acc);
-    acc = fmaf(bf16_lo(a.w), bf16_lo(b.w), acc); acc = fmaf(bf16_hi(a.w), bf16_hi(b.w), acc);
-  }
-  delta[(static_cast<int64_t>(seq) * Hq + head) * ld + qp] = acc;
 }
 
 // GROUPED = false: blockIdx.y = query head, fp32 partial dK / dV per query head (summed by
@@ -497,11 +475,14 @@ __global__ __launch_bounds__(256) void flash_bwd_group_sum_kernel(const float *_
   }
 }
 
+// Also computes delta = rowsum(dO * O) of its queries from the O / dO fragments it loads anyway
+// (each query's 64 values are split over lanes l and l ^ 32) and publishes it for the dK / dV
+// launch that follows: no separate delta pass over O and dO.
 __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
     const uint16_t *__restrict__ k, const uint16_t *__restrict__ v, const uint16_t *__restrict__ q,
-    const uint16_t *__restrict__ dout, const float *__restrict__ lse, const float *__restrict__ delta,
-    const int32_t *__restrict__ cu, const int32_t *__restrict__ blocks, int64_t ld, int Hq, int Hk, float scale,
-    uint16_t *__restrict__ dq) {
+    const uint16_t *__restrict__ o, const uint16_t *__restrict__ dout, const float *__restrict__ lse,
+    float *__restrict__ delta, const int32_t *__restrict__ cu, const int32_t *__restrict__ blocks, int64_t ld,
+    int Hq, int Hk, float scale, uint16_t *__restrict__ dq) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * KB * D];  // [buf][K | V][64 keys][64 d], swizzled
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ql = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
@@ -525,7 +506,22 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
   }
   const int64_t ridx = (static_cast<int64_t>(seq) * Hq + head) * ld + q_pos;
   const float lse2 = q_ok ? lse[ridx] * kLog2e_ : 0.f;
-  const float dlt = q_ok ? delta[ridx] : 0.f;
+  float dpart = 0.f;
+  if (q_ok) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint4 a = *reinterpret_cast<const uint4 *>(o + (s0 + q_pos) * ldq + head * D + 16 * s + 8 * h);
+      const uint4 b = __builtin_bit_cast(uint4, df[s]);
+      dpart = fmaf(bf16_lo(a.x), bf16_lo(b.x), dpart); dpart = fmaf(bf16_hi(a.x), bf16_hi(b.x), dpart);
+      dpart = fmaf(bf16_lo(a.y), bf16_lo(b.y), dpart); dpart = fmaf(bf16_hi(a.y), bf16_hi(b.y), dpart);
+      dpart = fmaf(bf16_lo(a.z), bf16_lo(b.z), dpart); dpart = fmaf(bf16_hi(a.z), bf16_hi(b.z), dpart);
+      dpart = fmaf(bf16_lo(a.w), bf16_lo(b.w), dpart); dpart = fmaf(bf16_hi(a.w), bf16_hi(b.w), dpart);
+    }
+  }
+  // lane half 0 holds d in {0-7, 16-23, 32-39, 48-55}, half 1 the rest: fixed-order pair sum
+  const float dother = __shfl_xor(dpart, 32);
+  const float dlt = h == 0 ? dpart + dother : dother + dpart;
+  if (q_ok && h == 0) delta[ridx] = dlt;
   f32x16 dqt[2];
 #pragma unroll
   for (int dh = 0; dh < 2; ++dh)
@@ -660,9 +656,12 @@ extern "C" int va_flash_attn_bwd(const void *q, const void *k, const void *v, co
                "null pointer argument");
   float *pdk = partial, *pdv = partial + Hq * T * D;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(flash_bwd_delta_kernel, dim3(static_cast<unsigned>(n_q_blocks), static_cast<unsigned>(Hq)),
-                     dim3(128), 0, s, static_cast<const uint16_t *>(o), static_cast<const uint16_t *>(dout),
-                     cu_seqlens, q_blocks, max_len, static_cast<int>(Hq), delta);
+  // dQ first: it also produces delta for the dK / dV launch
+  hipLaunchKernelGGL(flash_bwd_dq_kernel, dim3(static_cast<unsigned>(n_q_blocks), static_cast<unsigned>(Hq)),
+                     dim3(256), 0, s, static_cast<const uint16_t *>(k), static_cast<const uint16_t *>(v),
+                     static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(o),
+                     static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens, q_blocks, max_len,
+                     static_cast<int>(Hq), static_cast<int>(Hk), scale, static_cast<uint16_t *>(dq));
   // grouped dK / dV (one workgroup per key block x KV head, no partials) once the key blocks alone
   // give >= 2 workgroups per CU; otherwise per query head + the fixed-order group sum
   const bool grouped = g_flash_grouped_dkdv == 1 || (g_flash_grouped_dkdv < 0 && n_k_blocks * Hk >= 512);
@@ -687,10 +686,5 @@ extern "C" int va_flash_attn_bwd(const void *q, const void *k, const void *v, co
                        static_cast<int>(Hq), static_cast<int>(Hk), static_cast<uint16_t *>(dk),
                        static_cast<uint16_t *>(dv));
   }
-  hipLaunchKernelGGL(flash_bwd_dq_kernel, dim3(static_cast<unsigned>(n_q_blocks), static_cast<unsigned>(Hq)),
-                     dim3(256), 0, s, static_cast<const uint16_t *>(k), static_cast<const uint16_t *>(v),
-                     static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens,
-                     q_blocks, max_len, static_cast<int>(Hq), static_cast<int>(Hk), scale,
-                     static_cast<uint16_t *>(dq));
   return check_launch("flash_attn_bwd");
 }
