@@ -76,8 +76,8 @@ def parse():
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--response-len", type=int, default=1024)
-    ap.add_argument("--micro", type=int, default=64, help="ppo_micro_batch_size_per_gpu (responses)")
-    ap.add_argument("--logprob-micro", type=int, default=64, help="log_prob_micro_batch_size_per_gpu")
+    ap.add_argument("--micro", type=int, default=128, help="ppo_micro_batch_size_per_gpu (responses)")
+    ap.add_argument("--logprob-micro", type=int, default=128, help="log_prob_micro_batch_size_per_gpu")
     ap.add_argument("--dynamic-bsz", type=int, default=0,
                     help="use_dynamic_bsz with this ppo_max_token_len_per_gpu (and log-prob budget); 0 = off")
     ap.add_argument("--pad-multiple", type=int, default=2048,

@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         sacc[r] = 0.f;
-        pacc[r] = 0.f;
+        pacc[r] = -dlt[crow(r, h)];  // row constant as the initial accumulator: dP - delta
       }
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -396,7 +396,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
           p[r] = static_cast<unsigned>(crow(r, 0) - lo) >= span ? 0.f : p[r];
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) ds[r] = p[r] * (pacc[r] - dlt[crow(r, h)]);  // (dP - delta) * p
+      for (int r = 0; r < 16; ++r) ds[r] = p[r] * pacc[r];  // (dP - delta) * p
       // dV^T += dO^T P, dK^T += Q^T dS  (k = queries, permuted order of the accumulator rows)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -572,7 +572,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         sacc[r] = 0.f;
-        pacc[r] = 0.f;
+        pacc[r] = -dlt;  // row constant as the initial accumulator: dP - delta
       }
       const int krow = t * 32 + ql;
 #pragma unroll
@@ -592,7 +592,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
         for (int r = 0; r < 16; ++r) ds[r] = crow(r, 0) > lim ? 0.f : ds[r];
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) ds[r] *= pacc[r] - dlt;
+      for (int r = 0; r < 16; ++r) ds[r] *= pacc[r];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const bf16x8 db = pack_frag(ds + 8 * s);
