@@ -142,17 +142,24 @@ def test_critic_compute_values_and_update_match_reference():
         assert err <= 5e-2 * scale + 1e-6, (n, err, scale)
 
 
-def test_packed_critic_matches_padded():
-    """use_remove_padding (fused packed Qwen2 backbone, value head on response positions only) vs
-    the padded HF path: same values to bf16 level, same loss."""
+def _critic_builder(family):
+    from verl_amd.utils.model import build_llama_critic, build_qwen2_critic
+
+    return {"qwen2": build_qwen2_critic, "llama": build_llama_critic}[family]
+
+
+@pytest.mark.parametrize("family", ["qwen2", "llama"])
+def test_packed_critic_matches_padded(family):
+    """use_remove_padding (fused packed backbone, value head on response positions only) vs the
+    padded HF path: same values to bf16 level, same loss. Llama = BASELINE config 3's critic
+    architecture (tiny, with Llama-3.1 rope scaling)."""
     from verl_amd.utils.config import AttrDict, critic_config
-    from verl_amd.utils.model import build_qwen2_critic
     from verl_amd.workers.actor import attention
     from verl_amd.workers.critic import DataParallelPPOCritic
 
     if not attention.varlen_available(DEV):
         pytest.skip("flash varlen unavailable")
-    base = build_qwen2_critic("tiny", device=DEV, attn_implementation="sdpa", seed=2)
+    base = _critic_builder(family)("tiny", device=DEV, attn_implementation="sdpa", seed=2)
     for p in base.parameters():
         p.data = p.data.to(torch.bfloat16)
     data = _batch(seed=6)
@@ -171,21 +178,21 @@ def test_packed_critic_matches_padded():
     assert (out[True][~msk] == 0).all()
 
 
-def test_critic_worker_gae_step():
+@pytest.mark.parametrize("family,lr", [("qwen2", 2e-4), ("llama", 5e-5)])
+def test_critic_worker_gae_step(family, lr):
     """CriticWorker end to end with bf16/fp32-master mixed precision and dynamic bsz: values ->
     GAE (HIP scan) -> repeated critic updates on the same targets; the value loss falls."""
     from verl_amd.trainer.ppo.core_algos import AdvantageEstimator
     from verl_amd.trainer.ppo.ray_trainer import compute_advantage
     from verl_amd.utils.config import AttrDict, critic_config
-    from verl_amd.utils.model import build_qwen2_critic
     from verl_amd.workers.actor import attention
     from verl_amd.workers.dp_workers import CriticWorker
 
     rmpad = attention.varlen_available(DEV)
     cfg = critic_config(ppo_mini_batch_size=8, ppo_micro_batch_size_per_gpu=None, use_dynamic_bsz=True,
                         ppo_max_token_len_per_gpu=256, forward_max_token_len_per_gpu=256,
-                        model=AttrDict(use_remove_padding=rmpad), optim=AttrDict(lr=2e-4, weight_decay=0.0))
-    w = CriticWorker(cfg).init_model(build_qwen2_critic("tiny", device=DEV, attn_implementation="sdpa", seed=5))
+                        model=AttrDict(use_remove_padding=rmpad), optim=AttrDict(lr=lr, weight_decay=0.0))
+    w = CriticWorker(cfg).init_model(_critic_builder(family)("tiny", device=DEV, attn_implementation="sdpa", seed=5))
     data = _batch(seed=9)
     data.batch["values"] = w.compute_values(data).batch["values"]
     compute_advantage(data, AdvantageEstimator.GAE, gamma=1.0, lam=0.95)
@@ -195,5 +202,5 @@ def test_critic_worker_gae_step():
         met = w.update_critic(data).meta_info["metrics"]
         assert all(np.isfinite(v) for v in met["critic/vf_loss"])
         losses.append(float(np.mean(met["critic/vf_loss"])))
-        assert met["critic/lr"] == 2e-4
+        assert met["critic/lr"] == lr
     assert losses[-1] < losses[0], losses

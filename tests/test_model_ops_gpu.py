@@ -148,15 +148,20 @@ def test_rope_qkv_matches_hf():
     _grad_close(qb_in.grad, qa_in.grad, "rope dqkv", rtol=1e-2)
 
 
-def test_patched_actor_matches_unpatched():
+@pytest.mark.parametrize("family", ["qwen2", "llama"])
+def test_patched_actor_matches_unpatched(family):
+    """Fused packed backbone (gfx950 RMSNorm / SwiGLU / RoPE / flash attention, merged GEMMs) vs the
+    HF forward on the same packing: log-probs, entropies and every parameter gradient. Llama covers
+    BASELINE config 3's actor architecture (no q/k/v bias, untied head, Llama-3.1 rope scaling)."""
     from verl_amd.utils.config import actor_config
-    from verl_amd.utils.model import build_qwen2
+    from verl_amd.utils.model import build_llama, build_qwen2
     from verl_amd.utils.synthetic import make_grpo_batch
     from verl_amd.workers.actor import DataParallelPPOActor, attention
 
     if not attention.varlen_available(DEV):
         pytest.skip("flash varlen unavailable")
-    base = build_qwen2("tiny", device=DEV, attn_implementation="sdpa", seed=3)
+    build = {"qwen2": build_qwen2, "llama": build_llama}[family]
+    base = build("tiny", device=DEV, attn_implementation="sdpa", seed=3)
     for p in base.parameters():
         p.data = p.data.to(torch.bfloat16)
     data = make_grpo_batch(n_prompts=2, n=4, prompt_len=20, response_len=30, vocab=4096, min_prompt=3,

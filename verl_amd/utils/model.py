@@ -60,6 +60,53 @@ def create_random_mask(input_ids: torch.Tensor, max_ratio_of_valid_token: float,
     return masks
 
 
+def llama_config(size: str = "tiny", **overrides):
+    """Llama-architecture configs (BASELINE config 3 is Llama-3-8B PPO with a critic). "8b" follows
+    the public Llama-3-8B card (assumed: no checkpoint or network here); "tiny" keeps head_dim 64
+    and Llama-3.1's rope scaling so the packed backbone's kernels and the scaled-RoPE path are
+    exercised."""
+    from transformers import LlamaConfig
+
+    llama3_rope = dict(rope_type="llama3", factor=8.0, low_freq_factor=1.0, high_freq_factor=4.0,
+                       original_max_position_embeddings=8192)
+    presets = {
+        "8b": dict(hidden_size=4096, intermediate_size=14336, num_hidden_layers=32, num_attention_heads=32,
+                   num_key_value_heads=8, vocab_size=128256, tie_word_embeddings=False,
+                   max_position_embeddings=8192, rope_scaling=None),
+        "tiny": dict(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+                     num_key_value_heads=2, vocab_size=4096, tie_word_embeddings=False,
+                     max_position_embeddings=131072, rope_scaling=llama3_rope),
+    }
+    kw = dict(presets[size])
+    kw.update(rope_theta=500000.0, rms_norm_eps=1e-5, hidden_act="silu", attention_dropout=0.0, attention_bias=False,
+              mlp_bias=False, torch_dtype="float32")
+    kw.update(overrides)
+    return LlamaConfig(**kw)
+
+
+def build_llama(size: str = "tiny", device="cuda", dtype=torch.float32, seed: int = 0, **overrides):
+    from transformers import LlamaForCausalLM
+
+    torch.manual_seed(seed)
+    cfg = llama_config(size, **overrides)
+    with torch.device(device):
+        model = LlamaForCausalLM(cfg)
+    return model.to(dtype)
+
+
+def build_llama_critic(size: str = "tiny", device="cuda", dtype=torch.float32, seed: int = 0, **overrides):
+    """Llama value model as the reference builds its critic (fsdp_workers.py:1018-1031)."""
+    from transformers import LlamaForTokenClassification
+
+    torch.manual_seed(seed)
+    cfg = llama_config(size, **overrides)
+    cfg.num_labels = 1
+    cfg.classifier_dropout = 0.0
+    with torch.device(device):
+        model = LlamaForTokenClassification(cfg)
+    return model.to(dtype)
+
+
 def build_qwen2_critic(size: str = "0.5b", device="cuda", dtype=torch.float32, seed: int = 0, **overrides):
     """The reference's critic: AutoModelForTokenClassification with num_labels = 1 and
     classifier_dropout = 0 (fsdp_workers.py:1018-1031) on the Qwen2 architecture, random init."""

@@ -45,6 +45,13 @@ logger.setLevel(os.getenv("VERL_LOGGING_LEVEL", "WARN"))
 _NO_MASK = {"full_attention": None, "sliding_attention": None}
 
 
+def packed_mask_arg(backbone):
+    """attention_mask argument for an HF backbone run on packed tokens with the registered varlen
+    attention: Qwen2 takes a per-layer-type mask mapping (None everywhere skips mask creation),
+    other decoders (Llama) take None, which the registered no-op mask function keeps None."""
+    return _NO_MASK if getattr(backbone.config, "model_type", "") == "qwen2" else None
+
+
 def append_to_dict(data: dict, new_data: dict):
     for k, v in new_data.items():
         data.setdefault(k, []).append(v)
@@ -192,7 +199,8 @@ class DataParallelPPOActor(BasePPOActor):
                                             attn_kblocks=packing.attn_kblocks if fa else None)
                 else:
                     out = self._backbone(
-                        input_ids=ids, position_ids=pos, attention_mask=_NO_MASK, use_cache=False,
+                        input_ids=ids, position_ids=pos, attention_mask=packed_mask_arg(self._backbone),
+                        use_cache=False,
                         cu_seq_lens_q=packing.cu_seqlens, cu_seq_lens_k=packing.cu_seqlens,
                         max_length_q=packing.max_seqlen, max_length_k=packing.max_seqlen,
                     )

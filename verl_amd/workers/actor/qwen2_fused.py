@@ -32,19 +32,36 @@ from ... import kernels as K
 from . import attention
 
 
-def supports(backbone: torch.nn.Module) -> bool:
+def _decoder_families():
+    """HF decoder stacks with the Qwen2 layer structure (RMSNorm, q/k/v/o projections with optional
+    biases, rotate_half RoPE from the model's own rotary_emb, GQA, gate/up/down SiLU MLP): Qwen2 /
+    Qwen2.5 and Llama (incl. Llama-3's rope scaling: cos / sin come from the model's rotary_emb)."""
+    fams = []
     try:
-        from transformers.models.qwen2 import modeling_qwen2 as m
+        from transformers.models.qwen2 import modeling_qwen2
+
+        fams.append(modeling_qwen2.Qwen2Model)
     except ImportError:  # pragma: no cover
-        return False
-    if not isinstance(backbone, m.Qwen2Model):
+        pass
+    try:
+        from transformers.models.llama import modeling_llama
+
+        fams.append(modeling_llama.LlamaModel)
+    except ImportError:  # pragma: no cover
+        pass
+    return tuple(fams)
+
+
+def supports(backbone: torch.nn.Module) -> bool:
+    fams = _decoder_families()
+    if not fams or not isinstance(backbone, fams):
         return False
     cfg = backbone.config
     if getattr(cfg, "hidden_act", "silu") != "silu" or getattr(cfg, "use_sliding_window", False):
         return False
-    if getattr(cfg, "rope_scaling", None) not in (None, {}) and \
-            (cfg.rope_scaling or {}).get("rope_type", "default") != "default":
-        return False
+    rope = (getattr(cfg, "rope_scaling", None) or {})
+    if rope.get("rope_type", rope.get("type", "default")) in ("mrope", "longrope"):
+        return False  # multimodal / per-position factor tables: keep the HF forward
     h = cfg.hidden_size
     if h % 8 or h > 4096:
         return False

@@ -26,7 +26,7 @@ from ... import kernels as K
 from ...protocol import DataProto
 from ...utils.seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
 from ..actor import attention
-from ..actor.dp_actor import _NO_MASK, _plan_packing, _to_host, append_to_dict
+from ..actor.dp_actor import _plan_packing, _to_host, append_to_dict, packed_mask_arg
 from .base import BasePPOCritic
 
 __all__ = ["DataParallelPPOCritic"]
@@ -93,7 +93,8 @@ class DataParallelPPOCritic(BasePPOCritic):
                                             attn_kblocks=packing.attn_kblocks if fa else None)
                 else:
                     out = self._backbone(
-                        input_ids=ids.unsqueeze(0), position_ids=pos.unsqueeze(0), attention_mask=_NO_MASK,
+                        input_ids=ids.unsqueeze(0), position_ids=pos.unsqueeze(0),
+                        attention_mask=packed_mask_arg(self._backbone),
                         use_cache=False, cu_seq_lens_q=packing.cu_seqlens, cu_seq_lens_k=packing.cu_seqlens,
                         max_length_q=packing.max_seqlen, max_length_k=packing.max_seqlen,
                     )
