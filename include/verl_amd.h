@@ -122,12 +122,16 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   bwd 16-B vectors per lane per workgroup chunk 0: 4, 1: 2, 2: 8;
  *   VA_TUNE_FLASH_GROUPED_DKDV (va_flash_attn_bwd): -1 = auto, 0 = per-query-head fp32 partials +
  *   fixed-order group sum, 1 = one workgroup per key block x KV head summing its group in registers
- *   (results differ only in fp32 summation order). */
+ *   (results differ only in fp32 summation order);
+ *   VA_TUNE_GAE_VARIANT (va_gae_scan): 0 = auto, 1 = register chunks (rows of R <= 1024 only;
+ *   longer rows keep the LDS kernel), 2 = LDS-staged kernel (advantages/returns bitwise identical,
+ *   the fp64 row partials differ only in summation order). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3
 #define VA_TUNE_PIPELINE 4
 #define VA_TUNE_FLASH_GROUPED_DKDV 5
+#define VA_TUNE_GAE_VARIANT 6
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

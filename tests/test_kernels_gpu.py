@@ -311,7 +311,7 @@ def test_rloo_matches_oracle(K):
     _close(got, want, atol=1e-5, rtol=1e-5, what="rloo")
 
 
-@pytest.mark.parametrize("R", [1, 17, 256, 1024, 3000, 20000])
+@pytest.mark.parametrize("R", [1, 17, 64, 65, 256, 513, 1024, 1025, 3000, 20000])
 @pytest.mark.parametrize("gamma,lam", [(1.0, 1.0), (0.99, 0.95)])
 def test_gae_matches_oracle(K, R, gamma, lam):
     torch.manual_seed(R)
@@ -329,6 +329,28 @@ def test_gae_matches_oracle(K, R, gamma, lam):
     tol = 1e-4 * max(1.0, float(np.sqrt(R) / 8))
     _close(ret, want_ret, atol=tol, rtol=1e-4, what="gae returns")
     _close(adv, want_adv, atol=tol, rtol=1e-4, what="gae advantages")
+
+
+@pytest.mark.parametrize("B,R", [(7, 1), (33, 65), (512, 1024), (9, 1000)])
+def test_gae_register_and_lds_kernels_agree(K, B, R):
+    """The register-chunk and LDS-staged scans use the same chunking and op order: returns are
+    bitwise equal; whitened advantages differ at most by the fp64 partials' summation order."""
+    from verl_amd import _lib as L
+
+    torch.manual_seed(B + R)
+    rewards = (torch.randn(B, R) * (torch.rand(B, R) > 0.9)).to(DEV)
+    values = torch.randn(B, R).to(DEV)
+    lens = torch.randint(1, R + 1, (B,))
+    mask = (torch.arange(R)[None, :] < lens[:, None]).to(torch.int64).to(DEV)
+    outs = []
+    try:
+        for variant in (1, 2):
+            L.call("va_set_tuning", L.VA_TUNE_GAE_VARIANT, variant)
+            outs.append(K.gae_advantage_return(rewards, values, mask, 0.99, 0.95))
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_GAE_VARIANT, 0)
+    assert torch.equal(outs[0][1], outs[1][1])
+    _close(outs[0][0], outs[1][0].cpu(), atol=1e-6, rtol=1e-6, what="gae adv reg vs lds")
 
 
 def test_gae_multi_turn_property(K):

@@ -188,6 +188,12 @@ def main():
             res.append(report(f"gae_whiten_{tag}_i64mask", B * R * (4 + 4 + 8 + 4 + 4 + 4 + 4), med, mn, copy_gbps))
             med, mn = timeit(lambda: gae(mask_u8, L.VA_MASK_U8), args.iters)
             res.append(report(f"gae_whiten_{tag}_u8mask", B * R * (4 + 4 + 1 + 4 + 4 + 4 + 4), med, mn, copy_gbps))
+            for variant, vname in ((1, "reg"), (2, "lds")):  # A/B of the scan kernels (VA_TUNE_GAE_VARIANT)
+                L.call("va_set_tuning", L.VA_TUNE_GAE_VARIANT, variant)
+                med, mn = timeit(gae, args.iters)
+                res.append(report(f"gae_whiten_{tag}_i64mask_{vname}", B * R * (4 + 4 + 8 + 4 + 4 + 4 + 4), med, mn,
+                                  copy_gbps))
+            L.call("va_set_tuning", L.VA_TUNE_GAE_VARIANT, 0)
             old = -torch.rand(B, R, device=dev)
             new = old + 0.05 * torch.randn(B, R, device=dev)
             refl = old + 0.1 * torch.randn(B, R, device=dev)

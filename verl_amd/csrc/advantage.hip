@@ -164,6 +164,102 @@ __device__ __forceinline__ Aff compose(const Aff &second, const Aff &first) {
   return r;
 }
 
+// Register variant for rows of R <= 64 * 16 steps: lane k owns steps [k L, (k + 1) L) as in the
+// LDS kernel (same chunking, so the same arithmetic), but loads its chunk straight into registers
+// with every load independent and issued before the first use (the LDS kernel's strided staging
+// loop waits on each round trip), scans, and stores from registers.
+template <int MT, int LM>
+__global__ __launch_bounds__(256) void gae_scan_reg_kernel(
+    const float *__restrict__ rew, const float *__restrict__ val, const void *__restrict__ mask,
+    int64_t B, int64_t R, int L, float gamma, float gl, float *__restrict__ adv_raw,
+    float *__restrict__ ret, double *__restrict__ part) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + wave;
+  if (row >= B) return;  // waves are independent: no workgroup barrier below
+  const int64_t base = row * R;
+  const int64_t t0 = static_cast<int64_t>(lane) * L;
+  float r[LM], v[LM], m[LM];
+#pragma unroll
+  for (int i = 0; i < LM; ++i) {
+    const bool ok = i < L && t0 + i < R;
+    const int64_t t = ok ? t0 + i : 0;  // clamped address: the loads need no branch
+    const float rr = rew[base + t], vv = val[base + t], mm = load_mask<MT>(mask, base + t);
+    r[i] = ok ? rr : 0.f;
+    v[i] = ok ? vv : 0.f;
+    m[i] = ok ? mm : 0.f;
+  }
+  // 1) the chunk's affine map, steps from the chunk's end down to t0
+  Aff F{1.f, 0.f, 1.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = LM - 1; i >= 0; --i) {
+    if (i < L && t0 + i < R) {
+      Aff st;
+      st.a = m[i] * gl + (1.f - m[i]);
+      st.c = m[i] * gamma;
+      st.e = 1.f - m[i];
+      st.b1 = m[i] * (r[i] - v[i]);
+      st.b2 = m[i] * v[i];
+      F = compose(st, F);
+    }
+  }
+  // 2) reverse inclusive scan over lanes (as gae_scan_kernel)
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    Aff nb;
+    nb.a = __shfl_down(F.a, o, kWave);
+    nb.c = __shfl_down(F.c, o, kWave);
+    nb.e = __shfl_down(F.e, o, kWave);
+    nb.b1 = __shfl_down(F.b1, o, kWave);
+    nb.b2 = __shfl_down(F.b2, o, kWave);
+    if (lane + o < 64) F = compose(F, nb);
+  }
+  float g = __shfl_down(F.b1, 1, kWave);
+  float nv = __shfl_down(F.b2, 1, kWave);
+  if (lane == 63) {
+    g = 0.f;
+    nv = 0.f;
+  }
+  // 3) re-run the chunk in the reference op order (core_algos.py:229-236); r[i] <- g
+#pragma unroll
+  for (int i = LM - 1; i >= 0; --i) {
+    if (i < L && t0 + i < R) {
+      const float delta = (r[i] + gamma * nv) - v[i];
+      const float gnew = delta + gl * g;
+      nv = v[i] * m[i] + (1.f - m[i]) * nv;
+      g = gnew * m[i] + (1.f - m[i]) * g;
+      r[i] = g;
+    }
+  }
+  // 4) stores + row partials (n, sum, M2) of g over the mask
+  double n = 0.0, sum = 0.0;
+#pragma unroll
+  for (int i = 0; i < LM; ++i) {
+    if (i < L && t0 + i < R) {
+      adv_raw[base + t0 + i] = r[i];
+      ret[base + t0 + i] = r[i] + v[i];
+      n += m[i];
+      sum += static_cast<double>((m[i] != 0.f ? r[i] : 0.f) * m[i]);
+    }
+  }
+  n = wave_sum(n);
+  sum = wave_sum(sum);
+  const double mu = n > 0.0 ? sum / n : 0.0;
+  double m2 = 0.0;
+#pragma unroll
+  for (int i = 0; i < LM; ++i) {
+    if (i < L && t0 + i < R && m[i] != 0.f) {
+      const double d = static_cast<double>(r[i]) - mu;
+      m2 += static_cast<double>(m[i]) * d * d;
+    }
+  }
+  m2 = wave_sum(m2);
+  if (lane == 0) {
+    part[row * kPartStride + 0] = n;
+    part[row * kPartStride + 1] = sum;
+    part[row * kPartStride + 2] = m2;
+  }
+}
+
 template <int MT, bool LDS>
 __global__ __launch_bounds__(256) void gae_scan_kernel(
     const float *__restrict__ rew, const float *__restrict__ val, const void *__restrict__ mask,
@@ -182,11 +278,28 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(
   auto pidx = [L](int64_t t) -> int { return static_cast<int>((t / L) * (L + 1) + t % L); };
 
   if constexpr (LDS) {
-    for (int64_t t = lane; t < R; t += kWave) {
-      const int p = pidx(t);
-      sr[p] = rew[base + t];
-      sv[p] = val[base + t];
-      sm[p] = load_mask<MT>(mask, base + t);
+    // coalesced staging in batches of 8 row segments: the batch's 24 loads are all issued before
+    // the first LDS write waits on them (one memory round trip per batch, not per segment)
+    for (int64_t b0 = 0; b0 < R; b0 += 8 * kWave) {
+      float rr[8], vv[8], mm[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t t = b0 + j * kWave + lane;
+        const int64_t tc = t < R ? t : R - 1;  // clamped: no branch around the loads
+        rr[j] = rew[base + tc];
+        vv[j] = val[base + tc];
+        mm[j] = load_mask<MT>(mask, base + tc);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t t = b0 + j * kWave + lane;
+        if (t < R) {
+          const int p = pidx(t);
+          sr[p] = rr[j];
+          sv[p] = vv[j];
+          sm[p] = mm[j];
+        }
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -495,6 +608,9 @@ extern "C" int64_t va_gae_workspace_bytes(int64_t B) {
   return static_cast<int64_t>(sizeof(double)) * (B * kPartStride + 4);
 }
 
+// va_set_tuning(VA_TUNE_GAE_VARIANT): 0 auto, 1 register kernel (only where L <= 16), 2 LDS kernel
+int g_gae_variant = 0;
+
 extern "C" int va_gae_scan(const float *rewards, const float *values, const void *mask,
                            int mask_dtype, int64_t B, int64_t R, float gamma, float lam,
                            float *adv_raw, float *ret, double *row_partials, void *stream) {
@@ -505,6 +621,23 @@ extern "C" int va_gae_scan(const float *rewards, const float *values, const void
   const int L = static_cast<int>((R + 63) / 64);
   // gamma * lam is a Python-float product in the reference, applied as an fp32 scalar
   const float gl = static_cast<float>(static_cast<double>(gamma) * static_cast<double>(lam));
+  // register chunks for short rows of small batches (latency: one round trip, no LDS); many rows
+  // stream better through the coalesced LDS staging (lane-chunk loads touch 64 lines per
+  // instruction)
+  const bool reg = L <= 16 && (g_gae_variant == 1 || (g_gae_variant == 0 && B * R <= (1LL << 20)));
+  if (reg) {
+    const dim3 block(256), grid(static_cast<unsigned>((B + 3) / 4));
+#define VA_GAE_REG(LMV)                                                                              \
+  hipLaunchKernelGGL((gae_scan_reg_kernel<MT, LMV>), grid, block, 0, s, rewards, values, mask, B, R, L, \
+                     gamma, gl, adv_raw, ret, row_partials)
+    VA_DISPATCH_MASK(mask_dtype, {
+      if (L <= 4) VA_GAE_REG(4);
+      else if (L <= 8) VA_GAE_REG(8);
+      else VA_GAE_REG(16);
+    });
+#undef VA_GAE_REG
+    return check_launch("gae_scan");
+  }
   int waves = 4;
   while (waves > 1 && gae_lds_bytes(L, waves) > 160 * 1024) waves >>= 1;
   const bool use_lds = gae_lds_bytes(L, waves) <= 160 * 1024;
