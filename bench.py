@@ -169,10 +169,10 @@ def main():
     from verl_amd.utils.config import AttrDict, actor_config
     from verl_amd.utils.model import build_qwen2
     from verl_amd.utils.synthetic import make_grpo_batch
-    from verl_amd.workers.dp_workers import ActorWorker, init_distributed
+    from verl_amd.workers.dp_workers import ActorWorker, init_distributed, local_device_index
 
     rank, world = init_distributed()
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local_device_index()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world != args.gpus and rank == 0:

@@ -22,18 +22,28 @@ from .grad_sync import GradBucketReducer, MixedPrecisionParams
 
 
 def init_distributed(backend: str | None = None) -> tuple[int, int]:
-    """fsdp_workers.py:118-126: init the process group from the torchrun env (127.0.0.1)."""
+    """fsdp_workers.py:118-126: init the process group from the torchrun env (127.0.0.1).
+
+    ``VA_DIST_BACKEND`` overrides the backend (``gloo`` lets several ranks share one GPU for a
+    rehearsal of the multi-rank path; RCCL needs one GPU per rank)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+            backend = os.environ.get("VA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        local = local_device_index()
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 device_id=torch.device("cuda", local) if backend == "nccl" else None)
     return rank, world
+
+
+def local_device_index() -> int:
+    """LOCAL_RANK folded onto the visible GPUs (more ranks than GPUs only under VA_DIST_BACKEND=gloo)."""
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n = torch.cuda.device_count()  # counts devices without initialising HIP
+    return local % n if n > 0 else local
 
 
 def dispatch_dp_compute_data_proto(data: DataProto, world_size: int) -> list[DataProto]:
