@@ -35,30 +35,43 @@ def pmc_traffic(kernel: str, algo_bytes_per_launch: float, vocab: int):
     MI355X_MICROARCH.md §HBM corrections) of the same kernel, scaled to this launch's rows."""
     import glob
 
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_logprob.json")))
-    if not paths:
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_logprob*.json")))
+    cands = []
+    for p in paths:
+        d = json.load(open(p))
+        k = d["kernels"].get(kernel)
+        if k is None or d.get("vocab") != vocab:
+            continue
+        rows = algo_bytes_per_launch / (k["algo_bytes"] / d["rows_per_launch"])
+        cands.append((abs(d["rows_per_launch"] - rows), -len(cands), k, rows, p))
+    if not cands:
         return None, None
-    d = json.load(open(paths[-1]))
-    k = d["kernels"].get(kernel)
-    if k is None or d.get("vocab") != vocab:
-        return None, None
-    per_row_algo = k["algo_bytes"] / d["rows_per_launch"]
-    rows = algo_bytes_per_launch / per_row_algo
-    return k["traffic_bytes_per_row"] * rows, os.path.relpath(paths[-1], ROOT)
+    # the pass measured at this launch's own row count when there is one (else scaled per row)
+    _, _, k, rows, p = min(cands, key=lambda c: (c[0], c[1]))
+    return k["traffic_bytes_per_row"] * rows, os.path.relpath(p, ROOT)
 
 
-def hbm_ceiling(kernel: str):
+def hbm_ceiling(kernel: str, rows: int | None = None, inplace: bool = False):
     """Best plain-streaming rate measured on MI355X at the same footprint (tools/hbm_stream.hip,
-    profiles/r*/hbm_stream_*rows.jsonl): read-only for the forward, read+write for the backward."""
+    profiles/r*/hbm_stream_<rows>rows.jsonl, the file of the launch's own row count when present):
+    read-only for the forward, read+write (in place when the backward writes over its input) for
+    the backward."""
     import glob
+    import re
 
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "hbm_stream_*rows.jsonl")))
     if not paths:
         return None, None
-    mode = "read" if kernel.endswith("fwd") else "copy"
-    rows = [json.loads(line) for line in open(paths[-1]) if line.startswith("{")]
-    best = max((r["gbps"] for r in rows if r["mode"] == mode), default=None)
-    return best, os.path.relpath(paths[-1], ROOT)
+
+    def nrows(p):
+        m = re.search(r"hbm_stream_(\d+)rows", p)
+        return int(m.group(1)) if m else 0
+
+    path = min(paths, key=lambda p: (abs(nrows(p) - rows) if rows else 0, -paths.index(p)))
+    mode = "read" if kernel.endswith("fwd") else ("copy_inplace" if inplace else "copy")
+    recs = [json.loads(line) for line in open(path) if line.startswith("{")]
+    best = max((r["gbps"] for r in recs if r["mode"] == mode), default=None)
+    return best, os.path.relpath(path, ROOT)
 
 
 def _gemm_table_name():
@@ -85,6 +98,8 @@ def parse():
     ap.add_argument("--gemm-table", default="default",
                     help="tuned GEMM solution table (verl_amd/tuned/*.csv, 'default', or 'none')")
     ap.add_argument("--model", default="0.5b")
+    ap.add_argument("--logprob-inplace-bwd", type=int, default=0,
+                    help="1: dlogits over the logits (reference's inplace_backward); 0: fresh buffer (faster stream)")
     ap.add_argument("--no-rmpad", action="store_true")
     ap.add_argument("--no-mixed-precision", action="store_true", help="fp32 weights + autocast instead of bf16/fp32-master")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -189,6 +204,7 @@ def main():
             use_remove_padding=not args.no_rmpad,
             use_dynamic_bsz=args.dynamic_bsz > 0, ppo_max_token_len_per_gpu=args.dynamic_bsz or 16384,
             pack_pad_multiple=args.pad_multiple,
+            logprob_inplace_backward=bool(args.logprob_inplace_bwd),
             gemm_tuning_file=None if args.gemm_table in (None, "none") else args.gemm_table,
         ),
         rollout=AttrDict(log_prob_micro_batch_size_per_gpu=args.logprob_micro, temperature=1.0,
@@ -273,7 +289,8 @@ def main():
                 }
             else:
                 traffic, src = pmc_traffic(name, d["avg_bytes"], 151936)
-                ceil, ceil_src = hbm_ceiling(name)
+                per_row = 2 * 2 * 151936 + 28 if name.endswith("bwd") else 2 * 151936 + 20  # bf16 rows
+                ceil, ceil_src = hbm_ceiling(name, round(d["avg_bytes"] / per_row), bool(args.logprob_inplace_bwd))
                 roof = {
                     "kernel": name,
                     "bound": "hbm",
@@ -317,6 +334,7 @@ def main():
                 "dynamic_bsz_max_token_len": args.dynamic_bsz or None,
                 "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
                 "pack_pad_multiple": args.pad_multiple,
+                "logprob_inplace_backward": bool(args.logprob_inplace_bwd),
                 "gemm_table": _gemm_table_name(),
                 "parallelism": f"dp{world}",
                 "remove_padding": not args.no_rmpad,
