@@ -125,13 +125,17 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   (results differ only in fp32 summation order);
  *   VA_TUNE_GAE_VARIANT (va_gae_scan): 0 = auto, 1 = register chunks (rows of R <= 1024 only;
  *   longer rows keep the LDS kernel), 2 = LDS-staged kernel (advantages/returns bitwise identical,
- *   the fp64 row partials differ only in summation order). */
+ *   the fp64 row partials differ only in summation order);
+ *   VA_TUNE_BWD_FLAT (va_logprob_entropy_bwd): -1 = auto (one flat stream of equal 16-KB chunks over
+ *   the whole tensor when logits and dlogits are dense, row stride = vocab), 0 = per-row chunks
+ *   (bitwise identical results). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3
 #define VA_TUNE_PIPELINE 4
 #define VA_TUNE_FLASH_GROUPED_DKDV 5
 #define VA_TUNE_GAE_VARIANT 6
+#define VA_TUNE_BWD_FLAT 7
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

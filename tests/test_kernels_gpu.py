@@ -109,6 +109,43 @@ def test_logprob_entropy_bwd(K, dtype, temperature, with_entropy_grad):
         _close(got, want, atol=2e-3 * scale, rtol=1e-2, what="dlogits bf16")
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,V", [(1, 151936), (7, 151936), (5, 8200), (9, 8192), (3, 32000), (2, 4100)])
+@pytest.mark.parametrize("temperature,ent_grad", [(1.0, False), (0.7, True)])
+def test_logprob_bwd_flat_matches_per_row(K, dtype, n, V, temperature, ent_grad):
+    """The flat-stream backward (equal chunks over the whole dense tensor) and the per-row-chunk
+    backward compute each element identically: bitwise equal dlogits, including ignore_index
+    (-100) and out-of-range labels, the label sitting in a chunk that straddles two rows, and V
+    too narrow for the flat path (falls back)."""
+    from verl_amd import _lib as L
+
+    torch.manual_seed(n * 7 + V)
+    base = (torch.randn(n, V) * 2.0).to(dtype).to(DEV)
+    labels = torch.randint(0, V, (n,))
+    if n > 2:
+        labels[1] = -100
+        labels[2] = V + 5
+    labels[0] = V - 1
+    labels = labels.to(DEV)
+    g_lp = torch.randn(n, device=DEV)
+    g_h = torch.randn(n, device=DEV) if ent_grad else None
+    grads = []
+    try:
+        for flat in (-1, 0):
+            L.call("va_set_tuning", L.VA_TUNE_BWD_FLAT, flat)
+            x = base.clone().requires_grad_(True)
+            lp, h = K.logprob_entropy(x, labels, temperature)
+            out = (torch.nan_to_num(lp) * g_lp).sum()
+            if g_h is not None:
+                out = out + (h * g_h).sum()
+            out.backward()
+            grads.append(x.grad)
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_BWD_FLAT, -1)
+    assert torch.equal(torch.isnan(grads[0]), torch.isnan(grads[1]))
+    assert torch.equal(torch.nan_to_num(grads[0]), torch.nan_to_num(grads[1]))
+
+
 def test_logprob_inplace_backward(K):
     torch.manual_seed(3)
     n, V = 8, 4096

@@ -52,6 +52,41 @@ def report(name, nbytes, med_ms, min_ms, copy_gbps, extra=None):
     return d
 
 
+def bwd_ab(args, src, rounds=6):
+    """Interleaved A/B of the log-prob backward: flat stream vs per-row chunks, out of place vs
+    in place, 4 vs 8 vectors per lane (guide rule 24: interleave, report medians)."""
+    dev = src.device
+    x = src.view(args.rows, args.vocab)
+    labels = torch.randint(0, args.vocab, (args.rows,), device=dev)
+    lp, ent, lse = (torch.empty(args.rows, device=dev) for _ in range(3))
+    g1 = torch.randn(args.rows, device=dev)
+    dx = torch.empty_like(x)
+    lib = L.load()
+    st = K._stream(x)
+    L.call("va_logprob_entropy_fwd", K._p(x), L.VA_BF16, args.rows, args.vocab, args.vocab, K._p(labels), 1.0,
+           K._p(lp), K._p(ent), K._p(lse), st)
+
+    def bwd(out):
+        L.call("va_logprob_entropy_bwd", K._p(g1), None, K._p(x), L.VA_BF16, args.rows, args.vocab, args.vocab,
+               K._p(labels), K._p(lse), K._p(ent), 1.0, K._p(out), args.vocab, st)
+
+    variants = [(flat, ip, pipe) for flat in (-1, 0) for ip in (0, 1) for pipe in (0, 2)]
+    times = {v: [] for v in variants}
+    for _ in range(rounds):
+        for flat, ip, pipe in variants:
+            lib.va_set_tuning(L.VA_TUNE_BWD_FLAT, flat)
+            lib.va_set_tuning(L.VA_TUNE_PIPELINE, pipe)
+            times[(flat, ip, pipe)].append(timeit(lambda: bwd(x if ip else dx), 4, warmup=1)[0])
+    lib.va_set_tuning(L.VA_TUNE_BWD_FLAT, -1)
+    lib.va_set_tuning(L.VA_TUNE_PIPELINE, 0)
+    bb = args.rows * (4 * args.vocab + 28)
+    for (flat, ip, pipe), ts in times.items():
+        med = float(np.median(ts))
+        print(json.dumps(dict(kernel=f"bwd_{'flat' if flat else 'rows'}_{'inplace' if ip else 'outplace'}_u{8 if pipe else 4}",
+                              rows=args.rows, median_us=round(med * 1e3, 1), min_us=round(min(ts) * 1e3, 1),
+                              gbps=round(bb / (med * 1e-3) / 1e9, 1))), flush=True)
+
+
 def sweep(args, src, copy_gbps):
     """Interleaved A/B of waves-per-row x non-temporal for fwd and bwd (guide rule 24)."""
     dev = src.device
@@ -102,6 +137,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="all")
     ap.add_argument("--sweep", action="store_true", help="A/B the log-prob launch shapes (interleaved rounds)")
+    ap.add_argument("--bwd-ab", action="store_true", help="A/B the log-prob backward layouts (interleaved rounds)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -118,6 +154,9 @@ def main():
 
     if args.sweep:
         sweep(args, src, copy_gbps)
+        return
+    if args.bwd_ab:
+        bwd_ab(args, src)
         return
 
     if args.only in ("all", "logprob"):
@@ -148,6 +187,12 @@ def main():
 
         med, mn = timeit(bwd, args.iters)
         res.append(report("logprob_entropy_bwd", bwd_bytes, med, mn, copy_gbps, dict(rows=args.rows, vocab=args.vocab)))
+        L.call("va_set_tuning", L.VA_TUNE_BWD_FLAT, 0)  # A/B: per-row chunks
+        med, mn = timeit(bwd, args.iters)
+        res.append(report("logprob_entropy_bwd_rowchunks", bwd_bytes, med, mn, copy_gbps))
+        L.call("va_set_tuning", L.VA_TUNE_BWD_FLAT, -1)
+        med, mn = timeit(bwd, args.iters)
+        res.append(report("logprob_entropy_bwd_flat_again", bwd_bytes, med, mn, copy_gbps))
 
         def bwd_inplace():
             L.call("va_logprob_entropy_bwd", K._p(g1), None, K._p(x), L.VA_BF16, args.rows, args.vocab, args.vocab,

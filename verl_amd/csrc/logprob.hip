@@ -445,10 +445,85 @@ __global__ __launch_bounds__(256) void logprob_entropy_bwd_kernel(
   }
 }
 
+// Flat variant for dense [n_rows, V] logits and dlogits (stride = dstride = V, V a multiple of the
+// 16-B vector, V >= one workgroup chunk): the whole tensor is one stream of 16-B vectors cut into
+// equal 256 x U-vector chunks, so no workgroup carries a row's partial last chunk (the per-row
+// variant launches 19 chunks per 151,936-wide bf16 row, the last one 55 % full). A chunk spans at
+// most two rows: their scalars are two uniform loads each, the lane picks by its vector index.
+// Per element the arithmetic is the per-row kernel's (bitwise identical results).
+template <typename T, bool SCALE, bool NT, int U>
+__global__ __launch_bounds__(256) void logprob_entropy_bwd_flat_kernel(
+    const float *__restrict__ g_logp, const float *__restrict__ g_ent, const T *logits, int64_t n_rows,
+    int64_t V, const int64_t *__restrict__ labels, const float *__restrict__ lse_in,
+    const float *__restrict__ ent_in, float temperature, T *dlogits) {
+  using E = Elem<T>;
+  constexpr int VEC = E::kVec;
+  const int64_t nvec_row = V / VEC, nvec = n_rows * nvec_row;
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * (256 * U);  // first vector of the chunk
+  const int64_t r0 = c0 / nvec_row;                                    // wave-uniform
+  const int64_t split = (r0 + 1) * nvec_row;                           // first vector of row r0 + 1
+  const bool two = split < nvec && split < c0 + 256 * U;
+  const u32x4 *xv = reinterpret_cast<const u32x4 *>(logits);
+  u32x4 *dv = reinterpret_cast<u32x4 *>(dlogits);
+
+  u32x4 raw[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) raw[u] = vload<NT>(xv + min(c0 + u * 256 + threadIdx.x, nvec - 1));
+
+  // the (up to) two rows' scalars (as the per-row kernel derives them)
+  float glp_r[2], gh_r[2], kk_r[2], nlb_r[2];
+  int64_t lab_r[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t row = (j == 1 && two) ? r0 + 1 : r0;
+    const int64_t lab = labels[row];
+    const bool has_lab = (lab >= 0 && lab < V);
+    const float glp = (g_logp != nullptr && has_lab) ? g_logp[row] : 0.f;
+    const float gh = (g_ent != nullptr) ? g_ent[row] : 0.f;
+    const float lse = lse_in[row];
+    const float h = (g_ent != nullptr) ? ent_in[row] : 0.f;
+    glp_r[j] = glp;
+    gh_r[j] = gh;
+    kk_r[j] = fmaf(gh, h - lse, glp);
+    nlb_r[j] = -lse * kLog2e;
+    lab_r[j] = has_lab ? row * nvec_row * VEC + lab : -1;  // flat element index of the label
+  }
+
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = c0 + u * 256 + threadIdx.x;
+    if (i >= nvec) continue;
+    const int j = (two && i >= split) ? 1 : 0;
+    const float gh = j ? gh_r[1] : gh_r[0], kk = j ? kk_r[1] : kk_r[0], nlb = j ? nlb_r[1] : nlb_r[0];
+    float x[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      float z = elem<T>(raw[u], k);
+      if constexpr (SCALE) z = E::scale(z, temperature);
+      const float p = __builtin_amdgcn_exp2f(fmaf(z, kLog2e, nlb));
+      x[k] = -p * fmaf(gh, z, kk);
+    }
+    const int64_t lab = j ? lab_r[1] : lab_r[0];
+    if (lab >= i * VEC && lab < (i + 1) * VEC) {  // one lane per row
+      const int lk = static_cast<int>(lab - i * VEC);
+      const float glp = j ? glp_r[1] : glp_r[0];
+#pragma unroll
+      for (int k = 0; k < VEC; ++k)
+        if (k == lk) x[k] += glp;
+    }
+    if constexpr (SCALE) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) x[k] = x[k] / temperature;
+    }
+    vstore<NT>(dv + i, pack_vec<T>(x));
+  }
+}
+
 // ---- tuning (va_set_tuning) ---------------------------------------------------------------
 int g_fwd_wpr = 0;  // 0 = auto
 int g_bwd_wpr = 0;
 int g_nt = -1;
+int g_bwd_flat = -1;  // -1 auto (flat stream where the layout allows), 0 per-row chunks
 int g_pipe = 0;  // 0: 4 vectors per lane, no pipeline; 1: 2+2 pipelined; 2: 4+4 pipelined  // -1 = auto (non-temporal on: +10-12% fwd, +1-2% bwd measured)
 
 int auto_wpr(int64_t n_rows, int64_t V, int override_wpr) {
@@ -537,6 +612,26 @@ int launch_bwd(const float *g_logp, const float *g_ent, const void *logits, int6
                    ((dstride * static_cast<int64_t>(sizeof(T))) % 16 == 0);
   const bool scale = (temperature != 1.0f);
   const bool nt = g_nt != 0;  // auto (-1) and 1 both select non-temporal
+  const int fu = g_pipe == 1 ? 2 : (g_pipe == 2 ? 8 : 4);  // vectors per lane, as the per-row path
+  const int64_t nvec_row = V / Elem<T>::kVec;
+  if (g_bwd_flat != 0 && vec && stride == V && dstride == V && V % Elem<T>::kVec == 0 &&
+      nvec_row >= 256 * fu) {
+    const int64_t chunks = (n_rows * nvec_row + 256 * fu - 1) / (256 * fu);
+    const dim3 block(256), grid(static_cast<unsigned>(chunks));
+#define VA_KF(S, NTV, UU)                                                                         \
+  hipLaunchKernelGGL((logprob_entropy_bwd_flat_kernel<T, S, NTV, UU>), grid, block, 0, stream, g_logp, \
+                     g_ent, x, n_rows, V, labels, lse, ent, temperature, d)
+#define VA_KFU(S, NTV) \
+  do { if (fu == 2) VA_KF(S, NTV, 2); else if (fu == 8) VA_KF(S, NTV, 8); else VA_KF(S, NTV, 4); } while (0)
+    if (scale) {
+      if (nt) VA_KFU(true, true); else VA_KFU(true, false);
+    } else {
+      if (nt) VA_KFU(false, true); else VA_KFU(false, false);
+    }
+#undef VA_KFU
+#undef VA_KF
+    return check_launch("logprob_entropy_bwd");
+  }
 #define VA_BWD(S, VV) \
   launch_bwd_u<T, S, VV>(g_logp, g_ent, x, n_rows, V, stride, labels, lse, ent, temperature, d, dstride, stream, nt)
   if (scale) {
@@ -623,6 +718,7 @@ extern "C" int va_set_tuning(int key, int value) {
     case VA_TUNE_PIPELINE: va::g_pipe = value; return VA_OK;
     case VA_TUNE_FLASH_GROUPED_DKDV: g_flash_grouped_dkdv = value; return VA_OK;
     case VA_TUNE_GAE_VARIANT: g_gae_variant = value; return VA_OK;
+    case VA_TUNE_BWD_FLAT: va::g_bwd_flat = value; return VA_OK;
     default: va::set_error("unknown tuning key %d", key); return VA_E_ARG;
   }
 }
