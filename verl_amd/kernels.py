@@ -758,6 +758,10 @@ def weight_grad(dy2, x2):
 
         if gemm_tuning.has_tuned("nt", n_in, n_out, T):
             s = 1
+    if s > 1 and (T // s) * max(n_out, n_in) >= 2**31:
+        # the batched GEMM's batch stride must fit int32 (hipBLASLt strided-batched); a slice this
+        # large already fills the chip on its own (tools/lm_head_wgrad_bench.py: wrong sums past it)
+        s = 1
     if s > 1:
         h = T // s
         main = s * h
