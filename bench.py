@@ -107,6 +107,8 @@ def parse():
     ap.add_argument("--cpu-sample-rows", type=int, default=24576,
                     help="response tokens of the CPU baseline's log-prob sample (~10 s on 16 cores)")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
+    ap.add_argument("--tune", action="append", default=[],
+                    help="KEY=VALUE va_set_tuning override for A/B runs (e.g. 8=0: grid-stride SwiGLU)")
     return ap.parse_args()
 
 
@@ -188,6 +190,12 @@ def main():
 
     rank, world = init_distributed()
     local = local_device_index()
+    if args.tune:
+        from verl_amd import _lib as L
+
+        for kv in args.tune:
+            key, val = (int(x) for x in kv.split("="))
+            L.call("va_set_tuning", key, val)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world != args.gpus and rank == 0:
@@ -335,6 +343,7 @@ def main():
                 "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
                 "pack_pad_multiple": args.pad_multiple,
                 "logprob_inplace_backward": bool(args.logprob_inplace_bwd),
+                "tuning_overrides": args.tune or None,
                 "gemm_table": _gemm_table_name(),
                 "parallelism": f"dp{world}",
                 "remove_padding": not args.no_rmpad,

@@ -128,7 +128,10 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   the fp64 row partials differ only in summation order);
  *   VA_TUNE_BWD_FLAT (va_logprob_entropy_bwd): -1 = auto (one flat stream of equal 16-KB chunks over
  *   the whole tensor when logits and dlogits are dense, row stride = vocab), 0 = per-row chunks
- *   (bitwise identical results). */
+ *   (bitwise identical results);
+ *   VA_TUNE_SWIGLU_STREAM (va_swiglu_fwd/bwd): -1 = auto (streaming kernels: 4 / 2 vectors per lane
+ *   fwd / bwd, all loads issued first, non-temporal), 2 / 4 / 8 = streaming with that many vectors
+ *   per lane, 0 = grid-stride kernels (bitwise identical results). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3
@@ -136,6 +139,7 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_FLASH_GROUPED_DKDV 5
 #define VA_TUNE_GAE_VARIANT 6
 #define VA_TUNE_BWD_FLAT 7
+#define VA_TUNE_SWIGLU_STREAM 8
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

@@ -67,6 +67,30 @@ def test_swiglu_matches_hf():
     _grad_close(ub.grad, ua.grad, "swiglu du")
 
 
+@pytest.mark.parametrize("T,F_", [(1, 8), (3, 4864), (517, 4864), (77, 2056), (1025, 64)])
+def test_swiglu_stream_matches_grid_stride(T, F_):
+    """The streaming SwiGLU kernels (VA_TUNE_SWIGLU_STREAM, default) and the grid-stride ones do
+    the same per-element arithmetic: bitwise equal y and merged d(gate|up), ragged tails included."""
+    from verl_amd import _lib as L
+    from verl_amd import kernels as K
+
+    torch.manual_seed(T + F_)
+    gu = (torch.randn(T, 2 * F_, device=DEV) * 2).to(torch.bfloat16)
+    d = torch.randn(T, F_, device=DEV).to(torch.bfloat16)
+    outs = []
+    try:
+        for v in (-1, 0):
+            L.call("va_set_tuning", L.VA_TUNE_SWIGLU_STREAM, v)
+            x = gu.clone().requires_grad_(True)
+            y = K.swiglu_merged(x)
+            y.backward(d)
+            outs.append((y.detach(), x.grad))
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_SWIGLU_STREAM, -1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 def test_add_rmsnorm_matches_hf():
     """Residual add + RMSNorm (Qwen2DecoderLayer: h = residual + x; norm(h)); both outputs and the
     gradient that reaches x / residual through h and through the norm."""

@@ -230,6 +230,86 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const uint16_t *__restr
   }
 }
 
+// Streaming variants (the default): no grid-stride loop; workgroup b owns the 256 x U consecutive
+// 16-B vectors [b 256 U, (b + 1) 256 U) of the [T, F/8] vector grid, lane-interleaved per u, and
+// issues every load of its U vectors before the first use (U x 2 or 3 16-B loads in flight per
+// lane instead of one iteration's 2-3), with non-temporal loads / stores: the operands are
+// streamed once and are far larger than the L2s / MALL. Per element the arithmetic is the
+// grid-stride kernels' (bitwise identical outputs).
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16nt(const uint16_t *p) {
+  return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4v *>(p)));
+}
+__device__ __forceinline__ void st16nt(uint16_t *p, uint4 v) {
+  __builtin_nontemporal_store(__builtin_bit_cast(u32x4v, v), reinterpret_cast<u32x4v *>(p));
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void swiglu_fwd_stream_kernel(const uint16_t *__restrict__ gu, int64_t ldgu,
+                                                                int64_t uoff, uint32_t total, uint32_t vpr,
+                                                                int F, uint16_t *__restrict__ y) {
+  const uint32_t i0 = blockIdx.x * (256u * U) + threadIdx.x;
+  uint4 rg[U], ru[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t idx = min(i0 + u * 256u, total - 1);  // clamped: no branch around the loads
+    const uint32_t t = idx / vpr, c = (idx - t * vpr) * 8;
+    const uint16_t *gr = gu + static_cast<int64_t>(t) * ldgu + c;
+    rg[u] = ld16nt(gr);
+    ru[u] = ld16nt(gr + uoff);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t idx = i0 + u * 256u;
+    if (idx >= total) continue;
+    const uint32_t t = idx / vpr, c = (idx - t * vpr) * 8;
+    float g8[8], u8[8], o[8];
+    unpack8(rg[u], g8);
+    unpack8(ru[u], u8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = rbf(silu(g8[e])) * u8[e];
+    st16nt(y + static_cast<int64_t>(t) * F + c, pack8(o));
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void swiglu_bwd_stream_kernel(const uint16_t *__restrict__ dy,
+                                                                const uint16_t *__restrict__ gu, int64_t ldgu,
+                                                                int64_t uoff, uint32_t total, uint32_t vpr, int F,
+                                                                uint16_t *__restrict__ dgu, int64_t lddgu,
+                                                                int64_t duoff) {
+  const uint32_t i0 = blockIdx.x * (256u * U) + threadIdx.x;
+  uint4 rd[U], rg[U], ru[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t idx = min(i0 + u * 256u, total - 1);
+    const uint32_t t = idx / vpr, c = (idx - t * vpr) * 8;
+    const uint16_t *gr = gu + static_cast<int64_t>(t) * ldgu + c;
+    rd[u] = ld16nt(dy + static_cast<int64_t>(t) * F + c);
+    rg[u] = ld16nt(gr);
+    ru[u] = ld16nt(gr + uoff);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t idx = i0 + u * 256u;
+    if (idx >= total) continue;
+    const uint32_t t = idx / vpr, c = (idx - t * vpr) * 8;
+    float d8[8], g8[8], u8[8], og[8], ou[8];
+    unpack8(rd[u], d8);
+    unpack8(rg[u], g8);
+    unpack8(ru[u], u8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float s = 1.f / (1.f + __expf(-g8[e]));
+      ou[e] = d8[e] * rbf(g8[e] * s);
+      og[e] = d8[e] * u8[e] * (s * (1.f + g8[e] * (1.f - s)));
+    }
+    uint16_t *dr = dgu + static_cast<int64_t>(t) * lddgu + c;
+    st16nt(dr, pack8(og));
+    st16nt(dr + duoff, pack8(ou));
+  }
+}
+
 // ------------------------------------------------------------------ RoPE on the merged q|k|v
 // thread = (token t, head in [0, Hq + 2 Hk), chunk c of 8 elements in the first half of D)
 __global__ __launch_bounds__(256) void rope_qkv_fwd_kernel(
@@ -330,6 +410,10 @@ int64_t bwd_rows_per_block(int64_t T) {
 
 using namespace va;
 
+// va_set_tuning(VA_TUNE_SWIGLU_STREAM): -1 auto = streaming kernels (4 / 2 vectors per lane fwd / bwd), 2 / 4 / 8 =
+// streaming with that many vectors per lane, 0 = grid-stride kernels
+int g_swiglu_variant = -1;
+
 #define VA_NV_DISPATCH(nv, CALL)                   \
   switch (nv) {                                    \
     case 1: { constexpr int NV = 1; CALL; break; } \
@@ -412,7 +496,19 @@ extern "C" int va_swiglu_fwd(const void *gu, int64_t ldgu, int64_t uoff, int dty
     set_error("swiglu: 16-byte aligned buffers required");
     return VA_E_ALIGN;
   }
-  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(T * (F / 8), 1)), dim3(256), 0,
+  const int64_t total = T * (F / 8);
+  if (g_swiglu_variant != 0 && total < (1LL << 31)) {
+    const int u = g_swiglu_variant > 0 ? g_swiglu_variant : 4;
+#define VA_SWF(U)                                                                                                  \
+  hipLaunchKernelGGL(swiglu_fwd_stream_kernel<U>, dim3(static_cast<unsigned>((total + 256 * U - 1) / (256 * U))), \
+                     dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const uint16_t *>(gu), ldgu, uoff, \
+                     static_cast<uint32_t>(total), static_cast<uint32_t>(F / 8), static_cast<int>(F),             \
+                     static_cast<uint16_t *>(y))
+    if (u == 2) VA_SWF(2); else if (u == 8) VA_SWF(8); else VA_SWF(4);
+#undef VA_SWF
+    return check_launch("swiglu_fwd");
+  }
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(total, 1)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), static_cast<const uint16_t *>(gu), ldgu, uoff, T,
                      static_cast<int>(F), static_cast<uint16_t *>(y));
   return check_launch("swiglu_fwd");
@@ -430,7 +526,19 @@ extern "C" int va_swiglu_bwd(const void *dy, const void *gu, int64_t ldgu, int64
     set_error("swiglu: 16-byte aligned buffers required");
     return VA_E_ALIGN;
   }
-  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(T * (F / 8), 1)), dim3(256), 0,
+  const int64_t total = T * (F / 8);
+  if (g_swiglu_variant != 0 && total < (1LL << 31)) {
+    const int u = g_swiglu_variant > 0 ? g_swiglu_variant : 2;  // 2: best bwd (tools/elemwise_ab.py)
+#define VA_SWB(U)                                                                                                  \
+  hipLaunchKernelGGL(swiglu_bwd_stream_kernel<U>, dim3(static_cast<unsigned>((total + 256 * U - 1) / (256 * U))), \
+                     dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const uint16_t *>(dy),             \
+                     static_cast<const uint16_t *>(gu), ldgu, uoff, static_cast<uint32_t>(total),                   \
+                     static_cast<uint32_t>(F / 8), static_cast<int>(F), static_cast<uint16_t *>(dgu), lddgu, duoff)
+    if (u == 2) VA_SWB(2); else if (u == 8) VA_SWB(8); else VA_SWB(4);
+#undef VA_SWB
+    return check_launch("swiglu_bwd");
+  }
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(total, 1)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), static_cast<const uint16_t *>(dy),
                      static_cast<const uint16_t *>(gu), ldgu, uoff, T, static_cast<int>(F),
                      static_cast<uint16_t *>(dgu), lddgu, duoff);
