@@ -273,7 +273,7 @@ def main():
 
     log(rank, f"timed region: {elapsed:.2f}s for {args.steps} steps")
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N = 1 only
         cpu = cpu_baseline(args, rank)
         log(rank, f"cpu baseline: {cpu['value']} tokens/s on {cpu['cores']} threads")
 
