@@ -134,3 +134,45 @@ def test_headline_logprob_micro_batch_8x1024x151936():
     lp.sum().backward()
     rowsum = x.grad.float().sum(dim=-1)
     assert rowsum.abs().max().item() < 5e-2  # bf16-rounded gradients of onehot - softmax
+
+
+def test_bench_logprob_launch_131072x151936():
+    """The bench's own log-prob launch (micro-batch 128 x 1024 response rows x 151,936 bf16 = 40 GB,
+    2.49e9 16-B vectors: past 2^31, so the flat backward's 64-bit indexing is exercised): oracle on
+    sampled rows incl. the first and last, row-sum invariant on every row, and the flat backward
+    bitwise equal to the per-row-chunk backward. Peak ~120 GB of HBM."""
+    from verl_amd import _lib as L
+    from verl_amd import kernels as K
+
+    n, V = 128 * 1024, 151936
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(n, V, device=DEV, dtype=torch.bfloat16, generator=gen).mul_(2)
+    labels = torch.randint(0, V, (n,), device=DEV, generator=gen)
+    labels[-1] = V - 1
+    lp, ent, lse = (torch.empty(n, device=DEV) for _ in range(3))
+    st = K._stream(x)
+    L.call("va_logprob_entropy_fwd", K._p(x), L.VA_BF16, n, V, V, K._p(labels), 1.0, K._p(lp), K._p(ent), K._p(lse), st)
+    rows = torch.cat([torch.tensor([0, 1, n // 2, n - 2, n - 1]), torch.randperm(n)[:11]]).to(DEV)
+    sub = x[rows].cpu()
+    close(lp[rows], ref.logprobs_fp32_math(sub, labels[rows].cpu()).numpy(), 1e-4, 1e-4, "logp rows")
+    close(ent[rows], ref.entropy_from_logits(sub.float()).numpy(), 1e-4, 1e-4, "entropy rows")
+    g = torch.randn(n, device=DEV, generator=gen)
+    dx = torch.empty_like(x)
+    try:
+        L.call("va_set_tuning", L.VA_TUNE_BWD_FLAT, -1)
+        L.call("va_logprob_entropy_bwd", K._p(g), None, K._p(x), L.VA_BF16, n, V, V, K._p(labels), K._p(lse),
+               K._p(ent), 1.0, K._p(dx), V, st)
+        # oracle gradient of sum_i g_i logp_i on the sampled rows: g (onehot - softmax), float64
+        p = torch.softmax(sub.double(), dim=-1)
+        want = -p * g[rows].cpu().double()[:, None]
+        want[torch.arange(len(rows)), labels[rows].cpu()] += g[rows].cpu().double()
+        close(dx[rows], want.numpy(), 2e-3 * want.abs().max().item(), 1e-2, "dlogits rows")
+        rowsum = dx.sum(dim=-1, dtype=torch.float32)
+        assert rowsum.abs().max().item() < 5e-2 * g.abs().max().item()
+        dx2 = torch.empty_like(x)
+        L.call("va_set_tuning", L.VA_TUNE_BWD_FLAT, 0)
+        L.call("va_logprob_entropy_bwd", K._p(g), None, K._p(x), L.VA_BF16, n, V, V, K._p(labels), K._p(lse),
+               K._p(ent), 1.0, K._p(dx2), V, st)
+        assert torch.equal(dx, dx2)
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_BWD_FLAT, -1)
