@@ -67,3 +67,31 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(L, "LIB_PATH", tmp_path / "nope.so")
     with pytest.raises(L.NativeLibraryError, match="missing"):
         L.load()
+
+
+def test_header_constants_match_the_python_mirror():
+    """Every #define VA_* value in include/verl_amd.h equals the constant _lib.py mirrors."""
+    import re
+
+    text = L.HEADER_PATH.read_text()
+    defs = dict(re.findall(r"^#define (VA_[A-Z0-9_]+) \(?(-?\d+)\)?", text, re.M))
+    mirrored = {k: v for k, v in vars(L).items() if k.startswith("VA_") and isinstance(v, int)}
+    assert mirrored, "no constants mirrored"
+    for name, value in mirrored.items():
+        assert name in defs, name
+        assert int(defs[name]) == value, (name, defs[name], value)
+    for key in ("VA_TUNE_GAE_VARIANT", "VA_TUNE_BWD_FLAT", "VA_TUNE_SWIGLU_STREAM"):
+        assert key in mirrored
+
+
+def test_tuning_keys_and_wgrad_validation_without_device(lib):
+    for key in (L.VA_TUNE_GAE_VARIANT, L.VA_TUNE_BWD_FLAT, L.VA_TUNE_SWIGLU_STREAM):
+        assert lib.va_set_tuning(key, 0) == 0
+    assert lib.va_set_tuning(L.VA_TUNE_GAE_VARIANT, 0) == 0
+    assert lib.va_set_tuning(L.VA_TUNE_BWD_FLAT, -1) == 0
+    assert lib.va_set_tuning(L.VA_TUNE_SWIGLU_STREAM, -1) == 0
+    assert lib.va_set_tuning(99, 1) == -1
+    assert lib.va_wgrad_workspace_bytes(256, 128, 4) == 4 * 4 * 256 * 128
+    assert lib.va_wgrad_workspace_bytes(256, 128, 1) == 0
+    rc = lib.va_wgrad_bf16(None, 100, None, 128, 64, 100, 128, 1, None, None, None)
+    assert rc == -1 and b"multiples of 128" in lib.va_last_error()
