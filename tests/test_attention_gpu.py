@@ -130,6 +130,38 @@ def test_flash_backward_matches_fp32_reference(bwd, lens):
         assert e_ours < max(1.5 * e_torch, 1e-2), f"{what}: ours {e_ours:.3e} vs torch flash {e_torch:.3e}"
 
 
+@pytest.mark.parametrize("grouped", [0, 1])
+@pytest.mark.parametrize("lens", [[300, 129, 1000], [1, 33, 64, 65, 128, 129, 200], [1184, 1280]])
+def test_flash_backward_query_tile_64_equals_32(grouped, lens):
+    """dK / dV with 64-row staged query tiles (default) equal the 32-row tiles bitwise: the same
+    32-row products in the same order (sequence tails included)."""
+    from verl_amd import _lib as L
+    from verl_amd.workers.actor import attention as A
+
+    q, k, v, cu = _inputs(lens, seed=11 + len(lens))
+    cu_d = torch.tensor(cu, dtype=torch.int32, device=DEV)
+    mx = int(max(lens))
+    g = torch.randn_like(q)
+    blocks = torch.tensor(A.flash_block_table(cu), device=DEV)
+    kblocks = torch.tensor(A.flash_key_block_table(cu), device=DEV)
+    grads = []
+    old = A.FLASH_BWD
+    A.FLASH_BWD = "gfx950"
+    L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, grouped)
+    try:
+        for qt in (64, 32):
+            L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, qt)
+            qb, kb, vb = (t.clone().requires_grad_(True) for t in (q, k, v))
+            A.flash_attention(qb, kb, vb, cu_d, mx, blocks, kblocks=kblocks).backward(g)
+            grads.append((qb.grad, kb.grad, vb.grad))
+    finally:
+        A.FLASH_BWD = old
+        L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, -1)
+        L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 64)
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
 def test_actor_with_flash_forward_matches_torch_flash():
     import copy
 

@@ -1,0 +1,60 @@
+"""Interleaved A/B of the flash-attention backward's dK / dV query-tile height (VA_TUNE_FLASH_DKDV_QT
+32 vs 64) on a bench-shaped packed micro-batch (128 sequences of prompt U[64, 256] + 1024 tokens,
+14 query / 2 KV heads, D = 64). HIP-event timed fwd + bwd, median over rounds.
+
+  python tools/attn_bwd_ab.py [N_SEQ]
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from verl_amd import _lib as L  # noqa: E402
+from verl_amd.workers.actor import attention as A  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+    rng = np.random.default_rng(0)
+    lens = (rng.integers(64, 257, n) + 1024).tolist()
+    cu = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lens, out=cu[1:])
+    T, dev = int(cu[-1]), "cuda"
+    q = torch.randn(T, 14, 64, device=dev).to(torch.bfloat16).requires_grad_(True)
+    k = torch.randn(T, 2, 64, device=dev).to(torch.bfloat16).requires_grad_(True)
+    v = torch.randn(T, 2, 64, device=dev).to(torch.bfloat16).requires_grad_(True)
+    g = torch.randn(T, 14, 64, device=dev).to(torch.bfloat16)
+    cu_d = torch.tensor(cu, dtype=torch.int32, device=dev)
+    blocks = torch.tensor(A.flash_block_table(cu), device=dev)
+    kblocks = torch.tensor(A.flash_key_block_table(cu), device=dev)
+    mx = int(max(lens))
+    A.FLASH_BWD = "gfx950"
+
+    def step():
+        A.flash_attention(q, k, v, cu_d, mx, blocks, kblocks=kblocks).backward(g)
+
+    times = {32: [], 64: []}
+    for _ in range(6):
+        for qt in (32, 64):
+            L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, qt)
+            step()
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(5):
+                step()
+            b.record()
+            torch.cuda.synchronize()
+            times[qt].append(a.elapsed_time(b) / 5 * 1e3)
+    L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 64)
+    for qt, ts in times.items():
+        print(json.dumps({"case": f"flash_fwd_bwd_qt{qt}", "T": T, "median_us": round(float(np.median(ts)), 1)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

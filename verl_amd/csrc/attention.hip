@@ -276,15 +276,18 @@ __device__ __forceinline__ bf16x8 pack_frag(const float *x) {
 // all G query heads of its group in order (head-major) with dK / dV accumulated in registers, and
 // writes bf16 dK / dV directly (no partials, no group-sum launch; used when the key blocks alone fill
 // the chip).
-template <bool GROUPED>
+// QT = query rows per staged tile (32 or 64): the 64-row tile halves the barriers per MFMA; the
+// tile's 32-row halves run the same body (a 32-row offset keeps the images' XOR swizzle)
+template <bool GROUPED, int QT>
 __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
     const uint16_t *__restrict__ q, const uint16_t *__restrict__ k, const uint16_t *__restrict__ v,
     const uint16_t *__restrict__ dout, const float *__restrict__ lse, const float *__restrict__ delta,
     const int32_t *__restrict__ cu, const int32_t *__restrict__ kblocks, int64_t ld, int64_t T, int Hq, int Hk,
     float scale, float *__restrict__ pdk, float *__restrict__ pdv, uint16_t *__restrict__ dk_out,
     uint16_t *__restrict__ dv_out) {
-  constexpr int QT = 32;  // query rows per staged tile
-  // [buf][Q image 32x64 | dO image 32x64] bf16, then [buf][lse2 32 | delta 32] fp32
+  static_assert(QT == 32 || QT == 64, "QT");
+  constexpr int NCH = QT * 8 / 256;  // 16-B chunks per thread per image
+  // [buf][Q image QTx64 | dO image QTx64] bf16, then [buf][lse2 QT | delta QT] fp32
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * QT * D + 2 * 2 * QT * 2];
   float *rowc = reinterpret_cast<float *>(lds + 2 * 2 * QT * D);
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, kl = lane & 31;
@@ -324,21 +327,22 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   const int n_it = GROUPED ? n_qt * G : n_qt;  // grouped: head-major over the group's query heads
   // staging: one 16-B chunk of the Q tile and one of the dO tile per thread; lse2 / delta by 64 threads
   struct StageQ {
-    uint4 q, d;
+    uint4 q[NCH], d[NCH];
     float rc;
   };
   auto load_it = [&](int it) -> StageQ {
     StageQ st;
     const int hj = GROUPED ? it / n_qt : 0;
     const int hq = hq0 + hj, qt0 = qfirst + (it - hj * n_qt) * QT;
-    const int r = tid >> 3, ch = tid & 7, qp = qt0 + r;
-    {
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int idx = tid + u * 256, r = idx >> 3, ch = idx & 7, qp = qt0 + r;
       const bool ok = qp < len;
       const int64_t base = (s0 + (ok ? qp : len - 1)) * ldq + hq * D + ch * 8;  // clamped: no branch
       const uint4 a = *reinterpret_cast<const uint4 *>(q + base);
       const uint4 b = *reinterpret_cast<const uint4 *>(dout + base);
-      st.q = ok ? a : make_uint4(0, 0, 0, 0);
-      st.d = ok ? b : make_uint4(0, 0, 0, 0);
+      st.q[u] = ok ? a : make_uint4(0, 0, 0, 0);
+      st.d[u] = ok ? b : make_uint4(0, 0, 0, 0);
     }
     st.rc = 0.f;
     if (tid < 2 * QT) {
@@ -350,9 +354,12 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   };
   auto store_it = [&](int buf, const StageQ &st) {
     uint16_t *img = lds + buf * 2 * QT * D;
-    const int r = tid >> 3, ch = tid & 7;
-    *reinterpret_cast<uint4 *>(img + swz(r, ch * 8)) = st.q;
-    *reinterpret_cast<uint4 *>(img + QT * D + swz(r, ch * 8)) = st.d;
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int idx = tid + u * 256, r = idx >> 3, ch = idx & 7;
+      *reinterpret_cast<uint4 *>(img + swz(r, ch * 8)) = st.q[u];
+      *reinterpret_cast<uint4 *>(img + QT * D + swz(r, ch * 8)) = st.d[u];
+    }
     if (tid < 2 * QT) rowc[buf * 2 * QT + tid] = st.rc;
   };
   StageQ stq;
@@ -364,12 +371,14 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   for (int it = 0; it < n_it; ++it) {
     if (it + 1 < n_it) stq = load_it(it + 1);
     const int buf = it & 1;
-    const uint16_t *qi = lds + buf * 2 * QT * D;
+#pragma unroll
+    for (int sub = 0; sub < QT / 32; ++sub) {
+    const uint16_t *qi = lds + buf * 2 * QT * D + sub * 32 * D;
     const uint16_t *di = qi + QT * D;
-    const float *lse2 = rowc + buf * 2 * QT;
+    const float *lse2 = rowc + buf * 2 * QT + sub * 32;
     const float *dlt = lse2 + QT;
-    const int qt0 = qfirst + (GROUPED ? it % n_qt : it) * QT;
-    if (qt0 + QT - 1 >= k0 && k0 < len) {  // some query of the tile sees some key of the wave
+    const int qt0 = qfirst + (GROUPED ? it % n_qt : it) * QT + sub * 32;
+    if (qt0 + 31 >= k0 && k0 < len && qt0 < len) {  // some query of the 32-row half sees a wave key
       // S = Q K^T and dP = dO V^T, rows = queries (registers), columns = keys (lanes)
       f32x16 sacc, pacc;
 #pragma unroll
@@ -384,7 +393,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
         pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], pacc, 0, 0, 0);
       }
-      const bool need_mask = (qt0 < k0 + 31) || (qt0 + QT > len) || (k0 + 32 > len);
+      const bool need_mask = (qt0 < k0 + 31) || (qt0 + 32 > len) || (k0 + 32 > len);
       float p[16], ds[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -lse2[crow(r, h)]));
@@ -408,6 +417,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
         }
       }
     }
+    }  // sub
     if (it + 1 < n_it) store_it((it + 1) & 1, stq);
     __syncthreads();
   }
@@ -623,6 +633,8 @@ using namespace va;
 
 // va_set_tuning(VA_TUNE_FLASH_GROUPED_DKDV): -1 auto, 0 per-query-head partials + group sum, 1 grouped
 int g_flash_grouped_dkdv = -1;
+// va_set_tuning(VA_TUNE_FLASH_DKDV_QT): query rows per staged dK / dV tile, 32 or 64 (default)
+int g_flash_dkdv_qt = 64;
 
 extern "C" int va_flash_attn_fwd(const void *q, const void *k, const void *v, const int32_t *cu_seqlens,
                                  const int32_t *block_table, int64_t n_blocks, int64_t T, int64_t Hq, int64_t Hk,
@@ -665,19 +677,20 @@ extern "C" int va_flash_attn_bwd(const void *q, const void *k, const void *v, co
   // grouped dK / dV (one workgroup per key block x KV head, no partials) once the key blocks alone
   // give >= 2 workgroups per CU; otherwise per query head + the fixed-order group sum
   const bool grouped = g_flash_grouped_dkdv == 1 || (g_flash_grouped_dkdv < 0 && n_k_blocks * Hk >= 512);
+  const bool qt64 = g_flash_dkdv_qt != 32;
+#define VA_DKDV(GR, QTV)                                                                                         \
+  hipLaunchKernelGGL((flash_bwd_dkdv_kernel<GR, QTV>),                                                           \
+                     dim3(static_cast<unsigned>(n_k_blocks), static_cast<unsigned>(GR ? Hk : Hq)), dim3(256), 0, s, \
+                     static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(k),                          \
+                     static_cast<const uint16_t *>(v), static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens, \
+                     k_blocks, max_len, T, static_cast<int>(Hq), static_cast<int>(Hk), scale, pdk, pdv,            \
+                     static_cast<uint16_t *>(dk), static_cast<uint16_t *>(dv))
   if (grouped) {
-    hipLaunchKernelGGL(flash_bwd_dkdv_kernel<true>, dim3(static_cast<unsigned>(n_k_blocks), static_cast<unsigned>(Hk)),
-                       dim3(256), 0, s, static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(k),
-                       static_cast<const uint16_t *>(v), static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens,
-                       k_blocks, max_len, T, static_cast<int>(Hq), static_cast<int>(Hk), scale, pdk, pdv,
-                       static_cast<uint16_t *>(dk), static_cast<uint16_t *>(dv));
+    if (qt64) VA_DKDV(true, 64); else VA_DKDV(true, 32);
   } else {
-    hipLaunchKernelGGL(flash_bwd_dkdv_kernel<false>, dim3(static_cast<unsigned>(n_k_blocks), static_cast<unsigned>(Hq)),
-                       dim3(256), 0, s, static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(k),
-                       static_cast<const uint16_t *>(v), static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens,
-                       k_blocks, max_len, T, static_cast<int>(Hq), static_cast<int>(Hk), scale, pdk, pdv,
-                       static_cast<uint16_t *>(dk), static_cast<uint16_t *>(dv));
+    if (qt64) VA_DKDV(false, 64); else VA_DKDV(false, 32);
   }
+#undef VA_DKDV
   if (!grouped) {
     const int64_t granules = T * Hk * (D / 4);
     int64_t grid = (granules + 255) / 256;

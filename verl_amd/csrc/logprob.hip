@@ -710,6 +710,7 @@ extern "C" int va_logprob_entropy_bwd(const float *g_logp, const float *g_entrop
 extern int g_flash_grouped_dkdv;  // attention.hip
 extern int g_gae_variant;         // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
+extern int g_flash_dkdv_qt;       // attention.hip
 
 extern "C" int va_set_tuning(int key, int value) {
   switch (key) {
@@ -721,6 +722,13 @@ extern "C" int va_set_tuning(int key, int value) {
     case VA_TUNE_GAE_VARIANT: g_gae_variant = value; return VA_OK;
     case VA_TUNE_BWD_FLAT: va::g_bwd_flat = value; return VA_OK;
     case VA_TUNE_SWIGLU_STREAM: g_swiglu_variant = value; return VA_OK;
+    case VA_TUNE_FLASH_DKDV_QT:
+      if (value != 32 && value != 64) {
+        va::set_error("VA_TUNE_FLASH_DKDV_QT must be 32 or 64 (got %d)", value);
+        return VA_E_ARG;
+      }
+      g_flash_dkdv_qt = value;
+      return VA_OK;
     default: va::set_error("unknown tuning key %d", key); return VA_E_ARG;
   }
 }
