@@ -133,7 +133,9 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   fwd / bwd, all loads issued first, non-temporal), 2 / 4 / 8 = streaming with that many vectors
  *   per lane, 0 = grid-stride kernels (bitwise identical results);
  *   VA_TUNE_FLASH_DKDV_QT (va_flash_attn_bwd): query rows per staged dK / dV tile, 64 (default) or
- *   32 (bitwise identical results: the same per-32-row products in the same order). */
+ *   32 (bitwise identical results: the same per-32-row products in the same order);
+ *   VA_TUNE_FLASH_DQ_KB (va_flash_attn_bwd): keys per staged dQ block, 128 (default) or 64 (bitwise
+ *   identical results). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3
@@ -143,6 +145,7 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_BWD_FLAT 7
 #define VA_TUNE_SWIGLU_STREAM 8
 #define VA_TUNE_FLASH_DKDV_QT 9
+#define VA_TUNE_FLASH_DQ_KB 10
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

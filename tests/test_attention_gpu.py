@@ -133,8 +133,8 @@ def test_flash_backward_matches_fp32_reference(bwd, lens):
 @pytest.mark.parametrize("grouped", [0, 1])
 @pytest.mark.parametrize("lens", [[300, 129, 1000], [1, 33, 64, 65, 128, 129, 200], [1184, 1280]])
 def test_flash_backward_query_tile_64_equals_32(grouped, lens):
-    """dK / dV with 64-row staged query tiles (default) equal the 32-row tiles bitwise: the same
-    32-row products in the same order (sequence tails included)."""
+    """dK / dV with 64-row staged query tiles and dQ with 128-key staged blocks (defaults) equal the
+    32-row / 64-key stagings bitwise: the same 32-wide products in the same order (tails included)."""
     from verl_amd import _lib as L
     from verl_amd.workers.actor import attention as A
 
@@ -149,8 +149,9 @@ def test_flash_backward_query_tile_64_equals_32(grouped, lens):
     A.FLASH_BWD = "gfx950"
     L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, grouped)
     try:
-        for qt in (64, 32):
+        for qt, kblk in ((64, 128), (32, 64)):
             L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, qt)
+            L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, kblk)
             qb, kb, vb = (t.clone().requires_grad_(True) for t in (q, k, v))
             A.flash_attention(qb, kb, vb, cu_d, mx, blocks, kblocks=kblocks).backward(g)
             grads.append((qb.grad, kb.grad, vb.grad))
@@ -158,6 +159,7 @@ def test_flash_backward_query_tile_64_equals_32(grouped, lens):
         A.FLASH_BWD = old
         L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, -1)
         L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 64)
+        L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, 128)
     for a, b in zip(*grads):
         assert torch.equal(a, b)
 

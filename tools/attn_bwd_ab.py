@@ -1,5 +1,5 @@
-"""Interleaved A/B of the flash-attention backward's dK / dV query-tile height (VA_TUNE_FLASH_DKDV_QT
-32 vs 64) on a bench-shaped packed micro-batch (128 sequences of prompt U[64, 256] + 1024 tokens,
+"""Interleaved A/B of the flash-attention backward's staging sizes (dK / dV query-tile height
+VA_TUNE_FLASH_DKDV_QT, dQ key-block width VA_TUNE_FLASH_DQ_KB) on a bench-shaped packed micro-batch (128 sequences of prompt U[64, 256] + 1024 tokens,
 14 query / 2 KV heads, D = 64). HIP-event timed fwd + bwd, median over rounds.
 
   python tools/attn_bwd_ab.py [N_SEQ]
@@ -37,10 +37,12 @@ def main():
     def step():
         A.flash_attention(q, k, v, cu_d, mx, blocks, kblocks=kblocks).backward(g)
 
-    times = {32: [], 64: []}
+    variants = [(32, 64), (64, 64), (64, 128)]
+    times = {v: [] for v in variants}
     for _ in range(6):
-        for qt in (32, 64):
+        for qt, kb in variants:
             L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, qt)
+            L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, kb)
             step()
             torch.cuda.synchronize()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -49,11 +51,12 @@ def main():
                 step()
             b.record()
             torch.cuda.synchronize()
-            times[qt].append(a.elapsed_time(b) / 5 * 1e3)
+            times[(qt, kb)].append(a.elapsed_time(b) / 5 * 1e3)
     L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 64)
-    for qt, ts in times.items():
-        print(json.dumps({"case": f"flash_fwd_bwd_qt{qt}", "T": T, "median_us": round(float(np.median(ts)), 1)}),
-              flush=True)
+    L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, 128)
+    for (qt, kb), ts in times.items():
+        print(json.dumps({"case": f"flash_fwd_bwd_dkdv_qt{qt}_dq_kb{kb}", "T": T,
+                          "median_us": round(float(np.median(ts)), 1)}), flush=True)
 
 
 if __name__ == "__main__":

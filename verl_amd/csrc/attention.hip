@@ -488,12 +488,17 @@ __global__ __launch_bounds__(256) void flash_bwd_group_sum_kernel(const float *_
 // Also computes delta = rowsum(dO * O) of its queries from the O / dO fragments it loads anyway
 // (each query's 64 values are split over lanes l and l ^ 32) and publishes it for the dK / dV
 // launch that follows: no separate delta pass over O and dO.
+// KBQ = keys per staged block (64 or 128): 128 halves the barriers per MFMA; the block's 32-key
+// tiles run the same body
+template <int KBQ>
 __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
     const uint16_t *__restrict__ k, const uint16_t *__restrict__ v, const uint16_t *__restrict__ q,
     const uint16_t *__restrict__ o, const uint16_t *__restrict__ dout, const float *__restrict__ lse,
     float *__restrict__ delta, const int32_t *__restrict__ cu, const int32_t *__restrict__ blocks, int64_t ld,
     int Hq, int Hk, float scale, uint16_t *__restrict__ dq) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * KB * D];  // [buf][K | V][64 keys][64 d], swizzled
+  static_assert(KBQ == 64 || KBQ == 128, "KBQ");
+  constexpr int NCK = KBQ * 8 / 256;  // 16-B chunks per thread per operand
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * KBQ * D];  // [buf][K | V][KBQ keys][64 d], swizzled
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ql = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
   const int seq = blocks[2 * blockIdx.x], qs = blocks[2 * blockIdx.x + 1];
@@ -539,14 +544,14 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
     for (int r = 0; r < 16; ++r) dqt[dh][r] = 0.f;
 
   const int kv_end = min(len, qs + QB);
-  const int nkb = (kv_end + KB - 1) / KB;
+  const int nkb = (kv_end + KBQ - 1) / KBQ;
   const int wave_last_q = qs + wave * 32 + 31;
-  uint4 sk[2], sv[2];
+  uint4 sk[NCK], sv[NCK];
   auto load_block = [&](int kb) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NCK; ++u) {
       const int idx = tid + u * 256, r = idx >> 3, ch = idx & 7;
-      const int kk = kb * KB + r;
+      const int kk = kb * KBQ + r;
       const bool ok = kk < len;
       const int64_t base = (s0 + (ok ? kk : len - 1)) * ldk + kvh * D + ch * 8;  // clamped: no branch
       const uint4 a = *reinterpret_cast<const uint4 *>(k + base);
@@ -556,10 +561,10 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
     }
   };
   auto store_block = [&](int buf) {
-    uint16_t *lk = lds + buf * 2 * KB * D;
-    uint16_t *lv = lk + KB * D;
+    uint16_t *lk = lds + buf * 2 * KBQ * D;
+    uint16_t *lv = lk + KBQ * D;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NCK; ++u) {
       const int idx = tid + u * 256, r = idx >> 3, ch = idx & 7;
       *reinterpret_cast<uint4 *>(lk + swz(r, ch * 8)) = sk[u];
       *reinterpret_cast<uint4 *>(lv + swz(r, ch * 8)) = sv[u];
@@ -572,11 +577,11 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     if (kb + 1 < nkb) load_block(kb + 1);
-    const uint16_t *lk = lds + (kb & 1) * 2 * KB * D;
-    const uint16_t *lv = lk + KB * D;
+    const uint16_t *lk = lds + (kb & 1) * 2 * KBQ * D;
+    const uint16_t *lv = lk + KBQ * D;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int key0 = kb * KB + t * 32;
+    for (int t = 0; t < KBQ / 32; ++t) {
+      const int key0 = kb * KBQ + t * 32;
       if (key0 > wave_last_q || key0 >= len || qs + wave * 32 >= len) continue;
       f32x16 sacc, pacc;
 #pragma unroll
@@ -635,6 +640,8 @@ using namespace va;
 int g_flash_grouped_dkdv = -1;
 // va_set_tuning(VA_TUNE_FLASH_DKDV_QT): query rows per staged dK / dV tile, 32 or 64 (default)
 int g_flash_dkdv_qt = 64;
+// va_set_tuning(VA_TUNE_FLASH_DQ_KB): keys per staged dQ block, 64 or 128 (default)
+int g_flash_dq_kb = 128;
 
 extern "C" int va_flash_attn_fwd(const void *q, const void *k, const void *v, const int32_t *cu_seqlens,
                                  const int32_t *block_table, int64_t n_blocks, int64_t T, int64_t Hq, int64_t Hk,
@@ -669,11 +676,14 @@ extern "C" int va_flash_attn_bwd(const void *q, const void *k, const void *v, co
   float *pdk = partial, *pdv = partial + Hq * T * D;
   hipStream_t s = static_cast<hipStream_t>(stream);
   // dQ first: it also produces delta for the dK / dV launch
-  hipLaunchKernelGGL(flash_bwd_dq_kernel, dim3(static_cast<unsigned>(n_q_blocks), static_cast<unsigned>(Hq)),
-                     dim3(256), 0, s, static_cast<const uint16_t *>(k), static_cast<const uint16_t *>(v),
-                     static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(o),
-                     static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens, q_blocks, max_len,
-                     static_cast<int>(Hq), static_cast<int>(Hk), scale, static_cast<uint16_t *>(dq));
+#define VA_DQ(KBV)                                                                                               \
+  hipLaunchKernelGGL((flash_bwd_dq_kernel<KBV>), dim3(static_cast<unsigned>(n_q_blocks), static_cast<unsigned>(Hq)), \
+                     dim3(256), 0, s, static_cast<const uint16_t *>(k), static_cast<const uint16_t *>(v),             \
+                     static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(o),                              \
+                     static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens, q_blocks, max_len,                  \
+                     static_cast<int>(Hq), static_cast<int>(Hk), scale, static_cast<uint16_t *>(dq))
+  if (g_flash_dq_kb == 64) VA_DQ(64); else VA_DQ(128);
+#undef VA_DQ
   // grouped dK / dV (one workgroup per key block x KV head, no partials) once the key blocks alone
   // give >= 2 workgroups per CU; otherwise per query head + the fixed-order group sum
   const bool grouped = g_flash_grouped_dkdv == 1 || (g_flash_grouped_dkdv < 0 && n_k_blocks * Hk >= 512);
