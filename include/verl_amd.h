@@ -135,7 +135,9 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   VA_TUNE_FLASH_DKDV_QT (va_flash_attn_bwd): query rows per staged dK / dV tile, 64 (default) or
  *   32 (bitwise identical results: the same per-32-row products in the same order);
  *   VA_TUNE_FLASH_DQ_KB (va_flash_attn_bwd): keys per staged dQ block, 128 (default) or 64 (bitwise
- *   identical results). */
+ *   identical results);
+ *   VA_TUNE_FLASH_FWD_KB (va_flash_attn_fwd): keys per staged forward block, 64 (default) or 128
+ *   (bitwise identical results: the same 64-key online-softmax steps). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3
@@ -146,6 +148,7 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_SWIGLU_STREAM 8
 #define VA_TUNE_FLASH_DKDV_QT 9
 #define VA_TUNE_FLASH_DQ_KB 10
+#define VA_TUNE_FLASH_FWD_KB 11
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

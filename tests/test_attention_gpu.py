@@ -66,6 +66,33 @@ def test_flash_forward_matches_fp32_reference(lens):
         assert (lse[i, :, : b - a] - want_lse[:, a:b]).abs().max().item() < 1e-3
 
 
+@pytest.mark.parametrize("lens", [[1, 17, 128, 129, 300], [1184, 1100, 1280, 700], [64] * 9, [65, 191, 257]])
+def test_flash_forward_key_block_128_equals_64(lens):
+    """Forward with 128-key staged blocks equals 64-key blocks (default) bitwise: the same 64-key
+    online-softmax steps in the same order."""
+    from verl_amd import _lib as L
+    from verl_amd import kernels as K
+    from verl_amd.workers.actor import attention as A
+
+    q, k, v, cu = _inputs(lens, seed=3 + len(lens))
+    cu_d = torch.tensor(cu, dtype=torch.int32, device=DEV)
+    blocks = torch.tensor(A.flash_block_table(cu), device=DEV)
+    T, mx = q.shape[0], int(max(lens))
+    outs = []
+    try:
+        for kb in (128, 64):
+            L.call("va_set_tuning", L.VA_TUNE_FLASH_FWD_KB, kb)
+            o = torch.empty_like(q)
+            lse = torch.zeros(len(lens), 14, mx, device=DEV)
+            L.call("va_flash_attn_fwd", K._p(q), K._p(k), K._p(v), K._p(cu_d), K._p(blocks), blocks.shape[0], T, 14,
+                   2, 64, mx, 64 ** -0.5, K._p(o), K._p(lse), K._stream(q))
+            outs.append((o, lse))
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_FLASH_FWD_KB, 64)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 def test_flash_forward_matches_torch_flash_and_lse_convention():
     from verl_amd.workers.actor import attention as A
 

@@ -33,6 +33,7 @@ def main():
     kblocks = torch.tensor(A.flash_key_block_table(cu), device=dev)
     mx = int(max(lens))
     A.FLASH_BWD = "gfx950"
+    L.call("va_set_tuning", L.VA_TUNE_FLASH_FWD_KB, 64)
 
     def step():
         A.flash_attention(q, k, v, cu_d, mx, blocks, kblocks=kblocks).backward(g)
@@ -54,6 +55,24 @@ def main():
             times[(qt, kb)].append(a.elapsed_time(b) / 5 * 1e3)
     L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 64)
     L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, 128)
+    fwd_times = {64: [], 128: []}
+    with torch.no_grad():
+        for _ in range(6):
+            for kbf in (64, 128):
+                L.call("va_set_tuning", L.VA_TUNE_FLASH_FWD_KB, kbf)
+                A.flash_attention(q, k, v, cu_d, mx, blocks)
+                torch.cuda.synchronize()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(10):
+                    A.flash_attention(q, k, v, cu_d, mx, blocks)
+                b.record()
+                torch.cuda.synchronize()
+                fwd_times[kbf].append(a.elapsed_time(b) / 10 * 1e3)
+    L.call("va_set_tuning", L.VA_TUNE_FLASH_FWD_KB, 64)
+    for kbf, ts in fwd_times.items():
+        print(json.dumps({"case": f"flash_fwd_kb{kbf}", "T": T, "median_us": round(float(np.median(ts)), 1)}),
+              flush=True)
     for (qt, kb), ts in times.items():
         print(json.dumps({"case": f"flash_fwd_bwd_dkdv_qt{qt}_dq_kb{kb}", "T": T,
                           "median_us": round(float(np.median(ts)), 1)}), flush=True)

@@ -30,7 +30,7 @@ VA_LOSS_KL, VA_LOSS_ENTROPY, VA_LOSS_NTOKENS, VA_LOSS_NROWS, VA_LOSS_NOUT = 4, 5
 VA_VLOSS_LOSS, VA_VLOSS_CLIPFRAC, VA_VLOSS_VPRED_MEAN, VA_VLOSS_NTOKENS, VA_VLOSS_NOUT = 0, 1, 2, 3, 4
 VA_TUNE_FWD_WAVES_PER_ROW, VA_TUNE_BWD_WAVES_PER_ROW, VA_TUNE_NONTEMPORAL, VA_TUNE_PIPELINE = 1, 2, 3, 4
 VA_TUNE_FLASH_GROUPED_DKDV, VA_TUNE_GAE_VARIANT, VA_TUNE_BWD_FLAT, VA_TUNE_SWIGLU_STREAM = 5, 6, 7, 8
-VA_TUNE_FLASH_DKDV_QT, VA_TUNE_FLASH_DQ_KB = 9, 10
+VA_TUNE_FLASH_DKDV_QT, VA_TUNE_FLASH_DQ_KB, VA_TUNE_FLASH_FWD_KB = 9, 10, 11
 
 _P = c_void_p
 _SIGNATURES: dict[str, tuple] = {

@@ -48,11 +48,16 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
 // row (key / query index inside a 32 x 32 tile) held in register r by lane half h
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// KBF = keys per staged block (64 or 128): 128 halves the barriers (but measures slower: the
+// default is 64); each 64-key sub-block runs the same online-softmax step as a 64-key block
+template <int KBF>
 __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
     const uint16_t *__restrict__ q, const uint16_t *__restrict__ k, const uint16_t *__restrict__ v,
     const int32_t *__restrict__ cu, const int32_t *__restrict__ blocks, int64_t lse_ld, int Hq, int Hk,
     float scale, uint16_t *__restrict__ o, float *__restrict__ lse) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * KB * D];  // [buf][K | V][64 keys][64 d]
+  static_assert(KBF == 64 || KBF == 128, "KBF");
+  constexpr int NCF = KBF * 8 / 256;  // 16-B chunks per thread per operand
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * KBF * D];  // [buf][K | V][KBF keys][64 d]
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ql = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
   const int seq = blocks[2 * blockIdx.x], qs = blocks[2 * blockIdx.x + 1];
@@ -78,16 +83,16 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
   float m = -INFINITY, l = 0.f;
 
   const int kv_end = min(len, qs + QB);  // causal: keys <= the block's last query
-  const int nkb = (kv_end + KB - 1) / KB;
+  const int nkb = (kv_end + KBF - 1) / KBF;
   const int wave_last_q = qs + wave * 32 + 31;
 
-  // staging: 64 rows x 8 chunks of 16 B per operand = 512 chunks, 2 per thread per operand
-  uint4 sk[2], sv[2];
+  // staging: KBF rows x 8 chunks of 16 B per operand, NCF per thread per operand
+  uint4 sk[NCF], sv[NCF];
   auto load_block = [&](int kb) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NCF; ++u) {
       const int idx = tid + u * 256, r = idx >> 3, ch = idx & 7;
-      const int key = kb * KB + r;
+      const int key = kb * KBF + r;
       const bool ok = key < len;
       const int64_t base = (s0 + (ok ? key : len - 1)) * ldk + kvh * D + ch * 8;  // clamped: no branch
       const uint4 a = *reinterpret_cast<const uint4 *>(k + base);
@@ -97,10 +102,10 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
     }
   };
   auto store_block = [&](int buf) {
-    uint16_t *lk = lds + buf * 2 * KB * D;
-    uint16_t *lv = lk + KB * D;
+    uint16_t *lk = lds + buf * 2 * KBF * D;
+    uint16_t *lv = lk + KBF * D;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NCF; ++u) {
       const int idx = tid + u * 256, r = idx >> 3, ch = idx & 7;
       *reinterpret_cast<uint4 *>(lk + r * D + ((ch ^ (r & 7)) << 3)) = sk[u];
       *reinterpret_cast<uint4 *>(lv + r * D + (ch << 3)) = sv[u];
@@ -114,11 +119,13 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     if (kb + 1 < nkb) load_block(kb + 1);
-    const uint16_t *lk = lds + (kb & 1) * 2 * KB * D;
-    const uint16_t *lv = lk + KB * D;
-    const int key0 = kb * KB;
-    // the whole 64-key block is past this wave's queries (or the wave has none): skip
-    if (!(key0 > wave_last_q || qs + wave * 32 >= len)) {
+#pragma unroll
+    for (int sub = 0; sub < KBF / KB; ++sub) {
+    const uint16_t *lk = lds + (kb & 1) * 2 * KBF * D + sub * KB * D;
+    const uint16_t *lv = lds + (kb & 1) * 2 * KBF * D + KBF * D + sub * KB * D;
+    const int key0 = kb * KBF + sub * KB;
+    // the whole 64-key sub-block is past this wave's queries (or the wave has none): skip
+    if (!(key0 > wave_last_q || qs + wave * 32 >= len || key0 >= kv_end)) {
       const bool t1_live = key0 + 32 <= wave_last_q && key0 + 32 < len;  // second 32-key tile
       // ---- S^T = K Q^T for the block's two 32-key tiles (keys on rows, queries on lanes)
       f32x16 sacc[2];
@@ -208,6 +215,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
         }
       }
     }
+    }  // sub
     // the other buffer was last read in iteration kb - 1, which every wave finished before the
     // barrier that ended it: store, then one barrier publishes the block for iteration kb + 1
     if (kb + 1 < nkb) store_block((kb + 1) & 1);
@@ -642,6 +650,9 @@ int g_flash_grouped_dkdv = -1;
 int g_flash_dkdv_qt = 64;
 // va_set_tuning(VA_TUNE_FLASH_DQ_KB): keys per staged dQ block, 64 or 128 (default)
 int g_flash_dq_kb = 128;
+// va_set_tuning(VA_TUNE_FLASH_FWD_KB): keys per staged forward block, 64 (default) or 128 (slower:
+// 654 vs 573 us at 151,819 tokens, profiles/r01/attn_bwd_staging_ab.log)
+int g_flash_fwd_kb = 64;
 
 extern "C" int va_flash_attn_fwd(const void *q, const void *k, const void *v, const int32_t *cu_seqlens,
                                  const int32_t *block_table, int64_t n_blocks, int64_t T, int64_t Hq, int64_t Hk,
@@ -654,10 +665,13 @@ extern "C" int va_flash_attn_fwd(const void *q, const void *k, const void *v, co
   VA_CHECK_ARG(reinterpret_cast<uintptr_t>(q) % 16 == 0 && reinterpret_cast<uintptr_t>(k) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(v) % 16 == 0 && reinterpret_cast<uintptr_t>(o) % 16 == 0,
                "flash_attn_fwd: 16-byte aligned q / k / v / o required");
-  hipLaunchKernelGGL(flash_fwd_kernel, dim3(static_cast<unsigned>(n_blocks), static_cast<unsigned>(Hq)), dim3(256),
-                     0, static_cast<hipStream_t>(stream), static_cast<const uint16_t *>(q),
-                     static_cast<const uint16_t *>(k), static_cast<const uint16_t *>(v), cu_seqlens, block_table,
-                     max_len, static_cast<int>(Hq), static_cast<int>(Hk), scale, static_cast<uint16_t *>(o), lse);
+#define VA_FWD(KBV)                                                                                             \
+  hipLaunchKernelGGL((flash_fwd_kernel<KBV>), dim3(static_cast<unsigned>(n_blocks), static_cast<unsigned>(Hq)),     \
+                     dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const uint16_t *>(q),              \
+                     static_cast<const uint16_t *>(k), static_cast<const uint16_t *>(v), cu_seqlens, block_table,  \
+                     max_len, static_cast<int>(Hq), static_cast<int>(Hk), scale, static_cast<uint16_t *>(o), lse)
+  if (g_flash_fwd_kb == 64) VA_FWD(64); else VA_FWD(128);
+#undef VA_FWD
   return check_launch("flash_attn_fwd");
 }
 

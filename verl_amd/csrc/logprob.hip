@@ -712,6 +712,7 @@ extern int g_gae_variant;         // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
 extern int g_flash_dkdv_qt;       // attention.hip
 extern int g_flash_dq_kb;         // attention.hip
+extern int g_flash_fwd_kb;        // attention.hip
 
 extern "C" int va_set_tuning(int key, int value) {
   switch (key) {
@@ -736,6 +737,13 @@ extern "C" int va_set_tuning(int key, int value) {
         return VA_E_ARG;
       }
       g_flash_dq_kb = value;
+      return VA_OK;
+    case VA_TUNE_FLASH_FWD_KB:
+      if (value != 64 && value != 128) {
+        va::set_error("VA_TUNE_FLASH_FWD_KB must be 64 or 128 (got %d)", value);
+        return VA_E_ARG;
+      }
+      g_flash_fwd_kb = value;
       return VA_OK;
     default: va::set_error("unknown tuning key %d", key); return VA_E_ARG;
   }
