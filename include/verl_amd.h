@@ -132,8 +132,8 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   VA_TUNE_SWIGLU_STREAM (va_swiglu_fwd/bwd): -1 = auto (streaming kernels: 4 / 2 vectors per lane
  *   fwd / bwd, all loads issued first, non-temporal), 2 / 4 / 8 = streaming with that many vectors
  *   per lane, 0 = grid-stride kernels (bitwise identical results);
- *   VA_TUNE_FLASH_DKDV_QT (va_flash_attn_bwd): query rows per staged dK / dV tile, 64 (default) or
- *   32 (bitwise identical results: the same per-32-row products in the same order);
+ *   VA_TUNE_FLASH_DKDV_QT (va_flash_attn_bwd): query rows per staged dK / dV tile, 128 (default), 64
+ *   or 32 (bitwise identical results: the same per-32-row products in the same order);
  *   VA_TUNE_FLASH_DQ_KB (va_flash_attn_bwd): keys per staged dQ block, 128 (default) or 64 (bitwise
  *   identical results);
  *   VA_TUNE_FLASH_FWD_KB (va_flash_attn_fwd): keys per staged forward block, 64 (default) or 128

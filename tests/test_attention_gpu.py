@@ -160,8 +160,8 @@ def test_flash_backward_matches_fp32_reference(bwd, lens):
 @pytest.mark.parametrize("grouped", [0, 1])
 @pytest.mark.parametrize("lens", [[300, 129, 1000], [1, 33, 64, 65, 128, 129, 200], [1184, 1280]])
 def test_flash_backward_query_tile_64_equals_32(grouped, lens):
-    """dK / dV with 64-row staged query tiles and dQ with 128-key staged blocks (defaults) equal the
-    32-row / 64-key stagings bitwise: the same 32-wide products in the same order (tails included)."""
+    """dK / dV staged in 64- or 128-row query tiles (128 = default) and dQ in 128-key blocks equal
+    the 32-row / 64-key stagings bitwise: the same 32-wide products in the same order (tails too)."""
     from verl_amd import _lib as L
     from verl_amd.workers.actor import attention as A
 
@@ -176,7 +176,7 @@ def test_flash_backward_query_tile_64_equals_32(grouped, lens):
     A.FLASH_BWD = "gfx950"
     L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, grouped)
     try:
-        for qt, kblk in ((64, 128), (32, 64)):
+        for qt, kblk in ((64, 128), (32, 64), (128, 128)):
             L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, qt)
             L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, kblk)
             qb, kb, vb = (t.clone().requires_grad_(True) for t in (q, k, v))
@@ -185,10 +185,11 @@ def test_flash_backward_query_tile_64_equals_32(grouped, lens):
     finally:
         A.FLASH_BWD = old
         L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, -1)
-        L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 64)
+        L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 128)
         L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, 128)
-    for a, b in zip(*grads):
-        assert torch.equal(a, b)
+    for other in grads[1:]:
+        for a, b in zip(grads[0], other):
+            assert torch.equal(a, b)
 
 
 def test_actor_with_flash_forward_matches_torch_flash():

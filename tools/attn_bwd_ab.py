@@ -38,7 +38,7 @@ def main():
     def step():
         A.flash_attention(q, k, v, cu_d, mx, blocks, kblocks=kblocks).backward(g)
 
-    variants = [(32, 64), (64, 64), (64, 128)]
+    variants = [(32, 64), (64, 128), (128, 128)]
     times = {v: [] for v in variants}
     for _ in range(6):
         for qt, kb in variants:
@@ -53,7 +53,7 @@ def main():
             b.record()
             torch.cuda.synchronize()
             times[(qt, kb)].append(a.elapsed_time(b) / 5 * 1e3)
-    L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 64)
+    L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 128)
     L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, 128)
     fwd_times = {64: [], 128: []}
     with torch.no_grad():

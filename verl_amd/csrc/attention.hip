@@ -293,7 +293,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
     const int32_t *__restrict__ cu, const int32_t *__restrict__ kblocks, int64_t ld, int64_t T, int Hq, int Hk,
     float scale, float *__restrict__ pdk, float *__restrict__ pdv, uint16_t *__restrict__ dk_out,
     uint16_t *__restrict__ dv_out) {
-  static_assert(QT == 32 || QT == 64, "QT");
+  static_assert(QT == 32 || QT == 64 || QT == 128, "QT");
   constexpr int NCH = QT * 8 / 256;  // 16-B chunks per thread per image
   // [buf][Q image QTx64 | dO image QTx64] bf16, then [buf][lse2 QT | delta QT] fp32
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * QT * D + 2 * 2 * QT * 2];
@@ -646,8 +646,9 @@ using namespace va;
 
 // va_set_tuning(VA_TUNE_FLASH_GROUPED_DKDV): -1 auto, 0 per-query-head partials + group sum, 1 grouped
 int g_flash_grouped_dkdv = -1;
-// va_set_tuning(VA_TUNE_FLASH_DKDV_QT): query rows per staged dK / dV tile, 32 or 64 (default)
-int g_flash_dkdv_qt = 64;
+// va_set_tuning(VA_TUNE_FLASH_DKDV_QT): query rows per staged dK / dV tile, 32, 64 or 128 (default;
+// fwd+bwd 2,485 / 2,421 / 2,383 us at 151,819 tokens, profiles/r01/attn_bwd_staging_ab.log)
+int g_flash_dkdv_qt = 128;
 // va_set_tuning(VA_TUNE_FLASH_DQ_KB): keys per staged dQ block, 64 or 128 (default)
 int g_flash_dq_kb = 128;
 // va_set_tuning(VA_TUNE_FLASH_FWD_KB): keys per staged forward block, 64 (default) or 128 (slower:
@@ -701,7 +702,7 @@ extern "C" int va_flash_attn_bwd(const void *q, const void *k, const void *v, co
   // grouped dK / dV (one workgroup per key block x KV head, no partials) once the key blocks alone
   // give >= 2 workgroups per CU; otherwise per query head + the fixed-order group sum
   const bool grouped = g_flash_grouped_dkdv == 1 || (g_flash_grouped_dkdv < 0 && n_k_blocks * Hk >= 512);
-  const bool qt64 = g_flash_dkdv_qt != 32;
+  const int qt = g_flash_dkdv_qt;
 #define VA_DKDV(GR, QTV)                                                                                         \
   hipLaunchKernelGGL((flash_bwd_dkdv_kernel<GR, QTV>),                                                           \
                      dim3(static_cast<unsigned>(n_k_blocks), static_cast<unsigned>(GR ? Hk : Hq)), dim3(256), 0, s, \
@@ -710,9 +711,9 @@ extern "C" int va_flash_attn_bwd(const void *q, const void *k, const void *v, co
                      k_blocks, max_len, T, static_cast<int>(Hq), static_cast<int>(Hk), scale, pdk, pdv,            \
                      static_cast<uint16_t *>(dk), static_cast<uint16_t *>(dv))
   if (grouped) {
-    if (qt64) VA_DKDV(true, 64); else VA_DKDV(true, 32);
+    if (qt == 32) VA_DKDV(true, 32); else if (qt == 128) VA_DKDV(true, 128); else VA_DKDV(true, 64);
   } else {
-    if (qt64) VA_DKDV(false, 64); else VA_DKDV(false, 32);
+    if (qt == 32) VA_DKDV(false, 32); else if (qt == 128) VA_DKDV(false, 128); else VA_DKDV(false, 64);
   }
 #undef VA_DKDV
   if (!grouped) {

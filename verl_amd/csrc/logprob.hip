@@ -725,8 +725,8 @@ extern "C" int va_set_tuning(int key, int value) {
     case VA_TUNE_BWD_FLAT: va::g_bwd_flat = value; return VA_OK;
     case VA_TUNE_SWIGLU_STREAM: g_swiglu_variant = value; return VA_OK;
     case VA_TUNE_FLASH_DKDV_QT:
-      if (value != 32 && value != 64) {
-        va::set_error("VA_TUNE_FLASH_DKDV_QT must be 32 or 64 (got %d)", value);
+      if (value != 32 && value != 64 && value != 128) {
+        va::set_error("VA_TUNE_FLASH_DKDV_QT must be 32, 64 or 128 (got %d)", value);
         return VA_E_ARG;
       }
       g_flash_dkdv_qt = value;
