@@ -1,13 +1,22 @@
 """GRPO actor-update benchmark on MI355X (BASELINE.json metric).
 
 One step = the actor-update hot path on this rank's shard: old-logp forward (compute_log_prob),
-GRPO advantages, then update_policy (forward, fused clipped loss + k3 KL loss, backward,
-bucketed RCCL gradient all-reduce, grad clip, AdamW). Workload per rank: Qwen2.5-0.5B
-architecture (random init), 64 prompts x n=8 = 512 responses x 1024 tokens, prompts left-padded
-to 256, vocab 151,936 — configs[1] of BASELINE.json; weak scaling (every rank does that work).
+GRPO advantages (worker-side, exchanging group statistics when groups span ranks), then
+update_policy (forward, fused clipped loss + k3 KL loss, backward, bucketed RCCL gradient
+all-reduce, grad clip, AdamW). Workload: Qwen2.5-0.5B architecture (random init), 64 prompts x
+n=8 = 512 responses x 1024 tokens, prompts left-padded to 256, vocab 151,936 — configs[1] of
+BASELINE.json.
+
+Scaling: by default STRONG — one 512 x 1024 batch is split over the W ranks,
+64/W prompts (512/W responses) per rank with the prompt groups intact, as the reference's
+DP_COMPUTE_PROTO chunk does (single_controller/base/decorator.py:375-385, normalisation
+fsdp_workers.py:174-196). ``--balance`` reorders the batch with the Karmarkar-Karp balancer first
+(ray_trainer.py:1064-1079), which splits groups over ranks and exercises the cross-rank GRPO
+statistics. ``--scaling weak`` gives every rank its own full 512 x 1024 batch.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-  N > 1 is launched by torch.distributed.run (one process per GPU, RCCL).
+  N > 1 without a launcher: bench.py starts ``torch.distributed.run`` as a CHILD process (before
+  any GPU call; no exec) with N ranks on 127.0.0.1 and exits with its return code.
 Rank 0 prints ONE JSON line (see the driver contract in the task statement).
 """
 
@@ -16,18 +25,17 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak (no sparsity)
+VOCAB = 151936
 
 
 def pmc_traffic(kernel: str, algo_bytes_per_launch: float, vocab: int):
@@ -80,16 +88,21 @@ def _gemm_table_name():
     return os.path.basename(gemm_tuning._loaded) if gemm_tuning._loaded else None
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong: one 512x1024 batch split over the ranks (SURVEY §8e); weak: a full batch per rank")
+    ap.add_argument("--balance", action="store_true",
+                    help="Karmarkar-Karp balance the batch over ranks first (splits prompt groups across ranks)")
     ap.add_argument("--prompts", type=int, default=64)
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--response-len", type=int, default=1024)
-    ap.add_argument("--micro", type=int, default=128, help="ppo_micro_batch_size_per_gpu (responses)")
+    ap.add_argument("--micro", type=int, default=128,
+                    help="ppo_micro_batch_size_per_gpu (responses; capped at the rank's shard)")
     ap.add_argument("--logprob-micro", type=int, default=128, help="log_prob_micro_batch_size_per_gpu")
     ap.add_argument("--dynamic-bsz", type=int, default=0,
                     help="use_dynamic_bsz with this ppo_max_token_len_per_gpu (and log-prob budget); 0 = off")
@@ -100,16 +113,23 @@ def parse():
     ap.add_argument("--model", default="0.5b")
     ap.add_argument("--logprob-inplace-bwd", type=int, default=0,
                     help="1: dlogits over the logits (reference's inplace_backward); 0: fresh buffer (faster stream)")
+    ap.add_argument("--old-noise", type=float, default=0.05,
+                    help="old_log_probs = recomputed + N(0, s^2) (SURVEY §8d: ratios straddle the clip band)")
+    ap.add_argument("--zero", type=int, default=0, choices=[0, 1],
+                    help="1: ZeRO-style sharded fp32 master / AdamW state over the ranks (reduce-scatter + all-gather)")
     ap.add_argument("--no-rmpad", action="store_true")
     ap.add_argument("--no-mixed-precision", action="store_true", help="fp32 weights + autocast instead of bf16/fp32-master")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--cpu-sample-rows", type=int, default=24576,
-                    help="response tokens of the CPU baseline's log-prob sample (~10 s on 16 cores)")
+    ap.add_argument("--cpu-sample-rows", type=int, default=2048,
+                    help="response tokens per repetition of the CPU baseline's log-prob fwd+bwd sample")
+    ap.add_argument("--cpu-reps", type=int, default=5, help="timed repetitions (after 1 warm-up) of the CPU baseline")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
     ap.add_argument("--tune", action="append", default=[],
                     help="KEY=VALUE va_set_tuning override for A/B runs (e.g. 8=0: grid-stride SwiGLU)")
-    return ap.parse_args()
+    ap.add_argument("--launcher-check", action="store_true",
+                    help="only start the ranks, check the world size and print a JSON line (no GPU work)")
+    return ap.parse_args(argv)
 
 
 _T0 = time.perf_counter()
@@ -120,39 +140,51 @@ def log(rank, msg):
         print(f"[bench +{time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
-def _barrier(world):
-    if world > 1:
-        dist.barrier()
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
-def cpu_baseline(args, rank) -> dict | None:
-    """Oracle (eager PyTorch CPU restatement of the reference) on the box's host cores, bounded
-    sample: log-prob + entropy of ``cpu_sample_rows`` response tokens over the full vocab (fp32
-    row loop, torch_functional.py:116-133, 145-149) and GRPO + clipped loss + k3 KL over the
-    full 512 x 1024 batch (core_algos.py). Reported as hot-path tokens/s (not the whole update:
-    the model GEMMs are outside the oracle)."""
-    if rank != 0:
-        return None
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """Start ``torch.distributed.run`` with n ranks as a child process and return its exit code.
+
+    Called before anything touches the GPU (no HIP initialisation in this parent, and no exec):
+    the ranks are fresh processes. A failing rank makes torch.distributed.run exit non-zero."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def cpu_baseline(args) -> dict:
+    """The oracle (eager PyTorch CPU restatement of the reference, `port`) timed on the box's host
+    cores: BASELINE.md §2 / SURVEY §8d — 1 warm-up + median of ``cpu_reps`` repetitions of
+      * log-prob + entropy forward AND backward through autograd over the full vocab for
+        ``cpu_sample_rows`` response tokens (fp32 row loop, torch_functional.py:116-133, 145-149;
+        the headline's 524,288 x 151,936 logits cannot be materialised on a host, so this is a
+        bounded sample scaled per token);
+      * GRPO advantages + clipped loss + k3 KL forward/backward over the full 512 x 1024 batch
+        (core_algos.py:246-308, 722-794, 1034-1069).
+    Reported as hot-path tokens/s (model GEMMs excluded: they are not in the oracle)."""
+    import numpy as np
+    import torch
+
     from oracle import reference_ops as ref
 
-    # the box grants a CPU share (OMP_NUM_THREADS=16 there) although affinity lists every host CPU
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(len(os.sched_getaffinity(0)), 16)
+    affinity = len(os.sched_getaffinity(0))
+    # the box grants a CPU share (OMP_NUM_THREADS=16 there) while affinity lists every host CPU
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
+    cores = min(cores, affinity)
     torch.set_num_threads(cores)
-    V = 151936
-    chunk = min(args.cpu_sample_rows, 2048)  # one 1.2 GB fp32 logits buffer, reused per chunk
-    n_chunks = max(1, args.cpu_sample_rows // chunk)
-    rows = chunk * n_chunks
+    V = VOCAB
+    rows = args.cpu_sample_rows
     g = torch.Generator().manual_seed(0)
-    logits = torch.randn(chunk, V, generator=g) * 2
-    t_lp = 0.0
-    for _ in range(n_chunks):
-        labels = torch.randint(0, V, (chunk,), generator=g)
-        t0 = time.perf_counter()
-        lp = ref.logprobs_from_logits(logits, labels)
-        ent = ref.entropy_from_logits(logits)
-        t_lp += time.perf_counter() - t0
-        del lp, ent
-    del logits
+    logits = torch.randn(rows, V, generator=g) * 2
+    labels = torch.randint(0, V, (rows,), generator=g)
     B, R, n = args.prompts * args.n, args.response_len, args.n
     rewards = torch.zeros(B, R)
     rewards[:, -1] = torch.randint(0, 2, (B,), generator=g).float()
@@ -161,34 +193,116 @@ def cpu_baseline(args, rank) -> dict | None:
     new = -torch.rand(B, R, generator=g)
     old = new + 0.05 * torch.randn(B, R, generator=g)
     refl = new + 0.1 * torch.randn(B, R, generator=g)
-    t0 = time.perf_counter()
-    adv, _ = ref.compute_grpo_outcome_advantage(rewards, mask, index)
-    newr = new.clone().requires_grad_(True)
-    loss, _ = ref.actor_loss(old, newr, adv, mask, ref_log_prob=refl, kl_loss_type="low_var_kl")
-    loss.backward()
-    t_algo = time.perf_counter() - t0
+
+    def lp_pass():
+        x = logits.clone().requires_grad_(True)
+        t0 = time.perf_counter()
+        lp = ref.logprobs_from_logits(x, labels)
+        ent = ref.entropy_from_logits(x)
+        (lp.sum() + ent.sum()).backward()
+        dt = time.perf_counter() - t0
+        del x, lp, ent
+        return dt
+
+    def algo_pass():
+        t0 = time.perf_counter()
+        adv, _ = ref.compute_grpo_outcome_advantage(rewards, mask, index)
+        newr = new.clone().requires_grad_(True)
+        loss, _ = ref.actor_loss(old, newr, adv, mask, ref_log_prob=refl, kl_loss_type="low_var_kl")
+        loss.backward()
+        return time.perf_counter() - t0
+
+    lp_pass()  # warm-up
+    algo_pass()
+    t_lp = sorted(lp_pass() for _ in range(args.cpu_reps))[args.cpu_reps // 2]
+    t_algo = sorted(algo_pass() for _ in range(args.cpu_reps))[args.cpu_reps // 2]
     per_token = t_lp / rows + t_algo / (B * R)
     return {
         "value": round(1.0 / per_token, 1),
         "unit": "tokens/s",
         "cores": cores,
         "kind": "port",
-        "sample": (f"oracle log-prob+entropy fwd of {rows} tokens ({n_chunks} x {chunk}) x V={V} fp32 ({t_lp:.2f}s) + GRPO adv + "
-                   f"clipped loss + k3 KL fwd/bwd on {B}x{R} ({t_algo:.2f}s); model GEMMs excluded"),
+        "os_cpu_count": os.cpu_count(),
+        "affinity_cpus": affinity,
+        "torch_threads": torch.get_num_threads(),
+        "sample": (f"oracle log-prob+entropy fwd+bwd (autograd) of {rows} tokens x V={V} fp32 "
+                   f"(median {t_lp:.2f}s) + GRPO adv + clipped loss + k3 KL fwd/bwd on {B}x{R} "
+                   f"(median {t_algo:.2f}s); 1 warm-up + median of {args.cpu_reps}; model GEMMs excluded"),
     }
+
+
+def shard_batch(args, rank: int, world: int, dev):
+    """This rank's DataProto shard of the benchmark batch.
+
+    strong: the SAME 512 x 1024 batch is built on every rank (seeded), in prompt-group order, and
+    rank r takes rows [r B/W, (r+1) B/W) — 64/W whole prompt groups — then shuffles them (the
+    permutation _balance_batch would apply inside a rank). With ``balance`` the whole batch is
+    first shuffled and KK-balanced over the W ranks (groups split across ranks).
+    weak: every rank builds its own full batch (seed 1234 + rank)."""
+    import numpy as np
+    import torch
+
+    from verl_amd.trainer.ppo.ray_trainer import balance_batch
+    from verl_amd.utils.synthetic import make_grpo_batch
+
+    if args.scaling == "weak":
+        return make_grpo_batch(args.prompts, args.n, args.prompt_len, args.response_len, seed=1234 + rank,
+                               device=dev)
+    full = make_grpo_batch(args.prompts, args.n, args.prompt_len, args.response_len, seed=1234,
+                           permute=args.balance)
+    B = len(full)
+    if B % world:
+        raise SystemExit(f"{B} responses do not split evenly over {world} ranks")
+    if args.balance:
+        balance_batch(full, world, {})
+        shard = full.chunk(world)[rank]
+    else:
+        shard = full.chunk(world)[rank]
+        shard.reorder(torch.from_numpy(np.random.RandomState(1234 + rank).permutation(len(shard))))
+    shard.meta_info["global_token_num"] = shard.batch["attention_mask"].sum(-1).tolist()
+    return shard.to(dev)
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # not under a launcher: start one (child process, before any GPU call) and exit with its rc
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+
+    import torch
+    import torch.distributed as dist
+
+    from verl_amd.workers.dp_workers import init_distributed, local_device_index
+
+    if args.launcher_check:
+        os.environ.setdefault("VA_DIST_BACKEND", "gloo")
+    rank, world = init_distributed()
+    world_seen = dist.get_world_size() if dist.is_initialized() else 1
+    if world_seen != args.gpus:
+        print(f"[bench] rank {rank}: --gpus {args.gpus} but the process group has {world_seen} ranks",
+              file=sys.stderr, flush=True)
+        sys.exit(3)
+    if args.launcher_check:
+        fail = os.environ.get("VA_BENCH_FAIL_RANK")
+        if fail is not None and int(fail) == rank:
+            print(f"[bench] rank {rank}: failing on request (VA_BENCH_FAIL_RANK)", file=sys.stderr, flush=True)
+            sys.exit(7)
+        t = torch.tensor([rank + 1.0])
+        if world > 1:
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"launcher_check": True, "n_gpus": args.gpus, "world_seen": world_seen,
+                              "rank_sum": float(t.item())}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
     from verl_amd import kernels as K
     from verl_amd.trainer.ppo.core_algos import AdvantageEstimator
-    from verl_amd.trainer.ppo.ray_trainer import compute_advantage
     from verl_amd.utils.config import AttrDict, actor_config
     from verl_amd.utils.model import build_qwen2
-    from verl_amd.utils.synthetic import make_grpo_batch
-    from verl_amd.workers.dp_workers import ActorWorker, init_distributed, local_device_index
+    from verl_amd.workers.dp_workers import ActorWorker
 
-    rank, world = init_distributed()
     local = local_device_index()
     if args.tune:
         from verl_amd import _lib as L
@@ -198,15 +312,18 @@ def main():
             L.call("va_set_tuning", key, val)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
-    B = args.prompts * args.n
+    strong = args.scaling == "strong"
+    B_total = args.prompts * args.n * (1 if strong else world)
+    B = B_total // world if strong else args.prompts * args.n  # responses on this rank
     R = args.response_len
+    micro = min(args.micro, B)
+    lp_micro = min(args.logprob_micro, B)
     cfg = AttrDict(
         actor=actor_config(
-            ppo_mini_batch_size=args.prompts,  # prompts; x n / world in ActorWorker -> one optimizer step
-            ppo_micro_batch_size_per_gpu=args.micro,
+            # prompts per mini-batch; x rollout_n / world in ActorWorker -> one optimizer step per rank
+            ppo_mini_batch_size=args.prompts if strong else args.prompts * world,
+            ppo_micro_batch_size_per_gpu=micro,
             use_kl_loss=True, kl_loss_coef=0.001, kl_loss_type="low_var_kl",
             clip_ratio=0.2, clip_ratio_c=3.0, loss_agg_mode="token-mean", entropy_coeff=0,
             use_remove_padding=not args.no_rmpad,
@@ -215,27 +332,32 @@ def main():
             logprob_inplace_backward=bool(args.logprob_inplace_bwd),
             gemm_tuning_file=None if args.gemm_table in (None, "none") else args.gemm_table,
         ),
-        rollout=AttrDict(log_prob_micro_batch_size_per_gpu=args.logprob_micro, temperature=1.0,
+        rollout=AttrDict(log_prob_micro_batch_size_per_gpu=lp_micro, temperature=1.0,
                          log_prob_use_dynamic_bsz=args.dynamic_bsz > 0,
                          log_prob_max_token_len_per_gpu=args.dynamic_bsz or 16384),
     )
-    # weak scaling: every rank owns a full 512-response shard; normalise against world=1
-    worker = ActorWorker(cfg, rollout_n=args.n * world)
+    worker = ActorWorker(cfg, rollout_n=args.n)
     model = build_qwen2(args.model, device=dev, seed=0)
-    worker.init_model(model, mixed_precision=not args.no_mixed_precision)
-    log(rank, f"model ready ({sum(p.numel() for p in model.parameters()) / 1e6:.1f}M params), world={world}")
-    batch = make_grpo_batch(args.prompts, args.n, args.prompt_len, R, seed=1234 + rank, device=dev)
+    worker.init_model(model, mixed_precision=not args.no_mixed_precision, zero=bool(args.zero))
+    log(rank, f"model ready ({sum(p.numel() for p in model.parameters()) / 1e6:.1f}M params), world={world}, "
+              f"{args.scaling} scaling, {B} responses on this rank")
+    batch = shard_batch(args, rank, world, dev)
+    assert len(batch) == B, (len(batch), B)
     # reference-policy log-probs are an input of the step (ref = new + N(0, 0.1^2))
+    gen = torch.Generator(device=dev).manual_seed(99 + rank)
     with torch.no_grad():
         lp0 = worker.compute_log_prob(batch).batch["old_log_probs"]
-        gen = torch.Generator(device=dev).manual_seed(99 + rank)
         batch.batch["ref_log_prob"] = lp0 + 0.1 * torch.randn(lp0.shape, device=dev, generator=gen)
     del lp0
 
     def step():
         out = worker.compute_log_prob(batch)
-        batch.batch["old_log_probs"] = out.batch["old_log_probs"]
-        compute_advantage(batch, AdvantageEstimator.GRPO, norm_adv_by_std_in_grpo=True)
+        old = out.batch["old_log_probs"]
+        if args.old_noise:
+            # old = new + N(0, 0.05^2) so the timed step exercises the clip branches
+            old = old + args.old_noise * torch.randn(old.shape, device=dev, generator=gen)
+        batch.batch["old_log_probs"] = old
+        worker.compute_advantage(batch, AdvantageEstimator.GRPO, norm_adv_by_std_in_grpo=True)
         return worker.update_actor(batch)
 
     log(rank, "batch + reference log-probs ready")
@@ -246,7 +368,9 @@ def main():
     torch.cuda.synchronize()
     if not args.no_kernel_timing:
         K.TIMER = K.KernelTimer()
-    _barrier(world)
+    comm_timer = worker.actor.grad_reducer.start_timing() if world > 1 else None
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     metrics = None
@@ -254,7 +378,8 @@ def main():
         metrics = step()
         log(rank, f"timed step {i} issued")
     torch.cuda.synchronize()
-    _barrier(world)
+    if world > 1:
+        dist.barrier()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -262,6 +387,16 @@ def main():
     elapsed = float(t.item())
     ksum = K.TIMER.summary() if K.TIMER is not None else {}
     K.TIMER = None
+    comm = None
+    if world > 1:
+        exposed_ms = worker.actor.grad_reducer.stop_timing()
+        ex = torch.tensor([exposed_ms / args.steps], dtype=torch.float64, device=dev)
+        dist.all_reduce(ex, op=dist.ReduceOp.MAX)
+        comm = {"exposed_allreduce_ms_per_step": round(float(ex.item()), 3),
+                "isolated_allreduce_ms_per_step": round(worker.actor.grad_reducer.time_isolated_sync(), 3),
+                "grad_bytes": worker.actor.grad_reducer.grad_bytes(),
+                "backend": dist.get_backend()}
+    del comm_timer
 
     resp_tokens = int(batch.batch["response_mask"].sum().item())
     total_tokens = torch.tensor([resp_tokens, sum(batch.meta_info["global_token_num"])], dtype=torch.float64,
@@ -274,57 +409,45 @@ def main():
     log(rank, f"timed region: {elapsed:.2f}s for {args.steps} steps")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N = 1 only
-        cpu = cpu_baseline(args, rank)
+        cpu = cpu_baseline(args)
         log(rank, f"cpu baseline: {cpu['value']} tokens/s on {cpu['cores']} threads")
 
     if rank == 0:
         roof = None
         if ksum:
-            dom = max(ksum.items(), key=lambda kv: kv[1]["time_ms_total"])
-            name, d = dom
+            name, d = max(ksum.items(), key=lambda kv: kv[1]["time_ms_total"])
             if "tflops" in d:  # MFMA-bound fused lm_head + log-prob kernel
                 roof = {
-                    "kernel": name,
-                    "bound": "mfma",
-                    "achieved": round(d["tflops"], 1),
-                    "peak": MFMA_BF16_PEAK_TFLOPS,
-                    "unit": "TFLOP/s",
-                    "frac": round(d["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4),
-                    "traffic": None,
-                    "algo_flops_per_launch": d["avg_flops"],
-                    "avg_launch_us": round(d["avg_us"], 2),
+                    "kernel": name, "bound": "mfma", "achieved": round(d["tflops"], 1),
+                    "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(d["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                    "algo_flops_per_launch": d["avg_flops"], "avg_launch_us": round(d["avg_us"], 2),
                     "launches": d["launches"],
                 }
             else:
-                traffic, src = pmc_traffic(name, d["avg_bytes"], 151936)
-                per_row = 2 * 2 * 151936 + 28 if name.endswith("bwd") else 2 * 151936 + 20  # bf16 rows
+                traffic, src = pmc_traffic(name, d["avg_bytes"], VOCAB)
+                per_row = 2 * 2 * VOCAB + 28 if name.endswith("bwd") else 2 * VOCAB + 20  # bf16 rows
                 ceil, ceil_src = hbm_ceiling(name, round(d["avg_bytes"] / per_row), bool(args.logprob_inplace_bwd))
                 roof = {
-                    "kernel": name,
-                    "bound": "hbm",
-                    "achieved": round(d["gbps"], 1),
-                    "peak": HBM_PEAK_GBPS,
-                    "unit": "GB/s",
-                    "frac": round(d["gbps"] / HBM_PEAK_GBPS, 4),
-                    "traffic": round(traffic) if traffic else None,
-                    "traffic_source": src,
+                    "kernel": name, "bound": "hbm", "achieved": round(d["gbps"], 1), "peak": HBM_PEAK_GBPS,
+                    "unit": "GB/s", "frac": round(d["gbps"] / HBM_PEAK_GBPS, 4),
+                    "traffic": round(traffic) if traffic else None, "traffic_source": src,
                     "measured_stream_ceiling": ceil,
                     "frac_of_measured_ceiling": round(d["gbps"] / ceil, 4) if ceil else None,
-                    "ceiling_source": ceil_src,
-                    "algo_bytes_per_launch": d["avg_bytes"],
-                    "avg_launch_us": round(d["avg_us"], 2),
-                    "launches": d["launches"],
+                    "ceiling_source": ceil_src, "algo_bytes_per_launch": d["avg_bytes"],
+                    "avg_launch_us": round(d["avg_us"], 2), "launches": d["launches"],
                 }
         line = {
             "metric": "GRPO actor-update tokens/sec (512x1024)",
             "value": round(tok_s, 1),
             "unit": "tokens/s",
             "n_gpus": world,
+            "world_seen": world_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 2),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (random token ids, Bernoulli outcome rewards; random-init weights)",
@@ -332,17 +455,26 @@ def main():
                 "workload": "GRPO actor update: old-logp fwd + GRPO adv + fwd/fused clipped loss+k3 KL/bwd + "
                             "RCCL grad all-reduce + clip + AdamW",
                 "model": "Qwen2.5-0.5B architecture",
-                "global_batch": B * world,
+                "global_batch": B_total,
                 "responses_per_gpu": B,
+                "prompts_per_gpu": args.prompts // world if strong else args.prompts,
+                "groups_split_over_ranks": bool(args.balance and world > 1 and strong),
                 "seq_len": args.prompt_len + R,
                 "response_len": R,
-                "vocab": 151936,
-                "micro_batch": args.micro,
-                "logprob_micro_batch": args.logprob_micro,
+                "vocab": VOCAB,
+                "micro_batch": micro,
+                "logprob_micro_batch": lp_micro,
+                "old_logp_noise": args.old_noise,
+                "deviations_from_reference_defaults": (
+                    f"ppo_micro_batch_size_per_gpu {micro} (SURVEY §8d: 8; larger micro-batches fill the "
+                    "MI355X GEMMs, same loss semantics: token-mean per micro-batch / grad-accum); "
+                    + ("out-of-place log-prob backward (reference: in place)" if not args.logprob_inplace_bwd
+                       else "in-place log-prob backward as the reference")),
                 "dynamic_bsz_max_token_len": args.dynamic_bsz or None,
                 "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
                 "pack_pad_multiple": args.pad_multiple,
                 "logprob_inplace_backward": bool(args.logprob_inplace_bwd),
+                "zero_sharded_optimizer": bool(args.zero),
                 "tuning_overrides": args.tune or None,
                 "gemm_table": _gemm_table_name(),
                 "parallelism": f"dp{world}",
@@ -351,6 +483,7 @@ def main():
                 else "fp32 weights + bf16 autocast",
             },
             "perf_throughput": round(perf_throughput, 1),
+            "comm": comm,
             "roofline": roof,
             "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in ksum.items()},

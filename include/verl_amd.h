@@ -204,18 +204,37 @@ int va_masked_agg_bwd(const float *g, const void *mask, int mask_dtype, int64_t 
                       int mode, const void *workspace, float *dx, void *stream);
 
 /* ---------------------------------------------------------------------------------------
- * Outcome advantages over prompt groups (GRPO and relatives), one launch.
- * Replaces: core_algos.py:246-308 (compute_grpo_outcome_advantage) and the group-mean part of
- * :376-476 (RF++-baseline, RLOO). Groups are given in CSR form built on host from the uid
- * array (np.unique(return_inverse) + stable argsort; the host-side grouping of
- * core_algos.py:290-291): rows of group g are order[offsets[g] .. offsets[g+1]).
+ * Outcome advantages over prompt groups (GRPO and relatives).
+ * Replaces: core_algos.py:246-308 (compute_grpo_outcome_advantage), :311-370 (pass@k),
+ * :428-476 (RLOO), :479-530 (OPO) and the group-mean part of :376-424 (RF++-baseline). Groups
+ * are given in CSR form built on host from the uid array (np.unique(return_inverse) + stable
+ * argsort; the host-side grouping of core_algos.py:290-291): rows of group g are
+ * order[offsets[g] .. offsets[g+1]), in batch order (the reference's member order).
  *   score[b] = sum_t rewards[b,t] (unmasked, core_algos.py:282)
  *   adv[b,t] = a(b) * mask[b,t]; also writes scores[B] fp32 if non-NULL.
- * Singleton group: mean 0, std 1 (core_algos.py:293-295). ------------------------------ */
+ * Singleton group: mean 0, std 1 (core_algos.py:293-295).
+ * workspace: va_outcome_workspace_bytes(B). Three launches: va_row_scores, va_group_coef,
+ * va_broadcast_rows, which are also exported for the data-parallel form, where a batch's groups
+ * span ranks (the reference computes over the whole batch on the driver after _balance_batch,
+ * ray_trainer.py:1204-1205, 262-273): each rank scores its own rows, the (score, length) pairs
+ * are all-gathered, va_group_coef runs on the gathered batch and va_broadcast_rows on the
+ * rank's own rows (coef pointer offset by the rank's first global row).
+ *   va_row_scores:    scores[B] (+ lengths[B] = sum_t mask[b,t] if non-NULL, OPO)
+ *   va_group_coef:    coef[N] = a(b) for every row of the N-row (gathered) batch
+ *   va_broadcast_rows: adv[b,t] = coef[b] * mask[b,t]
+ * ------------------------------------------------------------------------------------ */
+int64_t va_outcome_workspace_bytes(int64_t B);
 int va_outcome_advantage(const float *rewards, const void *mask, int mask_dtype, int64_t B,
                          int64_t R, const int32_t *order, const int32_t *offsets,
                          int64_t n_groups, int64_t max_group_size, float epsilon, int estimator,
-                         float *adv, float *scores, void *stream);
+                         float *adv, float *scores, void *workspace, void *stream);
+int va_row_scores(const float *rewards, const void *mask, int mask_dtype, int64_t B, int64_t R,
+                  float *scores, float *lengths, void *stream);
+int va_group_coef(const float *scores, const float *lengths, const int32_t *order,
+                  const int32_t *offsets, int64_t n_groups, int64_t max_group_size, float epsilon,
+                  int estimator, float *coef, void *stream);
+int va_broadcast_rows(const float *coef, const void *mask, int mask_dtype, int64_t B, int64_t R,
+                      float *adv, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * GAE (core_algos.py:193-241): masked reverse recurrence per row as an LDS-staged chunked

@@ -160,3 +160,128 @@ def _dispatch_worker(rank, world, port):
 
 def test_dp_dispatch_collect_and_all_gather():
     _run(_dispatch_worker)
+
+
+# ------------------------------------------------------------------ ordered buckets + rank-0 sync
+def _order_worker(rank, world, port):
+    _init(rank, world, port)
+    from verl_amd.workers.grad_sync import GradBucketReducer
+
+    torch.manual_seed(100 + rank)  # different init per rank: the reducer must sync from rank 0
+    model = torch.nn.Sequential(torch.nn.Linear(6, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
+    red = GradBucketReducer(model.parameters(), bucket_bytes=256)
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    parts = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(parts, flat)
+    assert all(torch.equal(parts[0], p) for p in parts)
+    # launches happen in bucket order even when a later bucket completes first
+    launched = []
+    orig = red._collective
+    red._collective = lambda b: (launched.append(b.index), orig(b))[1]
+    red.zero_grad()
+    red.begin_sync()
+    red._mark_ready(red.buckets[-1])  # last bucket ready first: nothing may launch yet
+    assert launched == []
+    for b in red.buckets[:-1]:
+        red._mark_ready(b)
+    red.finish_sync()
+    assert launched == list(range(len(red.buckets)))
+    dist.destroy_process_group()
+
+
+def test_reducer_syncs_rank0_params_and_orders_collectives():
+    _run(_order_worker)
+
+
+# ------------------------------------------------------------------ ZeRO-sharded masters
+def _zero_worker(rank, world, port):
+    _init(rank, world, port)
+    from verl_amd.workers.grad_sync import MixedPrecisionParams, ShardedMixedPrecisionParams
+
+    def model():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(torch.nn.Linear(6, 40), torch.nn.Tanh(), torch.nn.Linear(40, 3))
+
+    a, b = model(), model()
+    rep = MixedPrecisionParams(a, bucket_bytes=512)
+    shd = ShardedMixedPrecisionParams(b, bucket_bytes=512)
+    assert len(shd.buckets) > 1
+    opt_a = torch.optim.AdamW(rep.optimizer_params(), lr=1e-2, weight_decay=0.01, foreach=False)
+    opt_b = torch.optim.AdamW(shd.optimizer_params(), lr=1e-2, weight_decay=0.01, foreach=False)
+    g = torch.Generator().manual_seed(5)
+    xs = [torch.randn(4, 6, generator=g) for _ in range(world * 2)]
+    for step in range(3):
+        for mgr, mod, opt in ((rep, a, opt_a), (shd, b, opt_b)):
+            mgr.zero_grad()
+            for i, x in enumerate(xs[rank * 2 : rank * 2 + 2]):
+                if i == 1:
+                    mgr.begin_sync()
+                (mod(x.bfloat16() + step).float().square().mean() / 2).backward()
+            mgr.finish_sync()
+        n_rep = torch.nn.utils.clip_grad_norm_(rep.optimizer_params(), max_norm=0.5, foreach=True)
+        n_shd = shd.clip_grad_norm_(0.5)
+        assert torch.allclose(n_rep, n_shd, rtol=1e-5), (n_rep, n_shd)
+        opt_a.step()
+        opt_b.step()
+        rep.after_step()
+        shd.after_step()
+        for (n, p), q in zip(a.named_parameters(), b.parameters(), strict=True):
+            assert p.dtype == q.dtype == torch.bfloat16
+            assert torch.allclose(p.float(), q.float(), atol=1e-2, rtol=0), (step, n)
+        # the shards of the masters equal the replicated masters (fp32)
+        full = torch.cat([m.detach().reshape(-1) for m in reversed(rep.optimizer_params())])
+        mine = torch.cat([s.detach() for s in shd.shards])
+        per = [s.numel() for s in shd.shards]
+        offs, o = [], 0
+        for bkt, n_per in zip(shd.buckets, per, strict=True):
+            n_real = sum(p.numel() for p in bkt.params)
+            lo = rank * n_per
+            hi = min(lo + n_per, n_real)
+            if hi > lo:
+                got = shd.shards[bkt.index].detach()[: hi - lo]
+                want = full[o + lo : o + hi]
+                assert torch.allclose(got, want, atol=1e-6, rtol=1e-5), (step, bkt.index)
+            o += n_real
+        del mine, offs
+    mem = shd.memory_bytes()
+    assert mem["fp32_master_shard"] * world >= sum(p.numel() for p in b.parameters()) * 4
+    dist.destroy_process_group()
+
+
+def test_zero_sharded_masters_match_replicated_dp():
+    _run(_zero_worker)
+
+
+# ------------------------------------------------------------------ cross-rank group scores
+def _gather_worker(rank, world, port):
+    _init(rank, world, port)
+    from verl_amd.trainer.ppo.dp_algos import check_groups_intact, gather_row_scores, uid_keys
+
+    # rank r holds rows [3r, 3r + 3) of a 3W-row batch whose groups straddle the ranks
+    rows = list(range(3 * rank, 3 * rank + 3))
+    uids = np.array([f"g{i // 2}" for i in rows], dtype=object)
+    scores = torch.tensor([float(i) for i in rows])
+    lens = torch.tensor([10.0 + i for i in rows])
+    s_all, l_all, keys, off = gather_row_scores(scores, lens, uids, None)
+    assert off == 3 * rank
+    assert s_all.tolist() == [float(i) for i in range(3 * world)]
+    assert l_all.tolist() == [10.0 + i for i in range(3 * world)]
+    full_uids = np.array([f"g{i // 2}" for i in range(3 * world)], dtype=object)
+    assert (keys == uid_keys(full_uids)).all()
+    assert not check_groups_intact(uids)
+    assert check_groups_intact(np.array([f"r{rank}-{i}" for i in range(3)], dtype=object))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_row_scores_rank_order(world):
+    port = _free_port()
+    mp.spawn(_gather_worker, args=(world, port), nprocs=world, join=True)
+
+
+def test_uid_keys_distinguish_types_and_values():
+    from verl_amd.trainer.ppo.dp_algos import uid_keys
+
+    k = uid_keys(np.array(["a", "b", "a", 1, "1"], dtype=object))
+    assert k[0] == k[2] and k[0] != k[1] and k[3] != k[4]
+    assert (k >= 0).all()

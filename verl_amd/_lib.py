@@ -57,10 +57,14 @@ _SIGNATURES: dict[str, tuple] = {
     "va_agg_workspace_bytes": (c_int64, [c_int64]),
     "va_masked_agg_fwd": (c_int, [_P, _P, c_int, c_int64, c_int64, c_int, _P, _P, _P]),
     "va_masked_agg_bwd": (c_int, [_P, _P, c_int, c_int64, c_int64, c_int, _P, _P, _P]),
+    "va_outcome_workspace_bytes": (c_int64, [c_int64]),
     "va_outcome_advantage": (
         c_int,
-        [_P, _P, c_int, c_int64, c_int64, _P, _P, c_int64, c_int64, c_float, c_int, _P, _P, _P],
+        [_P, _P, c_int, c_int64, c_int64, _P, _P, c_int64, c_int64, c_float, c_int, _P, _P, _P, _P],
     ),
+    "va_row_scores": (c_int, [_P, _P, c_int, c_int64, c_int64, _P, _P, _P]),
+    "va_group_coef": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_float, c_int, _P, _P]),
+    "va_broadcast_rows": (c_int, [_P, _P, c_int, c_int64, c_int64, _P, _P]),
     "va_gae_workspace_bytes": (c_int64, [c_int64]),
     "va_gae_scan": (c_int, [_P, _P, _P, c_int, c_int64, c_int64, c_float, c_float, _P, _P, _P, _P]),
     "va_masked_row_partials": (c_int, [_P, _P, c_int, c_int64, c_int64, _P, _P]),

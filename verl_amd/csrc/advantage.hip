@@ -9,10 +9,9 @@
 //   torch_functional.py:188-223 masked_var (unbiased; ValueError at mask sum 0/1),
 //                          masked_whiten: (x - mean) * rsqrt(var + 1e-8)
 //
-// GRPO: one workgroup per prompt group. Its 4 waves reduce the group's rewards rows (one
-// wave per row, 16-byte loads) into scores held in LDS, wave 0 forms mean / unbiased std in
-// fp64 in member order, and the waves write the advantage rows (a * mask). One launch, the
-// rewards are read once.
+// GRPO family: row scores (one wave per row) -> per-group coefficients (one wave per group, fp64
+// statistics in member order) -> a(b) * mask broadcast. The middle phase runs on all-gathered
+// scores when the groups of a batch span data-parallel ranks (trainer/ppo/dp_algos.py).
 //
 // GAE: one wave per response row, a 256-thread workgroup carries 4 rows. The row's rewards,
 // values and mask are staged into LDS (coalesced), each lane owns a contiguous chunk of
@@ -32,50 +31,76 @@ namespace {
 constexpr int kPartStride = 3;  // (n, sum, M2) per row, fp64
 
 // ---------------------------------------------------------------- outcome advantages
-template <int MT, int EST>
-__global__ __launch_bounds__(256) void outcome_adv_kernel(
-    const float *__restrict__ rewards, const void *__restrict__ mask, int64_t R,
-    const int32_t *__restrict__ order, const int32_t *__restrict__ offsets, float eps,
-    float *__restrict__ adv, float *__restrict__ scores_out) {
-  extern __shared__ float s_score[];  // [n] scores, [n] lengths (OPO), 4 floats of broadcast stats
+// Three streaming phases (also the data-parallel decomposition: phase 1 runs on each rank's rows,
+// the row scores are all-gathered, phase 2 runs on the global scores, phase 3 on local rows):
+//   1) row_scores: one wave per row, unmasked row sum of the rewards (core_algos.py:282) and, for
+//      OPO, the response length sum(mask) (core_algos.py:505); every 16-B load of the row issued
+//      before the first add;
+//   2) group_coef: one wave per prompt group; the members' scores are staged in LDS by the lanes,
+//      lane 0 forms the statistics in member order in fp64 (torch.mean / torch.std rounded to
+//      fp32), the lanes write each member's coefficient a(b);
+//   3) broadcast_rows: adv[b, t] = a(b) * mask[b, t] over the [B, R] matrix, 4 columns per lane.
+template <int MT, bool LEN>
+__global__ __launch_bounds__(256) void row_scores_kernel(const float *__restrict__ rewards,
+                                                         const void *__restrict__ mask, int64_t B,
+                                                         int64_t R, bool vec, float *__restrict__ scores,
+                                                         float *__restrict__ lengths) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float *r = rewards + row * R;
+  float acc = 0.f;
+  if (vec) {
+    const float4 *r4 = reinterpret_cast<const float4 *>(r);
+    const int64_t nv = R >> 2;
+    int64_t j = lane;
+    for (; j + 3 * kWave < nv; j += 4 * kWave) {  // 4 independent 16-B loads in flight per lane
+      const float4 a = r4[j], b = r4[j + kWave], c = r4[j + 2 * kWave], d = r4[j + 3 * kWave];
+      acc += (a.x + a.y) + (a.z + a.w);
+      acc += (b.x + b.y) + (b.z + b.w);
+      acc += (c.x + c.y) + (c.z + c.w);
+      acc += (d.x + d.y) + (d.z + d.w);
+    }
+    for (; j < nv; j += kWave) {
+      const float4 a = r4[j];
+      acc += (a.x + a.y) + (a.z + a.w);
+    }
+  } else {
+    for (int64_t j = lane; j < R; j += kWave) acc += r[j];
+  }
+  acc = wave_sum(acc);
+  float len = 0.f;
+  if constexpr (LEN) {
+    for (int64_t j = lane; j < R; j += kWave) len += load_mask<MT>(mask, row * R + j);
+    len = wave_sum(len);
+  }
+  if (lane == 0) {
+    scores[row] = acc;
+    if constexpr (LEN) lengths[row] = len;
+  }
+}
+
+template <int EST>
+__global__ __launch_bounds__(64) void group_coef_kernel(const float *__restrict__ scores,
+                                                        const float *__restrict__ lengths,
+                                                        const int32_t *__restrict__ order,
+                                                        const int32_t *__restrict__ offsets, float eps,
+                                                        float *__restrict__ coef) {
+  extern __shared__ float s_score[];  // [n] scores, [n] lengths (OPO), 4 floats of group stats
   const int g = blockIdx.x;
   const int beg = offsets[g];
   const int n = offsets[g + 1] - beg;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x;
   float *s_len = s_score + n;
   float *s_stat = s_len + n;
-
-  // 1) scores: unmasked row sums (core_algos.py:282), fp32 like the reference
-  const bool vec = (R % 4 == 0);
-  for (int k = wave; k < n; k += nw) {
-    const int64_t row = order[beg + k];
-    const float *r = rewards + row * R;
-    float acc = 0.f;
-    if (vec) {
-      const float4 *r4 = reinterpret_cast<const float4 *>(r);
-      for (int64_t j = lane; j < R / 4; j += kWave) {
-        const float4 q = r4[j];
-        acc += (q.x + q.y) + (q.z + q.w);
-      }
-    } else {
-      for (int64_t j = lane; j < R; j += kWave) acc += r[j];
-    }
-    acc = wave_sum(acc);
-    if constexpr (EST == VA_ADV_OPO) {  // response length = response_mask.sum(-1) (core_algos.py:505)
-      float len = 0.f;
-      for (int64_t j = lane; j < R; j += kWave) len += load_mask<MT>(mask, row * R + j);
-      len = wave_sum(len);
-      if (lane == 0) s_len[k] = len;
-    }
-    if (lane == 0) {
-      s_score[k] = acc;
-      if (scores_out) scores_out[row] = acc;
-    }
+  for (int k = lane; k < n; k += kWave) {
+    const int row = order[beg + k];
+    s_score[k] = scores[row];
+    if constexpr (EST == VA_ADV_OPO) s_len[k] = lengths[row];
   }
   __syncthreads();
-
-  // 2) group statistics in member order, fp64, rounded to fp32 as torch.mean / torch.std
-  if (threadIdx.x == 0) {
+  if (lane == 0) {
+    // group statistics in member order, fp64, rounded to fp32 as torch.mean / torch.std
     float mean32, std32;
     if (n == 1) {
       mean32 = 0.f;  // core_algos.py:293-295
@@ -123,10 +148,7 @@ __global__ __launch_bounds__(256) void outcome_adv_kernel(
   }
   __syncthreads();
   const float mean = s_stat[0], stdv = s_stat[1];
-
-  // 3) advantage rows: a * mask (core_algos.py:302-306)
-  for (int k = wave; k < n; k += nw) {
-    const int64_t row = order[beg + k];
+  for (int k = lane; k < n; k += kWave) {
     const float s = s_score[k];
     float a;
     if constexpr (EST == VA_ADV_GRPO) {
@@ -143,8 +165,33 @@ __global__ __launch_bounds__(256) void outcome_adv_kernel(
         a = s;
       }
     }
-    float *o = adv + row * R;
-    for (int64_t j = lane; j < R; j += kWave) o[j] = a * load_mask<MT>(mask, row * R + j);
+    coef[order[beg + k]] = a;
+  }
+}
+
+// adv[b, t] = coef[b] * mask[b, t] (core_algos.py:302-306); 4 consecutive columns per lane when
+// R % 4 == 0 (one 16-B store), two such quads in flight per lane per iteration.
+template <int MT, bool VEC>
+__global__ __launch_bounds__(256) void broadcast_rows_kernel(const float *__restrict__ coef,
+                                                             const void *__restrict__ mask,
+                                                             int64_t B, int64_t R,
+                                                             float *__restrict__ adv) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if constexpr (VEC) {
+    const int64_t nq = (B * R) >> 2;
+    for (; i < nq; i += stride) {
+      const int64_t e = i << 2;
+      const float a = coef[e / R];
+      float4 o;
+      o.x = a * load_mask<MT>(mask, e + 0);
+      o.y = a * load_mask<MT>(mask, e + 1);
+      o.z = a * load_mask<MT>(mask, e + 2);
+      o.w = a * load_mask<MT>(mask, e + 3);
+      reinterpret_cast<float4 *>(adv)[i] = o;
+    }
+  } else {
+    for (; i < B * R; i += stride) adv[i] = coef[i / R] * load_mask<MT>(mask, i);
   }
 }
 
@@ -573,35 +620,91 @@ int gae_lds_bytes(int L, int waves) { return waves * 3 * 64 * (L + 1) * 4; }
 
 using namespace va;
 
+extern "C" int va_row_scores(const float *rewards, const void *mask, int mask_dtype, int64_t B,
+                             int64_t R, float *scores, float *lengths, void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0, "bad shape (B=%lld R=%lld)", (long long)B, (long long)R);
+  VA_CHECK_ARG(rewards && scores && (!lengths || mask), "null pointer argument");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<unsigned>((B + 3) / 4)), block(256);
+  const bool vec = (R & 3) == 0 && (reinterpret_cast<uintptr_t>(rewards) & 15) == 0;
+  if (lengths) {
+    VA_DISPATCH_MASK(mask_dtype, {
+      hipLaunchKernelGGL((row_scores_kernel<MT, true>), grid, block, 0, s, rewards, mask, B, R, vec, scores,
+                         lengths);
+    });
+  } else {
+    hipLaunchKernelGGL((row_scores_kernel<VA_MASK_F32, false>), grid, block, 0, s, rewards, nullptr, B, R,
+                       vec, scores, nullptr);
+  }
+  return check_launch("row_scores");
+}
+
+extern "C" int va_group_coef(const float *scores, const float *lengths, const int32_t *order,
+                             const int32_t *offsets, int64_t n_groups, int64_t max_group_size,
+                             float epsilon, int estimator, float *coef, void *stream) {
+  VA_CHECK_ARG(n_groups > 0, "no groups");
+  VA_CHECK_ARG(max_group_size > 0 && max_group_size <= 16384, "group size %lld out of range",
+               (long long)max_group_size);
+  VA_CHECK_ARG(scores && order && offsets && coef, "null pointer argument");
+  VA_CHECK_ARG(estimator != VA_ADV_OPO || lengths, "OPO needs the response lengths");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const size_t shm = static_cast<size_t>(2 * max_group_size + 4) * sizeof(float);
+#define VA_LAUNCH_COEF(E)                                                                      \
+  hipLaunchKernelGGL((group_coef_kernel<E>), dim3(n_groups), dim3(64), shm, s, scores, lengths, \
+                     order, offsets, epsilon, coef)
+  switch (estimator) {
+    case VA_ADV_GRPO: VA_LAUNCH_COEF(VA_ADV_GRPO); break;
+    case VA_ADV_GRPO_NOSTD: VA_LAUNCH_COEF(VA_ADV_GRPO_NOSTD); break;
+    case VA_ADV_RLOO: VA_LAUNCH_COEF(VA_ADV_RLOO); break;
+    case VA_ADV_MEAN_ONLY: VA_LAUNCH_COEF(VA_ADV_MEAN_ONLY); break;
+    case VA_ADV_OPO: VA_LAUNCH_COEF(VA_ADV_OPO); break;
+    case VA_ADV_PASSK: VA_LAUNCH_COEF(VA_ADV_PASSK); break;
+    case VA_ADV_PASSK_NOSTD: VA_LAUNCH_COEF(VA_ADV_PASSK_NOSTD); break;
+    default: set_error("unknown estimator %d", estimator); return VA_E_ARG;
+  }
+#undef VA_LAUNCH_COEF
+  return check_launch("group_coef");
+}
+
+extern "C" int va_broadcast_rows(const float *coef, const void *mask, int mask_dtype, int64_t B,
+                                 int64_t R, float *adv, void *stream) {
+  VA_CHECK_ARG(B > 0 && R > 0, "bad shape (B=%lld R=%lld)", (long long)B, (long long)R);
+  VA_CHECK_ARG(coef && mask && adv, "null pointer argument");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool vec = (R & 3) == 0 && (reinterpret_cast<uintptr_t>(adv) & 15) == 0;
+  const int64_t work = vec ? (B * R) >> 2 : B * R;
+  int64_t grid = (work + 255) / 256;
+  if (grid > 16384) grid = 16384;
+  VA_DISPATCH_MASK(mask_dtype, {
+    if (vec)
+      hipLaunchKernelGGL((broadcast_rows_kernel<MT, true>), dim3(grid), dim3(256), 0, s, coef, mask, B, R, adv);
+    else
+      hipLaunchKernelGGL((broadcast_rows_kernel<MT, false>), dim3(grid), dim3(256), 0, s, coef, mask, B, R, adv);
+  });
+  return check_launch("broadcast_rows");
+}
+
+extern "C" int64_t va_outcome_workspace_bytes(int64_t B) {
+  return static_cast<int64_t>(sizeof(float)) * 3 * B;
+}
+
 extern "C" int va_outcome_advantage(const float *rewards, const void *mask, int mask_dtype,
                                     int64_t B, int64_t R, const int32_t *order,
                                     const int32_t *offsets, int64_t n_groups,
                                     int64_t max_group_size, float epsilon, int estimator,
-                                    float *adv, float *scores, void *stream) {
+                                    float *adv, float *scores, void *workspace, void *stream) {
   VA_CHECK_ARG(B > 0 && R > 0 && n_groups > 0 && n_groups <= B, "bad shape (B=%lld G=%lld)",
                (long long)B, (long long)n_groups);
-  VA_CHECK_ARG(max_group_size > 0 && max_group_size <= 16384, "group size %lld out of range",
-               (long long)max_group_size);
-  VA_CHECK_ARG(rewards && mask && order && offsets && adv, "null pointer argument");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const size_t shm = static_cast<size_t>(2 * max_group_size + 4) * sizeof(float);
-#define VA_LAUNCH_ADV(E)                                                                     \
-  VA_DISPATCH_MASK(mask_dtype, {                                                             \
-    hipLaunchKernelGGL((outcome_adv_kernel<MT, E>), dim3(n_groups), dim3(256), shm, s,        \
-                       rewards, mask, R, order, offsets, epsilon, adv, scores);              \
-  })
-  switch (estimator) {
-    case VA_ADV_GRPO: VA_LAUNCH_ADV(VA_ADV_GRPO); break;
-    case VA_ADV_GRPO_NOSTD: VA_LAUNCH_ADV(VA_ADV_GRPO_NOSTD); break;
-    case VA_ADV_RLOO: VA_LAUNCH_ADV(VA_ADV_RLOO); break;
-    case VA_ADV_MEAN_ONLY: VA_LAUNCH_ADV(VA_ADV_MEAN_ONLY); break;
-    case VA_ADV_OPO: VA_LAUNCH_ADV(VA_ADV_OPO); break;
-    case VA_ADV_PASSK: VA_LAUNCH_ADV(VA_ADV_PASSK); break;
-    case VA_ADV_PASSK_NOSTD: VA_LAUNCH_ADV(VA_ADV_PASSK_NOSTD); break;
-    default: set_error("unknown estimator %d", estimator); return VA_E_ARG;
-  }
-#undef VA_LAUNCH_ADV
-  return check_launch("outcome_advantage");
+  VA_CHECK_ARG(rewards && mask && order && offsets && adv && workspace, "null pointer argument");
+  float *ws = static_cast<float *>(workspace);
+  float *sc = scores ? scores : ws;
+  float *len = ws + B;
+  float *coef = ws + 2 * B;
+  int e = va_row_scores(rewards, mask, mask_dtype, B, R, sc, estimator == VA_ADV_OPO ? len : nullptr, stream);
+  if (e) return e;
+  e = va_group_coef(sc, len, order, offsets, n_groups, max_group_size, epsilon, estimator, coef, stream);
+  if (e) return e;
+  return va_broadcast_rows(coef, mask, mask_dtype, B, R, adv, stream);
 }
 
 extern "C" int64_t va_gae_workspace_bytes(int64_t B) {

@@ -480,10 +480,50 @@ def outcome_advantage(token_level_rewards, response_mask, index, epsilon: float,
     m, mcode = _mask(response_mask)
     order, offsets, G, gmax = group_csr(index, r.device)
     adv = torch.empty_like(r)
+    ws = torch.empty(max(1, L.load().va_outcome_workspace_bytes(B) // 4), dtype=torch.float32, device=r.device)
     L.call(
         "va_outcome_advantage", _p(r), _p(m), mcode, B, R, _p(order), _p(offsets), G, gmax, float(epsilon),
-        estimator, _p(adv), None, _stream(r),
+        estimator, _p(adv), None, _p(ws), _stream(r),
     )
+    return adv
+
+
+def row_scores(token_level_rewards, response_mask=None, lengths: bool = False):
+    """(scores [B], lengths [B] | None): unmasked reward row sums (core_algos.py:282) and, when
+    asked, response lengths sum(mask) (OPO, core_algos.py:505)."""
+    _require_device(token_level_rewards, response_mask)
+    r = _f32(token_level_rewards)
+    B, R = r.shape
+    scores = torch.empty(B, dtype=torch.float32, device=r.device)
+    lens = torch.empty(B, dtype=torch.float32, device=r.device) if lengths else None
+    if lengths:
+        m, mcode = _mask(response_mask)
+    else:
+        m, mcode = None, L.VA_MASK_F32
+    L.call("va_row_scores", _p(r), _p(m), mcode, B, R, _p(scores), _p(lens), _stream(r))
+    return scores, lens
+
+
+def group_coef(scores, lengths, order, offsets, n_groups: int, max_group_size: int, epsilon: float,
+               estimator: int):
+    """Per-row advantage coefficient a(b) of every row of a (possibly all-gathered) batch."""
+    _require_device(scores, lengths, order, offsets)
+    coef = torch.empty_like(scores)
+    L.call("va_group_coef", _p(scores), _p(lengths), _p(order), _p(offsets), n_groups, max_group_size,
+           float(epsilon), estimator, _p(coef), _stream(scores))
+    return coef
+
+
+def broadcast_rows(coef, response_mask):
+    """adv[b, t] = coef[b] * mask[b, t]."""
+    _require_device(coef, response_mask)
+    m, mcode = _mask(response_mask)
+    B, R = m.shape
+    c = _f32(coef)
+    if c.numel() != B:
+        raise ValueError(f"broadcast_rows: {c.numel()} coefficients for {B} rows")
+    adv = torch.empty(B, R, dtype=torch.float32, device=m.device)
+    L.call("va_broadcast_rows", _p(c), _p(m), mcode, B, R, _p(adv), _stream(adv))
     return adv
 
 

@@ -1,18 +1,29 @@
 """Data-parallel advantage estimation: each rank computes advantages for its own shard.
 
-The reference computes advantages on the driver over the whole batch (ray_trainer.py:214-291).
-Sharded over W ranks this is exact when the only batch-global quantity is exchanged:
+The reference computes advantages on the driver over the WHOLE batch (ray_trainer.py:214-291),
+after ``_balance_batch`` has reordered it (ray_trainer.py:1204-1205), so a prompt group may
+span data-parallel ranks. Sharded over W ranks this stays exact when the batch-global
+quantities are exchanged:
 
-  * GRPO / RLOO: groups (prompts) are kept intact on one rank, so no exchange;
-    ``check_groups_intact`` verifies it with one all_gather of the uid sets;
-  * GAE / RF++-baseline whitening (torch_functional.py:206-223) is batch-global: each rank
-    merges its rows' (count, sum, M2) into one fp64 triple on the device, the W triples are
-    all-gathered (24 bytes per rank), and every rank merges them in rank order with the same
-    kernel, so all ranks apply identical (mean, rstd) — bitwise equal to a single-process run
-    over the rows in that order up to the merge tree.
+  * group estimators (GRPO, Dr.GRPO, RLOO, OPO, pass@k, GPG, RF++-baseline): every rank scores
+    its own rows on the device (va_row_scores: unmasked reward sums, plus response lengths for
+    OPO), then ONE all-gather moves (uid key, score, length) — 16 bytes per response, 8 KB at
+    512 responses — so every rank holds the scores of the whole batch in global row order
+    (rank-major, the DP_COMPUTE_PROTO concat order, decorator.py:399-408). The group statistics
+    then run on the gathered batch (va_group_coef, members in batch order as the reference's
+    dict appends them, core_algos.py:290-291) and each rank writes only its own rows
+    (va_broadcast_rows). Results equal a single-process run over the concatenated batch
+    whether or not groups are intact. uid values are exchanged as 63-bit keys (blake2b of the
+    uid's type and value), so ranks agree on group identity without pickling strings;
+  * whitening (GAE, REINFORCE++, RF++-baseline; torch_functional.py:206-223) is batch-global:
+    each rank merges its rows' (count, sum, M2) into one fp64 triple on the device, the W
+    triples are all-gathered (24 bytes per rank), and every rank merges them in rank order with
+    the same kernel, so all ranks apply identical (mean, rstd).
 """
 
 from __future__ import annotations
+
+import hashlib
 
 import numpy as np
 import torch
@@ -20,10 +31,109 @@ import torch.distributed as dist
 
 from ... import _lib as L
 from ... import kernels as K
+from ...protocol import DataProto
+from .core_algos import AdvantageEstimator
+
+_GROUP_ESTIMATORS = {
+    AdvantageEstimator.GRPO: None,  # (code chosen by norm_adv_by_std_in_grpo)
+    AdvantageEstimator.RLOO: L.VA_ADV_RLOO,
+    AdvantageEstimator.OPO: L.VA_ADV_OPO,
+    AdvantageEstimator.GRPO_PASSK: None,
+    AdvantageEstimator.GPG: L.VA_ADV_MEAN_ONLY,
+    AdvantageEstimator.REINFORCE_PLUS_PLUS_BASELINE: L.VA_ADV_MEAN_ONLY,
+}
 
 
 def _world(group) -> int:
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+
+
+def _rank(group) -> int:
+    return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+
+
+def _all_gather(t: torch.Tensor, group=None) -> list[torch.Tensor]:
+    """all_gather of equal-shape tensors; gloo moves host tensors, RCCL device tensors."""
+    w = _world(group)
+    if w == 1:
+        return [t]
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        parts = [torch.empty_like(t, device="cpu") for _ in range(w)]
+        dist.all_gather(parts, t.cpu(), group=group)
+        return [p.to(t.device) for p in parts]
+    parts = [torch.empty_like(t) for _ in range(w)]
+    dist.all_gather(parts, t, group=group)
+    return parts
+
+
+def uid_keys(index) -> np.ndarray:
+    """63-bit key per uid: equal uids give equal keys on every rank (the reference groups by the
+    uid value itself, core_algos.py:290; uids are uuid4 strings, ray_trainer.py:1160)."""
+    cache: dict = {}
+    out = np.empty(len(index), dtype=np.int64)
+    for i, u in enumerate(index):
+        k = cache.get(u)
+        if k is None:
+            v = u.item() if isinstance(u, np.generic) else u
+            d = hashlib.blake2b(f"{type(v).__name__}:{v}".encode(), digest_size=8).digest()
+            k = int.from_bytes(d, "little") >> 1
+            cache[u] = k
+        out[i] = k
+    return out
+
+
+def gather_row_scores(scores: torch.Tensor, lengths: torch.Tensor | None, index, group=None):
+    """All-gather (uid key, score, length) of every rank's rows in rank order.
+
+    Returns (scores_all [N] fp32, lengths_all [N] fp32 | None, keys_all np.int64 [N], row_offset
+    of this rank in the global batch). One all-gather of the row counts, one of the payload;
+    the keys come back to the host (one sync) for the CSR grouping."""
+    dev = scores.device
+    B = scores.numel()
+    w, r = _world(group), _rank(group)
+    keys = uid_keys(index)
+    if w == 1:
+        return scores, lengths, keys, 0
+    sizes = [int(s.item()) for s in _all_gather(torch.tensor([B], dtype=torch.int64, device=dev), group)]
+    bmax = max(sizes)
+    payload = torch.zeros(bmax, 4, dtype=torch.int32, device=dev)
+    payload[:B, 0:2] = torch.from_numpy(keys).view(torch.int32).view(B, 2).to(dev, non_blocking=True)
+    payload[:B, 2] = scores.view(torch.int32)
+    if lengths is not None:
+        payload[:B, 3] = lengths.view(torch.int32)
+    parts = _all_gather(payload, group)
+    rows = torch.cat([p[:s] for p, s in zip(parts, sizes, strict=True)])
+    keys_all = rows[:, 0:2].contiguous().view(torch.int64).view(-1).cpu().numpy()
+    scores_all = rows[:, 2].contiguous().view(torch.float32)
+    lens_all = rows[:, 3].contiguous().view(torch.float32) if lengths is not None else None
+    return scores_all, lens_all, keys_all, sum(sizes[:r])
+
+
+def outcome_coef_dp(token_level_rewards, response_mask, index, epsilon: float, estimator: int, group=None,
+                    check_passk: bool = False):
+    """Per-row coefficients a(b) of THIS rank's rows, with the group statistics taken over the
+    whole (all-gathered) batch. Returns (coef_local [B], scores_all [N])."""
+    K._require_device(token_level_rewards, response_mask)
+    if len(index) == 0:
+        raise ValueError("no score in prompt index: <empty batch>")
+    B = token_level_rewards.shape[0]
+    scores, lens = K.row_scores(token_level_rewards, response_mask, lengths=(estimator == L.VA_ADV_OPO))
+    scores_all, lens_all, keys_all, off = gather_row_scores(scores, lens, index, group)
+    order, offsets, G, gmax = K.group_csr(keys_all, scores.device)
+    if check_passk:
+        counts = np.bincount(np.unique(keys_all, return_inverse=True)[1].reshape(-1))
+        if counts.min() < 2:
+            raise ValueError(f"Pass@k requires at least 2 samples per group. Got {int(counts.min())} for group "
+                             f"{int(np.argmin(counts))}.")
+    coef = K.group_coef(scores_all, lens_all, order, offsets, G, gmax, epsilon, estimator)
+    return coef[off : off + B], scores_all
+
+
+def outcome_advantage_dp(token_level_rewards, response_mask, index, epsilon: float, estimator: int, group=None):
+    """adv [B, R] of this rank's rows for a group estimator (GRPO family), batch-global groups."""
+    coef, _ = outcome_coef_dp(token_level_rewards, response_mask, index, epsilon, estimator, group,
+                              check_passk=estimator in (L.VA_ADV_PASSK, L.VA_ADV_PASSK_NOSTD))
+    return K.broadcast_rows(coef, response_mask)
 
 
 def global_whiten_stats(local_merged: torch.Tensor, group=None) -> torch.Tensor:
@@ -31,14 +141,7 @@ def global_whiten_stats(local_merged: torch.Tensor, group=None) -> torch.Tensor:
     w = _world(group)
     dev = local_merged.device
     if w > 1:
-        parts = [torch.empty_like(local_merged) for _ in range(w)]
-        if dist.get_backend(group) == "gloo":  # gloo moves host tensors; keep the protocol identical
-            cpu = [p.cpu() for p in parts]
-            dist.all_gather(cpu, local_merged.cpu(), group=group)
-            parts = [p.to(dev) for p in cpu]
-        else:
-            dist.all_gather(parts, local_merged, group=group)
-        triples = torch.stack(parts).contiguous()
+        triples = torch.stack(_all_gather(local_merged.contiguous(), group)).contiguous()
     else:
         triples = local_merged.view(1, 3).contiguous()
     stats = torch.empty(4, dtype=torch.float32, device=dev)
@@ -79,16 +182,68 @@ def compute_gae_advantage_return_dp(token_level_rewards, values, response_mask, 
 
 
 def check_groups_intact(index, group=None) -> bool:
-    """True when no uid appears on more than one rank (GRPO needs no exchange then)."""
+    """True when no uid appears on more than one rank (diagnostic: the group estimators above are
+    exact either way)."""
     w = _world(group)
     if w == 1:
         return True
-    mine = sorted(set(np.asarray(index).tolist()))
-    allsets: list = [None] * w
-    dist.all_gather_object(allsets, mine, group=group)
-    seen: set = set()
-    for s in allsets:
-        if seen.intersection(s):
-            return False
-        seen.update(s)
-    return True
+    keys = torch.from_numpy(np.unique(uid_keys(index)))
+    n = _all_gather(torch.tensor([keys.numel()]), group)
+    nmax = max(int(x.item()) for x in n)
+    pad = torch.full((nmax,), -1, dtype=torch.int64)
+    pad[: keys.numel()] = keys
+    allk = torch.cat([p[: int(c.item())] for p, c in zip(_all_gather(pad, group), n, strict=True)])
+    return allk.unique().numel() == allk.numel()
+
+
+@torch.no_grad()
+def compute_advantage_dp(data: DataProto, adv_estimator, gamma: float = 1.0, lam: float = 1.0, num_repeat: int = 1,
+                         norm_adv_by_std_in_grpo: bool = True, config=None, group=None) -> DataProto:
+    """ray_trainer.compute_advantage (ray_trainer.py:214-291) on this rank's shard of the batch,
+    with the batch-global statistics exchanged across the ranks of ``group``. With one rank it
+    is ray_trainer.compute_advantage itself."""
+    from . import core_algos
+    from .ray_trainer import compute_advantage, compute_response_mask
+
+    if _world(group) == 1:
+        return compute_advantage(data, adv_estimator, gamma=gamma, lam=lam, num_repeat=num_repeat,
+                                 norm_adv_by_std_in_grpo=norm_adv_by_std_in_grpo, config=config)
+    if "response_mask" not in data.batch.keys():
+        data.batch["response_mask"] = compute_response_mask(data)
+    est = AdvantageEstimator(adv_estimator) if not isinstance(adv_estimator, AdvantageEstimator) else adv_estimator
+    rewards = data.batch["token_level_rewards"]
+    mask = data.batch["response_mask"]
+    index = data.non_tensor_batch.get("uid")
+    if est == AdvantageEstimator.GAE:
+        adv, ret = compute_gae_advantage_return_dp(rewards, data.batch["values"], mask, gamma, lam, group)
+    elif est in (AdvantageEstimator.GRPO, AdvantageEstimator.RLOO, AdvantageEstimator.OPO,
+                 AdvantageEstimator.GRPO_PASSK):
+        if est == AdvantageEstimator.GRPO:
+            code = L.VA_ADV_GRPO if norm_adv_by_std_in_grpo else L.VA_ADV_GRPO_NOSTD
+        elif est == AdvantageEstimator.GRPO_PASSK:
+            norm = config.get("norm_adv_by_std_in_grpo", True) if config is not None else True
+            code = L.VA_ADV_PASSK if norm else L.VA_ADV_PASSK_NOSTD
+        else:
+            code = _GROUP_ESTIMATORS[est]
+        adv = outcome_advantage_dp(rewards, mask, index, 1e-6, code, group)
+        ret = adv
+    elif est == AdvantageEstimator.GPG:
+        coef, scores_all = outcome_coef_dp(rewards, mask, index, 1e-6, L.VA_ADV_MEAN_ONLY, group)
+        alpha = scores_all.shape[0] / torch.count_nonzero(scores_all).clamp(min=1)
+        adv = K.broadcast_rows(alpha * coef / 1.0, mask)
+        ret = adv
+    elif est == AdvantageEstimator.REINFORCE_PLUS_PLUS_BASELINE:
+        coef, _ = outcome_coef_dp(rewards, mask, index, 1e-6, L.VA_ADV_MEAN_ONLY, group)
+        centred = K.broadcast_rows(coef, mask)
+        adv = masked_whiten_dp(centred, mask, group, post_multiply_mask=True)
+        ret = adv
+    elif est == AdvantageEstimator.REINFORCE_PLUS_PLUS:
+        ret = K.discounted_returns(rewards, mask, config.gamma, L.VA_RET_RFPP)
+        adv = masked_whiten_dp(ret, mask, group, post_multiply_mask=True)
+    elif est == AdvantageEstimator.REMAX:  # per-row only: no exchange
+        adv, ret = core_algos.compute_remax_outcome_advantage(rewards, data.batch["reward_baselines"], mask)
+    else:
+        raise ValueError(f"Unknown advantage estimator simply: {est.value}")
+    data.batch["advantages"] = adv
+    data.batch["returns"] = ret
+    return data

@@ -272,9 +272,13 @@ class DataParallelPPOActor(BasePPOActor):
         assert self.config.grad_clip is not None
         if self.grad_reducer is not None:
             self.grad_reducer.finish_sync()
-        params = (self.grad_reducer.optimizer_params() if self.grad_reducer is not None
-                  else list(self.actor_module.parameters()))
-        grad_norm = torch.nn.utils.clip_grad_norm_(params, max_norm=self.config.grad_clip, foreach=True)
+        if self.grad_reducer is not None and hasattr(self.grad_reducer, "clip_grad_norm_"):
+            # sharded optimizer state: global norm over the ranks' shards (fsdp_utils.py:503-516)
+            grad_norm = self.grad_reducer.clip_grad_norm_(self.config.grad_clip)
+        else:
+            params = (self.grad_reducer.optimizer_params() if self.grad_reducer is not None
+                      else list(self.actor_module.parameters()))
+            grad_norm = torch.nn.utils.clip_grad_norm_(params, max_norm=self.config.grad_clip, foreach=True)
         if not torch.isfinite(grad_norm):
             rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
             print(f"WARN: rank {rank} grad_norm is not finite: {grad_norm}")

@@ -18,7 +18,7 @@ import torch.distributed as dist
 
 from ..protocol import DataProto
 from .actor import DataParallelPPOActor
-from .grad_sync import GradBucketReducer, MixedPrecisionParams
+from .grad_sync import GradBucketReducer, MixedPrecisionParams, ShardedMixedPrecisionParams
 
 
 def init_distributed(backend: str | None = None) -> tuple[int, int]:
@@ -56,6 +56,17 @@ def collect_dp_compute_data_proto(outputs: list[DataProto]) -> DataProto:
     return DataProto.concat(outputs)
 
 
+def make_param_manager(module: torch.nn.Module, bucket_mb: int, mixed_precision: bool, zero: bool):
+    """Parameter / gradient / optimizer-state layout of a trained role (see grad_sync.py)."""
+    if zero:
+        if not mixed_precision:
+            raise ValueError("zero=True shards the fp32 masters of the bf16 mixed-precision layout")
+        return ShardedMixedPrecisionParams(module, bucket_bytes=bucket_mb << 20)
+    if mixed_precision:
+        return MixedPrecisionParams(module, bucket_bytes=bucket_mb << 20)
+    return GradBucketReducer(module.parameters(), bucket_bytes=bucket_mb << 20)
+
+
 class ActorWorker:
     """update_actor / compute_log_prob of the actor role, one per GPU."""
 
@@ -79,17 +90,17 @@ class ActorWorker:
         self.actor = None
         self.module = None
 
-    def init_model(self, module: torch.nn.Module, bucket_mb: int = 256, mixed_precision: bool = True):
+    def init_model(self, module: torch.nn.Module, bucket_mb: int = 256, mixed_precision: bool = True,
+                   zero: bool = False):
         """fsdp_workers.py:562-670 (model already built by the caller; AdamW with the actor's optim
         config, fsdp_workers.py:418-423). mixed_precision=True is the FSDP MixedPrecision of the
-        reference (bf16 compute weights, fp32 master weights / grads / reduction, :337-347)."""
+        reference (bf16 compute weights, fp32 master weights / grads / reduction, :337-347).
+        zero=True shards the fp32 masters and AdamW state over the ranks (FSDP FULL_SHARD's
+        optimizer-state saving, :94-99, 371; grad_sync.ShardedMixedPrecisionParams)."""
         self.module = module
         optim = self.config.actor.optim
         fused = next(module.parameters()).is_cuda
-        if mixed_precision:
-            manager = MixedPrecisionParams(module, bucket_bytes=bucket_mb << 20)
-        else:
-            manager = GradBucketReducer(module.parameters(), bucket_bytes=bucket_mb << 20)
+        manager = make_param_manager(module, bucket_mb, mixed_precision, zero)
         opt = torch.optim.AdamW(manager.optimizer_params(), lr=optim.lr,
                                 betas=tuple(optim.get("betas", (0.9, 0.999))),
                                 weight_decay=optim.get("weight_decay", 0.01), fused=fused)
@@ -106,6 +117,18 @@ class ActorWorker:
         lp, ent = self.actor.compute_log_prob(data, calculate_entropy=True)
         return DataProto.from_dict(tensors={"old_log_probs": lp, "entropys": ent},
                                    meta_info={"temperature": data.meta_info["temperature"]})
+
+    def compute_advantage(self, data: DataProto, adv_estimator, gamma: float = 1.0, lam: float = 1.0,
+                          num_repeat: int = 1, norm_adv_by_std_in_grpo: bool = True, config=None) -> DataProto:
+        """The driver's compute_advantage (ray_trainer.py:214-291, called at :1297) run here on
+        this rank's shard, on the GPU: batch-global statistics (GRPO-family group stats, GAE /
+        RF++ whitening) are exchanged over the process group (trainer/ppo/dp_algos.py), so the
+        result equals the reference's whole-batch computation whether or not prompt groups were
+        split over ranks by _balance_batch."""
+        from ..trainer.ppo.dp_algos import compute_advantage_dp
+
+        return compute_advantage_dp(data, adv_estimator, gamma=gamma, lam=lam, num_repeat=num_repeat,
+                                    norm_adv_by_std_in_grpo=norm_adv_by_std_in_grpo, config=config)
 
     def update_actor(self, data: DataProto) -> DataProto:
         """fsdp_workers.py:672-716: one PPO update; metrics in meta_info."""
@@ -139,15 +162,13 @@ class CriticWorker:
             c.forward_micro_batch_size_per_gpu = c.get("ppo_micro_batch_size_per_gpu")
         self.critic = None
 
-    def init_model(self, module: torch.nn.Module, bucket_mb: int = 256, mixed_precision: bool = True):
+    def init_model(self, module: torch.nn.Module, bucket_mb: int = 256, mixed_precision: bool = True,
+                   zero: bool = False):
         from .critic import DataParallelPPOCritic
 
         optim = self.config.optim
         fused = next(module.parameters()).is_cuda
-        if mixed_precision:
-            manager = MixedPrecisionParams(module, bucket_bytes=bucket_mb << 20)
-        else:
-            manager = GradBucketReducer(module.parameters(), bucket_bytes=bucket_mb << 20)
+        manager = make_param_manager(module, bucket_mb, mixed_precision, zero)
         opt = torch.optim.AdamW(manager.optimizer_params(), lr=optim.lr,
                                 betas=tuple(optim.get("betas", (0.9, 0.999))),
                                 weight_decay=optim.get("weight_decay", 0.01), fused=fused)

@@ -9,9 +9,18 @@ Design (MI355X-first):
   * buckets are ordered as backward produces gradients (reverse parameter order), so the
     all-reduce of a full bucket is issued from a post-accumulate-grad hook while backward is
     still computing the earlier layers — communication overlaps compute;
+  * collectives are issued in ONE global order on every rank: bucket i is launched only after
+    buckets 0..i-1 have been (a bucket that fills early waits for its predecessors), so ranks
+    never issue RCCL calls in different orders;
   * only the LAST micro-batch of a mini-batch syncs (grad accumulation is local);
   * bucket size defaults to 256 MiB: xGMI rings are per-link bound, so few large messages;
-  * the result is the mean over ranks (SUM then scale by 1/W), FSDP's reduction.
+  * the result is the mean over ranks (RCCL's native AVG; SUM then 1/W on gloo), FSDP's reduction;
+  * at construction the parameters are broadcast from rank 0 (FSDP's sync_module_states), so
+    replicas start identical whatever each rank's initialisation was.
+
+``ShardedMixedPrecisionParams`` is the ZeRO-2-style variant: each
+rank owns 1/W of every bucket's fp32 master weights and AdamW state, gradients are
+reduce-scattered instead of all-reduced, and the updated bf16 shards are all-gathered back.
 """
 
 from __future__ import annotations
@@ -20,49 +29,180 @@ import torch
 import torch.distributed as dist
 
 
-class _Bucket:
-    __slots__ = ("buf", "params", "pending", "handle")
+def _world_of(group) -> int:
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
-    def __init__(self, buf, params):
+
+def _rank_of(group) -> int:
+    return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+
+
+def _group_params(params, bucket_bytes: int, elem_bytes: int = 4):
+    """Consecutive parameters (in backward order) packed into buckets of <= bucket_bytes."""
+    groups, cur, cur_bytes = [], [], 0
+    for p in params:
+        nb = p.numel() * elem_bytes
+        if cur and (cur_bytes + nb > bucket_bytes or p.device != cur[0].device):
+            groups.append(cur)
+            cur, cur_bytes = [], 0
+        cur.append(p)
+        cur_bytes += nb
+    if cur:
+        groups.append(cur)
+    return groups
+
+
+class _Bucket:
+    __slots__ = ("buf", "params", "pending", "handle", "index", "ready")
+
+    def __init__(self, buf, params, index):
         self.buf = buf
         self.params = params
         self.pending = len(params)
         self.handle = None
+        self.index = index
+        self.ready = False
 
 
-class GradBucketReducer:
-    def __init__(self, params, bucket_bytes: int = 256 << 20, process_group=None):
-        self.group = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
-        self.params = [p for p in params if p.requires_grad]
+class _OrderedBuckets:
+    """Shared machinery: ordered asynchronous bucket collectives + optional timing."""
+
+    group = None
+    world = 1
+    buckets: list
+
+    def _init_order(self):
         self.sync_enabled = False
+        self._next = 0
+        self._timing = None
+        self._use_avg = self.world > 1 and dist.get_backend(self.group) == "nccl"
+
+    def _collective(self, b: _Bucket):
+        """Start bucket b's all-reduce (mean over ranks)."""
+        op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
+        return dist.all_reduce(b.buf, op=op, group=self.group, async_op=True)
+
+    def _finish_bucket(self, b: _Bucket):
+        b.handle.wait()
+        if not self._use_avg:
+            b.buf.mul_(1.0 / self.world)
+
+    def _mark_ready(self, b: _Bucket):
+        """Bucket b is complete for this pass; launch every consecutive ready bucket in order."""
+        b.ready = True
+        while self._next < len(self.buckets) and self.buckets[self._next].ready:
+            nb = self.buckets[self._next]
+            nb.handle = self._collective(nb)
+            self._next += 1
+
+    def _reset_sync(self):
+        self._next = 0
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.handle = None
+            b.ready = False
+
+    def _finish_all(self):
+        """Launch whatever has not been launched (in order), wait, average."""
+        for b in self.buckets:
+            b.ready = True
+        if self.buckets:
+            self._mark_ready(self.buckets[-1])
+        ev0 = None
+        if self._timing is not None:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        for b in self.buckets:
+            self._finish_bucket(b)
+            b.handle = None
+        if ev0 is not None:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            self._timing.append((ev0, ev1))
+        self.sync_enabled = False
+
+    # ------------------------------------------------------------------ measurement (bench.py)
+    def start_timing(self):
+        """Record, per optimizer step, the compute-stream time spent waiting for the gradient
+        collectives after backward (the exposed, non-overlapped part)."""
+        self._timing = []
+        return self._timing
+
+    def stop_timing(self) -> float:
+        """Total exposed collective milliseconds since start_timing (synchronises)."""
+        torch.cuda.synchronize()
+        total = sum(a.elapsed_time(b) for a, b in (self._timing or []))
+        self._timing = None
+        return total
+
+    def grad_bytes(self) -> int:
+        return int(sum(b.buf.numel() * b.buf.element_size() for b in self.buckets))
+
+    def time_isolated_sync(self, reps: int = 3) -> float:
+        """Milliseconds of one step's gradient collectives run alone (no overlap), median of reps."""
+        if self.world <= 1:
+            return 0.0
+        times = []
+        for _ in range(reps + 1):
+            scratch = [torch.zeros_like(b.buf) for b in self.buckets]
+            dist.barrier(group=self.group)
+            torch.cuda.synchronize()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            hs = [self._raw_collective(s) for s in scratch]
+            for h in hs:
+                h.wait()
+            e1.record()
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1))
+            del scratch
+        return sorted(times[1:])[len(times[1:]) // 2]
+
+    def _raw_collective(self, buf):
+        op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
+        return dist.all_reduce(buf, op=op, group=self.group, async_op=True)
+
+
+@torch.no_grad()
+def _broadcast_from_rank0(tensors, group=None):
+    """FSDP sync_module_states: every rank starts from rank 0's values."""
+    if _world_of(group) <= 1:
+        return
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    for t in tensors:
+        if dist.get_backend(group) == "gloo" and t.is_cuda:
+            c = t.detach().cpu()
+            dist.broadcast(c, src=src, group=group)
+            t.copy_(c)
+        else:
+            dist.broadcast(t, src=src, group=group)
+
+
+class GradBucketReducer(_OrderedBuckets):
+    def __init__(self, params, bucket_bytes: int = 256 << 20, process_group=None, sync_params: bool = True):
+        self.group = process_group
+        self.world = _world_of(process_group)
+        self.params = [p for p in params if p.requires_grad]
         self._hooks = []
         self.buckets: list[_Bucket] = []
+        if sync_params:
+            _broadcast_from_rank0([p.data for p in self.params], process_group)
         # reverse order ~ the order in which backward finishes each parameter's gradient
-        ordered = list(reversed(self.params))
-        cur, cur_bytes = [], 0
-        groups = []
-        for p in ordered:
-            nb = p.numel() * 4
-            if cur and (cur_bytes + nb > bucket_bytes or p.device != cur[0].device):
-                groups.append(cur)
-                cur, cur_bytes = [], 0
-            cur.append(p)
-            cur_bytes += nb
-        if cur:
-            groups.append(cur)
+        groups = _group_params(list(reversed(self.params)), bucket_bytes)
         self._bucket_of = {}
-        for g in groups:
+        for i, g in enumerate(groups):
             n = sum(p.numel() for p in g)
             buf = torch.zeros(n, dtype=torch.float32, device=g[0].device)
             off = 0
             for p in g:
                 p.grad = buf[off : off + p.numel()].view_as(p)
                 off += p.numel()
-            b = _Bucket(buf, g)
+            b = _Bucket(buf, g, i)
             self.buckets.append(b)
             for p in g:
                 self._bucket_of[id(p)] = b
+        self._init_order()
         if self.world > 1:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
@@ -74,7 +214,7 @@ class GradBucketReducer:
         b = self._bucket_of[id(p)]
         b.pending -= 1
         if b.pending == 0:
-            b.handle = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self._mark_ready(b)
 
     # ------------------------------------------------------------------ API
     def zero_grad(self):
@@ -87,23 +227,14 @@ class GradBucketReducer:
     def begin_sync(self):
         """Call before the backward of the last micro-batch of a mini-batch."""
         self.sync_enabled = self.world > 1
-        for b in self.buckets:
-            b.pending = len(b.params)
-            b.handle = None
+        self._reset_sync()
 
     def finish_sync(self):
         """Wait for the bucket all-reduces and average; call after that backward."""
         if self.world <= 1:
             self.sync_enabled = False
             return
-        for b in self.buckets:
-            if b.handle is None:  # a parameter received no gradient in this backward
-                b.handle = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        for b in self.buckets:
-            b.handle.wait()
-            b.buf.mul_(1.0 / self.world)
-            b.handle = None
-        self.sync_enabled = False
+        self._finish_all()
 
     def optimizer_params(self):
         return self.params
@@ -120,7 +251,7 @@ class GradBucketReducer:
         self._hooks.clear()
 
 
-class MixedPrecisionParams:
+class MixedPrecisionParams(_OrderedBuckets):
     """bf16 compute weights + fp32 master weights + fp32 gradient buckets.
 
     The MI355X equivalent of the reference's FSDP MixedPrecision(param_dtype=bf16,
@@ -132,35 +263,24 @@ class MixedPrecisionParams:
         AdamW) and grad-norm clipping act on the masters;
       * after each parameter's bf16 gradient is produced, a post-accumulate-grad hook adds it
         into the fp32 bucket (accumulation over micro-batches in fp32) and frees it; on the last
-        micro-batch the hook launches the bucket's RCCL all-reduce as soon as the bucket is full,
-        overlapping communication with the rest of the backward;
+        micro-batch the bucket's RCCL all-reduce is launched as soon as it and every bucket
+        before it are full, overlapping communication with the rest of the backward;
       * after the optimizer step the masters are copied back to the bf16 weights (foreach copy).
     """
 
     def __init__(self, module: torch.nn.Module, bucket_bytes: int = 256 << 20, process_group=None,
-                 compute_dtype=torch.bfloat16):
+                 compute_dtype=torch.bfloat16, sync_params: bool = True):
         self.group = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.world = _world_of(process_group)
         self.compute_dtype = compute_dtype
         self.params = [p for p in module.parameters() if p.requires_grad]
-        self.sync_enabled = False
-        ordered = list(reversed(self.params))
-        groups, cur, cur_bytes = [], [], 0
-        for p in ordered:
-            nb = p.numel() * 4
-            if cur and cur_bytes + nb > bucket_bytes:
-                groups.append(cur)
-                cur, cur_bytes = [], 0
-            cur.append(p)
-            cur_bytes += nb
-        if cur:
-            groups.append(cur)
+        groups = _group_params(list(reversed(self.params)), bucket_bytes)
         self.buckets: list[_Bucket] = []
-        self.masters: list[torch.nn.Parameter] = []
+        self.master_bufs: list[torch.Tensor] = []
         self._master_of = {}
         self._gview = {}
         self._bucket_of = {}
-        for g in groups:
+        for i, g in enumerate(groups):
             n = sum(p.numel() for p in g)
             dev = g[0].device
             mbuf = torch.empty(n, dtype=torch.float32, device=dev)
@@ -175,15 +295,19 @@ class MixedPrecisionParams:
                 self._master_of[id(p)] = master
                 self._gview[id(p)] = master.grad
                 off += k
-            b = _Bucket(gbuf, g)
+            self.master_bufs.append(mbuf)
+            b = _Bucket(gbuf, g, i)
             self.buckets.append(b)
             for p in g:
                 self._bucket_of[id(p)] = b
+        if sync_params:
+            _broadcast_from_rank0(self.master_bufs, process_group)
         # masters in module order (optimizer state order == parameter order)
         self.masters = [self._master_of[id(p)] for p in self.params]
         for p in self.params:
-            p.data = p.data.to(compute_dtype)
+            p.data = self._master_of[id(p)].data.to(compute_dtype)
         self._ready: dict = {}
+        self._init_order()
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
 
     def _on_grad(self, p):
@@ -192,9 +316,9 @@ class MixedPrecisionParams:
         if len(self._ready[id(b)]) == len(b.params):
             self._flush(b)
 
-    def _flush(self, b):
+    def _flush(self, b, complete: bool = True):
         """Accumulate the bucket's ready bf16 gradients into its fp32 buffer (one multi-tensor
-        launch) and, on a syncing micro-batch, start the bucket's all-reduce."""
+        launch) and, on a syncing micro-batch, mark it ready for its (ordered) collective."""
         ready = self._ready.pop(id(b), [])
         if ready:
             if ready[0].is_cuda:
@@ -206,14 +330,14 @@ class MixedPrecisionParams:
                     self._gview[id(q)].add_(q.grad)
             for q in ready:
                 q.grad = None
-        if self.sync_enabled and b.handle is None and not self._ready.get(id(b)):
-            b.handle = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        if complete and self.sync_enabled and not b.ready:
+            self._mark_ready(b)
 
     def after_backward(self):
         """Flush buckets that did not complete (parameters without a gradient this pass)."""
         for b in self.buckets:
             if self._ready.get(id(b)):
-                self._flush(b)
+                self._flush(b, complete=False)
 
     # same interface as GradBucketReducer
     def zero_grad(self):
@@ -225,23 +349,14 @@ class MixedPrecisionParams:
 
     def begin_sync(self):
         self.sync_enabled = self.world > 1
-        for b in self.buckets:
-            b.pending = len(b.params)
-            b.handle = None
+        self._reset_sync()
 
     def finish_sync(self):
         self.after_backward()
         if self.world <= 1:
             self.sync_enabled = False
             return
-        for b in self.buckets:
-            if b.handle is None:
-                b.handle = dist.all_reduce(b.buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        for b in self.buckets:
-            b.handle.wait()
-            b.buf.mul_(1.0 / self.world)
-            b.handle = None
-        self.sync_enabled = False
+        self._finish_all()
 
     def optimizer_params(self):
         return self.masters
@@ -250,6 +365,204 @@ class MixedPrecisionParams:
     def after_step(self):
         """Refresh the bf16 compute weights from the fp32 masters."""
         torch._foreach_copy_([p.data for p in self.params], [m.data for m in self.masters])
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks.clear()
+
+
+def _reduce_scatter_avg(out: torch.Tensor, buf: torch.Tensor, group, use_avg: bool, async_op: bool = True):
+    """out = mean over ranks of buf's shard r (buf.numel() == W * out.numel())."""
+    if use_avg:
+        return dist.reduce_scatter_tensor(out, buf, op=dist.ReduceOp.AVG, group=group, async_op=async_op)
+    return _GlooReduceScatter(out, buf, group)
+
+
+class _GlooReduceScatter:
+    """gloo has no reduce-scatter: all-reduce the bucket and keep this rank's shard (tests only)."""
+
+    def __init__(self, out, buf, group):
+        self.out, self.buf, self.group = out, buf, group
+        self.world = _world_of(group)
+        self.rank = _rank_of(group)
+
+    def wait(self):
+        host = self.buf.detach().cpu() if self.buf.is_cuda else self.buf
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
+        n = self.out.numel()
+        self.out.copy_(host[self.rank * n : (self.rank + 1) * n].to(self.out.device))
+        self.out.mul_(1.0 / self.world)
+
+
+class ShardedMixedPrecisionParams(_OrderedBuckets):
+    """ZeRO-style data parallelism for the configs whose replicated optimizer state does not fit
+    (Llama-3-8B actor + critic, Qwen2.5-7B DAPO; the reference shards with FSDP FULL_SHARD,
+    fsdp_workers.py:94-99, 337-347, 371).
+
+    Per rank, for P parameters over W ranks:
+      * bf16 compute weights, full (2 P bytes): every parameter is a view into one flat bf16
+        buffer per bucket, so the post-step all-gather writes straight into the weights;
+      * fp32 gradient buckets, full (4 P bytes): bf16 micro-batch gradients accumulate into them
+        (as MixedPrecisionParams) and, on the last micro-batch, each bucket is REDUCE-SCATTERED
+        (RCCL AVG) in the fixed bucket order while backward continues;
+      * fp32 master weights + AdamW moments for this rank's 1/W of every bucket (12 P / W bytes),
+        as one flat parameter per bucket, so the fused AdamW runs over a few large tensors;
+      * after the step each rank rounds its master shard to bf16 and the shards are
+        all-gathered into the flat weight buffers.
+    Gradient clipping uses the global norm (one fp32 all-reduce of the local sum of squares,
+    fsdp2_clip_grad_norm_ fsdp_utils.py:503-516). AdamW is elementwise, so the updated weights
+    equal those of replicated data parallelism."""
+
+    def __init__(self, module: torch.nn.Module, bucket_bytes: int = 256 << 20, process_group=None,
+                 compute_dtype=torch.bfloat16, sync_params: bool = True):
+        self.group = process_group
+        self.world = _world_of(process_group)
+        self.rank = _rank_of(process_group)
+        self.compute_dtype = compute_dtype
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        groups = _group_params(list(reversed(self.params)), bucket_bytes)
+        W = self.world
+        self.buckets: list[_Bucket] = []
+        self.flat_weights: list[torch.Tensor] = []
+        self.shards: list[torch.nn.Parameter] = []
+        self._gview = {}
+        self._bucket_of = {}
+        self._layout = []
+        for i, g in enumerate(groups):
+            n = sum(p.numel() for p in g)
+            npad = -(-n // (W * 64)) * (W * 64)  # shards of whole 256-byte lines
+            dev = g[0].device
+            full = torch.zeros(npad, dtype=torch.float32, device=dev)
+            off = 0
+            for p in g:
+                full[off : off + p.numel()].copy_(p.detach().reshape(-1).float())
+                off += p.numel()
+            if sync_params:
+                _broadcast_from_rank0([full], process_group)
+            gbuf = torch.zeros(npad, dtype=torch.float32, device=dev)
+            wbuf = full.to(compute_dtype)
+            off = 0
+            for p in g:
+                k = p.numel()
+                self._gview[id(p)] = gbuf[off : off + k].view_as(p)
+                p.data = wbuf[off : off + k].view_as(p)
+                off += k
+            per = npad // W
+            shard = torch.nn.Parameter(full[self.rank * per : (self.rank + 1) * per].clone(), requires_grad=True)
+            shard.grad = torch.zeros(per, dtype=torch.float32, device=dev)
+            del full
+            self.flat_weights.append(wbuf)
+            self.shards.append(shard)
+            b = _Bucket(gbuf, g, i)
+            self.buckets.append(b)
+            for p in g:
+                self._bucket_of[id(p)] = b
+        self._ready: dict = {}
+        self._init_order()
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    # ------------------------------------------------------------------ collectives
+    def _collective(self, b: _Bucket):
+        return _reduce_scatter_avg(self.shards[b.index].grad, b.buf, self.group, self._use_avg)
+
+    def _finish_bucket(self, b: _Bucket):
+        b.handle.wait()
+
+    def _raw_collective(self, buf):
+        out = torch.empty(buf.numel() // self.world, dtype=buf.dtype, device=buf.device)
+        return _reduce_scatter_avg(out, buf, self.group, self._use_avg)
+
+    # ------------------------------------------------------------------ hooks (as MixedPrecisionParams)
+    def _on_grad(self, p):
+        b = self._bucket_of[id(p)]
+        self._ready.setdefault(id(b), []).append(p)
+        if len(self._ready[id(b)]) == len(b.params):
+            self._flush(b)
+
+    def _flush(self, b, complete: bool = True):
+        ready = self._ready.pop(id(b), [])
+        if ready:
+            if ready[0].is_cuda:
+                from .. import kernels as K
+
+                K.accumulate_grads([q.grad for q in ready], [self._gview[id(q)] for q in ready])
+            else:
+                for q in ready:
+                    self._gview[id(q)].add_(q.grad)
+            for q in ready:
+                q.grad = None
+        if complete and self.sync_enabled and not b.ready:
+            self._mark_ready(b)
+
+    def after_backward(self):
+        for b in self.buckets:
+            if self._ready.get(id(b)):
+                self._flush(b, complete=False)
+
+    def zero_grad(self):
+        for b in self.buckets:
+            b.buf.zero_()
+        for s in self.shards:
+            s.grad.zero_()
+        for p in self.params:
+            p.grad = None
+        self._ready = {}
+
+    def begin_sync(self):
+        self.sync_enabled = self.world > 1
+        self._reset_sync()
+
+    def finish_sync(self):
+        self.after_backward()
+        if self.world <= 1:  # one rank: the shard is the whole bucket
+            for b in self.buckets:
+                self.shards[b.index].grad.copy_(b.buf)
+            self.sync_enabled = False
+            return
+        self._finish_all()
+
+    def optimizer_params(self):
+        return self.shards
+
+    @torch.no_grad()
+    def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
+        """Global-norm clipping over the sharded gradients (torch.nn.utils.clip_grad_norm_
+        semantics: coef = max_norm / (norm + 1e-6), clamped to 1; the norm is returned)."""
+        grads = [s.grad for s in self.shards]
+        local = torch.stack(torch._foreach_norm(grads)).square().sum()
+        if self.world > 1:
+            if dist.get_backend(self.group) == "gloo" and local.is_cuda:
+                h = local.cpu()
+                dist.all_reduce(h, group=self.group)
+                local = h.to(local.device)
+            else:
+                dist.all_reduce(local, group=self.group)
+        norm = local.sqrt()
+        coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+        torch._foreach_mul_(grads, coef)
+        return norm
+
+    @torch.no_grad()
+    def after_step(self):
+        """Round the master shards to bf16 and all-gather them into the flat weight buffers."""
+        for s, wbuf in zip(self.shards, self.flat_weights, strict=True):
+            mine = s.detach().to(self.compute_dtype)
+            if self.world == 1:
+                wbuf.copy_(mine)
+            elif dist.get_backend(self.group) == "gloo":
+                parts = [torch.empty_like(mine, device="cpu") for _ in range(self.world)]
+                dist.all_gather(parts, mine.cpu(), group=self.group)
+                wbuf.copy_(torch.cat(parts).to(wbuf.device))
+            else:
+                dist.all_gather_into_tensor(wbuf, mine, group=self.group)
+
+    def memory_bytes(self) -> dict:
+        """Per-rank bytes of the parameter / gradient / optimizer state this manager holds."""
+        w = sum(t.numel() * t.element_size() for t in self.flat_weights)
+        g = sum(b.buf.numel() * 4 for b in self.buckets)
+        m = sum(s.numel() * 4 for s in self.shards)
+        return {"bf16_weights": w, "fp32_grads": g, "fp32_master_shard": m, "adamw_moments_shard": 2 * m}
 
     def remove(self):
         for h in self._hooks:
