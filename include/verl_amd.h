@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define VA_ABI_VERSION 1
+#define VA_ABI_VERSION 2
 
 /* error codes */
 #define VA_OK 0
@@ -70,6 +70,12 @@ extern "C" {
 /* discounted-return modes of va_discounted_returns */
 #define VA_RET_RFPP 0      /* REINFORCE++ return with reset after EOS core_algos.py:553-560 */
 #define VA_RET_REMAX 1     /* reverse cumsum of r*m, adv = ret - b*m  core_algos.py:597-600 */
+
+/* policy-loss modes of va_ppo_loss_fwd/bwd (register_policy_loss, dispatch dp_actor.py:419-443) */
+#define VA_PL_VANILLA 0  /* dual-clip PPO                          core_algos.py:722-794 */
+#define VA_PL_GPG 1      /* -lp * A                                core_algos.py:797-815 */
+#define VA_PL_CLIP_COV 2 /* max(l1, l2) * (1 - sel), unclamped     core_algos.py:818-905 */
+#define VA_PL_KL_COV 3   /* l1 + sel * coef * |lp - old|, unclamped core_algos.py:908-972 */
 
 /* scalar slots of the fused policy-loss output vector out[VA_LOSS_NOUT] */
 #define VA_LOSS_PG 0            /* pg_loss                 core_algos.py:791-792 */
@@ -152,15 +158,21 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------
- * Fused vanilla PPO clipped policy loss + optional KL-loss + optional entropy term, with
- * loss aggregation and the three metrics, over one [B, R] micro-batch.
- * Replaces: core_algos.py:722-794 (compute_policy_loss), :686-719 (agg_loss),
- * :1034-1069 (kl_penalty) as called at dp_actor.py:421-461.
+ * Fused PPO policy loss (vanilla dual-clip or a registered variant) + optional KL-loss +
+ * optional entropy term, with loss aggregation and the three metrics, over one [B, R]
+ * micro-batch.
+ * Replaces: core_algos.py:722-794 (compute_policy_loss), :797-972 (gpg / clip_cov / kl_cov),
+ * :686-719 (agg_loss), :1034-1069 (kl_penalty) as called at dp_actor.py:419-461.
  *   old_lp, lp, adv [B,R] fp32; mask [B,R] of `mask_dtype`;
  *   ref_lp [B,R] fp32 or NULL (kl_type must then be VA_KL_NONE);
  *   entropy [B,R] fp32 or NULL.
  *   clip_lo = 1 - clip_ratio_low, clip_hi = 1 + clip_ratio_high (rounded to fp32 on host, as
  *   torch.clamp casts its scalar bounds), clip_c = clip_ratio_c (> 1, asserted on host).
+ *   loss_mode = VA_PL_*; sel [B,R] uint8 = the variant's token selection (clip_cov: tokens whose
+ *   loss is zeroed; kl_cov: tokens that get + mode_coef * |lp - old|), chosen on the host side
+ *   with the reference's top-k / random draw; NULL for vanilla and gpg. Metric slots per mode:
+ *   vanilla as the reference; gpg: 0, 0, 0; clip_cov: masked_mean(sel), masked_mean(old - lp), 0;
+ *   kl_cov: 0, masked_mean(|lp - old|) (ppo_kl_abs), 0.
  *   out[VA_LOSS_NOUT] fp32 (device). workspace: va_ppo_loss_workspace_bytes(B).
  * The workspace holds per-row partial sums that the backward reads: keep it alive between
  * the forward and the backward of the same micro-batch. */
@@ -168,16 +180,18 @@ int64_t va_ppo_loss_workspace_bytes(int64_t B);
 int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float *adv, const void *mask,
                     int mask_dtype, const float *ref_lp, const float *entropy, int64_t B,
                     int64_t R, float clip_lo, float clip_hi, float clip_c, int agg_mode,
-                    int kl_type, float *out, void *workspace, void *stream);
+                    int kl_type, int loss_mode, const uint8_t *sel, float mode_coef, float *out,
+                    void *workspace, void *stream);
 
 /* Backward: g_out[VA_LOSS_NOUT] is d(loss)/d(out) as a device vector (only slots PG, KL,
  * ENTROPY are read; may be NULL = zeros). Writes d_lp [B,R] and, if non-NULL, d_entropy.
  * Tie and boundary gradients follow torch autograd of the reference expression:
- * maximum/minimum split ties 1/2-1/2, clamp passes inclusive of its bounds. */
+ * maximum/minimum split ties 1/2-1/2, clamp passes inclusive of its bounds, abs' gradient at 0 is 0. */
 int va_ppo_loss_bwd(const float *g_out, const float *old_lp, const float *lp, const float *adv,
                     const void *mask, int mask_dtype, const float *ref_lp, int64_t B, int64_t R,
                     float clip_lo, float clip_hi, float clip_c, int agg_mode, int kl_type,
-                    const void *workspace, float *d_lp, float *d_entropy, void *stream);
+                    int loss_mode, const uint8_t *sel, float mode_coef, const void *workspace,
+                    float *d_lp, float *d_entropy, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Elementwise KL estimators (core_algos.py:1034-1069), n elements.

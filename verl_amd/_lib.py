@@ -25,6 +25,7 @@ VA_KL_NONE, VA_KL_K1, VA_KL_ABS, VA_KL_K2, VA_KL_K3 = -1, 0, 1, 2, 3
 VA_ADV_GRPO, VA_ADV_GRPO_NOSTD, VA_ADV_RLOO, VA_ADV_MEAN_ONLY = 0, 1, 2, 3
 VA_ADV_OPO, VA_ADV_PASSK, VA_ADV_PASSK_NOSTD = 4, 5, 6
 VA_RET_RFPP, VA_RET_REMAX = 0, 1
+VA_PL_VANILLA, VA_PL_GPG, VA_PL_CLIP_COV, VA_PL_KL_COV = 0, 1, 2, 3
 VA_LOSS_PG, VA_LOSS_CLIPFRAC, VA_LOSS_PPO_KL, VA_LOSS_CLIPFRAC_LOWER = 0, 1, 2, 3
 VA_LOSS_KL, VA_LOSS_ENTROPY, VA_LOSS_NTOKENS, VA_LOSS_NROWS, VA_LOSS_NOUT = 4, 5, 6, 7, 8
 VA_VLOSS_LOSS, VA_VLOSS_CLIPFRAC, VA_VLOSS_VPRED_MEAN, VA_VLOSS_NTOKENS, VA_VLOSS_NOUT = 0, 1, 2, 3, 4
@@ -46,11 +47,13 @@ _SIGNATURES: dict[str, tuple] = {
     "va_ppo_loss_workspace_bytes": (c_int64, [c_int64]),
     "va_ppo_loss_fwd": (
         c_int,
-        [_P, _P, _P, _P, c_int, _P, _P, c_int64, c_int64, c_float, c_float, c_float, c_int, c_int, _P, _P, _P],
+        [_P, _P, _P, _P, c_int, _P, _P, c_int64, c_int64, c_float, c_float, c_float, c_int, c_int, c_int, _P,
+         c_float, _P, _P, _P],
     ),
     "va_ppo_loss_bwd": (
         c_int,
-        [_P, _P, _P, _P, _P, c_int, _P, c_int64, c_int64, c_float, c_float, c_float, c_int, c_int, _P, _P, _P, _P],
+        [_P, _P, _P, _P, _P, c_int, _P, c_int64, c_int64, c_float, c_float, c_float, c_int, c_int, c_int, _P,
+         c_float, _P, _P, _P, _P],
     ),
     "va_kl_penalty_fwd": (c_int, [_P, _P, c_int64, c_int, _P, _P]),
     "va_kl_penalty_bwd": (c_int, [_P, _P, _P, c_int64, c_int, _P, _P, _P]),
@@ -131,8 +134,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.va_abi_version() != 1:
-        raise NativeLibraryError(f"ABI version mismatch: {lib.va_abi_version()} != 1")
+    if lib.va_abi_version() != 2:
+        raise NativeLibraryError(f"ABI version mismatch: {lib.va_abi_version()} != 2")
     _lib = lib
     return lib
 

@@ -89,13 +89,41 @@ struct PolicyElem {
   float pg, clip, negkl, lower;
 };
 
-// compute_policy_loss elementwise part, core_algos.py:766-791 (same op order)
+// compute_policy_loss elementwise part, core_algos.py:766-791 (same op order), and the registered
+// variants (dispatch dp_actor.py:419-443): gpg core_algos.py:797-815, clip_cov :818-905 (sel = the
+// randomly chosen high-covariance tokens whose loss is zeroed, corr = 0), kl_cov :908-972 (sel =
+// the top-k covariance tokens that get + coef * |lp - old|). The variants do not clamp lp - old.
 __device__ __forceinline__ PolicyElem policy_elem(float old, float lp, float A, float lo,
-                                                  float hi, float c) {
+                                                  float hi, float c, int mode, bool sel,
+                                                  float coef) {
   PolicyElem e;
+  const float nA = -A;
+  if (mode == VA_PL_GPG) {
+    e.pg = (-lp) * A;
+    e.clip = 0.f;
+    e.negkl = 0.f;
+    e.lower = 0.f;
+    return e;
+  }
+  if (mode == VA_PL_CLIP_COV || mode == VA_PL_KL_COV) {
+    const float d = lp - old;
+    const float r = expf(d);
+    const float l1 = nA * r;
+    if (mode == VA_PL_CLIP_COV) {
+      const float l2 = nA * tclamp(r, lo, hi);
+      e.pg = tmax(l1, l2) * (sel ? 0.f : 1.f);
+      e.clip = sel ? 1.f : 0.f;  // masked_mean((corr == 0).float())
+      e.negkl = -d;              // ppo_kl = masked_mean(-negative_approx_kl)
+    } else {
+      e.pg = sel ? l1 + coef * fabsf(d) : l1;
+      e.clip = 0.f;
+      e.negkl = fabsf(d);  // the kl_cov metric slot is ppo_kl_abs = masked_mean(|lp - old|)
+    }
+    e.lower = 0.f;
+    return e;
+  }
   const float dc = tclamp(lp - old, -20.f, 20.f);
   const float r = expf(dc);
-  const float nA = -A;
   const float l1 = nA * r;
   const float l2 = nA * tclamp(r, lo, hi);
   const float c1 = tmax(l1, l2);
@@ -110,11 +138,32 @@ __device__ __forceinline__ PolicyElem policy_elem(float old, float lp, float A, 
 
 // d pg / d lp for a given upstream gradient w on pg (autograd chain order of the reference)
 __device__ __forceinline__ float policy_dlp(float w, float old, float lp, float A, float lo,
-                                           float hi, float c) {
+                                           float hi, float c, int mode, bool sel, float coef) {
+  const float nA = -A;
+  if (mode == VA_PL_GPG) return -(w * A);  // neg(lp) * A
+  if (mode == VA_PL_CLIP_COV) {
+    const float d = lp - old;
+    const float r = expf(d);
+    const float l1 = nA * r;
+    const float l2 = nA * tclamp(r, lo, hi);
+    const float g_c1 = w * (sel ? 0.f : 1.f);  // maximum(l1, l2) * corr
+    const float s1 = gmax_share(l1, l2), s2 = gmax_share(l2, l1);
+    const float g_l1 = s1 == 0.5f ? g_c1 / 2.f : g_c1 * s1;
+    const float g_l2 = s2 == 0.5f ? g_c1 / 2.f : g_c1 * s2;
+    const float g_r = g_l1 * nA + (g_l2 * nA) * pass_incl(r, lo, hi);
+    return g_r * r;
+  }
+  if (mode == VA_PL_KL_COV) {
+    const float d = lp - old;
+    const float r = expf(d);
+    const float g_r = w * nA;
+    if (!sel) return g_r * r;
+    const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);  // abs backward
+    return g_r * r + (w * coef) * sg;
+  }
   const float d = lp - old;
   const float dc = tclamp(d, -20.f, 20.f);
   const float r = expf(dc);
-  const float nA = -A;
   const float l1 = nA * r;
   const float l2 = nA * tclamp(r, lo, hi);
   const float c1 = tmax(l1, l2);
@@ -172,7 +221,8 @@ template <int MT, int KL>
 __global__ __launch_bounds__(256) void ppo_loss_rows_kernel(
     const float *__restrict__ old_lp, const float *__restrict__ lp, const float *__restrict__ adv,
     const void *__restrict__ mask, const float *__restrict__ ref, const float *__restrict__ ent,
-    int64_t R, float lo, float hi, float c, int agg, double *__restrict__ part) {
+    const uint8_t *__restrict__ sel, int64_t R, float lo, float hi, float c, int agg, int mode,
+    float coef, double *__restrict__ part) {
   __shared__ double scratch[4 * 7];
   const int64_t b = blockIdx.x;
   const int64_t base = b * R;
@@ -182,7 +232,8 @@ __global__ __launch_bounds__(256) void ppo_loss_rows_kernel(
     const int64_t i = base + t;
     const float m = load_mask<MT>(mask, i);
     const bool mb = (m != 0.f);
-    const PolicyElem e = policy_elem(old_lp[i], lp[i], adv[i], lo, hi, c);
+    const PolicyElem e =
+        policy_elem(old_lp[i], lp[i], adv[i], lo, hi, c, mode, sel != nullptr && sel[i] != 0, coef);
     v[0] += m;
     // masked_sum: where(mask.bool(), x, 0) * mask ; seq modes: x * mask
     v[1] += tok ? (mb ? e.pg : 0.f) * m : e.pg * m;
@@ -239,8 +290,9 @@ template <int MT, int KL>
 __global__ __launch_bounds__(256) void ppo_loss_bwd_kernel(
     const float *__restrict__ g_out, const float *__restrict__ old_lp,
     const float *__restrict__ lp, const float *__restrict__ adv, const void *__restrict__ mask,
-    const float *__restrict__ ref, int64_t B, int64_t R, float lo, float hi, float c, int agg,
-    const double *__restrict__ part, float *__restrict__ d_lp, float *__restrict__ d_ent) {
+    const float *__restrict__ ref, const uint8_t *__restrict__ sel, int64_t B, int64_t R, float lo,
+    float hi, float c, int agg, int mode, float coef, const double *__restrict__ part,
+    float *__restrict__ d_lp, float *__restrict__ d_ent) {
   const int64_t b = blockIdx.y;
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= R) return;
@@ -257,7 +309,7 @@ __global__ __launch_bounds__(256) void ppo_loss_bwd_kernel(
   const float keep = (!tok || mb) ? 1.f : 0.f;
   const float w_pg = agg_weight(agg, g_pg, m, n_b, n_tot, B, R) * keep;
   const float x_lp = lp[i];
-  float g = policy_dlp(w_pg, old_lp[i], x_lp, adv[i], lo, hi, c);
+  float g = policy_dlp(w_pg, old_lp[i], x_lp, adv[i], lo, hi, c, mode, sel != nullptr && sel[i] != 0, coef);
   if constexpr (KL != VA_KL_NONE) {
     const float w_kl = agg_weight(agg, g_kl, m, n_b, n_tot, B, R) * keep;
     g += w_kl * kl_dlp<KL>(x_lp, ref[i]);
@@ -521,10 +573,18 @@ static int check_agg(int agg, bool allow_reduce) {
   return VA_OK;
 }
 
+static int check_mode(int mode, const uint8_t *sel) {
+  VA_CHECK_ARG(mode >= VA_PL_VANILLA && mode <= VA_PL_KL_COV, "unknown policy loss mode %d", mode);
+  VA_CHECK_ARG(sel != nullptr || (mode != VA_PL_CLIP_COV && mode != VA_PL_KL_COV),
+               "policy loss mode %d needs the token selection", mode);
+  return VA_OK;
+}
+
 extern "C" int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float *adv,
                                const void *mask, int mask_dtype, const float *ref_lp,
                                const float *entropy, int64_t B, int64_t R, float clip_lo,
                                float clip_hi, float clip_c, int agg_mode, int kl_type,
+                               int loss_mode, const uint8_t *sel, float mode_coef,
                                float *out, void *workspace, void *stream) {
   VA_CHECK_ARG(B > 0 && R > 0, "empty batch (B=%lld, R=%lld)", (long long)B, (long long)R);
   VA_CHECK_ARG(B < (1ll << 31), "B too large");
@@ -532,11 +592,13 @@ extern "C" int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float
   VA_CHECK_ARG(kl_type == VA_KL_NONE || ref_lp != nullptr, "ref_lp required for kl_type %d",
                kl_type);
   if (int e = check_agg(agg_mode, false)) return e;
+  if (int e = check_mode(loss_mode, sel)) return e;
   hipStream_t s = static_cast<hipStream_t>(stream);
   double *part = static_cast<double *>(workspace);
   VA_DISPATCH_MASK(mask_dtype, VA_DISPATCH_KL(kl_type, {
     hipLaunchKernelGGL((ppo_loss_rows_kernel<MT, KL>), dim3(B), dim3(256), 0, s, old_lp, lp,
-                       adv, mask, ref_lp, entropy, R, clip_lo, clip_hi, clip_c, agg_mode, part);
+                       adv, mask, ref_lp, entropy, sel, R, clip_lo, clip_hi, clip_c, agg_mode,
+                       loss_mode, mode_coef, part);
   }));
   hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, B, R, agg_mode,
                      kl_type != VA_KL_NONE ? 1 : 0, entropy != nullptr ? 1 : 0, part + B * kNQ,
@@ -548,6 +610,7 @@ extern "C" int va_ppo_loss_bwd(const float *g_out, const float *old_lp, const fl
                                const float *adv, const void *mask, int mask_dtype,
                                const float *ref_lp, int64_t B, int64_t R, float clip_lo,
                                float clip_hi, float clip_c, int agg_mode, int kl_type,
+                               int loss_mode, const uint8_t *sel, float mode_coef,
                                const void *workspace, float *d_lp, float *d_entropy,
                                void *stream) {
   VA_CHECK_ARG(B > 0 && R > 0, "empty batch");
@@ -555,13 +618,14 @@ extern "C" int va_ppo_loss_bwd(const float *g_out, const float *old_lp, const fl
   VA_CHECK_ARG(old_lp && lp && adv && mask && workspace && d_lp, "null pointer argument");
   VA_CHECK_ARG(kl_type == VA_KL_NONE || ref_lp != nullptr, "ref_lp required");
   if (int e = check_agg(agg_mode, false)) return e;
+  if (int e = check_mode(loss_mode, sel)) return e;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const double *part = static_cast<const double *>(workspace);
   const dim3 grid(static_cast<unsigned>((R + 255) / 256), static_cast<unsigned>(B));
   VA_DISPATCH_MASK(mask_dtype, VA_DISPATCH_KL(kl_type, {
     hipLaunchKernelGGL((ppo_loss_bwd_kernel<MT, KL>), grid, dim3(256), 0, s, g_out, old_lp, lp,
-                       adv, mask, ref_lp, B, R, clip_lo, clip_hi, clip_c, agg_mode, part, d_lp,
-                       d_entropy);
+                       adv, mask, ref_lp, sel, B, R, clip_lo, clip_hi, clip_c, agg_mode, loss_mode,
+                       mode_coef, part, d_lp, d_entropy);
   }));
   return check_launch("ppo_loss_bwd");
 }

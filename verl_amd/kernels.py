@@ -127,62 +127,26 @@ def _as_2d(t: torch.Tensor) -> tuple[int, int]:
 
 
 # =============================================================================== log-prob
-class _LogprobEntropy(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, logits, labels, temperature, inplace_backward):
-        V = logits.shape[-1]
-        x = logits.reshape(-1, V)
-        if x.stride(-1) != 1:
-            x = x.contiguous()
-        n = x.shape[0]
-        lab = labels.reshape(-1)
-        if lab.dtype != torch.int64:
-            lab = lab.long()
-        lab = lab.contiguous()
-        if lab.shape[0] != n:
-            raise ValueError(f"labels ({lab.shape[0]}) do not match logits rows ({n})")
-        if x.dtype not in _DTYPE_CODES:
-            raise TypeError(f"unsupported logits dtype {x.dtype}")
-        logp = torch.empty(n, dtype=torch.float32, device=x.device)
-        ent = torch.empty(n, dtype=torch.float32, device=x.device)
-        lse = torch.empty(n, dtype=torch.float32, device=x.device)
-        st = _stream(x)
-        ev = TIMER.start(torch.cuda.current_stream(x.device)) if TIMER is not None else None
-        L.call(
-            "va_logprob_entropy_fwd", _p(x), _DTYPE_CODES[x.dtype], n, V, x.stride(0), _p(lab),
-            float(temperature), _p(logp), _p(ent), _p(lse), st,
-        )
-        if ev is not None:  # algorithmic bytes: s*V logits + 8 label + 12 outputs per row
-            TIMER.stop("logprob_entropy_fwd", n * (x.element_size() * V + 20), torch.cuda.current_stream(x.device), ev)
-        ctx.save_for_backward(x, lab, lse, ent)
-        ctx.temperature = float(temperature)
-        ctx.inplace = bool(inplace_backward)
-        ctx.in_shape = logits.shape
-        out_shape = logits.shape[:-1]
-        return logp.view(out_shape), ent.view(out_shape)
-
-    @staticmethod
-    def backward(ctx, g_logp, g_ent):
-        x, lab, lse, ent = ctx.saved_tensors
-        n, V = x.shape
-        g1 = None if g_logp is None else _f32(g_logp.reshape(-1))
-        g2 = None if g_ent is None else _f32(g_ent.reshape(-1))
-        dx = x if ctx.inplace else torch.empty_like(x)
-        ev = TIMER.start(torch.cuda.current_stream(x.device)) if TIMER is not None else None
-        L.call(
-            "va_logprob_entropy_bwd", _p(g1), _p(g2), _p(x), _DTYPE_CODES[x.dtype], n, V, x.stride(0),
-            _p(lab), _p(lse), _p(ent), ctx.temperature, _p(dx), dx.stride(0), _stream(x),
-        )
-        if ev is not None:  # read + write logits, 28 B of row scalars
-            TIMER.stop("logprob_entropy_bwd", n * (2 * x.element_size() * V + 28), torch.cuda.current_stream(x.device), ev)
-        return dx.view(ctx.in_shape), None, None, None
-
-
 def logprob_entropy(logits, labels, temperature: float = 1.0, inplace_backward: bool = False):
     """(log p[label], entropy) per row of ``logits[..., V]`` after the reference's
-    ``logits.div_(temperature)``; one fused HBM pass forward, one backward."""
+    ``logits.div_(temperature)``; one fused HBM pass forward, one backward
+    (torch.ops.verl_amd.logprob_entropy_fwd / _bwd, custom_ops.py)."""
     _require_device(logits, labels)
-    return _LogprobEntropy.apply(logits, labels, temperature, inplace_backward)
+    V = logits.shape[-1]
+    x = logits.reshape(-1, V)
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    lab = labels.reshape(-1)
+    if lab.dtype != torch.int64:
+        lab = lab.long()
+    lab = lab.contiguous()
+    if lab.shape[0] != x.shape[0]:
+        raise ValueError(f"labels ({lab.shape[0]}) do not match logits rows ({x.shape[0]})")
+    if x.dtype not in _DTYPE_CODES:
+        raise TypeError(f"unsupported logits dtype {x.dtype}")
+    logp, ent, _ = torch.ops.verl_amd.logprob_entropy_fwd(x, lab, float(temperature), bool(inplace_backward))
+    out_shape = logits.shape[:-1]
+    return logp.view(out_shape), ent.view(out_shape)
 
 
 # =============================================================================== fused lm_head + log-prob
@@ -271,40 +235,8 @@ def linear_logprob_entropy(hidden, weight, labels, temperature: float = 1.0):
 
 
 # =============================================================================== policy loss
-class _PolicyLoss(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, old_lp, lp, adv, mask, ref_lp, entropy, clip_lo, clip_hi, clip_c, agg, kl_type):
-        B, R = _as_2d(lp)
-        old_c, lp_c, adv_c = _f32(old_lp), _f32(lp), _f32(adv)
-        ref_c, ent_c = _f32(ref_lp), _f32(entropy)
-        m, mcode = _mask(mask)
-        out = torch.empty(L.VA_LOSS_NOUT, dtype=torch.float32, device=lp.device)
-        nbytes = L.load().va_ppo_loss_workspace_bytes(B)
-        ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=lp.device)
-        L.call(
-            "va_ppo_loss_fwd", _p(old_c), _p(lp_c), _p(adv_c), _p(m), mcode, _p(ref_c), _p(ent_c), B, R,
-            clip_lo, clip_hi, clip_c, agg, kl_type, _p(out), _p(ws), _stream(lp),
-        )
-        ctx.save_for_backward(old_c, lp_c, adv_c, m, ref_c, ws)
-        ctx.cfg = (B, R, mcode, clip_lo, clip_hi, clip_c, agg, kl_type, entropy is not None)
-        ctx.lp_shape = lp.shape
-        return out
-
-    @staticmethod
-    def backward(ctx, g_out):
-        old_c, lp_c, adv_c, m, ref_c, ws = ctx.saved_tensors
-        B, R, mcode, clip_lo, clip_hi, clip_c, agg, kl_type, has_ent = ctx.cfg
-        g = _f32(g_out)
-        d_lp = torch.empty_like(lp_c)
-        d_ent = torch.empty_like(lp_c) if has_ent and ctx.needs_input_grad[5] else None
-        L.call(
-            "va_ppo_loss_bwd", _p(g), _p(old_c), _p(lp_c), _p(adv_c), _p(m), mcode, _p(ref_c), B, R,
-            clip_lo, clip_hi, clip_c, agg, kl_type, _p(ws), _p(d_lp), _p(d_ent), _stream(lp_c),
-        )
-        d_lp = d_lp.view(ctx.lp_shape) if ctx.needs_input_grad[1] else None
-        if d_ent is not None:
-            d_ent = d_ent.view(ctx.lp_shape)
-        return None, d_lp, None, None, None, d_ent, None, None, None, None, None
+POLICY_LOSS_MODES = {"vanilla": L.VA_PL_VANILLA, "gpg": L.VA_PL_GPG, "clip_cov": L.VA_PL_CLIP_COV,
+                     "kl_cov": L.VA_PL_KL_COV}
 
 
 def fused_policy_loss(
@@ -319,11 +251,16 @@ def fused_policy_loss(
     ref_log_prob=None,
     kl_loss_type: str | None = None,
     entropy=None,
+    loss_mode: str = "vanilla",
+    selection=None,
+    mode_coef: float = 0.0,
 ) -> torch.Tensor:
-    """Fused compute_policy_loss + agg_loss(kl_penalty) + agg_loss(entropy) (dp_actor.py:421-459).
+    """Fused compute_policy_loss (or a registered variant: gpg / clip_cov / kl_cov) +
+    agg_loss(kl_penalty) + agg_loss(entropy) (dp_actor.py:419-459).
 
     Returns the 8-slot vector (see VA_LOSS_* in include/verl_amd.h) whose slots are the scalars
     the reference returns; gradients flow from slots PG, KL and ENTROPY to log_prob / entropy.
+    ``selection`` is the variant's token selection ([B, R] bool / uint8, clip_cov / kl_cov).
     """
     assert clip_ratio_c > 1.0, (
         "The lower bound of the clip_ratio_c for dual-clip PPO should be greater than 1.0,"
@@ -336,44 +273,22 @@ def fused_policy_loss(
         if kl_loss_type == "full" or kl_loss_type not in KL_TYPES:
             raise NotImplementedError
         kl_type = KL_TYPES[kl_loss_type]
-    _require_device(old_log_prob, log_prob, advantages, response_mask, ref_log_prob, entropy)
-    # torch.clamp casts its python-float bounds to the tensor dtype (fp32)
-    clip_lo = float(np.float32(1 - clip_ratio_low))
-    clip_hi = float(np.float32(1 + clip_ratio_high))
-    clip_c = float(np.float32(clip_ratio_c))
-    return _PolicyLoss.apply(
-        old_log_prob, log_prob, advantages, response_mask, ref_log_prob, entropy, clip_lo, clip_hi, clip_c,
-        AGG_MODES[loss_agg_mode], kl_type,
+    _require_device(old_log_prob, log_prob, advantages, response_mask, ref_log_prob, entropy, selection)
+    m, _ = _mask(response_mask)
+    sel = None
+    if selection is not None:
+        sel = selection.to(torch.uint8).contiguous()
+    # torch.clamp casts its python-float bounds to the tensor dtype (fp32): the C-ABI's float
+    # parameters apply the same rounding
+    out, _ = torch.ops.verl_amd.ppo_loss_fwd(
+        _f32(old_log_prob), _f32(log_prob), _f32(advantages), m, _f32(ref_log_prob), _f32(entropy), sel,
+        1.0 - clip_ratio_low, 1.0 + clip_ratio_high, float(clip_ratio_c), AGG_MODES[loss_agg_mode], kl_type,
+        POLICY_LOSS_MODES[loss_mode], float(mode_coef),
     )
+    return out
 
 
 # =============================================================================== value loss (critic)
-class _ValueLoss(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, vpreds, values, returns, mask, cliprange_value, agg):
-        B, R = _as_2d(vpreds)
-        vp, v, r = _f32(vpreds), _f32(values), _f32(returns)
-        m, mcode = _mask(mask)
-        out = torch.empty(L.VA_VLOSS_NOUT, dtype=torch.float32, device=vp.device)
-        nbytes = L.load().va_ppo_loss_workspace_bytes(B)
-        ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=vp.device)
-        L.call("va_value_loss_fwd", _p(vp), _p(v), _p(r), _p(m), mcode, B, R, cliprange_value, agg, _p(out), _p(ws),
-               _stream(vp))
-        ctx.save_for_backward(vp, v, r, m, ws)
-        ctx.cfg = (B, R, mcode, cliprange_value, agg, vpreds.shape, vpreds.dtype)
-        return out
-
-    @staticmethod
-    def backward(ctx, g_out):
-        vp, v, r, m, ws = ctx.saved_tensors
-        B, R, mcode, c, agg, shape, dtype = ctx.cfg
-        g = _f32(g_out)
-        d_vp = torch.empty_like(vp)
-        L.call("va_value_loss_bwd", _p(g), _p(vp), _p(v), _p(r), _p(m), mcode, B, R, c, agg, _p(ws), _p(d_vp),
-               _stream(vp))
-        return d_vp.view(shape).to(dtype), None, None, None, None, None
-
-
 def fused_value_loss(vpreds, values, returns, response_mask, cliprange_value: float,
                      loss_agg_mode: str = "token-mean") -> torch.Tensor:
     """compute_value_loss (core_algos.py:992-1031) + masked_mean(vpreds) in one fused kernel pair.
@@ -383,70 +298,28 @@ def fused_value_loss(vpreds, values, returns, response_mask, cliprange_value: fl
     if loss_agg_mode not in AGG_MODES:
         raise ValueError(f"Invalid loss_agg_mode: {loss_agg_mode}")
     _require_device(vpreds, values, returns, response_mask)
-    return _ValueLoss.apply(vpreds, values, returns, response_mask, float(np.float32(cliprange_value)),
-                            AGG_MODES[loss_agg_mode])
+    m, _ = _mask(response_mask)
+    out, _ = torch.ops.verl_amd.value_loss_fwd(_f32(vpreds), _f32(values), _f32(returns), m, float(cliprange_value),
+                                               AGG_MODES[loss_agg_mode])
+    return out
 
 
 # =============================================================================== kl penalty
-class _KLPenalty(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, lp, ref, kl_type):
-        a, b = _f32(lp), _f32(ref)
-        out = torch.empty_like(a)
-        L.call("va_kl_penalty_fwd", _p(a), _p(b), a.numel(), kl_type, _p(out), _stream(a))
-        ctx.save_for_backward(a, b)
-        ctx.kl_type = kl_type
-        return out.view(lp.shape)
-
-    @staticmethod
-    def backward(ctx, g):
-        a, b = ctx.saved_tensors
-        g = _f32(g)
-        d_lp = torch.empty_like(a) if ctx.needs_input_grad[0] else None
-        d_ref = torch.empty_like(a) if ctx.needs_input_grad[1] else None
-        L.call("va_kl_penalty_bwd", _p(g), _p(a), _p(b), a.numel(), ctx.kl_type, _p(d_lp), _p(d_ref), _stream(a))
-        return d_lp, d_ref, None
-
-
 def kl_penalty(logprob, ref_logprob, kl_type: str):
     _require_device(logprob, ref_logprob)
     if kl_type not in KL_TYPES:
         raise NotImplementedError
-    return _KLPenalty.apply(logprob, ref_logprob, KL_TYPES[kl_type])
+    return torch.ops.verl_amd.kl_penalty_fwd(_f32(logprob), _f32(ref_logprob), KL_TYPES[kl_type]).view(logprob.shape)
 
 
 # =============================================================================== masked aggregation
-class _MaskedAgg(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, mask, mode, B, R):
-        xc = _f32(x)
-        m, mcode = _mask(mask)
-        nout = B if mode == L.VA_REDUCE_ROW_MASKED_MEAN else 1
-        out = torch.empty(nout, dtype=torch.float32, device=x.device)
-        nbytes = L.load().va_agg_workspace_bytes(B)
-        ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=x.device)
-        L.call("va_masked_agg_fwd", _p(xc), _p(m), mcode, B, R, mode, _p(out), _p(ws), _stream(xc))
-        ctx.save_for_backward(m, ws)
-        ctx.cfg = (mcode, B, R, mode, x.shape)
-        return out
-
-    @staticmethod
-    def backward(ctx, g):
-        m, ws = ctx.saved_tensors
-        mcode, B, R, mode, shape = ctx.cfg
-        g = _f32(g)
-        dx = torch.empty(B * R, dtype=torch.float32, device=m.device)
-        L.call("va_masked_agg_bwd", _p(g), _p(m), mcode, B, R, mode, _p(ws), _p(dx), _stream(m))
-        return dx.view(shape), None, None, None, None
-
-
 def masked_aggregate(x, mask, mode: int):
     """Aggregate a [..., R] matrix over the mask; mode is a VA_AGG_* / VA_REDUCE_* code."""
     _require_device(x, mask)
     if x.shape != mask.shape:
         mask = mask.expand_as(x)
-    B, R = _as_2d(x)
-    out = _MaskedAgg.apply(x, mask, mode, B, R)
+    m, _ = _mask(mask)
+    out, _ = torch.ops.verl_amd.masked_agg_fwd(_f32(x), m, mode)
     if mode == L.VA_REDUCE_ROW_MASKED_MEAN:
         return out.view(x.shape[:-1])
     return out.view(())
@@ -476,55 +349,33 @@ def group_csr(index, device) -> tuple[torch.Tensor, torch.Tensor, int, int]:
 def outcome_advantage(token_level_rewards, response_mask, index, epsilon: float, estimator: int):
     _require_device(token_level_rewards, response_mask)
     r = _f32(token_level_rewards)
-    B, R = r.shape
-    m, mcode = _mask(response_mask)
+    m, _ = _mask(response_mask)
     order, offsets, G, gmax = group_csr(index, r.device)
-    adv = torch.empty_like(r)
-    ws = torch.empty(max(1, L.load().va_outcome_workspace_bytes(B) // 4), dtype=torch.float32, device=r.device)
-    L.call(
-        "va_outcome_advantage", _p(r), _p(m), mcode, B, R, _p(order), _p(offsets), G, gmax, float(epsilon),
-        estimator, _p(adv), None, _p(ws), _stream(r),
-    )
-    return adv
+    return torch.ops.verl_amd.outcome_advantage(r, m, order, offsets, G, gmax, float(epsilon), estimator)
 
 
 def row_scores(token_level_rewards, response_mask=None, lengths: bool = False):
     """(scores [B], lengths [B] | None): unmasked reward row sums (core_algos.py:282) and, when
     asked, response lengths sum(mask) (OPO, core_algos.py:505)."""
     _require_device(token_level_rewards, response_mask)
-    r = _f32(token_level_rewards)
-    B, R = r.shape
-    scores = torch.empty(B, dtype=torch.float32, device=r.device)
-    lens = torch.empty(B, dtype=torch.float32, device=r.device) if lengths else None
-    if lengths:
-        m, mcode = _mask(response_mask)
-    else:
-        m, mcode = None, L.VA_MASK_F32
-    L.call("va_row_scores", _p(r), _p(m), mcode, B, R, _p(scores), _p(lens), _stream(r))
-    return scores, lens
+    m = _mask(response_mask)[0] if lengths else None
+    scores, lens = torch.ops.verl_amd.row_scores(_f32(token_level_rewards), m, bool(lengths))
+    return scores, (lens if lengths else None)
 
 
 def group_coef(scores, lengths, order, offsets, n_groups: int, max_group_size: int, epsilon: float,
                estimator: int):
     """Per-row advantage coefficient a(b) of every row of a (possibly all-gathered) batch."""
     _require_device(scores, lengths, order, offsets)
-    coef = torch.empty_like(scores)
-    L.call("va_group_coef", _p(scores), _p(lengths), _p(order), _p(offsets), n_groups, max_group_size,
-           float(epsilon), estimator, _p(coef), _stream(scores))
-    return coef
+    return torch.ops.verl_amd.group_coef(_f32(scores), _f32(lengths), order, offsets, n_groups, max_group_size,
+                                         float(epsilon), estimator)
 
 
 def broadcast_rows(coef, response_mask):
     """adv[b, t] = coef[b] * mask[b, t]."""
     _require_device(coef, response_mask)
-    m, mcode = _mask(response_mask)
-    B, R = m.shape
-    c = _f32(coef)
-    if c.numel() != B:
-        raise ValueError(f"broadcast_rows: {c.numel()} coefficients for {B} rows")
-    adv = torch.empty(B, R, dtype=torch.float32, device=m.device)
-    L.call("va_broadcast_rows", _p(c), _p(m), mcode, B, R, _p(adv), _stream(adv))
-    return adv
+    m, _ = _mask(response_mask)
+    return torch.ops.verl_amd.broadcast_rows(_f32(coef), m)
 
 
 def discounted_returns(token_level_rewards, response_mask, gamma: float, mode: int, baselines=None):
@@ -532,17 +383,10 @@ def discounted_returns(token_level_rewards, response_mask, gamma: float, mode: i
     reverse-scan kernel."""
     _require_device(token_level_rewards, response_mask, baselines)
     r = _f32(token_level_rewards)
-    B, R = r.shape
-    m, mcode = _mask(response_mask)
-    ret = torch.empty_like(r)
-    if mode == L.VA_RET_REMAX:
-        b = _f32(baselines).reshape(B)
-        adv = torch.empty_like(r)
-        L.call("va_discounted_returns", _p(r), _p(m), mcode, B, R, float(gamma), mode, _p(b), _p(ret), _p(adv),
-               _stream(r))
-        return ret, adv
-    L.call("va_discounted_returns", _p(r), _p(m), mcode, B, R, float(gamma), mode, None, _p(ret), None, _stream(r))
-    return ret
+    m, _ = _mask(response_mask)
+    b = _f32(baselines).reshape(r.shape[0]) if mode == L.VA_RET_REMAX else None
+    ret, adv = torch.ops.verl_amd.discounted_returns(r, m, float(gamma), mode, b)
+    return (ret, adv) if mode == L.VA_RET_REMAX else ret
 
 
 _WHITEN_ERRORS = {
@@ -559,18 +403,9 @@ def _raise_whiten_flag(stats: torch.Tensor) -> None:
 
 def gae_advantage_return(rewards, values, mask, gamma: float, lam: float, check: bool = True):
     _require_device(rewards, values, mask)
-    r, v = _f32(rewards), _f32(values)
-    B, R = r.shape
-    m, mcode = _mask(mask)
-    adv = torch.empty_like(r)
-    ret = torch.empty_like(r)
-    stats = torch.empty(4, dtype=torch.float32, device=r.device)
-    nbytes = L.load().va_gae_workspace_bytes(B)
-    ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=r.device)
-    L.call(
-        "va_gae_advantage_return", _p(r), _p(v), _p(m), mcode, B, R, float(gamma), float(lam), _p(adv), _p(ret),
-        _p(stats), _p(ws), _stream(r),
-    )
+    m, _ = _mask(mask)
+    adv, ret, stats = torch.ops.verl_amd.gae_advantage_return(_f32(rewards), _f32(values), m, float(gamma),
+                                                              float(lam))
     if check:
         _raise_whiten_flag(stats)
     return adv, ret
@@ -582,23 +417,19 @@ def whiten_stats(values, mask) -> tuple[torch.Tensor, torch.Tensor]:
     x = _f32(values)
     if mask.shape != x.shape:
         mask = mask.expand_as(x)
-    B, R = _as_2d(x)
-    m, mcode = _mask(mask)
-    part = torch.empty(B * 3 + 3, dtype=torch.float64, device=x.device)
-    stats = torch.empty(4, dtype=torch.float32, device=x.device)
-    s = _stream(x)
-    L.call("va_masked_row_partials", _p(x), _p(m), mcode, B, R, _p(part), s)
-    merged = part[B * 3:]
-    L.call("va_whiten_finalize", _p(part), B, _p(merged), _p(stats), s)
+    B, _ = _as_2d(x)
+    m, _ = _mask(mask)
+    part = torch.ops.verl_amd.masked_row_partials(x, m)
+    merged, stats = torch.ops.verl_amd.whiten_finalize(part, B)
     return stats, merged
 
 
 def whiten_apply(values, mask, stats, post_multiply_mask: bool = False, out=None):
     x = _f32(values)
-    y = x.clone() if out is None else out.copy_(x)
-    B, R = _as_2d(y)
-    m, mcode = _mask(mask.expand_as(x)) if post_multiply_mask else (None, 0)
-    L.call("va_whiten_apply", _p(y), _p(stats), _p(m), mcode, B, R, 1 if post_multiply_mask else 0, _stream(y))
+    m = _mask(mask.expand_as(x))[0] if post_multiply_mask else None
+    y = torch.ops.verl_amd.whiten_apply(x, stats, m, bool(post_multiply_mask))
+    if out is not None:
+        return out.copy_(y)
     return y
 
 
@@ -606,16 +437,9 @@ def apply_kl_penalty(token_level_scores, old_log_prob, ref_log_prob, response_ma
     _require_device(token_level_scores, old_log_prob, ref_log_prob, response_mask)
     if kl_type not in KL_TYPES:
         raise NotImplementedError
-    s, o, r = _f32(token_level_scores), _f32(old_log_prob), _f32(ref_log_prob)
-    B, R = s.shape
-    m, mcode = _mask(response_mask)
-    rewards = torch.empty_like(s)
-    row_kl = torch.empty(B, dtype=torch.float32, device=s.device)
-    L.call(
-        "va_apply_kl_penalty", _p(s), _p(o), _p(r), _p(m), mcode, B, R, KL_TYPES[kl_type], float(beta),
-        _p(rewards), _p(row_kl), _stream(s),
-    )
-    return rewards, row_kl
+    m, _ = _mask(response_mask)
+    return torch.ops.verl_amd.apply_kl_penalty(_f32(token_level_scores), _f32(old_log_prob), _f32(ref_log_prob), m,
+                                               KL_TYPES[kl_type], float(beta))
 
 
 # =============================================================================== grad accumulation
@@ -883,3 +707,6 @@ def rope_qkv(qkv, cos, sin, num_q_heads: int, num_kv_heads: int, head_dim: int):
         raise ValueError(f"rope_qkv: qkv {tuple(qkv.shape)} does not hold {num_q_heads}+2x{num_kv_heads} heads of "
                          f"{head_dim}")
     return _RoPEQKV.apply(qkv, cos, sin, num_q_heads, num_kv_heads, head_dim)
+
+
+from . import custom_ops as _custom_ops  # noqa: E402,F401  (registers torch.ops.verl_amd.*)

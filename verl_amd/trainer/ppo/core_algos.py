@@ -14,8 +14,9 @@ the reference (core_algos.py:33-1069). The hot-path functions run as gfx950 kern
   compute_value_loss (critic) -> va_value_loss_fwd/bwd
 
 GPG's advantage reuses the group-mean kernel plus one device-side scale; the gpg / clip_cov /
-kl_cov policy-loss variants are device tensor ops (their top-k / random selection over the
-batch is not a streaming kernel's shape).
+kl_cov policy-loss variants run in the fused loss kernel (loss modes VA_PL_*); only their
+token selection (a batch-global top-k / random subset, not a streaming kernel's shape) is made
+with device tensor ops here.
 """
 
 from __future__ import annotations
@@ -278,18 +279,27 @@ def compute_actor_loss(old_log_prob, log_prob, advantages, response_mask, clip_r
                                entropy=entropy)
 
 
+def _variant_loss(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode, mode, selection=None, coef=0.0,
+                  clip_lo=0.2, clip_hi=0.2):
+    out = K.fused_policy_loss(old_log_prob, log_prob, advantages, response_mask, clip_lo, clip_hi, 3.0, loss_agg_mode,
+                              loss_mode=mode, selection=selection, mode_coef=coef)
+    return out[L.VA_LOSS_PG], out[L.VA_LOSS_CLIPFRAC], out[L.VA_LOSS_PPO_KL], out[L.VA_LOSS_CLIPFRAC_LOWER]
+
+
 @register_policy_loss("gpg")
 def compute_policy_loss_gpg(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode="token-mean", config=None):
-    """core_algos.py:797-815."""
-    pg_loss = agg_loss(-log_prob * advantages, response_mask, loss_agg_mode)
-    z = torch.tensor(0.0, device=log_prob.device)
-    return pg_loss, z, z, z
+    """core_algos.py:797-815: agg_loss(-log_prob * advantages); the fused loss kernel in mode
+    VA_PL_GPG (metric slots 0)."""
+    return _variant_loss(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode, "gpg")
 
 
 @register_policy_loss("clip_cov")
 def compute_policy_loss_clip_cov(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode="token-mean",
                                  config=None):
-    """core_algos.py:818-905 (device tensor ops)."""
+    """core_algos.py:818-905. The token selection (covariance window (lb, ub), tokens not already
+    clipped, a random subset of clip_cov_ratio * n_tokens drawn with the reference's
+    torch.randperm on the default CPU generator) is made here with device tensor ops; the loss,
+    its gradient and the metrics run in the fused kernel (VA_PL_CLIP_COV: max(l1, l2) * corr)."""
     pl = config.policy_loss
     clip_cov_ratio = pl.clip_cov_ratio if pl.clip_cov_ratio is not None else 0.0002
     cliprange = config.clip_ratio
@@ -298,61 +308,51 @@ def compute_policy_loss_clip_cov(old_log_prob, log_prob, advantages, response_ma
     ub = pl.clip_cov_ub if pl.clip_cov_ub is not None else 5.0
     lb = pl.clip_cov_lb if pl.clip_cov_lb is not None else 1.0
     assert clip_cov_ratio > 0, "clip_ratio should be larger than 0."
-    neg_kl = log_prob - old_log_prob
-    ratio = torch.exp(neg_kl)
-    ppo_kl = verl_F.masked_mean(-neg_kl, response_mask)
-    l1 = -advantages * ratio
-    corr = torch.ones_like(advantages)
-    l2 = -advantages * torch.clamp(ratio, 1 - lo, 1 + hi)
-    clip_by_origin = (l2 > l1) & (response_mask > 0)
-    cov_all = (advantages - verl_F.masked_mean(advantages, response_mask)) * (
-        log_prob - verl_F.masked_mean(log_prob.detach(), response_mask))
-    cov_all[response_mask == 0] = -torch.inf
-    cov_all[clip_by_origin] = -torch.inf
-    clip_num = max(int(clip_cov_ratio * response_mask.sum().item()), 1)
-    idx = torch.nonzero((cov_all < ub) & (cov_all > lb) & (response_mask > 0))
-    if len(idx) > 0:
-        perm = torch.randperm(len(idx))
-        idx = idx[perm[: min(clip_num, len(idx))]]
-    else:
-        idx = torch.empty((0, 2), device=cov_all.device, dtype=torch.long)
-    corr[idx[:, 0], idx[:, 1]] = 0
-    clipfrac = verl_F.masked_mean((corr == 0).float(), response_mask)
-    pg_loss = agg_loss(torch.maximum(l1, l2) * corr, response_mask, loss_agg_mode)
-    return pg_loss, clipfrac, ppo_kl, torch.tensor(0.0, device=log_prob.device)
+    with torch.no_grad():
+        lp = log_prob.detach()
+        ratio = torch.exp(lp - old_log_prob)
+        l1 = -advantages * ratio
+        l2 = -advantages * torch.clamp(ratio, 1 - lo, 1 + hi)
+        clip_by_origin = (l2 > l1) & (response_mask > 0)
+        cov_all = (advantages - verl_F.masked_mean(advantages, response_mask)) * (
+            lp - verl_F.masked_mean(lp, response_mask))
+        cov_all[response_mask == 0] = -torch.inf
+        cov_all[clip_by_origin] = -torch.inf
+        clip_num = max(int(clip_cov_ratio * response_mask.sum().item()), 1)
+        idx = torch.nonzero((cov_all < ub) & (cov_all > lb) & (response_mask > 0))
+        if len(idx) > 0:
+            perm = torch.randperm(len(idx))
+            idx = idx[perm[: min(clip_num, len(idx))].to(idx.device)]
+        sel = torch.zeros(advantages.shape, dtype=torch.uint8, device=advantages.device)
+        sel[idx[:, 0], idx[:, 1]] = 1
+    return _variant_loss(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode, "clip_cov", sel,
+                         clip_lo=lo, clip_hi=hi)
 
 
 @register_policy_loss("kl_cov")
 def compute_policy_loss_kl_cov(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode="token-mean",
                                config=None):
-    """core_algos.py:908-972 (device tensor ops)."""
+    """core_algos.py:908-972. The top-k covariance tokens (k = max(1, int(n_valid * kl_cov_ratio)),
+    torch.topk as the reference) are selected here; the loss (-A r + ppo_kl_coef |lp - old| on the
+    selection), its gradient and ppo_kl_abs run in the fused kernel (VA_PL_KL_COV)."""
     pl = config.policy_loss
     kl_cov_ratio = pl.kl_cov_ratio if pl.kl_cov_ratio is not None else 0.0002
     ppo_kl_coef = pl.ppo_kl_coef if pl.ppo_kl_coef is not None else 1.0
     assert kl_cov_ratio > 0, "kl_cov_ratio should be larger than 0."
-    neg_kl = log_prob - old_log_prob
-    abs_kl = neg_kl.abs()
-    ratio = torch.exp(neg_kl)
-    ppo_kl_abs = verl_F.masked_mean(neg_kl.abs(), response_mask)
-    l1 = -advantages * ratio
-    l_kl = -advantages * ratio + ppo_kl_coef * abs_kl
-    pg_losses = l1
-    valid = response_mask > 0
-    valid_idx = torch.nonzero(valid.reshape(-1), as_tuple=True)[0]
-    adv_v = advantages[valid].detach().reshape(-1)
-    lp_v = log_prob[valid].detach().reshape(-1)
-    k = min(kl_cov_ratio, len(adv_v))
-    if k != 0:
-        cov = (adv_v - adv_v.mean()) * (lp_v - lp_v.mean())
-        nk = max(1, int(len(cov) * kl_cov_ratio))
-        top = torch.topk(cov, nk, largest=True).indices
-        if len(top) != 0:
-            top = valid_idx[top]
-            R = advantages.shape[1]
-            pg_losses = pg_losses.clone()
-            pg_losses[top // R, top % R] = l_kl[top // R, top % R]
-    pg_loss = agg_loss(pg_losses, response_mask, loss_agg_mode)
-    return pg_loss, torch.tensor(0.0, device=log_prob.device), ppo_kl_abs, torch.tensor(0.0, device=log_prob.device)
+    with torch.no_grad():
+        valid = response_mask > 0
+        valid_idx = torch.nonzero(valid.reshape(-1), as_tuple=True)[0]
+        adv_v = advantages[valid].detach().reshape(-1)
+        lp_v = log_prob[valid].detach().reshape(-1)
+        sel = torch.zeros(advantages.shape, dtype=torch.uint8, device=advantages.device)
+        if min(kl_cov_ratio, len(adv_v)) != 0:
+            cov = (adv_v - adv_v.mean()) * (lp_v - lp_v.mean())
+            nk = max(1, int(len(cov) * kl_cov_ratio))
+            top = torch.topk(cov, nk, largest=True).indices
+            if len(top) != 0:
+                sel.view(-1)[valid_idx[top]] = 1
+    return _variant_loss(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode, "kl_cov", sel,
+                         coef=ppo_kl_coef)
 
 
 def compute_entropy_loss(logits, response_mask, loss_agg_mode: str = "token-mean"):

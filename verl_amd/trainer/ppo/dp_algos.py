@@ -138,15 +138,11 @@ def outcome_advantage_dp(token_level_rewards, response_mask, index, epsilon: flo
 
 def global_whiten_stats(local_merged: torch.Tensor, group=None) -> torch.Tensor:
     """local (n, sum, M2) fp64[3] on the device -> global fp32 stats {mean, rstd, n, flag}."""
-    w = _world(group)
-    dev = local_merged.device
-    if w > 1:
+    if _world(group) > 1:
         triples = torch.stack(_all_gather(local_merged.contiguous(), group)).contiguous()
     else:
         triples = local_merged.view(1, 3).contiguous()
-    stats = torch.empty(4, dtype=torch.float32, device=dev)
-    merged = torch.empty(3, dtype=torch.float64, device=dev)
-    L.call("va_whiten_finalize", K._p(triples), triples.shape[0], K._p(merged), K._p(stats), K._stream(stats))
+    _, stats = torch.ops.verl_amd.whiten_finalize(triples.view(-1), triples.shape[0])
     return stats
 
 
@@ -160,24 +156,16 @@ def masked_whiten_dp(values, mask, group=None, post_multiply_mask: bool = False)
 
 def compute_gae_advantage_return_dp(token_level_rewards, values, response_mask, gamma, lam, group=None):
     """GAE on this rank's rows; whitening statistics over all ranks (one 24-byte all-gather)."""
-    _require = K._require_device
-    _require(token_level_rewards, values, response_mask)
-    r, v = K._f32(token_level_rewards), K._f32(values)
-    B, R = r.shape
-    m, mcode = K._mask(response_mask)
-    adv = torch.empty_like(r)
-    ret = torch.empty_like(r)
-    part = torch.empty(B * 3 + 3, dtype=torch.float64, device=r.device)
-    s = K._stream(r)
+    K._require_device(token_level_rewards, values, response_mask)
+    m, _ = K._mask(response_mask)
     with torch.no_grad():
-        L.call("va_gae_scan", K._p(r), K._p(v), K._p(m), mcode, B, R, float(gamma), float(lam), K._p(adv), K._p(ret),
-               K._p(part), s)
-        local = part[B * 3:]
-        stats4 = torch.empty(4, dtype=torch.float32, device=r.device)
-        L.call("va_whiten_finalize", K._p(part), B, K._p(local), K._p(stats4), s)
+        adv_raw, ret, part = torch.ops.verl_amd.gae_scan(K._f32(token_level_rewards), K._f32(values), m,
+                                                         float(gamma), float(lam))
+        B = adv_raw.shape[0]
+        local, _ = torch.ops.verl_amd.whiten_finalize(part, B)
         stats = global_whiten_stats(local, group)
         K._raise_whiten_flag(stats)
-        L.call("va_whiten_apply", K._p(adv), K._p(stats), None, 0, B, R, 0, s)
+        adv = torch.ops.verl_amd.whiten_apply(adv_raw, stats, None, False)
     return adv, ret
 
 
