@@ -129,9 +129,11 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   VA_TUNE_FLASH_GROUPED_DKDV (va_flash_attn_bwd): -1 = auto, 0 = per-query-head fp32 partials +
  *   fixed-order group sum, 1 = one workgroup per key block x KV head summing its group in registers
  *   (results differ only in fp32 summation order);
- *   VA_TUNE_GAE_VARIANT (va_gae_scan): 0 = auto, 1 = register chunks (rows of R <= 1024 only;
- *   longer rows keep the LDS kernel), 2 = LDS-staged kernel (advantages/returns bitwise identical,
- *   the fp64 row partials differ only in summation order);
+ *   VA_TUNE_GAE_VARIANT (va_gae_scan): 0 = auto (quad-streaming kernel where R % 4 == 0, R <= 2048
+ *   and the rows are 16-byte aligned), 1 = register chunks (rows of R <= 1024 only; longer rows keep
+ *   the LDS kernel), 2 = LDS-staged kernel (1 and 2: advantages/returns bitwise identical, the fp64
+ *   row partials differ only in summation order), 3 = quad-streaming kernel (4-step lane quads
+ *   instead of 16-step lane chunks: the scan reassociates differently, within the same budget);
  *   VA_TUNE_BWD_FLAT (va_logprob_entropy_bwd): -1 = auto (one flat stream of equal 16-KB chunks over
  *   the whole tensor when logits and dlogits are dense, row stride = vocab), 0 = per-row chunks
  *   (bitwise identical results);
@@ -143,7 +145,12 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   VA_TUNE_FLASH_DQ_KB (va_flash_attn_bwd): keys per staged dQ block, 128 (default) or 64 (bitwise
  *   identical results);
  *   VA_TUNE_FLASH_FWD_KB (va_flash_attn_fwd): keys per staged forward block, 64 (default) or 128
- *   (bitwise identical results: the same 64-key online-softmax steps). */
+ *   (bitwise identical results: the same 64-key online-softmax steps);
+ *   VA_TUNE_GAE_PARTIALS (va_gae_scan): rows per whitening partial triple, 0 = auto, 1 (per row),
+ *   4 or 8 (per workgroup); results differ only in the fp64 merge order;
+ *   VA_TUNE_GAE_NT (va_gae_scan / va_gae_advantage_return): streaming-cache bits, 1 = non-temporal
+ *   r / v loads, 2 = non-temporal returns store, 4 = non-temporal raw / whitened advantage stores
+ *   (default 3; identical results). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3
@@ -155,6 +162,8 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_FLASH_DKDV_QT 9
 #define VA_TUNE_FLASH_DQ_KB 10
 #define VA_TUNE_FLASH_FWD_KB 11
+#define VA_TUNE_GAE_PARTIALS 12
+#define VA_TUNE_GAE_NT 13
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------
@@ -251,26 +260,35 @@ int va_broadcast_rows(const float *coef, const void *mask, int mask_dtype, int64
                       float *adv, void *stream);
 
 /* ---------------------------------------------------------------------------------------
- * GAE (core_algos.py:193-241): masked reverse recurrence per row as an LDS-staged chunked
- * affine scan, then the batch-global masked whitening (torch_functional.py:188-223).
+ * GAE (core_algos.py:193-241): masked reverse recurrence per row as a chunked affine scan, then
+ * the batch-global masked whitening (torch_functional.py:188-223).
  *   rewards, values [B,R] fp32, mask [B,R] -> adv [B,R] (whitened), ret [B,R] (= raw + values)
  *   row_stats: workspace (va_gae_workspace_bytes(B)).
  *   stats_out[4] fp32 (device): {mean, rsqrt(var + 1e-8), mask_sum, error_flag}
  *   error_flag = 1 when mask_sum == 0, 2 when mask_sum == 1 (the ValueErrors of
  *   torch_functional.py:195-200, raised by the host wrapper).
- * For data-parallel whitening the three phases are exported separately:
- *   va_gae_scan        -> adv_raw, ret, row partials (n, sum, M2) in fp64
- *   va_whiten_finalize -> merges K partial triples in index order (Chan), emits the merged
- *                         fp64 triple and the fp32 stats (call it again on all-gathered triples)
+ * Two or three launches: the scan (one wave per row, 16-byte quads per lane) writes P =
+ * va_gae_partial_count(B) partial (n, sum, M2) triples (one per row, or per workgroup of 4 / 8
+ * rows, see VA_TUNE_GAE_PARTIALS) into the workspace; when P > 4096 they are first merged in
+ * parallel slices; the last launch merges them in every workgroup (fixed order) and whitens adv
+ * in place.
+ * For data-parallel whitening the phases are exported separately:
+ *   va_gae_scan        -> adv_raw, ret, and the P partial triples at the start of row_partials
+ *                         (a workspace of va_gae_workspace_bytes(B) bytes)
+ *   va_whiten_finalize -> merges K partial triples in a fixed order (Chan), emits the merged
+ *                         fp64 triple and the fp32 stats (call it again on all-gathered triples);
+ *                         for K > 1024 it merges slices of 512 in parallel first, writing each
+ *                         slice's result over the slice's first triple (the partials are scratch)
  *   va_whiten_apply    -> x = (x - mean) * rstd [* mask] in place.
  * ------------------------------------------------------------------------------------ */
 int64_t va_gae_workspace_bytes(int64_t B);
+int64_t va_gae_partial_count(int64_t B);
 int va_gae_scan(const float *rewards, const float *values, const void *mask, int mask_dtype,
                 int64_t B, int64_t R, float gamma, float lam, float *adv_raw, float *ret,
                 double *row_partials, void *stream);
 int va_masked_row_partials(const float *x, const void *mask, int mask_dtype, int64_t B,
                            int64_t R, double *row_partials, void *stream);
-int va_whiten_finalize(const double *partials, int64_t K, double *merged, float *stats_out,
+int va_whiten_finalize(double *partials, int64_t K, double *merged, float *stats_out,
                        void *stream);
 int va_whiten_apply(float *x, const float *stats, const void *mask, int mask_dtype, int64_t B,
                     int64_t R, int post_multiply_mask, void *stream);

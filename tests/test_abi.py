@@ -37,7 +37,14 @@ def test_library_exports_every_header_symbol(lib):
 def test_abi_version_and_workspace_queries(lib):
     assert lib.va_abi_version() == 2
     assert lib.va_ppo_loss_workspace_bytes(10) == 8 * (10 * 8 + 8)
-    assert lib.va_gae_workspace_bytes(7) == 8 * (7 * 3 + 4)
+    assert lib.va_gae_workspace_bytes(7) == 8 * (6 * 7 + 8)
+    assert lib.va_gae_partial_count(7) == 7 and lib.va_gae_partial_count(8192) == 8192
+    try:
+        assert lib.va_set_tuning(L.VA_TUNE_GAE_PARTIALS, 4) == 0
+        assert lib.va_gae_partial_count(7) == 2 and lib.va_gae_partial_count(8192) == 2048
+        assert lib.va_set_tuning(L.VA_TUNE_GAE_PARTIALS, 3) == -1
+    finally:
+        lib.va_set_tuning(L.VA_TUNE_GAE_PARTIALS, 0)
 
 
 def test_argument_validation_without_device(lib):

@@ -443,3 +443,35 @@ def test_apply_kl_penalty(K):
     got_r, row_kl = K.apply_kl_penalty(scores.to(DEV), old.to(DEV), refl.to(DEV), mask.to(DEV), 0.05, "low_var_kl")
     _close(got_r, want_r, atol=1e-6, what="kl rewards")
     assert abs(row_kl.mean().item() - want_kl) < 1e-6
+
+
+@pytest.mark.parametrize("B,R", [(8192, 1024), (5, 1000), (3, 2048), (6, 260)])
+def test_gae_quad_kernel_vs_float64_twin(K, B, R):
+    """The quad-streaming scan (default where R % 4 == 0, R <= 2048) against the fp64 oracle at
+    16x the headline batch and at ragged shapes (R not a multiple of 256, partial workgroups)."""
+    g = torch.Generator().manual_seed(B * 7 + R)
+    rewards = torch.randn(B, R, generator=g) * (torch.rand(B, R, generator=g) > 0.9)
+    values = torch.randn(B, R, generator=g)
+    lens = torch.randint(1, R + 1, (B,), generator=g)
+    mask = (torch.arange(R)[None, :] < lens[:, None]).to(torch.int64)
+    mask[0] = (torch.rand(R, generator=g) > 0.5).long()  # multi-turn holes
+    want_adv, want_ret = ref.compute_gae_advantage_return(rewards.double(), values.double(), mask.double(), 0.99, 0.95)
+    adv, ret = K.gae_advantage_return(rewards.to(DEV), values.to(DEV), mask.to(DEV), 0.99, 0.95)
+    tol = 1e-4 * max(1.0, float(np.sqrt(R) / 8))
+    _close(ret, want_ret, atol=tol, rtol=1e-4, what="gae quad returns")
+    _close(adv, want_adv, atol=tol, rtol=1e-4, what="gae quad advantages")
+
+
+def test_gae_quad_kernel_multi_turn_property(K):
+    """The multi-turn property (values at mask == 0 do not matter, bitwise) on the quad kernel."""
+    g = torch.Generator().manual_seed(3)
+    B, R = 16, 1024
+    rewards = torch.randn(B, R, generator=g) * (torch.rand(B, R, generator=g) > 0.9)
+    mask = (torch.rand(B, R, generator=g) > 0.4).float()
+    v1 = torch.randn(B, R, generator=g)
+    v2 = torch.where(mask > 0, v1, torch.randn(B, R, generator=g) * 100)
+    a1, r1 = K.gae_advantage_return(rewards.to(DEV), v1.to(DEV), mask.to(DEV), 0.97, 0.9)
+    a2, r2 = K.gae_advantage_return(rewards.to(DEV), v2.to(DEV), mask.to(DEV), 0.97, 0.9)
+    m = mask.to(DEV)
+    assert torch.equal(a1, a2)
+    assert torch.equal(r1 * m, r2 * m)

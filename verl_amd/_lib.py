@@ -31,7 +31,8 @@ VA_LOSS_KL, VA_LOSS_ENTROPY, VA_LOSS_NTOKENS, VA_LOSS_NROWS, VA_LOSS_NOUT = 4, 5
 VA_VLOSS_LOSS, VA_VLOSS_CLIPFRAC, VA_VLOSS_VPRED_MEAN, VA_VLOSS_NTOKENS, VA_VLOSS_NOUT = 0, 1, 2, 3, 4
 VA_TUNE_FWD_WAVES_PER_ROW, VA_TUNE_BWD_WAVES_PER_ROW, VA_TUNE_NONTEMPORAL, VA_TUNE_PIPELINE = 1, 2, 3, 4
 VA_TUNE_FLASH_GROUPED_DKDV, VA_TUNE_GAE_VARIANT, VA_TUNE_BWD_FLAT, VA_TUNE_SWIGLU_STREAM = 5, 6, 7, 8
-VA_TUNE_FLASH_DKDV_QT, VA_TUNE_FLASH_DQ_KB, VA_TUNE_FLASH_FWD_KB = 9, 10, 11
+VA_TUNE_FLASH_DKDV_QT, VA_TUNE_FLASH_DQ_KB, VA_TUNE_FLASH_FWD_KB, VA_TUNE_GAE_PARTIALS = 9, 10, 11, 12
+VA_TUNE_GAE_NT = 13
 
 _P = c_void_p
 _SIGNATURES: dict[str, tuple] = {
@@ -69,6 +70,7 @@ _SIGNATURES: dict[str, tuple] = {
     "va_group_coef": (c_int, [_P, _P, _P, _P, c_int64, c_int64, c_float, c_int, _P, _P]),
     "va_broadcast_rows": (c_int, [_P, _P, c_int, c_int64, c_int64, _P, _P]),
     "va_gae_workspace_bytes": (c_int64, [c_int64]),
+    "va_gae_partial_count": (c_int64, [c_int64]),
     "va_gae_scan": (c_int, [_P, _P, _P, c_int, c_int64, c_int64, c_float, c_float, _P, _P, _P, _P]),
     "va_masked_row_partials": (c_int, [_P, _P, c_int, c_int64, c_int64, _P, _P]),
     "va_whiten_finalize": (c_int, [_P, c_int64, _P, _P, _P]),

@@ -25,6 +25,12 @@
 
 #include "va_common.h"
 
+int g_gae_partials = 0;  // va_set_tuning(VA_TUNE_GAE_PARTIALS), see gae_group_rows
+// va_set_tuning(VA_TUNE_GAE_NT): cache policy of the GAE streams, bit 0 = non-temporal loads of
+// r / v, bit 1 = non-temporal store of the returns, bit 2 = non-temporal stores of the raw
+// advantages (re-read by the whitening launch, so cached by default) and of the whitened output
+int g_gae_nt = 3;
+
 namespace va {
 namespace {
 
@@ -453,6 +459,219 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(
   }
 }
 
+// Streaming variant for R % 4 == 0 and R <= 256 * JM (the headline and its 16x batch: R = 1024,
+// J = 4): lane k owns the QUADS of steps t = 256 j + 4 k + {0..3}, j = 0..J-1, so every load and
+// store is a fully coalesced 16-byte vector per lane (a wave moves 1 KB per instruction), all
+// 4 J + 4 J + (1..2) J loads of the row are issued before the first use, and nothing goes
+// through LDS. The scan runs level by level from the last quad row j = J-1 down to 0: each lane
+// composes its quad's affine map, a 6-step wave reverse scan gives every quad its incoming
+// state from the carry (the state after all levels above), the lane re-runs its 4 steps in the
+// reference's op order, and lane 0's inclusive map advances the carry. Row partials (n, sum,
+// M2) in fp64 as the other variants.
+template <int MT, int JM>
+__device__ __forceinline__ Moments gae_row_quads(const float *__restrict__ rew, const float *__restrict__ val,
+                                                 const void *__restrict__ mask, int64_t row, int64_t R, int J,
+                                                 float gamma, float gl, float *__restrict__ adv_raw,
+                                                 float *__restrict__ ret, int nt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t base = row * R;
+  float r[JM][4], v[JM][4], m[JM][4];
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const int64_t t0 = 256 * j + 4 * lane;
+    const bool ok = j < J && t0 < R;
+    const int64_t tc = ok ? t0 : 0;  // clamped address: no branch around the loads
+    const float4 a = ld4(rew + base + tc, nt & 1);
+    const float4 b = ld4(val + base + tc, nt & 1);
+    float mm[4];
+    load_mask4<MT>(mask, base + tc, mm);
+    r[j][0] = ok ? a.x : 0.f, r[j][1] = ok ? a.y : 0.f, r[j][2] = ok ? a.z : 0.f, r[j][3] = ok ? a.w : 0.f;
+    v[j][0] = ok ? b.x : 0.f, v[j][1] = ok ? b.y : 0.f, v[j][2] = ok ? b.z : 0.f, v[j][3] = ok ? b.w : 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m[j][q] = ok ? mm[q] : 0.f;  // a masked-out step is the identity map
+  }
+  float cg = 0.f, cnv = 0.f;  // carry: state after every level above the current one
+#pragma unroll
+  for (int j = JM - 1; j >= 0; --j) {
+    if (j >= J) continue;
+    Aff F{1.f, 0.f, 1.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 3; q >= 0; --q) {
+      Aff st;
+      st.a = m[j][q] * gl + (1.f - m[j][q]);
+      st.c = m[j][q] * gamma;
+      st.e = 1.f - m[j][q];
+      st.b1 = m[j][q] * (r[j][q] - v[j][q]);
+      st.b2 = m[j][q] * v[j][q];
+      F = compose(st, F);
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      Aff nb;
+      nb.a = __shfl_down(F.a, o, kWave);
+      nb.c = __shfl_down(F.c, o, kWave);
+      nb.e = __shfl_down(F.e, o, kWave);
+      nb.b1 = __shfl_down(F.b1, o, kWave);
+      nb.b2 = __shfl_down(F.b2, o, kWave);
+      if (lane + o < 64) F = compose(F, nb);
+    }
+    // incoming state of quad k: the inclusive map of quad k+1 applied to the carry
+    Aff G;
+    G.a = __shfl_down(F.a, 1, kWave);
+    G.c = __shfl_down(F.c, 1, kWave);
+    G.e = __shfl_down(F.e, 1, kWave);
+    G.b1 = __shfl_down(F.b1, 1, kWave);
+    G.b2 = __shfl_down(F.b2, 1, kWave);
+    float g, nv;
+    if (lane == 63) {
+      g = cg;
+      nv = cnv;
+    } else {
+      g = G.a * cg + G.c * cnv + G.b1;
+      nv = G.e * cnv + G.b2;
+    }
+    // next carry: quad 0's inclusive map (the whole level) applied to the carry
+    const float a0 = __shfl(F.a, 0, kWave), c0 = __shfl(F.c, 0, kWave), e0 = __shfl(F.e, 0, kWave);
+    const float b10 = __shfl(F.b1, 0, kWave), b20 = __shfl(F.b2, 0, kWave);
+    const float ncg = a0 * cg + c0 * cnv + b10;
+    cnv = e0 * cnv + b20;
+    cg = ncg;
+    // re-run the quad in the reference op order (core_algos.py:229-236); r <- g
+#pragma unroll
+    for (int q = 3; q >= 0; --q) {
+      const float delta = (r[j][q] + gamma * nv) - v[j][q];
+      const float gnew = delta + gl * g;
+      nv = v[j][q] * m[j][q] + (1.f - m[j][q]) * nv;
+      g = gnew * m[j][q] + (1.f - m[j][q]) * g;
+      r[j][q] = g;
+    }
+  }
+  // stores + row partials (n, sum, M2) of g over the mask
+  double n = 0.0, sum = 0.0;
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const int64_t t0 = 256 * j + 4 * lane;
+    if (j < J && t0 < R) {
+      float4 a, b;
+      a.x = r[j][0], a.y = r[j][1], a.z = r[j][2], a.w = r[j][3];
+      b.x = r[j][0] + v[j][0], b.y = r[j][1] + v[j][1], b.z = r[j][2] + v[j][2], b.w = r[j][3] + v[j][3];
+      st4(adv_raw + base + t0, a, nt & 4);
+      st4(ret + base + t0, b, nt & 2);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        n += m[j][q];
+        sum += static_cast<double>((m[j][q] != 0.f ? r[j][q] : 0.f) * m[j][q]);
+      }
+    }
+  }
+  n = wave_sum(n);
+  sum = wave_sum(sum);
+  const double mu = n > 0.0 ? sum / n : 0.0;
+  double m2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (m[j][q] != 0.f) {
+        const double d = static_cast<double>(r[j][q]) - mu;
+        m2 += static_cast<double>(m[j][q]) * d * d;
+      }
+    }
+  }
+  m2 = wave_sum(m2);
+  return Moments{n, mu, m2};
+}
+
+// Partial triples of the GAE scan: one per group of w rows (w = 1: one per row, written by the
+// row's wave, the default; w = 4 / 8: one per workgroup of w waves, merged in wave order by the
+// last wave to finish). P = ceil(B / w). The consumer merges them in a fixed order (first in
+// parallel slices of 512 when P > 4096). va_set_tuning(VA_TUNE_GAE_PARTIALS, w) picks w
+// (0 = auto).
+int gae_group_rows(int64_t B) {
+  if (g_gae_partials == 1 || g_gae_partials == 4 || g_gae_partials == 8) return g_gae_partials;
+  return 1;  // measured fastest at 512 and 8,192 rows (profiles/r02/gae_partials_ab.txt)
+}
+int64_t gae_partial_count(int64_t B) {
+  const int w = gae_group_rows(B);
+  return (B + w - 1) / w;
+}
+
+// One partial triple per workgroup without a workgroup barrier at the end: each wave leaves its
+// moments in LDS and bumps an LDS counter (workgroup-scope acq_rel: ordering only, no cache
+// maintenance); the wave that arrives last merges the entries in wave order (the same order
+// whichever wave it is) and writes the triple. Waves retire independently, as with per-row
+// partials. `cnt` must be zeroed (and a barrier passed) at kernel start.
+__device__ __forceinline__ void store_wg_moments(Moments acc, double *__restrict__ part, double *sh, int *cnt) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
+  int prev = 0;
+  if (lane == 0) {
+    sh[wave * 3 + 0] = acc.n;
+    sh[wave * 3 + 1] = acc.mean;
+    sh[wave * 3 + 2] = acc.m2;
+    prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  prev = __shfl(prev, 0, kWave);
+  if (prev == waves - 1 && lane == 0) {
+    Moments t{0.0, 0.0, 0.0};
+    for (int w = 0; w < waves; ++w) t = merge_moments(t, Moments{sh[w * 3], sh[w * 3 + 1], sh[w * 3 + 2]});
+    part[blockIdx.x * kPartStride + 0] = t.n;
+    part[blockIdx.x * kPartStride + 1] = t.mean * t.n;
+    part[blockIdx.x * kPartStride + 2] = t.m2;
+  }
+}
+
+template <int MT, int JM, bool WG_MERGE>
+__global__ __launch_bounds__(512) void gae_scan_vec_kernel(
+    const float *__restrict__ rew, const float *__restrict__ val, const void *__restrict__ mask,
+    int64_t B, int64_t R, int J, float gamma, float gl, float *__restrict__ adv_raw,
+    float *__restrict__ ret, double *__restrict__ part, int nt) {
+  const int wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * waves + wave;
+  if constexpr (!WG_MERGE) {
+    if (row >= B) return;  // waves are independent: no workgroup barrier
+    const Moments m = gae_row_quads<MT, JM>(rew, val, mask, row, R, J, gamma, gl, adv_raw, ret, nt);
+    if ((threadIdx.x & 63) == 0) {
+      part[row * kPartStride + 0] = m.n;
+      part[row * kPartStride + 1] = m.mean * m.n;
+      part[row * kPartStride + 2] = m.m2;
+    }
+  } else {
+    __shared__ double sh[8 * 3];
+    __shared__ int cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();  // at kernel start, before any load: costs no overlap
+    Moments acc{0.0, 0.0, 0.0};
+    if (row < B) acc = gae_row_quads<MT, JM>(rew, val, mask, row, R, J, gamma, gl, adv_raw, ret, nt);
+    store_wg_moments(acc, part, sh, &cnt);
+  }
+}
+
+// Group the per-row triples of the fallback scan variants (rows[3 B]) into the same P partials
+// the streaming kernel writes: workgroup g merges rows g w .. g w + w - 1 in order.
+__global__ __launch_bounds__(64) void gae_group_partials_kernel(const double *__restrict__ rows, int64_t B,
+                                                                int w, double *__restrict__ part) {
+  __shared__ double sh[16 * 3];
+  if (threadIdx.x < w) {
+    Moments acc{0.0, 0.0, 0.0};
+    const int64_t row = static_cast<int64_t>(blockIdx.x) * w + threadIdx.x;
+    if (row < B) {
+      const double n = rows[row * kPartStride + 0];
+      acc = Moments{n, n > 0.0 ? rows[row * kPartStride + 1] / n : 0.0, rows[row * kPartStride + 2]};
+    }
+    sh[threadIdx.x * 3 + 0] = acc.n;
+    sh[threadIdx.x * 3 + 1] = acc.mean;
+    sh[threadIdx.x * 3 + 2] = acc.m2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Moments t{0.0, 0.0, 0.0};
+    for (int k = 0; k < w; ++k) t = merge_moments(t, Moments{sh[k * 3], sh[k * 3 + 1], sh[k * 3 + 2]});
+    part[blockIdx.x * kPartStride + 0] = t.n;
+    part[blockIdx.x * kPartStride + 1] = t.mean * t.n;
+    part[blockIdx.x * kPartStride + 2] = t.m2;
+  }
+}
+
 // Per-row (n, sum, M2) of an arbitrary [B, R] matrix (masked_whiten on non-GAE inputs).
 template <int MT>
 __global__ __launch_bounds__(256) void row_partials_kernel(const float *__restrict__ x,
@@ -488,57 +707,138 @@ __global__ __launch_bounds__(256) void row_partials_kernel(const float *__restri
   }
 }
 
-// Merge K (n, sum, M2) triples; emit the merged triple and the fp32 whitening stats
-// {mean, rsqrt(var + 1e-8), n, error_flag} with the reference's formulas. Each thread merges a
-// contiguous slice, then a fixed binary tree in LDS: the merge order depends only on K, so the
-// result is deterministic run to run.
-__global__ __launch_bounds__(256) void whiten_finalize_kernel(const double *__restrict__ part,
-                                                              int64_t K, double *__restrict__ merged,
-                                                              float *__restrict__ stats) {
-  __shared__ double sh[256 * 3];
-  Moments acc{0.0, 0.0, 0.0};
-  const int64_t per = (K + blockDim.x - 1) / blockDim.x;
-  const int64_t lo = threadIdx.x * per, hi = (lo + per < K) ? lo + per : K;
-  for (int64_t k = lo; k < hi; ++k) {
-    const double n = part[k * kPartStride + 0];
-    Moments mk{n, n > 0.0 ? part[k * kPartStride + 1] / n : 0.0, part[k * kPartStride + 2]};
-    acc = merge_moments(acc, mk);
-  }
-  sh[threadIdx.x * 3 + 0] = acc.n;
-  sh[threadIdx.x * 3 + 1] = acc.mean;
-  sh[threadIdx.x * 3 + 2] = acc.m2;
-  __syncthreads();
-  for (unsigned s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      const unsigned a = threadIdx.x, b = threadIdx.x + s;
-      const Moments m = merge_moments(Moments{sh[a * 3], sh[a * 3 + 1], sh[a * 3 + 2]},
-                                      Moments{sh[b * 3], sh[b * 3 + 1], sh[b * 3 + 2]});
-      sh[a * 3] = m.n;
-      sh[a * 3 + 1] = m.mean;
-      sh[a * 3 + 2] = m.m2;
+// Merge the (n, sum, M2) triples k = beg, beg + step, ... < end (triple k at part[3 k]) with one
+// 256-thread workgroup: thread t accumulates its entries t, t + 256, ... in order (the loads of a
+// batch of 8 issued before the first add), then a fixed wave / workgroup sum. The order depends
+// only on (beg, end, step): deterministic.
+constexpr int kMergeThreads = 256;
+constexpr int64_t kMergeSlice = 512;  // triples per first-level workgroup when K is large
+
+__device__ Moments block_merge(const double *__restrict__ part, int64_t beg, int64_t end, int64_t step,
+                               double *sh) {
+  // Shifted sums instead of a Chan tree: with c = the first partial's mean, every partial becomes
+  // (n, S1 = n (mean - c), S2 = M2 + n (mean - c)^2), which merge by plain additions (wave
+  // shuffles, no fp64 divisions, no LDS tree); mean = c + S1 / N, M2 = S2 - S1^2 / N at the end.
+  // c is a data value, so the final subtraction cancels at most a digit or two of fp64.
+  const double n0 = end > beg ? part[beg * kPartStride + 0] : 0.0;
+  const double c = n0 > 0.0 ? part[beg * kPartStride + 1] / n0 : 0.0;
+  double acc[3] = {0.0, 0.0, 0.0};
+  constexpr int kBatch = 8;
+  const int64_t count = end > beg ? (end - beg + step - 1) / step : 0;
+  for (int64_t i0 = 0; i0 < count; i0 += static_cast<int64_t>(kBatch) * kMergeThreads) {
+    double pn[kBatch], ps[kBatch], pm[kBatch];
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+      const int64_t idx = i0 + static_cast<int64_t>(i) * kMergeThreads + threadIdx.x;
+      const bool ok = idx < count;
+      const int64_t k = beg + (ok ? idx : 0) * step;
+      pn[i] = ok ? part[k * kPartStride + 0] : 0.0;
+      ps[i] = ok ? part[k * kPartStride + 1] : 0.0;
+      pm[i] = ok ? part[k * kPartStride + 2] : 0.0;
     }
-    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+      if (pn[i] > 0.0) {
+        const double d = ps[i] / pn[i] - c;
+        acc[0] += pn[i];
+        acc[1] += pn[i] * d;
+        acc[2] += pm[i] + pn[i] * d * d;
+      }
+    }
   }
-  if (threadIdx.x == 0) {
-    const Moments tot{sh[0], sh[1], sh[2]};
-    const double n = tot.n;
+  block_sum<3>(acc, sh);
+  const double N = acc[0];
+  if (N <= 0.0) return Moments{0.0, 0.0, 0.0};
+  return Moments{N, c + acc[1] / N, acc[2] - acc[1] * acc[1] / N};
+}
+
+__device__ __forceinline__ void whiten_stats_of(Moments tot, double *merged, float *stats, float &mean_out,
+                                                float &rstd_out) {
+  const double n = tot.n;
+  const double mean = (tot.mean * n) / (n + 1e-8);  // torch_functional.py:171-185, 188-223
+  const double dm = tot.mean - mean;
+  const double var_b = (tot.m2 + n * dm * dm) / (n + 1e-8);
+  float flag = 0.f;
+  double var = var_b;
+  if (n == 0.0) flag = 1.f;
+  else if (n == 1.0) flag = 2.f;
+  else var = var_b * (n / (n - 1.0));
+  const float var32 = static_cast<float>(var);
+  mean_out = static_cast<float>(mean);
+  rstd_out = 1.0f / sqrtf(var32 + 1e-8f);
+  if (merged != nullptr) {
     merged[0] = n;
     merged[1] = tot.mean * n;
     merged[2] = tot.m2;
-    // torch_functional.py:171-185, 188-223
-    const double mean = (tot.mean * n) / (n + 1e-8);
-    const double dm = tot.mean - mean;
-    const double var_b = (tot.m2 + n * dm * dm) / (n + 1e-8);
-    float flag = 0.f;
-    double var = var_b;
-    if (n == 0.0) flag = 1.f;
-    else if (n == 1.0) flag = 2.f;
-    else var = var_b * (n / (n - 1.0));
-    const float var32 = static_cast<float>(var);
-    stats[0] = static_cast<float>(mean);
-    stats[1] = 1.0f / sqrtf(var32 + 1e-8f);
+    stats[0] = mean_out;
+    stats[1] = rstd_out;
     stats[2] = static_cast<float>(n);
     stats[3] = flag;
+  }
+}
+
+// First level for large K: workgroup g merges the slice [g S, (g + 1) S) and writes the result
+// over the slice's first triple (no other workgroup reads that slot).
+__global__ __launch_bounds__(kMergeThreads) void whiten_merge_slices_kernel(double *__restrict__ part, int64_t K) {
+  __shared__ double sh[kMergeThreads * 3];
+  const int64_t beg = static_cast<int64_t>(blockIdx.x) * kMergeSlice;
+  const int64_t end = beg + kMergeSlice < K ? beg + kMergeSlice : K;
+  const Moments m = block_merge(part, beg, end, 1, sh);
+  if (threadIdx.x == 0) {
+    part[beg * kPartStride + 0] = m.n;
+    part[beg * kPartStride + 1] = m.mean * m.n;
+    part[beg * kPartStride + 2] = m.m2;
+  }
+}
+
+// Merge the triples 0, step, 2 step, ... < K; emit the merged triple and the fp32 whitening stats
+// {mean, rsqrt(var + 1e-8), n, error_flag} with the reference's formulas.
+__global__ __launch_bounds__(kMergeThreads) void whiten_finalize_kernel(const double *__restrict__ part,
+                                                                        int64_t K, int64_t step,
+                                                                        double *__restrict__ merged,
+                                                                        float *__restrict__ stats) {
+  __shared__ double sh[kMergeThreads * 3];
+  const Moments tot = block_merge(part, 0, K, step, sh);
+  if (threadIdx.x == 0) {
+    float mean, rstd;
+    whiten_stats_of(tot, merged, stats, mean, rstd);
+  }
+}
+
+// whiten_finalize + whiten_apply in one launch: every workgroup merges the K (<= a few hundred)
+// partial triples itself, in the same fixed order, so all of them apply identical statistics
+// (workgroup 0 also writes the merged triple and the stats for the caller's error check), then
+// streams its share of x = (x - mean) * rstd with 16-byte vectors.
+__global__ __launch_bounds__(kMergeThreads) void whiten_stats_apply_kernel(float *__restrict__ x,
+                                                                           const double *__restrict__ part,
+                                                                           int64_t K, int64_t step,
+                                                                           double *__restrict__ merged,
+                                                                           float *__restrict__ stats, int64_t nq,
+                                                                           int nt) {
+  __shared__ double sh[kMergeThreads * 3];
+  const Moments tot = block_merge(part, 0, K, step, sh);
+  float mean, rstd;
+  const bool writer = blockIdx.x == 0 && threadIdx.x == 0;
+  whiten_stats_of(tot, writer ? merged : nullptr, stats, mean, rstd);
+  // chunks of U quads per thread, all U loads issued before the first store
+  constexpr int U = 8;
+  const int64_t chunk = static_cast<int64_t>(blockDim.x) * U;
+  for (int64_t c0 = static_cast<int64_t>(blockIdx.x) * chunk; c0 < nq; c0 += static_cast<int64_t>(gridDim.x) * chunk) {
+    float4 a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = c0 + static_cast<int64_t>(u) * blockDim.x + threadIdx.x;
+      if (i < nq) a[u] = ld4(x + 4 * i, false);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = c0 + static_cast<int64_t>(u) * blockDim.x + threadIdx.x;
+      if (i < nq) {
+        float4 v = a[u];
+        v.x = (v.x - mean) * rstd, v.y = (v.y - mean) * rstd, v.z = (v.z - mean) * rstd, v.w = (v.w - mean) * rstd;
+        st4(x + 4 * i, v, nt & 4);
+      }
+    }
   }
 }
 
@@ -553,6 +853,42 @@ __global__ __launch_bounds__(256) void whiten_apply_kernel(float *__restrict__ x
     float v = (x[i] - mean) * rstd;
     if constexpr (POSTMASK) v = v * load_mask<MT>(mask, i);
     x[i] = v;
+  }
+}
+
+// The same with 16-byte vectors (n % 4 == 0, x 16-byte aligned): two quads per lane in flight.
+template <int MT, bool POSTMASK>
+__global__ __launch_bounds__(256) void whiten_apply_vec_kernel(float *__restrict__ x,
+                                                               const float *__restrict__ stats,
+                                                               const void *__restrict__ mask,
+                                                               int64_t nq) {
+  const float mean = stats[0], rstd = stats[1];
+  float4 *x4 = reinterpret_cast<float4 *>(x);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + stride < nq; i += 2 * stride) {
+    float4 a = x4[i], b = x4[i + stride];
+    a.x = (a.x - mean) * rstd, a.y = (a.y - mean) * rstd, a.z = (a.z - mean) * rstd, a.w = (a.w - mean) * rstd;
+    b.x = (b.x - mean) * rstd, b.y = (b.y - mean) * rstd, b.z = (b.z - mean) * rstd, b.w = (b.w - mean) * rstd;
+    if constexpr (POSTMASK) {
+      float ma[4], mb[4];
+      load_mask4<MT>(mask, 4 * i, ma);
+      load_mask4<MT>(mask, 4 * (i + stride), mb);
+      a.x *= ma[0], a.y *= ma[1], a.z *= ma[2], a.w *= ma[3];
+      b.x *= mb[0], b.y *= mb[1], b.z *= mb[2], b.w *= mb[3];
+    }
+    x4[i] = a;
+    x4[i + stride] = b;
+  }
+  for (; i < nq; i += stride) {
+    float4 a = x4[i];
+    a.x = (a.x - mean) * rstd, a.y = (a.y - mean) * rstd, a.z = (a.z - mean) * rstd, a.w = (a.w - mean) * rstd;
+    if constexpr (POSTMASK) {
+      float ma[4];
+      load_mask4<MT>(mask, 4 * i, ma);
+      a.x *= ma[0], a.y *= ma[1], a.z *= ma[2], a.w *= ma[3];
+    }
+    x4[i] = a;
   }
 }
 
@@ -707,11 +1043,14 @@ extern "C" int va_outcome_advantage(const float *rewards, const void *mask, int 
   return va_broadcast_rows(coef, mask, mask_dtype, B, R, adv, stream);
 }
 
+// workspace layout (doubles): [P <= B partial triples | B per-row triples (fallback variants) | merged 3 | pad]
 extern "C" int64_t va_gae_workspace_bytes(int64_t B) {
-  return static_cast<int64_t>(sizeof(double)) * (B * kPartStride + 4);
+  return static_cast<int64_t>(sizeof(double)) * (2 * B * kPartStride + 8);
 }
+extern "C" int64_t va_gae_partial_count(int64_t B) { return B > 0 ? gae_partial_count(B) : 0; }
 
-// va_set_tuning(VA_TUNE_GAE_VARIANT): 0 auto, 1 register kernel (only where L <= 16), 2 LDS kernel
+// va_set_tuning(VA_TUNE_GAE_VARIANT): 0 auto (quad-streaming kernel where it applies), 1 register
+// kernel (only where L <= 16), 2 LDS kernel, 3 quad-streaming kernel
 int g_gae_variant = 0;
 
 extern "C" int va_gae_scan(const float *rewards, const float *values, const void *mask,
@@ -727,19 +1066,58 @@ extern "C" int va_gae_scan(const float *rewards, const float *values, const void
   // register chunks for short rows of small batches (latency: one round trip, no LDS); many rows
   // stream better through the coalesced LDS staging (lane-chunk loads touch 64 lines per
   // instruction)
+  // streaming quad variant: 16-byte coalesced loads / stores straight to registers (default
+  // wherever it applies: R % 4 == 0, R <= 2048, 16-byte aligned rows)
+  const bool aligned = ((reinterpret_cast<uintptr_t>(rewards) | reinterpret_cast<uintptr_t>(values) |
+                         reinterpret_cast<uintptr_t>(adv_raw) | reinterpret_cast<uintptr_t>(ret)) & 15) == 0 &&
+                       (reinterpret_cast<uintptr_t>(mask) & 15) == 0;
+  if ((g_gae_variant == 0 || g_gae_variant == 3) && (R & 3) == 0 && R <= 2048 && aligned) {
+    const int J = static_cast<int>((R + 255) / 256);
+    const int w = gae_group_rows(B);
+    const dim3 block(w == 8 ? 512 : 256), grid(static_cast<unsigned>(w == 1 ? (B + 3) / 4 : gae_partial_count(B)));
+#define VA_GAE_VEC(JMV)                                                                                     \
+  do {                                                                                                      \
+    if (w == 1)                                                                                             \
+      hipLaunchKernelGGL((gae_scan_vec_kernel<MT, JMV, false>), grid, block, 0, s, rewards, values, mask, B, \
+                         R, J, gamma, gl, adv_raw, ret, row_partials, g_gae_nt);                            \
+    else                                                                                                    \
+      hipLaunchKernelGGL((gae_scan_vec_kernel<MT, JMV, true>), grid, block, 0, s, rewards, values, mask, B,  \
+                         R, J, gamma, gl, adv_raw, ret, row_partials, g_gae_nt);                            \
+  } while (0)
+    VA_DISPATCH_MASK(mask_dtype, {
+      if (J <= 1) VA_GAE_VEC(1);
+      else if (J <= 2) VA_GAE_VEC(2);
+      else if (J <= 4) VA_GAE_VEC(4);
+      else VA_GAE_VEC(8);
+    });
+#undef VA_GAE_VEC
+    return check_launch("gae_scan");
+  }
+  // fallback variants: per-row triples (directly the partials when w == 1, else in the scratch half
+  // of the workspace, then grouped)
+  const int64_t P = gae_partial_count(B);
+  const int wg = gae_group_rows(B);
+  double *rows = wg == 1 ? row_partials : row_partials + B * kPartStride;
+  auto group_rows = [&]() -> int {
+    if (int e = check_launch("gae_scan")) return e;
+    if (wg == 1) return VA_OK;
+    hipLaunchKernelGGL(gae_group_partials_kernel, dim3(static_cast<unsigned>(P)), dim3(64), 0, s, rows, B, wg,
+                       row_partials);
+    return check_launch("gae_group_partials");
+  };
   const bool reg = L <= 16 && (g_gae_variant == 1 || (g_gae_variant == 0 && B * R <= (1LL << 20)));
   if (reg) {
     const dim3 block(256), grid(static_cast<unsigned>((B + 3) / 4));
 #define VA_GAE_REG(LMV)                                                                              \
   hipLaunchKernelGGL((gae_scan_reg_kernel<MT, LMV>), grid, block, 0, s, rewards, values, mask, B, R, L, \
-                     gamma, gl, adv_raw, ret, row_partials)
+                     gamma, gl, adv_raw, ret, rows)
     VA_DISPATCH_MASK(mask_dtype, {
       if (L <= 4) VA_GAE_REG(4);
       else if (L <= 8) VA_GAE_REG(8);
       else VA_GAE_REG(16);
     });
 #undef VA_GAE_REG
-    return check_launch("gae_scan");
+    return group_rows();
   }
   int waves = 4;
   while (waves > 1 && gae_lds_bytes(L, waves) > 160 * 1024) waves >>= 1;
@@ -756,15 +1134,15 @@ extern "C" int va_gae_scan(const float *rewards, const float *values, const void
         return VA_E_LAUNCH;
       }
       hipLaunchKernelGGL((gae_scan_kernel<MT, true>), grid, block, shm, s, rewards, values, mask,
-                         B, R, L, gamma, gl, adv_raw, ret, row_partials);
+                         B, R, L, gamma, gl, adv_raw, ret, rows);
     });
   } else {
     VA_DISPATCH_MASK(mask_dtype, {
       hipLaunchKernelGGL((gae_scan_kernel<MT, false>), grid, block, 0, s, rewards, values, mask,
-                         B, R, L, gamma, gl, adv_raw, ret, row_partials);
+                         B, R, L, gamma, gl, adv_raw, ret, rows);
     });
   }
-  return check_launch("gae_scan");
+  return group_rows();
 }
 
 extern "C" int va_masked_row_partials(const float *x, const void *mask, int mask_dtype,
@@ -779,13 +1157,22 @@ extern "C" int va_masked_row_partials(const float *x, const void *mask, int mask
   return check_launch("masked_row_partials");
 }
 
-extern "C" int va_whiten_finalize(const double *partials, int64_t K, double *merged,
+extern "C" int va_whiten_finalize(double *partials, int64_t K, double *merged,
                                   float *stats_out, void *stream) {
   VA_CHECK_ARG(K > 0, "K must be > 0");
   VA_CHECK_ARG(partials && merged && stats_out, "null pointer argument");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(whiten_finalize_kernel, dim3(1), dim3(256), 0, s, partials, K, merged,
-                     stats_out);
+  if (K > 2 * kMergeSlice) {
+    // two levels: slices of kMergeSlice triples merged in parallel (in place), then their results
+    const int64_t G = (K + kMergeSlice - 1) / kMergeSlice;
+    hipLaunchKernelGGL(whiten_merge_slices_kernel, dim3(static_cast<unsigned>(G)), dim3(kMergeThreads), 0, s,
+                       partials, K);
+    hipLaunchKernelGGL(whiten_finalize_kernel, dim3(1), dim3(kMergeThreads), 0, s, partials, K, kMergeSlice,
+                       merged, stats_out);
+  } else {
+    hipLaunchKernelGGL(whiten_finalize_kernel, dim3(1), dim3(kMergeThreads), 0, s, partials, K, int64_t(1),
+                       merged, stats_out);
+  }
   return check_launch("whiten_finalize");
 }
 
@@ -796,6 +1183,23 @@ extern "C" int va_whiten_apply(float *x, const float *stats, const void *mask, i
   VA_CHECK_ARG(!post_multiply_mask || mask != nullptr, "mask required for post multiply");
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t n = B * R;
+  const bool vec = (n & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                   (!post_multiply_mask || (reinterpret_cast<uintptr_t>(mask) & 15) == 0);
+  if (vec) {
+    const int64_t nq = n >> 2;
+    int64_t grid = (nq + 511) / 512;  // two quads per lane
+    if (grid > 8192) grid = 8192;
+    if (grid < 1) grid = 1;
+    if (post_multiply_mask) {
+      VA_DISPATCH_MASK(mask_dtype, {
+        hipLaunchKernelGGL((whiten_apply_vec_kernel<MT, true>), dim3(grid), dim3(256), 0, s, x, stats, mask, nq);
+      });
+    } else {
+      hipLaunchKernelGGL((whiten_apply_vec_kernel<VA_MASK_F32, false>), dim3(grid), dim3(256), 0, s, x, stats,
+                         nullptr, nq);
+    }
+    return check_launch("whiten_apply");
+  }
   int64_t grid = (n + 255) / 256;
   if (grid > 8192) grid = 8192;
   if (post_multiply_mask) {
@@ -819,7 +1223,29 @@ extern "C" int va_gae_advantage_return(const float *rewards, const float *values
   int e = va_gae_scan(rewards, values, mask, mask_dtype, B, R, gamma, lam, adv, ret, part,
                       stream);
   if (e) return e;
-  e = va_whiten_finalize(part, B, part + B * kPartStride, stats_out, stream);
+  int64_t P = gae_partial_count(B);
+  double *merged = part + 2 * B * kPartStride;
+  const int64_t n = B * R;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(adv) & 15) == 0) {
+    // statistics + whitening in one launch (every workgroup merges the partials itself); many
+    // partials are first merged in parallel slices of kMergeSlice (in place)
+    int64_t step = 1;
+    if (P > 8 * kMergeSlice) {
+      const int64_t G = (P + kMergeSlice - 1) / kMergeSlice;
+      hipLaunchKernelGGL(whiten_merge_slices_kernel, dim3(static_cast<unsigned>(G)), dim3(kMergeThreads), 0, s,
+                         part, P);
+      step = kMergeSlice;
+    }
+    const int64_t nq = n >> 2;
+    int64_t grid = (nq + 8 * kMergeThreads - 1) / (8 * kMergeThreads);  // 8 quads per lane
+    if (grid > 2048) grid = 2048;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(whiten_stats_apply_kernel, dim3(static_cast<unsigned>(grid)), dim3(kMergeThreads), 0, s, adv,
+                       part, P, step, merged, stats_out, nq, g_gae_nt);
+    return check_launch("whiten_stats_apply");
+  }
+  e = va_whiten_finalize(part, P, merged, stats_out, stream);
   if (e) return e;
   return va_whiten_apply(adv, stats_out, mask, mask_dtype, B, R, 0, stream);
 }

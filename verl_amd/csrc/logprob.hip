@@ -709,6 +709,8 @@ extern "C" int va_logprob_entropy_bwd(const float *g_logp, const float *g_entrop
 
 extern int g_flash_grouped_dkdv;  // attention.hip
 extern int g_gae_variant;         // advantage.hip
+extern int g_gae_partials;        // advantage.hip
+extern int g_gae_nt;              // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
 extern int g_flash_dkdv_qt;       // attention.hip
 extern int g_flash_dq_kb;         // attention.hip
@@ -722,6 +724,14 @@ extern "C" int va_set_tuning(int key, int value) {
     case VA_TUNE_PIPELINE: va::g_pipe = value; return VA_OK;
     case VA_TUNE_FLASH_GROUPED_DKDV: g_flash_grouped_dkdv = value; return VA_OK;
     case VA_TUNE_GAE_VARIANT: g_gae_variant = value; return VA_OK;
+    case VA_TUNE_GAE_PARTIALS:
+      if (value != 0 && value != 1 && value != 4 && value != 8) {
+        va::set_error("VA_TUNE_GAE_PARTIALS must be 0, 1, 4 or 8 (got %d)", value);
+        return VA_E_ARG;
+      }
+      g_gae_partials = value;
+      return VA_OK;
+    case VA_TUNE_GAE_NT: g_gae_nt = value & 7; return VA_OK;
     case VA_TUNE_BWD_FLAT: va::g_bwd_flat = value; return VA_OK;
     case VA_TUNE_SWIGLU_STREAM: g_swiglu_variant = value; return VA_OK;
     case VA_TUNE_FLASH_DKDV_QT:

@@ -198,24 +198,6 @@ __device__ __forceinline__ float agg_weight(int agg, float g, float m, double n_
   }
 }
 
-// value of an aggregated loss from the row partials in slot q
-__device__ double agg_value(int agg, const double *part, int q, int64_t B, int64_t R,
-                            double n_tot, double *scratch) {
-  double acc[1] = {0.0};
-  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
-    const double s = part[b * kNQ + q];
-    if (agg == VA_AGG_SEQ_MEAN_TOKEN_MEAN) acc[0] += s / part[b * kNQ + 0];
-    else acc[0] += s;
-  }
-  block_sum<1>(acc, scratch);
-  switch (agg) {
-    case VA_AGG_TOKEN_MEAN: return acc[0] / (n_tot + 1e-8);
-    case VA_AGG_SEQ_MEAN_TOKEN_SUM: return acc[0] / static_cast<double>(B);
-    case VA_AGG_SEQ_MEAN_TOKEN_MEAN: return acc[0] / static_cast<double>(B);
-    default: return acc[0] / static_cast<double>(R);
-  }
-}
-
 // ------------------------------------------------------------------ policy loss forward
 template <int MT, int KL>
 __global__ __launch_bounds__(256) void ppo_loss_rows_kernel(
@@ -228,6 +210,7 @@ __global__ __launch_bounds__(256) void ppo_loss_rows_kernel(
   const int64_t base = b * R;
   const bool tok = (agg == VA_AGG_TOKEN_MEAN);
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 4
   for (int64_t t = threadIdx.x; t < R; t += blockDim.x) {
     const int64_t i = base + t;
     const float m = load_mask<MT>(mask, i);
@@ -253,32 +236,63 @@ __global__ __launch_bounds__(256) void ppo_loss_rows_kernel(
   if (threadIdx.x < 7) part[b * kNQ + threadIdx.x] = v[threadIdx.x];
 }
 
+// Row partial slots q of one row, with the seq-mean-token-mean division applied where it is the
+// aggregated quantity (agg_value's per-row term).
+__device__ __forceinline__ double agg_term(int agg, double s, double n_b) {
+  return agg == VA_AGG_SEQ_MEAN_TOKEN_MEAN ? s / n_b : s;
+}
+__device__ __forceinline__ double agg_finish(int agg, double acc, double n_tot, int64_t B, int64_t R) {
+  switch (agg) {
+    case VA_AGG_TOKEN_MEAN: return acc / (n_tot + 1e-8);
+    case VA_AGG_SEQ_MEAN_TOKEN_SUM: return acc / static_cast<double>(B);
+    case VA_AGG_SEQ_MEAN_TOKEN_MEAN: return acc / static_cast<double>(B);
+    default: return acc / static_cast<double>(R);
+  }
+}
+
+// One pass over the [B, 8] row partials: each thread loads its rows' 7 slots (all loads of a
+// batch of 4 rows issued before the adds), one block reduction of the 7 sums.
 __global__ __launch_bounds__(256) void ppo_loss_finalize_kernel(const double *__restrict__ part,
                                                                 int64_t B, int64_t R, int agg,
                                                                 int has_kl, int has_ent,
                                                                 double *__restrict__ totals,
                                                                 float *__restrict__ out) {
-  __shared__ double scratch[4 * 5];
-  double v[5] = {0, 0, 0, 0, 0};  // n, clip, negkl, lower, (unused)
-  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
-    v[0] += part[b * kNQ + 0];
-    v[1] += part[b * kNQ + 2];
-    v[2] += part[b * kNQ + 3];
-    v[3] += part[b * kNQ + 4];
+  __shared__ double scratch[4 * 7];
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};  // n, clip, negkl, lower, pg, kl, ent
+  constexpr int kBatch = 4;
+  for (int64_t b0 = 0; b0 < B; b0 += static_cast<int64_t>(kBatch) * blockDim.x) {
+    double p[kBatch][7];
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+      const int64_t b = b0 + static_cast<int64_t>(i) * blockDim.x + threadIdx.x;
+      const bool ok = b < B;
+      const double *row = part + (ok ? b : 0) * kNQ;
+#pragma unroll
+      for (int q = 0; q < 7; ++q) p[i][q] = ok ? row[q] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+      const int64_t b = b0 + static_cast<int64_t>(i) * blockDim.x + threadIdx.x;
+      if (b >= B) continue;
+      v[0] += p[i][0];
+      v[1] += p[i][2];
+      v[2] += p[i][3];
+      v[3] += p[i][4];
+      v[4] += agg_term(agg, p[i][1], p[i][0]);
+      v[5] += agg_term(agg, p[i][5], p[i][0]);
+      v[6] += agg_term(agg, p[i][6], p[i][0]);
+    }
   }
-  block_sum<5>(v, scratch);
-  const double n = v[0];
-  const double pg = agg_value(agg, part, 1, B, R, n, scratch);
-  const double kl = has_kl ? agg_value(agg, part, 5, B, R, n, scratch) : 0.0;
-  const double en = has_ent ? agg_value(agg, part, 6, B, R, n, scratch) : 0.0;
+  block_sum<7>(v, scratch);
   if (threadIdx.x == 0) {
+    const double n = v[0];
     const double den = n + 1e-8;
-    out[VA_LOSS_PG] = static_cast<float>(pg);
+    out[VA_LOSS_PG] = static_cast<float>(agg_finish(agg, v[4], n, B, R));
     out[VA_LOSS_CLIPFRAC] = static_cast<float>(v[1] / den);
     out[VA_LOSS_PPO_KL] = static_cast<float>(v[2] / den);
     out[VA_LOSS_CLIPFRAC_LOWER] = static_cast<float>(v[3] / den);
-    out[VA_LOSS_KL] = static_cast<float>(kl);
-    out[VA_LOSS_ENTROPY] = static_cast<float>(en);
+    out[VA_LOSS_KL] = has_kl ? static_cast<float>(agg_finish(agg, v[5], n, B, R)) : 0.f;
+    out[VA_LOSS_ENTROPY] = has_ent ? static_cast<float>(agg_finish(agg, v[6], n, B, R)) : 0.f;
     out[VA_LOSS_NTOKENS] = static_cast<float>(n);
     out[VA_LOSS_NROWS] = static_cast<float>(B);
     totals[0] = n;
@@ -327,6 +341,7 @@ __global__ __launch_bounds__(256) void masked_rows_kernel(const float *__restric
   __shared__ double scratch[4 * 3];
   const int64_t b = blockIdx.x;
   double v[3] = {0, 0, 0};  // n, where-sum, mul-sum
+#pragma unroll 4
   for (int64_t t = threadIdx.x; t < R; t += blockDim.x) {
     const int64_t i = b * R + t;
     const float m = load_mask<MT>(mask, i);
@@ -355,17 +370,29 @@ __global__ __launch_bounds__(256) void masked_agg_finalize_kernel(const double *
       out[b] = static_cast<float>(part[b * kNQ + 1] / (part[b * kNQ + 0] + 1e-8));
     return;
   }
-  double v[2] = {0, 0};
-  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
-    v[0] += part[b * kNQ + 0];
-    v[1] += part[b * kNQ + 1];
+  double v[2] = {0, 0};  // n, aggregated sum
+  constexpr int kBatch = 4;
+  const int term_agg = agg == VA_REDUCE_MASKED_SUM ? VA_AGG_TOKEN_MEAN : agg;
+  for (int64_t b0 = 0; b0 < B; b0 += static_cast<int64_t>(kBatch) * blockDim.x) {
+    double pn[kBatch], ps[kBatch];
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+      const int64_t b = b0 + static_cast<int64_t>(i) * blockDim.x + threadIdx.x;
+      const bool ok = b < B;
+      pn[i] = ok ? part[b * kNQ + 0] : 0.0;
+      ps[i] = ok ? part[b * kNQ + 1] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+      const int64_t b = b0 + static_cast<int64_t>(i) * blockDim.x + threadIdx.x;
+      if (b >= B) continue;
+      v[0] += pn[i];
+      v[1] += agg_term(term_agg, ps[i], pn[i]);
+    }
   }
   block_sum<2>(v, scratch);
-  double r;
-  if (agg == VA_REDUCE_MASKED_SUM) r = v[1];
-  else r = agg_value(agg, part, 1, B, R, v[0], scratch);
   if (threadIdx.x == 0) {
-    out[0] = static_cast<float>(r);
+    out[0] = static_cast<float>(agg == VA_REDUCE_MASKED_SUM ? v[1] : agg_finish(agg, v[1], v[0], B, R));
     totals[0] = v[0];
   }
 }
@@ -425,6 +452,7 @@ __global__ __launch_bounds__(256) void apply_kl_penalty_kernel(
   __shared__ double scratch[4 * 2];
   const int64_t b = blockIdx.x;
   double v[2] = {0, 0};
+#pragma unroll 4
   for (int64_t t = threadIdx.x; t < R; t += blockDim.x) {
     const int64_t i = b * R + t;
     const float m = load_mask<MT>(mask, i);
@@ -481,6 +509,7 @@ __global__ __launch_bounds__(256) void value_loss_rows_kernel(
   const int64_t b = blockIdx.x;
   const bool tok = (agg == VA_AGG_TOKEN_MEAN);
   double v[4] = {0, 0, 0, 0};  // n, loss, clip, vpred
+#pragma unroll 4
   for (int64_t t = threadIdx.x; t < R; t += blockDim.x) {
     const int64_t i = b * R + t;
     const float m = load_mask<MT>(mask, i);
@@ -499,19 +528,34 @@ __global__ __launch_bounds__(256) void value_loss_finalize_kernel(const double *
                                                                   int64_t B, int64_t R, int agg,
                                                                   double *__restrict__ totals,
                                                                   float *__restrict__ out) {
-  __shared__ double scratch[4 * 3];
-  double v[3] = {0, 0, 0};
-  for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
-    v[0] += part[b * kNQ + 0];
-    v[1] += part[b * kNQ + 2];
-    v[2] += part[b * kNQ + 3];
+  __shared__ double scratch[4 * 4];
+  double v[4] = {0, 0, 0, 0};  // n, clip, vpred, loss
+  constexpr int kBatch = 4;
+  for (int64_t b0 = 0; b0 < B; b0 += static_cast<int64_t>(kBatch) * blockDim.x) {
+    double p[kBatch][4];
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+      const int64_t b = b0 + static_cast<int64_t>(i) * blockDim.x + threadIdx.x;
+      const bool ok = b < B;
+      const double *row = part + (ok ? b : 0) * kNQ;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) p[i][q] = ok ? row[q] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+      const int64_t b = b0 + static_cast<int64_t>(i) * blockDim.x + threadIdx.x;
+      if (b >= B) continue;
+      v[0] += p[i][0];
+      v[1] += p[i][2];
+      v[2] += p[i][3];
+      v[3] += agg_term(agg, p[i][1], p[i][0]);
+    }
   }
-  block_sum<3>(v, scratch);
-  const double n = v[0];
-  const double loss = agg_value(agg, part, 1, B, R, n, scratch);
+  block_sum<4>(v, scratch);
   if (threadIdx.x == 0) {
+    const double n = v[0];
     const double den = n + 1e-8;
-    out[VA_VLOSS_LOSS] = 0.5f * static_cast<float>(loss);
+    out[VA_VLOSS_LOSS] = 0.5f * static_cast<float>(agg_finish(agg, v[3], n, B, R));
     out[VA_VLOSS_CLIPFRAC] = static_cast<float>(v[1] / den);
     out[VA_VLOSS_VPRED_MEAN] = static_cast<float>(v[2] / den);
     out[VA_VLOSS_NTOKENS] = static_cast<float>(n);

@@ -50,6 +50,42 @@ __device__ __forceinline__ float load_mask(const void *p, int64_t i) {
   else return static_cast<float>(static_cast<const uint8_t *>(p)[i]);
 }
 
+// 16-byte fp32 vector access with an optional non-temporal (streaming) hint.
+typedef float va_f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld4(const float *p, bool nt) {
+  const va_f32x4 v = nt ? __builtin_nontemporal_load(reinterpret_cast<const va_f32x4 *>(p))
+                        : *reinterpret_cast<const va_f32x4 *>(p);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st4(float *p, float4 v, bool nt) {
+  const va_f32x4 w{v.x, v.y, v.z, v.w};
+  if (nt) __builtin_nontemporal_store(w, reinterpret_cast<va_f32x4 *>(p));
+  else *reinterpret_cast<va_f32x4 *>(p) = w;
+}
+
+// Four consecutive mask elements starting at i (i % 4 == 0, base 16-byte aligned): one 16-byte
+// load for f32 / i32, two for i64, one 4-byte load for u8.
+template <int MT>
+__device__ __forceinline__ void load_mask4(const void *p, int64_t i, float (&o)[4]) {
+  if constexpr (MT == VA_MASK_F32) {
+    const float4 q = *reinterpret_cast<const float4 *>(static_cast<const float *>(p) + i);
+    o[0] = q.x, o[1] = q.y, o[2] = q.z, o[3] = q.w;
+  } else if constexpr (MT == VA_MASK_I64) {
+    const longlong2 *q = reinterpret_cast<const longlong2 *>(static_cast<const int64_t *>(p) + i);
+    const longlong2 a = q[0], b = q[1];
+    o[0] = static_cast<float>(a.x), o[1] = static_cast<float>(a.y);
+    o[2] = static_cast<float>(b.x), o[3] = static_cast<float>(b.y);
+  } else if constexpr (MT == VA_MASK_I32) {
+    const int4 q = *reinterpret_cast<const int4 *>(static_cast<const int32_t *>(p) + i);
+    o[0] = static_cast<float>(q.x), o[1] = static_cast<float>(q.y);
+    o[2] = static_cast<float>(q.z), o[3] = static_cast<float>(q.w);
+  } else {
+    const uint32_t w = *reinterpret_cast<const uint32_t *>(static_cast<const uint8_t *>(p) + i);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = static_cast<float>((w >> (8 * q)) & 0xffu);
+  }
+}
+
 // ---------------------------------------------------------------- wave / block reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -391,14 +391,19 @@ def _(coef, mask):
 
 
 # =============================================================================== GAE + whitening
+def _gae_ws_doubles(B: int) -> int:
+    return 6 * B + 8  # va_gae_workspace_bytes(B) / 8
+
+
 @_op("gae_scan")
 def gae_scan(rewards: Tensor, values: Tensor, mask: Tensor, gamma: float, lam: float) -> tuple[Tensor, Tensor, Tensor]:
-    """(raw advantages, returns, row partials fp64 [B*3 + 3]) — whitening not applied."""
+    """(raw advantages, returns, workspace fp64 whose first va_gae_partial_count(B) triples are the
+    partial (n, sum, M2) of the rows) — whitening not applied."""
     _check_f32(rewards, values)
     B, R = rewards.shape
     adv = torch.empty_like(rewards)
     ret = torch.empty_like(rewards)
-    part = torch.zeros(B * 3 + 3, dtype=_F64, device=rewards.device)
+    part = torch.zeros(_gae_ws_doubles(B), dtype=_F64, device=rewards.device)
     L.call("va_gae_scan", K._p(rewards), K._p(values), K._p(mask), _mcode(mask), B, R, gamma, lam, K._p(adv),
            K._p(ret), K._p(part), K._stream(rewards))
     return adv, ret, part
@@ -407,7 +412,7 @@ def gae_scan(rewards: Tensor, values: Tensor, mask: Tensor, gamma: float, lam: f
 @gae_scan.register_fake
 def _(rewards, values, mask, gamma, lam):
     B = rewards.shape[0]
-    return torch.empty_like(rewards), torch.empty_like(rewards), rewards.new_empty(B * 3 + 3, dtype=_F64)
+    return torch.empty_like(rewards), torch.empty_like(rewards), rewards.new_empty(_gae_ws_doubles(B), dtype=_F64)
 
 
 @_op("masked_row_partials")
@@ -428,8 +433,11 @@ def _(x, mask):
 
 @_op("whiten_finalize")
 def whiten_finalize(partials: Tensor, k: int) -> tuple[Tensor, Tensor]:
-    """Merge the first k (n, sum, M2) triples in index order: (merged fp64[3], stats fp32[4] =
-    {mean, rsqrt(var + 1e-8), n, error_flag})."""
+    """Merge the first k (n, sum, M2) triples in a fixed order: (merged fp64[3], stats fp32[4] =
+    {mean, rsqrt(var + 1e-8), n, error_flag}). The partials are read from a private copy when the
+    two-level merge (k > 1024) would overwrite them."""
+    if k > 1024:
+        partials = partials.clone()
     merged = torch.empty(3, dtype=_F64, device=partials.device)
     stats = torch.empty(4, dtype=_F32, device=partials.device)
     L.call("va_whiten_finalize", K._p(partials), k, K._p(merged), K._p(stats), K._stream(partials))
@@ -467,7 +475,7 @@ def gae_advantage_return(rewards: Tensor, values: Tensor, mask: Tensor, gamma: f
     adv = torch.empty_like(rewards)
     ret = torch.empty_like(rewards)
     stats = torch.empty(4, dtype=_F32, device=rewards.device)
-    ws = torch.empty(B * 3 + 4, dtype=_F64, device=rewards.device)
+    ws = torch.empty(_gae_ws_doubles(B), dtype=_F64, device=rewards.device)
     L.call("va_gae_advantage_return", K._p(rewards), K._p(values), K._p(mask), _mcode(mask), B, R, gamma, lam,
            K._p(adv), K._p(ret), K._p(stats), K._p(ws), K._stream(rewards))
     return adv, ret, stats

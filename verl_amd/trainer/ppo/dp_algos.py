@@ -161,8 +161,8 @@ def compute_gae_advantage_return_dp(token_level_rewards, values, response_mask, 
     with torch.no_grad():
         adv_raw, ret, part = torch.ops.verl_amd.gae_scan(K._f32(token_level_rewards), K._f32(values), m,
                                                          float(gamma), float(lam))
-        B = adv_raw.shape[0]
-        local, _ = torch.ops.verl_amd.whiten_finalize(part, B)
+        P = L.load().va_gae_partial_count(adv_raw.shape[0])
+        local, _ = torch.ops.verl_amd.whiten_finalize(part, P)
         stats = global_whiten_stats(local, group)
         K._raise_whiten_flag(stats)
         adv = torch.ops.verl_amd.whiten_apply(adv_raw, stats, None, False)
