@@ -1,0 +1,223 @@
+"""Parity of the EXACT configuration bench.py measures: packed remove-padding
+micro-batches, the fused packed backbone, the gfx950 flash attention (head_dim 64), bf16 weights
+with fp32 masters / gradients (MixedPrecisionParams), pack_pad_multiple, out-of-place log-prob
+backward — against the reference computation (dp_actor.py:80-270 padded path + the oracle loss,
+dp_actor.py:400-470) on tiny Qwen2 and Llama models.
+
+Error budget, derived from an fp64 run: the reference itself trains in bf16 (FSDP MixedPrecision
+param_dtype=bf16, fsdp_workers.py:337-347), so its own bf16 result differs from the exact (fp64)
+one. The bench configuration must stay within twice that intrinsic bf16 error (plus a small floor):
+  * log-probs (response tokens):  max |lp - lp64|            <= 2 max |lp_ref16 - lp64| + 2e-3
+  * policy-loss metrics:          |pg - pg64|                <= 2 |pg_ref16 - pg64| + 1e-4
+  * gradients (all parameters):   ||g - g64|| / ||g64||      <= 2 (same for ref16) + 1e-3
+where *_ref16 is the reference computation with bf16 parameters (HF model, padded, sdpa) and
+lp64 / g64 the same computation in float64.
+
+A 0.5B-architecture micro-batch (4 x 1024 responses, the bench's model) checks properties that
+need no fp64 run: finite gradients, grad norm within 2 % and gradient cosine >= 0.99 of the
+reference bf16 padded path, and sum_j dlogits[i, j] = 0 for every row (the log-softmax and entropy
+gradients are orthogonal to the all-ones vector) to |sum| <= 1e-2 sum_j |dlogits[i, j]|.
+"""
+
+import copy
+
+import pytest
+import torch
+
+from oracle import reference_ops as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+LOSS = dict(clip_ratio=0.2, loss_agg_mode="token-mean", ref_kl="low_var_kl", kl_coef=0.001)
+
+
+def _tiny(kind, dtype=torch.float32, seed=3):
+    from verl_amd.utils.model import build_llama, build_qwen2
+
+    if kind == "qwen2":  # head_dim 64 so the gfx950 flash kernels run, as on the 0.5B model
+        return build_qwen2("tiny", device=DEV, dtype=dtype, seed=seed, hidden_size=256, intermediate_size=512,
+                           num_attention_heads=4, num_key_value_heads=2, attn_implementation="sdpa")
+    return build_llama("tiny", device=DEV, dtype=dtype, seed=seed, attn_implementation="sdpa")
+
+
+def _params_to(model, dtype):
+    """Parameters in `dtype`, buffers (RoPE inv_freq) kept fp32: FSDP MixedPrecision's
+    param_dtype=bf16 / buffer_dtype=fp32 (fsdp_workers.py:337-347)."""
+    for p in model.parameters():
+        p.data = p.data.to(dtype)
+    return model
+
+
+def _data(model, B=8, P=48, R=96, V=4096, seed=21):
+    """A GRPO micro-batch pair whose old / ref log-probs sit around the model's own (fp64) log-probs,
+    so the clipped loss has both clipped and unclipped tokens."""
+    from verl_amd.utils.synthetic import make_grpo_batch
+
+    data = make_grpo_batch(n_prompts=B // 4, n=4, prompt_len=P, response_len=R, vocab=V, min_prompt=5,
+                           dense_responses=False, min_response=8, seed=seed, device=DEV)
+    b = data.batch
+    with torch.no_grad():
+        m64 = copy.deepcopy(model).double()
+        logits = m64(input_ids=b["input_ids"], attention_mask=b["attention_mask"], position_ids=b["position_ids"],
+                     use_cache=False).logits[:, -R - 1 : -1, :]
+        lp0 = torch.stack([ref.logprobs_from_logits(r, lab) for r, lab in zip(logits, b["responses"], strict=True)])
+        lp0 = lp0.float()
+        del m64, logits
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    b["old_log_probs"] = lp0 + 0.1 * torch.randn(B, R, device=DEV, generator=g)
+    b["ref_log_prob"] = lp0 + 0.1 * torch.randn(B, R, device=DEV, generator=g)
+    b["advantages"] = torch.randn(B, R, device=DEV, generator=g) * b["response_mask"]
+    data.meta_info.update(temperature=1.0, micro_batch_size=4, use_dynamic_bsz=False)
+    return data
+
+
+def _reference(model, data, dtype):
+    """dp_actor.py padded path + the oracle loss with model parameters in `dtype`; returns
+    (log-probs [B, R] fp64, pg_loss per micro-batch, {name: grad fp64})."""
+    model = model.double() if dtype == torch.float64 else _params_to(model, dtype)
+    model.zero_grad()
+    b = data.batch
+    R = b["responses"].shape[1]
+    lps, pgs = [], []
+    for s in (0, 4):
+        mb = {k: v[s : s + 4] for k, v in b.items()}
+        logits = model(input_ids=mb["input_ids"], attention_mask=mb["attention_mask"],
+                       position_ids=mb["position_ids"], use_cache=False).logits[:, -R - 1 : -1, :]
+        if dtype == torch.float64:
+            lp = torch.stack([ref.logprobs_from_logits(r, lab) for r, lab in zip(logits, mb["responses"], strict=True)])
+            cast = torch.float64
+        else:  # flash-attn cross-entropy semantics: fp32 math on the bf16 logits
+            lp = torch.stack([ref.logprobs_fp32_math(r, lab) for r, lab in zip(logits, mb["responses"], strict=True)])
+            cast = torch.float32
+        loss, met = ref.actor_loss(mb["old_log_probs"].to(cast), lp, mb["advantages"].to(cast), mb["response_mask"],
+                                   clip_ratio=LOSS["clip_ratio"], loss_agg_mode=LOSS["loss_agg_mode"],
+                                   ref_log_prob=mb["ref_log_prob"].to(cast), kl_loss_type=LOSS["ref_kl"],
+                                   kl_loss_coef=LOSS["kl_coef"], grad_scale=0.5)
+        loss.backward()
+        lps.append(lp.detach().double())
+        pgs.append(float(met["pg_loss"]))
+    grads = {n: p.grad.detach().double().clone() for n, p in model.named_parameters()}
+    return torch.cat(lps), pgs, grads
+
+
+def _bench_actor(model, pad_multiple=64):
+    """The bench's actor configuration (bench.py cfg) on `model` (fp32 init -> bf16 + fp32 masters)."""
+    from verl_amd.utils.config import actor_config
+    from verl_amd.workers.actor import DataParallelPPOActor
+    from verl_amd.workers.grad_sync import MixedPrecisionParams
+
+    mgr = MixedPrecisionParams(model, bucket_bytes=1 << 20)
+    opt = torch.optim.AdamW(mgr.optimizer_params(), lr=1e-6)
+    cfg = actor_config(ppo_mini_batch_size=8, ppo_micro_batch_size_per_gpu=4, use_kl_loss=True,
+                       kl_loss_coef=LOSS["kl_coef"], kl_loss_type=LOSS["ref_kl"], clip_ratio=LOSS["clip_ratio"],
+                       clip_ratio_c=3.0, loss_agg_mode=LOSS["loss_agg_mode"], entropy_coeff=0,
+                       use_remove_padding=True, pack_pad_multiple=pad_multiple, logprob_inplace_backward=False,
+                       grad_clip=1e9)
+    return DataParallelPPOActor(cfg, model, opt, grad_reducer=mgr), mgr
+
+
+def _run_bench(model, data):
+    actor, mgr = _bench_actor(model)
+    assert actor.fused_model_ops and actor.fused_attention and not actor.logprob_inplace_backward
+    lp, _ = actor.compute_log_prob(data, calculate_entropy=True)
+    grads = {}
+
+    def capture():
+        mgr.finish_sync()
+        for (n, _), m in zip(model.named_parameters(), mgr.optimizer_params(), strict=True):
+            grads[n] = m.grad.detach().double().clone()
+        return torch.tensor(0.0, device=DEV)
+
+    actor._optimizer_step = capture
+    metrics = actor.update_policy(data)
+    assert actor._fused_backbone, "the packed fused backbone did not engage"
+    return lp.double(), metrics["actor/pg_loss"], grads
+
+
+def _rel(g, g64):
+    num = sum(float((g[n] - g64[n]).square().sum()) for n in g64)
+    den = sum(float(g64[n].square().sum()) for n in g64)
+    return (num / den) ** 0.5
+
+
+@pytest.mark.parametrize("kind", ["qwen2", "llama"])
+def test_bench_configuration_within_bf16_budget_of_fp64(kind):
+    torch.manual_seed(0)
+    base = _tiny(kind)
+    data = _data(base)
+    m = data.batch["response_mask"].bool()
+    lp64, pg64, g64 = _reference(copy.deepcopy(base), data, torch.float64)
+    lp16, pg16, g16 = _reference(copy.deepcopy(base), data, torch.bfloat16)
+    lpb, pgb, gb = _run_bench(copy.deepcopy(base), data)
+    e_ref = float((lp16 - lp64)[m].abs().max())
+    e_b = float((lpb - lp64)[m].abs().max())
+    assert e_b <= 2 * e_ref + 2e-3, (kind, "log-prob", e_b, e_ref)
+    for b_, r_, x in zip(pgb, pg16, pg64, strict=True):
+        assert abs(b_ - x) <= 2 * abs(r_ - x) + 1e-4, (kind, "pg_loss", b_, r_, x)
+    assert set(gb) == set(g64)
+    r_ref, r_b = _rel(g16, g64), _rel(gb, g64)
+    assert r_b <= 2 * r_ref + 1e-3, (kind, "grad rel err", r_b, r_ref)
+    assert all(torch.isfinite(v).all() for v in gb.values())
+
+
+def test_bench_configuration_0p5b_microbatch_properties():
+    from verl_amd.utils.model import build_qwen2
+    from verl_amd.utils.synthetic import make_grpo_batch
+
+    torch.manual_seed(0)
+    base = build_qwen2("0.5b", device=DEV, seed=0, attn_implementation="sdpa")
+    data = make_grpo_batch(1, 4, 256, 1024, seed=5, device=DEV)
+    b = data.batch
+    B, R = b["responses"].shape
+    g = torch.Generator(device=DEV).manual_seed(7)
+    with torch.no_grad():
+        lp0 = torch.log_softmax(base(input_ids=b["input_ids"], attention_mask=b["attention_mask"],
+                                     position_ids=b["position_ids"], use_cache=False).logits[:, -R - 1 : -1, :],
+                                -1).gather(-1, b["responses"].unsqueeze(-1)).squeeze(-1)
+    b["old_log_probs"] = lp0 + 0.05 * torch.randn(B, R, device=DEV, generator=g)
+    b["ref_log_prob"] = lp0 + 0.1 * torch.randn(B, R, device=DEV, generator=g)
+    b["advantages"] = torch.randn(B, R, device=DEV, generator=g) * b["response_mask"]
+    data.meta_info.update(temperature=1.0, micro_batch_size=4, use_dynamic_bsz=False)
+
+    # reference bf16 padded path (one micro-batch of 4: grad_scale 1)
+    model_ref = _params_to(copy.deepcopy(base), torch.bfloat16)
+    logits = model_ref(input_ids=b["input_ids"], attention_mask=b["attention_mask"], position_ids=b["position_ids"],
+                       use_cache=False).logits[:, -R - 1 : -1, :]
+    lp = torch.stack([ref.logprobs_fp32_math(r, lab) for r, lab in zip(logits, b["responses"], strict=True)])
+    loss, _ = ref.actor_loss(b["old_log_probs"], lp, b["advantages"], b["response_mask"], clip_ratio=0.2,
+                             ref_log_prob=b["ref_log_prob"], kl_loss_type="low_var_kl", kl_loss_coef=0.001)
+    loss.backward()
+    g_ref = torch.cat([p.grad.float().reshape(-1) for p in model_ref.parameters()])
+    del model_ref, logits, lp, loss
+
+    model = copy.deepcopy(base)
+    actor, mgr = _bench_actor(model, pad_multiple=2048)
+    actor.config.ppo_mini_batch_size = 4
+    rows = []
+
+    def hook(_mod, _inp, out):
+        def grad_hook(gr):
+            gf = gr.float()
+            rows.append((gf.sum(-1), gf.abs().sum(-1)))
+        out.register_hook(grad_hook)
+
+    h = actor._lm_head.register_forward_hook(hook)
+    captured = {}
+
+    def capture():
+        mgr.finish_sync()
+        captured["g"] = torch.cat([m.grad.detach().float().reshape(-1) for m in mgr.optimizer_params()])
+        return torch.tensor(0.0, device=DEV)
+
+    actor._optimizer_step = capture
+    actor.update_policy(data)
+    h.remove()
+    gb = captured["g"]
+    assert torch.isfinite(gb).all()
+    n_ref, n_b = float(g_ref.norm()), float(gb.norm())
+    assert abs(n_b - n_ref) <= 0.02 * n_ref, (n_b, n_ref)
+    cos = float(torch.dot(gb.double(), g_ref.double()) / (gb.double().norm() * g_ref.double().norm()))
+    assert cos >= 0.99, cos
+    assert rows, "no dlogits seen"
+    for s, a in rows:
+        assert (s.abs() <= 1e-2 * a + 1e-6).all(), float((s.abs() / (a + 1e-30)).max())

@@ -1,0 +1,127 @@
+"""PPOTrainerStep / RayPPOTrainer orchestration on CPU with recording workers: the reference's
+fit() step order (ray_trainer.py:1195-1330), critic warmup gating, in-reward KL only when
+configured, metric reduction (utils/metric/utils.py:23-56)."""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import reference_ops as ref
+from verl_amd.protocol import DataProto
+from verl_amd.utils.config import AttrDict
+
+
+class _Actor:
+    def __init__(self, log, ref_policy=False):
+        self.log = log
+        self.ref_policy = object() if ref_policy else None
+
+    def compute_log_prob(self, data):
+        self.log.append("old_log_prob")
+        B, R = data.batch["responses"].shape
+        return DataProto.from_dict(tensors={"old_log_probs": -torch.ones(B, R), "entropys": torch.full((B, R), 2.0)})
+
+    def compute_ref_log_prob(self, data):
+        self.log.append("ref_log_prob")
+        return DataProto.from_dict(tensors={"ref_log_prob": -torch.ones_like(data.batch["old_log_probs"])})
+
+    def compute_advantage(self, data, est, **kw):
+        self.log.append(f"advantage:{est.value}")
+        assert "token_level_rewards" in data.batch.keys()
+        data.batch["advantages"] = data.batch["token_level_rewards"].clone()
+        data.batch["returns"] = data.batch["token_level_rewards"].clone()
+        return data
+
+    def update_actor(self, data):
+        self.log.append("update_actor")
+        assert "advantages" in data.batch.keys() and "old_log_probs" in data.batch.keys()
+        return DataProto(meta_info={"metrics": {"actor/pg_loss": [1.0, 3.0], "actor/grad_norm_max": [2.0, 5.0]}})
+
+
+class _Critic:
+    def __init__(self, log):
+        self.log = log
+
+    def compute_values(self, data):
+        self.log.append("values")
+        return DataProto.from_dict(tensors={"values": torch.zeros_like(data.batch["old_log_probs"])})
+
+    def update_critic(self, data):
+        self.log.append("update_critic")
+        return DataProto(meta_info={"metrics": {"critic/vf_loss": [0.5]}})
+
+
+def _batch(B=4, P=3, R=5):
+    ids = torch.randint(0, 10, (B, P + R))
+    am = torch.ones(B, P + R, dtype=torch.long)
+    return DataProto.from_dict(
+        tensors=dict(input_ids=ids, attention_mask=am, position_ids=torch.arange(P + R).expand(B, -1).clone(),
+                     responses=ids[:, P:].clone(), token_level_scores=torch.ones(B, R)),
+        non_tensors=dict(uid=np.array(["a", "a", "b", "b"], dtype=object)))
+
+
+def _cfg(est, warmup=0):
+    return AttrDict(algorithm=AttrDict(adv_estimator=est, gamma=1.0, lam=1.0, norm_adv_by_std_in_grpo=True,
+                                       use_kl_in_reward=False, kl_penalty="kl"),
+                    actor_rollout_ref=AttrDict(actor=AttrDict(loss_agg_mode="token-mean"), rollout=AttrDict(n=2)),
+                    trainer=AttrDict(critic_warmup=warmup))
+
+
+@pytest.fixture(autouse=True)
+def _cpu_agg(monkeypatch):
+    from verl_amd.trainer.ppo import trainer_step
+
+    monkeypatch.setattr(trainer_step.core_algos, "agg_loss", ref.agg_loss)
+
+
+def test_step_order_gae_with_critic_and_ref():
+    from verl_amd.trainer.ppo.trainer_step import PPOTrainerStep
+
+    log = []
+    step = PPOTrainerStep(_cfg("gae"), _Actor(log, ref_policy=True), critic=_Critic(log), device=torch.device("cpu"))
+    batch, met = step.step(_batch())
+    assert log == ["old_log_prob", "ref_log_prob", "values", "advantage:gae", "update_critic", "update_actor"]
+    assert "response_mask" in batch.batch.keys() and batch.meta_info["global_token_num"] == [8] * 4
+    assert met["actor/entropy"] == pytest.approx(2.0)
+    assert met["actor/pg_loss"] == pytest.approx(2.0) and met["actor/grad_norm_max"] == 5.0
+    assert met["critic/vf_loss"] == 0.5
+
+
+def test_critic_warmup_skips_actor_update_and_grpo_needs_no_critic():
+    from verl_amd.trainer.ppo.trainer_step import PPOTrainerStep
+
+    log = []
+    step = PPOTrainerStep(_cfg("gae", warmup=1), _Actor(log), critic=_Critic(log), device=torch.device("cpu"))
+    step.step(_batch())
+    assert "update_actor" not in log and log[-1] == "update_critic"
+    log.clear()
+    step.step(_batch())
+    assert log[-1] == "update_actor"
+    log2 = []
+    g = PPOTrainerStep(_cfg("grpo"), _Actor(log2), device=torch.device("cpu"))
+    g.step(_batch())
+    assert log2 == ["old_log_prob", "advantage:grpo", "update_actor"]
+    with pytest.raises(ValueError):
+        PPOTrainerStep(_cfg("gae"), _Actor([]), device=torch.device("cpu"))
+
+
+def test_ray_trainer_surface_builds_workers_from_the_role_mapping():
+    from verl_amd.trainer.ppo.ray_trainer import RayPPOTrainer
+    from verl_amd.trainer.ppo.trainer_step import Role
+
+    log = []
+    actor = _Actor(log, ref_policy=True)
+    tr = RayPPOTrainer(_cfg("grpo"), tokenizer=None,
+                       role_worker_mapping={Role.ActorRollout: lambda: actor, Role.RefPolicy: lambda: None})
+    tr.init_workers()
+    tr.step_runner.device = torch.device("cpu")
+    mets = tr.fit([_batch(), _batch()])
+    assert len(mets) == 2 and tr.global_steps == 2
+    assert log.count("ref_log_prob") == 2 and log.count("update_actor") == 2
+
+
+def test_reduce_metrics_matches_reference_rules():
+    from verl_amd.trainer.ppo.trainer_step import reduce_metrics
+
+    out = reduce_metrics({"loss": [1.0, 2.0, 3.0], "max_reward": [5.0, 8.0, 6.0], "min_error": [0.1, 0.05, 0.2]})
+    assert out == {"loss": 2.0, "max_reward": 8.0, "min_error": 0.05}

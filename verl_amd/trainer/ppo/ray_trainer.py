@@ -125,3 +125,79 @@ def filter_groups(batch: DataProto, metric: str = "acc"):
     kept = {uid for uid, vs in vals.items() if np.std(vs) > 0 or len(vs) == 1}
     idx = [i for i, uid in enumerate(uids) if uid in kept]
     return batch[idx], len(kept)
+
+
+class ResourcePoolManager:
+    """ray_trainer.py:81-126 without Ray: the GPUs are the torch.distributed ranks of this job, so
+    the spec is recorded for reference and the pools are this process group."""
+
+    def __init__(self, resource_pool_spec: Optional[dict] = None, mapping: Optional[dict] = None):
+        self.resource_pool_spec = resource_pool_spec or {}
+        self.mapping = mapping or {}
+
+    def create_resource_pool(self):
+        return None
+
+    def get_n_gpus(self) -> int:
+        import torch.distributed as dist
+
+        return dist.get_world_size() if dist.is_initialized() else 1
+
+
+class RayPPOTrainer:
+    """The reference's trainer surface (ray_trainer.py:293-400 constructor, :823 init_workers,
+    :1081 fit) for an SPMD job: every rank constructs it with the same arguments.
+
+    role_worker_mapping maps a Role to a zero-argument factory returning this rank's worker
+    (ActorWorker / CriticWorker; Role.RefPolicy may map to the actor itself when it holds the
+    reference policy). Rollout generation and reward models are outside this path: ``fit`` takes
+    rollout batches (input_ids / attention_mask / position_ids / responses [+ uid, scores]), and
+    reward_fn(batch) -> token_level_scores supplies the reward when the batch has none."""
+
+    def __init__(self, config, tokenizer=None, role_worker_mapping: Optional[dict] = None, resource_pool_manager=None,
+                 ray_worker_group_cls=None, processor=None, reward_fn=None, val_reward_fn=None, train_dataset=None,
+                 val_dataset=None, collate_fn=None, train_sampler=None, device_name="cuda"):
+        from .trainer_step import Role
+
+        self.config = config
+        self.tokenizer = tokenizer
+        self.processor = processor
+        self.reward_fn = reward_fn
+        self.val_reward_fn = val_reward_fn
+        self.role_worker_mapping = role_worker_mapping or {}
+        self.resource_pool_manager = resource_pool_manager or ResourcePoolManager()
+        self.device_name = device_name
+        assert Role.ActorRollout in self.role_worker_mapping, f"{self.role_worker_mapping.keys()=}"
+        self.use_reference_policy = Role.RefPolicy in self.role_worker_mapping
+        self.use_rm = Role.RewardModel in self.role_worker_mapping
+        self.use_critic = AdvantageEstimator(config.algorithm.adv_estimator) == AdvantageEstimator.GAE
+        self.step_runner = None
+        self.global_steps = 0
+
+    def init_workers(self):
+        """ray_trainer.py:823-907: build the role workers (here: call the factories)."""
+        from .trainer_step import PPOTrainerStep, Role
+
+        self.actor_rollout_wg = self.role_worker_mapping[Role.ActorRollout]()
+        self.critic_wg = self.role_worker_mapping[Role.Critic]() if self.use_critic else None
+        ref = None
+        if self.use_reference_policy:
+            ref = self.role_worker_mapping[Role.RefPolicy]()
+            if ref is None:
+                ref = self.actor_rollout_wg
+        self.ref_policy_wg = ref
+        self.step_runner = PPOTrainerStep(self.config, self.actor_rollout_wg, critic=self.critic_wg, ref=ref,
+                                          reward_fn=self.reward_fn)
+
+    def fit_step(self, batch: DataProto) -> dict:
+        """One iteration of fit() (ray_trainer.py:1195-1330) on this rank's shard."""
+        if self.step_runner is None:
+            self.init_workers()
+        self.step_runner.global_steps = self.global_steps
+        _, metrics = self.step_runner.step(batch)
+        self.global_steps += 1
+        return metrics
+
+    def fit(self, batches) -> list[dict]:
+        """ray_trainer.py:1081-1411 over an iterable of rollout shards; returns the per-step metrics."""
+        return [self.fit_step(b) for b in batches]

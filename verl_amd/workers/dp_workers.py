@@ -89,6 +89,7 @@ class ActorWorker:
             raise ValueError("ppo_micro_batch_size_per_gpu is required unless use_dynamic_bsz is set")
         self.actor = None
         self.module = None
+        self.ref_policy = None
 
     def init_model(self, module: torch.nn.Module, bucket_mb: int = 256, mixed_precision: bool = True,
                    zero: bool = False):
@@ -106,6 +107,31 @@ class ActorWorker:
                                 weight_decay=optim.get("weight_decay", 0.01), fused=fused)
         self.actor = DataParallelPPOActor(self.config.actor, module, opt, grad_reducer=manager)
         return self
+
+    def init_ref_model(self, module: torch.nn.Module, mixed_precision: bool = True):
+        """The reference policy held next to the actor (fsdp_workers.py:578-591, `_is_ref`): a frozen
+        copy run by a DataParallelPPOActor without optimizer (dp_actor.py:52-53), in bf16 like the
+        reference's FSDP param_dtype when mixed_precision."""
+        if mixed_precision:
+            for p in module.parameters():
+                p.data = p.data.to(torch.bfloat16)
+        for p in module.parameters():
+            p.requires_grad_(False)
+        self.ref_policy = DataParallelPPOActor(self.config.actor, module, None)
+        return self
+
+    def compute_ref_log_prob(self, data: DataProto) -> DataProto:
+        """fsdp_workers.py:802-835: ref_log_prob for this rank's shard (no entropy)."""
+        ref = self.config.get("ref") or {}
+        ro = self.config.rollout
+        data.meta_info["micro_batch_size"] = ref.get("log_prob_micro_batch_size_per_gpu",
+                                                     ro.get("log_prob_micro_batch_size_per_gpu"))
+        data.meta_info["temperature"] = ro.temperature
+        data.meta_info["max_token_len"] = ref.get("log_prob_max_token_len_per_gpu",
+                                                  ro.get("log_prob_max_token_len_per_gpu", 16384))
+        data.meta_info["use_dynamic_bsz"] = ref.get("log_prob_use_dynamic_bsz", ro.get("log_prob_use_dynamic_bsz", False))
+        lp, _ = self.ref_policy.compute_log_prob(data, calculate_entropy=False)
+        return DataProto.from_dict(tensors={"ref_log_prob": lp})
 
     def compute_log_prob(self, data: DataProto) -> DataProto:
         """fsdp_workers.py:758-800: old_log_probs (+ entropys) for this rank's shard."""
