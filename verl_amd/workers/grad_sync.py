@@ -428,7 +428,7 @@ class ShardedMixedPrecisionParams(_OrderedBuckets):
         self.shards: list[torch.nn.Parameter] = []
         self._gview = {}
         self._bucket_of = {}
-        self._layout = []
+        self._wslice = {}
         for i, g in enumerate(groups):
             n = sum(p.numel() for p in g)
             npad = -(-n // (W * 64)) * (W * 64)  # shards of whole 256-byte lines
@@ -447,6 +447,7 @@ class ShardedMixedPrecisionParams(_OrderedBuckets):
                 k = p.numel()
                 self._gview[id(p)] = gbuf[off : off + k].view_as(p)
                 p.data = wbuf[off : off + k].view_as(p)
+                self._wslice[id(p)] = (i, off)
                 off += k
             per = npad // W
             shard = torch.nn.Parameter(full[self.rank * per : (self.rank + 1) * per].clone(), requires_grad=True)
@@ -545,7 +546,9 @@ class ShardedMixedPrecisionParams(_OrderedBuckets):
 
     @torch.no_grad()
     def after_step(self):
-        """Round the master shards to bf16 and all-gather them into the flat weight buffers."""
+        """Round the master shards to bf16 and all-gather them into the flat weight buffers; a
+        parameter whose storage was re-pointed elsewhere since construction (the fused backbone
+        merges q|k|v and gate|up into one buffer, qwen2_fused.py) gets its slice copied over."""
         for s, wbuf in zip(self.shards, self.flat_weights, strict=True):
             mine = s.detach().to(self.compute_dtype)
             if self.world == 1:
@@ -556,6 +559,15 @@ class ShardedMixedPrecisionParams(_OrderedBuckets):
                 wbuf.copy_(torch.cat(parts).to(wbuf.device))
             else:
                 dist.all_gather_into_tensor(wbuf, mine, group=self.group)
+        dst, src = [], []
+        for p in self.params:
+            i, off = self._wslice[id(p)]
+            wbuf = self.flat_weights[i]
+            if p.data.data_ptr() != wbuf.data_ptr() + off * wbuf.element_size():
+                dst.append(p.data)
+                src.append(wbuf[off : off + p.numel()].view_as(p))
+        if dst:
+            torch._foreach_copy_(dst, src)
 
     def memory_bytes(self) -> dict:
         """Per-rank bytes of the parameter / gradient / optimizer state this manager holds."""
