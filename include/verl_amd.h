@@ -150,7 +150,13 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   4 or 8 (per workgroup); results differ only in the fp64 merge order;
  *   VA_TUNE_GAE_NT (va_gae_scan / va_gae_advantage_return): streaming-cache bits, 1 = non-temporal
  *   r / v loads, 2 = non-temporal returns store, 4 = non-temporal raw / whitened advantage stores
- *   (default 3; identical results). */
+ *   (default 3; identical results);
+ *   VA_TUNE_LOSS_VEC (va_ppo_loss_fwd): 1 = one wave per row with 16-byte lane quads (default where
+ *   R % 4 == 0, R <= 2048 and the rows are 16-byte aligned), 0 = one workgroup per row (fp64 row
+ *   sums in another order);
+ *   VA_TUNE_WHITEN_SLICE_MIN / VA_TUNE_WHITEN_GRID (va_gae_advantage_return): partial count above
+ *   which partials are merged in parallel slices first (default 4,096) and the statistics +
+ *   whitening launch's grid cap (default 2,048); only the fp64 merge order changes. */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3
@@ -164,6 +170,9 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_FLASH_FWD_KB 11
 #define VA_TUNE_GAE_PARTIALS 12
 #define VA_TUNE_GAE_NT 13
+#define VA_TUNE_LOSS_VEC 14
+#define VA_TUNE_WHITEN_SLICE_MIN 15
+#define VA_TUNE_WHITEN_GRID 16
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------
@@ -182,9 +191,10 @@ int va_set_tuning(int key, int value);
  *   with the reference's top-k / random draw; NULL for vanilla and gpg. Metric slots per mode:
  *   vanilla as the reference; gpg: 0, 0, 0; clip_cov: masked_mean(sel), masked_mean(old - lp), 0;
  *   kl_cov: 0, masked_mean(|lp - old|) (ppo_kl_abs), 0.
- *   out[VA_LOSS_NOUT] fp32 (device). workspace: va_ppo_loss_workspace_bytes(B).
- * The workspace holds per-row partial sums that the backward reads: keep it alive between
- * the forward and the backward of the same micro-batch. */
+ *   out[VA_LOSS_NOUT] fp32 (device). workspace: va_ppo_loss_workspace_bytes(B) = 8 (16 B + 8):
+ *   [B, 8] fp64 row partials, 8 fp64 totals (n first), then up to B per-workgroup aggregated
+ *   vectors that only the forward reads. The first 8 B + 8 doubles are what the backward reads:
+ *   keep them alive between the forward and the backward of the same micro-batch. */
 int64_t va_ppo_loss_workspace_bytes(int64_t B);
 int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float *adv, const void *mask,
                     int mask_dtype, const float *ref_lp, const float *entropy, int64_t B,

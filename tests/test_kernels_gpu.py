@@ -475,3 +475,69 @@ def test_gae_quad_kernel_multi_turn_property(K):
     m = mask.to(DEV)
     assert torch.equal(a1, a2)
     assert torch.equal(r1 * m, r2 * m)
+
+
+@pytest.mark.parametrize("R", [1024, 1000, 2048, 260, 17])
+@pytest.mark.parametrize("mode", ["vanilla", "gpg", "clip_cov", "kl_cov"])
+def test_policy_loss_streaming_forward_matches_workgroup_kernel(K, R, mode):
+    """VA_TUNE_LOSS_VEC: the wave-per-row streaming forward (default where it applies) and the
+    workgroup-per-row forward give the same 8 slots (fp64 row sums in another order) and bitwise
+    the same gradients (the backward reads only counts from the partials)."""
+    from verl_amd import _lib as L
+
+    g = torch.Generator().manual_seed(R)
+    B = 37
+    old = (-torch.rand(B, R, generator=g) * 3).to(DEV)
+    lp = (old.cpu() + 0.3 * torch.randn(B, R, generator=g)).to(DEV)
+    adv = torch.randn(B, R, generator=g).to(DEV)
+    ref_ = (old.cpu() + 0.1 * torch.randn(B, R, generator=g)).to(DEV)
+    ent = torch.rand(B, R, generator=g).to(DEV)
+    lens = torch.randint(1, R + 1, (B,), generator=g)
+    mask = (torch.arange(R)[None, :] < lens[:, None]).long().to(DEV)
+    sel = (torch.rand(B, R, generator=g) < 0.05).to(DEV) if mode in ("clip_cov", "kl_cov") else None
+    outs = []
+    try:
+        for v in (1, 0):
+            L.call("va_set_tuning", L.VA_TUNE_LOSS_VEC, v)
+            x = lp.clone().requires_grad_(True)
+            e = ent.clone().requires_grad_(True)
+            out = K.fused_policy_loss(old, x, adv, mask, 0.2, 0.28, 3.0, "token-mean", ref_log_prob=ref_,
+                                      kl_loss_type="low_var_kl", entropy=e, loss_mode=mode, selection=sel,
+                                      mode_coef=0.1)
+            (out[0] + 0.01 * out[4] - 0.001 * out[5]).backward()
+            outs.append((out.detach().cpu(), x.grad.cpu(), e.grad.cpu()))
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_LOSS_VEC, 1)
+    _close(outs[0][0], outs[1][0], atol=1e-6, rtol=1e-6, what="loss slots vec vs wg")
+    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
+
+
+@pytest.mark.parametrize("B", [1500, 4500, 9001])
+@pytest.mark.parametrize("agg", ["token-mean", "seq-mean-token-sum", "seq-mean-token-mean", "seq-mean-token-sum-norm"])
+def test_policy_loss_multi_row_workgroups_match_workgroup_kernel(K, B, agg):
+    """Large batches: the streaming forward's 4-row workgroups (ragged last workgroup) fold each
+    row's per-row aggregate into one vector per workgroup for the finalize (up to 2,251 vectors,
+    several load rounds of the 1,024-thread finalize); every loss slot equals the
+    workgroup-per-row kernel's up to fp64 summation order, for every aggregation mode."""
+    from verl_amd import _lib as L
+
+    R = 512
+    g = torch.Generator(device=DEV).manual_seed(B)
+    old = -torch.rand(B, R, device=DEV, generator=g) * 3
+    lp = old + 0.3 * torch.randn(B, R, device=DEV, generator=g)
+    adv = torch.randn(B, R, device=DEV, generator=g)
+    ref_ = old + 0.1 * torch.randn(B, R, device=DEV, generator=g)
+    ent = torch.rand(B, R, device=DEV, generator=g)
+    lens = torch.randint(1, R + 1, (B,), device=DEV, generator=g)  # seq-mean-token-mean: 0/0 rows are NaN
+    mask = (torch.arange(R, device=DEV)[None, :] < lens[:, None]).to(torch.bool)
+    outs = []
+    try:
+        for vec in (0, 1):
+            L.call("va_set_tuning", L.VA_TUNE_LOSS_VEC, vec)
+            out = K.fused_policy_loss(old, lp, adv, mask, 0.2, 0.28, 3.0, agg, ref_log_prob=ref_,
+                                      kl_loss_type="low_var_kl", entropy=ent)
+            outs.append(out.detach().cpu())
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_LOSS_VEC, 1)
+    for o in outs[1:]:
+        _close(o, outs[0], atol=1e-6, rtol=1e-6, what=f"loss slots multi-row vs wg ({agg}, B={B})")

@@ -23,10 +23,13 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--match", nargs="*", default=[])
     ap.add_argument("--min-launches", type=int, default=1)
+    ap.add_argument("--phases", type=int, default=1,
+                    help="split each (kernel, grid) series, in launch order, into this many equal parts "
+                         "(kernels whose grid does not change with the batch size)")
     args = ap.parse_args()
     groups = defaultdict(list)
     with open(args.trace) as f:
-        for row in csv.DictReader(f):
+        for row in sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"])):
             name = row["Kernel_Name"]
             if args.match and not any(m in name for m in args.match):
                 continue
@@ -38,8 +41,15 @@ def main():
     for (name, grid), d in sorted(groups.items()):
         if len(d) < args.min_launches:
             continue
-        print(json.dumps({"kernel": name, "grid": grid, "launches": len(d), "mean_us": round(statistics.mean(d), 3),
-                          "median_us": round(statistics.median(d), 3), "min_us": round(min(d), 3)}))
+        n = args.phases if len(d) % args.phases == 0 else 1
+        k = len(d) // n
+        for ph in range(n):
+            x = d[ph * k : (ph + 1) * k]
+            rec = {"kernel": name, "grid": grid, "launches": len(x), "mean_us": round(statistics.mean(x), 3),
+                   "median_us": round(statistics.median(x), 3), "min_us": round(min(x), 3)}
+            if n > 1:
+                rec["phase"] = ph
+            print(json.dumps(rec))
 
 
 if __name__ == "__main__":

@@ -34,7 +34,10 @@ from verl_amd import kernels as K  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--rows", type=int, nargs="*", default=[512, 8192])
+    ap.add_argument("--rows", type=int, nargs="*", default=[128, 512, 8192])
+    ap.add_argument("--loss-vec", type=int, default=1)
+    ap.add_argument("--whiten-slice-min", type=int, default=4096)
+    ap.add_argument("--whiten-grid", type=int, default=2048)
     ap.add_argument("--R", type=int, default=1024)
     ap.add_argument("--gae-variant", type=int, default=0)
     ap.add_argument("--gae-partials", type=int, default=0)
@@ -44,6 +47,9 @@ def main():
     L.call("va_set_tuning", L.VA_TUNE_GAE_VARIANT, args.gae_variant)
     L.call("va_set_tuning", L.VA_TUNE_GAE_PARTIALS, args.gae_partials)
     L.call("va_set_tuning", L.VA_TUNE_GAE_NT, args.gae_nt)
+    L.call("va_set_tuning", L.VA_TUNE_LOSS_VEC, args.loss_vec)
+    L.call("va_set_tuning", L.VA_TUNE_WHITEN_SLICE_MIN, args.whiten_slice_min)
+    L.call("va_set_tuning", L.VA_TUNE_WHITEN_GRID, args.whiten_grid)
     s = K._vp(torch.cuda.current_stream(dev).cuda_stream)
     out = []
     for B in args.rows:
@@ -98,7 +104,7 @@ def main():
             torch.cuda.synchronize()
             us = 1e3 * e0.elapsed_time(e1) / args.iters
             rec = {"op": name, "B": B, "R": R, "wall_us_per_call": round(us, 2), "gae_variant": args.gae_variant,
-                   "gae_partials": args.gae_partials, "gae_nt": args.gae_nt}
+                   "gae_partials": args.gae_partials, "gae_nt": args.gae_nt, "loss_vec": args.loss_vec}
             print(json.dumps(rec), flush=True)
             out.append(rec)
     L.call("va_set_tuning", L.VA_TUNE_GAE_VARIANT, 0)

@@ -32,7 +32,8 @@ VA_VLOSS_LOSS, VA_VLOSS_CLIPFRAC, VA_VLOSS_VPRED_MEAN, VA_VLOSS_NTOKENS, VA_VLOS
 VA_TUNE_FWD_WAVES_PER_ROW, VA_TUNE_BWD_WAVES_PER_ROW, VA_TUNE_NONTEMPORAL, VA_TUNE_PIPELINE = 1, 2, 3, 4
 VA_TUNE_FLASH_GROUPED_DKDV, VA_TUNE_GAE_VARIANT, VA_TUNE_BWD_FLAT, VA_TUNE_SWIGLU_STREAM = 5, 6, 7, 8
 VA_TUNE_FLASH_DKDV_QT, VA_TUNE_FLASH_DQ_KB, VA_TUNE_FLASH_FWD_KB, VA_TUNE_GAE_PARTIALS = 9, 10, 11, 12
-VA_TUNE_GAE_NT = 13
+VA_TUNE_GAE_NT, VA_TUNE_LOSS_VEC = 13, 14
+VA_TUNE_WHITEN_SLICE_MIN, VA_TUNE_WHITEN_GRID = 15, 16
 
 _P = c_void_p
 _SIGNATURES: dict[str, tuple] = {

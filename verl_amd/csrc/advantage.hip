@@ -476,15 +476,25 @@ __device__ __forceinline__ Moments gae_row_quads(const float *__restrict__ rew, 
   const int lane = threadIdx.x & 63;
   const int64_t base = row * R;
   float r[JM][4], v[JM][4], m[JM][4];
+  float4 ra[JM], va[JM];
+  Mask4Raw<MT> mr[JM];
 #pragma unroll
-  for (int j = 0; j < JM; ++j) {
+  for (int j = 0; j < JM; ++j) {  // every load of the row first (raw mask: converted after)
     const int64_t t0 = 256 * j + 4 * lane;
     const bool ok = j < J && t0 < R;
     const int64_t tc = ok ? t0 : 0;  // clamped address: no branch around the loads
-    const float4 a = ld4(rew + base + tc, nt & 1);
-    const float4 b = ld4(val + base + tc, nt & 1);
+    ra[j] = ld4(rew + base + tc, nt & 1);
+    va[j] = ld4(val + base + tc, nt & 1);
+    mr[j] = load_mask4_raw<MT>(mask, base + tc);
+  }
+#pragma unroll
+  for (int j = 0; j < JM; ++j) pin4(ra[j]), pin4(va[j]), pin_mask4<MT>(mr[j]);
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const bool ok = j < J && 256 * j + 4 * lane < R;
+    const float4 a = ra[j], b = va[j];
     float mm[4];
-    load_mask4<MT>(mask, base + tc, mm);
+    cvt_mask4<MT>(mr[j], mm);
     r[j][0] = ok ? a.x : 0.f, r[j][1] = ok ? a.y : 0.f, r[j][2] = ok ? a.z : 0.f, r[j][3] = ok ? a.w : 0.f;
     v[j][0] = ok ? b.x : 0.f, v[j][1] = ok ? b.y : 0.f, v[j][2] = ok ? b.z : 0.f, v[j][3] = ok ? b.w : 0.f;
 #pragma unroll
@@ -826,9 +836,9 @@ __global__ __launch_bounds__(kMergeThreads) void whiten_stats_apply_kernel(float
   for (int64_t c0 = static_cast<int64_t>(blockIdx.x) * chunk; c0 < nq; c0 += static_cast<int64_t>(gridDim.x) * chunk) {
     float4 a[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < U; ++u) {  // clamped, unconditional loads: all U in flight at once
       const int64_t i = c0 + static_cast<int64_t>(u) * blockDim.x + threadIdx.x;
-      if (i < nq) a[u] = ld4(x + 4 * i, false);
+      a[u] = ld4(x + 4 * (i < nq ? i : nq - 1), false);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1214,6 +1224,12 @@ extern "C" int va_whiten_apply(float *x, const float *stats, const void *mask, i
   return check_launch("whiten_apply");
 }
 
+// va_set_tuning(VA_TUNE_WHITEN_SLICE_MIN / VA_TUNE_WHITEN_GRID): partial count above which the
+// partials are first merged in parallel slices (default 4,096), and the statistics + whitening
+// launch's grid cap (default 2,048)
+int g_whiten_slice_min = 8 * 512;
+int g_whiten_grid = 2048;
+
 extern "C" int va_gae_advantage_return(const float *rewards, const float *values,
                                        const void *mask, int mask_dtype, int64_t B, int64_t R,
                                        float gamma, float lam, float *adv, float *ret,
@@ -1231,7 +1247,7 @@ extern "C" int va_gae_advantage_return(const float *rewards, const float *values
     // statistics + whitening in one launch (every workgroup merges the partials itself); many
     // partials are first merged in parallel slices of kMergeSlice (in place)
     int64_t step = 1;
-    if (P > 8 * kMergeSlice) {
+    if (P > g_whiten_slice_min) {
       const int64_t G = (P + kMergeSlice - 1) / kMergeSlice;
       hipLaunchKernelGGL(whiten_merge_slices_kernel, dim3(static_cast<unsigned>(G)), dim3(kMergeThreads), 0, s,
                          part, P);
@@ -1239,7 +1255,7 @@ extern "C" int va_gae_advantage_return(const float *rewards, const float *values
     }
     const int64_t nq = n >> 2;
     int64_t grid = (nq + 8 * kMergeThreads - 1) / (8 * kMergeThreads);  // 8 quads per lane
-    if (grid > 2048) grid = 2048;
+    if (grid > g_whiten_grid) grid = g_whiten_grid;
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(whiten_stats_apply_kernel, dim3(static_cast<unsigned>(grid)), dim3(kMergeThreads), 0, s, adv,
                        part, P, step, merged, stats_out, nq, g_gae_nt);

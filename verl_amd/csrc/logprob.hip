@@ -711,6 +711,9 @@ extern int g_flash_grouped_dkdv;  // attention.hip
 extern int g_gae_variant;         // advantage.hip
 extern int g_gae_partials;        // advantage.hip
 extern int g_gae_nt;              // advantage.hip
+extern int g_loss_vec;            // loss.hip
+extern int g_whiten_slice_min;    // advantage.hip
+extern int g_whiten_grid;         // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
 extern int g_flash_dkdv_qt;       // attention.hip
 extern int g_flash_dq_kb;         // attention.hip
@@ -732,6 +735,15 @@ extern "C" int va_set_tuning(int key, int value) {
       g_gae_partials = value;
       return VA_OK;
     case VA_TUNE_GAE_NT: g_gae_nt = value & 7; return VA_OK;
+    case VA_TUNE_LOSS_VEC: g_loss_vec = value; return VA_OK;
+    case VA_TUNE_WHITEN_SLICE_MIN: g_whiten_slice_min = value < 0 ? 0 : value; return VA_OK;
+    case VA_TUNE_WHITEN_GRID:
+      if (value < 1 || value > 65536) {
+        va::set_error("VA_TUNE_WHITEN_GRID must be 1..65536 (got %d)", value);
+        return VA_E_ARG;
+      }
+      g_whiten_grid = value;
+      return VA_OK;
     case VA_TUNE_BWD_FLAT: va::g_bwd_flat = value; return VA_OK;
     case VA_TUNE_SWIGLU_STREAM: g_swiglu_variant = value; return VA_OK;
     case VA_TUNE_FLASH_DKDV_QT:

@@ -199,12 +199,26 @@ __device__ __forceinline__ float agg_weight(int agg, float g, float m, double n_
 }
 
 // ------------------------------------------------------------------ policy loss forward
+// Row partial slots q of one row, with the seq-mean-token-mean division applied where it is the
+// aggregated quantity (agg_value's per-row term).
+__device__ __forceinline__ double agg_term(int agg, double s, double n_b) {
+  return agg == VA_AGG_SEQ_MEAN_TOKEN_MEAN ? s / n_b : s;
+}
+__device__ __forceinline__ double agg_finish(int agg, double acc, double n_tot, int64_t B, int64_t R) {
+  switch (agg) {
+    case VA_AGG_TOKEN_MEAN: return acc / (n_tot + 1e-8);
+    case VA_AGG_SEQ_MEAN_TOKEN_SUM: return acc / static_cast<double>(B);
+    case VA_AGG_SEQ_MEAN_TOKEN_MEAN: return acc / static_cast<double>(B);
+    default: return acc / static_cast<double>(R);
+  }
+}
+
 template <int MT, int KL>
 __global__ __launch_bounds__(256) void ppo_loss_rows_kernel(
     const float *__restrict__ old_lp, const float *__restrict__ lp, const float *__restrict__ adv,
     const void *__restrict__ mask, const float *__restrict__ ref, const float *__restrict__ ent,
     const uint8_t *__restrict__ sel, int64_t R, float lo, float hi, float c, int agg, int mode,
-    float coef, double *__restrict__ part) {
+    float coef, double *__restrict__ part, double *__restrict__ wsum) {
   __shared__ double scratch[4 * 7];
   const int64_t b = blockIdx.x;
   const int64_t base = b * R;
@@ -233,70 +247,175 @@ __global__ __launch_bounds__(256) void ppo_loss_rows_kernel(
     }
   }
   block_sum<7>(v, scratch);
-  if (threadIdx.x < 7) part[b * kNQ + threadIdx.x] = v[threadIdx.x];
-}
-
-// Row partial slots q of one row, with the seq-mean-token-mean division applied where it is the
-// aggregated quantity (agg_value's per-row term).
-__device__ __forceinline__ double agg_term(int agg, double s, double n_b) {
-  return agg == VA_AGG_SEQ_MEAN_TOKEN_MEAN ? s / n_b : s;
-}
-__device__ __forceinline__ double agg_finish(int agg, double acc, double n_tot, int64_t B, int64_t R) {
-  switch (agg) {
-    case VA_AGG_TOKEN_MEAN: return acc / (n_tot + 1e-8);
-    case VA_AGG_SEQ_MEAN_TOKEN_SUM: return acc / static_cast<double>(B);
-    case VA_AGG_SEQ_MEAN_TOKEN_MEAN: return acc / static_cast<double>(B);
-    default: return acc / static_cast<double>(R);
+  if (threadIdx.x < kNQ) {
+    const int q = threadIdx.x;
+    const double x = q < 7 ? v[q] : 0.0;
+    part[b * kNQ + q] = x;
+    wsum[b * kNQ + q] = (q == 1 || q == 5 || q == 6) ? agg_term(agg, x, v[0]) : x;
   }
 }
 
-// One pass over the [B, 8] row partials: each thread loads its rows' 7 slots (all loads of a
-// batch of 4 rows issued before the adds), one block reduction of the 7 sums.
-__global__ __launch_bounds__(256) void ppo_loss_finalize_kernel(const double *__restrict__ part,
-                                                                int64_t B, int64_t R, int agg,
+// Streaming variant (R % 4 == 0, R <= 256 * JM, 16-byte aligned rows): one wave per row, lane k owns
+// the quads t = 256 j + 4 k + {0..3}, so every load is a coalesced 16-byte vector and all of a row's
+// loads are issued before the first use (the workgroup-per-row kernel above waits on 4 dependent
+// load rounds per row at R = 1024). Same per-element arithmetic; the fp64 row sums are added in a
+// different (fixed) order.
+template <int MT, int KL, int JM>
+__global__ __launch_bounds__(256) void ppo_loss_rows_vec_kernel(
+    const float *__restrict__ old_lp, const float *__restrict__ lp, const float *__restrict__ adv,
+    const void *__restrict__ mask, const float *__restrict__ ref, const float *__restrict__ ent,
+    const uint8_t *__restrict__ sel, int64_t B, int64_t R, int J, float lo, float hi, float c, int agg,
+    int mode, float coef, double *__restrict__ part, double *__restrict__ wsum) {
+  __shared__ double wg[4 * kNQ];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const bool tok = (agg == VA_AGG_TOKEN_MEAN);
+  double acc = 0.0;  // lane q < 7: slot q of this wave's row, aggregated per row (agg_term)
+  // absent inputs read valid stand-in rows (lp's own, cache hits) so that every load is
+  // unconditional: a load under a branch makes the compiler wait for it at the join
+  const bool has_ent = ent != nullptr, has_sel = sel != nullptr;
+  const float *entp = has_ent ? ent : lp;
+  const uint8_t *selp = has_sel ? sel : reinterpret_cast<const uint8_t *>(lp);
+  {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * nw + wave;
+  if (b < B) {
+  const int64_t base = b * R;
+  float4 o[JM], l[JM], a[JM], rf[JM], h[JM];
+  Mask4Raw<MT> mr[JM];
+  uint32_t sw[JM];
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const int64_t t0 = 256 * j + 4 * lane;
+    const bool ok = j < J && t0 < R;
+    const int64_t i = base + (ok ? t0 : 0);
+    o[j] = ld4(old_lp + i, false);
+    l[j] = ld4(lp + i, false);
+    a[j] = ld4(adv + i, false);
+    if constexpr (KL != VA_KL_NONE) rf[j] = ld4(ref + i, false);
+    h[j] = ld4(entp + i, false);
+    mr[j] = load_mask4_raw<MT>(mask, i);
+    sw[j] = *reinterpret_cast<const uint32_t *>(selp + i);
+  }
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    pin4(o[j]), pin4(l[j]), pin4(a[j]), pin4(h[j]), pin_mask4<MT>(mr[j]), pin1(sw[j]);
+    if constexpr (KL != VA_KL_NONE) pin4(rf[j]);
+  }
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    if (!(j < J && 256 * j + 4 * lane < R)) continue;
+    const float ov[4] = {o[j].x, o[j].y, o[j].z, o[j].w};
+    const float lv[4] = {l[j].x, l[j].y, l[j].z, l[j].w};
+    const float av[4] = {a[j].x, a[j].y, a[j].z, a[j].w};
+    float mv[4];
+    cvt_mask4<MT>(mr[j], mv);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float mm = mv[q];
+      const bool mb = (mm != 0.f);
+      const PolicyElem e =
+          policy_elem(ov[q], lv[q], av[q], lo, hi, c, mode, has_sel && ((sw[j] >> (8 * q)) & 0xffu) != 0, coef);
+      v[0] += mm;
+      v[1] += tok ? (mb ? e.pg : 0.f) * mm : e.pg * mm;
+      v[2] += (mb ? e.clip : 0.f) * mm;
+      v[3] += (mb ? e.negkl : 0.f) * mm;
+      v[4] += (mb ? e.lower : 0.f) * mm;
+      if constexpr (KL != VA_KL_NONE) {
+        const float rv[4] = {rf[j].x, rf[j].y, rf[j].z, rf[j].w};
+        const float k = kl_fwd<KL>(lv[q], rv[q]);
+        v[5] += tok ? (mb ? k : 0.f) * mm : k * mm;
+      }
+      if (has_ent) {
+        const float hv[4] = {h[j].x, h[j].y, h[j].z, h[j].w};
+        v[6] += tok ? (mb ? hv[q] : 0.f) * mm : hv[q] * mm;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 7; ++q) v[q] = wave_sum(v[q]);
+  double x = lane < 7 ? v[0] : 0.0;
+#pragma unroll
+  for (int q = 1; q < 7; ++q) x = lane == q ? v[q] : x;
+  if (lane < kNQ) part[b * kNQ + lane] = x;
+  acc += (lane == 1 || lane == 5 || lane == 6) ? agg_term(agg, x, v[0]) : x;
+  }
+  }
+  // the workgroup's rows in order: the waves' vectors added in wave order
+  if (nw == 1) {
+    if (lane < kNQ) wsum[static_cast<int64_t>(blockIdx.x) * kNQ + lane] = acc;
+    return;
+  }
+  if (lane < kNQ) wg[wave * kNQ + lane] = acc;
+  __syncthreads();
+  if (threadIdx.x < kNQ) {
+    double t = 0.0;
+    for (int w = 0; w < nw; ++w) t += wg[w * kNQ + threadIdx.x];
+    wsum[static_cast<int64_t>(blockIdx.x) * kNQ + threadIdx.x] = t;
+  }
+}
+
+// Totals of the [B, 8] fp64 row partials, read fully coalesced: the flat index f = 8 b + q is
+// split over the workgroup's threads so thread t always sees slot q = t % 8 (blockDim % 8 == 0)
+// of rows t / 8, t / 8 + blockDim / 8, ...; slots in `term_mask` are aggregated per row with
+// agg_term (the row's n_b = slot 0 comes from lane t - q by a shuffle). 16 loads per thread are
+// issued before the adds. Every thread gets tot[q] = the sum over rows of slot q (fixed order).
+__device__ void sum_row_slots(const double *__restrict__ part, int64_t B, int agg, unsigned term_mask,
+                              double (&tot)[kNQ], double *scratch /* [16 waves][8] */) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int q = threadIdx.x & 7;
+  const bool term = (term_mask >> q) & 1u;
+  const int64_t rows_per_pass = blockDim.x >> 3;
+  constexpr int kBatch = 16;
+  double acc = 0.0;
+  for (int64_t r0 = 0; r0 < B; r0 += kBatch * rows_per_pass) {
+    double x[kBatch];
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+      const int64_t b = r0 + i * rows_per_pass + (threadIdx.x >> 3);
+      x[i] = b < B ? part[b * kNQ + q] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+      const double nb = __shfl(x[i], lane & ~7, kWave);
+      const int64_t b = r0 + i * rows_per_pass + (threadIdx.x >> 3);
+      if (b < B) acc += term ? agg_term(agg, x[i], nb) : x[i];
+    }
+  }
+  // lanes holding the same slot: xor 8, 16, 32; then the waves in order
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) acc += __shfl_xor(acc, o, kWave);
+  if (lane < 8) scratch[wave * 8 + lane] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kNQ; ++k) {
+    double t = 0.0;
+    for (int w = 0; w < nw; ++w) t += scratch[w * 8 + k];
+    tot[k] = t;
+  }
+}
+
+__global__ __launch_bounds__(1024) void ppo_loss_finalize_kernel(const double *__restrict__ wsum,
+                                                                int64_t G, int64_t B, int64_t R, int agg,
                                                                 int has_kl, int has_ent,
                                                                 double *__restrict__ totals,
                                                                 float *__restrict__ out) {
-  __shared__ double scratch[4 * 7];
-  double v[7] = {0, 0, 0, 0, 0, 0, 0};  // n, clip, negkl, lower, pg, kl, ent
-  constexpr int kBatch = 4;
-  for (int64_t b0 = 0; b0 < B; b0 += static_cast<int64_t>(kBatch) * blockDim.x) {
-    double p[kBatch][7];
-#pragma unroll
-    for (int i = 0; i < kBatch; ++i) {
-      const int64_t b = b0 + static_cast<int64_t>(i) * blockDim.x + threadIdx.x;
-      const bool ok = b < B;
-      const double *row = part + (ok ? b : 0) * kNQ;
-#pragma unroll
-      for (int q = 0; q < 7; ++q) p[i][q] = ok ? row[q] : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < kBatch; ++i) {
-      const int64_t b = b0 + static_cast<int64_t>(i) * blockDim.x + threadIdx.x;
-      if (b >= B) continue;
-      v[0] += p[i][0];
-      v[1] += p[i][2];
-      v[2] += p[i][3];
-      v[3] += p[i][4];
-      v[4] += agg_term(agg, p[i][1], p[i][0]);
-      v[5] += agg_term(agg, p[i][5], p[i][0]);
-      v[6] += agg_term(agg, p[i][6], p[i][0]);
-    }
-  }
-  block_sum<7>(v, scratch);
+  __shared__ double scratch[16 * 8];
+  double v[kNQ];
+  // slots: 0 n, 1 pg, 2 clip, 3 negkl, 4 lower, 5 kl, 6 ent (1, 5, 6 already aggregated per row)
+  sum_row_slots(wsum, G, agg, 0u, v, scratch);
   if (threadIdx.x == 0) {
     const double n = v[0];
     const double den = n + 1e-8;
-    out[VA_LOSS_PG] = static_cast<float>(agg_finish(agg, v[4], n, B, R));
-    out[VA_LOSS_CLIPFRAC] = static_cast<float>(v[1] / den);
-    out[VA_LOSS_PPO_KL] = static_cast<float>(v[2] / den);
-    out[VA_LOSS_CLIPFRAC_LOWER] = static_cast<float>(v[3] / den);
+    out[VA_LOSS_PG] = static_cast<float>(agg_finish(agg, v[1], n, B, R));
+    out[VA_LOSS_CLIPFRAC] = static_cast<float>(v[2] / den);
+    out[VA_LOSS_PPO_KL] = static_cast<float>(v[3] / den);
+    out[VA_LOSS_CLIPFRAC_LOWER] = static_cast<float>(v[4] / den);
     out[VA_LOSS_KL] = has_kl ? static_cast<float>(agg_finish(agg, v[5], n, B, R)) : 0.f;
     out[VA_LOSS_ENTROPY] = has_ent ? static_cast<float>(agg_finish(agg, v[6], n, B, R)) : 0.f;
     out[VA_LOSS_NTOKENS] = static_cast<float>(n);
     out[VA_LOSS_NROWS] = static_cast<float>(B);
-    totals[0] = n;
   }
+  if (threadIdx.x < kTotals) totals[threadIdx.x] = threadIdx.x == 0 ? v[0] : 0.0;
 }
 
 // ------------------------------------------------------------------ policy loss backward
@@ -351,50 +470,33 @@ __global__ __launch_bounds__(256) void masked_rows_kernel(const float *__restric
     v[2] += xv * m;
   }
   block_sum<3>(v, scratch);
-  if (threadIdx.x == 0) {
-    part[b * kNQ + 0] = v[0];
+  if (threadIdx.x < kNQ) {
     // slot 1 carries the sum the mode aggregates: where-form for token-mean/masked_sum/row mean
     const bool where_form = (agg == VA_AGG_TOKEN_MEAN || agg == VA_REDUCE_MASKED_SUM ||
                              agg == VA_REDUCE_ROW_MASKED_MEAN);
-    part[b * kNQ + 1] = where_form ? v[1] : v[2];
+    const int q = threadIdx.x;
+    part[b * kNQ + q] = q == 0 ? v[0] : (q == 1 ? (where_form ? v[1] : v[2]) : 0.0);
   }
 }
 
-__global__ __launch_bounds__(256) void masked_agg_finalize_kernel(const double *__restrict__ part,
-                                                                  int64_t B, int64_t R, int agg,
-                                                                  double *__restrict__ totals,
-                                                                  float *__restrict__ out) {
-  __shared__ double scratch[4 * 2];
+__global__ __launch_bounds__(1024) void masked_agg_finalize_kernel(const double *__restrict__ part,
+                                                                   int64_t B, int64_t R, int agg,
+                                                                   double *__restrict__ totals,
+                                                                   float *__restrict__ out) {
+  __shared__ double scratch[16 * 8];
   if (agg == VA_REDUCE_ROW_MASKED_MEAN) {
     for (int64_t b = threadIdx.x; b < B; b += blockDim.x)
       out[b] = static_cast<float>(part[b * kNQ + 1] / (part[b * kNQ + 0] + 1e-8));
+    if (threadIdx.x < kTotals) totals[threadIdx.x] = 0.0;
     return;
   }
-  double v[2] = {0, 0};  // n, aggregated sum
-  constexpr int kBatch = 4;
   const int term_agg = agg == VA_REDUCE_MASKED_SUM ? VA_AGG_TOKEN_MEAN : agg;
-  for (int64_t b0 = 0; b0 < B; b0 += static_cast<int64_t>(kBatch) * blockDim.x) {
-    double pn[kBatch], ps[kBatch];
-#pragma unroll
-    for (int i = 0; i < kBatch; ++i) {
-      const int64_t b = b0 + static_cast<int64_t>(i) * blockDim.x + threadIdx.x;
-      const bool ok = b < B;
-      pn[i] = ok ? part[b * kNQ + 0] : 0.0;
-      ps[i] = ok ? part[b * kNQ + 1] : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < kBatch; ++i) {
-      const int64_t b = b0 + static_cast<int64_t>(i) * blockDim.x + threadIdx.x;
-      if (b >= B) continue;
-      v[0] += pn[i];
-      v[1] += agg_term(term_agg, ps[i], pn[i]);
-    }
-  }
-  block_sum<2>(v, scratch);
+  double v[kNQ];  // slots: 0 n, 1 sum (aggregated per row)
+  sum_row_slots(part, B, term_agg, 1u << 1, v, scratch);
   if (threadIdx.x == 0) {
     out[0] = static_cast<float>(agg == VA_REDUCE_MASKED_SUM ? v[1] : agg_finish(agg, v[1], v[0], B, R));
-    totals[0] = v[0];
   }
+  if (threadIdx.x < kTotals) totals[threadIdx.x] = threadIdx.x == 0 ? v[0] : 0.0;
 }
 
 template <int MT>
@@ -521,46 +623,25 @@ __global__ __launch_bounds__(256) void value_loss_rows_kernel(
     v[3] += (mb ? vp[i] : 0.f) * m;
   }
   block_sum<4>(v, scratch);
-  if (threadIdx.x < 4) part[b * kNQ + threadIdx.x] = v[threadIdx.x];
+  if (threadIdx.x < kNQ) part[b * kNQ + threadIdx.x] = threadIdx.x < 4 ? v[threadIdx.x] : 0.0;
 }
 
-__global__ __launch_bounds__(256) void value_loss_finalize_kernel(const double *__restrict__ part,
-                                                                  int64_t B, int64_t R, int agg,
-                                                                  double *__restrict__ totals,
-                                                                  float *__restrict__ out) {
-  __shared__ double scratch[4 * 4];
-  double v[4] = {0, 0, 0, 0};  // n, clip, vpred, loss
-  constexpr int kBatch = 4;
-  for (int64_t b0 = 0; b0 < B; b0 += static_cast<int64_t>(kBatch) * blockDim.x) {
-    double p[kBatch][4];
-#pragma unroll
-    for (int i = 0; i < kBatch; ++i) {
-      const int64_t b = b0 + static_cast<int64_t>(i) * blockDim.x + threadIdx.x;
-      const bool ok = b < B;
-      const double *row = part + (ok ? b : 0) * kNQ;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) p[i][q] = ok ? row[q] : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < kBatch; ++i) {
-      const int64_t b = b0 + static_cast<int64_t>(i) * blockDim.x + threadIdx.x;
-      if (b >= B) continue;
-      v[0] += p[i][0];
-      v[1] += p[i][2];
-      v[2] += p[i][3];
-      v[3] += agg_term(agg, p[i][1], p[i][0]);
-    }
-  }
-  block_sum<4>(v, scratch);
+__global__ __launch_bounds__(1024) void value_loss_finalize_kernel(const double *__restrict__ part,
+                                                                   int64_t B, int64_t R, int agg,
+                                                                   double *__restrict__ totals,
+                                                                   float *__restrict__ out) {
+  __shared__ double scratch[16 * 8];
+  double v[kNQ];  // slots: 0 n, 1 loss (aggregated per row), 2 clip, 3 vpred
+  sum_row_slots(part, B, agg, 1u << 1, v, scratch);
   if (threadIdx.x == 0) {
     const double n = v[0];
     const double den = n + 1e-8;
-    out[VA_VLOSS_LOSS] = 0.5f * static_cast<float>(agg_finish(agg, v[3], n, B, R));
-    out[VA_VLOSS_CLIPFRAC] = static_cast<float>(v[1] / den);
-    out[VA_VLOSS_VPRED_MEAN] = static_cast<float>(v[2] / den);
+    out[VA_VLOSS_LOSS] = 0.5f * static_cast<float>(agg_finish(agg, v[1], n, B, R));
+    out[VA_VLOSS_CLIPFRAC] = static_cast<float>(v[2] / den);
+    out[VA_VLOSS_VPRED_MEAN] = static_cast<float>(v[3] / den);
     out[VA_VLOSS_NTOKENS] = static_cast<float>(n);
-    totals[0] = n;
   }
+  if (threadIdx.x < kTotals) totals[threadIdx.x] = threadIdx.x == 0 ? v[0] : 0.0;
 }
 
 template <int MT>
@@ -606,11 +687,26 @@ using namespace va;
     default: set_error("unknown kl type %d", (int)(kt)); return VA_E_ARG;         \
   }
 
+// policy loss: [B, 8] row partials | 8 totals | up to B aggregated 8-slot vectors (one per
+// forward workgroup) that only the forward's finalize reads
 extern "C" int64_t va_ppo_loss_workspace_bytes(int64_t B) {
+  return static_cast<int64_t>(sizeof(double)) * (2 * B * kNQ + kTotals);
+}
+extern "C" int64_t va_agg_workspace_bytes(int64_t B) {
   return static_cast<int64_t>(sizeof(double)) * (B * kNQ + kTotals);
 }
-extern "C" int64_t va_agg_workspace_bytes(int64_t B) { return va_ppo_loss_workspace_bytes(B); }
 
+// threads of the one-workgroup finalize: 8 per row slot vector, 16 rows' loads in flight each,
+// 256 .. 1,024 (one load pass up to 2,048 rows)
+static unsigned finalize_threads(int64_t B) {
+  int64_t t = (B * 8 + 15) / 16;
+  t = (t + 63) / 64 * 64;
+  return static_cast<unsigned>(t < 256 ? 256 : (t > 1024 ? 1024 : t));
+}
+
+// va_set_tuning(VA_TUNE_LOSS_VEC): 1 (default) = wave-per-row streaming forward where it applies,
+// 0 = the workgroup-per-row kernel (same per-element arithmetic, fp64 row sums in another order)
+int g_loss_vec = 1;
 static int check_agg(int agg, bool allow_reduce) {
   const int hi = allow_reduce ? VA_REDUCE_ROW_MASKED_MEAN : VA_AGG_SEQ_MEAN_TOKEN_SUM_NORM;
   VA_CHECK_ARG(agg >= 0 && agg <= hi, "Invalid loss_agg_mode code: %d", agg);
@@ -639,12 +735,40 @@ extern "C" int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float
   if (int e = check_mode(loss_mode, sel)) return e;
   hipStream_t s = static_cast<hipStream_t>(stream);
   double *part = static_cast<double *>(workspace);
-  VA_DISPATCH_MASK(mask_dtype, VA_DISPATCH_KL(kl_type, {
-    hipLaunchKernelGGL((ppo_loss_rows_kernel<MT, KL>), dim3(B), dim3(256), 0, s, old_lp, lp,
-                       adv, mask, ref_lp, entropy, sel, R, clip_lo, clip_hi, clip_c, agg_mode,
-                       loss_mode, mode_coef, part);
-  }));
-  hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, B, R, agg_mode,
+  const uintptr_t align = reinterpret_cast<uintptr_t>(old_lp) | reinterpret_cast<uintptr_t>(lp) |
+                          reinterpret_cast<uintptr_t>(adv) | reinterpret_cast<uintptr_t>(mask) |
+                          reinterpret_cast<uintptr_t>(ref_lp) | reinterpret_cast<uintptr_t>(entropy);
+  const bool vec = g_loss_vec != 0 && (R & 3) == 0 && R <= 2048 && (align & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(sel) & 3) == 0;
+  double *wsum = part + B * kNQ + kTotals;
+  int64_t G = B;
+  if (vec) {
+    const int J = static_cast<int>((R + 255) / 256);
+    // 4 rows (waves) per workgroup, whose aggregated vectors are summed in the workgroup, so the
+    // finalize's single CU reads B / 4 vectors (a CU reads at ~16-30 GB/s). One row per wave: rows
+    // run back to back in a wave (tried: 2 / 4 per wave) hold more registers (3 -> 2 waves per
+    // SIMD) and expose their load latency (41 -> 53 us at 8,192 x 1,024)
+    constexpr int nw = 4;
+    G = (B + nw - 1) / nw;
+    const dim3 grid(static_cast<unsigned>(G)), block(64 * nw);
+    VA_DISPATCH_MASK(mask_dtype, VA_DISPATCH_KL(kl_type, {
+      if (J <= 4)
+        hipLaunchKernelGGL((ppo_loss_rows_vec_kernel<MT, KL, 4>), grid, block, 0, s, old_lp, lp, adv, mask,
+                           ref_lp, entropy, sel, B, R, J, clip_lo, clip_hi, clip_c, agg_mode, loss_mode, mode_coef,
+                           part, wsum);
+      else
+        hipLaunchKernelGGL((ppo_loss_rows_vec_kernel<MT, KL, 8>), grid, block, 0, s, old_lp, lp, adv, mask,
+                           ref_lp, entropy, sel, B, R, J, clip_lo, clip_hi, clip_c, agg_mode, loss_mode, mode_coef,
+                           part, wsum);
+    }));
+  } else {
+    VA_DISPATCH_MASK(mask_dtype, VA_DISPATCH_KL(kl_type, {
+      hipLaunchKernelGGL((ppo_loss_rows_kernel<MT, KL>), dim3(B), dim3(256), 0, s, old_lp, lp,
+                         adv, mask, ref_lp, entropy, sel, R, clip_lo, clip_hi, clip_c, agg_mode,
+                         loss_mode, mode_coef, part, wsum);
+    }));
+  }
+  hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(finalize_threads(G)), 0, s, wsum, G, B, R, agg_mode,
                      kl_type != VA_KL_NONE ? 1 : 0, entropy != nullptr ? 1 : 0, part + B * kNQ,
                      out);
   return check_launch("ppo_loss_fwd");
@@ -686,7 +810,7 @@ extern "C" int va_masked_agg_fwd(const float *x, const void *mask, int mask_dtyp
     hipLaunchKernelGGL((masked_rows_kernel<MT>), dim3(B), dim3(256), 0, s, x, mask, R, mode,
                        part);
   });
-  hipLaunchKernelGGL(masked_agg_finalize_kernel, dim3(1), dim3(256), 0, s, part, B, R, mode,
+  hipLaunchKernelGGL(masked_agg_finalize_kernel, dim3(1), dim3(finalize_threads(B)), 0, s, part, B, R, mode,
                      part + B * kNQ, out);
   return check_launch("masked_agg_fwd");
 }
@@ -762,7 +886,7 @@ extern "C" int va_value_loss_fwd(const float *vpreds, const float *values, const
     hipLaunchKernelGGL((value_loss_rows_kernel<MT>), dim3(B), dim3(256), 0, s, vpreds, values,
                        returns, mask, R, cliprange_value, agg_mode, part);
   });
-  hipLaunchKernelGGL(value_loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, B, R, agg_mode,
+  hipLaunchKernelGGL(value_loss_finalize_kernel, dim3(1), dim3(finalize_threads(B)), 0, s, part, B, R, agg_mode,
                      part + B * kNQ, out);
   return check_launch("value_loss_fwd");
 }

@@ -86,6 +86,66 @@ __device__ __forceinline__ void load_mask4(const void *p, int64_t i, float (&o)[
   }
 }
 
+// Pin a loaded value in registers: the empty asm makes the value an asm output, so the compiler
+// cannot drop it under register pressure and re-issue the (read-only) load later, which would put
+// a second memory round trip on the wave's critical path.
+__device__ __forceinline__ void pin4(float4 &x) {
+  asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w));
+}
+__device__ __forceinline__ void pin1(uint32_t &x) { asm volatile("" : "+v"(x)); }
+
+// The same split in two: the raw 16-byte loads (issued with the other streams' loads) and the
+// conversion (done where the values are used), so no load waits on an earlier conversion.
+template <int MT> struct Mask4Raw { float4 f; };
+template <> struct Mask4Raw<VA_MASK_I64> { longlong2 a, b; };
+template <> struct Mask4Raw<VA_MASK_I32> { int4 q; };
+template <> struct Mask4Raw<VA_MASK_U8> { uint32_t w; };
+
+template <int MT>
+__device__ __forceinline__ Mask4Raw<MT> load_mask4_raw(const void *p, int64_t i) {
+  Mask4Raw<MT> r;
+  if constexpr (MT == VA_MASK_F32) {
+    r.f = *reinterpret_cast<const float4 *>(static_cast<const float *>(p) + i);
+  } else if constexpr (MT == VA_MASK_I64) {
+    const longlong2 *q = reinterpret_cast<const longlong2 *>(static_cast<const int64_t *>(p) + i);
+    r.a = q[0], r.b = q[1];
+  } else if constexpr (MT == VA_MASK_I32) {
+    r.q = *reinterpret_cast<const int4 *>(static_cast<const int32_t *>(p) + i);
+  } else {
+    r.w = *reinterpret_cast<const uint32_t *>(static_cast<const uint8_t *>(p) + i);
+  }
+  return r;
+}
+
+template <int MT>
+__device__ __forceinline__ void pin_mask4(Mask4Raw<MT> &r) {
+  if constexpr (MT == VA_MASK_F32) {
+    pin4(r.f);
+  } else if constexpr (MT == VA_MASK_I64) {
+    asm volatile("" : "+v"(r.a.x), "+v"(r.a.y), "+v"(r.b.x), "+v"(r.b.y));
+  } else if constexpr (MT == VA_MASK_I32) {
+    asm volatile("" : "+v"(r.q.x), "+v"(r.q.y), "+v"(r.q.z), "+v"(r.q.w));
+  } else {
+    pin1(r.w);
+  }
+}
+
+template <int MT>
+__device__ __forceinline__ void cvt_mask4(const Mask4Raw<MT> &r, float (&o)[4]) {
+  if constexpr (MT == VA_MASK_F32) {
+    o[0] = r.f.x, o[1] = r.f.y, o[2] = r.f.z, o[3] = r.f.w;
+  } else if constexpr (MT == VA_MASK_I64) {
+    o[0] = static_cast<float>(r.a.x), o[1] = static_cast<float>(r.a.y);
+    o[2] = static_cast<float>(r.b.x), o[3] = static_cast<float>(r.b.y);
+  } else if constexpr (MT == VA_MASK_I32) {
+    o[0] = static_cast<float>(r.q.x), o[1] = static_cast<float>(r.q.y);
+    o[2] = static_cast<float>(r.q.z), o[3] = static_cast<float>(r.q.w);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = static_cast<float>((r.w >> (8 * q)) & 0xffu);
+  }
+}
+
 // ---------------------------------------------------------------- wave / block reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
