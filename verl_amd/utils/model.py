@@ -18,6 +18,9 @@ def qwen2_config(size: str = "0.5b", **overrides):
     presets = {
         "0.5b": dict(hidden_size=896, intermediate_size=4864, num_hidden_layers=24, num_attention_heads=14,
                      num_key_value_heads=2, vocab_size=151936, tie_word_embeddings=True),
+        # BASELINE config 5 (DAPO): the public Qwen2.5-7B card's values (assumed, no checkpoint here)
+        "7b": dict(hidden_size=3584, intermediate_size=18944, num_hidden_layers=28, num_attention_heads=28,
+                   num_key_value_heads=4, vocab_size=152064, tie_word_embeddings=False),
         "tiny": dict(hidden_size=128, intermediate_size=352, num_hidden_layers=2, num_attention_heads=4,
                      num_key_value_heads=2, vocab_size=4096, tie_word_embeddings=True),
     }
