@@ -71,7 +71,10 @@ def main():
         lp = old + 0.05 * torch.randn(B, R, device=dev, generator=g)
         ref = old + 0.1 * torch.randn(B, R, device=dev, generator=g)
         lout = torch.empty(8, device=dev)
-        lws = torch.zeros(B * 8 + 8, dtype=torch.float64, device=dev)
+        lws = torch.zeros(L.load().va_ppo_loss_workspace_bytes(B) // 8, dtype=torch.float64, device=dev)
+        vout = torch.empty(8, device=dev)
+        aout = torch.empty(1, device=dev)
+        vgrad = torch.empty(B, R, device=dev)
         gout = torch.zeros(8, device=dev)
         gout[0] = 1.0
         gout[4] = 0.001
@@ -91,7 +94,17 @@ def main():
             L.call("va_ppo_loss_bwd", K._p(gout), K._p(old), K._p(lp), K._p(adv), K._p(mask), L.VA_MASK_I64, K._p(ref),
                    B, R, 0.8, 1.2, 3.0, 0, L.VA_KL_K3, 0, None, 0.0, K._p(lws), K._p(dlp), None, s)
 
-        for name, fn in (("gae_whiten", gae), ("grpo_adv", grpo), ("ppo_loss_fwd_bwd", loss)):
+        def vloss():  # critic: vpreds = values + noise, returns = ret of the GAE call
+            L.call("va_value_loss_fwd", K._p(lp), K._p(old), K._p(ref), K._p(mask), L.VA_MASK_I64, B, R, 0.5, 0,
+                   K._p(vout), K._p(lws), s)
+            L.call("va_value_loss_bwd", K._p(gout), K._p(lp), K._p(old), K._p(ref), K._p(mask), L.VA_MASK_I64, B, R,
+                   0.5, 0, K._p(lws), K._p(vgrad), s)
+
+        def agg():  # agg_loss(entropy, mask, token-mean): the actor/entropy metric
+            L.call("va_masked_agg_fwd", K._p(lp), K._p(mask), L.VA_MASK_I64, B, R, 0, K._p(aout), K._p(lws), s)
+
+        for name, fn in (("gae_whiten", gae), ("grpo_adv", grpo), ("ppo_loss_fwd_bwd", loss),
+                         ("value_loss_fwd_bwd", vloss), ("masked_agg_fwd", agg)):
             for _ in range(5):
                 fn()
             torch.cuda.synchronize()

@@ -487,6 +487,7 @@ __device__ __forceinline__ Moments gae_row_quads(const float *__restrict__ rew, 
     va[j] = ld4(val + base + tc, nt & 1);
     mr[j] = load_mask4_raw<MT>(mask, base + tc);
   }
+  loads_issued();
 #pragma unroll
   for (int j = 0; j < JM; ++j) pin4(ra[j]), pin4(va[j]), pin_mask4<MT>(mr[j]);
 #pragma unroll

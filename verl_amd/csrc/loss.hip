@@ -255,6 +255,31 @@ __global__ __launch_bounds__(256) void ppo_loss_rows_kernel(
   }
 }
 
+// Streaming forwards, shared tail: the wave-summed slots v[0..NS) of row b go to part[b][0..8)
+// (lane q writes slot q, zeros past NS); the slots in term_mask are aggregated per row (agg_term
+// with n_b = slot 0) into the lane's running vector `acc`.
+template <int NS>
+__device__ __forceinline__ void emit_row(const double (&v)[NS], int64_t b, int lane, unsigned term_mask, int agg,
+                                         double *__restrict__ part, double &acc) {
+  double x = lane < NS ? v[0] : 0.0;
+#pragma unroll
+  for (int q = 1; q < NS; ++q) x = lane == q ? v[q] : x;
+  if (lane < kNQ) part[b * kNQ + lane] = x;
+  acc += ((term_mask >> (lane & 31)) & 1u) && lane < kNQ ? agg_term(agg, x, v[0]) : x;
+}
+
+// ... then the workgroup's rows in order: the waves' vectors added in wave order into wsum[blockIdx]
+__device__ __forceinline__ void wg_sum_vectors(double acc, double *__restrict__ wsum, double *wg /* [16][8] */) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane < kNQ) wg[wave * kNQ + lane] = acc;
+  __syncthreads();
+  if (threadIdx.x < kNQ) {
+    double t = 0.0;
+    for (int w = 0; w < nw; ++w) t += wg[w * kNQ + threadIdx.x];
+    wsum[static_cast<int64_t>(blockIdx.x) * kNQ + threadIdx.x] = t;
+  }
+}
+
 // Streaming variant (R % 4 == 0, R <= 256 * JM, 16-byte aligned rows): one wave per row, lane k owns
 // the quads t = 256 j + 4 k + {0..3}, so every load is a coalesced 16-byte vector and all of a row's
 // loads are issued before the first use (the workgroup-per-row kernel above waits on 4 dependent
@@ -295,6 +320,7 @@ __global__ __launch_bounds__(256) void ppo_loss_rows_vec_kernel(
     mr[j] = load_mask4_raw<MT>(mask, i);
     sw[j] = *reinterpret_cast<const uint32_t *>(selp + i);
   }
+  loads_issued();
 #pragma unroll
   for (int j = 0; j < JM; ++j) {
     pin4(o[j]), pin4(l[j]), pin4(a[j]), pin4(h[j]), pin_mask4<MT>(mr[j]), pin1(sw[j]);
@@ -333,25 +359,10 @@ __global__ __launch_bounds__(256) void ppo_loss_rows_vec_kernel(
   }
 #pragma unroll
   for (int q = 0; q < 7; ++q) v[q] = wave_sum(v[q]);
-  double x = lane < 7 ? v[0] : 0.0;
-#pragma unroll
-  for (int q = 1; q < 7; ++q) x = lane == q ? v[q] : x;
-  if (lane < kNQ) part[b * kNQ + lane] = x;
-  acc += (lane == 1 || lane == 5 || lane == 6) ? agg_term(agg, x, v[0]) : x;
+  emit_row<7>(v, b, lane, (1u << 1) | (1u << 5) | (1u << 6), agg, part, acc);
   }
   }
-  // the workgroup's rows in order: the waves' vectors added in wave order
-  if (nw == 1) {
-    if (lane < kNQ) wsum[static_cast<int64_t>(blockIdx.x) * kNQ + lane] = acc;
-    return;
-  }
-  if (lane < kNQ) wg[wave * kNQ + lane] = acc;
-  __syncthreads();
-  if (threadIdx.x < kNQ) {
-    double t = 0.0;
-    for (int w = 0; w < nw; ++w) t += wg[w * kNQ + threadIdx.x];
-    wsum[static_cast<int64_t>(blockIdx.x) * kNQ + threadIdx.x] = t;
-  }
+  wg_sum_vectors(acc, wsum, wg);
 }
 
 // Totals of the [B, 8] fp64 row partials, read fully coalesced: the flat index f = 8 b + q is
@@ -452,11 +463,21 @@ __global__ __launch_bounds__(256) void ppo_loss_bwd_kernel(
 }
 
 // ------------------------------------------------------------------ masked aggregation
+// the per-row term of the masked aggregation (masked_sum adds plain row sums)
+__device__ __forceinline__ int masked_term_agg(int agg) {
+  return agg == VA_REDUCE_MASKED_SUM || agg == VA_REDUCE_ROW_MASKED_MEAN ? VA_AGG_TOKEN_MEAN : agg;
+}
+// slot 1 carries the sum the mode aggregates: where-form for token-mean / masked_sum / row mean
+__device__ __forceinline__ bool masked_where_form(int agg) {
+  return agg == VA_AGG_TOKEN_MEAN || agg == VA_REDUCE_MASKED_SUM || agg == VA_REDUCE_ROW_MASKED_MEAN;
+}
+
 template <int MT>
 __global__ __launch_bounds__(256) void masked_rows_kernel(const float *__restrict__ x,
                                                           const void *__restrict__ mask,
                                                           int64_t R, int agg,
-                                                          double *__restrict__ part) {
+                                                          double *__restrict__ part,
+                                                          double *__restrict__ wsum) {
   __shared__ double scratch[4 * 3];
   const int64_t b = blockIdx.x;
   double v[3] = {0, 0, 0};  // n, where-sum, mul-sum
@@ -471,15 +492,61 @@ __global__ __launch_bounds__(256) void masked_rows_kernel(const float *__restric
   }
   block_sum<3>(v, scratch);
   if (threadIdx.x < kNQ) {
-    // slot 1 carries the sum the mode aggregates: where-form for token-mean/masked_sum/row mean
-    const bool where_form = (agg == VA_AGG_TOKEN_MEAN || agg == VA_REDUCE_MASKED_SUM ||
-                             agg == VA_REDUCE_ROW_MASKED_MEAN);
     const int q = threadIdx.x;
-    part[b * kNQ + q] = q == 0 ? v[0] : (q == 1 ? (where_form ? v[1] : v[2]) : 0.0);
+    const double x = q == 0 ? v[0] : (q == 1 ? (masked_where_form(agg) ? v[1] : v[2]) : 0.0);
+    part[b * kNQ + q] = x;
+    wsum[b * kNQ + q] = q == 1 ? agg_term(masked_term_agg(agg), x, v[0]) : x;
   }
 }
 
+// Streaming form (R % 4 == 0, R <= 256 * JM, 16-byte aligned): one wave per row, 4 rows per
+// workgroup summed into one vector for the finalize (as the policy loss).
+template <int MT, int JM>
+__global__ __launch_bounds__(256) void masked_rows_vec_kernel(const float *__restrict__ x,
+                                                              const void *__restrict__ mask, int64_t B,
+                                                              int64_t R, int J, int agg,
+                                                              double *__restrict__ part,
+                                                              double *__restrict__ wsum) {
+  __shared__ double wg[4 * kNQ];
+  const int lane = threadIdx.x & 63;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  double acc = 0.0;
+  if (b < B) {
+    const int64_t base = b * R;
+    float4 xa[JM];
+    Mask4Raw<MT> mr[JM];
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+      const int64_t t0 = 256 * j + 4 * lane;
+      const int64_t i = base + (j < J && t0 < R ? t0 : 0);
+      xa[j] = ld4(x + i, false);
+      mr[j] = load_mask4_raw<MT>(mask, i);
+    }
+    double v[3] = {0, 0, 0};  // n, where-sum, mul-sum
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {  // selects, not a branch: a branch would sink the loads into it
+      const bool ok = j < J && 256 * j + 4 * lane < R;
+      const float xv[4] = {xa[j].x, xa[j].y, xa[j].z, xa[j].w};
+      float mv[4];
+      cvt_mask4<MT>(mr[j], mv);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float m = ok ? mv[q] : 0.f, xx = ok ? xv[q] : 0.f;
+        v[0] += m;
+        v[1] += (m != 0.f ? xx : 0.f) * m;
+        v[2] += xx * m;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) v[q] = wave_sum(v[q]);
+    const double rv[2] = {v[0], masked_where_form(agg) ? v[1] : v[2]};
+    emit_row<2>(rv, b, lane, 1u << 1, masked_term_agg(agg), part, acc);
+  }
+  wg_sum_vectors(acc, wsum, wg);
+}
+
 __global__ __launch_bounds__(1024) void masked_agg_finalize_kernel(const double *__restrict__ part,
+                                                                   const double *__restrict__ wsum, int64_t G,
                                                                    int64_t B, int64_t R, int agg,
                                                                    double *__restrict__ totals,
                                                                    float *__restrict__ out) {
@@ -490,9 +557,8 @@ __global__ __launch_bounds__(1024) void masked_agg_finalize_kernel(const double 
     if (threadIdx.x < kTotals) totals[threadIdx.x] = 0.0;
     return;
   }
-  const int term_agg = agg == VA_REDUCE_MASKED_SUM ? VA_AGG_TOKEN_MEAN : agg;
-  double v[kNQ];  // slots: 0 n, 1 sum (aggregated per row)
-  sum_row_slots(part, B, term_agg, 1u << 1, v, scratch);
+  double v[kNQ];  // slots: 0 n, 1 sum (already aggregated per row)
+  sum_row_slots(wsum, G, agg, 0u, v, scratch);
   if (threadIdx.x == 0) {
     out[0] = static_cast<float>(agg == VA_REDUCE_MASKED_SUM ? v[1] : agg_finish(agg, v[1], v[0], B, R));
   }
@@ -606,7 +672,8 @@ __device__ __forceinline__ float value_dvp(float w, float vp, float v, float ret
 template <int MT>
 __global__ __launch_bounds__(256) void value_loss_rows_kernel(
     const float *__restrict__ vp, const float *__restrict__ val, const float *__restrict__ ret,
-    const void *__restrict__ mask, int64_t R, float c, int agg, double *__restrict__ part) {
+    const void *__restrict__ mask, int64_t R, float c, int agg, double *__restrict__ part,
+    double *__restrict__ wsum) {
   __shared__ double scratch[4 * 4];
   const int64_t b = blockIdx.x;
   const bool tok = (agg == VA_AGG_TOKEN_MEAN);
@@ -623,16 +690,75 @@ __global__ __launch_bounds__(256) void value_loss_rows_kernel(
     v[3] += (mb ? vp[i] : 0.f) * m;
   }
   block_sum<4>(v, scratch);
-  if (threadIdx.x < kNQ) part[b * kNQ + threadIdx.x] = threadIdx.x < 4 ? v[threadIdx.x] : 0.0;
+  if (threadIdx.x < kNQ) {
+    const int q = threadIdx.x;
+    const double x = q < 4 ? v[q] : 0.0;
+    part[b * kNQ + q] = x;
+    wsum[b * kNQ + q] = q == 1 ? agg_term(agg, x, v[0]) : x;
+  }
 }
 
-__global__ __launch_bounds__(1024) void value_loss_finalize_kernel(const double *__restrict__ part,
+// Streaming form, as the policy loss: one wave per row, 4 rows per workgroup.
+template <int MT, int JM>
+__global__ __launch_bounds__(256) void value_loss_rows_vec_kernel(
+    const float *__restrict__ vp, const float *__restrict__ val, const float *__restrict__ ret,
+    const void *__restrict__ mask, int64_t B, int64_t R, int J, float c, int agg, double *__restrict__ part,
+    double *__restrict__ wsum) {
+  __shared__ double wg[4 * kNQ];
+  const int lane = threadIdx.x & 63;
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const bool tok = (agg == VA_AGG_TOKEN_MEAN);
+  double acc = 0.0;
+  if (b < B) {
+    const int64_t base = b * R;
+    float4 pa[JM], va[JM], ra[JM];
+    Mask4Raw<MT> mr[JM];
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+      const int64_t t0 = 256 * j + 4 * lane;
+      const int64_t i = base + (j < J && t0 < R ? t0 : 0);
+      pa[j] = ld4(vp + i, false);
+      va[j] = ld4(val + i, false);
+      ra[j] = ld4(ret + i, false);
+      mr[j] = load_mask4_raw<MT>(mask, i);
+    }
+    loads_issued();
+#pragma unroll
+    for (int j = 0; j < JM; ++j) pin4(pa[j]), pin4(va[j]), pin4(ra[j]), pin_mask4<MT>(mr[j]);
+    double v[4] = {0, 0, 0, 0};  // n, loss, clip, vpred
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+      if (!(j < J && 256 * j + 4 * lane < R)) continue;
+      const float pv[4] = {pa[j].x, pa[j].y, pa[j].z, pa[j].w};
+      const float vv[4] = {va[j].x, va[j].y, va[j].z, va[j].w};
+      const float rv[4] = {ra[j].x, ra[j].y, ra[j].z, ra[j].w};
+      float mv[4];
+      cvt_mask4<MT>(mr[j], mv);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float m = mv[q];
+        const bool mb = (m != 0.f);
+        const ValueElem e = value_elem(pv[q], vv[q], rv[q], c);
+        v[0] += m;
+        v[1] += tok ? (mb ? e.loss : 0.f) * m : e.loss * m;
+        v[2] += (mb ? e.clip : 0.f) * m;
+        v[3] += (mb ? pv[q] : 0.f) * m;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = wave_sum(v[q]);
+    emit_row<4>(v, b, lane, 1u << 1, agg, part, acc);
+  }
+  wg_sum_vectors(acc, wsum, wg);
+}
+
+__global__ __launch_bounds__(1024) void value_loss_finalize_kernel(const double *__restrict__ wsum, int64_t G,
                                                                    int64_t B, int64_t R, int agg,
                                                                    double *__restrict__ totals,
                                                                    float *__restrict__ out) {
   __shared__ double scratch[16 * 8];
-  double v[kNQ];  // slots: 0 n, 1 loss (aggregated per row), 2 clip, 3 vpred
-  sum_row_slots(part, B, agg, 1u << 1, v, scratch);
+  double v[kNQ];  // slots: 0 n, 1 loss (already aggregated per row), 2 clip, 3 vpred
+  sum_row_slots(wsum, G, agg, 0u, v, scratch);
   if (threadIdx.x == 0) {
     const double n = v[0];
     const double den = n + 1e-8;
@@ -687,14 +813,12 @@ using namespace va;
     default: set_error("unknown kl type %d", (int)(kt)); return VA_E_ARG;         \
   }
 
-// policy loss: [B, 8] row partials | 8 totals | up to B aggregated 8-slot vectors (one per
-// forward workgroup) that only the forward's finalize reads
+// policy / value loss and masked aggregation: [B, 8] row partials | 8 totals | up to B aggregated
+// 8-slot vectors (one per forward workgroup) that only the forward's finalize reads
 extern "C" int64_t va_ppo_loss_workspace_bytes(int64_t B) {
   return static_cast<int64_t>(sizeof(double)) * (2 * B * kNQ + kTotals);
 }
-extern "C" int64_t va_agg_workspace_bytes(int64_t B) {
-  return static_cast<int64_t>(sizeof(double)) * (B * kNQ + kTotals);
-}
+extern "C" int64_t va_agg_workspace_bytes(int64_t B) { return va_ppo_loss_workspace_bytes(B); }
 
 // threads of the one-workgroup finalize: 8 per row slot vector, 16 rows' loads in flight each,
 // 256 .. 1,024 (one load pass up to 2,048 rows)
@@ -707,6 +831,12 @@ static unsigned finalize_threads(int64_t B) {
 // va_set_tuning(VA_TUNE_LOSS_VEC): 1 (default) = wave-per-row streaming forward where it applies,
 // 0 = the workgroup-per-row kernel (same per-element arithmetic, fp64 row sums in another order)
 int g_loss_vec = 1;
+// the streaming (wave-per-row, 16-byte quad) forwards apply: VA_TUNE_LOSS_VEC on, R % 4 == 0,
+// R <= 2048 and every row base 16-byte aligned
+static bool stream_rows(int64_t R, uintptr_t ptr_or) {
+  return g_loss_vec != 0 && (R & 3) == 0 && R <= 2048 && (ptr_or & 15) == 0;
+}
+
 static int check_agg(int agg, bool allow_reduce) {
   const int hi = allow_reduce ? VA_REDUCE_ROW_MASKED_MEAN : VA_AGG_SEQ_MEAN_TOKEN_SUM_NORM;
   VA_CHECK_ARG(agg >= 0 && agg <= hi, "Invalid loss_agg_mode code: %d", agg);
@@ -806,12 +936,26 @@ extern "C" int va_masked_agg_fwd(const float *x, const void *mask, int mask_dtyp
   if (int e = check_agg(mode, true)) return e;
   hipStream_t s = static_cast<hipStream_t>(stream);
   double *part = static_cast<double *>(workspace);
-  VA_DISPATCH_MASK(mask_dtype, {
-    hipLaunchKernelGGL((masked_rows_kernel<MT>), dim3(B), dim3(256), 0, s, x, mask, R, mode,
-                       part);
-  });
-  hipLaunchKernelGGL(masked_agg_finalize_kernel, dim3(1), dim3(finalize_threads(B)), 0, s, part, B, R, mode,
-                     part + B * kNQ, out);
+  double *wsum = part + B * kNQ + kTotals;
+  int64_t G = B;
+  if (stream_rows(R, reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(mask))) {
+    const int J = static_cast<int>((R + 255) / 256);
+    G = (B + 3) / 4;
+    VA_DISPATCH_MASK(mask_dtype, {
+      if (J <= 4)
+        hipLaunchKernelGGL((masked_rows_vec_kernel<MT, 4>), dim3(G), dim3(256), 0, s, x, mask, B, R, J, mode, part,
+                           wsum);
+      else
+        hipLaunchKernelGGL((masked_rows_vec_kernel<MT, 8>), dim3(G), dim3(256), 0, s, x, mask, B, R, J, mode, part,
+                           wsum);
+    });
+  } else {
+    VA_DISPATCH_MASK(mask_dtype, {
+      hipLaunchKernelGGL((masked_rows_kernel<MT>), dim3(B), dim3(256), 0, s, x, mask, R, mode, part, wsum);
+    });
+  }
+  hipLaunchKernelGGL(masked_agg_finalize_kernel, dim3(1), dim3(finalize_threads(mode == VA_REDUCE_ROW_MASKED_MEAN ? B : G)),
+                     0, s, part, wsum, G, B, R, mode, part + B * kNQ, out);
   return check_launch("masked_agg_fwd");
 }
 
@@ -882,11 +1026,27 @@ extern "C" int va_value_loss_fwd(const float *vpreds, const float *values, const
   if (int e = check_agg(agg_mode, false)) return e;
   hipStream_t s = static_cast<hipStream_t>(stream);
   double *part = static_cast<double *>(workspace);
-  VA_DISPATCH_MASK(mask_dtype, {
-    hipLaunchKernelGGL((value_loss_rows_kernel<MT>), dim3(B), dim3(256), 0, s, vpreds, values,
-                       returns, mask, R, cliprange_value, agg_mode, part);
-  });
-  hipLaunchKernelGGL(value_loss_finalize_kernel, dim3(1), dim3(finalize_threads(B)), 0, s, part, B, R, agg_mode,
+  double *wsum = part + B * kNQ + kTotals;
+  int64_t G = B;
+  if (stream_rows(R, reinterpret_cast<uintptr_t>(vpreds) | reinterpret_cast<uintptr_t>(values) |
+                         reinterpret_cast<uintptr_t>(returns) | reinterpret_cast<uintptr_t>(mask))) {
+    const int J = static_cast<int>((R + 255) / 256);
+    G = (B + 3) / 4;
+    VA_DISPATCH_MASK(mask_dtype, {
+      if (J <= 4)
+        hipLaunchKernelGGL((value_loss_rows_vec_kernel<MT, 4>), dim3(G), dim3(256), 0, s, vpreds, values, returns,
+                           mask, B, R, J, cliprange_value, agg_mode, part, wsum);
+      else
+        hipLaunchKernelGGL((value_loss_rows_vec_kernel<MT, 8>), dim3(G), dim3(256), 0, s, vpreds, values, returns,
+                           mask, B, R, J, cliprange_value, agg_mode, part, wsum);
+    });
+  } else {
+    VA_DISPATCH_MASK(mask_dtype, {
+      hipLaunchKernelGGL((value_loss_rows_kernel<MT>), dim3(B), dim3(256), 0, s, vpreds, values,
+                         returns, mask, R, cliprange_value, agg_mode, part, wsum);
+    });
+  }
+  hipLaunchKernelGGL(value_loss_finalize_kernel, dim3(1), dim3(finalize_threads(G)), 0, s, wsum, G, B, R, agg_mode,
                      part + B * kNQ, out);
   return check_launch("value_loss_fwd");
 }

@@ -93,6 +93,9 @@ __device__ __forceinline__ void pin4(float4 &x) {
   asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w));
 }
 __device__ __forceinline__ void pin1(uint32_t &x) { asm volatile("" : "+v"(x)); }
+// Keep the loads issued so far above the pins that follow (a pin consumes its register, so a load
+// the compiler sank below an earlier pin would wait for that pin's load first).
+__device__ __forceinline__ void loads_issued() { asm volatile("" ::: "memory"); }
 
 // The same split in two: the raw 16-byte loads (issued with the other streams' loads) and the
 // conversion (done where the values are used), so no load waits on an earlier conversion.

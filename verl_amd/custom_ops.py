@@ -159,15 +159,10 @@ logprob_entropy_fwd.register_autograd(_lp_backward, setup_context=_lp_setup)
 
 
 # =============================================================================== policy loss
-def _loss_ws(B: int, device) -> Tensor:
-    # va_agg_workspace_bytes(B) / 8 doubles: [B, 8] row partials + 8 totals, every slot written by
-    # the forward (the workspace is an op output that autograd saves for the backward)
-    return torch.empty(B * 8 + 8, dtype=_F64, device=device)
-
-
-def _policy_ws(B: int, device) -> tuple[Tensor, Tensor]:
-    # va_ppo_loss_workspace_bytes(B) / 8 doubles; the op returns the leading B * 8 + 8 (the part
-    # the backward reads, fully written); the tail is the forward's own per-workgroup scratch
+def _loss_ws(B: int, device) -> tuple[Tensor, Tensor]:
+    # va_ppo_loss_workspace_bytes(B) / 8 doubles (= va_agg_workspace_bytes): the op returns the
+    # leading B * 8 + 8 ([B, 8] row partials + 8 totals, every slot written by the forward; autograd
+    # saves it for the backward); the tail is the forward's own per-workgroup scratch
     buf = torch.empty(2 * B * 8 + 8, dtype=_F64, device=device)
     return buf, buf[: B * 8 + 8]
 
@@ -182,7 +177,7 @@ def ppo_loss_fwd(old_lp: Tensor, lp: Tensor, adv: Tensor, mask: Tensor, ref_lp: 
     if sel is not None and (sel.dtype != torch.uint8 or not sel.is_contiguous()):
         raise TypeError("ppo_loss_fwd: sel must be contiguous uint8")
     out = torch.empty(L.VA_LOSS_NOUT, dtype=_F32, device=lp.device)
-    buf, ws = _policy_ws(B, lp.device)
+    buf, ws = _loss_ws(B, lp.device)
     L.call("va_ppo_loss_fwd", K._p(old_lp), K._p(lp), K._p(adv), K._p(mask), _mcode(mask), K._p(ref_lp),
            K._p(entropy), B, R, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode, K._p(sel), mode_coef,
            K._p(out), K._p(buf), K._stream(lp))
@@ -288,8 +283,8 @@ def masked_agg_fwd(x: Tensor, mask: Tensor, mode: int) -> tuple[Tensor, Tensor]:
     _check_f32(x)
     B, R = _rows(x)
     out = torch.empty(B if mode == L.VA_REDUCE_ROW_MASKED_MEAN else 1, dtype=_F32, device=x.device)
-    ws = _loss_ws(B, x.device)
-    L.call("va_masked_agg_fwd", K._p(x), K._p(mask), _mcode(mask), B, R, mode, K._p(out), K._p(ws), K._stream(x))
+    buf, ws = _loss_ws(B, x.device)
+    L.call("va_masked_agg_fwd", K._p(x), K._p(mask), _mcode(mask), B, R, mode, K._p(out), K._p(buf), K._stream(x))
     return out, ws
 
 
@@ -537,9 +532,9 @@ def value_loss_fwd(vpreds: Tensor, values: Tensor, returns: Tensor, mask: Tensor
     _check_f32(vpreds, values, returns)
     B, R = _rows(vpreds)
     out = torch.empty(L.VA_VLOSS_NOUT, dtype=_F32, device=vpreds.device)
-    ws = _loss_ws(B, vpreds.device)
+    buf, ws = _loss_ws(B, vpreds.device)
     L.call("va_value_loss_fwd", K._p(vpreds), K._p(values), K._p(returns), K._p(mask), _mcode(mask), B, R,
-           cliprange_value, agg_mode, K._p(out), K._p(ws), K._stream(vpreds))
+           cliprange_value, agg_mode, K._p(out), K._p(buf), K._stream(vpreds))
     return out, ws
 
 
