@@ -33,6 +33,7 @@ fi
 run small_$TAG 300 python tools/small_kernels_bench.py || exit $?
 run prof_small_$TAG 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_small_$TAG -o run -- python tools/small_kernels_bench.py || exit $?
 python3 tools/prof_split.py $O/prof_small_$TAG/run_kernel_trace.csv --match va:: > $O/prof_small_$TAG.split.jsonl || true
+if [[ ${BENCH:-1} == 0 ]]; then exit 0; fi
 run bench_$TAG 900 python bench.py --steps 3 --warmup 1 --out $O/bench_$TAG.json || exit $?
 run prof_$TAG 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$TAG -o run -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 1 --out $O/bench_prof_$TAG.json || exit $?
 f=$(find $O/prof_$TAG -name '*kernel_stats.csv' | head -1)

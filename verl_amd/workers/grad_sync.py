@@ -25,6 +25,8 @@ reduce-scattered instead of all-reduced, and the updated bf16 shards are all-gat
 
 from __future__ import annotations
 
+import weakref
+
 import torch
 import torch.distributed as dist
 
@@ -51,6 +53,27 @@ def _group_params(params, bucket_bytes: int, elem_bytes: int = 4):
         groups.append(cur)
     return groups
 
+
+
+def _grad_hook(owner):
+    """A post-accumulate-grad hook that calls ``owner._on_grad`` through a weak reference: a bound
+    method stored on the parameters would keep the manager (and through it every parameter, master
+    and gradient buffer) alive in a cycle the garbage collector cannot see through the autograd
+    hooks, so a dropped worker would never free its device memory. The hook handles are removed
+    when the owner is collected."""
+    ref = weakref.WeakMethod(owner._on_grad)
+
+    def hook(p):
+        fn = ref()
+        if fn is not None:
+            fn(p)
+
+    return hook
+
+
+def _remove_hooks(handles):
+    for h in handles:
+        h.remove()
 
 class _Bucket:
     __slots__ = ("buf", "params", "pending", "handle", "index", "ready")
@@ -205,7 +228,8 @@ class GradBucketReducer(_OrderedBuckets):
         self._init_order()
         if self.world > 1:
             for p in self.params:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                self._hooks.append(p.register_post_accumulate_grad_hook(_grad_hook(self)))
+            weakref.finalize(self, _remove_hooks, self._hooks)
 
     # ------------------------------------------------------------------ hooks
     def _on_grad(self, p):
@@ -308,7 +332,8 @@ class MixedPrecisionParams(_OrderedBuckets):
             p.data = self._master_of[id(p)].data.to(compute_dtype)
         self._ready: dict = {}
         self._init_order()
-        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        self._hooks = [p.register_post_accumulate_grad_hook(_grad_hook(self)) for p in self.params]
+        weakref.finalize(self, _remove_hooks, self._hooks)
 
     def _on_grad(self, p):
         b = self._bucket_of[id(p)]
@@ -461,7 +486,8 @@ class ShardedMixedPrecisionParams(_OrderedBuckets):
                 self._bucket_of[id(p)] = b
         self._ready: dict = {}
         self._init_order()
-        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+        self._hooks = [p.register_post_accumulate_grad_hook(_grad_hook(self)) for p in self.params]
+        weakref.finalize(self, _remove_hooks, self._hooks)
 
     # ------------------------------------------------------------------ collectives
     def _collective(self, b: _Bucket):
