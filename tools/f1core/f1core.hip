@@ -474,6 +474,147 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_v5(const uint16_t *__rest
     }
 }
 
+
+// v6: persistent over a run of column tiles (as v3) with the quadrant phases of v2, but ONE barrier
+// per phase and a 2-K-step prefetch distance. Per K-step g (of the (tile, k) sequence), phase s:
+//   reads (issued first, retired by lgkmcnt(0) BEFORE the barrier, so after it every wave's reads of
+//   this phase are done): s1 A0 + B0 frags, s2 B1, s3 A1, s4 none
+//   s4 only: vmcnt(8) before the barrier -> every half of step g+1 has landed (the 4 halves of step
+//   g+2 issued in s1..s3 stay in flight)
+//   raw s_barrier
+//   DMA into the halves this phase just finished reading, for step g+2: s1 A0 + B0, s2 B1, s3 A1
+//   16 MFMAs of quadrant s: (0,0) (0,1) (1,0) (1,1)
+// A frags of qm live across s1-s2 / s3-s4, B frags of both qn across the step.
+__global__ __launch_bounds__(kThreads, 1) void gemm_nt_v6(const uint16_t *__restrict__ A, const uint16_t *__restrict__ B,
+                                                        int64_t M, int64_t N, int K, int tiles_per_split,
+                                                        float *__restrict__ rowsum) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 4 * kHalf];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int64_t tiles_n = (N + BN - 1) / BN;
+  const int64_t m0 = static_cast<int64_t>(blockIdx.x) * BM;
+  const int64_t tn_begin = static_cast<int64_t>(blockIdx.y) * tiles_per_split;
+  int64_t tn_end = tn_begin + tiles_per_split;
+  if (tn_end > tiles_n) tn_end = tiles_n;
+  if (tn_begin >= tn_end) return;
+  const int nk = K / BK;
+  const int64_t nsteps = (tn_end - tn_begin) * nk;
+
+  auto issue = [&](int64_t g, int h) {  // half h of step g into buffer g & 1
+    uint16_t *img = half_img(lds, static_cast<int>(g & 1), h);
+    const int kt = static_cast<int>(g % nk);
+    const int64_t tn = tn_begin + g / nk;
+    if (h < 2) stage_half(A, m0 + h * 128, M, K, kt * BK, img, wave, lane);
+    else stage_half(B, tn * BN + (h - 2) * 128, N, K, kt * BK, img, wave, lane);
+  };
+  f32x4 acc[2][2][4][2];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[a][c][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  zero_acc();
+  bf16x8 fa[4][2], fb[2][2][2];
+  auto read_a = [&](const uint16_t *img) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        fa[i][s] = *reinterpret_cast<const bf16x8 *>(img + img_off(wr * 64 + i * 16 + (lane & 15), s * 4 + (lane >> 4)));
+  };
+  auto read_b = [&](const uint16_t *img, int qn) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        fb[qn][j][s] =
+            *reinterpret_cast<const bf16x8 *>(img + img_off(wc * 32 + j * 16 + (lane & 15), s * 4 + (lane >> 4)));
+  };
+  auto mfma = [&](int qm, int qn) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qm][qn][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[qn][j][s], acc[qm][qn][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: steps 0 and 1 in full; wait for step 0
+  issue(0, 0), issue(0, 2), issue(0, 3), issue(0, 1);
+  if (nsteps > 1) {
+    issue(1, 0), issue(1, 2), issue(1, 3), issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  for (int64_t g = 0; g < nsteps; ++g) {
+    const int cur = static_cast<int>(g & 1);
+    const bool pre = g + 2 < nsteps;
+    // s1: quadrant (0, 0)
+    read_a(half_img(lds, cur, 0));
+    read_b(half_img(lds, cur, 2), 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (pre) issue(g + 2, 0), issue(g + 2, 2);
+    mfma(0, 0);
+    // s2: quadrant (0, 1)
+    read_b(half_img(lds, cur, 3), 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (pre) issue(g + 2, 3);
+    mfma(0, 1);
+    // s3: quadrant (1, 0)
+    read_a(half_img(lds, cur, 1));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (pre) issue(g + 2, 1);
+    mfma(1, 0);
+    // s4: quadrant (1, 1); step g + 1 must have landed before this barrier
+    if (pre) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    mfma(1, 1);
+    if (g % nk == nk - 1) {  // tile done
+      const int64_t n0 = (tn_begin + g / nk) * BN;
+      const int64_t tn = tn_begin + g / nk;
+#pragma unroll
+      for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int64_t row = m0 + qm * 128 + wr * 64 + i * 16 + (lane >> 4) * 4 + e;
+            float srow = 0.f;
+#pragma unroll
+            for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                const int64_t col = n0 + qn * 128 + wc * 32 + j * 16 + (lane & 15);
+                srow += col < N ? acc[qm][qn][i][j][e] : 0.f;
+              }
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) srow += __shfl_xor(srow, o, 64);
+            if ((lane & 15) == 0 && row < M) rowsum[(tn * 4 + wc) * M + row] = srow;
+          }
+      zero_acc();
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int f1core_gemm_nt(int variant, const void *A, const void *B, int64_t M, int64_t N, int K, float *rowsum,
@@ -498,6 +639,17 @@ extern "C" int f1core_gemm_nt(int variant, const void *A, const void *B, int64_t
       const int per = static_cast<int>((tn + splits - 1) / splits);
       splits = static_cast<int>((tn + per - 1) / per);
       hipLaunchKernelGGL(gemm_nt_v3, dim3(static_cast<unsigned>(tm), static_cast<unsigned>(splits)), dim3(kThreads), 0,
+                         s, static_cast<const uint16_t *>(A), static_cast<const uint16_t *>(B), M, N, K, per, rowsum);
+      break;
+    }
+    case 6: {
+      const int64_t tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+      int splits = static_cast<int>((1024 + tm - 1) / tm);
+      if (splits > tn) splits = static_cast<int>(tn);
+      if (splits < 1) splits = 1;
+      const int per = static_cast<int>((tn + splits - 1) / splits);
+      splits = static_cast<int>((tn + per - 1) / per);
+      hipLaunchKernelGGL(gemm_nt_v6, dim3(static_cast<unsigned>(tm), static_cast<unsigned>(splits)), dim3(kThreads), 0,
                          s, static_cast<const uint16_t *>(A), static_cast<const uint16_t *>(B), M, N, K, per, rowsum);
       break;
     }

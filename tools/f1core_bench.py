@@ -46,7 +46,7 @@ def main():
             ref = A.float() @ B.float().T
             rsum = rs.view(-1, M).sum(0)
             rerr = (rsum - ref.sum(1)).abs().max().item()
-            if v == 3:  # no full-C output: the row sums carry the check
+            if v in (3, 6):  # no full-C output: the row sums carry the check
                 err, tol = rerr, 1e-3 * ref.sum(1).abs().max().item() + 1e-2
             else:
                 err, tol = (C - ref).abs().max().item(), 1e-3 * ref.abs().max().item()
