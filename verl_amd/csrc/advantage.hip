@@ -827,20 +827,27 @@ __global__ __launch_bounds__(kMergeThreads) void whiten_stats_apply_kernel(float
                                                                            float *__restrict__ stats, int64_t nq,
                                                                            int nt) {
   __shared__ double sh[kMergeThreads * 3];
+  // chunks of U quads per thread; the first chunk's loads are issued BEFORE the merge of the
+  // partials (they do not depend on the statistics), so the merge's dependent loads and barriers
+  // run under their latency instead of in front of the stream
+  constexpr int U = 8;
+  const int64_t chunk = static_cast<int64_t>(blockDim.x) * U;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * chunk;
+  int64_t c0 = static_cast<int64_t>(blockIdx.x) * chunk;
+  float4 a[U];
+  auto load_chunk = [&](int64_t c) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // clamped, unconditional loads: all U in flight at once
+      const int64_t i = c + static_cast<int64_t>(u) * blockDim.x + threadIdx.x;
+      a[u] = ld4(x + 4 * (i < nq ? i : nq - 1), false);
+    }
+  };
+  if (c0 < nq) load_chunk(c0);
   const Moments tot = block_merge(part, 0, K, step, sh);
   float mean, rstd;
   const bool writer = blockIdx.x == 0 && threadIdx.x == 0;
   whiten_stats_of(tot, writer ? merged : nullptr, stats, mean, rstd);
-  // chunks of U quads per thread, all U loads issued before the first store
-  constexpr int U = 8;
-  const int64_t chunk = static_cast<int64_t>(blockDim.x) * U;
-  for (int64_t c0 = static_cast<int64_t>(blockIdx.x) * chunk; c0 < nq; c0 += static_cast<int64_t>(gridDim.x) * chunk) {
-    float4 a[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {  // clamped, unconditional loads: all U in flight at once
-      const int64_t i = c0 + static_cast<int64_t>(u) * blockDim.x + threadIdx.x;
-      a[u] = ld4(x + 4 * (i < nq ? i : nq - 1), false);
-    }
+  for (; c0 < nq; c0 += stride) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t i = c0 + static_cast<int64_t>(u) * blockDim.x + threadIdx.x;
@@ -850,6 +857,7 @@ __global__ __launch_bounds__(kMergeThreads) void whiten_stats_apply_kernel(float
         st4(x + 4 * i, v, nt & 4);
       }
     }
+    if (c0 + stride < nq) load_chunk(c0 + stride);
   }
 }
 
