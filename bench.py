@@ -372,12 +372,22 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    prof_path = os.environ.get("VA_BENCH_CPROFILE")  # host-side profile of the timed steps (diagnostics)
+    prof = None
+    if prof_path and rank == 0:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     metrics = None
     for i in range(args.steps):
         metrics = step()
         log(rank, f"timed step {i} issued")
     torch.cuda.synchronize()
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(prof_path)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0

@@ -326,6 +326,16 @@ def masked_aggregate(x, mask, mode: int):
 
 
 # =============================================================================== advantages
+def h2d(a: np.ndarray, dtype, device) -> torch.Tensor:
+    """Host array -> device tensor without draining the stream: a copy from pageable memory waits
+    for the work already queued on the stream (a host sync in the middle of the step), so the
+    array goes through pinned memory (torch's caching host allocator) and an async copy."""
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=dtype))
+    if torch.device(device).type != "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 def group_csr(index, device) -> tuple[torch.Tensor, torch.Tensor, int, int]:
     """Host-side uid grouping (core_algos.py:290-291) into CSR: (order, offsets, G, max_size).
 
@@ -341,9 +351,7 @@ def group_csr(index, device) -> tuple[torch.Tensor, torch.Tensor, int, int]:
     counts = np.bincount(inverse)
     offsets = np.zeros(len(counts) + 1, dtype=np.int32)
     np.cumsum(counts, out=offsets[1:])
-    order_t = torch.from_numpy(order).to(device)
-    offs_t = torch.from_numpy(offsets).to(device)
-    return order_t, offs_t, int(len(counts)), int(counts.max())
+    return h2d(order, np.int32, device), h2d(offsets, np.int32, device), int(len(counts)), int(counts.max())
 
 
 def outcome_advantage(token_level_rewards, response_mask, index, epsilon: float, estimator: int):

@@ -108,7 +108,9 @@ def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device, pad_multiple: int =
     sel_hidden = packed_of[pos[valid]]
 
     def dev(a, dt):
-        return torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(device, non_blocking=True)
+        from ... import kernels as K
+
+        return K.h2d(a, dt, device)
 
     return _Packing(
         token_idx=dev(token_idx, np.int64),
@@ -131,6 +133,7 @@ class DataParallelPPOActor(BasePPOActor):
         self.actor_module = actor_module
         self.actor_optimizer = actor_optimizer
         self.grad_reducer = grad_reducer
+        self._am_cache = None  # (key, host attention mask): see _mask_host
         self.use_remove_padding = self.config.get("use_remove_padding", True)
         self.ulysses_sequence_parallel_size = self.config.get("ulysses_sequence_parallel_size", 1)
         if self.ulysses_sequence_parallel_size != 1:
@@ -243,13 +246,28 @@ class DataParallelPPOActor(BasePPOActor):
             return False
         return bool(self.use_fused_kernels or (self.fused_logprob_no_grad and not torch.is_grad_enabled()))
 
-    def _plans(self, data: DataProto, sizes: list[int] = None, idx_lists: list[list[int]] = None) -> list:
+    def _mask_host(self, am_t: torch.Tensor, refresh: bool) -> np.ndarray:
+        """Host copy of the attention mask. compute_log_prob (the step's first pass over the
+        batch) always copies it (refresh=True: the GPU is idle there anyway); update_policy reuses
+        that copy while the tensor is the same unmodified one (same storage, shape and version):
+        a second D2H copy at the start of the update would drain the queued old-logp pass and
+        advantage work and leave the GPU idle while the host plans the update."""
+        key = (am_t.data_ptr(), tuple(am_t.shape), am_t._version, am_t.device)
+        if not refresh and self._am_cache is not None and self._am_cache[0] == key:
+            return self._am_cache[1]
+        am = am_t.cpu().numpy()
+        self._am_cache = (key, am)
+        return am
+
+    def _plans(self, data: DataProto, sizes: list[int] = None, idx_lists: list[list[int]] = None,
+               am: np.ndarray = None) -> list:
         """Packing plans of consecutive micro-batches of ``sizes`` rows, or of the dynamic
-        micro-batches' row index lists, from one D2H copy of the attention mask."""
+        micro-batches' row index lists, from one host copy of the attention mask."""
         n_mb = len(sizes) if idx_lists is None else len(idx_lists)
         if not self.use_remove_padding:
             return [None] * n_mb
-        am = data.batch["attention_mask"].cpu().numpy()
+        if am is None:
+            am = data.batch["attention_mask"].cpu().numpy()
         R = data.batch["responses"].size(-1)
         dev = data.batch["input_ids"].device
         if idx_lists is not None:
@@ -279,15 +297,8 @@ class DataParallelPPOActor(BasePPOActor):
             params = (self.grad_reducer.optimizer_params() if self.grad_reducer is not None
                       else list(self.actor_module.parameters()))
             grad_norm = torch.nn.utils.clip_grad_norm_(params, max_norm=self.config.grad_clip, foreach=True)
-        if not torch.isfinite(grad_norm):
-            rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
-            print(f"WARN: rank {rank} grad_norm is not finite: {grad_norm}")
-            self._zero_grad()
-        else:
-            self.actor_optimizer.step()
-            if self.grad_reducer is not None:
-                self.grad_reducer.after_step()
-        return grad_norm
+        return step_unless_nonfinite(self.actor_optimizer, grad_norm, self._zero_grad,
+                                     self.grad_reducer.after_step if self.grad_reducer is not None else None)
 
     # ------------------------------------------------------------------ API
     @torch.no_grad()
@@ -298,14 +309,15 @@ class DataParallelPPOActor(BasePPOActor):
         temperature = data.meta_info["temperature"]
         use_dynamic_bsz = data.meta_info["use_dynamic_bsz"]
         data = data.select(batch_keys=["responses", "input_ids", "attention_mask", "position_ids"])
+        am = self._mask_host(data.batch["attention_mask"], refresh=True) if self.use_remove_padding else None
         if use_dynamic_bsz:
             # dp_actor.py:321-323: micro-batches cut by a token budget, restored afterwards
             max_token_len = data.meta_info["max_token_len"] * self.ulysses_sequence_parallel_size
             micro_batches, batch_idx_list = prepare_dynamic_batch(data, max_token_len=max_token_len)
-            plans = self._plans(data, idx_lists=batch_idx_list)
+            plans = self._plans(data, idx_lists=batch_idx_list, am=am)
         else:
             micro_batches = data.split(micro_batch_size)
-            plans = self._plans(data, [len(m) for m in micro_batches])
+            plans = self._plans(data, [len(m) for m in micro_batches], am=am)
         lps, ents = [], []
         for mb, plan in zip(micro_batches, plans, strict=True):
             ent, lp = self._forward_micro_batch(mb.batch, temperature, calculate_entropy, plan)
@@ -331,6 +343,7 @@ class DataParallelPPOActor(BasePPOActor):
         if cfg.use_kl_loss:
             keys.append("ref_log_prob")
         data = data.select(batch_keys=keys)
+        am_full = self._mask_host(data.batch["attention_mask"], refresh=False) if self.use_remove_padding else None
         mini_batches = data.split(cfg.ppo_mini_batch_size)
         if not cfg.use_dynamic_bsz:
             self.gradient_accumulation = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
@@ -344,15 +357,18 @@ class DataParallelPPOActor(BasePPOActor):
 
         dev_metrics: dict[str, list] = {}
         for _ in range(cfg.ppo_epochs):
+            row0 = 0
             for mini in mini_batches:
+                am = am_full[row0 : row0 + len(mini)] if am_full is not None else None  # split keeps row order
+                row0 += len(mini)
                 if cfg.use_dynamic_bsz:
                     # dp_actor.py:382-384
                     max_token_len = cfg.ppo_max_token_len_per_gpu * self.ulysses_sequence_parallel_size
                     micro_batches, idx_lists = prepare_dynamic_batch(mini, max_token_len=max_token_len)
-                    plans = self._plans(mini, idx_lists=idx_lists)
+                    plans = self._plans(mini, idx_lists=idx_lists, am=am)
                 else:
                     micro_batches = mini.split(cfg.ppo_micro_batch_size_per_gpu)
-                    plans = self._plans(mini, [len(m) for m in micro_batches])
+                    plans = self._plans(mini, [len(m) for m in micro_batches], am=am)
                 self._zero_grad()
                 for i, (mb, plan) in enumerate(zip(micro_batches, plans, strict=True)):
                     b = mb.batch
@@ -415,19 +431,57 @@ class DataParallelPPOActor(BasePPOActor):
         return _to_host(dev_metrics)
 
 
+def step_unless_nonfinite(optimizer, grad_norm: torch.Tensor, zero_grad, after_step=None):
+    """dp_actor.py:272-288: step unless the clipped-gradient norm is not finite (then warn and
+    drop the gradients). A fused device optimizer skips the step ON the device (its found_inf
+    input, the GradScaler mechanism: parameters, moments and step counts untouched), so the
+    update needs no host sync here; the warning is printed when the metrics reach the host
+    (``_to_host`` sees the non-finite grad_norm) and the dropped gradients are zeroed by the
+    next mini-batch's zero_grad as in the reference. Other optimizers keep the host check."""
+    fused = bool(optimizer.defaults.get("fused")) and grad_norm.is_cuda
+    if fused:
+        optimizer.found_inf = (~torch.isfinite(grad_norm)).to(torch.float32).reshape(())  # 0-d, as the step counts
+        try:
+            optimizer.step()
+        finally:
+            optimizer.found_inf = None
+        if after_step is not None:
+            after_step()  # re-derives the compute weights from unchanged masters when skipped
+        return grad_norm
+    if not torch.isfinite(grad_norm):
+        rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+        print(f"WARN: rank {rank} grad_norm is not finite: {grad_norm}")
+        zero_grad()
+    else:
+        optimizer.step()
+        if after_step is not None:
+            after_step()
+    return grad_norm
+
+
 def _to_host(dev_metrics: dict) -> dict:
     """One device->host transfer for every metric of the update (the reference calls .item()
-    per micro-batch, dp_actor.py:462-483)."""
-    keys, vals = [], []
-    for k, lst in dev_metrics.items():
-        for v in lst:
-            keys.append(k)
-            vals.append(v.float().reshape(()) if isinstance(v, torch.Tensor) else torch.tensor(float(v)))
-    if not vals:
-        return {}
-    dev = next((v.device for v in vals if v.is_cuda), torch.device("cpu"))
-    flat = torch.stack([v.to(dev) for v in vals]).cpu().tolist()
+    per micro-batch, dp_actor.py:462-483); host values (e.g. kl_coef) never go to the device."""
+    dev_keys, dev_vals, out_pos = [], [], []
     out: dict[str, list] = {}
-    for k, v in zip(keys, flat, strict=True):
-        out.setdefault(k, []).append(v)
+    for k, lst in dev_metrics.items():
+        dst = out.setdefault(k, [])
+        for v in lst:
+            if isinstance(v, torch.Tensor):
+                dev_keys.append(k)
+                out_pos.append(len(dst))
+                dev_vals.append(v.detach().float().reshape(()))
+                dst.append(None)
+            else:
+                dst.append(float(v))
+    if dev_vals:
+        devs = {v.device for v in dev_vals}
+        flat = torch.stack([v.to(dev_vals[0].device) for v in dev_vals]).cpu().tolist() if len(devs) == 1 else \
+            [float(v.cpu()) for v in dev_vals]
+        for k, i, v in zip(dev_keys, out_pos, flat, strict=True):
+            out[k][i] = v
+    for k, lst in out.items():
+        if k.endswith("grad_norm") and not all(np.isfinite(g) for g in lst):
+            rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+            print(f"WARN: rank {rank} {k} is not finite: {lst} (optimizer step skipped)")
     return out

@@ -26,7 +26,7 @@ from ... import kernels as K
 from ...protocol import DataProto
 from ...utils.seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
 from ..actor import attention
-from ..actor.dp_actor import _plan_packing, _to_host, append_to_dict, packed_mask_arg
+from ..actor.dp_actor import _plan_packing, _to_host, append_to_dict, packed_mask_arg, step_unless_nonfinite
 from .base import BasePPOCritic
 
 __all__ = ["DataParallelPPOCritic"]
@@ -137,17 +137,15 @@ class DataParallelPPOCritic(BasePPOCritic):
         assert self.config.grad_clip is not None
         if self.grad_reducer is not None:
             self.grad_reducer.finish_sync()
-        params = (self.grad_reducer.optimizer_params() if self.grad_reducer is not None
-                  else list(self.critic_module.parameters()))
-        grad_norm = torch.nn.utils.clip_grad_norm_(params, max_norm=self.config.grad_clip, foreach=True)
-        if not torch.isfinite(grad_norm):
-            print(f"WARN: grad_norm is not finite: {grad_norm}")
-            self._zero_grad()
+        if self.grad_reducer is not None and hasattr(self.grad_reducer, "clip_grad_norm_"):
+            # sharded optimizer state: global norm over the ranks' shards (fsdp_utils.py:503-516)
+            grad_norm = self.grad_reducer.clip_grad_norm_(self.config.grad_clip)
         else:
-            self.critic_optimizer.step()
-            if self.grad_reducer is not None:
-                self.grad_reducer.after_step()
-        return grad_norm
+            params = (self.grad_reducer.optimizer_params() if self.grad_reducer is not None
+                      else list(self.critic_module.parameters()))
+            grad_norm = torch.nn.utils.clip_grad_norm_(params, max_norm=self.config.grad_clip, foreach=True)
+        return step_unless_nonfinite(self.critic_optimizer, grad_norm, self._zero_grad,
+                                     self.grad_reducer.after_step if self.grad_reducer is not None else None)
 
     # ------------------------------------------------------------------ API
     @torch.no_grad()
