@@ -133,7 +133,7 @@ class DataParallelPPOActor(BasePPOActor):
         self.actor_module = actor_module
         self.actor_optimizer = actor_optimizer
         self.grad_reducer = grad_reducer
-        self._am_cache = None  # (key, host attention mask): see _mask_host
+        self._am_cache = None  # (key, device mask, host copy): see _mask_host
         self.use_remove_padding = self.config.get("use_remove_padding", True)
         self.ulysses_sequence_parallel_size = self.config.get("ulysses_sequence_parallel_size", 1)
         if self.ulysses_sequence_parallel_size != 1:
@@ -252,11 +252,13 @@ class DataParallelPPOActor(BasePPOActor):
         that copy while the tensor is the same unmodified one (same storage, shape and version):
         a second D2H copy at the start of the update would drain the queued old-logp pass and
         advantage work and leave the GPU idle while the host plans the update."""
+        # the cache holds the device tensor itself, so its storage cannot be freed and reused by
+        # another batch's mask while the key (pointer, shape, in-place version) is compared
         key = (am_t.data_ptr(), tuple(am_t.shape), am_t._version, am_t.device)
         if not refresh and self._am_cache is not None and self._am_cache[0] == key:
-            return self._am_cache[1]
+            return self._am_cache[2]
         am = am_t.cpu().numpy()
-        self._am_cache = (key, am)
+        self._am_cache = (key, am_t, am)
         return am
 
     def _plans(self, data: DataProto, sizes: list[int] = None, idx_lists: list[list[int]] = None,
