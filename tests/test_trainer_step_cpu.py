@@ -125,3 +125,24 @@ def test_reduce_metrics_matches_reference_rules():
 
     out = reduce_metrics({"loss": [1.0, 2.0, 3.0], "max_reward": [5.0, 8.0, 6.0], "min_error": [0.1, 0.05, 0.2]})
     assert out == {"loss": 2.0, "max_reward": 8.0, "min_error": 0.05}
+
+
+def test_attention_mask_host_copy_reuse_and_invalidation():
+    """The update reuses the host copy of the attention mask that compute_log_prob took in the same
+    step (no second D2H drain), and never a stale one: an in-place change or another tensor
+    invalidates it, and refresh=True always copies."""
+    from types import SimpleNamespace
+
+    from verl_amd.workers.actor.dp_actor import DataParallelPPOActor
+
+    me = SimpleNamespace(_am_cache=None)
+    am = torch.ones(4, 6, dtype=torch.int64)
+    a1 = DataParallelPPOActor._mask_host(me, am, refresh=True)
+    assert DataParallelPPOActor._mask_host(me, am, refresh=False) is a1  # reused
+    am[0, 0] = 0  # in place: version bump
+    a2 = DataParallelPPOActor._mask_host(me, am, refresh=False)
+    assert a2 is not a1 and a2[0, 0] == 0
+    other = torch.zeros(4, 6, dtype=torch.int64)
+    a3 = DataParallelPPOActor._mask_host(me, other, refresh=False)
+    assert a3 is not a2 and a3.sum() == 0
+    assert DataParallelPPOActor._mask_host(me, other, refresh=True) is not a3  # refresh copies
