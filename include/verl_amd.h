@@ -421,6 +421,9 @@ int va_flash_attn_bwd(const void *q, const void *k, const void *v, const void *o
  * dY / X row-major with leading dimensions ldy / ldx (multiples of 8); M, N multiples of 128.
  * splits > 1 cuts the tokens into that many slices whose fp32 partial tiles go to `workspace`
  * (va_wgrad_workspace_bytes) and are summed in slice order (deterministic) before the rounding.
+ * EXPERIMENTAL, not on the product path: the actor's weight gradients run in hipBLASLt
+ * (kernels.weight_grad); this kernel (0.61-0.72 PF/s) stays exported and parity-tested for the
+ * GEMM work DESIGN.md §7 lists, and is selected by nothing.
  * ------------------------------------------------------------------------------------ */
 int64_t va_wgrad_workspace_bytes(int64_t M, int64_t N, int splits);
 int va_wgrad_bf16(const void *dy, int64_t ldy, const void *x, int64_t ldx, int64_t T, int64_t M, int64_t N,

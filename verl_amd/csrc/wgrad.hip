@@ -1,7 +1,9 @@
 // Weight-gradient GEMM of the actor's linear layers on MI355X: dW[M, N] = dY[T, M]^T X[T, N]
 // (M = out_features, N = in_features, K = T tokens; bf16 in, fp32 accumulate, bf16 out).
-// Not a §8 row: it replaces the hipBLASLt calls of torch's linear backward for this shape class
-// (huge K, small output), which run at 0.43-0.89 PF/s there (profiles/r01/wgrad_layout_T151552.log).
+// EXPERIMENTAL, not on the product path (selected by nothing; the actor's weight gradients run in
+// hipBLASLt). Not a §8 row: written to replace the hipBLASLt calls of torch's linear backward for
+// this shape class (huge K, small output), which run at 0.43-0.89 PF/s there
+// (profiles/r01/wgrad_layout_T151552.log); at 0.61-0.72 PF/s it does not yet.
 //
 // Both operands are k-strided in memory (rows of dY / X are tokens), so the workgroup stages each
 // 64-token step as [k][m] / [k][n] LDS images (XOR-swizzled 16-B chunks, the attention kernels'

@@ -620,8 +620,9 @@ def wgrad_splits(T: int, n_out: int, n_in: int) -> int:
 
 
 def wgrad_gemm(dy2, x2, splits: int = 1):
-    """dW = dY^T X by the gfx950 weight-gradient kernel (wgrad.hip): bf16 [T, M] x [T, N] -> bf16
-    [M, N], fp32 accumulation, split-K partials summed in slice order."""
+    """EXPERIMENTAL (selected by nothing; weight_grad below uses hipBLASLt): dW = dY^T X by the
+    gfx950 weight-gradient kernel (wgrad.hip): bf16 [T, M] x [T, N] -> bf16 [M, N], fp32
+    accumulation, split-K partials summed in slice order."""
     _require_device(dy2, x2)
     T, M = dy2.shape
     N = x2.shape[1]
