@@ -156,7 +156,9 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   sums in another order);
  *   VA_TUNE_WHITEN_SLICE_MIN / VA_TUNE_WHITEN_GRID (va_gae_advantage_return): partial count above
  *   which partials are merged in parallel slices first (default 4,096) and the statistics +
- *   whitening launch's grid cap (default 2,048); only the fp64 merge order changes. */
+ *   whitening launch's grid cap (default 2,048); only the fp64 merge order changes;
+ *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
+ *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3
@@ -173,6 +175,7 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_LOSS_VEC 14
 #define VA_TUNE_WHITEN_SLICE_MIN 15
 #define VA_TUNE_WHITEN_GRID 16
+#define VA_TUNE_LINEAR_LOGPROB_TILE 17
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

@@ -16,6 +16,17 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.fixture(autouse=True, params=[256, 128], ids=["tile256", "tile128"])
+def tile(request):
+    """Every case runs on both forward kernels (VA_TUNE_LINEAR_LOGPROB_TILE): the 256 x 256
+    LDS-DMA one (default) and the 128 x 128 register-staged one."""
+    from verl_amd import _lib as L
+
+    L.call("va_set_tuning", L.VA_TUNE_LINEAR_LOGPROB_TILE, request.param)
+    yield request.param
+    L.call("va_set_tuning", L.VA_TUNE_LINEAR_LOGPROB_TILE, 256)
+
+
 def _exact_inputs(N, H, V, seed):
     g = torch.Generator().manual_seed(seed)
     h = (torch.randint(-4, 5, (N, H), generator=g).float() / 8).to(torch.bfloat16)

@@ -33,7 +33,7 @@ VA_TUNE_FWD_WAVES_PER_ROW, VA_TUNE_BWD_WAVES_PER_ROW, VA_TUNE_NONTEMPORAL, VA_TU
 VA_TUNE_FLASH_GROUPED_DKDV, VA_TUNE_GAE_VARIANT, VA_TUNE_BWD_FLAT, VA_TUNE_SWIGLU_STREAM = 5, 6, 7, 8
 VA_TUNE_FLASH_DKDV_QT, VA_TUNE_FLASH_DQ_KB, VA_TUNE_FLASH_FWD_KB, VA_TUNE_GAE_PARTIALS = 9, 10, 11, 12
 VA_TUNE_GAE_NT, VA_TUNE_LOSS_VEC = 13, 14
-VA_TUNE_WHITEN_SLICE_MIN, VA_TUNE_WHITEN_GRID = 15, 16
+VA_TUNE_WHITEN_SLICE_MIN, VA_TUNE_WHITEN_GRID, VA_TUNE_LINEAR_LOGPROB_TILE = 15, 16, 17
 
 _P = c_void_p
 _SIGNATURES: dict[str, tuple] = {

@@ -231,6 +231,192 @@ __global__ __launch_bounds__(256, 2) void linear_logprob_tiles_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 256 x 256 variant (VA_TUNE_LINEAR_LOGPROB_TILE = 256): 8 waves (2 x 4, 128 rows x 64 vocab each,
+// 8 x 4 v_mfma_f32_16x16x32_bf16 blocks), both operands staged by LDS-DMA (global_load_lds, 16 B
+// per lane) into two lane-linear buffers whose 16-byte chunk c of row r sits at c ^ ((r >> 1) & 7)
+// (swizzled on the global source address: conflict-free fragment reads), persistent over the
+// workgroup's vocab tiles with the next tile's first K-step staged during the current tile's last
+// (tools/f1core: this core runs the plain GEMM at 1,038 vs 825-865 TF/s for the 128 x 128 one).
+// Per finished tile each 16-lane group reduces its row's 64 logits (4 per lane) to (max, sum exp,
+// sum exp * x); the 4 waves sharing a row leave them in LDS and one thread per row folds them into
+// the row's running state, in fixed order.
+constexpr int TB = 256, TK = 64, T_THREADS = 512;
+
+// All-reduce over the 16 lanes of a row group with DPP moves (full-rate VALU) instead of
+// ds_bpermute (an LDS round trip each): quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror and
+// row_mirror; every step pairs values commutatively, so all 16 lanes end bitwise equal.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float red16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  return fmaxf(v, dpp_f<0x140>(v));
+}
+__device__ __forceinline__ float red16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  return v + dpp_f<0x140>(v);
+}
+constexpr int T_TILE = TB * TK;  // bf16 elements of one operand's K-step image
+
+__device__ __forceinline__ int t_img_off(int row, int c) { return row * TK + ((c ^ ((row >> 1) & 7)) << 3); }
+
+__device__ __forceinline__ void t_stage(const uint16_t *__restrict__ src, int64_t row0, int64_t nrows, int64_t ld,
+                                        int k0, uint16_t *img, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int g = wave * 4 + i;  // 32 groups of 8 rows (1 KB each)
+    const int row = g * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((row >> 1) & 7);
+    int64_t gr = row0 + row;
+    if (gr >= nrows) gr = nrows - 1;  // clamped rows / columns are computed and discarded
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + gr * ld + k0 + lc * 8), img + g * 8 * TK,
+                                     16, 0, 0);
+  }
+}
+
+template <bool SCALE>
+__global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_tiles256_kernel(
+    const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
+    const int64_t *__restrict__ labels, int64_t N, int K, int64_t V, int tiles_per_split, float temperature,
+    float *__restrict__ part, float *__restrict__ label_logit) {
+  // ONE LDS array (a second __shared__ object can cost a vmcnt(0) per K-step): 2 staging buffers
+  // of (hidden, weight) images, then per-row running state, the 4 waves' tile partials, labels
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE + 2 * (TB * 3 + 4 * TB * 3 + 2 * TB)];
+  float *s_state = reinterpret_cast<float *>(lds + 2 * 2 * T_TILE);  // [TB][3] m, s, t
+  float *s_part = s_state + TB * 3;                                   // [4 wc][TB][3]
+  float *s_lablogit = s_part + 4 * TB * 3;                            // [TB]
+  int *s_label = reinterpret_cast<int *>(s_lablogit + TB);            // [TB]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * TB;
+  const int64_t n_vt = (V + TB - 1) / TB;
+  const int64_t vt_begin = static_cast<int64_t>(blockIdx.y) * tiles_per_split;
+  int64_t vt_end = vt_begin + tiles_per_split;
+  if (vt_end > n_vt) vt_end = n_vt;
+  if (tid < TB) {
+    const int64_t r = row0 + tid;
+    const int64_t lab = r < N ? labels[r] : -1;
+    s_label[tid] = (lab >= 0 && lab < V) ? static_cast<int>(lab) : -1;
+    s_lablogit[tid] = 0.f;
+    s_state[tid * 3 + 0] = -INFINITY;
+    s_state[tid * 3 + 1] = 0.f;
+    s_state[tid * 3 + 2] = 0.f;
+  }
+  const int nk = K / TK;
+  const int64_t nsteps = vt_begin < vt_end ? (vt_end - vt_begin) * nk : 0;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nsteps > 0) {
+    t_stage(hid, row0, N, ldh, 0, lds, wave, lane);
+    t_stage(w, vt_begin * TB, V, ldw, 0, lds + T_TILE, wave, lane);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  for (int64_t st = 0; st < nsteps; ++st) {
+    const int buf = static_cast<int>(st & 1);
+    const int kt = static_cast<int>(st % nk);
+    const int64_t vt = vt_begin + st / nk;
+    const uint16_t *la = lds + buf * 2 * T_TILE;
+    const uint16_t *lb = la + T_TILE;
+    if (st + 1 < nsteps) {
+      uint16_t *na = lds + (buf ^ 1) * 2 * T_TILE;
+      t_stage(hid, row0, N, ldh, static_cast<int>((st + 1) % nk) * TK, na, wave, lane);
+      t_stage(w, (vt_begin + (st + 1) / nk) * TB, V, ldw, static_cast<int>((st + 1) % nk) * TK, na + T_TILE, wave,
+              lane);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = s * 4 + (lane >> 4);
+      bf16x8 fa[8], fb[4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8 *>(la + t_img_off(wr * 128 + i * 16 + (lane & 15), c));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8 *>(lb + t_img_off(wc * 64 + j * 16 + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt == nk - 1) {
+      // ---- epilogue of vocab tile vt: lane holds rows wr*128 + i*16 + (lane>>4)*4 + e, columns
+      //      vt*256 + wc*64 + j*16 + (lane&15); the 16 lanes of a group share the row
+      const int col0 = static_cast<int>(vt * TB) + wc * 64 + (lane & 15);  // V < 2^31
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int lr = wr * 128 + i * 16 + (lane >> 4) * 4 + e;
+          const int lab = s_label[lr];
+          float x[4];
+          float cm = -INFINITY;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int col = col0 + j * 16;
+            float v = round_bf16(acc[i][j][e]);  // the bf16 logits of the unfused path
+            if constexpr (SCALE) v = round_bf16(v / temperature);
+            if (col >= static_cast<int>(V)) v = -INFINITY;
+            if (col == lab) s_lablogit[lr] = v;
+            x[j] = v;
+            cm = fmaxf(cm, v);
+          }
+          cm = red16_max(cm);
+          const float nb = base_of(cm);
+          float ss = 0.f, tt = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float ex = __builtin_amdgcn_exp2f(fmaf(x[j], kLog2eF, -nb));
+            ss += ex;
+            tt = fmaf(ex, x[j] == -INFINITY ? 0.f : x[j], tt);
+          }
+          ss = red16_sum(ss);
+          tt = red16_sum(tt);
+          if ((lane & 15) == 0) {
+            float *pp = s_part + (wc * TB + lr) * 3;
+            pp[0] = cm, pp[1] = ss, pp[2] = tt;
+          }
+        }
+      __syncthreads();
+      if (tid < TB) {  // fold the 4 column slices of the tile into the row's state, wc order
+        RowAcc a{s_state[tid * 3 + 0], s_state[tid * 3 + 1], s_state[tid * 3 + 2]};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float *pp = s_part + (q * TB + tid) * 3;
+          merge_state(a, pp[0], pp[1], pp[2]);
+        }
+        s_state[tid * 3 + 0] = a.m, s_state[tid * 3 + 1] = a.s, s_state[tid * 3 + 2] = a.t;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  if (tid < TB && row0 + tid < N) {
+    const int64_t r = row0 + tid;
+    float *p = part + (static_cast<int64_t>(blockIdx.y) * N + r) * 3;
+    p[0] = s_state[tid * 3 + 0];
+    p[1] = s_state[tid * 3 + 1];
+    p[2] = s_state[tid * 3 + 2];
+    const int lab = s_label[tid];
+    if (lab >= vt_begin * TB && lab < vt_end * TB) label_logit[r] = s_lablogit[tid];
+  }
+}
+
 __global__ __launch_bounds__(256) void linear_logprob_merge_kernel(const float *__restrict__ part,
                                                                    const float *__restrict__ label_logit,
                                                                    const int64_t *__restrict__ labels,
@@ -267,6 +453,10 @@ __global__ __launch_bounds__(256) void linear_logprob_merge_kernel(const float *
 
 using namespace va;
 
+// va_set_tuning(VA_TUNE_LINEAR_LOGPROB_TILE): 128 (the 128 x 128 register-staged kernel) or 256
+// (the 256 x 256 LDS-DMA kernel above)
+int g_linear_logprob_tile = 256;
+
 extern "C" int64_t va_linear_logprob_workspace_bytes(int64_t N, int splits) {
   return static_cast<int64_t>(sizeof(float)) * (static_cast<int64_t>(splits) * N * 3 + N);
 }
@@ -288,6 +478,23 @@ extern "C" int va_linear_logprob_fwd(const void *hidden, int64_t ldh, const void
   hipStream_t s = static_cast<hipStream_t>(stream);
   float *part = static_cast<float *>(workspace);
   float *label_logit = part + static_cast<int64_t>(splits) * N * 3;
+  if (g_linear_logprob_tile == 256) {
+    const int64_t n_vt = (V + TB - 1) / TB;
+    int per = static_cast<int>((n_vt + splits - 1) / splits);
+    const int used = static_cast<int>((n_vt + per - 1) / per);  // <= splits: ranges the workspace holds
+    const dim3 grid(static_cast<unsigned>((N + TB - 1) / TB), static_cast<unsigned>(used));
+    if (temperature == 1.0f)
+      hipLaunchKernelGGL(linear_logprob_tiles256_kernel<false>, grid, dim3(T_THREADS), 0, s,
+                         static_cast<const uint16_t *>(hidden), ldh, static_cast<const uint16_t *>(weight), ldw,
+                         labels, N, static_cast<int>(H), V, per, temperature, part, label_logit);
+    else
+      hipLaunchKernelGGL(linear_logprob_tiles256_kernel<true>, grid, dim3(T_THREADS), 0, s,
+                         static_cast<const uint16_t *>(hidden), ldh, static_cast<const uint16_t *>(weight), ldw,
+                         labels, N, static_cast<int>(H), V, per, temperature, part, label_logit);
+    hipLaunchKernelGGL(linear_logprob_merge_kernel, dim3(static_cast<unsigned>((N + 255) / 256)), dim3(256), 0, s,
+                       part, label_logit, labels, N, V, used, logp, entropy, lse);
+    return check_launch("linear_logprob_fwd");
+  }
   const int64_t n_vtiles = (V + BN - 1) / BN;
   const int tiles_per_split = static_cast<int>((n_vtiles + splits - 1) / splits);
   const dim3 grid(static_cast<unsigned>((N + BM - 1) / BM), static_cast<unsigned>(splits));

@@ -713,6 +713,7 @@ extern int g_gae_partials;        // advantage.hip
 extern int g_gae_nt;              // advantage.hip
 extern int g_loss_vec;            // loss.hip
 extern int g_whiten_slice_min;    // advantage.hip
+extern int g_linear_logprob_tile;  // linear_logprob.hip
 extern int g_whiten_grid;         // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
 extern int g_flash_dkdv_qt;       // attention.hip
@@ -736,6 +737,13 @@ extern "C" int va_set_tuning(int key, int value) {
       return VA_OK;
     case VA_TUNE_GAE_NT: g_gae_nt = value & 7; return VA_OK;
     case VA_TUNE_LOSS_VEC: g_loss_vec = value; return VA_OK;
+    case VA_TUNE_LINEAR_LOGPROB_TILE:
+      if (value != 128 && value != 256) {
+        va::set_error("VA_TUNE_LINEAR_LOGPROB_TILE must be 128 or 256 (got %d)", value);
+        return VA_E_ARG;
+      }
+      g_linear_logprob_tile = value;
+      return VA_OK;
     case VA_TUNE_WHITEN_SLICE_MIN: g_whiten_slice_min = value < 0 ? 0 : value; return VA_OK;
     case VA_TUNE_WHITEN_GRID:
       if (value < 1 || value > 65536) {
