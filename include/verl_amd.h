@@ -357,6 +357,12 @@ int va_rope_qkv_fwd(const void *qkv, int64_t ld, const void *cos, const void *si
 int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *cos, const void *sin, int dtype,
                     int64_t T, int64_t Hq, int64_t Hk, int64_t D, void *dqkv, int64_t ld, void *stream);
 
+/* transpose_16: out [C, R] (row stride ld_out) = in [R, C] (row stride ld_in)^T for any 16-bit
+ * element type; R, C, strides multiples of 8, 16-byte aligned buffers. The layout step of the
+ * backward input-gradient GEMMs (dX = dY W over a K-contiguous W^T; no reference counterpart:
+ * the reference leaves this GEMM's layout to FSDP / autograd, dp_actor.py:465-470). */
+int va_transpose_16(const void *in, int64_t ld_in, int64_t R, int64_t C, void *out, int64_t ld_out, void *stream);
+
 /* ---------------------------------------------------------------------------------------
  * Fused lm_head + log-prob + entropy forward (the reference's use_fused_kernels
  * path, utils/kernel/kernels.py:120-663 + linear_cross_entropy.py:40-117): for hidden [N, H]

@@ -111,3 +111,11 @@ def test_tuning_keys_and_wgrad_validation_without_device(lib):
     assert lib.va_wgrad_workspace_bytes(256, 128, 1) == 0
     rc = lib.va_wgrad_bf16(None, 100, None, 128, 64, 100, 128, 1, None, None, None)
     assert rc == -1 and b"multiples of 128" in lib.va_last_error()
+
+
+def test_transpose_validation_without_device(lib):
+    rc = lib.va_transpose_16(None, 8, 7, 8, None, 8, None)
+    assert rc == -1 and b"multiples of 8" in lib.va_last_error()
+    rc = lib.va_transpose_16(None, 8, 16, 16, None, 16, None)
+    assert rc == -1 and b"strides" in lib.va_last_error()
+    assert lib.va_transpose_16(None, 8, 0, 8, None, 8, None) == 0  # empty: no-op

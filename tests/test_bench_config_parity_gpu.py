@@ -195,13 +195,23 @@ def test_bench_configuration_0p5b_microbatch_properties():
     actor.config.ppo_mini_batch_size = 4
     rows = []
 
-    def hook(_mod, _inp, out):
-        def grad_hook(gr):
-            gf = gr.float()
-            rows.append((gf.sum(-1), gf.abs().sum(-1)))
-        out.register_hook(grad_hook)
+    from verl_amd import kernels as K
 
-    h = actor._lm_head.register_forward_hook(hook)
+    def grad_hook(gr):
+        gf = gr.float()
+        rows.append((gf.sum(-1), gf.abs().sum(-1)))
+
+    # the actor runs the lm_head through K.linear (a module forward hook would route it back
+    # through nn.Linear): observe dlogits on that function's output
+    plain_linear = K.linear
+
+    def linear_seen(x, w):
+        out = plain_linear(x, w)
+        if w is actor._lm_head.weight and out.requires_grad:
+            out.register_hook(grad_hook)
+        return out
+
+    K.linear = linear_seen
     captured = {}
 
     def capture():
@@ -210,8 +220,10 @@ def test_bench_configuration_0p5b_microbatch_properties():
         return torch.tensor(0.0, device=DEV)
 
     actor._optimizer_step = capture
-    actor.update_policy(data)
-    h.remove()
+    try:
+        actor.update_policy(data)
+    finally:
+        K.linear = plain_linear
     gb = captured["g"]
     assert torch.isfinite(gb).all()
     n_ref, n_b = float(g_ref.norm()), float(gb.norm())

@@ -33,6 +33,7 @@ def main():
     import torch
     import torch.nn.functional as F
 
+    from verl_amd import kernels as K
     from verl_amd.utils import gemm_tuning
 
     dev = torch.device("cuda", 0)
@@ -71,6 +72,7 @@ def main():
         nn = timed(lambda: dy @ w)
         tn = timed(lambda: F.linear(dy, wt))
         tr = timed(lambda: w.t().contiguous())
+        tr16 = timed(lambda: K.transpose16(w))
         rows = slice(0, 8192)  # fp32 reference on a row sample
         ref = dy[rows].float() @ w.float()
         e_nn = float(((dy @ w)[rows].float() - ref).abs().max())
@@ -78,6 +80,7 @@ def main():
         fl = 2.0 * T * n_out * n_in
         print(json.dumps({"shape": name, "T": T, "out": n_out, "in": n_in, "nn_us": round(nn, 1),
                           "tn_us": round(tn, 1), "transpose_w_us": round(tr, 1),
+                          "transpose16_us": round(tr16, 1),
                           "nn_tf": round(fl / nn / 1e6, 1), "tn_tf": round(fl / tn / 1e6, 1),
                           "max_abs_err_nn": e_nn, "max_abs_err_tn": e_tn}), flush=True)
         del w, dy, wt

@@ -389,6 +389,45 @@ __global__ __launch_bounds__(256) void rope_qkv_bwd_kernel(
   }
 }
 
+// out[c][r] = in[r][c] for 16-bit elements, 64 x 64 tiles through LDS: each of 256 lanes moves
+// two 16-byte row chunks in and two 16-byte column chunks out, so both HBM sides are whole
+// 128-byte lines. LDS rows are padded to 66 elements: a column read of 8 rows by a wave touches
+// 32 distinct banks (lane pairs share a word). The backward GEMMs use it to give dX = dY W a
+// K-contiguous W^T operand (kernels.input_grad).
+constexpr int kTT = 64;
+__global__ __launch_bounds__(256) void transpose16_kernel(const uint16_t *__restrict__ in, int64_t ldi, int64_t R,
+                                                          int64_t C, uint16_t *__restrict__ out, int64_t ldo) {
+  __shared__ uint32_t tile32[kTT * (kTT + 2) / 2];
+  uint16_t *tile = reinterpret_cast<uint16_t *>(tile32);
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * kTT, c0 = static_cast<int64_t>(blockIdx.x) * kTT;
+  const int t = threadIdx.x;
+  uint4 v[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {  // both loads in flight before the LDS writes
+    const int64_t gr = r0 + p * 32 + (t >> 3), gc = c0 + (t & 7) * 8;
+    v[p] = (gr < R && gc < C) ? *reinterpret_cast<const uint4 *>(in + gr * ldi + gc) : uint4{0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    uint32_t *d = reinterpret_cast<uint32_t *>(tile + (p * 32 + (t >> 3)) * (kTT + 2) + (t & 7) * 8);
+    d[0] = v[p].x, d[1] = v[p].y, d[2] = v[p].z, d[3] = v[p].w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c = p * 32 + (t >> 3), rb = (t & 7) * 8;
+    const int64_t gc = c0 + c, gr = r0 + rb;
+    if (gc < C && gr < R) {
+      uint32_t w[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        w[k] = static_cast<uint32_t>(tile[(rb + 2 * k) * (kTT + 2) + c]) |
+               (static_cast<uint32_t>(tile[(rb + 2 * k + 1) * (kTT + 2) + c]) << 16);
+      *reinterpret_cast<uint4 *>(out + gc * ldo + gr) = uint4{w[0], w[1], w[2], w[3]};
+    }
+  }
+}
+
 int64_t grid_for(int64_t n, int per_thread) {
   int64_t g = (n + 256LL * per_thread - 1) / (256LL * per_thread);
   return g < 1 ? 1 : (g > 65536 ? 65536 : g);
@@ -591,4 +630,22 @@ extern "C" int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, c
                      static_cast<const uint16_t *>(sin), T, static_cast<int>(Hq), static_cast<int>(Hk),
                      static_cast<int>(D), static_cast<uint16_t *>(dqkv), ld);
   return check_launch("rope_qkv_bwd");
+}
+
+extern "C" int va_transpose_16(const void *in, int64_t ld_in, int64_t R, int64_t C, void *out, int64_t ld_out,
+                               void *stream) {
+  VA_CHECK_ARG(R >= 0 && C >= 0 && R % 8 == 0 && C % 8 == 0, "transpose_16: need R, C multiples of 8");
+  VA_CHECK_ARG(ld_in >= C && ld_out >= R && ld_in % 8 == 0 && ld_out % 8 == 0,
+               "transpose_16: strides must cover the rows and be multiples of 8");
+  if (R == 0 || C == 0) return VA_OK;
+  VA_CHECK_ARG(in && out, "null pointer argument");
+  VA_CHECK_ARG((R + kTT - 1) / kTT <= 65535, "transpose_16: more than 4,194,240 rows");
+  if (!(aligned16(in) && aligned16(out))) {
+    set_error("transpose_16: 16-byte aligned buffers required");
+    return VA_E_ALIGN;
+  }
+  hipLaunchKernelGGL(transpose16_kernel, dim3((C + kTT - 1) / kTT, (R + kTT - 1) / kTT), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint16_t *>(in), ld_in, R, C,
+                     static_cast<uint16_t *>(out), ld_out);
+  return check_launch("transpose_16");
 }

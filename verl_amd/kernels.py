@@ -610,11 +610,26 @@ def input_grad(dy, w):
     ("TN", the forward GEMMs' layout) and the same product runs 1.03-1.3x faster at 151,552 tokens
     (gate|up 2,526 -> 2,227 us, down 1,296 -> 1,150, o 336 -> 259 us untuned; 2.01 / 0.98 / 0.31 ms
     with their TunableOp entries; tools/dgrad_layout_bench.py, profiles/r02/dgrad_layout.log). The
-    copy is one read + write of W (10-46 us), paid per backward call. ``VERL_AMD_DGRAD_LAYOUT=nn``
+    copy is one read + write of W (transpose16), paid per backward call. ``VERL_AMD_DGRAD_LAYOUT=nn``
     keeps the plain product (A/B runs)."""
     if _DGRAD_TN and dy.is_cuda and dy.dtype == w.dtype == torch.bfloat16 and w.dim() == 2:
-        return torch.nn.functional.linear(dy, w.t().contiguous())
+        return torch.nn.functional.linear(dy, transpose16(w))
     return dy @ w
+
+
+def transpose16(x):
+    """x.t().contiguous() for a 2-D 16-bit tensor by va_transpose_16 (64 x 64 LDS tiles, whole
+    128-byte lines on both sides; torch's copy kernel moves the 272 MB lm_head weight at
+    ~0.25 TB/s). Shapes the kernel does not take (a dimension not a multiple of 8, unaligned or
+    column-strided input) go through torch's copy."""
+    _require_device(x)
+    R, C = x.shape
+    if (x.element_size() != 2 or R % 8 or C % 8 or x.stride(1) != 1 or x.stride(0) % 8
+            or x.data_ptr() % 16):
+        return x.t().contiguous()
+    out = torch.empty(C, R, dtype=x.dtype, device=x.device)
+    L.call("va_transpose_16", _p(x), x.stride(0), R, C, _p(out), R, _stream(x))
+    return out
 
 
 # weight gradients dW = dY^T X have K = tokens (tens of thousands) and an output of only
