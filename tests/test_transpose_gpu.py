@@ -63,3 +63,18 @@ def test_linear_autograd_matches_nn_linear():
     scale_x, scale_w = dx_ref.float().abs().max().item(), dw_ref.float().abs().max().item()
     assert (x.grad.float() - dx_ref.float()).abs().max().item() <= 2.0 ** -7 * scale_x
     assert (head.weight.grad.float() - dw_ref.float()).abs().max().item() <= 2.0 ** -7 * scale_w
+
+
+def test_weight_grad_swapped_order_for_vocab_sized_outputs():
+    """n_out >= WGRAD_SWAP_MIN_OUT (the lm_head): dW = (X^T dY)^T through va_transpose_16."""
+    from verl_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    n_out = K.WGRAD_SWAP_MIN_OUT + 64
+    dy = torch.randn(3000, n_out, device=DEV, generator=g).to(torch.bfloat16)
+    x = torch.randn(3000, 136, device=DEV, generator=g).to(torch.bfloat16)
+    got = K.weight_grad(dy, x)
+    assert got.shape == (n_out, 136) and got.is_contiguous()
+    ref = dy.float().t() @ x.float()
+    assert (got.float() - ref).abs().max().item() <= 2.0 ** -7 * ref.abs().max().item()
+    assert (got.float() - (dy.t() @ x).float()).abs().max().item() <= 2.0 ** -7 * ref.abs().max().item()

@@ -670,9 +670,17 @@ def wgrad_gemm(dy2, x2, splits: int = 1):
     return out
 
 
+WGRAD_SWAP_MIN_OUT = 65536  # the lm_head (V = 151,936 outputs)
+
+
 def weight_grad(dy2, x2):
     T, n_out = dy2.shape
     n_in = x2.shape[1]
+    if n_out >= WGRAD_SWAP_MIN_OUT and dy2.is_cuda and dy2.dtype == x2.dtype == torch.bfloat16:
+        # the lm_head: dW^T = X^T dY then one 16-bit transpose of the [n_in, V] result runs 36.5 vs
+        # 37.7 ms at 131,072 rows (tools/wgrad_swap_bench.py, profiles/r02/wgrad_swap_layout.log);
+        # for the backbone shapes the swapped order gains nothing
+        return transpose16(x2.t() @ dy2)
     s = wgrad_splits(T, n_out, n_in) if dy2.is_cuda and dy2.dtype == x2.dtype == torch.bfloat16 else 1
     if s > 1 and -(-n_out // 256) * -(-n_in // 256) >= 128:
         # >= 128 output tiles: a tuned plain GEMM (utils/gemm_tuning) beats the split (gate|up at
