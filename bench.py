@@ -117,6 +117,8 @@ def parse(argv=None):
                     help="old_log_probs = recomputed + N(0, s^2) (SURVEY §8d: ratios straddle the clip band)")
     ap.add_argument("--zero", type=int, default=0, choices=[0, 1],
                     help="1: ZeRO-style sharded fp32 master / AdamW state over the ranks (reduce-scatter + all-gather)")
+    ap.add_argument("--wgrad-stream", type=int, default=0, choices=[0, 1],
+                    help="1: backbone weight gradients + fp32 accumulation on a side stream (wgrad_side_stream)")
     ap.add_argument("--no-rmpad", action="store_true")
     ap.add_argument("--no-mixed-precision", action="store_true", help="fp32 weights + autocast instead of bf16/fp32-master")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -330,6 +332,7 @@ def main():
             use_dynamic_bsz=args.dynamic_bsz > 0, ppo_max_token_len_per_gpu=args.dynamic_bsz or 16384,
             pack_pad_multiple=args.pad_multiple,
             logprob_inplace_backward=bool(args.logprob_inplace_bwd),
+            wgrad_side_stream=bool(args.wgrad_stream),
             gemm_tuning_file=None if args.gemm_table in (None, "none") else args.gemm_table,
         ),
         rollout=AttrDict(log_prob_micro_batch_size_per_gpu=lp_micro, temperature=1.0,
@@ -485,6 +488,7 @@ def main():
                 "pack_pad_multiple": args.pad_multiple,
                 "logprob_inplace_backward": bool(args.logprob_inplace_bwd),
                 "zero_sharded_optimizer": bool(args.zero),
+                "wgrad_side_stream": bool(args.wgrad_stream),
                 "tuning_overrides": args.tune or None,
                 "gemm_table": _gemm_table_name(),
                 "parallelism": f"dp{world}",

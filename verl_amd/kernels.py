@@ -584,20 +584,47 @@ class _MergedLinear(torch.autograd.Function):
         ctx.n_w = n_w
         ctx.w_rows = [p.shape[0] for p in params[:n_w]]
         ctx.has_b = b_all is not None
+        ctx.params = params
         return torch.nn.functional.linear(x, w_all, b_all)
 
     @staticmethod
-    def backward(ctx, dy):
-        x, w_all = ctx.saved_tensors
-        dx = input_grad(dy, w_all)
-        x2 = x.reshape(-1, x.shape[-1])
-        dy2 = dy.reshape(-1, dy.shape[-1])
+    def _param_grads(ctx, dy2, x2):
         dw = weight_grad(dy2, x2)
         grads = list(torch.split(dw, ctx.w_rows, dim=0))
         if ctx.has_b:
             db = dy2.sum(0)
             grads += list(torch.split(db, ctx.w_rows, dim=0))
-        return (dx, None, None, None, *grads)
+        return grads
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w_all = ctx.saved_tensors
+        x2 = x.reshape(-1, x.shape[-1])
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        params = ctx.params
+        sink = WGRAD_SINK
+        if (sink is not None and dy.is_cuda and w_all.shape[0] < WGRAD_SWAP_MIN_OUT
+                and sink.owns_exclusively(params)):
+            # weight gradients off the critical path: the side stream starts as soon as dY exists,
+            # beside the input gradient, and hands the gradients to the parameter manager there
+            side = sink.wgrad_stream
+            main = torch.cuda.current_stream(dy.device)
+            side.wait_stream(main)
+            dx = input_grad(dy, w_all)
+            with torch.cuda.stream(side):
+                sink.deliver(params, _MergedLinear._param_grads(ctx, dy2, x2))
+            # dY and X stay referenced until the compute stream has waited for this launch (no
+            # record_stream: the host runs far ahead of the GPU, so blocks released by event would
+            # not be reusable by the next allocations and the backward's memory would pile up)
+            sink.throttle(main, keep=(dy, x))
+            return (dx, None, None, None, *([None] * len(params)))
+        dx = input_grad(dy, w_all)
+        return (dx, None, None, None, *_MergedLinear._param_grads(ctx, dy2, x2))
+
+
+# The parameter manager (workers/grad_sync.MixedPrecisionParams) that takes backbone weight
+# gradients on its side stream during a backward (set by the actor around loss.backward()), or None.
+WGRAD_SINK = None
 
 
 _DGRAD_TN = os.environ.get("VERL_AMD_DGRAD_LAYOUT", "tn") != "nn"

@@ -170,6 +170,17 @@ class DataParallelPPOActor(BasePPOActor):
         # round packed micro-batches up to a multiple of this many tokens (0 = off) and look the
         # model GEMMs up in a tuned solution table (utils/gemm_tuning.py)
         self.pack_pad_multiple = int(self.config.get("pack_pad_multiple", 0) or 0)
+        # backbone weight gradients + fp32 accumulation on a side stream beside the backward's
+        # critical path (workers/grad_sync.MixedPrecisionParams.enable_wgrad_stream)
+        self.wgrad_side_stream = bool(self.config.get("wgrad_side_stream", False))
+        if (self.wgrad_side_stream and grad_reducer is not None
+                and hasattr(grad_reducer, "enable_wgrad_stream")):
+            # the decoder layers' weights: one gradient source each (not the tied lm_head / embedding)
+            layers = getattr(self._backbone, "layers", None)
+            self.wgrad_side_stream = layers is not None and grad_reducer.enable_wgrad_stream(
+                list(layers.parameters()))
+        else:
+            self.wgrad_side_stream = False
         gemm_table = self.config.get("gemm_tuning_file", None)
         if gemm_table:
             from ...utils.gemm_tuning import use_tuned_gemms
@@ -425,7 +436,12 @@ class DataParallelPPOActor(BasePPOActor):
                     last = i == len(micro_batches) - 1
                     if last and self.grad_reducer is not None:
                         self.grad_reducer.begin_sync()
-                    loss.backward()
+                    if self.wgrad_side_stream:
+                        K.WGRAD_SINK = self.grad_reducer
+                    try:
+                        loss.backward()
+                    finally:
+                        K.WGRAD_SINK = None
                     if self.grad_reducer is not None:
                         self.grad_reducer.after_backward()
                     m.update({

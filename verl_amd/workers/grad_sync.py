@@ -25,6 +25,8 @@ reduce-scattered instead of all-reduced, and the updated bf16 shards are all-gat
 
 from __future__ import annotations
 
+import collections
+import os
 import weakref
 
 import torch
@@ -334,12 +336,83 @@ class MixedPrecisionParams(_OrderedBuckets):
         self._init_order()
         self._hooks = [p.register_post_accumulate_grad_hook(_grad_hook(self)) for p in self.params]
         weakref.finalize(self, _remove_hooks, self._hooks)
+        self.wgrad_stream = None
+        self.side_stream_grads = 0  # gradients delivered on the side stream (tests / diagnostics)
+        self._param_ids = {id(p) for p in self.params}
+        self._side_ids = set()
+        self._delivered = set()
+        self._side_events = collections.deque()
+        # how many side-stream weight-gradient launches may be outstanding before the compute stream
+        # waits for the oldest (a GPU-side wait): bounds the activations / gradients the side stream
+        # keeps alive when the compute stream's GEMMs starve it (unbounded lag -> +tens of GB)
+        self.wgrad_max_lag = int(os.environ.get("VA_WGRAD_MAX_LAG", "4"))
+
+    # ------------------------------------------------------------------ side-stream weight gradients
+    def enable_wgrad_stream(self, params=None):
+        """Run the weight gradients of ``params`` (the backbone projections, kernels._MergedLinear),
+        every gradient accumulation into the fp32 buckets and the bucket collectives' launch on one
+        side stream, so the backward's critical path (input gradients, attention, norms) overlaps
+        them: a weight gradient whose GEMM leaves CUs idle (gate|up: 152 tiles of 256 x 256 for 256
+        CUs) shares the chip with the next layer's input gradient. ``params`` must each receive
+        their gradient from ONE use (a tied lm_head / embedding weight must not be listed). The
+        compute stream waits for the side stream once per optimizer step (finish_sync)."""
+        if not self.params or not self.params[0].is_cuda:
+            return False
+        if self.wgrad_stream is None:
+            self.wgrad_stream = torch.cuda.Stream(device=self.params[0].device)
+        allowed = self._param_ids if params is None else {id(p) for p in params}
+        self._side_ids = allowed & self._param_ids
+        return True
+
+    def owns_exclusively(self, params) -> bool:
+        """True when every parameter was listed in enable_wgrad_stream (one gradient source each)."""
+        return self.wgrad_stream is not None and all(id(p) in self._side_ids for p in params)
+
+    def deliver(self, params, grads):
+        """Gradients produced on the side stream (the current stream of the caller)."""
+        for p, g in zip(params, grads):
+            if p.grad is not None:
+                raise RuntimeError("side-stream weight gradient for a parameter that already has one")
+            p.grad = g
+            self.side_stream_grads += 1
+            self._delivered.add(id(p))
+            self._enqueue(p)
+
+    def throttle(self, compute_stream, keep=()):
+        """Called on the compute stream after each side-stream launch (kernels._MergedLinear).
+        ``keep`` (the launch's compute-stream inputs) is released once the compute stream has been
+        made to wait for the launch: from then on, stream-ordered reuse of their blocks by the
+        compute stream is safe."""
+        ev = torch.cuda.Event()
+        ev.record(self.wgrad_stream)
+        self._side_events.append((ev, keep))
+        while len(self._side_events) > self.wgrad_max_lag:
+            compute_stream.wait_event(self._side_events.popleft()[0])
 
     def _on_grad(self, p):
+        if id(p) in self._delivered:
+            # autograd still runs the parameter's AccumulateGrad (and this hook) for the None the
+            # side-stream backward returned: the gradient was already handed over by deliver()
+            self._delivered.discard(id(p))
+            return
+        self._enqueue(p)
+
+    def _enqueue(self, p):
         b = self._bucket_of[id(p)]
         self._ready.setdefault(id(b), []).append(p)
         if len(self._ready[id(b)]) == len(b.params):
-            self._flush(b)
+            self._flush_ordered(b)
+
+    def _flush_ordered(self, b, complete: bool = True):
+        side = self.wgrad_stream
+        if side is None:
+            self._flush(b, complete)
+            return
+        cur = torch.cuda.current_stream(side.device)
+        if cur != side:
+            side.wait_stream(cur)  # gradients made on the compute stream so far
+        with torch.cuda.stream(side):
+            self._flush(b, complete)
 
     def _flush(self, b, complete: bool = True):
         """Accumulate the bucket's ready bf16 gradients into its fp32 buffer (one multi-tensor
@@ -350,6 +423,9 @@ class MixedPrecisionParams(_OrderedBuckets):
                 from .. import kernels as K
 
                 K.accumulate_grads([q.grad for q in ready], [self._gview[id(q)] for q in ready])
+                if self.wgrad_stream is not None:
+                    for q in ready:  # compute-stream gradients freed after the side stream reads them
+                        q.grad.record_stream(self.wgrad_stream)
             else:
                 for q in ready:
                     self._gview[id(q)].add_(q.grad)
@@ -358,14 +434,20 @@ class MixedPrecisionParams(_OrderedBuckets):
         if complete and self.sync_enabled and not b.ready:
             self._mark_ready(b)
 
+    def _join_wgrad_stream(self):
+        if self.wgrad_stream is not None:
+            torch.cuda.current_stream(self.wgrad_stream.device).wait_stream(self.wgrad_stream)
+        self._side_events.clear()  # after the wait: the kept inputs may be reused in stream order
+
     def after_backward(self):
         """Flush buckets that did not complete (parameters without a gradient this pass)."""
         for b in self.buckets:
             if self._ready.get(id(b)):
-                self._flush(b, complete=False)
+                self._flush_ordered(b, complete=False)
 
     # same interface as GradBucketReducer
     def zero_grad(self):
+        self._join_wgrad_stream()
         for b in self.buckets:
             b.buf.zero_()
         for p in self.params:
@@ -378,6 +460,7 @@ class MixedPrecisionParams(_OrderedBuckets):
 
     def finish_sync(self):
         self.after_backward()
+        self._join_wgrad_stream()
         if self.world <= 1:
             self.sync_enabled = False
             return
