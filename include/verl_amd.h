@@ -38,6 +38,9 @@ extern "C" {
 #define VA_F32 0
 #define VA_BF16 1
 #define VA_F16 2
+/* flag OR-ed into va_linear_logprob_fwd's dtype: fp32 logits (no bf16 rounding), the numerics of
+ * the reference's fused kernel (utils/kernel/kernels.py:120-663) instead of the unfused bf16 path */
+#define VA_LOGITS_F32 256
 
 /* mask dtype codes (response_mask / attention_mask slices) */
 #define VA_MASK_F32 0
@@ -367,7 +370,8 @@ int va_transpose_16(const void *in, int64_t ld_in, int64_t R, int64_t C, void *o
  * Fused lm_head + log-prob + entropy forward (the reference's use_fused_kernels
  * path, utils/kernel/kernels.py:120-663 + linear_cross_entropy.py:40-117): for hidden [N, H]
  * (row stride ldh) and weight [V, H] (row stride ldw), both bf16 and 16-byte aligned,
- *   logits = bf16(hidden @ weight^T), x = bf16(logits / temperature) (skipped at T == 1),
+ *   logits = bf16(hidden @ weight^T), x = bf16(logits / temperature) (skipped at T == 1) — or,
+ *   with dtype = VA_BF16 | VA_LOGITS_F32, the same in fp32 without the two roundings,
  *   logp[i] = x[i, labels[i]] - lse_i, entropy[i] = lse_i - sum softmax(x_i) x_i, lse[i],
  * without writing the logits. `splits` vocab ranges run in parallel and merge in fixed order.
  * workspace: va_linear_logprob_workspace_bytes(N, splits). entropy / lse may be NULL.

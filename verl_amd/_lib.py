@@ -18,6 +18,7 @@ HEADER_PATH = _PKG.parent / "include" / "verl_amd.h"
 
 # constants mirrored from include/verl_amd.h
 VA_F32, VA_BF16, VA_F16 = 0, 1, 2
+VA_LOGITS_F32 = 256  # va_linear_logprob_fwd dtype flag: fp32 logits (the reference's fused kernel)
 VA_MASK_F32, VA_MASK_I64, VA_MASK_I32, VA_MASK_U8 = 0, 1, 2, 3
 VA_AGG_TOKEN_MEAN, VA_AGG_SEQ_MEAN_TOKEN_SUM, VA_AGG_SEQ_MEAN_TOKEN_MEAN, VA_AGG_SEQ_MEAN_TOKEN_SUM_NORM = 0, 1, 2, 3
 VA_REDUCE_MASKED_SUM, VA_REDUCE_ROW_MASKED_MEAN = 4, 5

@@ -62,7 +62,7 @@ __device__ __forceinline__ void merge_state(RowAcc &a, float om, float os, float
 constexpr int LDS_ROW = BK + 8;  // bf16 elements per padded LDS row
 constexpr int TILE_ELEMS = BM * LDS_ROW;
 
-template <bool SCALE>
+template <bool SCALE, bool ROUND>
 __global__ __launch_bounds__(256, 2) void linear_logprob_tiles_kernel(
     const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
     const int64_t *__restrict__ labels, int64_t N, int K, int64_t V, int tiles_per_split, float temperature,
@@ -186,8 +186,9 @@ __global__ __launch_bounds__(256, 2) void linear_logprob_tiles_kernel(
 #pragma unroll
         for (int nb = 0; nb < 8; ++nb) {
           const int64_t col = col0 + nb * 16 + (lane & 15);
-          float v = round_bf16(acc[mb][nb][j]);  // the bf16 logits of the unfused path
-          if constexpr (SCALE) v = round_bf16(v / temperature);
+          // ROUND: the bf16 logits of the unfused path; else fp32 logits (the reference's fused kernel)
+          float v = ROUND ? round_bf16(acc[mb][nb][j]) : acc[mb][nb][j];
+          if constexpr (SCALE) v = ROUND ? round_bf16(v / temperature) : v / temperature;
           if (col >= V) v = -INFINITY;
           x[nb] = v;
           cm = fmaxf(cm, v);
@@ -280,7 +281,7 @@ __device__ __forceinline__ void t_stage(const uint16_t *__restrict__ src, int64_
   }
 }
 
-template <bool SCALE>
+template <bool SCALE, bool ROUND>
 __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_tiles256_kernel(
     const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
     const int64_t *__restrict__ labels, int64_t N, int K, int64_t V, int tiles_per_split, float temperature,
@@ -365,8 +366,9 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_tiles256_kernel(
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int col = col0 + j * 16;
-            float v = round_bf16(acc[i][j][e]);  // the bf16 logits of the unfused path
-            if constexpr (SCALE) v = round_bf16(v / temperature);
+            // ROUND: the bf16 logits of the unfused path; else fp32 logits (the reference's fused kernel)
+            float v = ROUND ? round_bf16(acc[i][j][e]) : acc[i][j][e];
+            if constexpr (SCALE) v = ROUND ? round_bf16(v / temperature) : v / temperature;
             if (col >= static_cast<int>(V)) v = -INFINITY;
             if (col == lab) s_lablogit[lr] = v;
             x[j] = v;
@@ -465,6 +467,8 @@ extern "C" int va_linear_logprob_fwd(const void *hidden, int64_t ldh, const void
                                      const int64_t *labels, int64_t N, int64_t H, int64_t V, float temperature,
                                      int splits, float *logp, float *entropy, float *lse, void *workspace,
                                      void *stream) {
+  const bool fp32_logits = (dtype & VA_LOGITS_F32) != 0;
+  dtype &= ~VA_LOGITS_F32;
   VA_CHECK_ARG(dtype == VA_BF16, "linear_logprob: only bf16 hidden / weight are implemented");
   VA_CHECK_ARG(N >= 0 && H > 0 && V > 0 && H % BK == 0 && H <= (1 << 20),
                "linear_logprob: need H %% 64 == 0 (H=%lld)", static_cast<long long>(H));
@@ -484,11 +488,13 @@ extern "C" int va_linear_logprob_fwd(const void *hidden, int64_t ldh, const void
     const int used = static_cast<int>((n_vt + per - 1) / per);  // <= splits: ranges the workspace holds
     const dim3 grid(static_cast<unsigned>((N + TB - 1) / TB), static_cast<unsigned>(used));
     if (temperature == 1.0f)
-      hipLaunchKernelGGL(linear_logprob_tiles256_kernel<false>, grid, dim3(T_THREADS), 0, s,
+      hipLaunchKernelGGL((fp32_logits ? linear_logprob_tiles256_kernel<false, false>
+                                     : linear_logprob_tiles256_kernel<false, true>), grid, dim3(T_THREADS), 0, s,
                          static_cast<const uint16_t *>(hidden), ldh, static_cast<const uint16_t *>(weight), ldw,
                          labels, N, static_cast<int>(H), V, per, temperature, part, label_logit);
     else
-      hipLaunchKernelGGL(linear_logprob_tiles256_kernel<true>, grid, dim3(T_THREADS), 0, s,
+      hipLaunchKernelGGL((fp32_logits ? linear_logprob_tiles256_kernel<true, false>
+                                     : linear_logprob_tiles256_kernel<true, true>), grid, dim3(T_THREADS), 0, s,
                          static_cast<const uint16_t *>(hidden), ldh, static_cast<const uint16_t *>(weight), ldw,
                          labels, N, static_cast<int>(H), V, per, temperature, part, label_logit);
     hipLaunchKernelGGL(linear_logprob_merge_kernel, dim3(static_cast<unsigned>((N + 255) / 256)), dim3(256), 0, s,
@@ -499,11 +505,13 @@ extern "C" int va_linear_logprob_fwd(const void *hidden, int64_t ldh, const void
   const int tiles_per_split = static_cast<int>((n_vtiles + splits - 1) / splits);
   const dim3 grid(static_cast<unsigned>((N + BM - 1) / BM), static_cast<unsigned>(splits));
   if (temperature == 1.0f) {
-    hipLaunchKernelGGL(linear_logprob_tiles_kernel<false>, grid, dim3(256), 0, s,
+    hipLaunchKernelGGL((fp32_logits ? linear_logprob_tiles_kernel<false, false>
+                                     : linear_logprob_tiles_kernel<false, true>), grid, dim3(256), 0, s,
                        static_cast<const uint16_t *>(hidden), ldh, static_cast<const uint16_t *>(weight), ldw,
                        labels, N, static_cast<int>(H), V, tiles_per_split, temperature, part, label_logit);
   } else {
-    hipLaunchKernelGGL(linear_logprob_tiles_kernel<true>, grid, dim3(256), 0, s,
+    hipLaunchKernelGGL((fp32_logits ? linear_logprob_tiles_kernel<true, false>
+                                     : linear_logprob_tiles_kernel<true, true>), grid, dim3(256), 0, s,
                        static_cast<const uint16_t *>(hidden), ldh, static_cast<const uint16_t *>(weight), ldw,
                        labels, N, static_cast<int>(H), V, tiles_per_split, temperature, part, label_logit);
   }

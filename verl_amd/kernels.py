@@ -159,7 +159,7 @@ def _linear_logprob_splits(n_rows: int) -> int:
     return int(min(64, max(1, -(-1024 // blocks))))
 
 
-def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float):
+def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float, fp32_logits: bool = False):
     N, H = hidden.shape
     V = weight.shape[0]
     splits = _linear_logprob_splits(N)
@@ -169,7 +169,8 @@ def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float):
     nbytes = L.load().va_linear_logprob_workspace_bytes(N, splits)
     ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=hidden.device)
     ev = TIMER.start(torch.cuda.current_stream(hidden.device)) if TIMER is not None else None
-    L.call("va_linear_logprob_fwd", _p(hidden), hidden.stride(0), _p(weight), weight.stride(0), L.VA_BF16, _p(labels),
+    dtype = L.VA_BF16 | (L.VA_LOGITS_F32 if fp32_logits else 0)
+    L.call("va_linear_logprob_fwd", _p(hidden), hidden.stride(0), _p(weight), weight.stride(0), dtype, _p(labels),
            N, H, V, float(temperature), splits, _p(logp), _p(ent), _p(lse), _p(ws), _stream(hidden))
     if ev is not None:  # MFMA-bound: algorithmic flops 2 N V H
         TIMER.stop("linear_logprob_fwd", 2 * N * V * H, torch.cuda.current_stream(hidden.device), ev)
@@ -179,15 +180,18 @@ def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float):
 class _LinearLogprob(torch.autograd.Function):
     """Forward: one fused MFMA pass (no logits in HBM). Backward: logits are recomputed per row
     chunk with a hipBLASLt GEMM, turned into dlogits in place by va_logprob_entropy_bwd, and
-    pushed through the two GEMMs of the lm_head (the reference's fused path also recomputes)."""
+    pushed through the two GEMMs of the lm_head (the reference's fused path also recomputes).
+    fp32_logits: the logits stay fp32 (no bf16 rounding) in both passes, as in the reference's
+    fused kernel; dlogits are rounded to bf16 for the two GEMMs, as its backward's tl.dot inputs."""
 
     CHUNK_BYTES = 2 << 30
 
     @staticmethod
-    def forward(ctx, hidden, weight, labels, temperature):
-        logp, ent, lse = _linear_logprob_fwd_raw(hidden, weight, labels, temperature)
+    def forward(ctx, hidden, weight, labels, temperature, fp32_logits):
+        logp, ent, lse = _linear_logprob_fwd_raw(hidden, weight, labels, temperature, fp32_logits)
         ctx.save_for_backward(hidden, weight, labels, lse, ent)
         ctx.temperature = float(temperature)
+        ctx.fp32_logits = bool(fp32_logits)
         return logp, ent
 
     @staticmethod
@@ -199,27 +203,33 @@ class _LinearLogprob(torch.autograd.Function):
         g2 = None if g_ent is None else _f32(g_ent)
         d_hidden = torch.empty_like(hidden) if ctx.needs_input_grad[0] else None
         d_weight = torch.zeros_like(weight, dtype=torch.float32) if ctx.needs_input_grad[1] else None
-        rows = max(1, int(_LinearLogprob.CHUNK_BYTES // (V * hidden.element_size())))
+        f32 = ctx.fp32_logits
+        rows = max(1, int(_LinearLogprob.CHUNK_BYTES // (V * (4 if f32 else hidden.element_size()))))
         for r0 in range(0, N, rows):
             r1 = min(N, r0 + rows)
             h = hidden[r0:r1]
-            logits = h @ weight.t()
+            logits = torch.mm(h, weight.t(), out_dtype=torch.float32) if f32 else h @ weight.t()
             L.call("va_logprob_entropy_bwd", _p(g1[r0:r1] if g1 is not None else None),
-                   _p(g2[r0:r1] if g2 is not None else None), _p(logits), L.VA_BF16, r1 - r0, V, logits.stride(0),
-                   _p(labels[r0:r1]), _p(lse[r0:r1]), _p(ent[r0:r1]), ctx.temperature, _p(logits), logits.stride(0),
-                   _stream(logits))
+                   _p(g2[r0:r1] if g2 is not None else None), _p(logits), L.VA_F32 if f32 else L.VA_BF16, r1 - r0, V,
+                   logits.stride(0), _p(labels[r0:r1]), _p(lse[r0:r1]), _p(ent[r0:r1]), ctx.temperature, _p(logits),
+                   logits.stride(0), _stream(logits))
+            if f32:
+                logits = logits.to(hidden.dtype)
             if d_hidden is not None:
                 torch.mm(logits, weight, out=d_hidden[r0:r1])
             if d_weight is not None:
                 d_weight.add_((logits.t() @ h).float())
         if d_weight is not None:
             d_weight = d_weight.to(weight.dtype)
-        return d_hidden, d_weight, None, None
+        return d_hidden, d_weight, None, None, None
 
 
-def linear_logprob_entropy(hidden, weight, labels, temperature: float = 1.0):
+def linear_logprob_entropy(hidden, weight, labels, temperature: float = 1.0, fp32_logits: bool = False):
     """(log p[label], entropy) of ``hidden @ weight.T`` (the lm_head) after ``div_(temperature)``,
-    computed by the fused MFMA kernel without materialising the [N, V] logits. bf16 only."""
+    computed by the fused MFMA kernel without materialising the [N, V] logits. bf16 only.
+    fp32_logits=False rounds the logits to bf16 as the unfused autocast path does (fused and
+    unfused agree); True keeps them fp32, the numerics of the reference's fused kernel
+    (utils/kernel/kernels.py:120-663, tests/utils/test_linear_cross_entropy.py tolerances)."""
     _require_device(hidden, weight, labels)
     _bf16_only(hidden, weight)
     if hidden.dim() != 2 or weight.dim() != 2 or hidden.shape[1] != weight.shape[1]:
@@ -231,7 +241,7 @@ def linear_logprob_entropy(hidden, weight, labels, temperature: float = 1.0):
     lab = labels.reshape(-1).long().contiguous()
     if lab.shape[0] != hidden.shape[0]:
         raise ValueError(f"labels ({lab.shape[0]}) do not match hidden rows ({hidden.shape[0]})")
-    return _LinearLogprob.apply(hidden, weight, lab, float(temperature))
+    return _LinearLogprob.apply(hidden, weight, lab, float(temperature), bool(fp32_logits))
 
 
 # =============================================================================== policy loss

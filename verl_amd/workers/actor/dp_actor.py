@@ -162,6 +162,9 @@ class DataParallelPPOActor(BasePPOActor):
         # gfx950 flash-attention forward (attention.hip) inside the fused packed backbone
         self.fused_attention = self.config.get("fused_attention", True)
         self.fused_logprob_no_grad = self.config.get("fused_logprob_no_grad", False)
+        # the fused kernel's logits: bf16-rounded like the unfused autocast path (default: fused and
+        # unfused agree) or fp32 like the reference's own fused kernel
+        self.fused_kernel_fp32_logits = bool(self.config.get("fused_kernel_fp32_logits", False))
         # the log-prob backward writes dlogits over the logits (flash-attn inplace_backward, as the
         # reference) or into a fresh [N, V] buffer: on MI355X the out-of-place stream runs ~4 %
         # faster (a read+write pass whose writes hit other DRAM pages than its reads) for one more
@@ -230,7 +233,7 @@ class DataParallelPPOActor(BasePPOActor):
                     w = self._lm_head.weight
                     lp_sel, ent_sel = K.linear_logprob_entropy(
                         h_sel.to(torch.bfloat16), w if w.dtype == torch.bfloat16 else w.to(torch.bfloat16), labels,
-                        temperature)
+                        temperature, fp32_logits=self.fused_kernel_fp32_logits)
                 else:
                     head = self._lm_head
                     if (isinstance(head, nn.Linear) and head.bias is None and h_sel.is_cuda
