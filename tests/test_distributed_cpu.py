@@ -307,3 +307,27 @@ def test_dropped_worker_frees_its_parameters(zero):
     del m, w
     gc.collect()
     assert all(r() is None for r in refs)
+
+
+@pytest.mark.parametrize("max_norm", [1e-3, 1e3])
+def test_bucket_clip_equals_torch_clip(max_norm):
+    """MixedPrecisionParams.clip_grad_norm_ (flat fp32 buckets) = torch.nn.utils.clip_grad_norm_ on
+    the masters: same norm, same clipped gradients (to fp32 reduction-order rounding)."""
+    from verl_amd.workers.grad_sync import MixedPrecisionParams
+
+    def model():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(torch.nn.Linear(6, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
+
+    a, b = model(), model()
+    ma, mb = MixedPrecisionParams(a, bucket_bytes=256), MixedPrecisionParams(b, bucket_bytes=256)
+    assert len(ma.buckets) > 1
+    x = torch.randn(5, 6, generator=torch.Generator().manual_seed(1))
+    for mod, mgr in ((a, ma), (b, mb)):
+        mod(x.bfloat16()).float().square().sum().backward()
+        mgr.finish_sync()
+    n_torch = torch.nn.utils.clip_grad_norm_(ma.optimizer_params(), max_norm=max_norm, foreach=True)
+    n_mine = mb.clip_grad_norm_(max_norm)
+    assert torch.allclose(n_torch, n_mine, rtol=1e-6), (n_torch, n_mine)
+    for p, q in zip(ma.optimizer_params(), mb.optimizer_params(), strict=True):
+        assert torch.allclose(p.grad, q.grad, rtol=1e-6, atol=1e-9)

