@@ -8,5 +8,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p8 
 f=$(find $O/p8 -name '*kernel_stats.csv' | head -1)
 python3 tools/prof_summary.py "$f" > $O/p8.summary.txt
 t=$(find $O/p8 -name '*kernel_trace.csv' | head -1)
-python3 tools/trace_gaps.py "$t" --window 0.5 > $O/p8.gaps.txt || true
+python3 tools/trace_gaps.py "$t" --window 0.74 > $O/p8.gaps.txt || true
 find $O/p8 \( -name "*kernel_trace.csv" -o -name "*.db" \) -delete
