@@ -30,6 +30,12 @@ import subprocess
 import sys
 import time
 
+# HIP runtime: kernel arguments in device memory (read by the dispatch without a host-memory round
+# trip; interleaved same-box A/B: 180.4 / 180.5K vs 179.7 / 179.8K tokens/s at N = 1, 174.0K vs
+# 172.8K on the N = 8 per-rank workload, profiles/r02/bench_hip_env_ab.txt). Set before anything
+# initialises HIP; the launcher's child ranks inherit it. An explicit setting wins.
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -489,6 +495,7 @@ def main():
                 "logprob_inplace_backward": bool(args.logprob_inplace_bwd),
                 "zero_sharded_optimizer": bool(args.zero),
                 "wgrad_side_stream": bool(args.wgrad_stream),
+                "hip_env": {"HIP_FORCE_DEV_KERNARG": os.environ.get("HIP_FORCE_DEV_KERNARG")},
                 "tuning_overrides": args.tune or None,
                 "gemm_table": _gemm_table_name(),
                 "parallelism": f"dp{world}",
