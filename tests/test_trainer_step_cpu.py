@@ -90,13 +90,19 @@ def test_step_order_gae_with_critic_and_ref():
 def test_critic_warmup_skips_actor_update_and_grpo_needs_no_critic():
     from verl_amd.trainer.ppo.trainer_step import PPOTrainerStep
 
+    # fit() numbers steps from 1 (ray_trainer.py:1099, 1118) and updates the actor once
+    # critic_warmup <= global_steps (:1315): warmup 2 skips step 1 only, warmup 1 skips nothing
     log = []
-    step = PPOTrainerStep(_cfg("gae", warmup=1), _Actor(log), critic=_Critic(log), device=torch.device("cpu"))
+    step = PPOTrainerStep(_cfg("gae", warmup=2), _Actor(log), critic=_Critic(log), device=torch.device("cpu"))
     step.step(_batch())
     assert "update_actor" not in log and log[-1] == "update_critic"
     log.clear()
     step.step(_batch())
     assert log[-1] == "update_actor"
+    log.clear()
+    one = PPOTrainerStep(_cfg("gae", warmup=1), _Actor(log), critic=_Critic(log), device=torch.device("cpu"))
+    one.step(_batch())
+    assert log[-2:] == ["update_critic", "update_actor"]
     log2 = []
     g = PPOTrainerStep(_cfg("grpo"), _Actor(log2), device=torch.device("cpu"))
     g.step(_batch())
@@ -116,7 +122,8 @@ def test_ray_trainer_surface_builds_workers_from_the_role_mapping():
     tr.init_workers()
     tr.step_runner.device = torch.device("cpu")
     mets = tr.fit([_batch(), _batch()])
-    assert len(mets) == 2 and tr.global_steps == 2
+    assert len(mets) == 2 and tr.global_steps == 3  # steps 1 and 2 ran
+    assert [m["training/global_step"] for m in mets] == [1, 2]
     assert log.count("ref_log_prob") == 2 and log.count("update_actor") == 2
 
 

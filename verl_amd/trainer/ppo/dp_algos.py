@@ -175,13 +175,53 @@ def check_groups_intact(index, group=None) -> bool:
     w = _world(group)
     if w == 1:
         return True
-    keys = torch.from_numpy(np.unique(uid_keys(index)))
-    n = _all_gather(torch.tensor([keys.numel()]), group)
+    # RCCL moves device tensors only: stage the exchange on this rank's GPU under nccl
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    keys = torch.from_numpy(np.unique(uid_keys(index))).to(dev)
+    n = _all_gather(torch.tensor([keys.numel()], device=dev), group)
     nmax = max(int(x.item()) for x in n)
-    pad = torch.full((nmax,), -1, dtype=torch.int64)
+    pad = torch.full((nmax,), -1, dtype=torch.int64, device=dev)
     pad[: keys.numel()] = keys
     allk = torch.cat([p[: int(c.item())] for p, c in zip(_all_gather(pad, group), n, strict=True)])
     return allk.unique().numel() == allk.numel()
+
+
+@torch.no_grad()
+def agg_loss_dp(loss_mat: torch.Tensor, loss_mask: torch.Tensor, loss_agg_mode: str, group=None) -> torch.Tensor:
+    """core_algos.agg_loss (core_algos.py:686-719) over the union of all ranks' rows, as the
+    reference's driver computes the actor/entropy metric on the whole batch (ray_trainer.py:
+    1224-1228). Each rank reduces its rows to (numerator, denominator) in fp64 and one all-reduce
+    sums them: token-mean = sum(x m) / (sum m + 1e-8); seq-mean-token-sum / -token-mean = the mean
+    over all rows of the row sums / row means; seq-mean-token-sum-norm = sum(x m) / R."""
+    from .core_algos import agg_loss
+
+    if _world(group) == 1:
+        return agg_loss(loss_mat, loss_mask, loss_agg_mode)
+    x = loss_mat.double() * loss_mask.double()
+    m = loss_mask.double()
+    if loss_agg_mode == "token-mean":
+        num, den = x.sum(), m.sum()
+    elif loss_agg_mode == "seq-mean-token-sum":
+        num, den = x.sum(-1).sum(), torch.tensor(float(x.shape[0]), dtype=torch.float64, device=x.device)
+    elif loss_agg_mode == "seq-mean-token-mean":
+        num = (x.sum(-1) / m.sum(-1)).sum()
+        den = torch.tensor(float(x.shape[0]), dtype=torch.float64, device=x.device)
+    elif loss_agg_mode == "seq-mean-token-sum-norm":
+        num, den = x.sum() / loss_mask.shape[-1], torch.ones((), dtype=torch.float64, device=x.device)
+    else:
+        raise ValueError(f"Invalid loss_agg_mode: {loss_agg_mode}")
+    t = torch.stack([num, den])
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, group=group)
+        t = h.to(loss_mat.device)
+    else:
+        dist.all_reduce(t, group=group)
+    if loss_agg_mode == "token-mean":
+        return (t[0] / (t[1] + 1e-8)).float()
+    if loss_agg_mode == "seq-mean-token-sum-norm":
+        return t[0].float()
+    return (t[0] / t[1]).float()
 
 
 @torch.no_grad()

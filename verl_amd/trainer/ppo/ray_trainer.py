@@ -190,14 +190,20 @@ class RayPPOTrainer:
                                           reward_fn=self.reward_fn)
 
     def fit_step(self, batch: DataProto) -> dict:
-        """One iteration of fit() (ray_trainer.py:1195-1330) on this rank's shard."""
+        """One iteration of fit() (ray_trainer.py:1195-1330) on this rank's shard. Steps are
+        numbered from 1 as in fit() (global_steps = 0, then += 1 before the first step,
+        ray_trainer.py:1099, 1118), which is what critic_warmup compares against (:1315)."""
         if self.step_runner is None:
             self.init_workers()
+        if self.global_steps == 0:
+            self.global_steps = 1
         self.step_runner.global_steps = self.global_steps
         _, metrics = self.step_runner.step(batch)
+        metrics["training/global_step"] = self.global_steps
         self.global_steps += 1
         return metrics
 
     def fit(self, batches) -> list[dict]:
         """ray_trainer.py:1081-1411 over an iterable of rollout shards; returns the per-step metrics."""
+        self.global_steps = 0
         return [self.fit_step(b) for b in batches]

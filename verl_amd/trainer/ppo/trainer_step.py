@@ -168,7 +168,9 @@ class PPOTrainerStep:
             raise ValueError("GAE needs a critic worker")
         self.use_reference_policy = ref is not None or hasattr(actor, "ref_policy") and actor.ref_policy is not None
         self.kl_ctrl_in_reward = core_algos.get_kl_controller(algo.kl_ctrl) if algo.get("use_kl_in_reward") else None
-        self.global_steps = 0
+        # the number of the step about to run: fit() counts from 1 (ray_trainer.py:1099, 1118), so
+        # critic_warmup = k holds the actor back for steps 1..k-1
+        self.global_steps = 1
 
     # ------------------------------------------------------------------ host -> device, once
     def to_device(self, batch: DataProto) -> DataProto:
@@ -186,6 +188,7 @@ class PPOTrainerStep:
     # ------------------------------------------------------------------ the step
     def step(self, batch: DataProto) -> tuple[DataProto, dict]:
         """ray_trainer.py:1195-1330 from the rollout output on; returns (batch, metrics)."""
+        from .dp_algos import agg_loss_dp
         from .ray_trainer import compute_response_mask
 
         cfg = self.config
@@ -205,7 +208,8 @@ class PPOTrainerStep:
         # old log-probs (+ entropy metric), :1221-1230
         old = self.actor.compute_log_prob(batch)
         entropys = old.batch["entropys"]
-        ent = core_algos.agg_loss(entropys, batch.batch["response_mask"], cfg.actor_rollout_ref.actor.loss_agg_mode)
+        # over the whole batch as the reference's driver (ray_trainer.py:1224-1228)
+        ent = agg_loss_dp(entropys, batch.batch["response_mask"], cfg.actor_rollout_ref.actor.loss_agg_mode, self.group)
         metrics["actor/entropy"] = ent.detach()
         batch.batch["old_log_probs"] = old.batch["old_log_probs"]
 

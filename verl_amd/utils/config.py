@@ -60,7 +60,8 @@ def actor_config(**overrides) -> AttrDict:
         use_remove_padding=True,
         use_fused_kernels=False,
         fused_logprob_no_grad=False,
-        optim=AttrDict(lr=1e-6, weight_decay=0.01, betas=(0.9, 0.999)),
+        optim=AttrDict(lr=1e-6, weight_decay=0.01, betas=(0.9, 0.999), lr_warmup_steps=-1, lr_warmup_steps_ratio=0.0,
+                       min_lr_ratio=0.0, num_cycles=0.5, warmup_style="constant", total_training_steps=-1),
     )
     for k, v in overrides.items():
         cfg[k] = v
@@ -88,7 +89,8 @@ def critic_config(**overrides) -> AttrDict:
         grad_clip=1.0,
         ulysses_sequence_parallel_size=1,
         model=AttrDict(use_remove_padding=False, enable_gradient_checkpointing=True),
-        optim=AttrDict(lr=1e-5, weight_decay=0.01, betas=(0.9, 0.999)),
+        optim=AttrDict(lr=1e-5, weight_decay=0.01, betas=(0.9, 0.999), lr_warmup_steps_ratio=0.0, min_lr_ratio=None,
+                       warmup_style="constant", total_training_steps=-1),
     )
     for k, v in overrides.items():
         cfg[k] = v

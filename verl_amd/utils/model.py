@@ -122,3 +122,45 @@ def build_qwen2_critic(size: str = "0.5b", device="cuda", dtype=torch.float32, s
     with torch.device(device):
         model = Qwen2ForTokenClassification(cfg)
     return model.to(dtype)
+
+
+def qwen2_vl_config(size: str = "tiny", **text_overrides):
+    """Qwen2-VL configs (BASELINE config 4: Qwen2-VL-7B GRPO). "7b" follows the public
+    Qwen2-VL-7B-Instruct card (assumed: no checkpoint or network here): Qwen2 decoder with
+    multimodal RoPE sections (16, 24, 24) over head_dim 128, and a 32-block ViT (embed 1280, 16
+    heads, 14-px patches, 2 x 2 spatial merge). "tiny" keeps head_dim 64 so the gfx950 flash
+    kernels run, with sections (8, 12, 12)."""
+    from transformers import Qwen2VLConfig
+
+    presets = {
+        "7b": (dict(hidden_size=3584, intermediate_size=18944, num_hidden_layers=28, num_attention_heads=28,
+                    num_key_value_heads=4, vocab_size=152064, tie_word_embeddings=False, mrope_section=[16, 24, 24]),
+               dict(depth=32, embed_dim=1280, hidden_size=3584, num_heads=16, mlp_ratio=4),
+               dict(image_token_id=151655, video_token_id=151656, vision_start_token_id=151652,
+                    vision_end_token_id=151653, bos_token_id=151643, eos_token_id=151645)),
+        "tiny": (dict(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=4096, tie_word_embeddings=False, mrope_section=[8, 12, 12]),
+                 dict(depth=1, embed_dim=64, hidden_size=256, num_heads=4, mlp_ratio=2),
+                 dict(image_token_id=4091, video_token_id=4092, vision_start_token_id=4093, vision_end_token_id=4094,
+                      bos_token_id=4090, eos_token_id=4095)),
+    }
+    text, vision, tokens = (dict(d) for d in presets[size])
+    sec = text.pop("mrope_section")
+    text.update(rope_theta=1000000.0, rms_norm_eps=1e-6, max_position_embeddings=32768, use_sliding_window=False,
+                hidden_act="silu", attention_dropout=0.0, rope_scaling={"type": "mrope", "mrope_section": sec})
+    text.update(text_overrides)
+    vision.update(patch_size=14, spatial_merge_size=2, temporal_patch_size=2, in_channels=3)
+    tie = text.pop("tie_word_embeddings")
+    return Qwen2VLConfig(text_config=dict(text, tie_word_embeddings=tie, bos_token_id=tokens["bos_token_id"],
+                                          eos_token_id=tokens["eos_token_id"]),
+                         vision_config=vision, tie_word_embeddings=tie, **tokens)
+
+
+def build_qwen2_vl(size: str = "tiny", device="cuda", dtype=torch.float32, seed: int = 0, **text_overrides):
+    from transformers import Qwen2VLForConditionalGeneration
+
+    torch.manual_seed(seed)
+    cfg = qwen2_vl_config(size, **text_overrides)
+    with torch.device(device):
+        model = Qwen2VLForConditionalGeneration(cfg)
+    return model.to(dtype)

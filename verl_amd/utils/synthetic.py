@@ -64,3 +64,89 @@ def make_grpo_batch(
         data.reorder(torch.from_numpy(rs.permutation(B)))
     data.meta_info["global_token_num"] = data.batch["attention_mask"].sum(-1).tolist()
     return data.to(device)
+
+
+def make_vl_grpo_batch(
+    model,
+    n_prompts: int = 4,
+    n: int = 4,
+    prompt_len: int = 96,
+    response_len: int = 128,
+    image_grid=(1, 4, 8),
+    min_text: int = 8,
+    dense_responses: bool = False,
+    min_response: int = 16,
+    seed: int = 1234,
+    device="cpu",
+    permute: bool = True,
+) -> DataProto:
+    """A Qwen2-VL GRPO batch (BASELINE config 4): each prompt is left padding, <vision_start>, the
+    image's placeholder tokens (t*h*w / merge^2 of them), <vision_end>, text; one image per prompt
+    with random pixel patches. position_ids [B, 3, P+R]: the model's get_rope_index over the
+    prompt (rl_dataset's mrope ids), then last prompt position + 1..R on all three rows
+    (vllm_rollout_spmd.py:353-363). multi_modal_inputs: one dict per row (pixel_values,
+    image_grid_thw), as the reference's dataset emits them."""
+    cfg = model.config
+    vcfg = cfg.vision_config
+    vocab = cfg.text_config.vocab_size
+    g = torch.Generator().manual_seed(seed)
+    rs = np.random.RandomState(seed)
+    B, P, R = n_prompts * n, prompt_len, response_len
+    t, h, w = image_grid
+    merge = vcfg.spatial_merge_size
+    n_img = t * h * w // (merge * merge)
+    fixed = n_img + 2
+    assert P >= fixed + min_text
+    text_hi = min(vocab, cfg.image_token_id, cfg.video_token_id, cfg.vision_start_token_id) - 1
+    p_len = torch.randint(fixed + min_text, P + 1, (n_prompts,), generator=g)
+    prompts = torch.zeros(n_prompts, P, dtype=torch.long)
+    types = torch.zeros(n_prompts, P, dtype=torch.int32)
+    p_mask = torch.zeros(n_prompts, P, dtype=torch.long)
+    for i in range(n_prompts):
+        s = P - int(p_len[i])
+        body = torch.randint(0, text_hi, (int(p_len[i]),), generator=g)
+        body[0] = cfg.vision_start_token_id
+        body[1 : 1 + n_img] = cfg.image_token_id
+        body[1 + n_img] = cfg.vision_end_token_id
+        prompts[i, s:] = body
+        types[i, s + 1 : s + 1 + n_img] = 1
+        p_mask[i, s:] = 1
+    grid = torch.tensor([list(image_grid)] * n_prompts)
+    with torch.no_grad():
+        pos, _ = model.model.get_rope_index(prompts.to(model.device), types.to(model.device), image_grid_thw=grid,
+                                            attention_mask=p_mask.to(model.device))
+    pos = pos.cpu().transpose(0, 1)  # [n_prompts, 3, P]
+    feat = vcfg.in_channels * vcfg.temporal_patch_size * vcfg.patch_size ** 2
+    pixels = [torch.randn(t * h * w, feat, generator=g) for _ in range(n_prompts)]
+
+    prompts, p_mask, pos = (x.repeat_interleave(n, dim=0) for x in (prompts, p_mask, pos))
+    if dense_responses:
+        r_len = torch.full((B,), R, dtype=torch.long)
+    else:
+        r_len = torch.randint(min_response, R + 1, (B,), generator=g)
+    r_mask = (torch.arange(R)[None, :] < r_len[:, None]).long()
+    responses = torch.randint(0, text_hi, (B, R), generator=g) * r_mask
+    delta = torch.arange(1, R + 1).view(1, 1, R).expand(B, 3, R)
+    position_ids = torch.cat([pos, pos[..., -1:] + delta], dim=-1)
+    input_ids = torch.cat([prompts, responses], dim=1)
+    attention_mask = torch.cat([p_mask, r_mask], dim=1)
+    scores = torch.bernoulli(torch.full((B,), 0.5), generator=g)
+    token_level_scores = torch.zeros(B, R)
+    token_level_scores[torch.arange(B), r_len - 1] = scores
+    uid = np.array([f"prompt-{i // n}" for i in range(B)], dtype=object)
+    mm = np.empty(B, dtype=object)
+    for i in range(B):
+        mm[i] = {"pixel_values": pixels[i // n], "image_grid_thw": grid[i // n : i // n + 1]}
+    data = DataProto.from_dict(
+        tensors=dict(
+            input_ids=input_ids, attention_mask=attention_mask, position_ids=position_ids, responses=responses,
+            response_mask=attention_mask[:, -R:].clone(), token_level_scores=token_level_scores,
+            token_level_rewards=token_level_scores.clone(),
+        ),
+        non_tensors=dict(uid=uid, multi_modal_inputs=mm),
+        meta_info=dict(temperature=1.0),
+    )
+    if permute:
+        data.reorder(torch.from_numpy(rs.permutation(B)))
+    data.meta_info["global_token_num"] = data.batch["attention_mask"].sum(-1).tolist()
+    return data.to(device)

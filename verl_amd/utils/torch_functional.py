@@ -17,6 +17,7 @@ __all__ = [
     "entropy_from_logits", "entropy_from_logits_with_chunking", "masked_sum", "masked_mean", "masked_var",
     "masked_whiten", "clip_by_value", "get_response_mask", "distributed_mean_max_min_std",
     "distributed_masked_mean", "allgather_dict_tensors", "broadcast_dict_tensor",
+    "get_constant_schedule_with_warmup", "get_cosine_schedule_with_warmup",
 ]
 
 
@@ -170,3 +171,63 @@ def allgather_dict_tensors(tensors, size, group, dim=0):
         torch.distributed.all_gather(parts, val, group=group, async_op=False)
         out[key] = torch.cat(parts, dim=dim)
     return out
+
+
+# ------------------------------------------------------------------ LR schedules (host)
+def get_cosine_schedule_with_warmup(optimizer, num_warmup_steps: int, num_training_steps: int,
+                                    min_lr_ratio: float = 0.0, num_cycles: float = 0.5, last_epoch: int = -1):
+    """torch_functional.py:509-550: a linear ramp from min_lr_ratio to 1 over the warmup steps,
+    then 0.5 (1 + min) + 0.5 (1 - min) cos(2 pi cycles progress), floored at min_lr_ratio."""
+    import math
+
+    from torch.optim.lr_scheduler import LambdaLR
+
+    min_lr_ratio = 0.0 if min_lr_ratio is None else min_lr_ratio
+    assert 0.0 <= min_lr_ratio <= 1.0
+    half_span, mid = (1.0 - min_lr_ratio) * 0.5, (1.0 + min_lr_ratio) * 0.5
+    warm, total = int(num_warmup_steps), int(num_training_steps)
+
+    def factor(step: int) -> float:
+        if step < warm:
+            return min_lr_ratio + (1.0 - min_lr_ratio) * (float(step) / float(max(1, warm)))
+        progress = float(step - warm) / float(max(1, total - warm))
+        return max(min_lr_ratio, math.cos(math.pi * float(num_cycles) * 2.0 * progress) * half_span + mid)
+
+    return LambdaLR(optimizer, factor, last_epoch)
+
+
+def get_constant_schedule_with_warmup(optimizer, num_warmup_steps: int, last_epoch: int = -1):
+    """torch_functional.py:553-575: step / warmup during the warmup steps, then 1."""
+    from torch.optim.lr_scheduler import LambdaLR
+
+    warm = num_warmup_steps
+
+    def factor(step: int) -> float:
+        return float(step) / float(max(1.0, warm)) if step < warm else 1.0
+
+    return LambdaLR(optimizer, factor, last_epoch)
+
+
+def build_lr_scheduler(optimizer, optim_config, role: str = "actor", rank: int = 0):
+    """The scheduler the reference's workers build next to the optimizer (actor:
+    fsdp_workers.py:425-450, critic: :1149-1170): warmup steps from lr_warmup_steps, or from
+    lr_warmup_steps_ratio x total_training_steps when negative; "constant" or "cosine"
+    (the actor's cosine takes min_lr_ratio / num_cycles, the critic's uses the defaults)."""
+    total_steps = optim_config.get("total_training_steps", 0)
+    num_warmup_steps = int(optim_config.get("lr_warmup_steps", -1))
+    warmup_style = optim_config.get("warmup_style", "constant")
+    if num_warmup_steps < 0:
+        num_warmup_steps = int(optim_config.get("lr_warmup_steps_ratio", 0.0) * total_steps)
+    if rank == 0:
+        print(f"Total steps: {total_steps}, num_warmup_steps: {num_warmup_steps}")
+    if warmup_style == "constant":
+        return get_constant_schedule_with_warmup(optimizer=optimizer, num_warmup_steps=num_warmup_steps)
+    if warmup_style == "cosine":
+        if role == "actor":
+            return get_cosine_schedule_with_warmup(optimizer=optimizer, num_warmup_steps=num_warmup_steps,
+                                                   num_training_steps=total_steps,
+                                                   min_lr_ratio=optim_config.get("min_lr_ratio", 0.0),
+                                                   num_cycles=optim_config.get("num_cycles", 0.5))
+        return get_cosine_schedule_with_warmup(optimizer=optimizer, num_warmup_steps=num_warmup_steps,
+                                               num_training_steps=total_steps)
+    raise NotImplementedError(f"Warmup style {warmup_style} is not supported")

@@ -174,6 +174,22 @@ def register() -> str:
     return _NAME
 
 
+def use_packed_attention(model, backbone) -> None:
+    """Route the decoder's HF attention through the packed varlen function. For Qwen2-VL only the
+    language model's config is switched: its vision tower runs full (non-causal) attention over
+    image patches with its own implementation."""
+    name = register()
+    from .qwen2_fused import text_backbone
+
+    stack = text_backbone(backbone)
+    if stack is not backbone:
+        stack.config._attn_implementation = name
+    elif hasattr(model, "set_attn_implementation"):
+        model.set_attn_implementation(name)
+    else:
+        model.config._attn_implementation = name
+
+
 def varlen_available(device) -> bool:
     """True when PyTorch-ROCm's flash varlen kernel runs on this device."""
     try:

@@ -10,7 +10,11 @@ reference. What changes is how the hot path maps onto the GPU:
     lm_head (the reference materialises logits for prompt tokens too and slices afterwards,
     dp_actor.py:219-237); log-probs at masked-out positions are 0 here;
   * temperature, log-softmax, label gather and entropy are ONE fused gfx950 kernel pass over
-    the logits (va_logprob_entropy_fwd); its backward writes dlogits in place;
+    the logits (va_logprob_entropy_fwd); its backward writes dlogits in place (the reference's
+    inplace_backward) or, with logprob_inplace_backward=False (the bench), into a fresh buffer;
+  * Qwen2-VL (BASELINE config 4): mrope position ids [B, 3, S] pack to [3, T] and the fused
+    backbone selects the rotary sections (qwen2_fused.rotary); multi_modal_inputs go through the
+    model's own vision tower (HF; outside SURVEY §8) onto the placeholder tokens;
   * the clipped policy loss, KL loss, entropy aggregation and metrics are one fused kernel
     (va_ppo_loss_fwd/bwd); metrics stay on device and are read once per update;
   * gradients are averaged across DP ranks by a bucketed RCCL all-reduce overlapped with the
@@ -72,12 +76,18 @@ class _Packing:
     pad_pos: torch.Tensor = None  # [pad] int64 position ids of the dummy sequence
 
     def gather(self, input_ids: torch.Tensor, position_ids: torch.Tensor):
-        """Packed (ids [T], pos [T]) of the real tokens, followed by the dummy sequence."""
+        """Packed (ids [T], pos [T]) of the real tokens, followed by the dummy sequence. Qwen2-VL's
+        mrope position ids [B, 3, S] pack to [3, T] (dp_actor.py:106-121: (bsz, 3, seqlen) ->
+        (3, bsz, seqlen) -> (3, total_nnz)); the dummy sequence gets 0..pad-1 on all three rows."""
         ids = input_ids.reshape(-1).index_select(0, self.token_idx)
-        pos = position_ids.reshape(-1).index_select(0, self.token_idx)
+        if position_ids.dim() == 3:
+            c = position_ids.shape[1]
+            pos = position_ids.transpose(0, 1).reshape(c, -1).index_select(1, self.token_idx)
+        else:
+            pos = position_ids.reshape(-1).index_select(0, self.token_idx)
         if self.pad:
             ids = torch.cat([ids, ids.new_zeros(self.pad)])
-            pos = torch.cat([pos, self.pad_pos])
+            pos = torch.cat([pos, self.pad_pos.expand(*pos.shape[:-1], self.pad)], dim=-1)
         return ids, pos
 
 
@@ -125,6 +135,39 @@ def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device, pad_multiple: int =
     )
 
 
+def _mm_kwargs(multi_modal_inputs, device=None) -> dict:
+    """dp_actor.py:94-98: the rows' multi-modal tensors concatenated along dim 0, on ``device``
+    (the reference's FSDP module moves forward inputs to its device)."""
+    if multi_modal_inputs is None or len(multi_modal_inputs) == 0:
+        return {}
+    return {k: torch.cat([d[k] for d in multi_modal_inputs], dim=0).to(device) for k in multi_modal_inputs[0]}
+
+
+def hf_packed_hidden(backbone, ids: torch.Tensor, pos: torch.Tensor, packing: _Packing, multi_modal_inputs=None):
+    """The HF backbone on one packed sequence (dp_actor.py:167-174: input_ids (1, nnz), position_ids
+    (1, nnz) or (3, 1, nnz) for mrope, no attention mask, flash varlen via cu_seq_lens) -> [T, H]."""
+    pos = pos.unsqueeze(0) if pos.dim() == 1 else pos.unsqueeze(1)
+    inputs = dict(input_ids=ids.unsqueeze(0))
+    if multi_modal_inputs:
+        # the vision tower's outputs scattered over the placeholders here (qwen2_fused.input_embeddings),
+        # so the packed-attention kwargs below reach the decoder only, never the vision tower
+        from .qwen2_fused import input_embeddings
+
+        inputs = dict(inputs_embeds=input_embeddings(backbone, ids, multi_modal_inputs).unsqueeze(0))
+    out = backbone(
+        **inputs, position_ids=pos, attention_mask=packed_mask_arg(backbone),
+        use_cache=False, cu_seq_lens_q=packing.cu_seqlens, cu_seq_lens_k=packing.cu_seqlens,
+        max_length_q=packing.max_seqlen, max_length_k=packing.max_seqlen,
+    )
+    return out.last_hidden_state[0]
+
+
+def _multi_modal(mb: DataProto):
+    """The micro-batch's multi_modal_inputs (non-tensor key, dp_actor.py:315-317), or None."""
+    v = mb.non_tensor_batch.get("multi_modal_inputs") if mb.non_tensor_batch else None
+    return None if v is None else list(v)
+
+
 class DataParallelPPOActor(BasePPOActor):
     def __init__(self, config, actor_module: nn.Module, actor_optimizer: torch.optim.Optimizer = None,
                  grad_reducer=None):
@@ -142,11 +185,7 @@ class DataParallelPPOActor(BasePPOActor):
         self._backbone = getattr(actor_module, base_prefix)
         self._lm_head = actor_module.get_output_embeddings()
         if self.use_remove_padding:
-            name = attention.register()
-            if hasattr(actor_module, "set_attn_implementation"):
-                actor_module.set_attn_implementation(name)
-            else:
-                actor_module.config._attn_implementation = name
+            attention.use_packed_attention(actor_module, self._backbone)
         self.device_name = "cuda"
         # bf16 autocast as the reference (dp_actor.py:100); None runs the model in its own dtype
         self.autocast_dtype = self.config.get("autocast_dtype", torch.bfloat16)
@@ -191,8 +230,10 @@ class DataParallelPPOActor(BasePPOActor):
             use_tuned_gemms(gemm_table)
 
     # ------------------------------------------------------------------ forward
-    def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False, packing: _Packing = None):
-        """Returns (entropy or None, log_probs), both [bs, response_len] fp32."""
+    def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False, packing: _Packing = None,
+                             multi_modal_inputs=None):
+        """Returns (entropy or None, log_probs), both [bs, response_len] fp32. ``multi_modal_inputs``:
+        the micro-batch's per-row dicts (non-tensor batch key of the same name, dp_actor.py:89-98)."""
         responses = micro_batch["responses"]
         R = responses.size(-1)
         input_ids = micro_batch["input_ids"]
@@ -203,11 +244,7 @@ class DataParallelPPOActor(BasePPOActor):
                 if packing is None:
                     packing = _plan_packing(micro_batch["attention_mask"].cpu().numpy(), R, input_ids.device,
                                             self.pack_pad_multiple)
-                pos_ids = micro_batch["position_ids"]
-                if pos_ids.dim() == 3:
-                    raise NotImplementedError("mrope position ids (VLM) are out of scope")
-                ids, pos = packing.gather(input_ids, pos_ids)
-                ids, pos = ids.unsqueeze(0), pos.unsqueeze(0)
+                ids, pos = packing.gather(input_ids, micro_batch["position_ids"])
                 if self._fused_backbone is None:
                     from . import qwen2_fused
 
@@ -216,17 +253,12 @@ class DataParallelPPOActor(BasePPOActor):
                     from .qwen2_fused import packed_forward
 
                     fa = self.fused_attention
-                    hidden = packed_forward(self._backbone, ids[0], pos[0], packing.cu_seqlens, packing.max_seqlen,
+                    hidden = packed_forward(self._backbone, ids, pos, packing.cu_seqlens, packing.max_seqlen,
                                             attn_blocks=packing.attn_blocks if fa else None,
-                                            attn_kblocks=packing.attn_kblocks if fa else None)
+                                            attn_kblocks=packing.attn_kblocks if fa else None,
+                                            multi_modal_inputs=multi_modal_inputs)
                 else:
-                    out = self._backbone(
-                        input_ids=ids, position_ids=pos, attention_mask=packed_mask_arg(self._backbone),
-                        use_cache=False,
-                        cu_seq_lens_q=packing.cu_seqlens, cu_seq_lens_k=packing.cu_seqlens,
-                        max_length_q=packing.max_seqlen, max_length_k=packing.max_seqlen,
-                    )
-                    hidden = out.last_hidden_state[0]
+                    hidden = hf_packed_hidden(self._backbone, ids, pos, packing, multi_modal_inputs)
                 h_sel = hidden.index_select(0, packing.sel_hidden)
                 labels = responses.reshape(-1).index_select(0, packing.sel_out)
                 if self._use_fused_lm_head():
@@ -251,9 +283,12 @@ class DataParallelPPOActor(BasePPOActor):
                 if calculate_entropy:
                     entropy = ent_sel.new_zeros(B * R).index_copy(0, packing.sel_out, ent_sel).view(B, R)
             else:
+                pos_ids = micro_batch["position_ids"]
+                if pos_ids.dim() == 3:  # qwen2vl mrope (bsz, 3, seqlen) -> (3, bsz, seqlen), dp_actor.py:106-107
+                    pos_ids = pos_ids.transpose(0, 1)
                 out = self._backbone(
                     input_ids=input_ids, attention_mask=micro_batch["attention_mask"],
-                    position_ids=micro_batch["position_ids"], use_cache=False,
+                    position_ids=pos_ids, use_cache=False, **_mm_kwargs(multi_modal_inputs, input_ids.device),
                 )
                 hidden = out.last_hidden_state[:, -R - 1 : -1]
                 logits = self._lm_head(hidden)
@@ -273,7 +308,13 @@ class DataParallelPPOActor(BasePPOActor):
         batch) always copies it (refresh=True: the GPU is idle there anyway); update_policy reuses
         that copy while the tensor is the same unmodified one (same storage, shape and version):
         a second D2H copy at the start of the update would drain the queued old-logp pass and
-        advantage work and leave the GPU idle while the host plans the update."""
+        advantage work and leave the GPU idle while the host plans the update.
+
+        Contract: the attention mask must not change between compute_log_prob and update_policy
+        of one step other than through ordinary in-place tensor writes (which bump the version);
+        writes through ``.data`` or through another tensor sharing the storage are not seen and
+        would leave the update planned from the stale copy. The step driver
+        (trainer_step.PPOTrainerStep) never writes the mask."""
         # the cache holds the device tensor itself, so its storage cannot be freed and reused by
         # another batch's mask while the key (pointer, shape, in-place version) is compared
         key = (am_t.data_ptr(), tuple(am_t.shape), am_t._version, am_t.device)
@@ -314,15 +355,7 @@ class DataParallelPPOActor(BasePPOActor):
         assert self.config.grad_clip is not None
         if self.grad_reducer is not None:
             self.grad_reducer.finish_sync()
-        if (self.grad_reducer is not None and hasattr(self.grad_reducer, "clip_grad_norm_")
-                and not (_TORCH_CLIP and not hasattr(self.grad_reducer, "shards"))):
-            # the manager's own clip (fsdp_utils.py:503-516): over the flat fp32 buckets, or the
-            # global norm over the ranks' shards for the sharded optimizer state
-            grad_norm = self.grad_reducer.clip_grad_norm_(self.config.grad_clip)
-        else:
-            params = (self.grad_reducer.optimizer_params() if self.grad_reducer is not None
-                      else list(self.actor_module.parameters()))
-            grad_norm = torch.nn.utils.clip_grad_norm_(params, max_norm=self.config.grad_clip, foreach=True)
+        grad_norm = clip_grad_norm(self.grad_reducer, self.actor_module, self.config.grad_clip)
         return step_unless_nonfinite(self.actor_optimizer, grad_norm, self._zero_grad,
                                      self.grad_reducer.after_step if self.grad_reducer is not None else None)
 
@@ -334,7 +367,9 @@ class DataParallelPPOActor(BasePPOActor):
         micro_batch_size = data.meta_info["micro_batch_size"]
         temperature = data.meta_info["temperature"]
         use_dynamic_bsz = data.meta_info["use_dynamic_bsz"]
-        data = data.select(batch_keys=["responses", "input_ids", "attention_mask", "position_ids"])
+        has_mm = "multi_modal_inputs" in data.non_tensor_batch.keys()
+        data = data.select(batch_keys=["responses", "input_ids", "attention_mask", "position_ids"],
+                           non_tensor_batch_keys=["multi_modal_inputs"] if has_mm else [])
         am = self._mask_host(data.batch["attention_mask"], refresh=True) if self.use_remove_padding else None
         if use_dynamic_bsz:
             # dp_actor.py:321-323: micro-batches cut by a token budget, restored afterwards
@@ -346,7 +381,7 @@ class DataParallelPPOActor(BasePPOActor):
             plans = self._plans(data, [len(m) for m in micro_batches], am=am)
         lps, ents = [], []
         for mb, plan in zip(micro_batches, plans, strict=True):
-            ent, lp = self._forward_micro_batch(mb.batch, temperature, calculate_entropy, plan)
+            ent, lp = self._forward_micro_batch(mb.batch, temperature, calculate_entropy, plan, _multi_modal(mb))
             lps.append(lp)
             if calculate_entropy:
                 ents.append(ent)
@@ -368,7 +403,8 @@ class DataParallelPPOActor(BasePPOActor):
                 "advantages"]
         if cfg.use_kl_loss:
             keys.append("ref_log_prob")
-        data = data.select(batch_keys=keys)
+        has_mm = "multi_modal_inputs" in data.non_tensor_batch.keys()
+        data = data.select(batch_keys=keys, non_tensor_batch_keys=["multi_modal_inputs"] if has_mm else [])
         am_full = self._mask_host(data.batch["attention_mask"], refresh=False) if self.use_remove_padding else None
         mini_batches = data.split(cfg.ppo_mini_batch_size)
         if not cfg.use_dynamic_bsz:
@@ -400,7 +436,7 @@ class DataParallelPPOActor(BasePPOActor):
                     b = mb.batch
                     response_mask = b["response_mask"]
                     calc_ent = entropy_coeff != 0
-                    entropy, log_prob = self._forward_micro_batch(b, temperature, calc_ent, plan)
+                    entropy, log_prob = self._forward_micro_batch(b, temperature, calc_ent, plan, _multi_modal(mb))
                     m = {}
                     if loss_mode == "vanilla":
                         out = core_algos.compute_actor_loss(
@@ -465,6 +501,18 @@ class DataParallelPPOActor(BasePPOActor):
 # VERL_AMD_TORCH_CLIP=1: torch.nn.utils.clip_grad_norm_ over the masters even when the parameter
 # manager has its bucket clip (A/B runs; the sharded manager always uses its own)
 _TORCH_CLIP = os.environ.get("VERL_AMD_TORCH_CLIP", "0") == "1"
+
+
+def clip_grad_norm(grad_reducer, module: nn.Module, max_norm: float) -> torch.Tensor:
+    """Global gradient-norm clip of the actor or critic (dp_actor.py:272-280, dp_critic.py:138-146):
+    the parameter manager's own clip (fsdp_utils.py:503-516) over its flat fp32 buckets, or the
+    global norm over the ranks' shards for the sharded optimizer state; torch's clip_grad_norm_
+    over the masters without a manager or with VERL_AMD_TORCH_CLIP=1 (replicated managers only)."""
+    if (grad_reducer is not None and hasattr(grad_reducer, "clip_grad_norm_")
+            and not (_TORCH_CLIP and not hasattr(grad_reducer, "shards"))):
+        return grad_reducer.clip_grad_norm_(max_norm)
+    params = grad_reducer.optimizer_params() if grad_reducer is not None else list(module.parameters())
+    return torch.nn.utils.clip_grad_norm_(params, max_norm=max_norm, foreach=True)
 
 
 def step_unless_nonfinite(optimizer, grad_norm: torch.Tensor, zero_grad, after_step=None):

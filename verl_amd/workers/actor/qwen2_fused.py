@@ -21,7 +21,12 @@ the GEMM reads the merged matrix with no per-call concatenation while optimizers
 the fp32-master copy-back keep addressing the original Parameters.
 
 Only bf16 Qwen2-family backbones (RMSNorm + SwiGLU MLP + rotate_half RoPE + GQA with q/k/v bias)
-take this path; anything else keeps the HF forward.
+take this path; anything else keeps the HF forward. Qwen2-VL's language model (BASELINE config 4)
+is the same decoder with multimodal RoPE: its packed position ids are [3, T] (temporal, height,
+width; dp_actor.py:106-121) and the rotary cos / sin of each channel section come from one of the
+three rows (transformers' apply_multimodal_rotary_pos_emb), after which the same rope_qkv kernel
+applies. Image / video embeddings come from the model's own vision tower (HF, outside SURVEY §8)
+and are scattered over the placeholder tokens of the packed sequence, as the HF model does.
 """
 
 from __future__ import annotations
@@ -49,26 +54,106 @@ def _decoder_families():
         fams.append(modeling_llama.LlamaModel)
     except ImportError:  # pragma: no cover
         pass
+    vl = _qwen2_vl_text_model()
+    if vl is not None:
+        fams.append(vl)
     return tuple(fams)
 
 
+def _qwen2_vl_text_model():
+    try:
+        from transformers.models.qwen2_vl import modeling_qwen2_vl
+
+        return modeling_qwen2_vl.Qwen2VLTextModel
+    except ImportError:  # pragma: no cover
+        return None
+
+
+def text_backbone(backbone: torch.nn.Module) -> torch.nn.Module:
+    """The decoder stack of an actor / critic backbone: Qwen2-VL's Qwen2VLModel keeps it as
+    ``language_model`` beside the vision tower ``visual``; text models are their own stack."""
+    lm = getattr(backbone, "language_model", None)
+    return lm if lm is not None and hasattr(backbone, "visual") else backbone
+
+
+def mrope_section(stack: torch.nn.Module):
+    """Channel sections (temporal, height, width) of a multimodal-RoPE decoder stack, else None."""
+    vl = _qwen2_vl_text_model()
+    if vl is None or not isinstance(stack, vl):
+        return None
+    rope = getattr(stack.config, "rope_parameters", None) or getattr(stack.config, "rope_scaling", None) or {}
+    sec = rope.get("mrope_section")
+    return list(sec) if sec else None
+
+
 def supports(backbone: torch.nn.Module) -> bool:
+    stack = text_backbone(backbone)
     fams = _decoder_families()
-    if not fams or not isinstance(backbone, fams):
+    if not fams or not isinstance(stack, fams):
         return False
-    cfg = backbone.config
+    cfg = stack.config
     if getattr(cfg, "hidden_act", "silu") != "silu" or getattr(cfg, "use_sliding_window", False):
         return False
-    rope = (getattr(cfg, "rope_scaling", None) or {})
-    if rope.get("rope_type", rope.get("type", "default")) in ("mrope", "longrope"):
-        return False  # multimodal / per-position factor tables: keep the HF forward
     h = cfg.hidden_size
     if h % 8 or h > 4096:
         return False
     d = getattr(cfg, "head_dim", None) or h // cfg.num_attention_heads
     if d % 16:
         return False
-    return all(p.dtype == torch.bfloat16 for p in backbone.parameters())
+    sec = mrope_section(stack)
+    if sec is not None:
+        if sum(sec) != d // 2:
+            return False
+    else:
+        rope = (getattr(cfg, "rope_scaling", None) or {})
+        if rope.get("rope_type", rope.get("type", "default")) in ("mrope", "longrope"):
+            return False  # per-position factor tables / unknown multimodal layouts: keep the HF forward
+    return all(p.dtype == torch.bfloat16 for p in stack.parameters())
+
+
+def rotary(stack: torch.nn.Module, x: torch.Tensor, position_ids: torch.Tensor):
+    """cos / sin [1, T, D] of packed positions: [T] for 1-D RoPE; [3, T] (or [T], replicated as
+    the HF text model does for text-only input) for multimodal RoPE, where channel section i of
+    the doubled section list takes row i % 3 (apply_multimodal_rotary_pos_emb)."""
+    sec = mrope_section(stack)
+    if sec is None:
+        return stack.rotary_emb(x.unsqueeze(0), position_ids.unsqueeze(0))
+    if position_ids.dim() == 1:
+        position_ids = position_ids.expand(3, -1)
+    cos, sin = stack.rotary_emb(x.unsqueeze(0), position_ids.unsqueeze(1))  # [3, 1, T, D]
+    parts = sec * 2
+    cos = torch.cat([c[i % 3] for i, c in enumerate(cos.split(parts, dim=-1))], dim=-1)
+    sin = torch.cat([s_[i % 3] for i, s_ in enumerate(sin.split(parts, dim=-1))], dim=-1)
+    return cos, sin
+
+
+def input_embeddings(backbone: torch.nn.Module, input_ids: torch.Tensor, multi_modal_inputs: list = None):
+    """Token embeddings of a packed sequence [T] -> [T, H]. For Qwen2-VL with multi_modal_inputs
+    (one dict per row: pixel_values / image_grid_thw, pixel_values_videos / video_grid_thw,
+    concatenated in row order as dp_actor.py:94-98), the vision tower's outputs replace the image /
+    video placeholder tokens in order (Qwen2VLModel.forward). The packing keeps row order and token
+    order, so the placeholders meet the images in the same order as in the padded batch."""
+    stack = text_backbone(backbone)
+    x = stack.embed_tokens(input_ids)
+    if not multi_modal_inputs:
+        return x
+    if stack is backbone:
+        raise NotImplementedError("multi_modal_inputs given to a text-only backbone")
+    mm = {k: torch.cat([d[k] for d in multi_modal_inputs], dim=0).to(input_ids.device) for k in multi_modal_inputs[0]}
+    cfg = backbone.config
+    for pix, grid, tok, fn in (("pixel_values", "image_grid_thw", "image_token_id", "get_image_features"),
+                               ("pixel_values_videos", "video_grid_thw", "video_token_id", "get_video_features")):
+        if pix not in mm:
+            continue
+        out = getattr(backbone, fn)(mm[pix], mm[grid])
+        emb = getattr(out, "pooler_output", out)
+        emb = torch.cat(list(emb), dim=0) if isinstance(emb, (list, tuple)) else emb
+        sel = input_ids == getattr(cfg, tok)
+        n = int(sel.sum())
+        if n != emb.shape[0]:
+            raise ValueError(f"{pix}: {emb.shape[0]} vision embeddings for {n} placeholder tokens")
+        x = x.masked_scatter(sel.unsqueeze(-1), emb.to(x.dtype))
+    return x
 
 
 def _merged(module, key: str, params: list):
@@ -117,17 +202,20 @@ def _attention(attn, y, cos, sin, cu, max_len, hq, hk, d, attn_blocks=None, attn
 
 
 def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor, cu_seqlens: torch.Tensor,
-                   max_seqlen: int, attn_blocks: torch.Tensor = None, attn_kblocks: torch.Tensor = None) -> torch.Tensor:
-    """input_ids / position_ids [T] (packed), cu_seqlens [B+1] int32 -> last hidden state [T, H] bf16
-    (after the final norm), i.e. Qwen2Model(...).last_hidden_state[0] on the same packing."""
-    cfg = backbone.config
+                   max_seqlen: int, attn_blocks: torch.Tensor = None, attn_kblocks: torch.Tensor = None,
+                   multi_modal_inputs: list = None) -> torch.Tensor:
+    """input_ids [T] and position_ids [T] (or [3, T], mrope) packed, cu_seqlens [B+1] int32 -> last
+    hidden state [T, H] bf16 (after the final norm), i.e. Qwen2Model(...).last_hidden_state[0] on
+    the same packing."""
+    stack = text_backbone(backbone)
+    cfg = stack.config
     hq = cfg.num_attention_heads
     hk = cfg.num_key_value_heads
     d = getattr(cfg, "head_dim", None) or cfg.hidden_size // hq
-    x = backbone.embed_tokens(input_ids)  # [T, H]
-    cos, sin = backbone.rotary_emb(x.unsqueeze(0), position_ids.unsqueeze(0))  # [1, T, D] bf16
+    x = input_embeddings(backbone, input_ids, multi_modal_inputs)  # [T, H]
+    cos, sin = rotary(stack, x, position_ids)  # [1, T, D] bf16
     residual = x
-    layers = backbone.layers[: cfg.num_hidden_layers]
+    layers = stack.layers[: cfg.num_hidden_layers]
     h = None
     for i, layer in enumerate(layers):
         ln = layer.input_layernorm
@@ -143,7 +231,7 @@ def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor
         dp = mlp.down_proj
         a = K.swiglu_merged(gu)
         h = K.linear(a, dp.weight) if dp.bias is None else dp(a)
-    norm = backbone.norm
+    norm = stack.norm
     if h is None:
         return K.rmsnorm(residual, norm.weight, norm.variance_epsilon)
     _, y = K.add_rmsnorm(h, residual, norm.weight, norm.variance_epsilon)

@@ -26,7 +26,8 @@ from ... import kernels as K
 from ...protocol import DataProto
 from ...utils.seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
 from ..actor import attention
-from ..actor.dp_actor import _plan_packing, _to_host, append_to_dict, packed_mask_arg, step_unless_nonfinite
+from ..actor.dp_actor import (_mm_kwargs, _multi_modal, _plan_packing, _to_host, append_to_dict, clip_grad_norm,
+                              hf_packed_hidden, step_unless_nonfinite)
 from .base import BasePPOCritic
 
 __all__ = ["DataParallelPPOCritic"]
@@ -50,11 +51,7 @@ class DataParallelPPOCritic(BasePPOCritic):
         if self._head is None:
             raise NotImplementedError("critic needs a token-classification value head (.score, num_labels=1)")
         if self.use_remove_padding:
-            name = attention.register()
-            if hasattr(critic_module, "set_attn_implementation"):
-                critic_module.set_attn_implementation(name)
-            else:
-                critic_module.config._attn_implementation = name
+            attention.use_packed_attention(critic_module, self._backbone)
         self.fused_model_ops = self.use_remove_padding and self.config.get("fused_model_ops", True)
         self._fused_backbone = None
         # as the actor: pad packed micro-batches to a multiple of this many tokens (0 = off) and
@@ -66,14 +63,13 @@ class DataParallelPPOCritic(BasePPOCritic):
             use_tuned_gemms(self.config.gemm_tuning_file)
 
     # ------------------------------------------------------------------ forward
-    def _forward_micro_batch(self, micro_batch, packing=None) -> torch.Tensor:
-        """values [bs, response_len] fp32 (dp_critic.py:57-136)."""
+    def _forward_micro_batch(self, micro_batch, packing=None, multi_modal_inputs=None) -> torch.Tensor:
+        """values [bs, response_len] fp32 (dp_critic.py:57-136); mrope position ids [bs, 3, S] and
+        multi_modal_inputs as the actor (dp_critic.py:59-90)."""
         R = micro_batch["responses"].size(-1)
         input_ids = micro_batch["input_ids"]
         B, S = input_ids.shape
         position_ids = micro_batch["position_ids"]
-        if position_ids.dim() == 3:
-            raise NotImplementedError("mrope position ids (VLM) are out of scope")
         with torch.autocast(device_type=self.device_name, dtype=torch.bfloat16):
             if self.use_remove_padding:
                 if packing is None:
@@ -90,20 +86,18 @@ class DataParallelPPOCritic(BasePPOCritic):
                     fa = self.config.get("fused_attention", True)
                     hidden = packed_forward(self._backbone, ids, pos, packing.cu_seqlens, packing.max_seqlen,
                                             attn_blocks=packing.attn_blocks if fa else None,
-                                            attn_kblocks=packing.attn_kblocks if fa else None)
+                                            attn_kblocks=packing.attn_kblocks if fa else None,
+                                            multi_modal_inputs=multi_modal_inputs)
                 else:
-                    out = self._backbone(
-                        input_ids=ids.unsqueeze(0), position_ids=pos.unsqueeze(0),
-                        attention_mask=packed_mask_arg(self._backbone),
-                        use_cache=False, cu_seq_lens_q=packing.cu_seqlens, cu_seq_lens_k=packing.cu_seqlens,
-                        max_length_q=packing.max_seqlen, max_length_k=packing.max_seqlen,
-                    )
-                    hidden = out.last_hidden_state[0]
+                    hidden = hf_packed_hidden(self._backbone, ids, pos, packing, multi_modal_inputs)
                 v_sel = self._head(hidden.index_select(0, packing.sel_hidden)).squeeze(-1).float()
                 values = v_sel.new_zeros(B * R).index_copy(0, packing.sel_out, v_sel).view(B, R)
             else:
+                if position_ids.dim() == 3:  # qwen2vl mrope (dp_critic.py:71-72)
+                    position_ids = position_ids.transpose(0, 1)
                 out = self.critic_module(input_ids=input_ids, attention_mask=micro_batch["attention_mask"],
-                                         position_ids=position_ids, use_cache=False)
+                                         position_ids=position_ids, use_cache=False,
+                                         **_mm_kwargs(multi_modal_inputs, input_ids.device))
                 values = out.logits[:, -R - 1 : -1].squeeze(-1).float()
         return values
 
@@ -137,14 +131,7 @@ class DataParallelPPOCritic(BasePPOCritic):
         assert self.config.grad_clip is not None
         if self.grad_reducer is not None:
             self.grad_reducer.finish_sync()
-        if self.grad_reducer is not None and hasattr(self.grad_reducer, "clip_grad_norm_"):
-            # the manager's own clip (fsdp_utils.py:503-516): over the flat fp32 buckets, or the
-            # global norm over the ranks' shards for the sharded optimizer state
-            grad_norm = self.grad_reducer.clip_grad_norm_(self.config.grad_clip)
-        else:
-            params = (self.grad_reducer.optimizer_params() if self.grad_reducer is not None
-                      else list(self.critic_module.parameters()))
-            grad_norm = torch.nn.utils.clip_grad_norm_(params, max_norm=self.config.grad_clip, foreach=True)
+        grad_norm = clip_grad_norm(self.grad_reducer, self.critic_module, self.config.grad_clip)
         return step_unless_nonfinite(self.critic_optimizer, grad_norm, self._zero_grad,
                                      self.grad_reducer.after_step if self.grad_reducer is not None else None)
 
@@ -155,7 +142,9 @@ class DataParallelPPOCritic(BasePPOCritic):
         self.critic_module.eval()
         micro_batch_size = data.meta_info["micro_batch_size"]
         use_dynamic_bsz = data.meta_info["use_dynamic_bsz"]
-        data = data.select(batch_keys=["responses", "input_ids", "response_mask", "attention_mask", "position_ids"])
+        has_mm = "multi_modal_inputs" in data.non_tensor_batch.keys()
+        data = data.select(batch_keys=["responses", "input_ids", "response_mask", "attention_mask", "position_ids"],
+                           non_tensor_batch_keys=["multi_modal_inputs"] if has_mm else [])
         if use_dynamic_bsz:
             max_token_len = data.meta_info["max_token_len"] * self.ulysses_sequence_parallel_size
             micro_batches, batch_idx_list = prepare_dynamic_batch(data, max_token_len=max_token_len)
@@ -163,7 +152,8 @@ class DataParallelPPOCritic(BasePPOCritic):
         else:
             micro_batches = data.split(micro_batch_size)
             plans = self._plans(data, [len(m) for m in micro_batches])
-        vals = [self._forward_micro_batch(mb.batch, plan) for mb, plan in zip(micro_batches, plans, strict=True)]
+        vals = [self._forward_micro_batch(mb.batch, plan, _multi_modal(mb))
+                for mb, plan in zip(micro_batches, plans, strict=True)]
         values = torch.concat(vals, dim=0)
         if use_dynamic_bsz:
             values = restore_dynamic_batch(values, batch_idx_list)
@@ -175,7 +165,8 @@ class DataParallelPPOCritic(BasePPOCritic):
         self.critic_module.train()
         cfg = self.config
         keys = ["input_ids", "responses", "response_mask", "attention_mask", "position_ids", "values", "returns"]
-        data = data.select(batch_keys=keys)
+        has_mm = "multi_modal_inputs" in data.non_tensor_batch.keys()
+        data = data.select(batch_keys=keys, non_tensor_batch_keys=["multi_modal_inputs"] if has_mm else [])
         mini_batches = data.split(cfg.ppo_mini_batch_size)
         dev_metrics: dict = {}
         for _ in range(cfg.ppo_epochs):
@@ -192,7 +183,7 @@ class DataParallelPPOCritic(BasePPOCritic):
                 for i, (mb, plan) in enumerate(zip(micro_batches, plans, strict=True)):
                     b = mb.batch
                     response_mask = b["response_mask"]
-                    vpreds = self._forward_micro_batch(b, plan)
+                    vpreds = self._forward_micro_batch(b, plan, _multi_modal(mb))
                     out = K.fused_value_loss(vpreds, b["values"], b["returns"], response_mask, cfg.cliprange_value,
                                              cfg.loss_agg_mode)
                     vf_loss = out[L.VA_VLOSS_LOSS]

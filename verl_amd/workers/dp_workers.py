@@ -12,11 +12,14 @@ batch; an SPMD caller passes each rank its own shard directly.
 from __future__ import annotations
 
 import os
+import time
 
 import torch
 import torch.distributed as dist
 
 from ..protocol import DataProto
+from ..utils.flops_counter import FlopsCounter
+from ..utils.torch_functional import build_lr_scheduler
 from .actor import DataParallelPPOActor
 from .grad_sync import GradBucketReducer, MixedPrecisionParams, ShardedMixedPrecisionParams
 
@@ -106,6 +109,9 @@ class ActorWorker:
                                 betas=tuple(optim.get("betas", (0.9, 0.999))),
                                 weight_decay=optim.get("weight_decay", 0.01), fused=fused)
         self.actor = DataParallelPPOActor(self.config.actor, module, opt, grad_reducer=manager)
+        self.actor_optimizer = opt
+        self.actor_lr_scheduler = build_lr_scheduler(opt, optim, role="actor", rank=self.rank)
+        self.flops_counter = FlopsCounter(module.config)
         return self
 
     def init_ref_model(self, module: torch.nn.Module, mixed_precision: bool = True):
@@ -157,8 +163,19 @@ class ActorWorker:
                                     norm_adv_by_std_in_grpo=norm_adv_by_std_in_grpo, config=config)
 
     def update_actor(self, data: DataProto) -> DataProto:
-        """fsdp_workers.py:672-716: one PPO update; metrics in meta_info."""
+        """fsdp_workers.py:672-716: one PPO update; metrics in meta_info, with the RPC's own
+        additions: perf/mfu/actor (model FLOPs of the whole batch's tokens, meta_info
+        global_token_num, over the update's wall time and the device peak, / world size),
+        perf/max_memory_* and perf/cpu_memory_used_gb, actor/lr (the rate this update used),
+        then one LR-scheduler step. update_policy returns its metrics through one device->host
+        copy, so the host clock here spans the device work of the update."""
+        t0 = time.perf_counter()
         metrics = self.actor.update_policy(data)
+        delta_time = time.perf_counter() - t0
+        metrics.update(perf_metrics(self.flops_counter, data, delta_time, self.config.actor.get("ppo_epochs", 1),
+                                    self.world_size, "actor"))
+        metrics["actor/lr"] = self.actor_lr_scheduler.get_last_lr()[0]
+        self.actor_lr_scheduler.step()
         return DataProto(meta_info={"metrics": metrics})
 
 
@@ -199,6 +216,8 @@ class CriticWorker:
                                 betas=tuple(optim.get("betas", (0.9, 0.999))),
                                 weight_decay=optim.get("weight_decay", 0.01), fused=fused)
         self.critic = DataParallelPPOCritic(self.config, module, opt, grad_reducer=manager)
+        self.critic_lr_scheduler = build_lr_scheduler(opt, optim, role="critic", rank=self.rank)
+        self.flops_counter = FlopsCounter(module.config)
         return self
 
     def compute_values(self, data: DataProto) -> DataProto:
@@ -210,7 +229,34 @@ class CriticWorker:
         return DataProto.from_dict(tensors={"values": values})
 
     def update_critic(self, data: DataProto) -> DataProto:
-        """fsdp_workers.py:1231-1264 (metrics + critic/lr)."""
+        """fsdp_workers.py:1231-1264: metrics + perf/mfu/critic + critic/lr, then one LR-scheduler
+        step."""
+        t0 = time.perf_counter()
         metrics = self.critic.update_critic(data=data)
-        metrics["critic/lr"] = self.critic.critic_optimizer.param_groups[0]["lr"]
+        delta_time = time.perf_counter() - t0
+        mfu = perf_metrics(self.flops_counter, data, delta_time, self.config.get("ppo_epochs", 1), self.world_size,
+                           "critic")
+        metrics["perf/mfu/critic"] = mfu["perf/mfu/critic"]
+        metrics["critic/lr"] = self.critic_lr_scheduler.get_last_lr()[0]
+        self.critic_lr_scheduler.step()
         return DataProto(meta_info={"metrics": metrics})
+
+
+def perf_metrics(flops_counter, data: DataProto, delta_time: float, ppo_epochs: int, world_size: int,
+                 role: str) -> dict:
+    """fsdp_workers.py:690-697: MFU of one update (estimated FLOP/s x epochs / promised / world)
+    and the memory high-water marks. global_token_num lists the valid tokens of every sequence
+    of the whole batch (set by the trainer, ray_trainer.py:1207); without it the rank's own
+    attention mask stands in."""
+    import psutil
+
+    tokens = data.meta_info.get("global_token_num")
+    if tokens is None:
+        tokens = data.batch["attention_mask"].sum(-1).tolist()
+    est, promised = flops_counter.estimate_flops(tokens, delta_time)
+    out = {f"perf/mfu/{role}": est * ppo_epochs / promised / world_size}
+    if torch.cuda.is_available():
+        out["perf/max_memory_allocated_gb"] = torch.cuda.max_memory_allocated() / (1024**3)
+        out["perf/max_memory_reserved_gb"] = torch.cuda.max_memory_reserved() / (1024**3)
+    out["perf/cpu_memory_used_gb"] = psutil.virtual_memory().used / (1024**3)
+    return out
