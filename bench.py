@@ -136,7 +136,10 @@ def parse(argv=None):
     ap.add_argument("--tune", action="append", default=[],
                     help="KEY=VALUE va_set_tuning override for A/B runs (e.g. 8=0: grid-stride SwiGLU)")
     ap.add_argument("--launcher-check", action="store_true",
-                    help="only start the ranks, check the world size and print a JSON line (no GPU work)")
+                    help="only start the ranks, check the world size, run the cross-rank replica check on a "
+                         "small CPU module and print a JSON line (no GPU work)")
+    ap.add_argument("--responses", choices=["dense", "realistic"], default="dense",
+                    help="response lengths: dense (all R valid) or realistic (U[128, R], SURVEY §8d)")
     return ap.parse_args(argv)
 
 
@@ -253,11 +256,12 @@ def shard_batch(args, rank: int, world: int, dev):
     from verl_amd.trainer.ppo.ray_trainer import balance_batch
     from verl_amd.utils.synthetic import make_grpo_batch
 
+    dense = args.responses == "dense"
     if args.scaling == "weak":
         return make_grpo_batch(args.prompts, args.n, args.prompt_len, args.response_len, seed=1234 + rank,
-                               device=dev)
+                               device=dev, dense_responses=dense, min_response=128)
     full = make_grpo_batch(args.prompts, args.n, args.prompt_len, args.response_len, seed=1234,
-                           permute=args.balance)
+                           permute=args.balance, dense_responses=dense, min_response=128)
     B = len(full)
     if B % world:
         raise SystemExit(f"{B} responses do not split evenly over {world} ranks")
@@ -298,11 +302,24 @@ def main():
         t = torch.tensor([rank + 1.0])
         if world > 1:
             dist.all_reduce(t)
+        # the end-of-run replica check on a small CPU model (same seed on every rank);
+        # VA_BENCH_PERTURB_RANK changes one rank's weights after the "update" to prove it fires
+        from verl_amd.utils.replica_check import replica_check
+
+        torch.manual_seed(0)
+        mod = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.Linear(32, 4))
+        perturb = os.environ.get("VA_BENCH_PERTURB_RANK")
+        if perturb is not None and int(perturb) == rank:
+            with torch.no_grad():
+                mod[1].weight[0, 0] += 1e-3
+        rc = replica_check(mod, None, {"actor/grad_norm": [1.5]}, ["actor/grad_norm"], 0.25)
         if rank == 0:
             print(json.dumps({"launcher_check": True, "n_gpus": args.gpus, "world_seen": world_seen,
-                              "rank_sum": float(t.item())}), flush=True)
+                              "rank_sum": float(t.item()), **rc}), flush=True)
         if world > 1:
             dist.destroy_process_group()
+        if not rc["replicas_identical"]:
+            sys.exit(4)
         return
 
     from verl_amd import kernels as K
@@ -400,10 +417,10 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, -elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed, fastest = float(t[0].item()), -float(t[1].item())
     ksum = K.TIMER.summary() if K.TIMER is not None else {}
     K.TIMER = None
     comm = None
@@ -426,6 +443,14 @@ def main():
     perf_throughput = float(total_tokens[1].item()) * args.steps / elapsed / world  # metric_utils.py:249-257
 
     log(rank, f"timed region: {elapsed:.2f}s for {args.steps} steps")
+    # after the timed region: every rank must hold the same model (FSDP's by-construction
+    # consistency, fsdp_workers.py:370-405) and the same globally-reduced metrics
+    from verl_amd.utils.replica_check import replica_check
+
+    rcheck = replica_check(worker.module, worker.actor.grad_reducer,
+                           metrics.meta_info["metrics"] if metrics is not None else {},
+                           ["actor/grad_norm", "actor/lr"], elapsed - fastest)
+    log(rank, f"replica check: {rcheck}")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N = 1 only
         cpu = cpu_baseline(args)
@@ -484,9 +509,16 @@ def main():
                 "micro_batch": micro,
                 "logprob_micro_batch": lp_micro,
                 "old_logp_noise": args.old_noise,
+                "response_lengths": (f"dense: all {R} valid" if args.responses == "dense"
+                                     else f"realistic: U[128, {R}]"),
                 "deviations_from_reference_defaults": (
                     f"ppo_micro_batch_size_per_gpu {micro} (SURVEY §8d: 8; larger micro-batches fill the "
-                    "MI355X GEMMs, same loss semantics: token-mean per micro-batch / grad-accum); "
+                    "MI355X GEMMs); the loss is the reference's token-mean per micro-batch / grad-accum "
+                    "(dp_actor.py:465-470), "
+                    + ("which with dense responses (every micro-batch holds the same token count) equals the "
+                       "reference's at micro-batch 8; " if args.responses == "dense" else
+                       f"which with variable response lengths weights tokens differently at micro-batch {micro} "
+                       "than at 8 (each micro-batch's mean is over its own token count); ")
                     + ("out-of-place log-prob backward (reference: in place)" if not args.logprob_inplace_bwd
                        else "in-place log-prob backward as the reference")),
                 "dynamic_bsz_max_token_len": args.dynamic_bsz or None,
@@ -509,7 +541,10 @@ def main():
             "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in ksum.items()},
             "cpu_baseline": cpu,
-            "final_metrics": {k: v[-1] for k, v in (metrics.meta_info["metrics"].items() if metrics is not None else [])},
+            "replicas_identical": rcheck["replicas_identical"],
+            "replica_check": rcheck,
+            "final_metrics": {k: (v[-1] if isinstance(v, list) else v)
+                              for k, v in (metrics.meta_info["metrics"].items() if metrics is not None else [])},
         }
         s = json.dumps(line)
         print(s, flush=True)
@@ -518,6 +553,9 @@ def main():
                 f.write(s + "\n")
     if world > 1:
         dist.destroy_process_group()
+    if not rcheck["replicas_identical"]:
+        print(f"[bench] rank {rank}: replicas differ after the run: {rcheck}", file=sys.stderr, flush=True)
+        sys.exit(4)
 
 
 if __name__ == "__main__":

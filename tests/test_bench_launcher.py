@@ -40,3 +40,34 @@ def test_world_size_mismatch_is_an_error():
     # under an explicit single-process "launcher" env, --gpus 2 must not silently run one rank
     res = _run(2, {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert res.returncode != 0
+
+
+def test_replica_check_passes_when_ranks_agree_and_fails_when_one_rank_differs():
+    """the end-of-run replica check (utils/replica_check.py) runs through the
+    same launcher; equal replicas report replicas_identical, one rank's weight changed after the
+    update makes the command exit non-zero."""
+    res = _run(2)
+    assert res.returncode == 0, res.stderr[-2000:]
+    rec = [json.loads(x) for x in res.stdout.splitlines() if x.startswith("{")][0]
+    assert rec["replicas_identical"] is True and rec["weights_equal"] and rec["metrics_equal"]
+    bad = _run(2, {"VA_BENCH_PERTURB_RANK": "1"})
+    assert bad.returncode != 0
+    rec = [json.loads(x) for x in bad.stdout.splitlines() if x.startswith("{")][0]
+    assert rec["replicas_identical"] is False and not rec["weights_equal"] and rec["metrics_equal"]
+
+
+def test_bits_checksum_is_order_independent_and_position_sensitive():
+    import torch
+
+    from verl_amd.utils.replica_check import bits_checksum
+
+    g = torch.Generator().manual_seed(0)
+    a = torch.randn(1000, generator=g)
+    b = a.clone()
+    b[[3, 7]] = b[[7, 3]]  # swapped pair
+    c = a.clone()
+    c[5] = torch.nextafter(c[5], torch.tensor(10.0))  # one ulp
+    x = bits_checksum([a, a.to(torch.bfloat16)])
+    assert int(x) == int(bits_checksum([a, a.to(torch.bfloat16)]))
+    assert int(x) != int(bits_checksum([b, a.to(torch.bfloat16)]))
+    assert int(x) != int(bits_checksum([c, a.to(torch.bfloat16)]))
