@@ -70,6 +70,7 @@ def test_flops_counter_qwen2_closed_form_and_device_table():
     assert get_device_flops("T", "AMD Instinct MI300X") == pytest.approx(1336.0)
     assert get_device_flops("P", "AMD Instinct MI350X") == pytest.approx(2.3)
     assert get_device_flops("T", "some GPU") == float("inf")
+    assert get_device_flops("T", "AMD Radeon Graphics gfx950:sramecc+:xnack-") == pytest.approx(2500.0)
 
 
 def test_flops_counter_reads_vl_text_config():

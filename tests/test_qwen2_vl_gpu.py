@@ -12,7 +12,8 @@ Parity: a tiny random-init Qwen2VLForConditionalGeneration (head_dim 64 so the g
 kernels run; mrope sections (8, 12, 12)), one image per prompt with get_rope_index's 3-D ids,
 compute_log_prob + update_policy against the reference computation (padded HF forward with the
 (3, B, S) ids and pixel values + the oracle loss) in float64 and in the reference's own bf16,
-with the error budget of tests/test_bench_config_parity_gpu.py:
+with the error budget of tests/test_bench_config_parity_gpu.py (old log-probs placed so that no
+token sits within rounding noise of a clip boundary):
   log-probs  max |lp - lp64|         <= 2 max |lp_ref16 - lp64| + 2e-3
   pg_loss    |pg - pg64|             <= 2 |pg_ref16 - pg64| + 1e-4
   gradients  ||g - g64|| / ||g64||   <= 2 (same for ref16) + 1e-3   (all parameters, vision tower too)
@@ -84,7 +85,10 @@ def _data(model, images=True, seed=21):
         lp0 = lp0.float()
         del m64, logits
     g = torch.Generator(device=DEV).manual_seed(seed)
-    b["old_log_probs"] = lp0 + 0.1 * torch.randn(B, R, device=DEV, generator=g)
+    # old = lp0 + {-0.5, 0, +0.5}: ratios 1 (unclipped) or e^{+-0.5} (clipped), none within bf16
+    # noise of the 1 +- 0.2 clip boundary, so both computations take the same clip branch per token
+    # (a token near the boundary flips branch on rounding noise and its gradient jumps)
+    b["old_log_probs"] = lp0 + 0.5 * torch.randint(-1, 2, (B, R), device=DEV, generator=g).float()
     b["ref_log_prob"] = lp0 + 0.1 * torch.randn(B, R, device=DEV, generator=g)
     b["advantages"] = torch.randn(B, R, device=DEV, generator=g) * b["response_mask"]
     data.meta_info.update(temperature=1.0, micro_batch_size=MB, use_dynamic_bsz=False)

@@ -33,11 +33,25 @@ _UNITS = {"B": 1.0, "K": 1e3, "M": 1e6, "G": 1e9, "T": 1e12, "P": 1e15}
 VALID_CONFIG_TYPE = {"llama", "qwen2", "qwen2_vl", "qwen2_5_vl", "qwen3", "qwen2_moe", "qwen3_moe"}
 
 
+# by ISA when the marketing name is missing (ROCm reports "AMD Radeon Graphics" without the
+# amdgpu.ids table): gfx950 = MI350 series, taken as the MI355X of this deployment; gfx942 = MI300X
+_ARCH_FLOPS = (("gfx950", 2.5e15), ("gfx942", 1336e12))
+
+
+def _device_name() -> str:
+    if not torch.cuda.is_available():
+        return ""
+    name = torch.cuda.get_device_name()
+    if not any(key in name for key, _ in _DEVICE_FLOPS):
+        name = f"{name} {getattr(torch.cuda.get_device_properties(0), 'gcnArchName', '')}"
+    return name
+
+
 def get_device_flops(unit: str = "T", device_name: str | None = None) -> float:
     """Promised dense bf16 FLOP/s of this device in ``unit`` (float('inf') when unknown)."""
     if device_name is None:
-        device_name = torch.cuda.get_device_name() if torch.cuda.is_available() else ""
-    for key, flops in _DEVICE_FLOPS:
+        device_name = _device_name()
+    for key, flops in _DEVICE_FLOPS + _ARCH_FLOPS:
         if key in device_name:
             return flops / _UNITS[unit]
     return float("inf")

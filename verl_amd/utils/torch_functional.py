@@ -218,8 +218,10 @@ def build_lr_scheduler(optimizer, optim_config, role: str = "actor", rank: int =
     warmup_style = optim_config.get("warmup_style", "constant")
     if num_warmup_steps < 0:
         num_warmup_steps = int(optim_config.get("lr_warmup_steps_ratio", 0.0) * total_steps)
-    if rank == 0:
-        print(f"Total steps: {total_steps}, num_warmup_steps: {num_warmup_steps}")
+    if rank == 0:  # the reference prints this; stderr keeps a driver's JSON stdout clean
+        import sys
+
+        print(f"Total steps: {total_steps}, num_warmup_steps: {num_warmup_steps}", file=sys.stderr)
     if warmup_style == "constant":
         return get_constant_schedule_with_warmup(optimizer=optimizer, num_warmup_steps=num_warmup_steps)
     if warmup_style == "cosine":
