@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define VA_ABI_VERSION 2
+#define VA_ABI_VERSION 3
 
 /* error codes */
 #define VA_OK 0
@@ -426,21 +426,6 @@ int va_flash_attn_bwd(const void *q, const void *k, const void *v, const void *o
                       const int32_t *cu_seqlens, const int32_t *q_blocks, int64_t n_q_blocks, const int32_t *k_blocks,
                       int64_t n_k_blocks, int64_t T, int64_t Hq, int64_t Hk, int64_t head_dim, int64_t max_len,
                       float scale, float *delta, float *partial, void *dq, void *dk, void *dv, void *stream);
-
-/* ---------------------------------------------------------------------------------------
- * Weight gradient of a linear layer, dW[M, N] = dY[T, M]^T X[T, N] (bf16 in, fp32 accumulate,
- * bf16 out), the weight half of torch's linear backward that the actor's merged q|k|v, o,
- * gate|up and down projections issue (dp_actor.py:465-470 loss.backward through the model).
- * dY / X row-major with leading dimensions ldy / ldx (multiples of 8); M, N multiples of 128.
- * splits > 1 cuts the tokens into that many slices whose fp32 partial tiles go to `workspace`
- * (va_wgrad_workspace_bytes) and are summed in slice order (deterministic) before the rounding.
- * EXPERIMENTAL, not on the product path: the actor's weight gradients run in hipBLASLt
- * (kernels.weight_grad); this kernel (0.61-0.72 PF/s) stays exported and parity-tested for the
- * GEMM work DESIGN.md §7 lists, and is selected by nothing.
- * ------------------------------------------------------------------------------------ */
-int64_t va_wgrad_workspace_bytes(int64_t M, int64_t N, int splits);
-int va_wgrad_bf16(const void *dy, int64_t ldy, const void *x, int64_t ldx, int64_t T, int64_t M, int64_t N,
-                  int splits, float *workspace, void *out, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Host-side (no GPU) sequence-length balancing. Replaces verl/utils/seqlen_balancing.py:26-127

@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_abi_version_and_workspace_queries(lib):
-    assert lib.va_abi_version() == 2
+    assert lib.va_abi_version() == 3
     assert lib.va_ppo_loss_workspace_bytes(10) == 8 * (2 * 10 * 8 + 8)
     assert lib.va_agg_workspace_bytes(10) == 8 * (2 * 10 * 8 + 8)
     assert lib.va_gae_workspace_bytes(7) == 8 * (6 * 7 + 8)
@@ -100,17 +100,13 @@ def test_header_constants_match_the_python_mirror():
         assert key in mirrored
 
 
-def test_tuning_keys_and_wgrad_validation_without_device(lib):
+def test_tuning_keys_without_device(lib):
     for key in (L.VA_TUNE_GAE_VARIANT, L.VA_TUNE_BWD_FLAT, L.VA_TUNE_SWIGLU_STREAM):
         assert lib.va_set_tuning(key, 0) == 0
     assert lib.va_set_tuning(L.VA_TUNE_GAE_VARIANT, 0) == 0
     assert lib.va_set_tuning(L.VA_TUNE_BWD_FLAT, -1) == 0
     assert lib.va_set_tuning(L.VA_TUNE_SWIGLU_STREAM, -1) == 0
     assert lib.va_set_tuning(99, 1) == -1
-    assert lib.va_wgrad_workspace_bytes(256, 128, 4) == 4 * 4 * 256 * 128
-    assert lib.va_wgrad_workspace_bytes(256, 128, 1) == 0
-    rc = lib.va_wgrad_bf16(None, 100, None, 128, 64, 100, 128, 1, None, None, None)
-    assert rc == -1 and b"multiples of 128" in lib.va_last_error()
 
 
 def test_transpose_validation_without_device(lib):

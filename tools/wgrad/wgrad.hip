@@ -1,7 +1,8 @@
 // Weight-gradient GEMM of the actor's linear layers on MI355X: dW[M, N] = dY[T, M]^T X[T, N]
 // (M = out_features, N = in_features, K = T tokens; bf16 in, fp32 accumulate, bf16 out).
-// EXPERIMENTAL, not on the product path (selected by nothing; the actor's weight gradients run in
-// hipBLASLt). Not a §8 row: written to replace the hipBLASLt calls of torch's linear backward for
+// EXPERIMENTAL, moved out of the product library (round 3): not built by verl_amd/build.py, not in
+// the C-ABI; the actor's weight gradients run in hipBLASLt. Kept as the starting point DESIGN.md §7
+// names (a 256-row tile with 128 x 64 wave tiles and LDS-DMA staging). Not a §8 row: written to replace the hipBLASLt calls of torch's linear backward for
 // this shape class (huge K, small output), which run at 0.43-0.89 PF/s there
 // (profiles/r01/wgrad_layout_T151552.log); at 0.61-0.72 PF/s it does not yet.
 //

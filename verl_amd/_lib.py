@@ -84,8 +84,6 @@ _SIGNATURES: dict[str, tuple] = {
     "va_apply_kl_penalty": (c_int, [_P, _P, _P, _P, c_int, c_int64, c_int64, c_int, c_float, _P, _P, _P]),
     "va_accumulate_grads": (c_int, [c_int, _P, _P, c_int, _P, c_float, _P]),
     "va_rmsnorm_workspace_bytes": (c_int64, [c_int64, c_int64]),
-    "va_wgrad_workspace_bytes": (c_int64, [c_int64, c_int64, c_int]),
-    "va_wgrad_bf16": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int64, c_int64, c_int, _P, _P, _P]),
     "va_rmsnorm_fwd": (c_int, [_P, _P, _P, c_int, c_int64, c_int64, c_float, _P, _P, _P, _P]),
     "va_rmsnorm_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, _P, _P, _P, _P]),
     "va_swiglu_fwd": (c_int, [_P, c_int64, c_int64, c_int, c_int64, c_int64, _P, _P]),
@@ -139,8 +137,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.va_abi_version() != 2:
-        raise NativeLibraryError(f"ABI version mismatch: {lib.va_abi_version()} != 2")
+    if lib.va_abi_version() != 3:
+        raise NativeLibraryError(f"ABI version mismatch: {lib.va_abi_version()} != 3")
     _lib = lib
     return lib
 

@@ -688,25 +688,6 @@ def wgrad_splits(T: int, n_out: int, n_in: int) -> int:
     return s
 
 
-def wgrad_gemm(dy2, x2, splits: int = 1):
-    """EXPERIMENTAL (selected by nothing; weight_grad below uses hipBLASLt): dW = dY^T X by the
-    gfx950 weight-gradient kernel (wgrad.hip): bf16 [T, M] x [T, N] -> bf16 [M, N], fp32
-    accumulation, split-K partials summed in slice order."""
-    _require_device(dy2, x2)
-    T, M = dy2.shape
-    N = x2.shape[1]
-    if dy2.dtype != torch.bfloat16 or x2.dtype != torch.bfloat16 or dy2.stride(1) != 1 or x2.stride(1) != 1:
-        raise ValueError("wgrad_gemm: bf16 operands with unit column stride required")
-    out = torch.empty(M, N, dtype=torch.bfloat16, device=dy2.device)
-    ws = None
-    if splits > 1:
-        nb = L.load().va_wgrad_workspace_bytes(M, N, splits)
-        ws = torch.empty(nb // 4, dtype=torch.float32, device=dy2.device)
-    L.call("va_wgrad_bf16", _p(dy2), dy2.stride(0), _p(x2), x2.stride(0), T, M, N, splits, _p(ws), _p(out),
-           _stream(dy2))
-    return out
-
-
 WGRAD_SWAP_MIN_OUT = 65536  # the lm_head (V = 151,936 outputs)
 
 

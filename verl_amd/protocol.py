@@ -13,6 +13,7 @@ from __future__ import annotations
 import copy
 import io
 import logging
+import pathlib
 import pickle
 from collections.abc import Iterator
 from dataclasses import dataclass, field
@@ -25,22 +26,23 @@ __all__ = ["DataProto", "DataProtoItem", "TensorBatch", "union_tensor_dict", "pa
            "unpad_dataproto", "DataProtoConfig", "collate_fn"]
 
 
-class _DataProtoConfigMeta(type):
-    _config: dict = {}
+class _TypedSwitches(type):
+    """Class-level boolean switches: ``DataProtoConfig.auto_padding = True`` is type-checked on
+    assignment (the reference's metaclass property, protocol.py:33-45; same message)."""
+
+    def __setattr__(cls, name, value):
+        if name in cls._switches and not isinstance(value, bool):
+            raise AssertionError(f"enabled must be a boolean, got {value} as {type(value)}")
+        super().__setattr__(name, value)
+
+
+class DataProtoConfig(metaclass=_TypedSwitches):
+    """Global switch for auto-padding in chunk() (protocol.py:47-63); a batch can also opt in
+    through ``meta_info[auto_padding_key]``."""
+
+    _switches = ("auto_padding",)
+    auto_padding = False
     auto_padding_key = "_verl_auto_padding"
-
-    @property
-    def auto_padding(cls):
-        return cls._config.get(cls.auto_padding_key, False)
-
-    @auto_padding.setter
-    def auto_padding(cls, enabled: bool):
-        assert isinstance(enabled, bool), f"enabled must be a boolean, got {enabled} as {type(enabled)}"
-        cls._config[cls.auto_padding_key] = enabled
-
-
-class DataProtoConfig(metaclass=_DataProtoConfigMeta):
-    """Global switch for auto-padding in chunk() (protocol.py:47-63)."""
 
 
 class TensorBatch(dict):
@@ -104,6 +106,12 @@ class TensorBatch(dict):
         n = len(next(iter(parts.values()))) if parts else 0
         return [TensorBatch({k: p[i] for k, p in parts.items()}) for i in range(n)]
 
+    def update_from(self, tensors: dict) -> "TensorBatch":
+        """Insert several tensors (batch size checked per key), keeping insertion order."""
+        for k, v in tensors.items():
+            self[k] = v
+        return self
+
     def clone(self) -> "TensorBatch":
         return TensorBatch({k: v.clone() for k, v in self.items()}, batch_size=self.batch_size)
 
@@ -114,6 +122,15 @@ class TensorBatch(dict):
     def __repr__(self):
         body = ", ".join(f"{k}: {tuple(v.shape)} {v.dtype}" for k, v in self.items())
         return f"TensorBatch(batch_size={tuple(self.batch_size)}, {{{body}}})"
+
+
+def _key_list(keys):
+    """None, one key or a list of keys -> None or a list (rename's argument forms)."""
+    if keys is None or isinstance(keys, list):
+        return keys
+    if isinstance(keys, str):
+        return [keys]
+    raise TypeError(f"keys must be a list or a string, but got {type(keys)}")
 
 
 def _index_len(item, n):
@@ -128,17 +145,16 @@ def _cat_batches(batches: list[TensorBatch]) -> TensorBatch:
 
 
 def union_tensor_dict(tensor_dict1: TensorBatch, tensor_dict2: TensorBatch) -> TensorBatch:
-    """protocol.py:105-118: merge; conflicting keys must hold equal tensors."""
-    assert tensor_dict1.batch_size == tensor_dict2.batch_size, (
-        f"Two tensor dict must have identical batch size. Got {tensor_dict1.batch_size} and {tensor_dict2.batch_size}"
-    )
-    for key in tensor_dict2.keys():
-        if key not in tensor_dict1.keys():
-            tensor_dict1[key] = tensor_dict2[key]
-        else:
-            assert tensor_dict1[key].equal(tensor_dict2[key]), (
-                f"{key} in tensor_dict1 and tensor_dict2 are not the same object"
-            )
+    """protocol.py:105-118: add ``tensor_dict2``'s keys to ``tensor_dict1`` in place; a key held by
+    both must hold equal tensors (AssertionError texts as the reference)."""
+    if tensor_dict1.batch_size != tensor_dict2.batch_size:
+        raise AssertionError(f"Two tensor dict must have identical batch size. Got {tensor_dict1.batch_size} "
+                             f"and {tensor_dict2.batch_size}")
+    shared = [k for k in tensor_dict2 if k in tensor_dict1]
+    differing = next((k for k in shared if not tensor_dict1[k].equal(tensor_dict2[k])), None)
+    if differing is not None:
+        raise AssertionError(f"{differing} in tensor_dict1 and tensor_dict2 are not the same object")
+    tensor_dict1.update_from({k: v for k, v in tensor_dict2.items() if k not in tensor_dict1})
     return tensor_dict1
 
 
@@ -153,32 +169,31 @@ def _arrays_equal(a: np.ndarray, b: np.ndarray) -> bool:
 
 
 def union_numpy_dict(d1: dict, d2: dict) -> dict:
-    """protocol.py:121-132."""
-    for key, val in d2.items():
-        if key in d1:
-            assert isinstance(val, np.ndarray) and isinstance(d1[key], np.ndarray)
-            assert _arrays_equal(val, d1[key]), f"{key} in tensor_dict1 and tensor_dict2 are not the same object"
-        d1[key] = val
+    """protocol.py:121-132: merge object arrays into ``d1``; shared keys must hold equal arrays
+    (NaN == NaN for this purpose)."""
+    for key in d1.keys() & d2.keys():
+        a, b = d1[key], d2[key]
+        if not (isinstance(a, np.ndarray) and isinstance(b, np.ndarray)) or not _arrays_equal(b, a):
+            raise AssertionError(f"{key} in tensor_dict1 and tensor_dict2 are not the same object")
+    d1.update(d2)
     return d1
 
 
 def union_two_dict(dict1: dict, dict2: dict) -> dict:
-    for key, val in dict2.items():
-        if key in dict1:
-            assert dict1[key] == val, f"{key} in meta_dict1 and meta_dict2 are not the same object"
-        dict1[key] = val
+    """meta_info merge: shared keys must be equal."""
+    clash = next((k for k in dict2 if k in dict1 and dict1[k] != dict2[k]), None)
+    if clash is not None:
+        raise AssertionError(f"{clash} in meta_dict1 and meta_dict2 are not the same object")
+    dict1.update(dict2)
     return dict1
 
 
 def list_of_dict_to_dict_of_list(list_of_dict: list[dict]) -> dict:
-    if not list_of_dict:
-        return {}
-    out = {k: [] for k in list_of_dict[0]}
-    for d in list_of_dict:
-        for k, v in d.items():
-            assert k in out
-            out[k].append(v)
-    return out
+    """[{k: v_i}] -> {k: [v_i]}; every dict must carry only the first dict's keys."""
+    keys = list(list_of_dict[0]) if list_of_dict else []
+    if any(set(d) - set(keys) for d in list_of_dict):
+        raise AssertionError("list_of_dict entries carry keys the first entry does not have")
+    return {k: [d[k] for d in list_of_dict if k in d] for k in keys}
 
 
 @dataclass
@@ -241,14 +256,13 @@ class DataProto:
         self.meta_info = meta_info
 
     def save_to_disk(self, filepath):
-        with open(filepath, "wb") as f:
-            pickle.dump(self, f)
+        """Writes __getstate__'s form (tensors via torch.save, numpy arrays, meta_info)."""
+        pathlib.Path(filepath).write_bytes(pickle.dumps(self))
 
     @staticmethod
     def load_from_disk(filepath) -> "DataProto":
-        """Loads a file written by save_to_disk of THIS package (it unpickles: trusted files only)."""
-        with open(filepath, "rb") as f:
-            return pickle.load(f)
+        """Reads a file written by save_to_disk of THIS package (it unpickles: trusted files only)."""
+        return pickle.loads(pathlib.Path(filepath).read_bytes())
 
     def print_size(self, prefix=""):
         t = sum(v.element_size() * v.numel() for v in self.batch.values()) if self.batch is not None else 0
@@ -272,15 +286,13 @@ class DataProto:
     # ------------------------------------------------------------------ construction
     @classmethod
     def from_single_dict(cls, data: dict, meta_info=None, auto_padding=False):
-        tensors, non_tensors = {}, {}
-        for key, val in data.items():
-            if isinstance(val, torch.Tensor):
-                tensors[key] = val
-            elif isinstance(val, np.ndarray):
-                non_tensors[key] = val
-            else:
-                raise ValueError(f"Unsupported type in data {type(val)}")
-        return cls.from_dict(tensors=tensors, non_tensors=non_tensors, meta_info=meta_info, auto_padding=auto_padding)
+        """Tensors go to ``batch``, numpy arrays to ``non_tensor_batch`` (protocol.py:255-268)."""
+        odd = next((v for v in data.values() if not isinstance(v, torch.Tensor | np.ndarray)), None)
+        if odd is not None:
+            raise ValueError(f"Unsupported type in data {type(odd)}")
+        return cls.from_dict(tensors={k: v for k, v in data.items() if isinstance(v, torch.Tensor)},
+                             non_tensors={k: v for k, v in data.items() if isinstance(v, np.ndarray)},
+                             meta_info=meta_info, auto_padding=auto_padding)
 
     @classmethod
     def from_dict(cls, tensors=None, non_tensors=None, meta_info=None, num_batch_dims=1, auto_padding=False):
@@ -291,19 +303,15 @@ class DataProto:
         meta_info = meta_info if meta_info is not None else {}
         non_tensors = non_tensors if non_tensors is not None else {}
         assert isinstance(non_tensors, dict)
-        batch_size, pivot = None, None
-        for key, t in tensors.items():
-            if batch_size is None:
-                batch_size, pivot = t.shape[:num_batch_dims], key
-            else:
-                assert batch_size == t.shape[:num_batch_dims], (
-                    f"Not all the tensor in tensors have the same batch size with batch_dims={num_batch_dims}. "
-                    f"Got {pivot} has {batch_size}, {key} has {t.shape[:num_batch_dims]}"
-                )
-        for key, val in non_tensors.items():
-            if not isinstance(val, np.ndarray):
-                non_tensors[key] = np.array(val, dtype=object)
-        batch = TensorBatch(tensors, batch_size=batch_size) if tensors else None
+        lead = {k: t.shape[:num_batch_dims] for k, t in tensors.items()}
+        pivot = next(iter(lead), None)
+        odd = next((k for k, sz in lead.items() if sz != lead[pivot]), None)
+        if odd is not None:
+            raise AssertionError(f"Not all the tensor in tensors have the same batch size with batch_dims="
+                                 f"{num_batch_dims}. Got {pivot} has {lead[pivot]}, {odd} has {lead[odd]}")
+        non_tensors.update({k: np.array(v, dtype=object) for k, v in non_tensors.items()
+                            if not isinstance(v, np.ndarray)})
+        batch = TensorBatch(tensors, batch_size=lead[pivot]) if tensors else None
         if auto_padding:
             meta_info[DataProtoConfig.auto_padding_key] = True
         return cls(batch=batch, non_tensor_batch=non_tensors, meta_info=meta_info)
@@ -356,35 +364,23 @@ class DataProto:
         return type(self)(batch=batch, non_tensor_batch=non_tensor, meta_info=self.meta_info)
 
     def pop(self, batch_keys=None, non_tensor_batch_keys=None, meta_info_keys=None) -> "DataProto":
-        tensors = {}
-        for key in batch_keys or []:
-            assert key in self.batch.keys()
-            tensors[key] = self.batch.pop(key)
-        non_tensors = {}
-        for key in non_tensor_batch_keys or []:
-            assert key in self.non_tensor_batch.keys()
-            non_tensors[key] = self.non_tensor_batch.pop(key)
-        meta = {}
-        for key in meta_info_keys or []:
-            assert key in self.meta_info.keys()
-            meta[key] = self.meta_info.pop(key)
-        return DataProto.from_dict(tensors=tensors, non_tensors=non_tensors, meta_info=meta)
+        """Remove the named keys from this batch and return them as a new DataProto."""
+        def take(store, keys):
+            missing = [k for k in keys or [] if k not in store]
+            if missing:
+                raise AssertionError(f"keys {missing} not present")
+            return {k: store.pop(k) for k in keys or []}
+
+        return DataProto.from_dict(tensors=take(self.batch, batch_keys),
+                                   non_tensors=take(self.non_tensor_batch, non_tensor_batch_keys),
+                                   meta_info=take(self.meta_info, meta_info_keys))
 
     def rename(self, old_keys=None, new_keys=None) -> "DataProto":
-        def norm(keys):
-            if keys is None:
-                return keys
-            if isinstance(keys, str):
-                return [keys]
-            if isinstance(keys, list):
-                return keys
-            raise TypeError(f"keys must be a list or a string, but got {type(keys)}")
-
-        old_keys, new_keys = norm(old_keys), norm(new_keys)
+        """Rename batch keys in place (protocol.py:420-445; same TypeError / ValueError texts)."""
+        old_keys, new_keys = _key_list(old_keys), _key_list(new_keys)
         if len(new_keys) != len(old_keys):
             raise ValueError(
-                f"new_keys and old_keys must have the same length, but got {len(new_keys)} and {len(old_keys)}"
-            )
+                f"new_keys and old_keys must have the same length, but got {len(new_keys)} and {len(old_keys)}")
         self.batch.rename_key_(tuple(old_keys), tuple(new_keys))
         return self
 
@@ -481,19 +477,15 @@ class DataProto:
         return type(self)(batch=batch, non_tensor_batch=non_tensor, meta_info=self.meta_info)
 
     def sample_level_repeat(self, repeat_times) -> "DataProto":
-        """protocol.py:855-901 — per-sample repeat counts."""
-        if isinstance(repeat_times, tuple):
-            repeat_times = list(repeat_times)
-        elif isinstance(repeat_times, torch.Tensor):
-            assert repeat_times.dim() == 1
+        """protocol.py:855-901 — per-sample repeat counts (list / tuple / 1-D tensor or array)."""
+        if isinstance(repeat_times, torch.Tensor | np.ndarray):
+            if repeat_times.ndim != 1:
+                raise AssertionError(f"repeat_times must be 1-D, got {repeat_times.ndim} dims")
             repeat_times = repeat_times.tolist()
-        elif isinstance(repeat_times, np.ndarray):
-            assert repeat_times.ndim == 1
-            repeat_times = repeat_times.tolist()
-        else:
-            assert isinstance(repeat_times, list), (
-                f"repeat_times type must be in [list, torch.Tensor, np.ndarray, tuple], got {type(repeat_times)}"
-            )
+        elif not isinstance(repeat_times, list | tuple):
+            raise AssertionError(
+                f"repeat_times type must be in [list, torch.Tensor, np.ndarray, tuple], got {type(repeat_times)}")
+        repeat_times = [int(r) for r in repeat_times]
         reps = torch.tensor(repeat_times)
         batch = None
         if self.batch is not None:

@@ -3,9 +3,13 @@
 Registries, enum, KL controllers, function names / signatures / defaults and error texts follow
 the reference (core_algos.py:33-1069). The hot-path functions run as gfx950 kernels:
 
-  compute_gae_advantage_return     -> va_gae_advantage_return (chunked LDS scan + whiten)
-  compute_grpo_outcome_advantage   -> va_outcome_advantage (one workgroup per prompt group)
-  compute_rloo_outcome_advantage   -> va_outcome_advantage (RLOO epilogue)
+  compute_gae_advantage_return     -> va_gae_scan (quad-streaming register scan: one wave per row,
+                                      16-B loads, wave-level affine-map scan) + one fused
+                                      statistics / whitening launch
+  compute_grpo_outcome_advantage   -> va_row_scores -> va_group_coef -> va_broadcast_rows (three
+                                      phases: per-row reward sums, per-group fp64 mean / unbiased
+                                      std, broadcast a(b) x mask over [B, R])
+  compute_rloo_outcome_advantage   -> the same three phases with the RLOO epilogue
   compute_reinforce_plus_plus_baseline_outcome_advantage -> mean-only + whiten kernels
   compute_policy_loss / agg_loss / kl_penalty / compute_entropy_loss -> fused loss kernels
 
