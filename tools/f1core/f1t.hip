@@ -63,6 +63,56 @@ __device__ __forceinline__ void merge_st(St &a, float om, float os, float ot) {
   a.m = nm;
 }
 
+// Fold one finished 256 x 256 tile into the lane's per-token online state. Rounding to bf16 is
+// monotonic, so the tile max of the rounded logits is the rounded max of the raw accumulators: one
+// max pass over acc (v_max3), then ONE pass of round -> exp2 -> sums. TAIL: the last vocab tile,
+// whose rows past V are -inf (weight 0; kept out of the x-weighted sum, 0 * -inf being NaN).
+template <bool TAIL>
+__device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[8][4], int v0, const int (&lab)[4], float (&m)[4],
+                                              float (&s)[4], float (&t)[4], float (&ll)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float rm = acc[0][j][0];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rm = fmaxf(rm, acc[i][j][e]);
+    const float lm = __uint_as_float(pack2_bf16(rm, 0.f) << 16);
+    const int d = lab[j] - v0;  // label at (i, e) = (d >> 4, d & 3) when d in [0, 128), d & 12 == 0
+    if (d >= 0 && d < 128 && (d & 12) == 0) {
+      const int uu = (d >> 4) * 4 + (d & 3);
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v = (i * 4 + e) == uu ? acc[i][j][e] : v;
+      ll[j] = __uint_as_float(pack2_bf16(v, 0.f) << 16);
+    }
+    const float nm = fmaxf(m[j], lm);
+    const float nb = base_of(nm);
+    const float alpha = __builtin_amdgcn_exp2f(base_of(m[j]) - nb);
+    float ss = 0.f, tt = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const uint32_t p = pack2_bf16(acc[i][j][e], acc[i][j][e + 1]);
+        float x0 = __uint_as_float(p << 16), x1 = __uint_as_float(p & 0xffff0000u);
+        const float e0 = __builtin_amdgcn_exp2f(fmaf(x0, kLog2eF, -nb));
+        const float e1 = __builtin_amdgcn_exp2f(fmaf(x1, kLog2eF, -nb));
+        ss += e0 + e1;
+        if (TAIL) {
+          x0 = x0 == -INFINITY ? 0.f : x0;
+          x1 = x1 == -INFINITY ? 0.f : x1;
+        }
+        tt = fmaf(e0, x0, fmaf(e1, x1, tt));
+      }
+    s[j] = fmaf(s[j], alpha, ss);
+    t[j] = fmaf(t[j], alpha, tt);
+    m[j] = nm;
+  }
+}
+
 // EPI 0: core only (a cheap checksum keeps the MFMAs live); 1: full online-softmax epilogue
 template <int EPI, bool REMAP>
 __global__ __launch_bounds__(NT, 1) void lp_t_kernel(const uint16_t *__restrict__ hid, int64_t ldh,
@@ -145,8 +195,6 @@ __global__ __launch_bounds__(NT, 1) void lp_t_kernel(const uint16_t *__restrict_
           for (int j = 0; j < 4; ++j) chk += acc[i][j][0] + acc[i][j][3];
       } else {
         // acc[i][j][e] = logit of vocab v0 + i*16 + e (v0 below) for token j of this lane.
-        // Rounding to bf16 is monotonic, so the tile max of the rounded logits is the rounded max
-        // of the raw accumulators: one max pass over acc, then ONE pass of round -> exp -> sums.
         const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;
         if (vt * TB + TB > V) {  // uniform: only the last vocab tile has rows past V
 #pragma unroll
@@ -156,45 +204,9 @@ __global__ __launch_bounds__(NT, 1) void lp_t_kernel(const uint16_t *__restrict_
               if (v0 + i * 16 + e >= V)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc[i][j][e] = -INFINITY;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float rm = acc[0][j][0];
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) rm = fmaxf(rm, acc[i][j][e]);
-          const float lm = __uint_as_float(pack2_bf16(rm, 0.f) << 16);
-          const int d = lab[j] - v0;  // label at (i, e) = (d >> 4, d & 3) when d in [0, 128), d & 12 == 0
-          if (d >= 0 && d < 128 && (d & 12) == 0) {
-            const int uu = (d >> 4) * 4 + (d & 3);
-            float v = 0.f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v = (i * 4 + e) == uu ? acc[i][j][e] : v;
-            ll[j] = __uint_as_float(pack2_bf16(v, 0.f) << 16);
-          }
-          const float nm = fmaxf(m[j], lm);
-          const float nb = base_of(nm);
-          const float alpha = __builtin_amdgcn_exp2f(base_of(m[j]) - nb);
-          float ss = 0.f, tt = 0.f;
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int e = 0; e < 4; e += 2) {
-              const uint32_t p = pack2_bf16(acc[i][j][e], acc[i][j][e + 1]);
-              const float x0 = __uint_as_float(p << 16), x1 = __uint_as_float(p & 0xffff0000u);
-              const float e0 = __builtin_amdgcn_exp2f(fmaf(x0, kLog2eF, -nb));
-              const float e1 = __builtin_amdgcn_exp2f(fmaf(x1, kLog2eF, -nb));
-              ss += e0 + e1;
-              // a masked row is -inf with weight 0: its x * e is 0 * -inf = NaN, so keep it out
-              tt = fmaf(e0, x0 == -INFINITY ? 0.f : x0, tt);
-              tt = fmaf(e1, x1 == -INFINITY ? 0.f : x1, tt);
-            }
-          s[j] = fmaf(s[j], alpha, ss);
-          t[j] = fmaf(t[j], alpha, tt);
-          m[j] = nm;
+          tile_epilogue<true>(acc, v0, lab, m, s, t, ll);
+        } else {
+          tile_epilogue<false>(acc, v0, lab, m, s, t, ll);
         }
       }
 #pragma unroll

@@ -149,9 +149,16 @@ def check(rc: int, what: str) -> None:
         raise RuntimeError(f"verl_amd native call {what} failed ({rc}): {msg}")
 
 
+# va_set_tuning values set through call() in this process (key -> value), for host-side
+# heuristics that depend on a kernel choice (e.g. the fused lm_head kernel's vocab split count)
+TUNING: dict = {}
+
+
 def call(name: str, *args) -> None:
     lib = load()
     check(getattr(lib, name)(*args), name)
+    if name == "va_set_tuning":
+        TUNING[int(args[0])] = int(args[1])
 
 
 __all__ = ["load", "call", "check", "header_symbols", "LIB_PATH", "NativeLibraryError", "c_double"]

@@ -233,36 +233,21 @@ __global__ __launch_bounds__(256, 2) void linear_logprob_tiles_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// 256 x 256 variant (VA_TUNE_LINEAR_LOGPROB_TILE = 256): 8 waves (2 x 4, 128 rows x 64 vocab each,
-// 8 x 4 v_mfma_f32_16x16x32_bf16 blocks), both operands staged by LDS-DMA (global_load_lds, 16 B
-// per lane) into two lane-linear buffers whose 16-byte chunk c of row r sits at c ^ ((r >> 1) & 7)
-// (swizzled on the global source address: conflict-free fragment reads), persistent over the
-// workgroup's vocab tiles with the next tile's first K-step staged during the current tile's last
-// (tools/f1core: this core runs the plain GEMM at 1,038 vs 825-865 TF/s for the 128 x 128 one).
-// Per finished tile each 16-lane group reduces its row's 64 logits (4 per lane) to (max, sum exp,
-// sum exp * x); the 4 waves sharing a row leave them in LDS and one thread per row folds them into
-// the row's running state, in fixed order.
+// 256 x 256 TRANSPOSED kernel (VA_TUNE_LINEAR_LOGPROB_TILE = 256, default). The tile is computed as
+// S^T = W_tile . H_tile^T: the vocab index is the MFMA row (registers) and the token the MFMA column
+// (lane & 15), so every lane owns whole tokens and keeps their online (max, sum 2^(xL-B),
+// sum 2^(xL-B) x) state in registers for the whole persistent sweep over its vocab tiles: no
+// per-tile cross-lane reduction, LDS round trip or barrier (the round-2 row-on-lane layout spent
+// ~20 % of the kernel there). The 4 lane groups and the 2 vocab wave-rows are merged once at the end.
+// Core: 8 waves = 2 (vocab halves) x 4 (token quarters), 128 x 64 per wave = 8 x 4
+// v_mfma_f32_16x16x32_bf16 blocks; both operands staged by LDS-DMA (global_load_lds, 16 B per lane)
+// into two lane-linear buffers whose 16-byte chunk c of row r sits at c ^ ((r >> 1) & 7) (swizzled
+// on the global source address: conflict-free fragment reads); the next step's K-chunk is staged
+// during the current one, across vocab tiles. Grid: row blocks x vocab splits as ONE dimension,
+// remapped so that each XCD gets a contiguous run of (row block, split) ids, split fastest: the few
+// row blocks an XCD works on at a time keep their hidden panels in its L2 while the W tiles stream
+// (tools/f1core/f1t.hip; at 131,072 x 896 x 151,936: 30.1 ms core-only vs 32.3 without the remap).
 constexpr int TB = 256, TK = 64, T_THREADS = 512;
-
-// All-reduce over the 16 lanes of a row group with DPP moves (full-rate VALU) instead of
-// ds_bpermute (an LDS round trip each): quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror and
-// row_mirror; every step pairs values commutatively, so all 16 lanes end bitwise equal.
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float red16_max(float v) {
-  v = fmaxf(v, dpp_f<0xB1>(v));
-  v = fmaxf(v, dpp_f<0x4E>(v));
-  v = fmaxf(v, dpp_f<0x141>(v));
-  return fmaxf(v, dpp_f<0x140>(v));
-}
-__device__ __forceinline__ float red16_sum(float v) {
-  v += dpp_f<0xB1>(v);
-  v += dpp_f<0x4E>(v);
-  v += dpp_f<0x141>(v);
-  return v + dpp_f<0x140>(v);
-}
 constexpr int T_TILE = TB * TK;  // bf16 elements of one operand's K-step image
 
 __device__ __forceinline__ int t_img_off(int row, int c) { return row * TK + ((c ^ ((row >> 1) & 7)) << 3); }
@@ -281,36 +266,104 @@ __device__ __forceinline__ void t_stage(const uint16_t *__restrict__ src, int64_
   }
 }
 
+// the logit as the unfused path holds it: bf16(acc) (ROUND), then bf16(x / T) (SCALE: div_ in bf16)
 template <bool SCALE, bool ROUND>
-__global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_tiles256_kernel(
+__device__ __forceinline__ float logit_of(float a, float temperature) {
+  float v = ROUND ? round_bf16(a) : a;
+  if constexpr (SCALE) v = ROUND ? round_bf16(v / temperature) : v / temperature;
+  return v;
+}
+
+// Fold one finished tile into the lane's per-token state. The logit map (bf16 rounding, division by
+// T > 0) is monotonic, so the tile max of the logits is the map of the raw accumulators' max: one
+// max pass over acc, then ONE pass of map -> exp2 -> sums. TAIL: the last vocab tile, whose rows
+// past V are -inf (weight 0, kept out of the x-weighted sum: 0 * -inf is NaN).
+template <bool SCALE, bool ROUND, bool TAIL>
+__device__ __forceinline__ void t_tile_epilogue(const f32x4 (&acc)[8][4], int v0, const int (&lab)[4], float (&m)[4],
+                                                float (&s)[4], float (&t)[4], float (&ll)[4], float temperature) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float rm = acc[0][j][0];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rm = fmaxf(rm, acc[i][j][e]);
+    const float lm = logit_of<SCALE, ROUND>(rm, temperature);
+    const int d = lab[j] - v0;  // the label sits at (i, e) = (d >> 4, d & 3) when d in [0, 128), d & 12 == 0
+    if (d >= 0 && d < 128 && (d & 12) == 0) {
+      const int uu = (d >> 4) * 4 + (d & 3);
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v = (i * 4 + e) == uu ? acc[i][j][e] : v;
+      ll[j] = logit_of<SCALE, ROUND>(v, temperature);
+    }
+    const float nm = fmaxf(m[j], lm);
+    const float nb = base_of(nm);
+    const float alpha = __builtin_amdgcn_exp2f(base_of(m[j]) - nb);
+    float ss = 0.f, tt = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        float x0, x1;
+        if constexpr (ROUND && !SCALE) {  // both roundings in one v_cvt_pk_bf16_f32
+          const uint32_t p = pack2_bf16(acc[i][j][e], acc[i][j][e + 1]);
+          x0 = __uint_as_float(p << 16);
+          x1 = __uint_as_float(p & 0xffff0000u);
+        } else {
+          x0 = logit_of<SCALE, ROUND>(acc[i][j][e], temperature);
+          x1 = logit_of<SCALE, ROUND>(acc[i][j][e + 1], temperature);
+        }
+        const float e0 = __builtin_amdgcn_exp2f(fmaf(x0, kLog2eF, -nb));
+        const float e1 = __builtin_amdgcn_exp2f(fmaf(x1, kLog2eF, -nb));
+        ss += e0 + e1;
+        if constexpr (TAIL) {
+          x0 = x0 == -INFINITY ? 0.f : x0;
+          x1 = x1 == -INFINITY ? 0.f : x1;
+        }
+        tt = fmaf(e0, x0, fmaf(e1, x1, tt));
+      }
+    s[j] = fmaf(s[j], alpha, ss);
+    t[j] = fmaf(t[j], alpha, tt);
+    m[j] = nm;
+  }
+}
+
+template <bool SCALE, bool ROUND, bool REMAP>
+__global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
     const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
-    const int64_t *__restrict__ labels, int64_t N, int K, int64_t V, int tiles_per_split, float temperature,
-    float *__restrict__ part, float *__restrict__ label_logit) {
-  // ONE LDS array (a second __shared__ object can cost a vmcnt(0) per K-step): 2 staging buffers
-  // of (hidden, weight) images, then per-row running state, the 4 waves' tile partials, labels
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE + 2 * (TB * 3 + 4 * TB * 3 + 2 * TB)];
-  float *s_state = reinterpret_cast<float *>(lds + 2 * 2 * T_TILE);  // [TB][3] m, s, t
-  float *s_part = s_state + TB * 3;                                   // [4 wc][TB][3]
-  float *s_lablogit = s_part + 4 * TB * 3;                            // [TB]
-  int *s_label = reinterpret_cast<int *>(s_lablogit + TB);            // [TB]
+    const int64_t *__restrict__ labels, int64_t N, int K, int64_t V, int splits, int tiles_per_split,
+    float temperature, float *__restrict__ part, float *__restrict__ label_logit) {
+  // ONE LDS array (a second __shared__ object can cost a vmcnt(0) per K-step): 2 staging buffers of
+  // (weight, hidden) images; reused for the final merge of the two vocab wave-rows
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
-  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * TB;
-  const int64_t n_vt = (V + TB - 1) / TB;
-  const int64_t vt_begin = static_cast<int64_t>(blockIdx.y) * tiles_per_split;
-  int64_t vt_end = vt_begin + tiles_per_split;
-  if (vt_end > n_vt) vt_end = n_vt;
-  if (tid < TB) {
-    const int64_t r = row0 + tid;
-    const int64_t lab = r < N ? labels[r] : -1;
-    s_label[tid] = (lab >= 0 && lab < V) ? static_cast<int>(lab) : -1;
-    s_lablogit[tid] = 0.f;
-    s_state[tid * 3 + 0] = -INFINITY;
-    s_state[tid * 3 + 1] = 0.f;
-    s_state[tid * 3 + 2] = 0.f;
+  int64_t L = blockIdx.x;
+  if (REMAP) {  // blocks b, b + 8, ... share an XCD: give each XCD a contiguous run of logical ids
+    const int64_t nl = gridDim.x >> 3;
+    L = (L & 7) * nl + (L >> 3);
   }
+  const int64_t rb = L / splits, sp = L % splits;
+  const int64_t row0 = rb * TB;
+  const int64_t n_vt = (V + TB - 1) / TB;
+  const int64_t vt_begin = sp * tiles_per_split;
+  const int64_t vt_end = vt_begin + tiles_per_split < n_vt ? vt_begin + tiles_per_split : n_vt;
   const int nk = K / TK;
   const int64_t nsteps = vt_begin < vt_end ? (vt_end - vt_begin) * nk : 0;
+
+  // this lane's 4 tokens (columns of the transposed tile), their labels and online states
+  int lab[4];
+  float m[4], s[4], t[4], ll[4];  // ll: the label's logit, -inf until this lane meets it
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t r = row0 + wc * 64 + j * 16 + (lane & 15);
+    const int64_t lb = r < N ? labels[r] : -1;
+    lab[j] = (lb >= 0 && lb < V) ? static_cast<int>(lb) : -1;
+    m[j] = -INFINITY, s[j] = 0.f, t[j] = 0.f, ll[j] = -INFINITY;
+  }
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -319,8 +372,8 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_tiles256_kernel(
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (nsteps > 0) {
-    t_stage(hid, row0, N, ldh, 0, lds, wave, lane);
-    t_stage(w, vt_begin * TB, V, ldw, 0, lds + T_TILE, wave, lane);
+    t_stage(w, vt_begin * TB, V, ldw, 0, lds, wave, lane);
+    t_stage(hid, row0, N, ldh, 0, lds + T_TILE, wave, lane);
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
@@ -332,13 +385,13 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_tiles256_kernel(
     const uint16_t *lb = la + T_TILE;
     if (st + 1 < nsteps) {
       uint16_t *na = lds + (buf ^ 1) * 2 * T_TILE;
-      t_stage(hid, row0, N, ldh, static_cast<int>((st + 1) % nk) * TK, na, wave, lane);
-      t_stage(w, (vt_begin + (st + 1) / nk) * TB, V, ldw, static_cast<int>((st + 1) % nk) * TK, na + T_TILE, wave,
-              lane);
+      const int k1 = static_cast<int>((st + 1) % nk) * TK;
+      t_stage(w, (vt_begin + (st + 1) / nk) * TB, V, ldw, k1, na, wave, lane);
+      t_stage(hid, row0, N, ldh, k1, na + T_TILE, wave, lane);
     }
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int c = s * 4 + (lane >> 4);
+    for (int q = 0; q < 2; ++q) {
+      const int c = q * 4 + (lane >> 4);
       bf16x8 fa[8], fb[4];
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -352,53 +405,19 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_tiles256_kernel(
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
     if (kt == nk - 1) {
-      // ---- epilogue of vocab tile vt: lane holds rows wr*128 + i*16 + (lane>>4)*4 + e, columns
-      //      vt*256 + wc*64 + j*16 + (lane&15); the 16 lanes of a group share the row
-      const int col0 = static_cast<int>(vt * TB) + wc * 64 + (lane & 15);  // V < 2^31
+      // acc[i][j][e] = logit of vocab v0 + i * 16 + e for token j of this lane
+      const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;  // V < 2^31
+      if (vt * TB + TB > V) {  // uniform: only the last vocab tile has rows past V
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int lr = wr * 128 + i * 16 + (lane >> 4) * 4 + e;
-          const int lab = s_label[lr];
-          float x[4];
-          float cm = -INFINITY;
+          for (int e = 0; e < 4; ++e)
+            if (v0 + i * 16 + e >= V)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int col = col0 + j * 16;
-            // ROUND: the bf16 logits of the unfused path; else fp32 logits (the reference's fused kernel)
-            float v = ROUND ? round_bf16(acc[i][j][e]) : acc[i][j][e];
-            if constexpr (SCALE) v = ROUND ? round_bf16(v / temperature) : v / temperature;
-            if (col >= static_cast<int>(V)) v = -INFINITY;
-            if (col == lab) s_lablogit[lr] = v;
-            x[j] = v;
-            cm = fmaxf(cm, v);
-          }
-          cm = red16_max(cm);
-          const float nb = base_of(cm);
-          float ss = 0.f, tt = 0.f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float ex = __builtin_amdgcn_exp2f(fmaf(x[j], kLog2eF, -nb));
-            ss += ex;
-            tt = fmaf(ex, x[j] == -INFINITY ? 0.f : x[j], tt);
-          }
-          ss = red16_sum(ss);
-          tt = red16_sum(tt);
-          if ((lane & 15) == 0) {
-            float *pp = s_part + (wc * TB + lr) * 3;
-            pp[0] = cm, pp[1] = ss, pp[2] = tt;
-          }
-        }
-      __syncthreads();
-      if (tid < TB) {  // fold the 4 column slices of the tile into the row's state, wc order
-        RowAcc a{s_state[tid * 3 + 0], s_state[tid * 3 + 1], s_state[tid * 3 + 2]};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float *pp = s_part + (q * TB + tid) * 3;
-          merge_state(a, pp[0], pp[1], pp[2]);
-        }
-        s_state[tid * 3 + 0] = a.m, s_state[tid * 3 + 1] = a.s, s_state[tid * 3 + 2] = a.t;
+              for (int j = 0; j < 4; ++j) acc[i][j][e] = -INFINITY;
+        t_tile_epilogue<SCALE, ROUND, true>(acc, v0, lab, m, s, t, ll, temperature);
+      } else {
+        t_tile_epilogue<SCALE, ROUND, false>(acc, v0, lab, m, s, t, ll, temperature);
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -408,14 +427,44 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_tiles256_kernel(
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
-  if (tid < TB && row0 + tid < N) {
-    const int64_t r = row0 + tid;
-    float *p = part + (static_cast<int64_t>(blockIdx.y) * N + r) * 3;
-    p[0] = s_state[tid * 3 + 0];
-    p[1] = s_state[tid * 3 + 1];
-    p[2] = s_state[tid * 3 + 2];
-    const int lab = s_label[tid];
-    if (lab >= vt_begin * TB && lab < vt_end * TB) label_logit[r] = s_lablogit[tid];
+
+  // merge the 4 lane groups (lanes l, l ^ 16, l ^ 32, l ^ 48 hold the same tokens), then the two
+  // vocab wave-rows through LDS (free now: every DMA was waited for), in fixed order
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    RowAcc a{m[j], s[j], t[j]};
+    float l2 = ll[j];
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      const float om = __shfl_xor(a.m, o, kWave), os = __shfl_xor(a.s, o, kWave), ot = __shfl_xor(a.t, o, kWave);
+      merge_state(a, om, os, ot);
+      l2 = fmaxf(l2, __shfl_xor(l2, o, kWave));  // one lane of the token holds it (or none: -inf)
+    }
+    m[j] = a.m, s[j] = a.s, t[j] = a.t, ll[j] = l2;
+  }
+  float *red = reinterpret_cast<float *>(lds);  // [4 wc][64 tokens][4]: m, s, t, label logit
+  if (wr == 1 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float *p = red + (wc * 64 + j * 16 + lane) * 4;
+      p[0] = m[j], p[1] = s[j], p[2] = t[j], p[3] = ll[j];
+    }
+  }
+  __syncthreads();
+  if (wr == 0 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float *p = red + (wc * 64 + j * 16 + lane) * 4;
+      RowAcc a{m[j], s[j], t[j]};
+      merge_state(a, p[0], p[1], p[2]);
+      const int64_t r = row0 + wc * 64 + j * 16 + lane;
+      if (r < N) {
+        float *o = part + (sp * N + r) * 3;
+        o[0] = a.m, o[1] = a.s, o[2] = a.t;
+        const float lv = fmaxf(ll[j], p[3]);
+        if (lv != -INFINITY) label_logit[r] = lv;  // the split holding the label writes it
+      }
+    }
   }
 }
 
@@ -459,6 +508,18 @@ using namespace va;
 // (the 256 x 256 LDS-DMA kernel above)
 int g_linear_logprob_tile = 256;
 
+template <bool SC, bool RD>
+static void launch_t256(bool remap, dim3 grid, hipStream_t s, const uint16_t *h16, int64_t ldh, const uint16_t *w16,
+                        int64_t ldw, const int64_t *labels, int64_t N, int64_t H, int64_t V, int used, int per,
+                        float temperature, float *part, float *label_logit) {
+  if (remap)
+    hipLaunchKernelGGL((linear_logprob_t256_kernel<SC, RD, true>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16, ldw,
+                       labels, N, static_cast<int>(H), V, used, per, temperature, part, label_logit);
+  else
+    hipLaunchKernelGGL((linear_logprob_t256_kernel<SC, RD, false>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16, ldw,
+                       labels, N, static_cast<int>(H), V, used, per, temperature, part, label_logit);
+}
+
 extern "C" int64_t va_linear_logprob_workspace_bytes(int64_t N, int splits) {
   return static_cast<int64_t>(sizeof(float)) * (static_cast<int64_t>(splits) * N * 3 + N);
 }
@@ -484,19 +545,25 @@ extern "C" int va_linear_logprob_fwd(const void *hidden, int64_t ldh, const void
   float *label_logit = part + static_cast<int64_t>(splits) * N * 3;
   if (g_linear_logprob_tile == 256) {
     const int64_t n_vt = (V + TB - 1) / TB;
-    int per = static_cast<int>((n_vt + splits - 1) / splits);
+    const int per = static_cast<int>((n_vt + splits - 1) / splits);
     const int used = static_cast<int>((n_vt + per - 1) / per);  // <= splits: ranges the workspace holds
-    const dim3 grid(static_cast<unsigned>((N + TB - 1) / TB), static_cast<unsigned>(used));
-    if (temperature == 1.0f)
-      hipLaunchKernelGGL((fp32_logits ? linear_logprob_tiles256_kernel<false, false>
-                                     : linear_logprob_tiles256_kernel<false, true>), grid, dim3(T_THREADS), 0, s,
-                         static_cast<const uint16_t *>(hidden), ldh, static_cast<const uint16_t *>(weight), ldw,
-                         labels, N, static_cast<int>(H), V, per, temperature, part, label_logit);
-    else
-      hipLaunchKernelGGL((fp32_logits ? linear_logprob_tiles256_kernel<true, false>
-                                     : linear_logprob_tiles256_kernel<true, true>), grid, dim3(T_THREADS), 0, s,
-                         static_cast<const uint16_t *>(hidden), ldh, static_cast<const uint16_t *>(weight), ldw,
-                         labels, N, static_cast<int>(H), V, per, temperature, part, label_logit);
+    const int64_t nwg = ((N + TB - 1) / TB) * used;
+    VA_CHECK_ARG(nwg < (int64_t{1} << 31), "linear_logprob: grid too large");
+    const dim3 grid(static_cast<unsigned>(nwg));
+    const bool remap = nwg % 8 == 0;
+    const auto *h16 = static_cast<const uint16_t *>(hidden);
+    const auto *w16 = static_cast<const uint16_t *>(weight);
+    if (temperature == 1.0f) {
+      if (fp32_logits) launch_t256<false, false>(remap, grid, s, h16, ldh, w16, ldw, labels, N, H, V, used, per,
+                                                 temperature, part, label_logit);
+      else launch_t256<false, true>(remap, grid, s, h16, ldh, w16, ldw, labels, N, H, V, used, per, temperature, part,
+                                    label_logit);
+    } else {
+      if (fp32_logits) launch_t256<true, false>(remap, grid, s, h16, ldh, w16, ldw, labels, N, H, V, used, per,
+                                                temperature, part, label_logit);
+      else launch_t256<true, true>(remap, grid, s, h16, ldh, w16, ldw, labels, N, H, V, used, per, temperature, part,
+                                   label_logit);
+    }
     hipLaunchKernelGGL(linear_logprob_merge_kernel, dim3(static_cast<unsigned>((N + 255) / 256)), dim3(256), 0, s,
                        part, label_logit, labels, N, V, used, logp, entropy, lse);
     return check_launch("linear_logprob_fwd");

@@ -151,10 +151,16 @@ def logprob_entropy(logits, labels, temperature: float = 1.0, inplace_backward: 
 
 # =============================================================================== fused lm_head + log-prob
 def _linear_logprob_splits(n_rows: int) -> int:
-    """Vocab ranges per row block: enough workgroups (~4 per CU of 256) without tiny ranges."""
+    """Vocab ranges per row block. The 256-row kernel (default): ~4,096 workgroups (16 per CU, which
+    the XCD remap turns into 32 resident (row block, range) pairs per XCD: 4 hidden panels x 8
+    ranges at 131,072 rows; tools/f1t_bench.py: 4 or 8 ranges 33.9 ms, 16: 34.3); the 128-row
+    kernel: ~1,024 workgroups."""
     env = os.environ.get("VERL_AMD_LINEAR_LOGPROB_SPLITS")
     if env:
         return int(env)
+    if L.TUNING.get(L.VA_TUNE_LINEAR_LOGPROB_TILE, 256) == 256:
+        blocks = max(1, (n_rows + 255) // 256)
+        return int(min(64, max(1, -(-4096 // blocks))))
     blocks = max(1, (n_rows + 127) // 128)
     return int(min(64, max(1, -(-1024 // blocks))))
 
