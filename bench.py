@@ -125,6 +125,8 @@ def parse(argv=None):
                     help="1: ZeRO-style sharded fp32 master / AdamW state over the ranks (reduce-scatter + all-gather)")
     ap.add_argument("--wgrad-stream", type=int, default=0, choices=[0, 1],
                     help="1: backbone weight gradients + fp32 accumulation on a side stream (wgrad_side_stream)")
+    ap.add_argument("--fused-no-grad", type=int, default=1, choices=[0, 1],
+                    help="1: the no-grad old-logp pass runs the fused lm_head + log-prob kernel (f1, fused_logprob_no_grad)")
     ap.add_argument("--no-rmpad", action="store_true")
     ap.add_argument("--no-mixed-precision", action="store_true", help="fp32 weights + autocast instead of bf16/fp32-master")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -355,6 +357,7 @@ def main():
             use_dynamic_bsz=args.dynamic_bsz > 0, ppo_max_token_len_per_gpu=args.dynamic_bsz or 16384,
             pack_pad_multiple=args.pad_multiple,
             logprob_inplace_backward=bool(args.logprob_inplace_bwd),
+            fused_logprob_no_grad=bool(args.fused_no_grad),
             wgrad_side_stream=bool(args.wgrad_stream),
             gemm_tuning_file=None if args.gemm_table in (None, "none") else args.gemm_table,
         ),
@@ -457,30 +460,32 @@ def main():
         log(rank, f"cpu baseline: {cpu['value']} tokens/s on {cpu['cores']} threads")
 
     if rank == 0:
-        roof = None
-        if ksum:
-            name, d = max(ksum.items(), key=lambda kv: kv[1]["time_ms_total"])
-            if "tflops" in d:  # MFMA-bound fused lm_head + log-prob kernel
-                roof = {
-                    "kernel": name, "bound": "mfma", "achieved": round(d["tflops"], 1),
-                    "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(d["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
-                    "algo_flops_per_launch": d["avg_flops"], "avg_launch_us": round(d["avg_us"], 2),
-                    "launches": d["launches"],
-                }
-            else:
-                traffic, src = pmc_traffic(name, d["avg_bytes"], VOCAB)
-                per_row = 2 * 2 * VOCAB + 28 if name.endswith("bwd") else 2 * VOCAB + 20  # bf16 rows
-                ceil, ceil_src = hbm_ceiling(name, round(d["avg_bytes"] / per_row), bool(args.logprob_inplace_bwd))
-                roof = {
-                    "kernel": name, "bound": "hbm", "achieved": round(d["gbps"], 1), "peak": HBM_PEAK_GBPS,
-                    "unit": "GB/s", "frac": round(d["gbps"] / HBM_PEAK_GBPS, 4),
-                    "traffic": round(traffic) if traffic else None, "traffic_source": src,
-                    "measured_stream_ceiling": ceil,
-                    "frac_of_measured_ceiling": round(d["gbps"] / ceil, 4) if ceil else None,
-                    "ceiling_source": ceil_src, "algo_bytes_per_launch": d["avg_bytes"],
-                    "avg_launch_us": round(d["avg_us"], 2), "launches": d["launches"],
-                }
+        roof = roof_f1 = None
+        hbm = {k: v for k, v in ksum.items() if "tflops" not in v}
+        if hbm:
+            # the §8 roofline claim rests on the streaming log-prob kernels: the
+            # dominant HBM-bound one by time
+            name, d = max(hbm.items(), key=lambda kv: kv[1]["time_ms_total"])
+            traffic, src = pmc_traffic(name, d["avg_bytes"], VOCAB)
+            per_row = 2 * 2 * VOCAB + 28 if name.endswith("bwd") else 2 * VOCAB + 20  # bf16 rows
+            ceil, ceil_src = hbm_ceiling(name, round(d["avg_bytes"] / per_row), bool(args.logprob_inplace_bwd))
+            roof = {
+                "kernel": name, "bound": "hbm", "achieved": round(d["gbps"], 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(d["gbps"] / HBM_PEAK_GBPS, 4),
+                "traffic": round(traffic) if traffic else None, "traffic_source": src,
+                "measured_stream_ceiling": ceil,
+                "frac_of_measured_ceiling": round(d["gbps"] / ceil, 4) if ceil else None,
+                "ceiling_source": ceil_src, "algo_bytes_per_launch": d["avg_bytes"],
+                "avg_launch_us": round(d["avg_us"], 2), "launches": d["launches"],
+            }
+        f1 = ksum.get("linear_logprob_fwd")
+        if f1 is not None:  # MFMA-bound fused lm_head + log-prob kernel (f1): 2 N V H flops per launch
+            roof_f1 = {
+                "kernel": "linear_logprob_fwd", "bound": "mfma", "achieved": round(f1["tflops"], 1),
+                "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(f1["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4),
+                "traffic": None, "algo_flops_per_launch": f1["avg_flops"], "avg_launch_us": round(f1["avg_us"], 2),
+                "launches": f1["launches"], "time_ms_total": round(f1["time_ms_total"], 2),
+            }
         line = {
             "metric": "GRPO actor-update tokens/sec (512x1024)",
             "value": round(tok_s, 1),
@@ -520,11 +525,15 @@ def main():
                        f"which with variable response lengths weights tokens differently at micro-batch {micro} "
                        "than at 8 (each micro-batch's mean is over its own token count); ")
                     + ("out-of-place log-prob backward (reference: in place)" if not args.logprob_inplace_bwd
-                       else "in-place log-prob backward as the reference")),
+                       else "in-place log-prob backward as the reference")
+                    + ("; the no-grad old-logp pass runs the fused lm_head + log-prob kernel (the reference's "
+                       "use_fused_kernels option, off by default there; same bf16-rounded logits, tests)"
+                       if args.fused_no_grad else "")),
                 "dynamic_bsz_max_token_len": args.dynamic_bsz or None,
                 "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
                 "pack_pad_multiple": args.pad_multiple,
                 "logprob_inplace_backward": bool(args.logprob_inplace_bwd),
+                "fused_logprob_no_grad": bool(args.fused_no_grad),
                 "zero_sharded_optimizer": bool(args.zero),
                 "wgrad_side_stream": bool(args.wgrad_stream),
                 "hip_env": {"HIP_FORCE_DEV_KERNARG": os.environ.get("HIP_FORCE_DEV_KERNARG")},
@@ -538,6 +547,7 @@ def main():
             "perf_throughput": round(perf_throughput, 1),
             "comm": comm,
             "roofline": roof,
+            "roofline_f1": roof_f1,
             "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in ksum.items()},
             "cpu_baseline": cpu,
