@@ -113,6 +113,413 @@ __device__ __forceinline__ void tile_epilogue(const f32x4 (&acc)[8][4], int v0, 
   }
 }
 
+// One token column j of a finished tile (the per-column body of tile_epilogue), packed-fp32 form:
+// the exp2 argument, the sum and the x-weighted sum of two logits per v_pk_* instruction.
+template <bool TAIL>
+__device__ __forceinline__ void col_epilogue(const f32x4 (&acc)[8][4], int j, int v0, int labj, float &mj, float &sj,
+                                             float &tj, float &llj) {
+  float rm = acc[0][j][0];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rm = fmaxf(rm, acc[i][j][e]);
+  const float lm = __uint_as_float(pack2_bf16(rm, 0.f) << 16);
+  const int d = labj - v0;
+  if (d >= 0 && d < 128 && (d & 12) == 0) {
+    const int uu = (d >> 4) * 4 + (d & 3);
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v = (i * 4 + e) == uu ? acc[i][j][e] : v;
+    llj = __uint_as_float(pack2_bf16(v, 0.f) << 16);
+  }
+  const float nm = fmaxf(mj, lm);
+  const float nb = base_of(nm);
+  const float alpha = __builtin_amdgcn_exp2f(base_of(mj) - nb);
+  const f32x2 l2e = {kLog2eF, kLog2eF}, nnb = {-nb, -nb};
+  f32x2 ss = {0.f, 0.f}, tt = {0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; e += 2) {
+      const uint32_t p = pack2_bf16(acc[i][j][e], acc[i][j][e + 1]);
+      f32x2 x = {__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+      const f32x2 arg = x * l2e + nnb;
+      const f32x2 ex = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+      ss += ex;
+      if (TAIL) {
+        x.x = x.x == -INFINITY ? 0.f : x.x;
+        x.y = x.y == -INFINITY ? 0.f : x.y;
+      }
+      tt = ex * x + tt;
+    }
+  sj = fmaf(sj, alpha, ss.x + ss.y);
+  tj = fmaf(tj, alpha, tt.x + tt.y);
+  mj = nm;
+}
+
+// v6/v7: T1 with the tile epilogue DEFERRED into the next tile's first K-step, column by column:
+// the epilogue of token column j (VALU + exp) is issued right before that K-step's 16 MFMAs of
+// column j (which start the new tile from zero), so the compiler can overlap column j+1's VALU
+// work with column j's MFMAs in the matrix pipe, with no extra registers. The last tile's epilogue
+// (the only one that can be the vocab tail) runs after the loop.
+template <bool PK>
+__global__ __launch_bounds__(NT, 1) void lp_td_kernel(const uint16_t *__restrict__ hid, int64_t ldh,
+                                                      const uint16_t *__restrict__ w, int64_t ldw,
+                                                      const int64_t *__restrict__ labels, int64_t N, int K, int64_t V,
+                                                      int splits, int tiles_per_split, float *__restrict__ part,
+                                                      float *__restrict__ label_logit) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  int64_t L = blockIdx.x;
+  {
+    const int64_t nl = gridDim.x >> 3;
+    L = (L & 7) * nl + (L >> 3);
+  }
+  const int64_t rb = L / splits, sp = L % splits;
+  const int64_t row0 = rb * TB;
+  const int64_t n_vt = (V + TB - 1) / TB;
+  const int64_t vt_begin = sp * tiles_per_split;
+  const int64_t vt_end = vt_begin + tiles_per_split < n_vt ? vt_begin + tiles_per_split : n_vt;
+  const int nk = K / TK;
+  const int nsteps = vt_begin < vt_end ? static_cast<int>((vt_end - vt_begin) * nk) : 0;
+
+  int lab[4];
+  float m[4], s[4], t[4], ll[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t r = row0 + wc * 64 + j * 16 + (lane & 15);
+    const int64_t lb = r < N ? labels[r] : -1;
+    lab[j] = (lb >= 0 && lb < V) ? static_cast<int>(lb) : -1;
+    m[j] = -INFINITY, s[j] = 0.f, t[j] = 0.f, ll[j] = -INFINITY;
+  }
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nsteps > 0) {
+    stage(w, vt_begin * TB, V, ldw, 0, lds, wave, lane);
+    stage(hid, row0, N, ldh, 0, lds + T_TILE, wave, lane);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  int64_t vt = vt_begin, vt_n = vt_begin;
+  int kt = 0, kt_n = 1;
+  if (kt_n == nk) kt_n = 0, ++vt_n;
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    const uint16_t *la = lds + buf * 2 * T_TILE;
+    const uint16_t *lb = la + T_TILE;
+    if (st + 1 < nsteps) {
+      uint16_t *na = lds + (buf ^ 1) * 2 * T_TILE;
+      stage(w, vt_n * TB, V, ldw, kt_n * TK, na, wave, lane);
+      stage(hid, row0, N, ldh, kt_n * TK, na + T_TILE, wave, lane);
+    }
+    if (kt == 0 && st > 0) {
+      // the previous tile (vt - 1, never the vocab tail: a tile follows it) column by column
+      const int v0 = static_cast<int>((vt - 1) * TB) + wr * 128 + (lane >> 4) * 4;
+      bf16x8 fa[8][2], fb[4][2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = q * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          fa[i][q] = *reinterpret_cast<const bf16x8 *>(la + img_off(wr * 128 + i * 16 + (lane & 15), c));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          fb[j][q] = *reinterpret_cast<const bf16x8 *>(lb + img_off(wc * 64 + j * 16 + (lane & 15), c));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (PK) col_epilogue<false>(acc, j, v0, lab[j], m[j], s[j], t[j], ll[j]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], fb[j][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = q * 4 + (lane >> 4);
+        bf16x8 fa[8], fb[4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          fa[i] = *reinterpret_cast<const bf16x8 *>(la + img_off(wr * 128 + i * 16 + (lane & 15), c));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          fb[j] = *reinterpret_cast<const bf16x8 *>(lb + img_off(wc * 64 + j * 16 + (lane & 15), c));
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    vt = vt_n, kt = kt_n;
+    if (++kt_n == nk) kt_n = 0, ++vt_n;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  if (nsteps > 0) {  // the last tile: possibly the vocab tail
+    const int64_t vl = vt_end - 1;
+    const int v0 = static_cast<int>(vl * TB) + wr * 128 + (lane >> 4) * 4;
+    if (vl * TB + TB > V) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (v0 + i * 16 + e >= V)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j][e] = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) col_epilogue<true>(acc, j, v0, lab[j], m[j], s[j], t[j], ll[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) col_epilogue<false>(acc, j, v0, lab[j], m[j], s[j], t[j], ll[j]);
+    }
+  }
+
+  float *red = reinterpret_cast<float *>(lds);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    St a{m[j], s[j], t[j]};
+    float l2 = ll[j];
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      const float om = __shfl_xor(a.m, o, 64), os = __shfl_xor(a.s, o, 64), ot = __shfl_xor(a.t, o, 64);
+      merge_st(a, om, os, ot);
+      l2 = fmaxf(l2, __shfl_xor(l2, o, 64));
+    }
+    m[j] = a.m, s[j] = a.s, t[j] = a.t, ll[j] = l2;
+  }
+  if (wr == 1 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float *p = red + ((wc * 64) + j * 16 + lane) * 4;
+      p[0] = m[j], p[1] = s[j], p[2] = t[j], p[3] = ll[j];
+    }
+  }
+  __syncthreads();
+  if (wr == 0 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float *p = red + ((wc * 64) + j * 16 + lane) * 4;
+      St a{m[j], s[j], t[j]};
+      merge_st(a, p[0], p[1], p[2]);
+      const int64_t r = row0 + wc * 64 + j * 16 + lane;
+      if (r < N) {
+        float *o = part + (sp * N + r) * 3;
+        o[0] = a.m, o[1] = a.s, o[2] = a.t;
+        const float lv = fmaxf(ll[j], p[3]);
+        if (lv != -INFINITY) label_logit[r] = lv;
+      }
+    }
+  }
+}
+
+// v8: the tile epilogue split in two. At the tile's last K-step only the cheap part runs: the
+// per-token tile max (one max3 pass), the running-max update and the rescale of (s, t), and the
+// label's (row block, element) position. The expensive part -- bf16 rounding, exp2 and the two sums
+// for every logit -- is DEFERRED into the next tile's first K-step, ROW BLOCK by row block: the 16
+// logits of row block i (4 tokens x 4) are folded right before that K-step's 8 MFMAs of row block i
+// restart it from zero, so block i+1's VALU work can overlap block i's MFMAs in the matrix pipe.
+// Registers: both k-substeps of the B fragments (32) + one row block of A fragments (8) at a time.
+__global__ __launch_bounds__(NT, 1) void lp_tr_kernel(const uint16_t *__restrict__ hid, int64_t ldh,
+                                                      const uint16_t *__restrict__ w, int64_t ldw,
+                                                      const int64_t *__restrict__ labels, int64_t N, int K, int64_t V,
+                                                      int splits, int tiles_per_split, float *__restrict__ part,
+                                                      float *__restrict__ label_logit) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  int64_t L = blockIdx.x;
+  {
+    const int64_t nl = gridDim.x >> 3;
+    L = (L & 7) * nl + (L >> 3);
+  }
+  const int64_t rb = L / splits, sp = L % splits;
+  const int64_t row0 = rb * TB;
+  const int64_t n_vt = (V + TB - 1) / TB;
+  const int64_t vt_begin = sp * tiles_per_split;
+  const int64_t vt_end = vt_begin + tiles_per_split < n_vt ? vt_begin + tiles_per_split : n_vt;
+  const int nk = K / TK;
+  const int nsteps = vt_begin < vt_end ? static_cast<int>((vt_end - vt_begin) * nk) : 0;
+
+  int lab[4], lsel[4];  // lsel: (row block * 4 + element) of the label in the pending tile, or -1
+  float m[4], s[4], t[4], ll[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t r = row0 + wc * 64 + j * 16 + (lane & 15);
+    const int64_t lb = r < N ? labels[r] : -1;
+    lab[j] = (lb >= 0 && lb < V) ? static_cast<int>(lb) : -1;
+    m[j] = -INFINITY, s[j] = 0.f, t[j] = 0.f, ll[j] = -INFINITY, lsel[j] = -1;
+  }
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nsteps > 0) {
+    stage(w, vt_begin * TB, V, ldw, 0, lds, wave, lane);
+    stage(hid, row0, N, ldh, 0, lds + T_TILE, wave, lane);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  int64_t vt = vt_begin, vt_n = vt_begin;
+  int kt = 0, kt_n = 1;
+  if (kt_n == nk) kt_n = 0, ++vt_n;
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    const uint16_t *la = lds + buf * 2 * T_TILE;
+    const uint16_t *lb = la + T_TILE;
+    if (st + 1 < nsteps) {
+      uint16_t *na = lds + (buf ^ 1) * 2 * T_TILE;
+      stage(w, vt_n * TB, V, ldw, kt_n * TK, na, wave, lane);
+      stage(hid, row0, N, ldh, kt_n * TK, na + T_TILE, wave, lane);
+    }
+    {
+      // one MFMA order for every K-step: B fragments of both k-substeps, then row block by row
+      // block (A fragments of block i only); at a tile's first K-step the previous tile's deferred
+      // logits of block i are folded first (uniform branch), then block i restarts from zero
+      const bool defer = kt == 0 && st > 0;
+      bf16x8 fb[4][2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          fb[j][q] = *reinterpret_cast<const bf16x8 *>(lb + img_off(wc * 64 + j * 16 + (lane & 15), q * 4 + (lane >> 4)));
+      float nb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nb[j] = base_of(m[j]);
+      f32x2 ss[4], tt[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ss[j] = f32x2{0.f, 0.f}, tt[j] = f32x2{0.f, 0.f};
+      const f32x2 l2e = {kLog2eF, kLog2eF};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8 fa0 = *reinterpret_cast<const bf16x8 *>(la + img_off(wr * 128 + i * 16 + (lane & 15), lane >> 4));
+        const bf16x8 fa1 = *reinterpret_cast<const bf16x8 *>(la + img_off(wr * 128 + i * 16 + (lane & 15), 4 + (lane >> 4)));
+        if (defer) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if ((lsel[j] >> 2) == i) {
+              const int e = lsel[j] & 3;
+              const float v = e == 0 ? acc[i][j][0] : e == 1 ? acc[i][j][1] : e == 2 ? acc[i][j][2] : acc[i][j][3];
+              ll[j] = __uint_as_float(pack2_bf16(v, 0.f) << 16);
+            }
+            const f32x2 nnb = {-nb[j], -nb[j]};
+#pragma unroll
+            for (int e = 0; e < 4; e += 2) {
+              const uint32_t p = pack2_bf16(acc[i][j][e], acc[i][j][e + 1]);
+              const f32x2 x = {__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+              const f32x2 arg = x * l2e + nnb;
+              const f32x2 ex = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+              ss[j] += ex;
+              tt[j] = ex * x + tt[j];
+            }
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb[j][1], acc[i][j], 0, 0, 0);
+        }
+      }
+      if (defer) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s[j] += ss[j].x + ss[j].y;
+          t[j] += tt[j].x + tt[j].y;
+        }
+      }
+    }
+    if (kt == nk - 1 && st + 1 < nsteps) {
+      // the cheap half of this tile's epilogue (never the vocab tail: another tile follows)
+      const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float rm = acc[0][j][0];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rm = fmaxf(rm, acc[i][j][e]);
+        const float nm = fmaxf(m[j], __uint_as_float(pack2_bf16(rm, 0.f) << 16));
+        const float alpha = __builtin_amdgcn_exp2f(base_of(m[j]) - base_of(nm));
+        s[j] *= alpha;
+        t[j] *= alpha;
+        m[j] = nm;
+        const int d = lab[j] - v0;
+        lsel[j] = (d >= 0 && d < 128 && (d & 12) == 0) ? ((d >> 4) * 4 + (d & 3)) : -1;
+      }
+    }
+    vt = vt_n, kt = kt_n;
+    if (++kt_n == nk) kt_n = 0, ++vt_n;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  if (nsteps > 0) {  // the last tile, whole: possibly the vocab tail
+    const int64_t vl = vt_end - 1;
+    const int v0 = static_cast<int>(vl * TB) + wr * 128 + (lane >> 4) * 4;
+    if (vl * TB + TB > V) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (v0 + i * 16 + e >= V)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j][e] = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) col_epilogue<true>(acc, j, v0, lab[j], m[j], s[j], t[j], ll[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) col_epilogue<false>(acc, j, v0, lab[j], m[j], s[j], t[j], ll[j]);
+    }
+  }
+
+  float *red = reinterpret_cast<float *>(lds);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    St a{m[j], s[j], t[j]};
+    float l2 = ll[j];
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      const float om = __shfl_xor(a.m, o, 64), os = __shfl_xor(a.s, o, 64), ot = __shfl_xor(a.t, o, 64);
+      merge_st(a, om, os, ot);
+      l2 = fmaxf(l2, __shfl_xor(l2, o, 64));
+    }
+    m[j] = a.m, s[j] = a.s, t[j] = a.t, ll[j] = l2;
+  }
+  if (wr == 1 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float *p = red + ((wc * 64) + j * 16 + lane) * 4;
+      p[0] = m[j], p[1] = s[j], p[2] = t[j], p[3] = ll[j];
+    }
+  }
+  __syncthreads();
+  if (wr == 0 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float *p = red + ((wc * 64) + j * 16 + lane) * 4;
+      St a{m[j], s[j], t[j]};
+      merge_st(a, p[0], p[1], p[2]);
+      const int64_t r = row0 + wc * 64 + j * 16 + lane;
+      if (r < N) {
+        float *o = part + (sp * N + r) * 3;
+        o[0] = a.m, o[1] = a.s, o[2] = a.t;
+        const float lv = fmaxf(ll[j], p[3]);
+        if (lv != -INFINITY) label_logit[r] = lv;
+      }
+    }
+  }
+}
+
 // EPI 0: core only (a cheap checksum keeps the MFMAs live); 1: full online-softmax epilogue
 template <int EPI, bool REMAP>
 __global__ __launch_bounds__(NT, 1) void lp_t_kernel(const uint16_t *__restrict__ hid, int64_t ldh,
@@ -262,6 +669,276 @@ __global__ __launch_bounds__(NT, 1) void lp_t_kernel(const uint16_t *__restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// v4/v5: the same tile with the 8-phase (4 per K-step) staggered schedule: per K-step the wave's
+// 128 x 64 output is done as 4 quadrants (qm, qn) of 4 x 2 blocks x 2 k-substeps = 16 MFMAs, one
+// per phase, in the order (0,0) (0,1) (1,1) (1,0) so each phase reads at most one operand half:
+// P1 A-half 0 + B-half 0, P2 B-half 1, P3 A-half 1, P4 nothing. Each phase issues ONE half-image
+// (16 KB, 2 x glds per thread) for a later K-step; the LDS image of a K-step is 4 half-images
+// (A qm: rows of both wave-rows for quadrant row qm; B qn: columns of all 4 wave-columns for qn).
+// Raw s_barrier twice per phase (before the MFMAs, after them), counted vmcnt(4) once per K-step
+// (P4), never 0 in steady state. Wave-row 1 runs ONE BARRIER BEHIND wave-row 0 (an extra barrier
+// at the start): the two waves on a SIMD (w, w + 4) alternate, one in its MFMA half while the
+// other reads fragments / issues DMA (ping-pong).
+// DMA order for step x (buffer x & 1), restaging two steps ahead once a half's last read is
+// >= 2 phases old: P3(x): A0(x+2), P4(x): B0(x+2), P1(x+1): B1(x+2), P2(x+1): A1(x+2).
+constexpr int HALF = 128 * TK;  // bf16 elements of a half-image
+
+__device__ __forceinline__ void stage_half(const uint16_t *__restrict__ src, int64_t base_row, int64_t nrows,
+                                           int64_t ld, int k0, int is_b, int qx, uint16_t *img, int wave, int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int g = wave * 2 + u;  // 16 groups of 8 rows
+    const int r = g * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((r >> 1) & 7);
+    // A half qm: vocab (r >> 6) * 128 + qm * 64 + (r & 63); B half qn: token (r >> 5) * 64 + qn * 32 + (r & 31)
+    const int trow = is_b ? ((r >> 5) * 64 + qx * 32 + (r & 31)) : ((r >> 6) * 128 + qx * 64 + (r & 63));
+    int64_t gr = base_row + trow;
+    if (gr >= nrows) gr = nrows - 1;
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + gr * ld + k0 + lc * 8), img + g * 8 * TK, 16,
+                                     0, 0);
+  }
+}
+
+template <int EPI, bool REMAP, bool DEEP = false>
+__global__ __launch_bounds__(NT, 1) void lp_t8_kernel(const uint16_t *__restrict__ hid, int64_t ldh,
+                                                      const uint16_t *__restrict__ w, int64_t ldw,
+                                                      const int64_t *__restrict__ labels, int64_t N, int K, int64_t V,
+                                                      int splits, int tiles_per_split, float *__restrict__ part,
+                                                      float *__restrict__ label_logit) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 4 * HALF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  int64_t L = blockIdx.x;
+  if (REMAP) {
+    const int64_t nl = gridDim.x >> 3;
+    L = (L & 7) * nl + (L >> 3);
+  }
+  const int64_t rb = L / splits, sp = L % splits;
+  const int64_t row0 = rb * TB;
+  const int64_t n_vt = (V + TB - 1) / TB;
+  const int64_t vt_begin = sp * tiles_per_split;
+  const int64_t vt_end = vt_begin + tiles_per_split < n_vt ? vt_begin + tiles_per_split : n_vt;
+  const int nk = K / TK;
+  const int64_t nsteps = vt_begin < vt_end ? (vt_end - vt_begin) * nk : 0;
+
+  int lab[4];
+  float m[4], s[4], t[4], ll[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t r = row0 + wc * 64 + j * 16 + (lane & 15);
+    const int64_t lb = r < N ? labels[r] : -1;
+    lab[j] = (lb >= 0 && lb < V) ? static_cast<int>(lb) : -1;
+    m[j] = -INFINITY, s[j] = 0.f, t[j] = 0.f, ll[j] = -INFINITY;
+  }
+  float chk = 0.f;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // half h (0 A0, 1 A1, 2 B0, 3 B1) of the step at vocab tile vt, k-chunk kt, into buffer b
+  auto issue = [&](int b, int64_t vt, int kt, int h) {
+    uint16_t *img = lds + (b * 4 + h) * HALF;
+    if (h < 2) stage_half(w, vt * TB, V, ldw, kt * TK, 0, h, img, wave, lane);
+    else stage_half(hid, row0, N, ldh, kt * TK, 1, h - 2, img, wave, lane);
+  };
+  auto rd = [&](const uint16_t *img, int row, int q) {
+    return *reinterpret_cast<const bf16x8 *>(img + ((row * TK) + (((q * 4 + (lane >> 4)) ^ ((row >> 1) & 7)) << 3)));
+  };
+
+  // (vocab tile, k-chunk) of steps st, st + 1, st + 2, advanced incrementally (no 64-bit divisions)
+  int64_t vt0 = vt_begin, vt1 = vt_begin, vt2 = vt_begin;
+  int kt0 = 0, kt1 = 1, kt2 = 2;
+  if (kt1 >= nk) kt1 -= nk, ++vt1;
+  if (kt2 >= nk) { kt2 -= nk, ++vt2; if (kt2 >= nk) kt2 -= nk, ++vt2; }
+  if (nsteps > 0) {
+    for (int h = 0; h < 4; ++h) issue(0, vt0, kt0, h);
+    if (nsteps > 1) {  // the steady-state issue order A0, B0, B1, A1 (the vmcnt counts rely on it)
+      issue(1, vt1, kt1, 0);
+      issue(1, vt1, kt1, 2);
+      issue(1, vt1, kt1, 3);
+      issue(1, vt1, kt1, 1);
+    }
+  }
+  if (nsteps > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger: wave-row 1 one barrier behind
+
+  bf16x8 fa0[4][2], fa1[4][2], fb0[2][2], fb1[2][2];
+  for (int64_t st = 0; st < nsteps; ++st) {
+    const int b0 = static_cast<int>(st & 1), b1 = b0 ^ 1;
+    const uint16_t *buf = lds + b0 * 4 * HALF;
+    const bool pre1 = st >= 1 && st + 1 < nsteps;  // B1 / A1 of step st + 1 (step 1: in the prologue)
+    const bool pre2 = st + 2 < nsteps;             // A0 / B0 of step st + 2
+    // ---- P1: quadrant (0,0): read A0, B0; issue B1(st+1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) fa0[i][q] = rd(buf + 0 * HALF, wr * 64 + i * 16 + (lane & 15), q);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) fb0[j][q] = rd(buf + 2 * HALF, wc * 32 + j * 16 + (lane & 15), q);
+    if (pre1) issue(b1, vt1, kt1, 3);
+    if (DEEP && st > 0) {  // B1(st), first read in P2: 4 half-tiles may stay in flight
+      if (st + 1 < nsteps) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[i][q], fb0[j][q], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- P2: quadrant (0,1): read B1; issue A1(st+1)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) fb1[j][q] = rd(buf + 3 * HALF, wc * 32 + j * 16 + (lane & 15), q);
+    if (pre1) issue(b1, vt1, kt1, 1);
+    if (DEEP && st > 0) {  // A1(st), first read in P3
+      if (st + 1 < nsteps) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[i][q], fb1[j][q], acc[i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- P3: quadrant (1,1): read A1; issue A0(st+2)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) fa1[i][q] = rd(buf + 1 * HALF, wr * 64 + i * 16 + (lane & 15), q);
+    if (pre2) issue(b0, vt2, kt2, 0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i][q], fb1[j][q], acc[4 + i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- P4: quadrant (1,0): no reads; issue B0(st+2); retire step st+1 (vmcnt)
+    if (pre2) issue(b0, vt2, kt2, 2);
+    if (DEEP) {  // A0(st+1), B0(st+1), first read in P1 of st+1: 4 half-tiles stay in flight
+      if (pre2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {  // all of step st+1
+      if (pre2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[i][q], fb0[j][q], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    const bool tile_end = kt0 == nk - 1;
+    const int64_t vt = vt0;
+    vt0 = vt1, kt0 = kt1, vt1 = vt2, kt1 = kt2;
+    if (++kt2 == nk) kt2 = 0, ++vt2;
+    if (tile_end) {
+      if constexpr (EPI == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) chk += acc[i][j][0] + acc[i][j][3];
+      } else {
+        const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;
+        if (vt * TB + TB > V) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (v0 + i * 16 + e >= V)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j][e] = -INFINITY;
+          tile_epilogue<true>(acc, v0, lab, m, s, t, ll);
+        } else {
+          tile_epilogue<false>(acc, v0, lab, m, s, t, ll);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the two wave-rows
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  float *red = reinterpret_cast<float *>(lds);
+  if constexpr (EPI == 0) {
+    if (lane == 0 && chk == 12345.f) part[0] = chk;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    St a{m[j], s[j], t[j]};
+    float l2 = ll[j];
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      const float om = __shfl_xor(a.m, o, 64), os = __shfl_xor(a.s, o, 64), ot = __shfl_xor(a.t, o, 64);
+      merge_st(a, om, os, ot);
+      l2 = fmaxf(l2, __shfl_xor(l2, o, 64));
+    }
+    m[j] = a.m, s[j] = a.s, t[j] = a.t, ll[j] = l2;
+  }
+  if (wr == 1 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float *p = red + ((wc * 64) + j * 16 + lane) * 4;
+      p[0] = m[j], p[1] = s[j], p[2] = t[j], p[3] = ll[j];
+    }
+  }
+  __syncthreads();
+  if (wr == 0 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float *p = red + ((wc * 64) + j * 16 + lane) * 4;
+      St a{m[j], s[j], t[j]};
+      merge_st(a, p[0], p[1], p[2]);
+      const int64_t r = row0 + wc * 64 + j * 16 + lane;
+      if (r < N) {
+        float *o = part + (sp * N + r) * 3;
+        o[0] = a.m, o[1] = a.s, o[2] = a.t;
+        const float lv = fmaxf(ll[j], p[3]);
+        if (lv != -INFINITY) label_logit[r] = lv;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void merge_kernel(const float *__restrict__ part, const float *__restrict__ label_logit,
                                                     const int64_t *__restrict__ labels, int64_t N, int64_t V, int splits,
                                                     float *__restrict__ logp, float *__restrict__ entropy,
@@ -288,6 +965,9 @@ __global__ __launch_bounds__(256) void merge_kernel(const float *__restrict__ pa
 
 }  // namespace
 
+
+static bool remap8(int64_t nwg) { return nwg % 8 == 0; }
+
 // variant: 0 core only + remap, 1 full + remap, 2 full without remap, 3 core only without remap
 extern "C" int f1t_fwd(int variant, const void *hidden, const void *weight, const int64_t *labels, int64_t N, int64_t H,
                        int64_t V, int splits, float *logp, float *entropy, float *lse, float *workspace, void *stream) {
@@ -304,6 +984,39 @@ extern "C" int f1t_fwd(int variant, const void *hidden, const void *weight, cons
   const auto *h = static_cast<const uint16_t *>(hidden);
   const auto *w = static_cast<const uint16_t *>(weight);
   const dim3 grid(static_cast<unsigned>(nwg));
+  if (variant == 9 || variant == 10) {
+    if (!remap8(nwg)) return -3;
+    if (variant == 9) hipLaunchKernelGGL((lp_t8_kernel<0, true, true>), grid, dim3(NT), 0, st, h, H, w, H, labels, N, (int)H, V, used, per, part, label_logit);
+    else hipLaunchKernelGGL((lp_t8_kernel<1, true, true>), grid, dim3(NT), 0, st, h, H, w, H, labels, N, (int)H, V, used, per, part, label_logit);
+    if (variant == 9) return hipGetLastError() == hipSuccess ? 0 : -2;
+    hipLaunchKernelGGL(merge_kernel, dim3(static_cast<unsigned>((N + 255) / 256)), dim3(256), 0, st, part, label_logit,
+                       labels, N, V, used, logp, entropy, lse);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
+  if (variant == 8) {
+    if (!remap8(nwg)) return -3;
+    hipLaunchKernelGGL(lp_tr_kernel, grid, dim3(NT), 0, st, h, H, w, H, labels, N, (int)H, V, used, per, part, label_logit);
+    hipLaunchKernelGGL(merge_kernel, dim3(static_cast<unsigned>((N + 255) / 256)), dim3(256), 0, st, part, label_logit,
+                       labels, N, V, used, logp, entropy, lse);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
+  if (variant == 6 || variant == 7) {  // 6: deferred column epilogue; 7: same loop without the epilogue work
+    if (!remap8(nwg)) return -3;
+    if (variant == 6) hipLaunchKernelGGL((lp_td_kernel<true>), grid, dim3(NT), 0, st, h, H, w, H, labels, N, (int)H, V, used, per, part, label_logit);
+    else hipLaunchKernelGGL((lp_td_kernel<false>), grid, dim3(NT), 0, st, h, H, w, H, labels, N, (int)H, V, used, per, part, label_logit);
+    hipLaunchKernelGGL(merge_kernel, dim3(static_cast<unsigned>((N + 255) / 256)), dim3(256), 0, st, part, label_logit,
+                       labels, N, V, used, logp, entropy, lse);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
+  if (variant == 4 || variant == 5) {
+    if (!remap8(nwg)) return -3;
+    if (variant == 4) hipLaunchKernelGGL((lp_t8_kernel<0, true>), grid, dim3(NT), 0, st, h, H, w, H, labels, N, (int)H, V, used, per, part, label_logit);
+    else hipLaunchKernelGGL((lp_t8_kernel<1, true>), grid, dim3(NT), 0, st, h, H, w, H, labels, N, (int)H, V, used, per, part, label_logit);
+    if (variant == 4) return hipGetLastError() == hipSuccess ? 0 : -2;
+    hipLaunchKernelGGL(merge_kernel, dim3(static_cast<unsigned>((N + 255) / 256)), dim3(256), 0, st, part, label_logit,
+                       labels, N, V, used, logp, entropy, lse);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
   if (variant == 0 || variant == 3) {
     if (remap) hipLaunchKernelGGL((lp_t_kernel<0, true>), grid, dim3(NT), 0, st, h, H, w, H, labels, N, (int)H, V, used, per, part, label_logit);
     else hipLaunchKernelGGL((lp_t_kernel<0, false>), grid, dim3(NT), 0, st, h, H, w, H, labels, N, (int)H, V, used, per, part, label_logit);
