@@ -2,7 +2,7 @@
 # GPU box: rocprofv3 kernel-trace stats of one headline bench step (after 1 warmup).
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out
+mkdir -p gpurun_out "$(dirname "gpurun_out/${1:-prof_bench}")"
 OUT=${1:-prof_bench}
 shift
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$OUT -o run -- python3 bench.py --no-cpu-baseline --no-kernel-timing --steps 1 --warmup 1 "$@" > gpurun_out/$OUT.log 2>&1
