@@ -20,7 +20,8 @@ for d in ("fetch", "tcc"):
     for r in rows:
         n = r["Kernel_Name"]
         if "lp_t_kernel" in n or "Cijk" in n:
-            key = ("lp_t_kernel<1,true> (remap)" if "Lb1E" in n else "lp_t_kernel<1,false> (no remap)") if "lp_t" in n else n[:40]
+            remap = ("true>" in n) or ("Lb1E" in n)
+            key = ("lp_t_kernel<1,true> (remap)" if remap else "lp_t_kernel<1,false> (no remap)") if "lp_t" in n else n[:40]
             per[(key, r["Counter_Name"])].append(float(r["Counter_Value"]))
     for (k, c), v in per.items():
         big = [x for x in v]
