@@ -331,3 +331,32 @@ def test_bucket_clip_equals_torch_clip(max_norm):
     assert torch.allclose(n_torch, n_mine, rtol=1e-6), (n_torch, n_mine)
     for p, q in zip(ma.optimizer_params(), mb.optimizer_params(), strict=True):
         assert torch.allclose(p.grad, q.grad, rtol=1e-6, atol=1e-9)
+
+
+# ------------------------------------------------------------------ batch-global agg_loss metric
+def _agg_dp_worker(rank, world, port):
+    _init(rank, world, port)
+    from oracle import reference_ops as ref
+    from verl_amd.trainer.ppo.dp_algos import agg_loss_dp
+
+    g = torch.Generator().manual_seed(7)
+    B, R = 6, 9
+    x = torch.randn(world * B, R, generator=g)
+    mask = (torch.rand(world * B, R, generator=g) > 0.3).long()
+    mask[:, 0] = 1
+    mask[1, 3:] = 0  # unequal token counts per row and per rank
+    mine = slice(rank * B, (rank + 1) * B)
+    for mode in ("token-mean", "seq-mean-token-sum", "seq-mean-token-mean", "seq-mean-token-sum-norm"):
+        got = agg_loss_dp(x[mine], mask[mine], mode)
+        want = ref.agg_loss(x, mask, mode)  # the reference's driver: agg_loss over the whole batch
+        assert torch.allclose(got, want.float(), rtol=1e-6, atol=1e-6), (mode, float(got), float(want))
+    with pytest.raises(ValueError, match="Invalid loss_agg_mode"):
+        agg_loss_dp(x[mine], mask[mine], "bogus")
+    dist.destroy_process_group()
+
+
+def test_agg_loss_dp_equals_whole_batch_agg_loss():
+    """the actor/entropy metric is agg_loss over the WHOLE batch on the reference's
+    driver (ray_trainer.py:1224-1228); each rank's shard reduces to (numerator, denominator) and one
+    all-reduce gives the same value for every agg mode."""
+    _run(_agg_dp_worker)

@@ -212,3 +212,72 @@ def test_plan_packing_pad_multiple_appends_one_dummy_sequence():
         assert len(gi) == nnz + pk.pad and (gi[nnz:] == 0).all()
         assert torch.equal(gp[nnz:], torch.arange(pk.pad))
     assert _plan_packing(am, R, "cpu", pad_multiple=1).pad == 0
+
+
+def test_plan_packing_gathers_mrope_position_ids():
+    """Qwen2-VL mrope ids [B, 3, S] pack to [3, T] in the same token order as the ids
+    (dp_actor.py:106-121: transpose to (3, B, S), index the (B S) tokens, (3, 1, T)); the dummy
+    sequence gets 0..pad-1 on all three rows."""
+    import numpy as np
+    import torch
+
+    from verl_amd.workers.actor.dp_actor import _plan_packing
+
+    rs = np.random.RandomState(1)
+    B, P, R = 4, 6, 5
+    am = np.zeros((B, P + R), dtype=np.int64)
+    for i in range(B):
+        am[i, P - rs.randint(1, P + 1) : P + rs.randint(1, R + 1)] = 1
+    pk = _plan_packing(am, R, "cpu", pad_multiple=8)
+    ids = torch.arange(B * (P + R)).view(B, P + R)
+    pos3 = torch.stack([ids * 10, ids * 10 + 1, ids * 10 + 2], dim=1)  # [B, 3, S], row c tagged c
+    gi, gp = pk.gather(ids, pos3)
+    nnz = int(am.sum())
+    assert gp.shape == (3, nnz + pk.pad)
+    for c in range(3):
+        assert torch.equal(gp[c, :nnz], gi[:nnz] * 10 + c)
+        assert torch.equal(gp[c, nnz:], torch.arange(pk.pad))
+    # reference form: (3, B, S) -> rows of the flattened (B S) at the real tokens
+    ref = pos3.transpose(0, 1).reshape(3, -1)[:, torch.from_numpy(np.flatnonzero(am.reshape(-1)))]
+    assert torch.equal(gp[:, :nnz], ref)
+
+
+def test_rewritten_helpers_keep_the_reference_error_surface():
+    import numpy as np
+    import pytest
+    import torch
+
+    from verl_amd.protocol import DataProto, DataProtoConfig, TensorBatch, union_numpy_dict, union_tensor_dict
+
+    with pytest.raises(AssertionError, match="enabled must be a boolean"):
+        DataProtoConfig.auto_padding = 1
+    DataProtoConfig.auto_padding = True
+    assert DataProtoConfig.auto_padding is True
+    DataProtoConfig.auto_padding = False
+    a = TensorBatch({"x": torch.zeros(2)})
+    with pytest.raises(AssertionError, match="identical batch size"):
+        union_tensor_dict(a, TensorBatch({"y": torch.zeros(3)}))
+    with pytest.raises(AssertionError, match="x in tensor_dict1 and tensor_dict2 are not the same object"):
+        union_tensor_dict(a, TensorBatch({"x": torch.ones(2)}))
+    merged = union_tensor_dict(a, TensorBatch({"x": torch.zeros(2), "y": torch.ones(2)}))
+    assert list(merged.keys()) == ["x", "y"]
+    with pytest.raises(AssertionError, match="u in tensor_dict1"):
+        union_numpy_dict({"u": np.array([1, 2], dtype=object)}, {"u": np.array([1, 3], dtype=object)})
+    nan = np.array([float("nan")], dtype=object)
+    assert union_numpy_dict({"v": nan}, {"v": nan.copy()})["v"] is not None
+    with pytest.raises(ValueError, match="Unsupported type in data"):
+        DataProto.from_single_dict({"x": torch.zeros(2), "bad": [1, 2]})
+    with pytest.raises(AssertionError, match="Not all the tensor in tensors have the same batch size"):
+        DataProto.from_dict(tensors={"a": torch.zeros(2), "b": torch.zeros(3)})
+    d = DataProto.from_dict(tensors={"a": torch.zeros(2)}, non_tensors={"n": [1, 2]})
+    assert d.non_tensor_batch["n"].dtype == object
+    with pytest.raises(TypeError, match="keys must be a list or a string"):
+        d.rename(old_keys=1, new_keys="b")
+    with pytest.raises(ValueError, match="must have the same length"):
+        d.rename(old_keys=["a"], new_keys=["b", "c"])
+    with pytest.raises(AssertionError):
+        d.pop(batch_keys=["missing"])
+    with pytest.raises(AssertionError, match="repeat_times type must be in"):
+        d.sample_level_repeat({1: 2})
+    r = d.sample_level_repeat(np.array([2, 1]))
+    assert len(r) == 3 and r.non_tensor_batch["n"].tolist() == [1, 1, 2]
