@@ -302,31 +302,34 @@ __device__ __forceinline__ void t_tile_epilogue(const f32x4 (&acc)[8][4], int v0
     const float nm = fmaxf(m[j], lm);
     const float nb = base_of(nm);
     const float alpha = __builtin_amdgcn_exp2f(base_of(m[j]) - nb);
-    float ss = 0.f, tt = 0.f;
+    // pairs of logits in packed fp32 (v_pk_fma_f32 / v_pk_add_f32): ~3 VALU slots + 1 exp per logit
+    // instead of ~5 + 1, the halves of ss / tt summed once per tile (33.1-33.2 vs 33.6-33.8 ms at
+    // 131,072 x 896 x 151,936, tools/f1_ab.py; profiles/r03/f1_packed_epilogue_ab.log)
+    const va_f32x2 l2e = {kLog2eF, kLog2eF}, nnb = {-nb, -nb};
+    va_f32x2 ss = {0.f, 0.f}, tt = {0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int e = 0; e < 4; e += 2) {
-        float x0, x1;
+        va_f32x2 x;
         if constexpr (ROUND && !SCALE) {  // both roundings in one v_cvt_pk_bf16_f32
           const uint32_t p = pack2_bf16(acc[i][j][e], acc[i][j][e + 1]);
-          x0 = __uint_as_float(p << 16);
-          x1 = __uint_as_float(p & 0xffff0000u);
+          x = va_f32x2{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
         } else {
-          x0 = logit_of<SCALE, ROUND>(acc[i][j][e], temperature);
-          x1 = logit_of<SCALE, ROUND>(acc[i][j][e + 1], temperature);
+          x = va_f32x2{logit_of<SCALE, ROUND>(acc[i][j][e], temperature),
+                       logit_of<SCALE, ROUND>(acc[i][j][e + 1], temperature)};
         }
-        const float e0 = __builtin_amdgcn_exp2f(fmaf(x0, kLog2eF, -nb));
-        const float e1 = __builtin_amdgcn_exp2f(fmaf(x1, kLog2eF, -nb));
-        ss += e0 + e1;
+        const va_f32x2 arg = __builtin_elementwise_fma(x, l2e, nnb);
+        const va_f32x2 ex = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+        ss = ss + ex;
         if constexpr (TAIL) {
-          x0 = x0 == -INFINITY ? 0.f : x0;
-          x1 = x1 == -INFINITY ? 0.f : x1;
+          x.x = x.x == -INFINITY ? 0.f : x.x;
+          x.y = x.y == -INFINITY ? 0.f : x.y;
         }
-        tt = fmaf(e0, x0, fmaf(e1, x1, tt));
+        tt = __builtin_elementwise_fma(ex, x, tt);
       }
-    s[j] = fmaf(s[j], alpha, ss);
-    t[j] = fmaf(t[j], alpha, tt);
+    s[j] = fmaf(s[j], alpha, ss.x + ss.y);
+    t[j] = fmaf(t[j], alpha, tt.x + tt.y);
     m[j] = nm;
   }
 }
