@@ -65,6 +65,19 @@ def pmc_traffic(kernel: str, algo_bytes_per_launch: float, vocab: int):
     return k["traffic_bytes_per_row"] * rows, os.path.relpath(p, ROOT)
 
 
+def pmc_traffic_f1(flops_per_launch: float):
+    """HBM-side bytes per launch of the fused lm_head kernel (f1) from the committed PMC passes
+    (tools/f1_pmc.sh: FETCH_SIZE x2 + WRITE_SIZE) when they were taken at this launch's shape."""
+    import glob
+
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_f1_product.json")), reverse=True):
+        d = json.load(open(p))
+        n, h, v = d["shape"]
+        if abs(2.0 * n * v * h - flops_per_launch) <= 1e-6 * flops_per_launch:
+            return d["traffic_bytes_per_launch"], os.path.relpath(p, ROOT)
+    return None, None
+
+
 def hbm_ceiling(kernel: str, rows: int | None = None, inplace: bool = False):
     """Best plain-streaming rate measured on MI355X at the same footprint (tools/hbm_stream.hip,
     profiles/r*/hbm_stream_<rows>rows.jsonl, the file of the launch's own row count when present):
@@ -480,10 +493,12 @@ def main():
             }
         f1 = ksum.get("linear_logprob_fwd")
         if f1 is not None:  # MFMA-bound fused lm_head + log-prob kernel (f1): 2 N V H flops per launch
+            f1_traffic, f1_src = pmc_traffic_f1(f1["avg_flops"])
             roof_f1 = {
                 "kernel": "linear_logprob_fwd", "bound": "mfma", "achieved": round(f1["tflops"], 1),
                 "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(f1["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4),
-                "traffic": None, "algo_flops_per_launch": f1["avg_flops"], "avg_launch_us": round(f1["avg_us"], 2),
+                "traffic": round(f1_traffic) if f1_traffic else None, "traffic_source": f1_src,
+                "algo_flops_per_launch": f1["avg_flops"], "avg_launch_us": round(f1["avg_us"], 2),
                 "launches": f1["launches"], "time_ms_total": round(f1["time_ms_total"], 2),
             }
         line = {
