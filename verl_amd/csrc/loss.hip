@@ -285,7 +285,10 @@ __device__ __forceinline__ void wg_sum_vectors(double acc, double *__restrict__ 
 // loads are issued before the first use (the workgroup-per-row kernel above waits on 4 dependent
 // load rounds per row at R = 1024). Same per-element arithmetic; the fp64 row sums are added in a
 // different (fixed) order.
-template <int MT, int KL, int JM>
+// ENT / SEL: the optional entropy rows and token selection exist (compile-time, so that an absent
+// input holds no registers: with both absent the k3 / int64-mask kernel drops from 136 VGPRs, 3 waves
+// per SIMD, to fewer)
+template <int MT, int KL, int JM, bool ENT, bool SEL>
 __global__ __launch_bounds__(256) void ppo_loss_rows_vec_kernel(
     const float *__restrict__ old_lp, const float *__restrict__ lp, const float *__restrict__ adv,
     const void *__restrict__ mask, const float *__restrict__ ref, const float *__restrict__ ent,
@@ -295,11 +298,9 @@ __global__ __launch_bounds__(256) void ppo_loss_rows_vec_kernel(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const bool tok = (agg == VA_AGG_TOKEN_MEAN);
   double acc = 0.0;  // lane q < 7: slot q of this wave's row, aggregated per row (agg_term)
-  // absent inputs read valid stand-in rows (lp's own, cache hits) so that every load is
-  // unconditional: a load under a branch makes the compiler wait for it at the join
-  const bool has_ent = ent != nullptr, has_sel = sel != nullptr;
-  const float *entp = has_ent ? ent : lp;
-  const uint8_t *selp = has_sel ? sel : reinterpret_cast<const uint8_t *>(lp);
+  // every load is unconditional (compile-time presence): a load under a branch makes the compiler
+  // wait for it at the join
+  constexpr bool has_ent = ENT, has_sel = SEL;
   {
   const int64_t b = static_cast<int64_t>(blockIdx.x) * nw + wave;
   if (b < B) {
@@ -316,14 +317,16 @@ __global__ __launch_bounds__(256) void ppo_loss_rows_vec_kernel(
     l[j] = ld4(lp + i, false);
     a[j] = ld4(adv + i, false);
     if constexpr (KL != VA_KL_NONE) rf[j] = ld4(ref + i, false);
-    h[j] = ld4(entp + i, false);
+    if constexpr (ENT) h[j] = ld4(ent + i, false);
     mr[j] = load_mask4_raw<MT>(mask, i);
-    sw[j] = *reinterpret_cast<const uint32_t *>(selp + i);
+    if constexpr (SEL) sw[j] = *reinterpret_cast<const uint32_t *>(sel + i);
   }
   loads_issued();
 #pragma unroll
   for (int j = 0; j < JM; ++j) {
-    pin4(o[j]), pin4(l[j]), pin4(a[j]), pin4(h[j]), pin_mask4<MT>(mr[j]), pin1(sw[j]);
+    pin4(o[j]), pin4(l[j]), pin4(a[j]), pin_mask4<MT>(mr[j]);
+    if constexpr (ENT) pin4(h[j]);
+    if constexpr (SEL) pin1(sw[j]);
     if constexpr (KL != VA_KL_NONE) pin4(rf[j]);
   }
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -881,16 +884,24 @@ extern "C" int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float
     constexpr int nw = 4;
     G = (B + nw - 1) / nw;
     const dim3 grid(static_cast<unsigned>(G)), block(64 * nw);
+#define VA_PPO_ROWS(JM_, ENT_, SEL_)                                                                            \
+  hipLaunchKernelGGL((ppo_loss_rows_vec_kernel<MT, KL, JM_, ENT_, SEL_>), grid, block, 0, s, old_lp, lp, adv, mask, \
+                     ref_lp, entropy, sel, B, R, J, clip_lo, clip_hi, clip_c, agg_mode, loss_mode, mode_coef, part,   \
+                     wsum)
+#define VA_PPO_ROWS_OPT(JM_)                                                                                    \
+  if (entropy != nullptr && sel != nullptr) VA_PPO_ROWS(JM_, true, true);                                      \
+  else if (entropy != nullptr) VA_PPO_ROWS(JM_, true, false);                                                  \
+  else if (sel != nullptr) VA_PPO_ROWS(JM_, false, true);                                                      \
+  else VA_PPO_ROWS(JM_, false, false)
     VA_DISPATCH_MASK(mask_dtype, VA_DISPATCH_KL(kl_type, {
-      if (J <= 4)
-        hipLaunchKernelGGL((ppo_loss_rows_vec_kernel<MT, KL, 4>), grid, block, 0, s, old_lp, lp, adv, mask,
-                           ref_lp, entropy, sel, B, R, J, clip_lo, clip_hi, clip_c, agg_mode, loss_mode, mode_coef,
-                           part, wsum);
-      else
-        hipLaunchKernelGGL((ppo_loss_rows_vec_kernel<MT, KL, 8>), grid, block, 0, s, old_lp, lp, adv, mask,
-                           ref_lp, entropy, sel, B, R, J, clip_lo, clip_hi, clip_c, agg_mode, loss_mode, mode_coef,
-                           part, wsum);
+      if (J <= 4) {
+        VA_PPO_ROWS_OPT(4);
+      } else {
+        VA_PPO_ROWS_OPT(8);
+      }
     }));
+#undef VA_PPO_ROWS_OPT
+#undef VA_PPO_ROWS
   } else {
     VA_DISPATCH_MASK(mask_dtype, VA_DISPATCH_KL(kl_type, {
       hipLaunchKernelGGL((ppo_loss_rows_kernel<MT, KL>), dim3(B), dim3(256), 0, s, old_lp, lp,
