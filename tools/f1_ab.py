@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--rows", type=int, default=131072)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--unfused", action="store_true",
+                    help="also time the unfused path (hipBLASLt lm_head GEMM + logprob_entropy_fwd), e.g. under rocprofv3")
     args = ap.parse_args()
     from verl_amd import _lib as L
     from verl_amd import kernels as K
@@ -49,9 +51,27 @@ def main():
             times.append(e0.elapsed_time(e1) / args.iters)
     times.sort()
     ms = times[len(times) // 2]
+    unfused_ms = None
+    if args.unfused:
+        logits = torch.empty(N, V, dtype=torch.bfloat16, device=dev)
+        with torch.no_grad():
+            for _ in range(3):
+                K.logprob_entropy(torch.matmul(h, w.t(), out=logits), lab, 1.0)
+            torch.cuda.synchronize()
+            ut = []
+            for _ in range(5):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.iters):
+                    K.logprob_entropy(torch.matmul(h, w.t(), out=logits), lab, 1.0)
+                e1.record()
+                torch.cuda.synchronize()
+                ut.append(e0.elapsed_time(e1) / args.iters)
+        unfused_ms = round(sorted(ut)[2], 3)
+        del logits
     print(json.dumps({"tag": args.tag, "lib": str(L.LIB_PATH), "rows": N, "ms_median": round(ms, 3),
                       "ms_all": [round(t, 3) for t in times], "tflops": round(2.0 * N * V * H / ms / 1e9, 1),
-                      "max_dlp_vs_unfused": dlp, "max_dent_vs_unfused": dent}), flush=True)
+                      "max_dlp_vs_unfused": dlp, "max_dent_vs_unfused": dent, "unfused_ms": unfused_ms}), flush=True)
 
 
 if __name__ == "__main__":
