@@ -477,12 +477,14 @@ def test_gae_quad_kernel_multi_turn_property(K):
     assert torch.equal(r1 * m, r2 * m)
 
 
+@pytest.mark.parametrize("with_entropy", [True, False])
 @pytest.mark.parametrize("R", [1024, 1000, 2048, 260, 17])
 @pytest.mark.parametrize("mode", ["vanilla", "gpg", "clip_cov", "kl_cov"])
-def test_policy_loss_streaming_forward_matches_workgroup_kernel(K, R, mode):
+def test_policy_loss_streaming_forward_matches_workgroup_kernel(K, R, mode, with_entropy):
     """VA_TUNE_LOSS_VEC: the wave-per-row streaming forward (default where it applies) and the
     workgroup-per-row forward give the same 8 slots (fp64 row sums in another order) and bitwise
-    the same gradients (the backward reads only counts from the partials)."""
+    the same gradients (the backward reads only counts from the partials). Covers the four
+    instances of the streaming kernel's compile-time optional inputs (entropy rows x selection)."""
     from verl_amd import _lib as L
 
     g = torch.Generator().manual_seed(R)
@@ -500,16 +502,20 @@ def test_policy_loss_streaming_forward_matches_workgroup_kernel(K, R, mode):
         for v in (1, 0):
             L.call("va_set_tuning", L.VA_TUNE_LOSS_VEC, v)
             x = lp.clone().requires_grad_(True)
-            e = ent.clone().requires_grad_(True)
+            e = ent.clone().requires_grad_(True) if with_entropy else None
             out = K.fused_policy_loss(old, x, adv, mask, 0.2, 0.28, 3.0, "token-mean", ref_log_prob=ref_,
                                       kl_loss_type="low_var_kl", entropy=e, loss_mode=mode, selection=sel,
                                       mode_coef=0.1)
             (out[0] + 0.01 * out[4] - 0.001 * out[5]).backward()
-            outs.append((out.detach().cpu(), x.grad.cpu(), e.grad.cpu()))
+            outs.append((out.detach().cpu(), x.grad.cpu(), e.grad.cpu() if with_entropy else None))
     finally:
         L.call("va_set_tuning", L.VA_TUNE_LOSS_VEC, 1)
     _close(outs[0][0], outs[1][0], atol=1e-6, rtol=1e-6, what="loss slots vec vs wg")
-    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
+    assert torch.equal(outs[0][1], outs[1][1])
+    if with_entropy:
+        assert torch.equal(outs[0][2], outs[1][2])
+    else:
+        assert outs[0][0][5].item() == 0.0  # the entropy slot of a loss without entropy rows
 
 
 @pytest.mark.parametrize("B", [1500, 4500, 9001])
