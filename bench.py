@@ -107,6 +107,24 @@ def _gemm_table_name():
     return os.path.basename(gemm_tuning._loaded) if gemm_tuning._loaded else None
 
 
+def _micro_text(micro: int, pass_rows: int, args) -> str:
+    """The loss micro-batch part of config.deviations_from_reference_defaults."""
+    if args.dynamic_bsz:
+        return (f"use_dynamic_bsz with a {args.dynamic_bsz}-token budget (loss scaled by rows / mini-batch, "
+                "dp_actor.py:465-467); ")
+    passes = (f"update passes of {pass_rows} responses, each holding {pass_rows // micro} of those micro-batches, "
+              "aggregated one by one by the fused loss kernel (seg_rows: the same loss, gradient and "
+              "per-micro-batch metric lists as separate passes, tests/test_actor_gpu.py); " if pass_rows > micro
+              else "")
+    if micro == 8:
+        return "none for the loss micro-batch (ppo_micro_batch_size_per_gpu 8, SURVEY §8d); " + passes
+    same = ("equal to the reference's at 8 with dense responses (equal token counts per micro-batch); "
+            if args.responses == "dense" else
+            f"with variable response lengths it weights tokens differently than at 8 (each micro-batch's "
+            "token-mean is over its own token count, dp_actor.py:465-470); ")
+    return f"ppo_micro_batch_size_per_gpu {micro} (SURVEY §8d: 8): " + same + passes
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,8 +138,12 @@ def parse(argv=None):
     ap.add_argument("--n", type=int, default=8)
     ap.add_argument("--prompt-len", type=int, default=256)
     ap.add_argument("--response-len", type=int, default=1024)
-    ap.add_argument("--micro", type=int, default=128,
-                    help="ppo_micro_batch_size_per_gpu (responses; capped at the rank's shard)")
+    ap.add_argument("--micro", type=int, default=8,
+                    help="ppo_micro_batch_size_per_gpu: the loss micro-batch (responses; SURVEY §8d: 8)")
+    ap.add_argument("--compute-micro", type=int, default=128,
+                    help="compute_micro_batch_size_per_gpu: responses per update forward/backward pass, holding "
+                         "compute-micro / micro loss micro-batches that the fused loss aggregates one by one "
+                         "(capped at the rank's shard)")
     ap.add_argument("--logprob-micro", type=int, default=128, help="log_prob_micro_batch_size_per_gpu")
     ap.add_argument("--dynamic-bsz", type=int, default=0,
                     help="use_dynamic_bsz with this ppo_max_token_len_per_gpu (and log-prob budget); 0 = off")
@@ -358,12 +380,14 @@ def main():
     B = B_total // world if strong else args.prompts * args.n  # responses on this rank
     R = args.response_len
     micro = min(args.micro, B)
+    cmicro = max(micro, min(args.compute_micro, B))
     lp_micro = min(args.logprob_micro, B)
     cfg = AttrDict(
         actor=actor_config(
             # prompts per mini-batch; x rollout_n / world in ActorWorker -> one optimizer step per rank
             ppo_mini_batch_size=args.prompts if strong else args.prompts * world,
             ppo_micro_batch_size_per_gpu=micro,
+            compute_micro_batch_size_per_gpu=cmicro,
             use_kl_loss=True, kl_loss_coef=0.001, kl_loss_type="low_var_kl",
             clip_ratio=0.2, clip_ratio_c=3.0, loss_agg_mode="token-mean", entropy_coeff=0,
             use_remove_padding=not args.no_rmpad,
@@ -527,18 +551,13 @@ def main():
                 "response_len": R,
                 "vocab": VOCAB,
                 "micro_batch": micro,
+                "compute_micro_batch": worker.actor._pass_rows("vanilla") if not args.dynamic_bsz else None,
                 "logprob_micro_batch": lp_micro,
                 "old_logp_noise": args.old_noise,
                 "response_lengths": (f"dense: all {R} valid" if args.responses == "dense"
                                      else f"realistic: U[128, {R}]"),
                 "deviations_from_reference_defaults": (
-                    f"ppo_micro_batch_size_per_gpu {micro} (SURVEY §8d: 8; larger micro-batches fill the "
-                    "MI355X GEMMs); the loss is the reference's token-mean per micro-batch / grad-accum "
-                    "(dp_actor.py:465-470), "
-                    + ("which with dense responses (every micro-batch holds the same token count) equals the "
-                       "reference's at micro-batch 8; " if args.responses == "dense" else
-                       f"which with variable response lengths weights tokens differently at micro-batch {micro} "
-                       "than at 8 (each micro-batch's mean is over its own token count); ")
+                    _micro_text(micro, worker.actor._pass_rows("vanilla"), args)
                     + ("out-of-place log-prob backward (reference: in place)" if not args.logprob_inplace_bwd
                        else "in-place log-prob backward as the reference")
                     + ("; the no-grad old-logp pass runs the fused lm_head + log-prob kernel (the reference's "

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define VA_ABI_VERSION 3
+#define VA_ABI_VERSION 4
 
 /* error codes */
 #define VA_OK 0
@@ -197,7 +197,12 @@ int va_set_tuning(int key, int value);
  *   with the reference's top-k / random draw; NULL for vanilla and gpg. Metric slots per mode:
  *   vanilla as the reference; gpg: 0, 0, 0; clip_cov: masked_mean(sel), masked_mean(old - lp), 0;
  *   kl_cov: 0, masked_mean(|lp - old|) (ppo_kl_abs), 0.
- *   out[VA_LOSS_NOUT] fp32 (device). workspace: va_ppo_loss_workspace_bytes(B) = 8 (16 B + 8):
+ *   seg_rows: 0 (or >= B) aggregates the whole [B, R] batch into out[VA_LOSS_NOUT]; 0 < seg_rows < B
+ *   splits it into S = ceil(B / seg_rows) loss micro-batches of seg_rows consecutive rows (the last
+ *   may be shorter), each aggregated on its own as a separate call over its rows would be (its own
+ *   token and row counts: the reference's agg_loss per micro-batch, dp_actor.py:419-470), into
+ *   out[S][VA_LOSS_NOUT].
+ *   out fp32 (device). workspace: va_ppo_loss_workspace_bytes(B) = 8 (16 B + 8):
  *   [B, 8] fp64 row partials, 8 fp64 totals (n first), then up to B per-workgroup aggregated
  *   vectors that only the forward reads. The first 8 B + 8 doubles are what the backward reads:
  *   keep them alive between the forward and the backward of the same micro-batch. */
@@ -205,18 +210,19 @@ int64_t va_ppo_loss_workspace_bytes(int64_t B);
 int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float *adv, const void *mask,
                     int mask_dtype, const float *ref_lp, const float *entropy, int64_t B,
                     int64_t R, float clip_lo, float clip_hi, float clip_c, int agg_mode,
-                    int kl_type, int loss_mode, const uint8_t *sel, float mode_coef, float *out,
-                    void *workspace, void *stream);
+                    int kl_type, int loss_mode, const uint8_t *sel, float mode_coef,
+                    int64_t seg_rows, float *out, void *workspace, void *stream);
 
-/* Backward: g_out[VA_LOSS_NOUT] is d(loss)/d(out) as a device vector (only slots PG, KL,
- * ENTROPY are read; may be NULL = zeros). Writes d_lp [B,R] and, if non-NULL, d_entropy.
+/* Backward: g_out[S][VA_LOSS_NOUT] is d(loss)/d(out) as a device array (only slots PG, KL,
+ * ENTROPY are read; may be NULL = zeros), seg_rows as in the forward (S = 1 when 0). Writes
+ * d_lp [B,R] and, if non-NULL, d_entropy.
  * Tie and boundary gradients follow torch autograd of the reference expression:
  * maximum/minimum split ties 1/2-1/2, clamp passes inclusive of its bounds, abs' gradient at 0 is 0. */
 int va_ppo_loss_bwd(const float *g_out, const float *old_lp, const float *lp, const float *adv,
                     const void *mask, int mask_dtype, const float *ref_lp, int64_t B, int64_t R,
                     float clip_lo, float clip_hi, float clip_c, int agg_mode, int kl_type,
-                    int loss_mode, const uint8_t *sel, float mode_coef, const void *workspace,
-                    float *d_lp, float *d_entropy, void *stream);
+                    int loss_mode, const uint8_t *sel, float mode_coef, int64_t seg_rows,
+                    const void *workspace, float *d_lp, float *d_entropy, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Elementwise KL estimators (core_algos.py:1034-1069), n elements.
@@ -392,8 +398,10 @@ int va_discounted_returns(const float *rewards, const void *mask, int mask_dtype
  * Critic: fused clipped value loss (core_algos.py:992-1031, clip_by_value torch_functional.py:
  * 136-142) + the critic's vpred_mean metric (dp_critic.py:236-242).
  *   vpreds, values, returns [B, R] fp32; mask [B, R] of mask_dtype; agg_mode = VA_AGG_*.
- *   out[VA_VLOSS_NOUT] fp32 (device); workspace: va_ppo_loss_workspace_bytes(B).
- * Backward: g_out[VA_VLOSS_NOUT] = d(loss)/d(out) (slots LOSS and VPRED_MEAN are read) ->
+ *   seg_rows as va_ppo_loss_fwd: 0 aggregates the whole batch into out[VA_VLOSS_NOUT]; 0 < seg_rows
+ *   < B gives out[S][VA_VLOSS_NOUT] for the S loss micro-batches of seg_rows rows (dp_critic.py:
+ *   218-242 per micro-batch). workspace: va_ppo_loss_workspace_bytes(B).
+ * Backward: g_out[S][VA_VLOSS_NOUT] = d(loss)/d(out) (slots LOSS and VPRED_MEAN are read) ->
  *   d_vpreds [B, R]. Ties follow torch.maximum / minimum autograd (gradient halves).
  * ------------------------------------------------------------------------------------ */
 #define VA_VLOSS_LOSS 0       /* vf_loss            core_algos.py:1029 */
@@ -402,11 +410,11 @@ int va_discounted_returns(const float *rewards, const void *mask, int mask_dtype
 #define VA_VLOSS_NTOKENS 3    /* sum(response_mask) (diagnostic) */
 #define VA_VLOSS_NOUT 4
 int va_value_loss_fwd(const float *vpreds, const float *values, const float *returns, const void *mask,
-                      int mask_dtype, int64_t B, int64_t R, float cliprange_value, int agg_mode, float *out,
-                      void *workspace, void *stream);
+                      int mask_dtype, int64_t B, int64_t R, float cliprange_value, int agg_mode,
+                      int64_t seg_rows, float *out, void *workspace, void *stream);
 int va_value_loss_bwd(const float *g_out, const float *vpreds, const float *values, const float *returns,
                       const void *mask, int mask_dtype, int64_t B, int64_t R, float cliprange_value,
-                      int agg_mode, const void *workspace, float *d_vpreds, void *stream);
+                      int agg_mode, int64_t seg_rows, const void *workspace, float *d_vpreds, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Causal varlen flash-attention forward for the actor backbone (not a §8 row). q [T, Hq, 64],

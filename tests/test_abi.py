@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_abi_version_and_workspace_queries(lib):
-    assert lib.va_abi_version() == 3
+    assert lib.va_abi_version() == 4
     assert lib.va_ppo_loss_workspace_bytes(10) == 8 * (2 * 10 * 8 + 8)
     assert lib.va_agg_workspace_bytes(10) == 8 * (2 * 10 * 8 + 8)
     assert lib.va_gae_workspace_bytes(7) == 8 * (6 * 7 + 8)
@@ -52,13 +52,15 @@ def test_argument_validation_without_device(lib):
     # invalid shapes are rejected before any HIP call
     rc = lib.va_logprob_entropy_fwd(None, 1, 4, 0, 0, None, 1.0, None, None, None, None)
     assert rc == -1 and b"vocab" in lib.va_last_error()
-    rc = lib.va_ppo_loss_fwd(None, None, None, None, 0, None, None, 0, 5, 0.8, 1.2, 3.0, 0, -1, 0, None, 0.0, None,
-                             None, None)
+    rc = lib.va_ppo_loss_fwd(None, None, None, None, 0, None, None, 0, 5, 0.8, 1.2, 3.0, 0, -1, 0, None, 0.0, 0,
+                             None, None, None)
     assert rc == -1 and b"empty batch" in lib.va_last_error()
     # the clip_cov / kl_cov modes need their token selection
-    rc = lib.va_ppo_loss_fwd(1, 1, 1, 1, 0, None, None, 2, 5, 0.8, 1.2, 3.0, 0, -1, L.VA_PL_CLIP_COV, None, 0.0, 1,
-                             1, None)
+    rc = lib.va_ppo_loss_fwd(1, 1, 1, 1, 0, None, None, 2, 5, 0.8, 1.2, 3.0, 0, -1, L.VA_PL_CLIP_COV, None, 0.0, 0,
+                             1, 1, None)
     assert rc == -1 and b"selection" in lib.va_last_error()
+    rc = lib.va_ppo_loss_fwd(1, 1, 1, 1, 0, None, None, 2, 5, 0.8, 1.2, 3.0, 0, -1, 0, None, 0.0, -1, 1, 1, None)
+    assert rc == -1 and b"seg_rows" in lib.va_last_error()
     assert lib.va_outcome_workspace_bytes(10) == 4 * 3 * 10
     rc = lib.va_group_coef(1, None, 1, 1, 4, 8, 1e-6, L.VA_ADV_OPO, 1, None)
     assert rc == -1 and b"lengths" in lib.va_last_error()

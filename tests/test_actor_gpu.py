@@ -78,10 +78,16 @@ def test_rmpad_varlen_path_matches_padded_path():
     assert (lp_pk[~m] == 0).all()
 
 
-@pytest.mark.parametrize("agg", ["token-mean", "seq-mean-token-mean"])
-def test_update_policy_gradients_match_reference(agg):
+@pytest.mark.parametrize("agg,mb,cmb", [("token-mean", 4, None), ("seq-mean-token-mean", 4, None),
+                                         ("token-mean", 4, 8), ("seq-mean-token-mean", 3, 6),
+                                         ("seq-mean-token-sum", 2, 8), ("seq-mean-token-sum-norm", 3, 8)])
+def test_update_policy_gradients_match_reference(agg, mb, cmb):
     """One mini-batch of update_policy (fp32, padded path) vs the reference loss written with
-    the oracle and torch autograd on an identical model copy: same gradients, same metrics."""
+    the oracle and torch autograd on an identical model copy: same gradients, same metrics.
+    cmb = compute_micro_batch_size_per_gpu: several loss micro-batches of mb rows in one pass
+    (the fused loss aggregates each on its own) must give the reference's per-micro-batch
+    metric lists and its accumulated gradient (micro-batches [0:mb], [mb:2mb], ..., the last
+    one ragged when mb does not divide 8)."""
     from verl_amd.utils.model import build_qwen2
 
     torch.manual_seed(0)
@@ -97,9 +103,9 @@ def test_update_policy_gradients_match_reference(agg):
     b["ref_log_prob"] = lp0 + 0.1 * torch.randn(lp0.shape, device=DEV, generator=g)
     b["advantages"] = torch.randn(8, R, device=DEV, generator=g) * b["response_mask"]
     data.meta_info.update(temperature=1.0)
-    cfg = dict(use_remove_padding=False, autocast_dtype=None, ppo_mini_batch_size=8, ppo_micro_batch_size_per_gpu=4,
+    cfg = dict(use_remove_padding=False, autocast_dtype=None, ppo_mini_batch_size=8, ppo_micro_batch_size_per_gpu=mb,
                use_kl_loss=True, kl_loss_type="low_var_kl", kl_loss_coef=0.01, loss_agg_mode=agg, entropy_coeff=0.01,
-               clip_ratio=0.2, grad_clip=1e9)
+               clip_ratio=0.2, grad_clip=1e9, compute_micro_batch_size_per_gpu=cmb)
     actor = _actor(model, **cfg)
     # capture gradients before the optimizer step
     grads = {}
@@ -111,22 +117,27 @@ def test_update_policy_gradients_match_reference(agg):
 
     actor._optimizer_step = capture
     metrics = actor.update_policy(data)
-    # reference: the same two micro-batches, oracle loss, torch autograd
+    if cmb:
+        assert actor._pass_rows("vanilla") == cmb // mb * mb
+    # reference: the same micro-batches of mb rows, oracle loss, torch autograd, / (8 // mb)
     model_ref.zero_grad()
-    pg_losses = []
-    for s in (0, 4):
-        sl = slice(s, s + 4)
-        mb = {k: v[sl] for k, v in b.items()}
-        out = model_ref(input_ids=mb["input_ids"], attention_mask=mb["attention_mask"],
-                        position_ids=mb["position_ids"], use_cache=False).logits[:, -R - 1 : -1, :]
-        lp = torch.stack([ref.logprobs_from_logits(r, lab) for r, lab in zip(out, mb["responses"], strict=True)])
+    pg_losses, kl_losses = [], []
+    for s in range(0, 8, mb):
+        sl = slice(s, s + mb)
+        mbat = {k: v[sl] for k, v in b.items()}
+        out = model_ref(input_ids=mbat["input_ids"], attention_mask=mbat["attention_mask"],
+                        position_ids=mbat["position_ids"], use_cache=False).logits[:, -R - 1 : -1, :]
+        lp = torch.stack([ref.logprobs_from_logits(r, lab) for r, lab in zip(out, mbat["responses"], strict=True)])
         ent = ref.entropy_from_logits(out)
-        loss, met = ref.actor_loss(mb["old_log_probs"], lp, mb["advantages"], mb["response_mask"], clip_ratio=0.2,
-                                   loss_agg_mode=agg, entropy=ent, entropy_coeff=0.01, ref_log_prob=mb["ref_log_prob"],
-                                   kl_loss_type="low_var_kl", kl_loss_coef=0.01, grad_scale=0.5)
+        loss, met = ref.actor_loss(mbat["old_log_probs"], lp, mbat["advantages"], mbat["response_mask"], clip_ratio=0.2,
+                                   loss_agg_mode=agg, entropy=ent, entropy_coeff=0.01, ref_log_prob=mbat["ref_log_prob"],
+                                   kl_loss_type="low_var_kl", kl_loss_coef=0.01, grad_scale=1.0 / (8 // mb))
         loss.backward()
         pg_losses.append(met["pg_loss"].item())
+        kl_losses.append(met["kl_loss"].item())
+    assert len(metrics["actor/pg_loss"]) == len(pg_losses) == len(metrics["actor/kl_coef"])
     assert np.allclose(metrics["actor/pg_loss"], pg_losses, atol=1e-5, rtol=1e-4)
+    assert np.allclose(metrics["actor/kl_loss"], kl_losses, atol=1e-6, rtol=1e-4)
     for n, p in model_ref.named_parameters():
         gr = p.grad
         scale = gr.abs().max().item() + 1e-12

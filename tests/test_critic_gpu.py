@@ -93,9 +93,12 @@ def _ref_values(model, b):
     return out[:, -R - 1 : -1].squeeze(-1)
 
 
-def test_critic_compute_values_and_update_match_reference():
+@pytest.mark.parametrize("mb,cmb", [(4, None), (4, 8), (3, 8)])
+def test_critic_compute_values_and_update_match_reference(mb, cmb):
     """fp32 padded path: compute_values == HF value model slice x mask; update_critic gradients ==
-    oracle clipped value loss through torch autograd on an identical model copy."""
+    oracle clipped value loss through torch autograd on an identical model copy. cmb =
+    compute_micro_batch_size_per_gpu: the loss micro-batches of mb rows aggregated one by one
+    inside larger passes give the same per-micro-batch metrics and accumulated gradient."""
     from verl_amd.utils.config import critic_config
     from verl_amd.utils.model import build_qwen2_critic
     from verl_amd.workers.critic import DataParallelPPOCritic
@@ -105,7 +108,8 @@ def test_critic_compute_values_and_update_match_reference():
     model_ref = copy.deepcopy(model)
     data = _batch(seed=4)
     b = data.batch
-    cfg = critic_config(ppo_mini_batch_size=8, ppo_micro_batch_size_per_gpu=4, grad_clip=1e9, cliprange_value=0.5)
+    cfg = critic_config(ppo_mini_batch_size=8, ppo_micro_batch_size_per_gpu=mb, grad_clip=1e9, cliprange_value=0.5,
+                        compute_micro_batch_size_per_gpu=cmb)
     critic = DataParallelPPOCritic(cfg, model, torch.optim.AdamW(model.parameters(), lr=1e-3))
     data.meta_info.update(micro_batch_size=3, use_dynamic_bsz=False)
     values = critic.compute_values(data)
@@ -125,15 +129,16 @@ def test_critic_compute_values_and_update_match_reference():
 
     critic._optimizer_step = capture
     metrics = critic.update_critic(data)
-    assert len(metrics["critic/vf_loss"]) == 2 and len(metrics["critic/grad_norm"]) == 1
+    starts = range(0, 8, mb)
+    assert len(metrics["critic/vf_loss"]) == len(starts) and len(metrics["critic/grad_norm"]) == 1
     model_ref.zero_grad()
     losses = []
-    for s in (0, 4):
-        mb = {k: v[s : s + 4] for k, v in b.items()}
+    for s in starts:
+        mbat = {k: v[s : s + mb] for k, v in b.items()}
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            vp = _ref_values(model_ref, mb).float()
-        loss, _ = ref.compute_value_loss(vp, mb["returns"], mb["values"], mb["response_mask"], 0.5)
-        (loss / 2).backward()
+            vp = _ref_values(model_ref, mbat).float()
+        loss, _ = ref.compute_value_loss(vp, mbat["returns"], mbat["values"], mbat["response_mask"], 0.5)
+        (loss / (8 // mb)).backward()
         losses.append(loss.item())
     assert np.allclose(metrics["critic/vf_loss"], losses, atol=1e-4, rtol=1e-3)
     for n, p in model_ref.named_parameters():

@@ -46,17 +46,20 @@ def test_opcheck_logprob_entropy():
     _check(ops.logprob_entropy_bwd_, (g, g, logits.clone(), labels, lse, ent, 1.0))
 
 
-@pytest.mark.parametrize("mode,kl", [(0, 3), (0, -1), (1, 0), (2, 3), (3, 1)])
-def test_opcheck_ppo_loss(mode, kl):
-    _, _, old, adv, mask, ref = _inputs()
+@pytest.mark.parametrize("mode,kl,seg", [(0, 3, 0), (0, -1, 0), (1, 0, 0), (2, 3, 0), (3, 1, 0), (0, 3, 3)])
+def test_opcheck_ppo_loss(mode, kl, seg):
+    B = 8 if seg else 4  # seg 3: loss micro-batches of rows [0:3], [3:6], [6:8] -> out [3, 8]
+    _, _, old, adv, mask, ref = _inputs(B=B)
     lp = (old + 0.05 * torch.randn_like(old)).requires_grad_(True)
     ent = torch.rand_like(old).requires_grad_(True)
     sel = (torch.rand_like(old) < 0.1).to(torch.uint8) if mode in (2, 3) else None
-    args = (old, lp, adv, mask, ref if kl >= 0 else None, ent, sel, 0.8, 1.2, 3.0, 0, kl, mode, 0.1)
+    args = (old, lp, adv, mask, ref if kl >= 0 else None, ent, sel, 0.8, 1.2, 3.0, 0, kl, mode, 0.1, seg)
     _check(ops.ppo_loss_fwd, args)
     out, ws = ops.ppo_loss_fwd(*args)
+    assert out.shape == ((3, 8) if seg else (8,))
     g = torch.ones_like(out)
-    _check(ops.ppo_loss_bwd, (g, old, lp.detach(), adv, mask, args[4], sel, ws, 0.8, 1.2, 3.0, 0, kl, mode, 0.1, True))
+    _check(ops.ppo_loss_bwd, (g, old, lp.detach(), adv, mask, args[4], sel, ws, 0.8, 1.2, 3.0, 0, kl, mode, 0.1, True,
+                              seg))
 
 
 def test_opcheck_kl_agg_value():
@@ -74,6 +77,11 @@ def test_opcheck_kl_agg_value():
     _check(ops.value_loss_fwd, (vp, old, ref, mask, 0.5, 0))
     out, ws = ops.value_loss_fwd(vp.detach(), old, ref, mask, 0.5, 0)
     _check(ops.value_loss_bwd, (torch.ones_like(out), vp.detach(), old, ref, mask, ws, 0.5, 0))
+    # two loss micro-batches of 2 rows: out [2, 4]
+    _check(ops.value_loss_fwd, (vp, old, ref, mask, 0.5, 0, 2))
+    out, ws = ops.value_loss_fwd(vp.detach(), old, ref, mask, 0.5, 0, 2)
+    assert out.shape == (2, 4)
+    _check(ops.value_loss_bwd, (torch.ones_like(out), vp.detach(), old, ref, mask, ws, 0.5, 0, 2))
 
 
 def test_opcheck_advantage_ops():

@@ -432,37 +432,110 @@ __global__ __launch_bounds__(1024) void ppo_loss_finalize_kernel(const double *_
   if (threadIdx.x < kTotals) totals[threadIdx.x] = threadIdx.x == 0 ? v[0] : 0.0;
 }
 
+// ------------------------------------------------------------------ loss micro-batch segments
+// One [B, R] launch can hold several of the reference's loss micro-batches (dp_actor.py:388-470:
+// agg_loss per micro-batch of ppo_micro_batch_size_per_gpu rows, each / gradient_accumulation):
+// segment s = rows [s * seg_rows, min(B, (s + 1) * seg_rows)) is aggregated on its own, exactly as
+// a separate call over those rows would (its own token count n_s, its own row count B_s).
+//
+// Slot q of one segment summed over its rows in a fixed order that both the forward's finalize and
+// the backward reproduce (so n_s is the same double in both): lane 8 k + q adds rows b0 + k, b0 + k
+// + 8, ... in order, then the 8 k-partials meet by xor 8, 16, 32. Every lane of the wave returns
+// the segment sum of its slot q = lane & 7 (term slots aggregated per row with agg_term).
+__device__ __forceinline__ double seg_slot_sum(const double *__restrict__ part, int64_t b0, int64_t b1, int agg,
+                                               unsigned term_mask) {
+  const int lane = threadIdx.x & 63, q = lane & 7, k = lane >> 3;
+  const bool term = (term_mask >> q) & 1u;
+  double acc = 0.0;
+  for (int64_t b = b0 + k; b < b1; b += 8) {
+    const double x = part[b * kNQ + q];
+    acc += term ? agg_term(agg, x, part[b * kNQ]) : x;
+  }
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) acc += __shfl_xor(acc, o, kWave);
+  return acc;
+}
+
+// The batch totals slots after the row partials (every workspace slot the op returns is written):
+// n over all rows, then zeros. Segment workgroup 0 writes them.
+__device__ __forceinline__ void seg_write_totals(double *__restrict__ part, int64_t B, int agg) {
+  if (blockIdx.x != 0) return;
+  const double n = seg_slot_sum(part, 0, B, agg, 0u);
+  if (threadIdx.x < kTotals) part[B * kNQ + threadIdx.x] = threadIdx.x == 0 ? n : 0.0;
+}
+
+// One 64-thread workgroup per segment: out[s][VA_LOSS_NOUT] as the one-segment finalize writes it.
+__global__ __launch_bounds__(64) void ppo_loss_seg_finalize_kernel(double *__restrict__ part, int64_t B,
+                                                                   int64_t R, int64_t seg_rows, int agg,
+                                                                   int has_kl, int has_ent,
+                                                                   float *__restrict__ out) {
+  seg_write_totals(part, B, agg);
+  const int64_t s = blockIdx.x;
+  const int64_t b0 = s * seg_rows, b1 = b0 + seg_rows < B ? b0 + seg_rows : B;
+  const double x = seg_slot_sum(part, b0, b1, agg, (1u << 1) | (1u << 5) | (1u << 6));
+  double v[kNQ];
+#pragma unroll
+  for (int q = 0; q < kNQ; ++q) v[q] = __shfl(x, q, kWave);
+  if (threadIdx.x == 0) {
+    const double n = v[0];
+    const double den = n + 1e-8;
+    const int64_t Bs = b1 - b0;
+    float *o = out + s * VA_LOSS_NOUT;
+    o[VA_LOSS_PG] = static_cast<float>(agg_finish(agg, v[1], n, Bs, R));
+    o[VA_LOSS_CLIPFRAC] = static_cast<float>(v[2] / den);
+    o[VA_LOSS_PPO_KL] = static_cast<float>(v[3] / den);
+    o[VA_LOSS_CLIPFRAC_LOWER] = static_cast<float>(v[4] / den);
+    o[VA_LOSS_KL] = has_kl ? static_cast<float>(agg_finish(agg, v[5], n, Bs, R)) : 0.f;
+    o[VA_LOSS_ENTROPY] = has_ent ? static_cast<float>(agg_finish(agg, v[6], n, Bs, R)) : 0.f;
+    o[VA_LOSS_NTOKENS] = static_cast<float>(n);
+    o[VA_LOSS_NROWS] = static_cast<float>(Bs);
+  }
+}
+
 // ------------------------------------------------------------------ policy loss backward
+// seg_rows in (0, B): row b belongs to segment b / seg_rows, whose upstream gradients are
+// g_out[s][*] and whose token / row counts replace the batch totals (see seg_slot_sum).
 template <int MT, int KL>
 __global__ __launch_bounds__(256) void ppo_loss_bwd_kernel(
     const float *__restrict__ g_out, const float *__restrict__ old_lp,
     const float *__restrict__ lp, const float *__restrict__ adv, const void *__restrict__ mask,
     const float *__restrict__ ref, const uint8_t *__restrict__ sel, int64_t B, int64_t R, float lo,
-    float hi, float c, int agg, int mode, float coef, const double *__restrict__ part,
+    float hi, float c, int agg, int mode, float coef, int64_t seg_rows, const double *__restrict__ part,
     float *__restrict__ d_lp, float *__restrict__ d_ent) {
   const int64_t b = blockIdx.y;
+  const float *gs = g_out;  // this row's segment's upstream gradients
+  double n_tot;
+  int64_t Bs = B;
+  if (seg_rows > 0) {  // uniform per workgroup; every wave computes the segment's n_s (before any exit)
+    const int64_t s = b / seg_rows;
+    const int64_t b0 = s * seg_rows, b1 = b0 + seg_rows < B ? b0 + seg_rows : B;
+    n_tot = __shfl(seg_slot_sum(part, b0, b1, agg, 0u), 0, kWave);
+    Bs = b1 - b0;
+    if (gs) gs += s * VA_LOSS_NOUT;
+  } else {
+    n_tot = part[B * kNQ + 0];
+  }
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= R) return;
   const int64_t i = b * R + t;
-  const float g_pg = g_out ? g_out[VA_LOSS_PG] : 0.f;
-  const float g_kl = g_out ? g_out[VA_LOSS_KL] : 0.f;
-  const float g_en = g_out ? g_out[VA_LOSS_ENTROPY] : 0.f;
+  const float g_pg = gs ? gs[VA_LOSS_PG] : 0.f;
+  const float g_kl = gs ? gs[VA_LOSS_KL] : 0.f;
+  const float g_en = gs ? gs[VA_LOSS_ENTROPY] : 0.f;
   const double n_b = part[b * kNQ + 0];
-  const double n_tot = part[B * kNQ + 0];
   const float m = load_mask<MT>(mask, i);
   const bool mb = (m != 0.f);
   const bool tok = (agg == VA_AGG_TOKEN_MEAN);
   // token-mean routes through where(mask.bool(), x, 0): zero where mask == 0
   const float keep = (!tok || mb) ? 1.f : 0.f;
-  const float w_pg = agg_weight(agg, g_pg, m, n_b, n_tot, B, R) * keep;
+  const float w_pg = agg_weight(agg, g_pg, m, n_b, n_tot, Bs, R) * keep;
   const float x_lp = lp[i];
   float g = policy_dlp(w_pg, old_lp[i], x_lp, adv[i], lo, hi, c, mode, sel != nullptr && sel[i] != 0, coef);
   if constexpr (KL != VA_KL_NONE) {
-    const float w_kl = agg_weight(agg, g_kl, m, n_b, n_tot, B, R) * keep;
+    const float w_kl = agg_weight(agg, g_kl, m, n_b, n_tot, Bs, R) * keep;
     g += w_kl * kl_dlp<KL>(x_lp, ref[i]);
   }
   d_lp[i] = g;
-  if (d_ent != nullptr) d_ent[i] = agg_weight(agg, g_en, m, n_b, n_tot, B, R) * keep;
+  if (d_ent != nullptr) d_ent[i] = agg_weight(agg, g_en, m, n_b, n_tot, Bs, R) * keep;
 }
 
 // ------------------------------------------------------------------ masked aggregation
@@ -773,24 +846,57 @@ __global__ __launch_bounds__(1024) void value_loss_finalize_kernel(const double 
   if (threadIdx.x < kTotals) totals[threadIdx.x] = threadIdx.x == 0 ? v[0] : 0.0;
 }
 
+// Loss micro-batch segments as the policy loss (seg_slot_sum): out[s][VA_VLOSS_NOUT] per segment.
+__global__ __launch_bounds__(64) void value_loss_seg_finalize_kernel(double *__restrict__ part, int64_t B,
+                                                                     int64_t R, int64_t seg_rows, int agg,
+                                                                     float *__restrict__ out) {
+  seg_write_totals(part, B, agg);
+  const int64_t s = blockIdx.x;
+  const int64_t b0 = s * seg_rows, b1 = b0 + seg_rows < B ? b0 + seg_rows : B;
+  const double x = seg_slot_sum(part, b0, b1, agg, 1u << 1);
+  double v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = __shfl(x, q, kWave);
+  if (threadIdx.x == 0) {
+    const double n = v[0];
+    const double den = n + 1e-8;
+    float *o = out + s * VA_VLOSS_NOUT;
+    o[VA_VLOSS_LOSS] = 0.5f * static_cast<float>(agg_finish(agg, v[1], n, b1 - b0, R));
+    o[VA_VLOSS_CLIPFRAC] = static_cast<float>(v[2] / den);
+    o[VA_VLOSS_VPRED_MEAN] = static_cast<float>(v[3] / den);
+    o[VA_VLOSS_NTOKENS] = static_cast<float>(n);
+  }
+}
+
 template <int MT>
 __global__ __launch_bounds__(256) void value_loss_bwd_kernel(
     const float *__restrict__ g_out, const float *__restrict__ vp, const float *__restrict__ val,
     const float *__restrict__ ret, const void *__restrict__ mask, int64_t B, int64_t R, float c,
-    int agg, const double *__restrict__ part, float *__restrict__ d_vp) {
+    int agg, int64_t seg_rows, const double *__restrict__ part, float *__restrict__ d_vp) {
   const int64_t b = blockIdx.y;
+  const float *gs = g_out;  // this row's segment's upstream gradients
+  double n_tot;
+  int64_t Bs = B;
+  if (seg_rows > 0) {  // uniform per workgroup, before any exit (see ppo_loss_bwd_kernel)
+    const int64_t s = b / seg_rows;
+    const int64_t b0 = s * seg_rows, b1 = b0 + seg_rows < B ? b0 + seg_rows : B;
+    n_tot = __shfl(seg_slot_sum(part, b0, b1, agg, 0u), 0, kWave);
+    Bs = b1 - b0;
+    if (gs) gs += s * VA_VLOSS_NOUT;
+  } else {
+    n_tot = part[B * kNQ + 0];
+  }
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= R) return;
   const int64_t i = b * R + t;
   // vf_loss = 0.5 * agg(.)  ->  d agg = 0.5 * g ;  vpred_mean = masked_mean(vp)
-  const float g_loss = g_out ? g_out[VA_VLOSS_LOSS] * 0.5f : 0.f;
-  const float g_mean = g_out ? g_out[VA_VLOSS_VPRED_MEAN] : 0.f;
+  const float g_loss = gs ? gs[VA_VLOSS_LOSS] * 0.5f : 0.f;
+  const float g_mean = gs ? gs[VA_VLOSS_VPRED_MEAN] : 0.f;
   const double n_b = part[b * kNQ + 0];
-  const double n_tot = part[B * kNQ + 0];
   const float m = load_mask<MT>(mask, i);
   const bool mb = (m != 0.f);
   const float keep = (agg != VA_AGG_TOKEN_MEAN || mb) ? 1.f : 0.f;
-  const float w = agg_weight(agg, g_loss, m, n_b, n_tot, B, R) * keep;
+  const float w = agg_weight(agg, g_loss, m, n_b, n_tot, Bs, R) * keep;
   float g = value_dvp(w, vp[i], val[i], ret[i], c);
   g += (g_mean / static_cast<float>(n_tot + 1e-8)) * m * (mb ? 1.f : 0.f);
   d_vp[i] = g;
@@ -858,8 +964,9 @@ extern "C" int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float
                                const float *entropy, int64_t B, int64_t R, float clip_lo,
                                float clip_hi, float clip_c, int agg_mode, int kl_type,
                                int loss_mode, const uint8_t *sel, float mode_coef,
-                               float *out, void *workspace, void *stream) {
+                               int64_t seg_rows, float *out, void *workspace, void *stream) {
   VA_CHECK_ARG(B > 0 && R > 0, "empty batch (B=%lld, R=%lld)", (long long)B, (long long)R);
+  VA_CHECK_ARG(seg_rows >= 0, "seg_rows must be >= 0");
   VA_CHECK_ARG(B < (1ll << 31), "B too large");
   VA_CHECK_ARG(old_lp && lp && adv && mask && out && workspace, "null pointer argument");
   VA_CHECK_ARG(kl_type == VA_KL_NONE || ref_lp != nullptr, "ref_lp required for kl_type %d",
@@ -909,6 +1016,12 @@ extern "C" int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float
                          loss_mode, mode_coef, part, wsum);
     }));
   }
+  if (seg_rows > 0 && seg_rows < B) {  // several loss micro-batches: one finalize workgroup each
+    const int64_t S = (B + seg_rows - 1) / seg_rows;
+    hipLaunchKernelGGL(ppo_loss_seg_finalize_kernel, dim3(static_cast<unsigned>(S)), dim3(64), 0, s, part, B, R,
+                       seg_rows, agg_mode, kl_type != VA_KL_NONE ? 1 : 0, entropy != nullptr ? 1 : 0, out);
+    return check_launch("ppo_loss_fwd");
+  }
   hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(finalize_threads(G)), 0, s, wsum, G, B, R, agg_mode,
                      kl_type != VA_KL_NONE ? 1 : 0, entropy != nullptr ? 1 : 0, part + B * kNQ,
                      out);
@@ -920,9 +1033,11 @@ extern "C" int va_ppo_loss_bwd(const float *g_out, const float *old_lp, const fl
                                const float *ref_lp, int64_t B, int64_t R, float clip_lo,
                                float clip_hi, float clip_c, int agg_mode, int kl_type,
                                int loss_mode, const uint8_t *sel, float mode_coef,
-                               const void *workspace, float *d_lp, float *d_entropy,
+                               int64_t seg_rows, const void *workspace, float *d_lp, float *d_entropy,
                                void *stream) {
   VA_CHECK_ARG(B > 0 && R > 0, "empty batch");
+  VA_CHECK_ARG(seg_rows >= 0, "seg_rows must be >= 0");
+  if (seg_rows >= B) seg_rows = 0;  // one segment: the batch totals
   VA_CHECK_ARG(B < 65536, "B must be < 65536 for the 2-D backward grid");
   VA_CHECK_ARG(old_lp && lp && adv && mask && workspace && d_lp, "null pointer argument");
   VA_CHECK_ARG(kl_type == VA_KL_NONE || ref_lp != nullptr, "ref_lp required");
@@ -934,7 +1049,7 @@ extern "C" int va_ppo_loss_bwd(const float *g_out, const float *old_lp, const fl
   VA_DISPATCH_MASK(mask_dtype, VA_DISPATCH_KL(kl_type, {
     hipLaunchKernelGGL((ppo_loss_bwd_kernel<MT, KL>), grid, dim3(256), 0, s, g_out, old_lp, lp,
                        adv, mask, ref_lp, sel, B, R, clip_lo, clip_hi, clip_c, agg_mode, loss_mode,
-                       mode_coef, part, d_lp, d_entropy);
+                       mode_coef, seg_rows, part, d_lp, d_entropy);
   }));
   return check_launch("ppo_loss_bwd");
 }
@@ -1029,9 +1144,10 @@ extern "C" int va_apply_kl_penalty(const float *scores, const float *old_lp, con
 
 extern "C" int va_value_loss_fwd(const float *vpreds, const float *values, const float *returns,
                                  const void *mask, int mask_dtype, int64_t B, int64_t R,
-                                 float cliprange_value, int agg_mode, float *out, void *workspace,
-                                 void *stream) {
+                                 float cliprange_value, int agg_mode, int64_t seg_rows, float *out,
+                                 void *workspace, void *stream) {
   VA_CHECK_ARG(B > 0 && R > 0, "empty batch (B=%lld, R=%lld)", (long long)B, (long long)R);
+  VA_CHECK_ARG(seg_rows >= 0, "seg_rows must be >= 0");
   VA_CHECK_ARG(B < (1ll << 31), "B too large");
   VA_CHECK_ARG(vpreds && values && returns && mask && out && workspace, "null pointer argument");
   if (int e = check_agg(agg_mode, false)) return e;
@@ -1057,6 +1173,11 @@ extern "C" int va_value_loss_fwd(const float *vpreds, const float *values, const
                          returns, mask, R, cliprange_value, agg_mode, part, wsum);
     });
   }
+  if (seg_rows > 0 && seg_rows < B) {  // several loss micro-batches: one finalize workgroup each
+    hipLaunchKernelGGL(value_loss_seg_finalize_kernel, dim3(static_cast<unsigned>((B + seg_rows - 1) / seg_rows)),
+                       dim3(64), 0, s, part, B, R, seg_rows, agg_mode, out);
+    return check_launch("value_loss_fwd");
+  }
   hipLaunchKernelGGL(value_loss_finalize_kernel, dim3(1), dim3(finalize_threads(G)), 0, s, wsum, G, B, R, agg_mode,
                      part + B * kNQ, out);
   return check_launch("value_loss_fwd");
@@ -1064,16 +1185,18 @@ extern "C" int va_value_loss_fwd(const float *vpreds, const float *values, const
 
 extern "C" int va_value_loss_bwd(const float *g_out, const float *vpreds, const float *values,
                                  const float *returns, const void *mask, int mask_dtype, int64_t B,
-                                 int64_t R, float cliprange_value, int agg_mode,
+                                 int64_t R, float cliprange_value, int agg_mode, int64_t seg_rows,
                                  const void *workspace, float *d_vpreds, void *stream) {
   VA_CHECK_ARG(B > 0 && R > 0 && B < 65536, "bad shape");
+  VA_CHECK_ARG(seg_rows >= 0, "seg_rows must be >= 0");
+  if (seg_rows >= B) seg_rows = 0;
   VA_CHECK_ARG(vpreds && values && returns && mask && workspace && d_vpreds, "null pointer argument");
   if (int e = check_agg(agg_mode, false)) return e;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid(static_cast<unsigned>((R + 255) / 256), static_cast<unsigned>(B));
   VA_DISPATCH_MASK(mask_dtype, {
     hipLaunchKernelGGL((value_loss_bwd_kernel<MT>), grid, dim3(256), 0, s, g_out, vpreds, values,
-                       returns, mask, B, R, cliprange_value, agg_mode,
+                       returns, mask, B, R, cliprange_value, agg_mode, seg_rows,
                        static_cast<const double *>(workspace), d_vpreds);
   });
   return check_launch("value_loss_bwd");

@@ -167,66 +167,80 @@ def _loss_ws(B: int, device) -> tuple[Tensor, Tensor]:
     return buf, buf[: B * 8 + 8]
 
 
+def _loss_out_shape(B: int, seg_rows: int) -> tuple:
+    """[VA_LOSS_NOUT] for one aggregated batch; [S, VA_LOSS_NOUT] for S = ceil(B / seg_rows) loss
+    micro-batches (0 < seg_rows < B)."""
+    if 0 < seg_rows < B:
+        return (-(-B // seg_rows), L.VA_LOSS_NOUT)
+    return (L.VA_LOSS_NOUT,)
+
+
 @_op("ppo_loss_fwd")
 def ppo_loss_fwd(old_lp: Tensor, lp: Tensor, adv: Tensor, mask: Tensor, ref_lp: Optional[Tensor],
                  entropy: Optional[Tensor], sel: Optional[Tensor], clip_lo: float, clip_hi: float, clip_c: float,
-                 agg_mode: int, kl_type: int, loss_mode: int, mode_coef: float) -> tuple[Tensor, Tensor]:
-    """(out[8] fp32 = VA_LOSS_* slots, row-partials workspace fp64) of the fused policy loss."""
+                 agg_mode: int, kl_type: int, loss_mode: int, mode_coef: float,
+                 seg_rows: int = 0) -> tuple[Tensor, Tensor]:
+    """(out fp32 = VA_LOSS_* slots, [8] or [S, 8] per loss micro-batch of seg_rows rows; row-partials
+    workspace fp64) of the fused policy loss."""
     _check_f32(old_lp, lp, adv, ref_lp, entropy)
     B, R = _rows(lp)
     if sel is not None and (sel.dtype != torch.uint8 or not sel.is_contiguous()):
         raise TypeError("ppo_loss_fwd: sel must be contiguous uint8")
-    out = torch.empty(L.VA_LOSS_NOUT, dtype=_F32, device=lp.device)
+    out = torch.empty(_loss_out_shape(B, seg_rows), dtype=_F32, device=lp.device)
     buf, ws = _loss_ws(B, lp.device)
     L.call("va_ppo_loss_fwd", K._p(old_lp), K._p(lp), K._p(adv), K._p(mask), _mcode(mask), K._p(ref_lp),
            K._p(entropy), B, R, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode, K._p(sel), mode_coef,
-           K._p(out), K._p(buf), K._stream(lp))
+           seg_rows, K._p(out), K._p(buf), K._stream(lp))
     return out, ws
 
 
 @ppo_loss_fwd.register_fake
-def _(old_lp, lp, adv, mask, ref_lp, entropy, sel, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode, mode_coef):
+def _(old_lp, lp, adv, mask, ref_lp, entropy, sel, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode, mode_coef,
+      seg_rows=0):
     B = lp.numel() // lp.shape[-1] if lp.dim() > 1 else 1
-    return lp.new_empty(L.VA_LOSS_NOUT, dtype=_F32), lp.new_empty(B * 8 + 8, dtype=_F64)
+    return lp.new_empty(_loss_out_shape(B, seg_rows), dtype=_F32), lp.new_empty(B * 8 + 8, dtype=_F64)
 
 
 @_op("ppo_loss_bwd")
 def ppo_loss_bwd(g_out: Tensor, old_lp: Tensor, lp: Tensor, adv: Tensor, mask: Tensor, ref_lp: Optional[Tensor],
                  sel: Optional[Tensor], ws: Tensor, clip_lo: float, clip_hi: float, clip_c: float, agg_mode: int,
-                 kl_type: int, loss_mode: int, mode_coef: float, need_entropy: bool) -> tuple[Tensor, Tensor]:
+                 kl_type: int, loss_mode: int, mode_coef: float, need_entropy: bool,
+                 seg_rows: int = 0) -> tuple[Tensor, Tensor]:
     """(d_lp [B, R] fp32, d_entropy [B, R] fp32 or [0] when not needed)."""
     _check_f32(g_out, old_lp, lp, adv, ref_lp)
     B, R = _rows(lp)
+    if g_out.shape != _loss_out_shape(B, seg_rows):
+        raise ValueError(f"ppo_loss_bwd: g_out shape {tuple(g_out.shape)} != {_loss_out_shape(B, seg_rows)}")
     d_lp = torch.empty(lp.shape, dtype=_F32, device=lp.device)
     d_ent = torch.empty(lp.shape if need_entropy else (0,), dtype=_F32, device=lp.device)
     L.call("va_ppo_loss_bwd", K._p(g_out), K._p(old_lp), K._p(lp), K._p(adv), K._p(mask), _mcode(mask), K._p(ref_lp),
-           B, R, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode, K._p(sel), mode_coef, K._p(ws), K._p(d_lp),
-           K._p(d_ent) if need_entropy else None, K._stream(lp))
+           B, R, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode, K._p(sel), mode_coef, seg_rows, K._p(ws),
+           K._p(d_lp), K._p(d_ent) if need_entropy else None, K._stream(lp))
     return d_lp, d_ent
 
 
 @ppo_loss_bwd.register_fake
 def _(g_out, old_lp, lp, adv, mask, ref_lp, sel, ws, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode,
-      mode_coef, need_entropy):
+      mode_coef, need_entropy, seg_rows=0):
     return lp.new_empty(lp.shape), lp.new_empty(lp.shape if need_entropy else (0,))
 
 
 def _loss_setup(ctx, inputs, output):
-    old_lp, lp, adv, mask, ref_lp, entropy, sel, clip_lo, clip_hi, clip_c, agg, kl, mode, coef = inputs
+    old_lp, lp, adv, mask, ref_lp, entropy, sel, clip_lo, clip_hi, clip_c, agg, kl, mode, coef, seg_rows = inputs
     _, ws = output
     ctx.mark_non_differentiable(ws)
     ctx.save_for_backward(old_lp, lp, adv, mask, ref_lp, sel, ws)
-    ctx.cfg = (clip_lo, clip_hi, clip_c, agg, kl, mode, coef, entropy is not None)
+    ctx.cfg = (clip_lo, clip_hi, clip_c, agg, kl, mode, coef, entropy is not None, seg_rows)
 
 
 def _loss_backward(ctx, g_out, g_ws):
     old_lp, lp, adv, mask, ref_lp, sel, ws = ctx.saved_tensors
-    clip_lo, clip_hi, clip_c, agg, kl, mode, coef, has_ent = ctx.cfg
+    clip_lo, clip_hi, clip_c, agg, kl, mode, coef, has_ent, seg_rows = ctx.cfg
     need_ent = has_ent and ctx.needs_input_grad[5]
     d_lp, d_ent = torch.ops.verl_amd.ppo_loss_bwd(g_out.float().contiguous(), old_lp, lp, adv, mask, ref_lp, sel, ws,
-                                                  clip_lo, clip_hi, clip_c, agg, kl, mode, coef, need_ent)
+                                                  clip_lo, clip_hi, clip_c, agg, kl, mode, coef, need_ent, seg_rows)
     return (None, d_lp if ctx.needs_input_grad[1] else None, None, None, None, d_ent if need_ent else None,
-            None, None, None, None, None, None, None, None)
+            None, None, None, None, None, None, None, None, None)
 
 
 ppo_loss_fwd.register_autograd(_loss_backward, setup_context=_loss_setup)
@@ -526,52 +540,62 @@ def _(rewards, mask, gamma, mode, baselines):
 
 
 # =============================================================================== value loss (critic)
+def _vloss_out_shape(B: int, seg_rows: int) -> tuple:
+    if 0 < seg_rows < B:
+        return (-(-B // seg_rows), L.VA_VLOSS_NOUT)
+    return (L.VA_VLOSS_NOUT,)
+
+
 @_op("value_loss_fwd")
 def value_loss_fwd(vpreds: Tensor, values: Tensor, returns: Tensor, mask: Tensor, cliprange_value: float,
-                   agg_mode: int) -> tuple[Tensor, Tensor]:
+                   agg_mode: int, seg_rows: int = 0) -> tuple[Tensor, Tensor]:
+    """(out fp32 = VA_VLOSS_* slots, [4] or [S, 4] per loss micro-batch of seg_rows rows; workspace)."""
     _check_f32(vpreds, values, returns)
     B, R = _rows(vpreds)
-    out = torch.empty(L.VA_VLOSS_NOUT, dtype=_F32, device=vpreds.device)
+    out = torch.empty(_vloss_out_shape(B, seg_rows), dtype=_F32, device=vpreds.device)
     buf, ws = _loss_ws(B, vpreds.device)
     L.call("va_value_loss_fwd", K._p(vpreds), K._p(values), K._p(returns), K._p(mask), _mcode(mask), B, R,
-           cliprange_value, agg_mode, K._p(out), K._p(buf), K._stream(vpreds))
+           cliprange_value, agg_mode, seg_rows, K._p(out), K._p(buf), K._stream(vpreds))
     return out, ws
 
 
 @value_loss_fwd.register_fake
-def _(vpreds, values, returns, mask, cliprange_value, agg_mode):
+def _(vpreds, values, returns, mask, cliprange_value, agg_mode, seg_rows=0):
     B = vpreds.numel() // vpreds.shape[-1] if vpreds.dim() > 1 else 1
-    return vpreds.new_empty(L.VA_VLOSS_NOUT, dtype=_F32), vpreds.new_empty(B * 8 + 8, dtype=_F64)
+    return vpreds.new_empty(_vloss_out_shape(B, seg_rows), dtype=_F32), vpreds.new_empty(B * 8 + 8, dtype=_F64)
 
 
 @_op("value_loss_bwd")
 def value_loss_bwd(g_out: Tensor, vpreds: Tensor, values: Tensor, returns: Tensor, mask: Tensor, ws: Tensor,
-                   cliprange_value: float, agg_mode: int) -> Tensor:
+                   cliprange_value: float, agg_mode: int, seg_rows: int = 0) -> Tensor:
     _check_f32(g_out, vpreds, values, returns)
     B, R = _rows(vpreds)
+    if g_out.shape != _vloss_out_shape(B, seg_rows):
+        raise ValueError(f"value_loss_bwd: g_out shape {tuple(g_out.shape)} != {_vloss_out_shape(B, seg_rows)}")
     d = torch.empty_like(vpreds)
     L.call("va_value_loss_bwd", K._p(g_out), K._p(vpreds), K._p(values), K._p(returns), K._p(mask), _mcode(mask), B,
-           R, cliprange_value, agg_mode, K._p(ws), K._p(d), K._stream(vpreds))
+           R, cliprange_value, agg_mode, seg_rows, K._p(ws), K._p(d), K._stream(vpreds))
     return d
 
 
 @value_loss_bwd.register_fake
-def _(g_out, vpreds, values, returns, mask, ws, cliprange_value, agg_mode):
+def _(g_out, vpreds, values, returns, mask, ws, cliprange_value, agg_mode, seg_rows=0):
     return torch.empty_like(vpreds)
 
 
 def _vloss_setup(ctx, inputs, output):
-    vpreds, values, returns, mask, c, agg = inputs
+    vpreds, values, returns, mask, c, agg, seg_rows = inputs
     ctx.mark_non_differentiable(output[1])
     ctx.save_for_backward(vpreds, values, returns, mask, output[1])
-    ctx.cfg = (c, agg)
+    ctx.cfg = (c, agg, seg_rows)
 
 
 def _vloss_backward(ctx, g_out, g_ws):
     vpreds, values, returns, mask, ws = ctx.saved_tensors
-    c, agg = ctx.cfg
-    d = torch.ops.verl_amd.value_loss_bwd(g_out.float().contiguous(), vpreds, values, returns, mask, ws, c, agg)
-    return d, None, None, None, None, None
+    c, agg, seg_rows = ctx.cfg
+    d = torch.ops.verl_amd.value_loss_bwd(g_out.float().contiguous(), vpreds, values, returns, mask, ws, c, agg,
+                                          seg_rows)
+    return d, None, None, None, None, None, None
 
 
 value_loss_fwd.register_autograd(_vloss_backward, setup_context=_vloss_setup)

@@ -60,6 +60,8 @@ def actor_config(**overrides) -> AttrDict:
         use_remove_padding=True,
         use_fused_kernels=False,
         fused_logprob_no_grad=False,
+        # (verl_amd) responses per update forward/backward pass; None = ppo_micro_batch_size_per_gpu
+        compute_micro_batch_size_per_gpu=None,
         optim=AttrDict(lr=1e-6, weight_decay=0.01, betas=(0.9, 0.999), lr_warmup_steps=-1, lr_warmup_steps_ratio=0.0,
                        min_lr_ratio=0.0, num_cycles=0.5, warmup_style="constant", total_training_steps=-1),
     )
@@ -88,6 +90,8 @@ def critic_config(**overrides) -> AttrDict:
         loss_agg_mode="token-mean",
         grad_clip=1.0,
         ulysses_sequence_parallel_size=1,
+        # (verl_amd) responses per update forward/backward pass; None = ppo_micro_batch_size_per_gpu
+        compute_micro_batch_size_per_gpu=None,
         model=AttrDict(use_remove_padding=False, enable_gradient_checkpointing=True),
         optim=AttrDict(lr=1e-5, weight_decay=0.01, betas=(0.9, 0.999), lr_warmup_steps_ratio=0.0, min_lr_ratio=None,
                        warmup_style="constant", total_training_steps=-1),

@@ -228,6 +228,24 @@ class DataParallelPPOActor(BasePPOActor):
             from ...utils.gemm_tuning import use_tuned_gemms
 
             use_tuned_gemms(gemm_table)
+        # rows per forward / backward pass of update_policy (None: ppo_micro_batch_size_per_gpu, the
+        # reference). A multiple of ppo_micro_batch_size_per_gpu runs that many of the reference's
+        # loss micro-batches in ONE pass: the fused loss kernel aggregates each micro-batch of
+        # ppo_micro_batch_size_per_gpu rows on its own (seg_rows), so the loss, its gradient and the
+        # per-micro-batch metric lists are the reference's (dp_actor.py:388-483) while the model
+        # GEMMs see the larger token count.
+        self.compute_micro_batch_size = self.config.get("compute_micro_batch_size_per_gpu", None)
+
+    def _pass_rows(self, loss_mode: str) -> int:
+        """Rows per update pass: compute_micro_batch_size_per_gpu rounded down to a multiple of
+        ppo_micro_batch_size_per_gpu, where the fused vanilla loss can aggregate per micro-batch;
+        the reference's micro-batch otherwise (registered loss variants draw their token selection
+        per micro-batch, so they keep it)."""
+        mb = int(self.config.ppo_micro_batch_size_per_gpu)
+        cmb = self.compute_micro_batch_size
+        if not cmb or loss_mode != "vanilla" or int(cmb) <= mb:
+            return mb
+        return int(cmb) // mb * mb
 
     # ------------------------------------------------------------------ forward
     def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False, packing: _Packing = None,
@@ -429,7 +447,8 @@ class DataParallelPPOActor(BasePPOActor):
                     micro_batches, idx_lists = prepare_dynamic_batch(mini, max_token_len=max_token_len)
                     plans = self._plans(mini, idx_lists=idx_lists, am=am)
                 else:
-                    micro_batches = mini.split(cfg.ppo_micro_batch_size_per_gpu)
+                    seg_mb = int(cfg.ppo_micro_batch_size_per_gpu)
+                    micro_batches = mini.split(self._pass_rows(loss_mode))
                     plans = self._plans(mini, [len(m) for m in micro_batches], am=am)
                 self._zero_grad()
                 for i, (mb, plan) in enumerate(zip(micro_batches, plans, strict=True)):
@@ -438,20 +457,23 @@ class DataParallelPPOActor(BasePPOActor):
                     calc_ent = entropy_coeff != 0
                     entropy, log_prob = self._forward_micro_batch(b, temperature, calc_ent, plan, _multi_modal(mb))
                     m = {}
+                    # several of the reference's loss micro-batches in this pass: aggregated one by one
+                    seg = seg_mb if not cfg.use_dynamic_bsz and len(mb) > seg_mb else 0
                     if loss_mode == "vanilla":
                         out = core_algos.compute_actor_loss(
                             b["old_log_probs"], log_prob, b["advantages"], response_mask, clip_low, clip_high,
                             clip_c, agg_mode, entropy=entropy if calc_ent else None,
                             ref_log_prob=b["ref_log_prob"] if cfg.use_kl_loss else None,
-                            kl_loss_type=cfg.kl_loss_type if cfg.use_kl_loss else None,
+                            kl_loss_type=cfg.kl_loss_type if cfg.use_kl_loss else None, seg_rows=seg,
                         )
-                        pg_loss, pg_clipfrac = out[L.VA_LOSS_PG], out[L.VA_LOSS_CLIPFRAC]
-                        ppo_kl, pg_clipfrac_lower = out[L.VA_LOSS_PPO_KL], out[L.VA_LOSS_CLIPFRAC_LOWER]
+                        # [8] or [S, 8]: the slots below are scalars or one value per loss micro-batch
+                        pg_loss, pg_clipfrac = out[..., L.VA_LOSS_PG], out[..., L.VA_LOSS_CLIPFRAC]
+                        ppo_kl, pg_clipfrac_lower = out[..., L.VA_LOSS_PPO_KL], out[..., L.VA_LOSS_CLIPFRAC_LOWER]
                         policy_loss = pg_loss
                         if calc_ent:
-                            policy_loss = pg_loss - out[L.VA_LOSS_ENTROPY] * entropy_coeff
+                            policy_loss = pg_loss - out[..., L.VA_LOSS_ENTROPY] * entropy_coeff
                         if cfg.use_kl_loss:
-                            kl_loss = out[L.VA_LOSS_KL]
+                            kl_loss = out[..., L.VA_LOSS_KL]
                             policy_loss = policy_loss + kl_loss * cfg.kl_loss_coef
                             m["actor/kl_loss"] = kl_loss.detach()
                             m["actor/kl_coef"] = cfg.kl_loss_coef
@@ -472,6 +494,10 @@ class DataParallelPPOActor(BasePPOActor):
                     if cfg.use_dynamic_bsz:
                         # relative to the dynamic bsz (dp_actor.py:465-467)
                         loss = policy_loss * (response_mask.shape[0] / cfg.ppo_mini_batch_size)
+                    elif seg:
+                        # sum over the pass's micro-batches of policy_loss / gradient_accumulation: the
+                        # gradient the reference accumulates over their separate backward passes
+                        loss = (policy_loss / self.gradient_accumulation).sum()
                     else:
                         loss = policy_loss / self.gradient_accumulation
                     last = i == len(micro_batches) - 1
@@ -491,7 +517,12 @@ class DataParallelPPOActor(BasePPOActor):
                         "actor/ppo_kl": ppo_kl.detach(),
                         "actor/pg_clipfrac_lower": pg_clipfrac_lower.detach(),
                     })
-                    append_to_dict(dev_metrics, m)
+                    if seg:  # one metric entry per loss micro-batch, in order, as the reference appends
+                        for k in range(pg_loss.shape[0]):
+                            append_to_dict(dev_metrics, {
+                                key: (v[k] if isinstance(v, torch.Tensor) else v) for key, v in m.items()})
+                    else:
+                        append_to_dict(dev_metrics, m)
                 grad_norm = self._optimizer_step()
                 append_to_dict(dev_metrics, {"actor/grad_norm": grad_norm.detach()})
         self._zero_grad()

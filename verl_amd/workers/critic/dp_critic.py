@@ -61,6 +61,14 @@ class DataParallelPPOCritic(BasePPOCritic):
             from ...utils.gemm_tuning import use_tuned_gemms
 
             use_tuned_gemms(self.config.gemm_tuning_file)
+        # as the actor: rows per update pass, a multiple of ppo_micro_batch_size_per_gpu whose loss
+        # micro-batches the fused value loss aggregates one by one (None: the reference's micro-batch)
+        self.compute_micro_batch_size = self.config.get("compute_micro_batch_size_per_gpu", None)
+
+    def _pass_rows(self) -> int:
+        mb = int(self.config.ppo_micro_batch_size_per_gpu)
+        cmb = self.compute_micro_batch_size
+        return int(cmb) // mb * mb if cmb and int(cmb) > mb else mb
 
     # ------------------------------------------------------------------ forward
     def _forward_micro_batch(self, micro_batch, packing=None, multi_modal_inputs=None) -> torch.Tensor:
@@ -177,18 +185,23 @@ class DataParallelPPOCritic(BasePPOCritic):
                     plans = self._plans(mini, idx_lists=idx_lists)
                 else:
                     self.gradient_accumulation = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
-                    micro_batches = mini.split(cfg.ppo_micro_batch_size_per_gpu)
+                    micro_batches = mini.split(self._pass_rows())
                     plans = self._plans(mini, [len(m) for m in micro_batches])
                 self._zero_grad()
                 for i, (mb, plan) in enumerate(zip(micro_batches, plans, strict=True)):
                     b = mb.batch
                     response_mask = b["response_mask"]
                     vpreds = self._forward_micro_batch(b, plan, _multi_modal(mb))
+                    # several of the reference's loss micro-batches in this pass: aggregated one by one
+                    seg = (int(cfg.ppo_micro_batch_size_per_gpu)
+                           if not cfg.use_dynamic_bsz and len(mb) > int(cfg.ppo_micro_batch_size_per_gpu) else 0)
                     out = K.fused_value_loss(vpreds, b["values"], b["returns"], response_mask, cfg.cliprange_value,
-                                             cfg.loss_agg_mode)
-                    vf_loss = out[L.VA_VLOSS_LOSS]
+                                             cfg.loss_agg_mode, seg_rows=seg)
+                    vf_loss = out[..., L.VA_VLOSS_LOSS]  # scalar, or one value per loss micro-batch
                     if cfg.use_dynamic_bsz:
                         loss = vf_loss * (response_mask.shape[0] / cfg.ppo_mini_batch_size)
+                    elif seg:
+                        loss = (vf_loss / self.gradient_accumulation).sum()
                     else:
                         loss = vf_loss / self.gradient_accumulation
                     if i == len(micro_batches) - 1 and self.grad_reducer is not None:
@@ -196,11 +209,13 @@ class DataParallelPPOCritic(BasePPOCritic):
                     loss.backward()
                     if self.grad_reducer is not None:
                         self.grad_reducer.after_backward()
-                    append_to_dict(dev_metrics, {
-                        "critic/vf_loss": vf_loss.detach(),
-                        "critic/vf_clipfrac": out[L.VA_VLOSS_CLIPFRAC].detach(),
-                        "critic/vpred_mean": out[L.VA_VLOSS_VPRED_MEAN].detach(),
-                    })
+                    met = out.detach()
+                    for row in (met if seg else [met]):  # one metric entry per loss micro-batch, in order
+                        append_to_dict(dev_metrics, {
+                            "critic/vf_loss": row[L.VA_VLOSS_LOSS],
+                            "critic/vf_clipfrac": row[L.VA_VLOSS_CLIPFRAC],
+                            "critic/vpred_mean": row[L.VA_VLOSS_VPRED_MEAN],
+                        })
                 grad_norm = self._optimizer_step()
                 append_to_dict(dev_metrics, {"critic/grad_norm": grad_norm.detach()})
         self._zero_grad()
