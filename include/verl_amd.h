@@ -203,9 +203,10 @@ int va_set_tuning(int key, int value);
  *   token and row counts: the reference's agg_loss per micro-batch, dp_actor.py:419-470), into
  *   out[S][VA_LOSS_NOUT].
  *   out fp32 (device). workspace: va_ppo_loss_workspace_bytes(B) = 8 (16 B + 8):
- *   [B, 8] fp64 row partials, 8 fp64 totals (n first), then up to B per-workgroup aggregated
- *   vectors that only the forward reads. The first 8 B + 8 doubles are what the backward reads:
- *   keep them alive between the forward and the backward of the same micro-batch. */
+ *   [B, 8] fp64 row partials, 8 fp64 totals (n first; zeros with segments), then up to B per-workgroup aggregated
+ *   vectors that only the forward reads, whose first S slots the segmented forward overwrites with
+ *   the segments' token counts. The first 8 B + 8 doubles (+ S with segments) are what the backward
+ *   reads: keep them alive between the forward and the backward of the same micro-batch. */
 int64_t va_ppo_loss_workspace_bytes(int64_t B);
 int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float *adv, const void *mask,
                     int mask_dtype, const float *ref_lp, const float *entropy, int64_t B,

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--gae-variant", type=int, default=0)
     ap.add_argument("--gae-partials", type=int, default=0)
     ap.add_argument("--gae-nt", type=int, default=3)
+    ap.add_argument("--seg-rows", type=int, default=0, help="policy / value loss micro-batch segments (seg_rows)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     L.call("va_set_tuning", L.VA_TUNE_GAE_VARIANT, args.gae_variant)
@@ -70,14 +71,15 @@ def main():
         old = -torch.rand(B, R, device=dev, generator=g)
         lp = old + 0.05 * torch.randn(B, R, device=dev, generator=g)
         ref = old + 0.1 * torch.randn(B, R, device=dev, generator=g)
-        lout = torch.empty(8, device=dev)
+        nseg = -(-B // args.seg_rows) if 0 < args.seg_rows < B else 1  # output rows (loss micro-batches)
+        lout = torch.empty(nseg * 8, device=dev)
         lws = torch.zeros(L.load().va_ppo_loss_workspace_bytes(B) // 8, dtype=torch.float64, device=dev)
-        vout = torch.empty(8, device=dev)
+        vout = torch.empty(nseg * 8, device=dev)
         aout = torch.empty(1, device=dev)
         vgrad = torch.empty(B, R, device=dev)
-        gout = torch.zeros(8, device=dev)
-        gout[0] = 1.0
-        gout[4] = 0.001
+        gout = torch.zeros(nseg, 8, device=dev)
+        gout[:, 0] = 1.0
+        gout[:, 4] = 0.001
         dlp = torch.empty(B, R, device=dev)
 
         def gae():
@@ -90,15 +92,15 @@ def main():
 
         def loss():
             L.call("va_ppo_loss_fwd", K._p(old), K._p(lp), K._p(adv), K._p(mask), L.VA_MASK_I64, K._p(ref), None, B, R,
-                   0.8, 1.2, 3.0, 0, L.VA_KL_K3, 0, None, 0.0, 0, K._p(lout), K._p(lws), s)
+                   0.8, 1.2, 3.0, 0, L.VA_KL_K3, 0, None, 0.0, args.seg_rows, K._p(lout), K._p(lws), s)
             L.call("va_ppo_loss_bwd", K._p(gout), K._p(old), K._p(lp), K._p(adv), K._p(mask), L.VA_MASK_I64, K._p(ref),
-                   B, R, 0.8, 1.2, 3.0, 0, L.VA_KL_K3, 0, None, 0.0, 0, K._p(lws), K._p(dlp), None, s)
+                   B, R, 0.8, 1.2, 3.0, 0, L.VA_KL_K3, 0, None, 0.0, args.seg_rows, K._p(lws), K._p(dlp), None, s)
 
         def vloss():  # critic: vpreds = values + noise, returns = ret of the GAE call
-            L.call("va_value_loss_fwd", K._p(lp), K._p(old), K._p(ref), K._p(mask), L.VA_MASK_I64, B, R, 0.5, 0, 0,
+            L.call("va_value_loss_fwd", K._p(lp), K._p(old), K._p(ref), K._p(mask), L.VA_MASK_I64, B, R, 0.5, 0, args.seg_rows,
                    K._p(vout), K._p(lws), s)
             L.call("va_value_loss_bwd", K._p(gout), K._p(lp), K._p(old), K._p(ref), K._p(mask), L.VA_MASK_I64, B, R,
-                   0.5, 0, 0, K._p(lws), K._p(vgrad), s)
+                   0.5, 0, args.seg_rows, K._p(lws), K._p(vgrad), s)
 
         def agg():  # agg_loss(entropy, mask, token-mean): the actor/entropy metric
             L.call("va_masked_agg_fwd", K._p(lp), K._p(mask), L.VA_MASK_I64, B, R, 0, K._p(aout), K._p(lws), s)
@@ -117,7 +119,8 @@ def main():
             torch.cuda.synchronize()
             us = 1e3 * e0.elapsed_time(e1) / args.iters
             rec = {"op": name, "B": B, "R": R, "wall_us_per_call": round(us, 2), "gae_variant": args.gae_variant,
-                   "gae_partials": args.gae_partials, "gae_nt": args.gae_nt, "loss_vec": args.loss_vec}
+                   "gae_partials": args.gae_partials, "gae_nt": args.gae_nt, "loss_vec": args.loss_vec,
+                   "seg_rows": args.seg_rows}
             print(json.dumps(rec), flush=True)
             out.append(rec)
     L.call("va_set_tuning", L.VA_TUNE_GAE_VARIANT, 0)

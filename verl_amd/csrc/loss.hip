@@ -438,30 +438,38 @@ __global__ __launch_bounds__(1024) void ppo_loss_finalize_kernel(const double *_
 // segment s = rows [s * seg_rows, min(B, (s + 1) * seg_rows)) is aggregated on its own, exactly as
 // a separate call over those rows would (its own token count n_s, its own row count B_s).
 //
-// Slot q of one segment summed over its rows in a fixed order that both the forward's finalize and
-// the backward reproduce (so n_s is the same double in both): lane 8 k + q adds rows b0 + k, b0 + k
+// Slot q of one segment summed over its rows in a fixed order: lane 8 k + q adds rows b0 + k, b0 + k
 // + 8, ... in order, then the 8 k-partials meet by xor 8, 16, 32. Every lane of the wave returns
 // the segment sum of its slot q = lane & 7 (term slots aggregated per row with agg_term).
 __device__ __forceinline__ double seg_slot_sum(const double *__restrict__ part, int64_t b0, int64_t b1, int agg,
                                                unsigned term_mask) {
   const int lane = threadIdx.x & 63, q = lane & 7, k = lane >> 3;
   const bool term = (term_mask >> q) & 1u;
+  constexpr int kU = 4;  // rows per lane whose loads are in flight together (adds stay in row order)
   double acc = 0.0;
-  for (int64_t b = b0 + k; b < b1; b += 8) {
-    const double x = part[b * kNQ + q];
-    acc += term ? agg_term(agg, x, part[b * kNQ]) : x;
+  for (int64_t base = b0 + k; base < b1; base += 8 * kU) {
+    double x[kU], nb[kU];
+#pragma unroll
+    for (int i = 0; i < kU; ++i) {
+      const int64_t b = base + 8 * i;
+      x[i] = b < b1 ? part[b * kNQ + q] : 0.0;
+      nb[i] = b < b1 ? part[b * kNQ] : 1.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kU; ++i)
+      if (base + 8 * i < b1) acc += term ? agg_term(agg, x[i], nb[i]) : x[i];
   }
 #pragma unroll
   for (int o = 8; o < 64; o <<= 1) acc += __shfl_xor(acc, o, kWave);
   return acc;
 }
 
-// The batch totals slots after the row partials (every workspace slot the op returns is written):
-// n over all rows, then zeros. Segment workgroup 0 writes them.
-__device__ __forceinline__ void seg_write_totals(double *__restrict__ part, int64_t B, int agg) {
-  if (blockIdx.x != 0) return;
-  const double n = seg_slot_sum(part, 0, B, agg, 0u);
-  if (threadIdx.x < kTotals) part[B * kNQ + threadIdx.x] = threadIdx.x == 0 ? n : 0.0;
+// With segments the 8 batch totals slots after the row partials are zeros (segment workgroup 0
+// writes them, so every workspace slot the op returns is written) and segment s's token count n_s
+// goes to part[8 B + 8 + s], where the backward reads it (the forward's per-workgroup vectors that
+// lived there are consumed by then: the segmented finalize reads the row partials).
+__device__ __forceinline__ void seg_write_totals(double *__restrict__ part, int64_t B) {
+  if (blockIdx.x == 0 && threadIdx.x < kTotals) part[B * kNQ + threadIdx.x] = 0.0;
 }
 
 // One 64-thread workgroup per segment: out[s][VA_LOSS_NOUT] as the one-segment finalize writes it.
@@ -469,7 +477,7 @@ __global__ __launch_bounds__(64) void ppo_loss_seg_finalize_kernel(double *__res
                                                                    int64_t R, int64_t seg_rows, int agg,
                                                                    int has_kl, int has_ent,
                                                                    float *__restrict__ out) {
-  seg_write_totals(part, B, agg);
+  seg_write_totals(part, B);
   const int64_t s = blockIdx.x;
   const int64_t b0 = s * seg_rows, b1 = b0 + seg_rows < B ? b0 + seg_rows : B;
   const double x = seg_slot_sum(part, b0, b1, agg, (1u << 1) | (1u << 5) | (1u << 6));
@@ -480,6 +488,7 @@ __global__ __launch_bounds__(64) void ppo_loss_seg_finalize_kernel(double *__res
     const double n = v[0];
     const double den = n + 1e-8;
     const int64_t Bs = b1 - b0;
+    part[B * kNQ + kTotals + s] = n;
     float *o = out + s * VA_LOSS_NOUT;
     o[VA_LOSS_PG] = static_cast<float>(agg_finish(agg, v[1], n, Bs, R));
     o[VA_LOSS_CLIPFRAC] = static_cast<float>(v[2] / den);
@@ -506,10 +515,10 @@ __global__ __launch_bounds__(256) void ppo_loss_bwd_kernel(
   const float *gs = g_out;  // this row's segment's upstream gradients
   double n_tot;
   int64_t Bs = B;
-  if (seg_rows > 0) {  // uniform per workgroup; every wave computes the segment's n_s (before any exit)
+  if (seg_rows > 0) {  // uniform per workgroup: the segment's token count from the forward's finalize
     const int64_t s = b / seg_rows;
     const int64_t b0 = s * seg_rows, b1 = b0 + seg_rows < B ? b0 + seg_rows : B;
-    n_tot = __shfl(seg_slot_sum(part, b0, b1, agg, 0u), 0, kWave);
+    n_tot = part[B * kNQ + kTotals + s];
     Bs = b1 - b0;
     if (gs) gs += s * VA_LOSS_NOUT;
   } else {
@@ -850,7 +859,7 @@ __global__ __launch_bounds__(1024) void value_loss_finalize_kernel(const double 
 __global__ __launch_bounds__(64) void value_loss_seg_finalize_kernel(double *__restrict__ part, int64_t B,
                                                                      int64_t R, int64_t seg_rows, int agg,
                                                                      float *__restrict__ out) {
-  seg_write_totals(part, B, agg);
+  seg_write_totals(part, B);
   const int64_t s = blockIdx.x;
   const int64_t b0 = s * seg_rows, b1 = b0 + seg_rows < B ? b0 + seg_rows : B;
   const double x = seg_slot_sum(part, b0, b1, agg, 1u << 1);
@@ -860,6 +869,7 @@ __global__ __launch_bounds__(64) void value_loss_seg_finalize_kernel(double *__r
   if (threadIdx.x == 0) {
     const double n = v[0];
     const double den = n + 1e-8;
+    part[B * kNQ + kTotals + s] = n;
     float *o = out + s * VA_VLOSS_NOUT;
     o[VA_VLOSS_LOSS] = 0.5f * static_cast<float>(agg_finish(agg, v[1], n, b1 - b0, R));
     o[VA_VLOSS_CLIPFRAC] = static_cast<float>(v[2] / den);
@@ -877,10 +887,10 @@ __global__ __launch_bounds__(256) void value_loss_bwd_kernel(
   const float *gs = g_out;  // this row's segment's upstream gradients
   double n_tot;
   int64_t Bs = B;
-  if (seg_rows > 0) {  // uniform per workgroup, before any exit (see ppo_loss_bwd_kernel)
+  if (seg_rows > 0) {  // uniform per workgroup (see ppo_loss_bwd_kernel)
     const int64_t s = b / seg_rows;
     const int64_t b0 = s * seg_rows, b1 = b0 + seg_rows < B ? b0 + seg_rows : B;
-    n_tot = __shfl(seg_slot_sum(part, b0, b1, agg, 0u), 0, kWave);
+    n_tot = part[B * kNQ + kTotals + s];
     Bs = b1 - b0;
     if (gs) gs += s * VA_VLOSS_NOUT;
   } else {

@@ -159,12 +159,17 @@ logprob_entropy_fwd.register_autograd(_lp_backward, setup_context=_lp_setup)
 
 
 # =============================================================================== policy loss
-def _loss_ws(B: int, device) -> tuple[Tensor, Tensor]:
+def _loss_ws(B: int, device, n_seg: int = 0) -> tuple[Tensor, Tensor]:
     # va_ppo_loss_workspace_bytes(B) / 8 doubles (= va_agg_workspace_bytes): the op returns the
-    # leading B * 8 + 8 ([B, 8] row partials + 8 totals, every slot written by the forward; autograd
-    # saves it for the backward); the tail is the forward's own per-workgroup scratch
+    # leading B * 8 + 8 ([B, 8] row partials + 8 totals) + n_seg (the loss micro-batch segments'
+    # token counts), every slot written by the forward; autograd saves it for the backward. The
+    # tail is the forward's own per-workgroup scratch.
     buf = torch.empty(2 * B * 8 + 8, dtype=_F64, device=device)
-    return buf, buf[: B * 8 + 8]
+    return buf, buf[: B * 8 + 8 + n_seg]
+
+
+def _n_seg(B: int, seg_rows: int) -> int:
+    return -(-B // seg_rows) if 0 < seg_rows < B else 0
 
 
 def _loss_out_shape(B: int, seg_rows: int) -> tuple:
@@ -187,7 +192,7 @@ def ppo_loss_fwd(old_lp: Tensor, lp: Tensor, adv: Tensor, mask: Tensor, ref_lp: 
     if sel is not None and (sel.dtype != torch.uint8 or not sel.is_contiguous()):
         raise TypeError("ppo_loss_fwd: sel must be contiguous uint8")
     out = torch.empty(_loss_out_shape(B, seg_rows), dtype=_F32, device=lp.device)
-    buf, ws = _loss_ws(B, lp.device)
+    buf, ws = _loss_ws(B, lp.device, _n_seg(B, seg_rows))
     L.call("va_ppo_loss_fwd", K._p(old_lp), K._p(lp), K._p(adv), K._p(mask), _mcode(mask), K._p(ref_lp),
            K._p(entropy), B, R, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode, K._p(sel), mode_coef,
            seg_rows, K._p(out), K._p(buf), K._stream(lp))
@@ -198,7 +203,8 @@ def ppo_loss_fwd(old_lp: Tensor, lp: Tensor, adv: Tensor, mask: Tensor, ref_lp: 
 def _(old_lp, lp, adv, mask, ref_lp, entropy, sel, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode, mode_coef,
       seg_rows=0):
     B = lp.numel() // lp.shape[-1] if lp.dim() > 1 else 1
-    return lp.new_empty(_loss_out_shape(B, seg_rows), dtype=_F32), lp.new_empty(B * 8 + 8, dtype=_F64)
+    return (lp.new_empty(_loss_out_shape(B, seg_rows), dtype=_F32),
+            lp.new_empty(B * 8 + 8 + _n_seg(B, seg_rows), dtype=_F64))
 
 
 @_op("ppo_loss_bwd")
@@ -553,7 +559,7 @@ def value_loss_fwd(vpreds: Tensor, values: Tensor, returns: Tensor, mask: Tensor
     _check_f32(vpreds, values, returns)
     B, R = _rows(vpreds)
     out = torch.empty(_vloss_out_shape(B, seg_rows), dtype=_F32, device=vpreds.device)
-    buf, ws = _loss_ws(B, vpreds.device)
+    buf, ws = _loss_ws(B, vpreds.device, _n_seg(B, seg_rows))
     L.call("va_value_loss_fwd", K._p(vpreds), K._p(values), K._p(returns), K._p(mask), _mcode(mask), B, R,
            cliprange_value, agg_mode, seg_rows, K._p(out), K._p(buf), K._stream(vpreds))
     return out, ws
@@ -562,7 +568,8 @@ def value_loss_fwd(vpreds: Tensor, values: Tensor, returns: Tensor, mask: Tensor
 @value_loss_fwd.register_fake
 def _(vpreds, values, returns, mask, cliprange_value, agg_mode, seg_rows=0):
     B = vpreds.numel() // vpreds.shape[-1] if vpreds.dim() > 1 else 1
-    return vpreds.new_empty(_vloss_out_shape(B, seg_rows), dtype=_F32), vpreds.new_empty(B * 8 + 8, dtype=_F64)
+    return (vpreds.new_empty(_vloss_out_shape(B, seg_rows), dtype=_F32),
+            vpreds.new_empty(B * 8 + 8 + _n_seg(B, seg_rows), dtype=_F64))
 
 
 @_op("value_loss_bwd")
