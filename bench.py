@@ -110,8 +110,11 @@ def _gemm_table_name():
 def _micro_text(micro: int, pass_rows: int, args) -> str:
     """The loss micro-batch part of config.deviations_from_reference_defaults."""
     if args.dynamic_bsz:
+        merged = (f"update passes of up to {args.compute_max_tokens} tokens, each holding several of those "
+                  "micro-batches, aggregated one by one by the fused loss kernel (seg_off); "
+                  if args.compute_max_tokens else "")
         return (f"use_dynamic_bsz with a {args.dynamic_bsz}-token budget (loss scaled by rows / mini-batch, "
-                "dp_actor.py:465-467); ")
+                "dp_actor.py:465-467); " + merged)
     passes = (f"update passes of {pass_rows} responses, each holding {pass_rows // micro} of those micro-batches, "
               "aggregated one by one by the fused loss kernel (seg_rows: the same loss, gradient and "
               "per-micro-batch metric lists as separate passes, tests/test_actor_gpu.py); " if pass_rows > micro
@@ -147,6 +150,12 @@ def parse(argv=None):
     ap.add_argument("--logprob-micro", type=int, default=128, help="log_prob_micro_batch_size_per_gpu")
     ap.add_argument("--dynamic-bsz", type=int, default=0,
                     help="use_dynamic_bsz with this ppo_max_token_len_per_gpu (and log-prob budget); 0 = off")
+    ap.add_argument("--compute-max-tokens", type=int, default=0,
+                    help="with --dynamic-bsz: compute_max_token_len_per_gpu, tokens per update pass holding several "
+                         "token-budget micro-batches (0 = one micro-batch per pass, as the reference)")
+    ap.add_argument("--logprob-max-tokens", type=int, default=0,
+                    help="with --dynamic-bsz: log_prob_max_token_len_per_gpu of the no-grad old-logp pass (per-token "
+                         "results, independent of it; 0 = the --dynamic-bsz budget)")
     ap.add_argument("--pad-multiple", type=int, default=2048,
                     help="round packed micro-batches up to a multiple of this many tokens (pack_pad_multiple)")
     ap.add_argument("--gemm-table", default="default",
@@ -392,6 +401,7 @@ def main():
             clip_ratio=0.2, clip_ratio_c=3.0, loss_agg_mode="token-mean", entropy_coeff=0,
             use_remove_padding=not args.no_rmpad,
             use_dynamic_bsz=args.dynamic_bsz > 0, ppo_max_token_len_per_gpu=args.dynamic_bsz or 16384,
+            compute_max_token_len_per_gpu=args.compute_max_tokens or None,
             pack_pad_multiple=args.pad_multiple,
             logprob_inplace_backward=bool(args.logprob_inplace_bwd),
             fused_logprob_no_grad=bool(args.fused_no_grad),
@@ -400,7 +410,7 @@ def main():
         ),
         rollout=AttrDict(log_prob_micro_batch_size_per_gpu=lp_micro, temperature=1.0,
                          log_prob_use_dynamic_bsz=args.dynamic_bsz > 0,
-                         log_prob_max_token_len_per_gpu=args.dynamic_bsz or 16384),
+                         log_prob_max_token_len_per_gpu=args.logprob_max_tokens or args.dynamic_bsz or 16384),
     )
     worker = ActorWorker(cfg, rollout_n=args.n)
     model = build_qwen2(args.model, device=dev, seed=0)
@@ -564,6 +574,8 @@ def main():
                        "use_fused_kernels option, off by default there; same bf16-rounded logits, tests)"
                        if args.fused_no_grad else "")),
                 "dynamic_bsz_max_token_len": args.dynamic_bsz or None,
+                "compute_max_token_len": args.compute_max_tokens or None,
+                "logprob_max_token_len": (args.logprob_max_tokens or args.dynamic_bsz) if args.dynamic_bsz else None,
                 "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
                 "pack_pad_multiple": args.pad_multiple,
                 "logprob_inplace_backward": bool(args.logprob_inplace_bwd),

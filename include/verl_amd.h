@@ -201,7 +201,10 @@ int va_set_tuning(int key, int value);
  *   splits it into S = ceil(B / seg_rows) loss micro-batches of seg_rows consecutive rows (the last
  *   may be shorter), each aggregated on its own as a separate call over its rows would be (its own
  *   token and row counts: the reference's agg_loss per micro-batch, dp_actor.py:419-470), into
- *   out[S][VA_LOSS_NOUT].
+ *   out[S][VA_LOSS_NOUT]. seg_off (device, n_seg + 1 ascending int32 row offsets, seg_off[0] = 0,
+ *   seg_off[n_seg] = B, every segment non-empty, 1 <= n_seg <= B) instead gives n_seg segments of
+ *   any sizes (the reference's token-budget micro-batches, dp_actor.py:382-384); seg_rows is then
+ *   ignored. The offsets are device data: the host checks only n_seg.
  *   out fp32 (device). workspace: va_ppo_loss_workspace_bytes(B) = 8 (16 B + 8):
  *   [B, 8] fp64 row partials, 8 fp64 totals (n first; zeros with segments), then up to B per-workgroup aggregated
  *   vectors that only the forward reads, whose first S slots the segmented forward overwrites with
@@ -212,7 +215,8 @@ int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float *adv, cons
                     int mask_dtype, const float *ref_lp, const float *entropy, int64_t B,
                     int64_t R, float clip_lo, float clip_hi, float clip_c, int agg_mode,
                     int kl_type, int loss_mode, const uint8_t *sel, float mode_coef,
-                    int64_t seg_rows, float *out, void *workspace, void *stream);
+                    int64_t seg_rows, const int32_t *seg_off, int64_t n_seg, float *out,
+                    void *workspace, void *stream);
 
 /* Backward: g_out[S][VA_LOSS_NOUT] is d(loss)/d(out) as a device array (only slots PG, KL,
  * ENTROPY are read; may be NULL = zeros), seg_rows as in the forward (S = 1 when 0). Writes
@@ -223,7 +227,8 @@ int va_ppo_loss_bwd(const float *g_out, const float *old_lp, const float *lp, co
                     const void *mask, int mask_dtype, const float *ref_lp, int64_t B, int64_t R,
                     float clip_lo, float clip_hi, float clip_c, int agg_mode, int kl_type,
                     int loss_mode, const uint8_t *sel, float mode_coef, int64_t seg_rows,
-                    const void *workspace, float *d_lp, float *d_entropy, void *stream);
+                    const int32_t *seg_off, int64_t n_seg, const void *workspace, float *d_lp,
+                    float *d_entropy, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Elementwise KL estimators (core_algos.py:1034-1069), n elements.
@@ -399,7 +404,7 @@ int va_discounted_returns(const float *rewards, const void *mask, int mask_dtype
  * Critic: fused clipped value loss (core_algos.py:992-1031, clip_by_value torch_functional.py:
  * 136-142) + the critic's vpred_mean metric (dp_critic.py:236-242).
  *   vpreds, values, returns [B, R] fp32; mask [B, R] of mask_dtype; agg_mode = VA_AGG_*.
- *   seg_rows as va_ppo_loss_fwd: 0 aggregates the whole batch into out[VA_VLOSS_NOUT]; 0 < seg_rows
+ *   seg_rows / seg_off / n_seg as va_ppo_loss_fwd: 0 / NULL aggregates the whole batch into out[VA_VLOSS_NOUT]; 0 < seg_rows
  *   < B gives out[S][VA_VLOSS_NOUT] for the S loss micro-batches of seg_rows rows (dp_critic.py:
  *   218-242 per micro-batch). workspace: va_ppo_loss_workspace_bytes(B).
  * Backward: g_out[S][VA_VLOSS_NOUT] = d(loss)/d(out) (slots LOSS and VPRED_MEAN are read) ->
@@ -412,10 +417,12 @@ int va_discounted_returns(const float *rewards, const void *mask, int mask_dtype
 #define VA_VLOSS_NOUT 4
 int va_value_loss_fwd(const float *vpreds, const float *values, const float *returns, const void *mask,
                       int mask_dtype, int64_t B, int64_t R, float cliprange_value, int agg_mode,
-                      int64_t seg_rows, float *out, void *workspace, void *stream);
+                      int64_t seg_rows, const int32_t *seg_off, int64_t n_seg, float *out, void *workspace,
+                      void *stream);
 int va_value_loss_bwd(const float *g_out, const float *vpreds, const float *values, const float *returns,
                       const void *mask, int mask_dtype, int64_t B, int64_t R, float cliprange_value,
-                      int agg_mode, int64_t seg_rows, const void *workspace, float *d_vpreds, void *stream);
+                      int agg_mode, int64_t seg_rows, const int32_t *seg_off, int64_t n_seg,
+                      const void *workspace, float *d_vpreds, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Causal varlen flash-attention forward for the actor backbone (not a §8 row). q [T, Hq, 64],

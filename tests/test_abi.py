@@ -53,14 +53,18 @@ def test_argument_validation_without_device(lib):
     rc = lib.va_logprob_entropy_fwd(None, 1, 4, 0, 0, None, 1.0, None, None, None, None)
     assert rc == -1 and b"vocab" in lib.va_last_error()
     rc = lib.va_ppo_loss_fwd(None, None, None, None, 0, None, None, 0, 5, 0.8, 1.2, 3.0, 0, -1, 0, None, 0.0, 0,
-                             None, None, None)
+                             None, 0, None, None, None)
     assert rc == -1 and b"empty batch" in lib.va_last_error()
     # the clip_cov / kl_cov modes need their token selection
     rc = lib.va_ppo_loss_fwd(1, 1, 1, 1, 0, None, None, 2, 5, 0.8, 1.2, 3.0, 0, -1, L.VA_PL_CLIP_COV, None, 0.0, 0,
-                             1, 1, None)
+                             None, 0, 1, 1, None)
     assert rc == -1 and b"selection" in lib.va_last_error()
-    rc = lib.va_ppo_loss_fwd(1, 1, 1, 1, 0, None, None, 2, 5, 0.8, 1.2, 3.0, 0, -1, 0, None, 0.0, -1, 1, 1, None)
-    assert rc == -1 and b"seg_rows" in lib.va_last_error()
+    # loss micro-batch segments: negative seg_rows, or offsets with n_seg outside [1, B]
+    rc = lib.va_ppo_loss_fwd(1, 1, 1, 1, 0, None, None, 2, 5, 0.8, 1.2, 3.0, 0, -1, 0, None, 0.0, -1, None, 0, 1, 1,
+                             None)
+    assert rc == -1 and b"bad segments" in lib.va_last_error()
+    rc = lib.va_value_loss_fwd(1, 1, 1, 1, 0, 2, 5, 0.5, 0, 0, 1, 3, 1, 1, None)
+    assert rc == -1 and b"bad segments" in lib.va_last_error()
     assert lib.va_outcome_workspace_bytes(10) == 4 * 3 * 10
     rc = lib.va_group_coef(1, None, 1, 1, 4, 8, 1e-6, L.VA_ADV_OPO, 1, None)
     assert rc == -1 and b"lengths" in lib.va_last_error()

@@ -172,10 +172,13 @@ def test_worker_step_runs_and_learns():
     assert abs(met["actor/ppo_kl"][0]) < 1e-3
 
 
-def test_dynamic_bsz_log_prob_and_update_match_reference():
+@pytest.mark.parametrize("merge", [None, 3, 100])
+def test_dynamic_bsz_log_prob_and_update_match_reference(merge):
     """use_dynamic_bsz (dp_actor.py:321-347, 382-384, 465-467): token-budget micro-batches give the
     same log-probs as fixed micro-batches, and update_policy's gradient is the reference's sum of
-    per-micro-batch losses scaled by rows / ppo_mini_batch_size."""
+    per-micro-batch losses scaled by rows / ppo_mini_batch_size. merge: compute_max_token_len_per_gpu
+    = merge x the micro-batch budget, so passes hold several micro-batches (aggregated one by one
+    from their row offsets: same metric lists, same gradient)."""
     from verl_amd.utils.model import build_qwen2
     from verl_amd.utils.seqlen_balancing import prepare_dynamic_batch
 
@@ -189,7 +192,8 @@ def test_dynamic_bsz_log_prob_and_update_match_reference():
     budget = 2 * S  # several micro-batches of uneven row counts
     actor = _actor(model, use_remove_padding=False, autocast_dtype=None, ppo_mini_batch_size=8,
                    ppo_micro_batch_size_per_gpu=None, use_dynamic_bsz=True, ppo_max_token_len_per_gpu=budget,
-                   use_kl_loss=False, entropy_coeff=0.0, clip_ratio=0.2, grad_clip=1e9)
+                   use_kl_loss=False, entropy_coeff=0.0, clip_ratio=0.2, grad_clip=1e9,
+                   compute_max_token_len_per_gpu=merge * budget if merge else None)
     data.meta_info.update(micro_batch_size=None, temperature=1.0, use_dynamic_bsz=True, max_token_len=budget)
     lp_dyn, ent_dyn = actor.compute_log_prob(data, calculate_entropy=True)
     with torch.no_grad():
@@ -209,20 +213,23 @@ def test_dynamic_bsz_log_prob_and_update_match_reference():
         return torch.tensor(0.0, device=DEV)
 
     actor._optimizer_step = capture
-    actor.update_policy(data)
+    metrics = actor.update_policy(data)
     sel = data.select(batch_keys=["responses", "response_mask", "input_ids", "attention_mask", "position_ids",
                                   "old_log_probs", "advantages"])
     micro, idx_lists = prepare_dynamic_batch(sel, max_token_len=budget)
-    assert len(micro) > 1 and len({len(ix) for ix in idx_lists}) >= 1
+    assert len(micro) > 2 and len({len(ix) for ix in idx_lists}) >= 1
     model_ref.zero_grad()
+    pg_losses = []
     for mbp in micro:
         mb = mbp.batch
         out = model_ref(input_ids=mb["input_ids"], attention_mask=mb["attention_mask"],
                         position_ids=mb["position_ids"], use_cache=False).logits[:, -R - 1 : -1, :]
         lp = torch.stack([ref.logprobs_from_logits(r, lab) for r, lab in zip(out, mb["responses"], strict=True)])
-        loss, _ = ref.actor_loss(mb["old_log_probs"], lp, mb["advantages"], mb["response_mask"], clip_ratio=0.2,
-                                 loss_agg_mode="token-mean", grad_scale=len(mbp) / 8)
+        loss, met = ref.actor_loss(mb["old_log_probs"], lp, mb["advantages"], mb["response_mask"], clip_ratio=0.2,
+                                   loss_agg_mode="token-mean", grad_scale=len(mbp) / 8)
         loss.backward()
+        pg_losses.append(met["pg_loss"].item())
+    assert np.allclose(metrics["actor/pg_loss"], pg_losses, atol=1e-5, rtol=1e-4)
     for n, p in model_ref.named_parameters():
         scale = p.grad.abs().max().item() + 1e-12
         assert torch.allclose(grads[n], p.grad, atol=1e-4 * scale, rtol=1e-3), n

@@ -60,6 +60,13 @@ def test_opcheck_ppo_loss(mode, kl, seg):
     g = torch.ones_like(out)
     _check(ops.ppo_loss_bwd, (g, old, lp.detach(), adv, mask, args[4], sel, ws, 0.8, 1.2, 3.0, 0, kl, mode, 0.1, True,
                               seg))
+    if seg:  # the same 3 segments as row offsets
+        off = torch.tensor([0, 2, 3, 8], dtype=torch.int32, device=DEV)
+        args = args[:-1] + (0, off)
+        _check(ops.ppo_loss_fwd, args)
+        out, ws = ops.ppo_loss_fwd(*args)
+        _check(ops.ppo_loss_bwd, (torch.ones_like(out), old, lp.detach(), adv, mask, args[4], sel, ws, 0.8, 1.2, 3.0, 0,
+                                  kl, mode, 0.1, True, 0, off))
 
 
 def test_opcheck_kl_agg_value():

@@ -127,3 +127,40 @@ def test_value_loss_segments_equal_separate_calls(agg, B, R, seg):
         assert torch.allclose(out[s], o, rtol=1e-6, atol=1e-7, equal_nan=True), (s, out[s], o)
         (o[L.VA_VLOSS_LOSS] * w[s, 0] + o[L.VA_VLOSS_VPRED_MEAN] * w[s, 1]).backward()
         assert _bits_equal(vp_a.grad[sl], vp_b.grad), s
+
+
+@pytest.mark.parametrize("sizes", [[3, 1, 7, 5], [16], [1] * 9, [2, 30, 2]])
+def test_variable_segments_equal_separate_calls(sizes):
+    """seg_off: segments of any sizes (the reference's token-budget micro-batches), policy and value
+    loss, against separate launches over each segment's rows."""
+    from verl_amd import _lib as L
+    from verl_amd import kernels as K
+
+    B, R = sum(sizes), 1024
+    old, lp, adv, mask, ref_lp, ent = _inputs(max(B, 4), R, seed=len(sizes))
+    old, lp, adv, mask, ref_lp, ent = (t[:B].contiguous() for t in (old, lp, adv, mask, ref_lp, ent))
+    off = [0]
+    for s in sizes:
+        off.append(off[-1] + s)
+    lp_a = lp.clone().requires_grad_(True)
+    out = K.fused_policy_loss(old, lp_a, adv, mask, 0.2, 0.28, 3.0, "seq-mean-token-sum", ref_log_prob=ref_lp,
+                              kl_loss_type="low_var_kl", seg_off=off)
+    vp_a = (lp + 0.3).requires_grad_(True)
+    vout = K.fused_value_loss(vp_a, lp, ref_lp, mask, 0.5, "token-mean", seg_off=off)
+    S = len(sizes)
+    assert out.shape == (S, L.VA_LOSS_NOUT) and vout.shape == (S, L.VA_VLOSS_NOUT)
+    w = torch.rand(S, 3, device=DEV)
+    (out[:, L.VA_LOSS_PG] * w[:, 0] + out[:, L.VA_LOSS_KL] * w[:, 1] + vout[:, L.VA_VLOSS_LOSS] * w[:, 2]).sum().backward()
+    for s in range(S):
+        sl = slice(off[s], off[s + 1])
+        lp_b = lp[sl].clone().requires_grad_(True)
+        o = K.fused_policy_loss(old[sl].contiguous(), lp_b, adv[sl].contiguous(), mask[sl].contiguous(), 0.2, 0.28, 3.0,
+                                "seq-mean-token-sum", ref_log_prob=ref_lp[sl].contiguous(), kl_loss_type="low_var_kl")
+        vp_b = (lp[sl] + 0.3).requires_grad_(True)
+        vo = K.fused_value_loss(vp_b, lp[sl].contiguous(), ref_lp[sl].contiguous(), mask[sl].contiguous(), 0.5,
+                                "token-mean")
+        assert torch.allclose(out[s], o, rtol=1e-6, atol=1e-7, equal_nan=True), (s, out[s], o)
+        assert torch.allclose(vout[s], vo, rtol=1e-6, atol=1e-7, equal_nan=True), (s, vout[s], vo)
+        (o[L.VA_LOSS_PG] * w[s, 0] + o[L.VA_LOSS_KL] * w[s, 1] + vo[L.VA_VLOSS_LOSS] * w[s, 2]).backward()
+        assert _bits_equal(lp_a.grad[sl], lp_b.grad), s
+        assert _bits_equal(vp_a.grad[sl], vp_b.grad), s

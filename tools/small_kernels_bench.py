@@ -92,15 +92,15 @@ def main():
 
         def loss():
             L.call("va_ppo_loss_fwd", K._p(old), K._p(lp), K._p(adv), K._p(mask), L.VA_MASK_I64, K._p(ref), None, B, R,
-                   0.8, 1.2, 3.0, 0, L.VA_KL_K3, 0, None, 0.0, args.seg_rows, K._p(lout), K._p(lws), s)
+                   0.8, 1.2, 3.0, 0, L.VA_KL_K3, 0, None, 0.0, args.seg_rows, None, 0, K._p(lout), K._p(lws), s)
             L.call("va_ppo_loss_bwd", K._p(gout), K._p(old), K._p(lp), K._p(adv), K._p(mask), L.VA_MASK_I64, K._p(ref),
-                   B, R, 0.8, 1.2, 3.0, 0, L.VA_KL_K3, 0, None, 0.0, args.seg_rows, K._p(lws), K._p(dlp), None, s)
+                   B, R, 0.8, 1.2, 3.0, 0, L.VA_KL_K3, 0, None, 0.0, args.seg_rows, None, 0, K._p(lws), K._p(dlp), None, s)
 
         def vloss():  # critic: vpreds = values + noise, returns = ret of the GAE call
-            L.call("va_value_loss_fwd", K._p(lp), K._p(old), K._p(ref), K._p(mask), L.VA_MASK_I64, B, R, 0.5, 0, args.seg_rows,
+            L.call("va_value_loss_fwd", K._p(lp), K._p(old), K._p(ref), K._p(mask), L.VA_MASK_I64, B, R, 0.5, 0, args.seg_rows, None, 0,
                    K._p(vout), K._p(lws), s)
             L.call("va_value_loss_bwd", K._p(gout), K._p(lp), K._p(old), K._p(ref), K._p(mask), L.VA_MASK_I64, B, R,
-                   0.5, 0, args.seg_rows, K._p(lws), K._p(vgrad), s)
+                   0.5, 0, args.seg_rows, None, 0, K._p(lws), K._p(vgrad), s)
 
         def agg():  # agg_loss(entropy, mask, token-mean): the actor/entropy metric
             L.call("va_masked_agg_fwd", K._p(lp), K._p(mask), L.VA_MASK_I64, B, R, 0, K._p(aout), K._p(lws), s)

@@ -51,12 +51,12 @@ _SIGNATURES: dict[str, tuple] = {
     "va_ppo_loss_fwd": (
         c_int,
         [_P, _P, _P, _P, c_int, _P, _P, c_int64, c_int64, c_float, c_float, c_float, c_int, c_int, c_int, _P,
-         c_float, c_int64, _P, _P, _P],
+         c_float, c_int64, _P, c_int64, _P, _P, _P],
     ),
     "va_ppo_loss_bwd": (
         c_int,
         [_P, _P, _P, _P, _P, c_int, _P, c_int64, c_int64, c_float, c_float, c_float, c_int, c_int, c_int, _P,
-         c_float, c_int64, _P, _P, _P, _P],
+         c_float, c_int64, _P, c_int64, _P, _P, _P, _P],
     ),
     "va_kl_penalty_fwd": (c_int, [_P, _P, c_int64, c_int, _P, _P]),
     "va_kl_penalty_bwd": (c_int, [_P, _P, _P, c_int64, c_int, _P, _P, _P]),
@@ -89,8 +89,10 @@ _SIGNATURES: dict[str, tuple] = {
     "va_swiglu_fwd": (c_int, [_P, c_int64, c_int64, c_int, c_int64, c_int64, _P, _P]),
     "va_swiglu_bwd": (c_int, [_P, _P, c_int64, c_int64, c_int, c_int64, c_int64, _P, c_int64, c_int64, _P]),
     "va_rope_qkv_fwd": (c_int, [_P, c_int64, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, _P, _P, _P]),
-    "va_value_loss_fwd": (c_int, [_P, _P, _P, _P, c_int, c_int64, c_int64, c_float, c_int, c_int64, _P, _P, _P]),
-    "va_value_loss_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_float, c_int, c_int64, _P, _P, _P]),
+    "va_value_loss_fwd": (c_int, [_P, _P, _P, _P, c_int, c_int64, c_int64, c_float, c_int, c_int64, _P, c_int64, _P,
+                                  _P, _P]),
+    "va_value_loss_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_float, c_int, c_int64, _P, c_int64,
+                                  _P, _P, _P]),
     "va_discounted_returns": (c_int, [_P, _P, c_int, c_int64, c_int64, c_float, c_int, _P, _P, _P, _P]),
     "va_linear_logprob_workspace_bytes": (c_int64, [c_int64, c_int]),
     "va_linear_logprob_fwd": (

@@ -438,6 +438,35 @@ __global__ __launch_bounds__(1024) void ppo_loss_finalize_kernel(const double *_
 // segment s = rows [s * seg_rows, min(B, (s + 1) * seg_rows)) is aggregated on its own, exactly as
 // a separate call over those rows would (its own token count n_s, its own row count B_s).
 //
+// The segments of one launch: `off` (device, n + 1 ascending row offsets, off[0] = 0, off[n] = B,
+// every segment non-empty) for variable-size segments (the reference's token-budget micro-batches,
+// dp_actor.py:382-384), else uniform runs of `rows` rows (the last one shorter); rows == 0 and off ==
+// nullptr: one segment, the whole batch.
+struct Segs {
+  int64_t rows;
+  const int32_t *off;
+  int64_t n;
+};
+__device__ __forceinline__ bool seg_on(const Segs &g) { return g.off != nullptr || g.rows > 0; }
+__device__ __forceinline__ void seg_range(const Segs &g, int64_t s, int64_t B, int64_t &b0, int64_t &b1) {
+  if (g.off != nullptr) {
+    b0 = g.off[s], b1 = g.off[s + 1];
+  } else {
+    b0 = s * g.rows, b1 = b0 + g.rows < B ? b0 + g.rows : B;
+  }
+}
+// segment of row b (uniform per workgroup: a binary search over the offsets, or a division)
+__device__ __forceinline__ int64_t seg_of(const Segs &g, int64_t b) {
+  if (g.off == nullptr) return b / g.rows;
+  int64_t lo = 0, hi = g.n - 1;  // largest s with off[s] <= b
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (g.off[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
 // Slot q of one segment summed over its rows in a fixed order: lane 8 k + q adds rows b0 + k, b0 + k
 // + 8, ... in order, then the 8 k-partials meet by xor 8, 16, 32. Every lane of the wave returns
 // the segment sum of its slot q = lane & 7 (term slots aggregated per row with agg_term).
@@ -474,12 +503,13 @@ __device__ __forceinline__ void seg_write_totals(double *__restrict__ part, int6
 
 // One 64-thread workgroup per segment: out[s][VA_LOSS_NOUT] as the one-segment finalize writes it.
 __global__ __launch_bounds__(64) void ppo_loss_seg_finalize_kernel(double *__restrict__ part, int64_t B,
-                                                                   int64_t R, int64_t seg_rows, int agg,
+                                                                   int64_t R, Segs segs, int agg,
                                                                    int has_kl, int has_ent,
                                                                    float *__restrict__ out) {
   seg_write_totals(part, B);
   const int64_t s = blockIdx.x;
-  const int64_t b0 = s * seg_rows, b1 = b0 + seg_rows < B ? b0 + seg_rows : B;
+  int64_t b0, b1;
+  seg_range(segs, s, B, b0, b1);
   const double x = seg_slot_sum(part, b0, b1, agg, (1u << 1) | (1u << 5) | (1u << 6));
   double v[kNQ];
 #pragma unroll
@@ -502,22 +532,23 @@ __global__ __launch_bounds__(64) void ppo_loss_seg_finalize_kernel(double *__res
 }
 
 // ------------------------------------------------------------------ policy loss backward
-// seg_rows in (0, B): row b belongs to segment b / seg_rows, whose upstream gradients are
-// g_out[s][*] and whose token / row counts replace the batch totals (see seg_slot_sum).
+// With segments row b belongs to segment s = seg_of(b), whose upstream gradients are g_out[s][*] and
+// whose token / row counts replace the batch totals.
 template <int MT, int KL>
 __global__ __launch_bounds__(256) void ppo_loss_bwd_kernel(
     const float *__restrict__ g_out, const float *__restrict__ old_lp,
     const float *__restrict__ lp, const float *__restrict__ adv, const void *__restrict__ mask,
     const float *__restrict__ ref, const uint8_t *__restrict__ sel, int64_t B, int64_t R, float lo,
-    float hi, float c, int agg, int mode, float coef, int64_t seg_rows, const double *__restrict__ part,
+    float hi, float c, int agg, int mode, float coef, Segs segs, const double *__restrict__ part,
     float *__restrict__ d_lp, float *__restrict__ d_ent) {
   const int64_t b = blockIdx.y;
   const float *gs = g_out;  // this row's segment's upstream gradients
   double n_tot;
   int64_t Bs = B;
-  if (seg_rows > 0) {  // uniform per workgroup: the segment's token count from the forward's finalize
-    const int64_t s = b / seg_rows;
-    const int64_t b0 = s * seg_rows, b1 = b0 + seg_rows < B ? b0 + seg_rows : B;
+  if (seg_on(segs)) {  // uniform per workgroup: the segment's token count from the forward's finalize
+    const int64_t s = seg_of(segs, b);
+    int64_t b0, b1;
+    seg_range(segs, s, B, b0, b1);
     n_tot = part[B * kNQ + kTotals + s];
     Bs = b1 - b0;
     if (gs) gs += s * VA_LOSS_NOUT;
@@ -857,11 +888,12 @@ __global__ __launch_bounds__(1024) void value_loss_finalize_kernel(const double 
 
 // Loss micro-batch segments as the policy loss (seg_slot_sum): out[s][VA_VLOSS_NOUT] per segment.
 __global__ __launch_bounds__(64) void value_loss_seg_finalize_kernel(double *__restrict__ part, int64_t B,
-                                                                     int64_t R, int64_t seg_rows, int agg,
+                                                                     int64_t R, Segs segs, int agg,
                                                                      float *__restrict__ out) {
   seg_write_totals(part, B);
   const int64_t s = blockIdx.x;
-  const int64_t b0 = s * seg_rows, b1 = b0 + seg_rows < B ? b0 + seg_rows : B;
+  int64_t b0, b1;
+  seg_range(segs, s, B, b0, b1);
   const double x = seg_slot_sum(part, b0, b1, agg, 1u << 1);
   double v[4];
 #pragma unroll
@@ -882,14 +914,15 @@ template <int MT>
 __global__ __launch_bounds__(256) void value_loss_bwd_kernel(
     const float *__restrict__ g_out, const float *__restrict__ vp, const float *__restrict__ val,
     const float *__restrict__ ret, const void *__restrict__ mask, int64_t B, int64_t R, float c,
-    int agg, int64_t seg_rows, const double *__restrict__ part, float *__restrict__ d_vp) {
+    int agg, Segs segs, const double *__restrict__ part, float *__restrict__ d_vp) {
   const int64_t b = blockIdx.y;
   const float *gs = g_out;  // this row's segment's upstream gradients
   double n_tot;
   int64_t Bs = B;
-  if (seg_rows > 0) {  // uniform per workgroup (see ppo_loss_bwd_kernel)
-    const int64_t s = b / seg_rows;
-    const int64_t b0 = s * seg_rows, b1 = b0 + seg_rows < B ? b0 + seg_rows : B;
+  if (seg_on(segs)) {  // uniform per workgroup (see ppo_loss_bwd_kernel)
+    const int64_t s = seg_of(segs, b);
+    int64_t b0, b1;
+    seg_range(segs, s, B, b0, b1);
     n_tot = part[B * kNQ + kTotals + s];
     Bs = b1 - b0;
     if (gs) gs += s * VA_VLOSS_NOUT;
@@ -956,6 +989,22 @@ static bool stream_rows(int64_t R, uintptr_t ptr_or) {
   return g_loss_vec != 0 && (R & 3) == 0 && R <= 2048 && (ptr_or & 15) == 0;
 }
 
+static bool seg_on_host(const Segs &g) { return g.off != nullptr || g.rows > 0; }
+
+// segments of a policy / value loss launch (see Segs): returns the count S (1 = no segments) or < 0
+static int64_t host_segs(int64_t B, int64_t seg_rows, const int32_t *seg_off, int64_t n_seg, Segs &g) {
+  g = Segs{0, nullptr, 1};
+  if (seg_off != nullptr) {
+    if (n_seg < 1 || n_seg > B) return -1;
+    g = Segs{0, seg_off, n_seg};
+    return n_seg;
+  }
+  if (seg_rows < 0) return -1;
+  if (seg_rows == 0 || seg_rows >= B) return 1;
+  g = Segs{seg_rows, nullptr, (B + seg_rows - 1) / seg_rows};
+  return g.n;
+}
+
 static int check_agg(int agg, bool allow_reduce) {
   const int hi = allow_reduce ? VA_REDUCE_ROW_MASKED_MEAN : VA_AGG_SEQ_MEAN_TOKEN_SUM_NORM;
   VA_CHECK_ARG(agg >= 0 && agg <= hi, "Invalid loss_agg_mode code: %d", agg);
@@ -974,9 +1023,12 @@ extern "C" int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float
                                const float *entropy, int64_t B, int64_t R, float clip_lo,
                                float clip_hi, float clip_c, int agg_mode, int kl_type,
                                int loss_mode, const uint8_t *sel, float mode_coef,
-                               int64_t seg_rows, float *out, void *workspace, void *stream) {
+                               int64_t seg_rows, const int32_t *seg_off, int64_t n_seg, float *out,
+                               void *workspace, void *stream) {
   VA_CHECK_ARG(B > 0 && R > 0, "empty batch (B=%lld, R=%lld)", (long long)B, (long long)R);
-  VA_CHECK_ARG(seg_rows >= 0, "seg_rows must be >= 0");
+  Segs segs;
+  const int64_t S = host_segs(B, seg_rows, seg_off, n_seg, segs);
+  VA_CHECK_ARG(S >= 1, "bad segments (seg_rows=%lld, n_seg=%lld)", (long long)seg_rows, (long long)n_seg);
   VA_CHECK_ARG(B < (1ll << 31), "B too large");
   VA_CHECK_ARG(old_lp && lp && adv && mask && out && workspace, "null pointer argument");
   VA_CHECK_ARG(kl_type == VA_KL_NONE || ref_lp != nullptr, "ref_lp required for kl_type %d",
@@ -1026,10 +1078,9 @@ extern "C" int va_ppo_loss_fwd(const float *old_lp, const float *lp, const float
                          loss_mode, mode_coef, part, wsum);
     }));
   }
-  if (seg_rows > 0 && seg_rows < B) {  // several loss micro-batches: one finalize workgroup each
-    const int64_t S = (B + seg_rows - 1) / seg_rows;
+  if (seg_on_host(segs)) {  // several loss micro-batches: one finalize workgroup each
     hipLaunchKernelGGL(ppo_loss_seg_finalize_kernel, dim3(static_cast<unsigned>(S)), dim3(64), 0, s, part, B, R,
-                       seg_rows, agg_mode, kl_type != VA_KL_NONE ? 1 : 0, entropy != nullptr ? 1 : 0, out);
+                       segs, agg_mode, kl_type != VA_KL_NONE ? 1 : 0, entropy != nullptr ? 1 : 0, out);
     return check_launch("ppo_loss_fwd");
   }
   hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(finalize_threads(G)), 0, s, wsum, G, B, R, agg_mode,
@@ -1043,11 +1094,12 @@ extern "C" int va_ppo_loss_bwd(const float *g_out, const float *old_lp, const fl
                                const float *ref_lp, int64_t B, int64_t R, float clip_lo,
                                float clip_hi, float clip_c, int agg_mode, int kl_type,
                                int loss_mode, const uint8_t *sel, float mode_coef,
-                               int64_t seg_rows, const void *workspace, float *d_lp, float *d_entropy,
-                               void *stream) {
+                               int64_t seg_rows, const int32_t *seg_off, int64_t n_seg, const void *workspace,
+                               float *d_lp, float *d_entropy, void *stream) {
   VA_CHECK_ARG(B > 0 && R > 0, "empty batch");
-  VA_CHECK_ARG(seg_rows >= 0, "seg_rows must be >= 0");
-  if (seg_rows >= B) seg_rows = 0;  // one segment: the batch totals
+  Segs segs;
+  VA_CHECK_ARG(host_segs(B, seg_rows, seg_off, n_seg, segs) >= 1, "bad segments (seg_rows=%lld, n_seg=%lld)",
+               (long long)seg_rows, (long long)n_seg);
   VA_CHECK_ARG(B < 65536, "B must be < 65536 for the 2-D backward grid");
   VA_CHECK_ARG(old_lp && lp && adv && mask && workspace && d_lp, "null pointer argument");
   VA_CHECK_ARG(kl_type == VA_KL_NONE || ref_lp != nullptr, "ref_lp required");
@@ -1059,7 +1111,7 @@ extern "C" int va_ppo_loss_bwd(const float *g_out, const float *old_lp, const fl
   VA_DISPATCH_MASK(mask_dtype, VA_DISPATCH_KL(kl_type, {
     hipLaunchKernelGGL((ppo_loss_bwd_kernel<MT, KL>), grid, dim3(256), 0, s, g_out, old_lp, lp,
                        adv, mask, ref_lp, sel, B, R, clip_lo, clip_hi, clip_c, agg_mode, loss_mode,
-                       mode_coef, seg_rows, part, d_lp, d_entropy);
+                       mode_coef, segs, part, d_lp, d_entropy);
   }));
   return check_launch("ppo_loss_bwd");
 }
@@ -1154,10 +1206,12 @@ extern "C" int va_apply_kl_penalty(const float *scores, const float *old_lp, con
 
 extern "C" int va_value_loss_fwd(const float *vpreds, const float *values, const float *returns,
                                  const void *mask, int mask_dtype, int64_t B, int64_t R,
-                                 float cliprange_value, int agg_mode, int64_t seg_rows, float *out,
-                                 void *workspace, void *stream) {
+                                 float cliprange_value, int agg_mode, int64_t seg_rows, const int32_t *seg_off,
+                                 int64_t n_seg, float *out, void *workspace, void *stream) {
   VA_CHECK_ARG(B > 0 && R > 0, "empty batch (B=%lld, R=%lld)", (long long)B, (long long)R);
-  VA_CHECK_ARG(seg_rows >= 0, "seg_rows must be >= 0");
+  Segs segs;
+  const int64_t S = host_segs(B, seg_rows, seg_off, n_seg, segs);
+  VA_CHECK_ARG(S >= 1, "bad segments (seg_rows=%lld, n_seg=%lld)", (long long)seg_rows, (long long)n_seg);
   VA_CHECK_ARG(B < (1ll << 31), "B too large");
   VA_CHECK_ARG(vpreds && values && returns && mask && out && workspace, "null pointer argument");
   if (int e = check_agg(agg_mode, false)) return e;
@@ -1183,9 +1237,9 @@ extern "C" int va_value_loss_fwd(const float *vpreds, const float *values, const
                          returns, mask, R, cliprange_value, agg_mode, part, wsum);
     });
   }
-  if (seg_rows > 0 && seg_rows < B) {  // several loss micro-batches: one finalize workgroup each
-    hipLaunchKernelGGL(value_loss_seg_finalize_kernel, dim3(static_cast<unsigned>((B + seg_rows - 1) / seg_rows)),
-                       dim3(64), 0, s, part, B, R, seg_rows, agg_mode, out);
+  if (seg_on_host(segs)) {  // several loss micro-batches: one finalize workgroup each
+    hipLaunchKernelGGL(value_loss_seg_finalize_kernel, dim3(static_cast<unsigned>(S)), dim3(64), 0, s, part, B, R,
+                       segs, agg_mode, out);
     return check_launch("value_loss_fwd");
   }
   hipLaunchKernelGGL(value_loss_finalize_kernel, dim3(1), dim3(finalize_threads(G)), 0, s, wsum, G, B, R, agg_mode,
@@ -1196,17 +1250,19 @@ extern "C" int va_value_loss_fwd(const float *vpreds, const float *values, const
 extern "C" int va_value_loss_bwd(const float *g_out, const float *vpreds, const float *values,
                                  const float *returns, const void *mask, int mask_dtype, int64_t B,
                                  int64_t R, float cliprange_value, int agg_mode, int64_t seg_rows,
-                                 const void *workspace, float *d_vpreds, void *stream) {
+                                 const int32_t *seg_off, int64_t n_seg, const void *workspace, float *d_vpreds,
+                                 void *stream) {
   VA_CHECK_ARG(B > 0 && R > 0 && B < 65536, "bad shape");
-  VA_CHECK_ARG(seg_rows >= 0, "seg_rows must be >= 0");
-  if (seg_rows >= B) seg_rows = 0;
+  Segs segs;
+  VA_CHECK_ARG(host_segs(B, seg_rows, seg_off, n_seg, segs) >= 1, "bad segments (seg_rows=%lld, n_seg=%lld)",
+               (long long)seg_rows, (long long)n_seg);
   VA_CHECK_ARG(vpreds && values && returns && mask && workspace && d_vpreds, "null pointer argument");
   if (int e = check_agg(agg_mode, false)) return e;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const dim3 grid(static_cast<unsigned>((R + 255) / 256), static_cast<unsigned>(B));
   VA_DISPATCH_MASK(mask_dtype, {
     hipLaunchKernelGGL((value_loss_bwd_kernel<MT>), grid, dim3(256), 0, s, g_out, vpreds, values,
-                       returns, mask, B, R, cliprange_value, agg_mode, seg_rows,
+                       returns, mask, B, R, cliprange_value, agg_mode, segs,
                        static_cast<const double *>(workspace), d_vpreds);
   });
   return check_launch("value_loss_bwd");

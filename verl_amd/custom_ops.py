@@ -168,85 +168,98 @@ def _loss_ws(B: int, device, n_seg: int = 0) -> tuple[Tensor, Tensor]:
     return buf, buf[: B * 8 + 8 + n_seg]
 
 
-def _n_seg(B: int, seg_rows: int) -> int:
+def _n_seg(B: int, seg_rows: int, seg_off: Optional[Tensor] = None) -> int:
+    """Loss micro-batch segments of one launch: len(seg_off) - 1 (variable sizes), ceil(B / seg_rows)
+    for 0 < seg_rows < B, else 0 (one aggregate)."""
+    if seg_off is not None:
+        return seg_off.numel() - 1
     return -(-B // seg_rows) if 0 < seg_rows < B else 0
 
 
-def _loss_out_shape(B: int, seg_rows: int) -> tuple:
-    """[VA_LOSS_NOUT] for one aggregated batch; [S, VA_LOSS_NOUT] for S = ceil(B / seg_rows) loss
-    micro-batches (0 < seg_rows < B)."""
-    if 0 < seg_rows < B:
-        return (-(-B // seg_rows), L.VA_LOSS_NOUT)
-    return (L.VA_LOSS_NOUT,)
+def _check_seg_off(seg_off: Optional[Tensor], B: int):
+    if seg_off is not None and (seg_off.dtype != torch.int32 or not seg_off.is_contiguous() or seg_off.dim() != 1
+                                or not 2 <= seg_off.numel() <= B + 1):
+        raise ValueError("seg_off must be a contiguous int32 [n_seg + 1] tensor of row offsets, 1 <= n_seg <= B")
+
+
+def _loss_out_shape(B: int, seg_rows: int, seg_off: Optional[Tensor] = None, nout: int = L.VA_LOSS_NOUT) -> tuple:
+    """[nout] for one aggregated batch; [S, nout] for S loss micro-batches (see _n_seg)."""
+    S = _n_seg(B, seg_rows, seg_off)
+    return (S, nout) if S else (nout,)
 
 
 @_op("ppo_loss_fwd")
 def ppo_loss_fwd(old_lp: Tensor, lp: Tensor, adv: Tensor, mask: Tensor, ref_lp: Optional[Tensor],
                  entropy: Optional[Tensor], sel: Optional[Tensor], clip_lo: float, clip_hi: float, clip_c: float,
                  agg_mode: int, kl_type: int, loss_mode: int, mode_coef: float,
-                 seg_rows: int = 0) -> tuple[Tensor, Tensor]:
-    """(out fp32 = VA_LOSS_* slots, [8] or [S, 8] per loss micro-batch of seg_rows rows; row-partials
-    workspace fp64) of the fused policy loss."""
+                 seg_rows: int = 0, seg_off: Optional[Tensor] = None) -> tuple[Tensor, Tensor]:
+    """(out fp32 = VA_LOSS_* slots, [8] or [S, 8] per loss micro-batch (seg_rows rows each, or the
+    row ranges of seg_off); row-partials workspace fp64) of the fused policy loss."""
     _check_f32(old_lp, lp, adv, ref_lp, entropy)
     B, R = _rows(lp)
     if sel is not None and (sel.dtype != torch.uint8 or not sel.is_contiguous()):
         raise TypeError("ppo_loss_fwd: sel must be contiguous uint8")
-    out = torch.empty(_loss_out_shape(B, seg_rows), dtype=_F32, device=lp.device)
-    buf, ws = _loss_ws(B, lp.device, _n_seg(B, seg_rows))
+    _check_seg_off(seg_off, B)
+    out = torch.empty(_loss_out_shape(B, seg_rows, seg_off), dtype=_F32, device=lp.device)
+    buf, ws = _loss_ws(B, lp.device, _n_seg(B, seg_rows, seg_off))
     L.call("va_ppo_loss_fwd", K._p(old_lp), K._p(lp), K._p(adv), K._p(mask), _mcode(mask), K._p(ref_lp),
            K._p(entropy), B, R, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode, K._p(sel), mode_coef,
-           seg_rows, K._p(out), K._p(buf), K._stream(lp))
+           seg_rows, K._p(seg_off), _n_seg(B, seg_rows, seg_off), K._p(out), K._p(buf), K._stream(lp))
     return out, ws
 
 
 @ppo_loss_fwd.register_fake
 def _(old_lp, lp, adv, mask, ref_lp, entropy, sel, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode, mode_coef,
-      seg_rows=0):
+      seg_rows=0, seg_off=None):
     B = lp.numel() // lp.shape[-1] if lp.dim() > 1 else 1
-    return (lp.new_empty(_loss_out_shape(B, seg_rows), dtype=_F32),
-            lp.new_empty(B * 8 + 8 + _n_seg(B, seg_rows), dtype=_F64))
+    return (lp.new_empty(_loss_out_shape(B, seg_rows, seg_off), dtype=_F32),
+            lp.new_empty(B * 8 + 8 + _n_seg(B, seg_rows, seg_off), dtype=_F64))
 
 
 @_op("ppo_loss_bwd")
 def ppo_loss_bwd(g_out: Tensor, old_lp: Tensor, lp: Tensor, adv: Tensor, mask: Tensor, ref_lp: Optional[Tensor],
                  sel: Optional[Tensor], ws: Tensor, clip_lo: float, clip_hi: float, clip_c: float, agg_mode: int,
                  kl_type: int, loss_mode: int, mode_coef: float, need_entropy: bool,
-                 seg_rows: int = 0) -> tuple[Tensor, Tensor]:
+                 seg_rows: int = 0, seg_off: Optional[Tensor] = None) -> tuple[Tensor, Tensor]:
     """(d_lp [B, R] fp32, d_entropy [B, R] fp32 or [0] when not needed)."""
     _check_f32(g_out, old_lp, lp, adv, ref_lp)
     B, R = _rows(lp)
-    if g_out.shape != _loss_out_shape(B, seg_rows):
-        raise ValueError(f"ppo_loss_bwd: g_out shape {tuple(g_out.shape)} != {_loss_out_shape(B, seg_rows)}")
+    _check_seg_off(seg_off, B)
+    want = _loss_out_shape(B, seg_rows, seg_off)
+    if g_out.shape != want:
+        raise ValueError(f"ppo_loss_bwd: g_out shape {tuple(g_out.shape)} != {want}")
     d_lp = torch.empty(lp.shape, dtype=_F32, device=lp.device)
     d_ent = torch.empty(lp.shape if need_entropy else (0,), dtype=_F32, device=lp.device)
     L.call("va_ppo_loss_bwd", K._p(g_out), K._p(old_lp), K._p(lp), K._p(adv), K._p(mask), _mcode(mask), K._p(ref_lp),
-           B, R, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode, K._p(sel), mode_coef, seg_rows, K._p(ws),
-           K._p(d_lp), K._p(d_ent) if need_entropy else None, K._stream(lp))
+           B, R, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode, K._p(sel), mode_coef, seg_rows,
+           K._p(seg_off), _n_seg(B, seg_rows, seg_off), K._p(ws), K._p(d_lp), K._p(d_ent) if need_entropy else None,
+           K._stream(lp))
     return d_lp, d_ent
 
 
 @ppo_loss_bwd.register_fake
 def _(g_out, old_lp, lp, adv, mask, ref_lp, sel, ws, clip_lo, clip_hi, clip_c, agg_mode, kl_type, loss_mode,
-      mode_coef, need_entropy, seg_rows=0):
+      mode_coef, need_entropy, seg_rows=0, seg_off=None):
     return lp.new_empty(lp.shape), lp.new_empty(lp.shape if need_entropy else (0,))
 
 
 def _loss_setup(ctx, inputs, output):
-    old_lp, lp, adv, mask, ref_lp, entropy, sel, clip_lo, clip_hi, clip_c, agg, kl, mode, coef, seg_rows = inputs
+    old_lp, lp, adv, mask, ref_lp, entropy, sel, clip_lo, clip_hi, clip_c, agg, kl, mode, coef, seg_rows, seg_off = inputs
     _, ws = output
     ctx.mark_non_differentiable(ws)
-    ctx.save_for_backward(old_lp, lp, adv, mask, ref_lp, sel, ws)
+    ctx.save_for_backward(old_lp, lp, adv, mask, ref_lp, sel, ws, seg_off)
     ctx.cfg = (clip_lo, clip_hi, clip_c, agg, kl, mode, coef, entropy is not None, seg_rows)
 
 
 def _loss_backward(ctx, g_out, g_ws):
-    old_lp, lp, adv, mask, ref_lp, sel, ws = ctx.saved_tensors
+    old_lp, lp, adv, mask, ref_lp, sel, ws, seg_off = ctx.saved_tensors
     clip_lo, clip_hi, clip_c, agg, kl, mode, coef, has_ent, seg_rows = ctx.cfg
     need_ent = has_ent and ctx.needs_input_grad[5]
     d_lp, d_ent = torch.ops.verl_amd.ppo_loss_bwd(g_out.float().contiguous(), old_lp, lp, adv, mask, ref_lp, sel, ws,
-                                                  clip_lo, clip_hi, clip_c, agg, kl, mode, coef, need_ent, seg_rows)
+                                                  clip_lo, clip_hi, clip_c, agg, kl, mode, coef, need_ent, seg_rows,
+                                                  seg_off)
     return (None, d_lp if ctx.needs_input_grad[1] else None, None, None, None, d_ent if need_ent else None,
-            None, None, None, None, None, None, None, None, None)
+            None, None, None, None, None, None, None, None, None, None)
 
 
 ppo_loss_fwd.register_autograd(_loss_backward, setup_context=_loss_setup)
@@ -546,63 +559,63 @@ def _(rewards, mask, gamma, mode, baselines):
 
 
 # =============================================================================== value loss (critic)
-def _vloss_out_shape(B: int, seg_rows: int) -> tuple:
-    if 0 < seg_rows < B:
-        return (-(-B // seg_rows), L.VA_VLOSS_NOUT)
-    return (L.VA_VLOSS_NOUT,)
-
-
 @_op("value_loss_fwd")
 def value_loss_fwd(vpreds: Tensor, values: Tensor, returns: Tensor, mask: Tensor, cliprange_value: float,
-                   agg_mode: int, seg_rows: int = 0) -> tuple[Tensor, Tensor]:
-    """(out fp32 = VA_VLOSS_* slots, [4] or [S, 4] per loss micro-batch of seg_rows rows; workspace)."""
+                   agg_mode: int, seg_rows: int = 0, seg_off: Optional[Tensor] = None) -> tuple[Tensor, Tensor]:
+    """(out fp32 = VA_VLOSS_* slots, [4] or [S, 4] per loss micro-batch (as ppo_loss_fwd); workspace)."""
     _check_f32(vpreds, values, returns)
     B, R = _rows(vpreds)
-    out = torch.empty(_vloss_out_shape(B, seg_rows), dtype=_F32, device=vpreds.device)
-    buf, ws = _loss_ws(B, vpreds.device, _n_seg(B, seg_rows))
+    _check_seg_off(seg_off, B)
+    out = torch.empty(_loss_out_shape(B, seg_rows, seg_off, L.VA_VLOSS_NOUT), dtype=_F32, device=vpreds.device)
+    buf, ws = _loss_ws(B, vpreds.device, _n_seg(B, seg_rows, seg_off))
     L.call("va_value_loss_fwd", K._p(vpreds), K._p(values), K._p(returns), K._p(mask), _mcode(mask), B, R,
-           cliprange_value, agg_mode, seg_rows, K._p(out), K._p(buf), K._stream(vpreds))
+           cliprange_value, agg_mode, seg_rows, K._p(seg_off), _n_seg(B, seg_rows, seg_off), K._p(out), K._p(buf),
+           K._stream(vpreds))
     return out, ws
 
 
 @value_loss_fwd.register_fake
-def _(vpreds, values, returns, mask, cliprange_value, agg_mode, seg_rows=0):
+def _(vpreds, values, returns, mask, cliprange_value, agg_mode, seg_rows=0, seg_off=None):
     B = vpreds.numel() // vpreds.shape[-1] if vpreds.dim() > 1 else 1
-    return (vpreds.new_empty(_vloss_out_shape(B, seg_rows), dtype=_F32),
-            vpreds.new_empty(B * 8 + 8 + _n_seg(B, seg_rows), dtype=_F64))
+    return (vpreds.new_empty(_loss_out_shape(B, seg_rows, seg_off, L.VA_VLOSS_NOUT), dtype=_F32),
+            vpreds.new_empty(B * 8 + 8 + _n_seg(B, seg_rows, seg_off), dtype=_F64))
 
 
 @_op("value_loss_bwd")
 def value_loss_bwd(g_out: Tensor, vpreds: Tensor, values: Tensor, returns: Tensor, mask: Tensor, ws: Tensor,
-                   cliprange_value: float, agg_mode: int, seg_rows: int = 0) -> Tensor:
+                   cliprange_value: float, agg_mode: int, seg_rows: int = 0,
+                   seg_off: Optional[Tensor] = None) -> Tensor:
     _check_f32(g_out, vpreds, values, returns)
     B, R = _rows(vpreds)
-    if g_out.shape != _vloss_out_shape(B, seg_rows):
-        raise ValueError(f"value_loss_bwd: g_out shape {tuple(g_out.shape)} != {_vloss_out_shape(B, seg_rows)}")
+    _check_seg_off(seg_off, B)
+    want = _loss_out_shape(B, seg_rows, seg_off, L.VA_VLOSS_NOUT)
+    if g_out.shape != want:
+        raise ValueError(f"value_loss_bwd: g_out shape {tuple(g_out.shape)} != {want}")
     d = torch.empty_like(vpreds)
     L.call("va_value_loss_bwd", K._p(g_out), K._p(vpreds), K._p(values), K._p(returns), K._p(mask), _mcode(mask), B,
-           R, cliprange_value, agg_mode, seg_rows, K._p(ws), K._p(d), K._stream(vpreds))
+           R, cliprange_value, agg_mode, seg_rows, K._p(seg_off), _n_seg(B, seg_rows, seg_off), K._p(ws), K._p(d),
+           K._stream(vpreds))
     return d
 
 
 @value_loss_bwd.register_fake
-def _(g_out, vpreds, values, returns, mask, ws, cliprange_value, agg_mode, seg_rows=0):
+def _(g_out, vpreds, values, returns, mask, ws, cliprange_value, agg_mode, seg_rows=0, seg_off=None):
     return torch.empty_like(vpreds)
 
 
 def _vloss_setup(ctx, inputs, output):
-    vpreds, values, returns, mask, c, agg, seg_rows = inputs
+    vpreds, values, returns, mask, c, agg, seg_rows, seg_off = inputs
     ctx.mark_non_differentiable(output[1])
-    ctx.save_for_backward(vpreds, values, returns, mask, output[1])
+    ctx.save_for_backward(vpreds, values, returns, mask, output[1], seg_off)
     ctx.cfg = (c, agg, seg_rows)
 
 
 def _vloss_backward(ctx, g_out, g_ws):
-    vpreds, values, returns, mask, ws = ctx.saved_tensors
+    vpreds, values, returns, mask, ws, seg_off = ctx.saved_tensors
     c, agg, seg_rows = ctx.cfg
     d = torch.ops.verl_amd.value_loss_bwd(g_out.float().contiguous(), vpreds, values, returns, mask, ws, c, agg,
-                                          seg_rows)
-    return d, None, None, None, None, None, None
+                                          seg_rows, seg_off)
+    return d, None, None, None, None, None, None, None
 
 
 value_loss_fwd.register_autograd(_vloss_backward, setup_context=_vloss_setup)

@@ -271,6 +271,7 @@ def fused_policy_loss(
     selection=None,
     mode_coef: float = 0.0,
     seg_rows: int = 0,
+    seg_off=None,
 ) -> torch.Tensor:
     """Fused compute_policy_loss (or a registered variant: gpg / clip_cov / kl_cov) +
     agg_loss(kl_penalty) + agg_loss(entropy) (dp_actor.py:419-459).
@@ -280,6 +281,8 @@ def fused_policy_loss(
     ``selection`` is the variant's token selection ([B, R] bool / uint8, clip_cov / kl_cov).
     ``seg_rows`` in (0, B): the rows are S = ceil(B / seg_rows) consecutive loss micro-batches, each
     aggregated on its own (the reference's per-micro-batch agg_loss), and the result is [S, 8].
+    ``seg_off`` (S + 1 ascending row offsets from 0 to B; list, array or int32 device tensor) gives S
+    segments of any sizes instead.
     """
     assert clip_ratio_c > 1.0, (
         "The lower bound of the clip_ratio_c for dual-clip PPO should be greater than 1.0,"
@@ -302,25 +305,36 @@ def fused_policy_loss(
     out, _ = torch.ops.verl_amd.ppo_loss_fwd(
         _f32(old_log_prob), _f32(log_prob), _f32(advantages), m, _f32(ref_log_prob), _f32(entropy), sel,
         1.0 - clip_ratio_low, 1.0 + clip_ratio_high, float(clip_ratio_c), AGG_MODES[loss_agg_mode], kl_type,
-        POLICY_LOSS_MODES[loss_mode], float(mode_coef), int(seg_rows),
+        POLICY_LOSS_MODES[loss_mode], float(mode_coef), int(seg_rows), seg_offsets(seg_off, log_prob.device),
     )
     return out
 
 
+def seg_offsets(seg_off, device):
+    """Loss micro-batch row offsets as the contiguous int32 device tensor the loss ops take (None
+    stays None). A host list / array goes up asynchronously through pinned memory."""
+    if seg_off is None:
+        return None
+    if isinstance(seg_off, torch.Tensor) and seg_off.is_cuda:
+        return seg_off.to(torch.int32).contiguous()
+    return h2d(np.asarray(seg_off, dtype=np.int32), np.int32, device)
+
+
 # =============================================================================== value loss (critic)
 def fused_value_loss(vpreds, values, returns, response_mask, cliprange_value: float,
-                     loss_agg_mode: str = "token-mean", seg_rows: int = 0) -> torch.Tensor:
+                     loss_agg_mode: str = "token-mean", seg_rows: int = 0, seg_off=None) -> torch.Tensor:
     """compute_value_loss (core_algos.py:992-1031) + masked_mean(vpreds) in one fused kernel pair.
     Returns the 4-slot vector VA_VLOSS_* (vf_loss, vf_clipfrac, vpred_mean, n_tokens); gradients
     flow from slots LOSS and VPRED_MEAN to vpreds (bf16 vpreds are upcast exactly, as the
     reference's mixed-dtype ops promote them). ``seg_rows`` in (0, B): [S, 4], one row per loss
-    micro-batch of seg_rows rows (as fused_policy_loss)."""
+    micro-batch of seg_rows rows or of the seg_off row ranges (as fused_policy_loss)."""
     if loss_agg_mode not in AGG_MODES:
         raise ValueError(f"Invalid loss_agg_mode: {loss_agg_mode}")
     _require_device(vpreds, values, returns, response_mask)
     m, _ = _mask(response_mask)
     out, _ = torch.ops.verl_amd.value_loss_fwd(_f32(vpreds), _f32(values), _f32(returns), m, float(cliprange_value),
-                                               AGG_MODES[loss_agg_mode], int(seg_rows))
+                                               AGG_MODES[loss_agg_mode], int(seg_rows),
+                                               seg_offsets(seg_off, vpreds.device))
     return out
 
 

@@ -274,13 +274,14 @@ def compute_policy_loss(old_log_prob, log_prob, advantages, response_mask, clipr
 
 def compute_actor_loss(old_log_prob, log_prob, advantages, response_mask, clip_ratio_low, clip_ratio_high,
                        clip_ratio_c=3.0, loss_agg_mode="token-mean", entropy=None, ref_log_prob=None,
-                       kl_loss_type=None, seg_rows=0):
+                       kl_loss_type=None, seg_rows=0, seg_off=None):
     """The fused form the actor uses (dp_actor.py:421-461): one kernel for the clipped policy
     loss, the three metrics, agg_loss(kl_penalty) and agg_loss(entropy). Returns the 8-slot
-    vector (VA_LOSS_*), or [S, 8] for S loss micro-batches of ``seg_rows`` rows each."""
+    vector (VA_LOSS_*), or [S, 8] for S loss micro-batches (``seg_rows`` rows each, or the row
+    ranges of the ``seg_off`` offsets)."""
     return K.fused_policy_loss(old_log_prob, log_prob, advantages, response_mask, clip_ratio_low, clip_ratio_high,
                                clip_ratio_c, loss_agg_mode, ref_log_prob=ref_log_prob, kl_loss_type=kl_loss_type,
-                               entropy=entropy, seg_rows=seg_rows)
+                               entropy=entropy, seg_rows=seg_rows, seg_off=seg_off)
 
 
 def _variant_loss(old_log_prob, log_prob, advantages, response_mask, loss_agg_mode, mode, selection=None, coef=0.0,

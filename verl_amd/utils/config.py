@@ -62,6 +62,8 @@ def actor_config(**overrides) -> AttrDict:
         fused_logprob_no_grad=False,
         # (verl_amd) responses per update forward/backward pass; None = ppo_micro_batch_size_per_gpu
         compute_micro_batch_size_per_gpu=None,
+        # (verl_amd) use_dynamic_bsz: tokens per update pass holding several token-budget micro-batches
+        compute_max_token_len_per_gpu=None,
         optim=AttrDict(lr=1e-6, weight_decay=0.01, betas=(0.9, 0.999), lr_warmup_steps=-1, lr_warmup_steps_ratio=0.0,
                        min_lr_ratio=0.0, num_cycles=0.5, warmup_style="constant", total_training_steps=-1),
     )

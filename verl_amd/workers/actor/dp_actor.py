@@ -247,6 +247,44 @@ class DataParallelPPOActor(BasePPOActor):
             return mb
         return int(cmb) // mb * mb
 
+    def _dynamic_passes(self, mini: DataProto, micro_batches: list, idx_lists: list, am, loss_mode: str):
+        """use_dynamic_bsz: consecutive token-budget micro-batches (in the reference's order) merged
+        into passes of at most compute_max_token_len_per_gpu tokens. Returns (pass batches, their
+        row index lists, per pass None or (int32 row offsets of its micro-batches on the device,
+        device fp32 rows_s / ppo_mini_batch_size)). Without the key or for registered loss variants:
+        the reference's micro-batches, one per pass."""
+        budget = self.config.get("compute_max_token_len_per_gpu", None)
+        none = [None] * len(micro_batches)
+        if not budget or loss_mode != "vanilla" or len(micro_batches) < 2:
+            return micro_batches, idx_lists, none
+        if am is None:  # padded path: no host copy yet (rearrange_micro_batches has synced already)
+            am = mini.batch["attention_mask"].cpu().numpy()
+        tokens = [int(am[np.asarray(ix, dtype=np.int64)].sum()) for ix in idx_lists]
+        groups, cur, cur_tok = [], [], 0
+        for j, t in enumerate(tokens):
+            if cur and cur_tok + t > budget:
+                groups.append(cur)
+                cur, cur_tok = [], 0
+            cur.append(j)
+            cur_tok += t
+        groups.append(cur)
+        dev = mini.batch["input_ids"].device
+        mini_rows = float(self.config.ppo_mini_batch_size)
+        out_mb, out_idx, out_seg = [], [], []
+        for g in groups:
+            if len(g) == 1:
+                out_mb.append(micro_batches[g[0]])
+                out_idx.append(idx_lists[g[0]])
+                out_seg.append(None)
+                continue
+            merged = [r for j in g for r in idx_lists[j]]
+            rows = [len(idx_lists[j]) for j in g]
+            out_mb.append(mini.select_idxs(np.asarray(merged, dtype=np.int64)))
+            out_idx.append(merged)
+            out_seg.append((K.seg_offsets(np.concatenate([[0], np.cumsum(rows)]), dev),
+                            K.h2d(np.asarray(rows, dtype=np.float32) / mini_rows, np.float32, dev)))
+        return out_mb, out_idx, out_seg
+
     # ------------------------------------------------------------------ forward
     def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False, packing: _Packing = None,
                              multi_modal_inputs=None):
@@ -445,19 +483,23 @@ class DataParallelPPOActor(BasePPOActor):
                     # dp_actor.py:382-384
                     max_token_len = cfg.ppo_max_token_len_per_gpu * self.ulysses_sequence_parallel_size
                     micro_batches, idx_lists = prepare_dynamic_batch(mini, max_token_len=max_token_len)
+                    micro_batches, idx_lists, seg_offs = self._dynamic_passes(mini, micro_batches, idx_lists, am,
+                                                                              loss_mode)
                     plans = self._plans(mini, idx_lists=idx_lists, am=am)
                 else:
                     seg_mb = int(cfg.ppo_micro_batch_size_per_gpu)
                     micro_batches = mini.split(self._pass_rows(loss_mode))
                     plans = self._plans(mini, [len(m) for m in micro_batches], am=am)
+                    seg_offs = [None] * len(micro_batches)
                 self._zero_grad()
-                for i, (mb, plan) in enumerate(zip(micro_batches, plans, strict=True)):
+                for i, (mb, plan, seg_off) in enumerate(zip(micro_batches, plans, seg_offs, strict=True)):
                     b = mb.batch
                     response_mask = b["response_mask"]
                     calc_ent = entropy_coeff != 0
                     entropy, log_prob = self._forward_micro_batch(b, temperature, calc_ent, plan, _multi_modal(mb))
                     m = {}
                     # several of the reference's loss micro-batches in this pass: aggregated one by one
+                    # (uniform runs of seg_mb rows, or the token-budget micro-batches' row ranges seg_off)
                     seg = seg_mb if not cfg.use_dynamic_bsz and len(mb) > seg_mb else 0
                     if loss_mode == "vanilla":
                         out = core_algos.compute_actor_loss(
@@ -465,6 +507,7 @@ class DataParallelPPOActor(BasePPOActor):
                             clip_c, agg_mode, entropy=entropy if calc_ent else None,
                             ref_log_prob=b["ref_log_prob"] if cfg.use_kl_loss else None,
                             kl_loss_type=cfg.kl_loss_type if cfg.use_kl_loss else None, seg_rows=seg,
+                            seg_off=None if seg_off is None else seg_off[0],
                         )
                         # [8] or [S, 8]: the slots below are scalars or one value per loss micro-batch
                         pg_loss, pg_clipfrac = out[..., L.VA_LOSS_PG], out[..., L.VA_LOSS_CLIPFRAC]
@@ -491,7 +534,10 @@ class DataParallelPPOActor(BasePPOActor):
                             policy_loss = policy_loss + kl_loss * cfg.kl_loss_coef
                             m["actor/kl_loss"] = kl_loss.detach()
                             m["actor/kl_coef"] = cfg.kl_loss_coef
-                    if cfg.use_dynamic_bsz:
+                    if cfg.use_dynamic_bsz and seg_off is not None:
+                        # each micro-batch's loss relative to the dynamic bsz: sum_s policy_loss_s * rows_s / mini
+                        loss = (policy_loss * seg_off[1]).sum()
+                    elif cfg.use_dynamic_bsz:
                         # relative to the dynamic bsz (dp_actor.py:465-467)
                         loss = policy_loss * (response_mask.shape[0] / cfg.ppo_mini_batch_size)
                     elif seg:
@@ -517,7 +563,7 @@ class DataParallelPPOActor(BasePPOActor):
                         "actor/ppo_kl": ppo_kl.detach(),
                         "actor/pg_clipfrac_lower": pg_clipfrac_lower.detach(),
                     })
-                    if seg:  # one metric entry per loss micro-batch, in order, as the reference appends
+                    if seg or seg_off is not None:  # one entry per loss micro-batch, in order (the reference's)
                         for k in range(pg_loss.shape[0]):
                             append_to_dict(dev_metrics, {
                                 key: (v[k] if isinstance(v, torch.Tensor) else v) for key, v in m.items()})
