@@ -209,3 +209,46 @@ def test_critic_worker_gae_step(family, lr):
         losses.append(float(np.mean(met["critic/vf_loss"])))
         assert met["critic/lr"] == lr
     assert losses[-1] < losses[0], losses
+
+
+def test_critic_dynamic_bsz_merged_passes_match_reference_micro_batches():
+    """use_dynamic_bsz with compute_max_token_len_per_gpu: the token-budget micro-batches merged into
+    larger passes (the fused value loss aggregating each by its row offsets) give the reference's
+    per-micro-batch vf_loss list and accumulated gradient (sum of vf_loss_s * rows_s / mini,
+    dp_critic.py:218-232), against one pass per micro-batch on an identical model copy."""
+    from verl_amd.utils.config import critic_config
+    from verl_amd.utils.model import build_qwen2_critic
+    from verl_amd.workers.critic import DataParallelPPOCritic
+
+    torch.manual_seed(0)
+    model = build_qwen2_critic("tiny", device=DEV, attn_implementation="sdpa")
+    model_ref = copy.deepcopy(model)
+    data = _batch(seed=12)
+    b = data.batch
+    S = b["input_ids"].shape[1]
+    g = torch.Generator(device=DEV).manual_seed(3)
+    b["values"] = torch.randn(b["response_mask"].shape, device=DEV, generator=g) * b["response_mask"]
+    b["returns"] = b["values"] + torch.randn(b["values"].shape, device=DEV, generator=g) * b["response_mask"]
+    grads, metrics = [], []
+    for m, merge in ((model_ref, None), (model, 100 * S)):
+        cfg = critic_config(ppo_mini_batch_size=8, ppo_micro_batch_size_per_gpu=None, use_dynamic_bsz=True,
+                            ppo_max_token_len_per_gpu=2 * S, grad_clip=1e9, cliprange_value=0.5,
+                            compute_max_token_len_per_gpu=merge)
+        critic = DataParallelPPOCritic(cfg, m, torch.optim.AdamW(m.parameters(), lr=1e-3))
+        got = {}
+
+        def capture(m=m, got=got):
+            for n, p in m.named_parameters():
+                got[n] = p.grad.detach().clone()
+            return torch.tensor(0.0, device=DEV)
+
+        critic._optimizer_step = capture
+        metrics.append(critic.update_critic(data))
+        grads.append(got)
+    ref_l, new_l = metrics[0]["critic/vf_loss"], metrics[1]["critic/vf_loss"]
+    assert len(ref_l) == len(new_l) > 2
+    assert np.allclose(new_l, ref_l, atol=1e-3, rtol=2e-2), (new_l, ref_l)
+    for n in grads[0]:
+        scale = grads[0][n].abs().max().item() + 1e-12
+        err = (grads[1][n] - grads[0][n]).abs().max().item()
+        assert err <= 5e-2 * scale + 1e-6, (n, err, scale)

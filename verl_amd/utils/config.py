@@ -94,6 +94,8 @@ def critic_config(**overrides) -> AttrDict:
         ulysses_sequence_parallel_size=1,
         # (verl_amd) responses per update forward/backward pass; None = ppo_micro_batch_size_per_gpu
         compute_micro_batch_size_per_gpu=None,
+        # (verl_amd) use_dynamic_bsz: tokens per update pass holding several token-budget micro-batches
+        compute_max_token_len_per_gpu=None,
         model=AttrDict(use_remove_padding=False, enable_gradient_checkpointing=True),
         optim=AttrDict(lr=1e-5, weight_decay=0.01, betas=(0.9, 0.999), lr_warmup_steps_ratio=0.0, min_lr_ratio=None,
                        warmup_style="constant", total_training_steps=-1),

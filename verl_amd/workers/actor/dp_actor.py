@@ -168,6 +168,46 @@ def _multi_modal(mb: DataProto):
     return None if v is None else list(v)
 
 
+def merge_dynamic_passes(config, mini: DataProto, micro_batches: list, idx_lists: list, am, enabled: bool = True):
+    """use_dynamic_bsz: consecutive token-budget micro-batches (in the reference's order,
+    seqlen_balancing.rearrange_micro_batches) merged into update passes of at most
+    ``config.compute_max_token_len_per_gpu`` tokens, for the actor and the critic. Returns (pass
+    batches, their row index lists, per pass None or (int32 row offsets of its micro-batches on the
+    device, device fp32 rows_s / ppo_mini_batch_size)). Without the key or with ``enabled`` False:
+    the reference's micro-batches, one per pass."""
+    budget = config.get("compute_max_token_len_per_gpu", None)
+    none = [None] * len(micro_batches)
+    if not budget or not enabled or len(micro_batches) < 2:
+        return micro_batches, idx_lists, none
+    if am is None:  # padded path: no host copy yet (rearrange_micro_batches has synced already)
+        am = mini.batch["attention_mask"].cpu().numpy()
+    tokens = [int(am[np.asarray(ix, dtype=np.int64)].sum()) for ix in idx_lists]
+    groups, cur, cur_tok = [], [], 0
+    for j, t in enumerate(tokens):
+        if cur and cur_tok + t > budget:
+            groups.append(cur)
+            cur, cur_tok = [], 0
+        cur.append(j)
+        cur_tok += t
+    groups.append(cur)
+    dev = mini.batch["input_ids"].device
+    mini_rows = float(config.ppo_mini_batch_size)
+    out_mb, out_idx, out_seg = [], [], []
+    for g in groups:
+        if len(g) == 1:
+            out_mb.append(micro_batches[g[0]])
+            out_idx.append(idx_lists[g[0]])
+            out_seg.append(None)
+            continue
+        merged = [r for j in g for r in idx_lists[j]]
+        rows = [len(idx_lists[j]) for j in g]
+        out_mb.append(mini.select_idxs(np.asarray(merged, dtype=np.int64)))
+        out_idx.append(merged)
+        out_seg.append((K.seg_offsets(np.concatenate([[0], np.cumsum(rows)]), dev),
+                        K.h2d(np.asarray(rows, dtype=np.float32) / mini_rows, np.float32, dev)))
+    return out_mb, out_idx, out_seg
+
+
 class DataParallelPPOActor(BasePPOActor):
     def __init__(self, config, actor_module: nn.Module, actor_optimizer: torch.optim.Optimizer = None,
                  grad_reducer=None):
@@ -247,43 +287,6 @@ class DataParallelPPOActor(BasePPOActor):
             return mb
         return int(cmb) // mb * mb
 
-    def _dynamic_passes(self, mini: DataProto, micro_batches: list, idx_lists: list, am, loss_mode: str):
-        """use_dynamic_bsz: consecutive token-budget micro-batches (in the reference's order) merged
-        into passes of at most compute_max_token_len_per_gpu tokens. Returns (pass batches, their
-        row index lists, per pass None or (int32 row offsets of its micro-batches on the device,
-        device fp32 rows_s / ppo_mini_batch_size)). Without the key or for registered loss variants:
-        the reference's micro-batches, one per pass."""
-        budget = self.config.get("compute_max_token_len_per_gpu", None)
-        none = [None] * len(micro_batches)
-        if not budget or loss_mode != "vanilla" or len(micro_batches) < 2:
-            return micro_batches, idx_lists, none
-        if am is None:  # padded path: no host copy yet (rearrange_micro_batches has synced already)
-            am = mini.batch["attention_mask"].cpu().numpy()
-        tokens = [int(am[np.asarray(ix, dtype=np.int64)].sum()) for ix in idx_lists]
-        groups, cur, cur_tok = [], [], 0
-        for j, t in enumerate(tokens):
-            if cur and cur_tok + t > budget:
-                groups.append(cur)
-                cur, cur_tok = [], 0
-            cur.append(j)
-            cur_tok += t
-        groups.append(cur)
-        dev = mini.batch["input_ids"].device
-        mini_rows = float(self.config.ppo_mini_batch_size)
-        out_mb, out_idx, out_seg = [], [], []
-        for g in groups:
-            if len(g) == 1:
-                out_mb.append(micro_batches[g[0]])
-                out_idx.append(idx_lists[g[0]])
-                out_seg.append(None)
-                continue
-            merged = [r for j in g for r in idx_lists[j]]
-            rows = [len(idx_lists[j]) for j in g]
-            out_mb.append(mini.select_idxs(np.asarray(merged, dtype=np.int64)))
-            out_idx.append(merged)
-            out_seg.append((K.seg_offsets(np.concatenate([[0], np.cumsum(rows)]), dev),
-                            K.h2d(np.asarray(rows, dtype=np.float32) / mini_rows, np.float32, dev)))
-        return out_mb, out_idx, out_seg
 
     # ------------------------------------------------------------------ forward
     def _forward_micro_batch(self, micro_batch, temperature, calculate_entropy=False, packing: _Packing = None,
@@ -483,8 +486,9 @@ class DataParallelPPOActor(BasePPOActor):
                     # dp_actor.py:382-384
                     max_token_len = cfg.ppo_max_token_len_per_gpu * self.ulysses_sequence_parallel_size
                     micro_batches, idx_lists = prepare_dynamic_batch(mini, max_token_len=max_token_len)
-                    micro_batches, idx_lists, seg_offs = self._dynamic_passes(mini, micro_batches, idx_lists, am,
-                                                                              loss_mode)
+                    # registered loss variants draw their token selection per micro-batch: never merged
+                    micro_batches, idx_lists, seg_offs = merge_dynamic_passes(cfg, mini, micro_batches, idx_lists, am,
+                                                                              loss_mode == "vanilla")
                     plans = self._plans(mini, idx_lists=idx_lists, am=am)
                 else:
                     seg_mb = int(cfg.ppo_micro_batch_size_per_gpu)

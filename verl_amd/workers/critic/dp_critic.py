@@ -27,7 +27,7 @@ from ...protocol import DataProto
 from ...utils.seqlen_balancing import prepare_dynamic_batch, restore_dynamic_batch
 from ..actor import attention
 from ..actor.dp_actor import (_mm_kwargs, _multi_modal, _plan_packing, _to_host, append_to_dict, clip_grad_norm,
-                              hf_packed_hidden, step_unless_nonfinite)
+                              hf_packed_hidden, merge_dynamic_passes, step_unless_nonfinite)
 from .base import BasePPOCritic
 
 __all__ = ["DataParallelPPOCritic"]
@@ -182,13 +182,16 @@ class DataParallelPPOCritic(BasePPOCritic):
                 if cfg.use_dynamic_bsz:
                     max_token_len = cfg.ppo_max_token_len_per_gpu * self.ulysses_sequence_parallel_size
                     micro_batches, idx_lists = prepare_dynamic_batch(mini, max_token_len=max_token_len)
+                    micro_batches, idx_lists, seg_offs = merge_dynamic_passes(cfg, mini, micro_batches, idx_lists,
+                                                                              None)
                     plans = self._plans(mini, idx_lists=idx_lists)
                 else:
                     self.gradient_accumulation = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
                     micro_batches = mini.split(self._pass_rows())
                     plans = self._plans(mini, [len(m) for m in micro_batches])
+                    seg_offs = [None] * len(micro_batches)
                 self._zero_grad()
-                for i, (mb, plan) in enumerate(zip(micro_batches, plans, strict=True)):
+                for i, (mb, plan, seg_off) in enumerate(zip(micro_batches, plans, seg_offs, strict=True)):
                     b = mb.batch
                     response_mask = b["response_mask"]
                     vpreds = self._forward_micro_batch(b, plan, _multi_modal(mb))
@@ -196,9 +199,12 @@ class DataParallelPPOCritic(BasePPOCritic):
                     seg = (int(cfg.ppo_micro_batch_size_per_gpu)
                            if not cfg.use_dynamic_bsz and len(mb) > int(cfg.ppo_micro_batch_size_per_gpu) else 0)
                     out = K.fused_value_loss(vpreds, b["values"], b["returns"], response_mask, cfg.cliprange_value,
-                                             cfg.loss_agg_mode, seg_rows=seg)
+                                             cfg.loss_agg_mode, seg_rows=seg,
+                                             seg_off=None if seg_off is None else seg_off[0])
                     vf_loss = out[..., L.VA_VLOSS_LOSS]  # scalar, or one value per loss micro-batch
-                    if cfg.use_dynamic_bsz:
+                    if cfg.use_dynamic_bsz and seg_off is not None:
+                        loss = (vf_loss * seg_off[1]).sum()  # sum_s vf_loss_s * rows_s / mini (dp_critic.py:226)
+                    elif cfg.use_dynamic_bsz:
                         loss = vf_loss * (response_mask.shape[0] / cfg.ppo_mini_batch_size)
                     elif seg:
                         loss = (vf_loss / self.gradient_accumulation).sum()
@@ -210,7 +216,7 @@ class DataParallelPPOCritic(BasePPOCritic):
                     if self.grad_reducer is not None:
                         self.grad_reducer.after_backward()
                     met = out.detach()
-                    for row in (met if seg else [met]):  # one metric entry per loss micro-batch, in order
+                    for row in (met if seg or seg_off is not None else [met]):  # one entry per loss micro-batch
                         append_to_dict(dev_metrics, {
                             "critic/vf_loss": row[L.VA_VLOSS_LOSS],
                             "critic/vf_clipfrac": row[L.VA_VLOSS_CLIPFRAC],
