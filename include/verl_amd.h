@@ -378,6 +378,16 @@ int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *
  * the reference leaves this GEMM's layout to FSDP / autograd, dp_actor.py:465-470). */
 int va_transpose_16(const void *in, int64_t ld_in, int64_t R, int64_t C, void *out, int64_t ld_out, void *stream);
 
+/* weight_grad: dW [M, N] bf16 (row-major, contiguous) = dY [K, M]^T X [K, N] (row strides ldy / ldx,
+ * bf16, fp32 accumulation), the backward weight gradient of the backbone's linear layers (K = packed
+ * tokens; no reference counterpart: torch's linear backward under FSDP, dp_actor.py:465-470). K a
+ * multiple of 32; M, N, strides multiples of 8; 16-byte aligned buffers. splits > 1 cuts K into that
+ * many slices (fp32 partials in workspace = va_weight_grad_workspace_bytes(M, N, splits), summed in
+ * slice order, rounded once). Not a §8 row. */
+int64_t va_weight_grad_workspace_bytes(int64_t M, int64_t N, int splits);
+int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_t ldx, int64_t K, int64_t M, int64_t N,
+                   int splits, float *workspace, void *out, void *stream);
+
 /* ---------------------------------------------------------------------------------------
  * Fused lm_head + log-prob + entropy forward (the reference's use_fused_kernels
  * path, utils/kernel/kernels.py:120-663 + linear_cross_entropy.py:40-117): for hidden [N, H]

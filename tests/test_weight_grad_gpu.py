@@ -1,0 +1,77 @@
+"""va_weight_grad (csrc/wgrad.hip): dW = dY^T X of the backbone's linear layers against an fp32
+torch reference, across split-K counts, ragged M / N (clamped columns), strided operands, the
+product dispatch (kernels.weight_grad) and run-to-run determinism."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _call(dy, x, splits):
+    from verl_amd import _lib as L
+    from verl_amd import kernels as K
+
+    T, M = dy.shape
+    N = x.shape[1]
+    out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+    nb = L.load().va_weight_grad_workspace_bytes(M, N, splits)
+    ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=DEV)
+    L.call("va_weight_grad", K._p(dy), dy.stride(0), K._p(x), x.stride(0), T, M, N, splits, K._p(ws), K._p(out),
+           K._stream(dy))
+    return out
+
+
+def _ref(dy, x):
+    return torch.mm(dy.t().float(), x.float())
+
+
+def _check(got, want):
+    scale = want.abs().max().item()
+    err = (got.float() - want).abs().max().item()
+    assert err <= 8e-3 * scale + 1e-6, (err, scale)
+
+
+@pytest.mark.parametrize("T,M,N", [(2048, 1152, 896), (4096, 896, 4864), (1024, 200, 136), (96, 264, 512)])
+@pytest.mark.parametrize("splits", [1, 3, 8])
+def test_weight_grad_matches_fp32_reference(T, M, N, splits):
+    g = torch.Generator(device=DEV).manual_seed(T + M + N)
+    dy = (torch.randn(T, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
+    got = _call(dy, x, splits)
+    assert not torch.isnan(got.float()).any()
+    _check(got, _ref(dy, x))
+    assert torch.equal(got, _call(dy, x, splits))  # deterministic
+
+
+def test_weight_grad_strided_operands_and_zero_tokens():
+    g = torch.Generator(device=DEV).manual_seed(5)
+    wide = torch.randn(512, 1024, device=DEV, generator=g).to(torch.bfloat16)
+    dy, x = wide[:, :256], wide[:, 512:768]  # row stride 1024, 16-byte aligned column offsets
+    _check(_call(dy, x, 2), _ref(dy, x))
+    z = _call(dy[:0], x[:0], 1)
+    assert torch.equal(z, torch.zeros_like(z))
+
+
+def test_weight_grad_rejects_bad_shapes():
+    from verl_amd import _lib as L
+
+    dy = torch.zeros(100, 64, dtype=torch.bfloat16, device=DEV)  # 100 tokens: not a multiple of 32
+    x = torch.zeros(100, 64, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(RuntimeError, match="multiple of 32"):
+        _call(dy, x, 1)
+
+
+def test_product_dispatch_uses_it_and_falls_back():
+    """kernels.weight_grad: the own kernel for bf16 [T % 32 == 0] operands (same bits as the direct
+    call at the chosen split), hipBLASLt otherwise (T not a multiple of 32)."""
+    from verl_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(9)
+    dy = (torch.randn(4096, 1152, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    x = torch.randn(4096, 896, device=DEV, generator=g).to(torch.bfloat16)
+    got = K.weight_grad(dy, x)
+    assert torch.equal(got, _call(dy, x, K.own_wgrad_splits(1152, 896)))
+    odd = K.weight_grad(dy[:4000], x[:4000])  # hipBLASLt path
+    _check(odd, _ref(dy[:4000], x[:4000]))

@@ -53,12 +53,13 @@ def main():
     ap.add_argument("--cases", nargs="*", default=list(CASES))
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--variants", type=int, nargs="*", default=[0, 1], help="0: 64-token steps, 2 buffers; 1: ring")
     args = ap.parse_args()
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "wgrad", "libwg256.so"))
     lib.wg256_bf16.restype = ctypes.c_int
     lib.wg256_bf16.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
-                               ctypes.c_void_p]
+                               ctypes.c_void_p, ctypes.c_int]
     lib.wg256_workspace_bytes.restype = ctypes.c_int64
     lib.wg256_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
     from verl_amd import kernels as K
@@ -81,22 +82,24 @@ def main():
                "product_tflops": round(flops / prod_us / 1e6, 1), "product_rel_err": prod_err}
         out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
         s_ = torch.cuda.current_stream(dev).cuda_stream
-        for sp in splits_list:
-            ws_b = lib.wg256_workspace_bytes(M, N, sp)
-            ws = torch.empty(max(ws_b // 4, 1), dtype=torch.float32, device=dev)
+        for var in args.variants:
+            for sp in splits_list:
+                ws_b = lib.wg256_workspace_bytes(M, N, sp)
+                ws = torch.empty(max(ws_b // 4, 1), dtype=torch.float32, device=dev)
 
-            def run(sp=sp, ws=ws):
-                rc = lib.wg256_bf16(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), Kt, M, N, sp,
-                                    ws.data_ptr(), out.data_ptr(), s_)
-                assert rc == 0, rc
+                def run(sp=sp, ws=ws, var=var):
+                    rc = lib.wg256_bf16(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), Kt, M, N, sp,
+                                        ws.data_ptr(), out.data_ptr(), s_, var)
+                    assert rc == 0, rc
 
-            run()
-            torch.cuda.synchronize()
-            err = (out.float() - ref).abs().max().item() / scale
-            us = timed(run, args.iters, args.reps)
-            rec[f"s{sp}_us"] = round(us, 1)
-            rec[f"s{sp}_tflops"] = round(flops / us / 1e6, 1)
-            rec[f"s{sp}_rel_err"] = err
+                out.zero_()
+                run()
+                torch.cuda.synchronize()
+                err = (out.float() - ref).abs().max().item() / scale
+                us = timed(run, args.iters, args.reps)
+                rec[f"v{var}s{sp}_us"] = round(us, 1)
+                rec[f"v{var}s{sp}_tflops"] = round(flops / us / 1e6, 1)
+                rec[f"v{var}s{sp}_rel_err"] = err
         print(json.dumps(rec), flush=True)
         del dy, x, ref, prod, out
         torch.cuda.empty_cache()

@@ -109,6 +109,8 @@ _SIGNATURES: dict[str, tuple] = {
     "va_karmarkar_karp": (c_int, [_P, c_int64, c_int64, c_int, _P, _P]),
     "va_rope_qkv_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, c_int64, _P]),
     "va_transpose_16": (c_int, [_P, c_int64, c_int64, c_int64, _P, c_int64, _P]),
+    "va_weight_grad_workspace_bytes": (c_int64, [c_int64, c_int64, c_int]),
+    "va_weight_grad": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int64, c_int64, c_int, _P, _P, _P]),
 }
 
 _lib = None

@@ -714,10 +714,46 @@ def wgrad_splits(T: int, n_out: int, n_in: int) -> int:
 
 WGRAD_SWAP_MIN_OUT = 65536  # the lm_head (V = 151,936 outputs)
 
+# the backbone weight gradients through va_weight_grad (csrc/wgrad.hip, 256 x 256 tiles, 4-deep LDS-DMA
+# ring) instead of hipBLASLt: at 151,552 tokens gate|up 2,956 -> 2,699 us, down 1,624 -> 1,437, q|k|v
+# 443 -> 376, o 316 -> 305 (tools/wgrad256_bench.py, profiles/r03/wgrad256_probe.jsonl).
+# VERL_AMD_WGRAD=hipblaslt keeps hipBLASLt (A/B runs).
+_OWN_WGRAD = os.environ.get("VERL_AMD_WGRAD", "own") != "hipblaslt"
+
+
+def own_wgrad_splits(n_out: int, n_in: int) -> int:
+    """K slices of va_weight_grad: one round of workgroups when it fills >= 85 % of the 256 CUs
+    (down 3, q|k|v 12, o 16 at H = 896), else about three full rounds (gate|up: 152 tiles x 5)."""
+    tiles = -(-n_out // 256) * -(-n_in // 256)
+    one = 256 // tiles
+    if one >= 1 and tiles * one >= 0.85 * 256:
+        return one
+    return max(1, round(768 / tiles))
+
+
+def _own_weight_grad(dy2, x2):
+    """dY^T X by va_weight_grad, or None when the operands do not fit it (then hipBLASLt)."""
+    T, n_out = dy2.shape
+    n_in = x2.shape[1]
+    if (not _OWN_WGRAD or not dy2.is_cuda or dy2.dtype != torch.bfloat16 or x2.dtype != torch.bfloat16
+            or T % 32 or n_out % 8 or n_in % 8 or n_out >= WGRAD_SWAP_MIN_OUT or dy2.stride(1) != 1
+            or x2.stride(1) != 1 or dy2.stride(0) % 8 or x2.stride(0) % 8 or (dy2.data_ptr() | x2.data_ptr()) % 16):
+        return None
+    s = own_wgrad_splits(n_out, n_in)
+    out = torch.empty(n_out, n_in, dtype=torch.bfloat16, device=dy2.device)
+    nb = L.load().va_weight_grad_workspace_bytes(n_out, n_in, s)
+    ws = torch.empty(nb // 4, dtype=torch.float32, device=dy2.device) if nb else None
+    L.call("va_weight_grad", _p(dy2), dy2.stride(0), _p(x2), x2.stride(0), T, n_out, n_in, s, _p(ws), _p(out),
+           _stream(dy2))
+    return out
+
 
 def weight_grad(dy2, x2):
     T, n_out = dy2.shape
     n_in = x2.shape[1]
+    own = _own_weight_grad(dy2, x2)
+    if own is not None:
+        return own
     if n_out >= WGRAD_SWAP_MIN_OUT and dy2.is_cuda and dy2.dtype == x2.dtype == torch.bfloat16:
         # the lm_head: dW^T = X^T dY then one 16-bit transpose of the [n_in, V] result runs 36.5 vs
         # 37.7 ms at 131,072 rows (tools/wgrad_swap_bench.py, profiles/r02/wgrad_swap_layout.log);
