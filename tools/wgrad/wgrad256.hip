@@ -268,7 +268,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad256_ring_kernel(const uint16_t *__
 
 // Ring variant 2: the transposed reads as inline asm (tr_read_asm), so the compiler neither drains
 // the DMA before them nor needs compile-time buffer offsets: a rolled step loop, fewer registers.
-template <bool PARTIAL>
+template <bool PARTIAL, int OPT = 0>
 __global__ __launch_bounds__(NT, 1) void wgrad256_ring2_kernel(const uint16_t *__restrict__ dy, int64_t ldy,
                                                                const uint16_t *__restrict__ x, int64_t ldx, int64_t K,
                                                                int M, int N, int splits, int64_t kslice,
@@ -326,6 +326,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad256_ring2_kernel(const uint16_t *_
       frag_asm(ia, ss, wm * 128 + 64, lane, a4, a5);
       frag_asm(ia, ss, wm * 128 + 96, lane, a6, a7);
       asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1));
+      if constexpr (OPT == 1) __builtin_amdgcn_s_setprio(1);
       const bf16x8 fb0 = join(b0, b1);
       bf16x8 fa = join(a0, a1);
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb0, acc[0][0], 0, 0, 0);
@@ -344,6 +345,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad256_ring2_kernel(const uint16_t *_
       fa = join(a6, a7);
       acc[3][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb0, acc[3][0], 0, 0, 0);
       acc[3][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb1, acc[3][1], 0, 0, 0);
+      if constexpr (OPT == 1) __builtin_amdgcn_s_setprio(0);
     }
   }
 
@@ -404,8 +406,10 @@ extern "C" int wg256_bf16(const void *dy, int64_t ldy, const void *x, int64_t ld
   const int64_t kslice = (steps + splits - 1) / splits * bk;
   const int nwg = static_cast<int>(((M + BM - 1) / BM) * ((N + BN - 1) / BN) * splits);
   if (variant >= 1) {
-    auto kern = splits == 1 ? (variant == 2 ? wgrad256_ring2_kernel<false> : wgrad256_ring_kernel<false>)
-                            : (variant == 2 ? wgrad256_ring2_kernel<true> : wgrad256_ring_kernel<true>);
+    auto kern = splits == 1 ? (variant == 3 ? wgrad256_ring2_kernel<false, 1>
+                               : variant == 2 ? wgrad256_ring2_kernel<false, 0> : wgrad256_ring_kernel<false>)
+                            : (variant == 3 ? wgrad256_ring2_kernel<true, 1>
+                               : variant == 2 ? wgrad256_ring2_kernel<true, 0> : wgrad256_ring_kernel<true>);
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(NT), 0, st, static_cast<const uint16_t *>(dy), ldy,
                        static_cast<const uint16_t *>(x), ldx, K, static_cast<int>(M), static_cast<int>(N), splits,
                        kslice, splits == 1 ? nullptr : workspace,
