@@ -28,6 +28,13 @@ CASES = {  # (K tokens, M = n_out, N = n_in, splits to try)
     "qkv": (151552, 1152, 896, [8, 12, 16, 24, 32]),
     "o": (151552, 896, 896, [8, 16, 24, 32]),
     "lm_head": (131072, 151936, 896, [1, 2]),
+    # BASELINE configs 3 / 5 (Llama-3-8B, Qwen2.5-7B) at 32,768 tokens per pass: the product's split choice
+    "l8_gateup": (32768, 28672, 4096, [1]),
+    "l8_down": (32768, 4096, 14336, [1]),
+    "l8_qkv": (32768, 6144, 4096, [1, 2]),
+    "l8_o": (32768, 4096, 4096, [1, 3]),
+    "q7_gateup": (32768, 37888, 3584, [1]),
+    "q7_qkv": (32768, 4608, 3584, [1, 2]),
 }
 
 

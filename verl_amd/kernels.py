@@ -731,10 +731,18 @@ def own_wgrad_splits(n_out: int, n_in: int) -> int:
     return max(1, round(768 / tiles))
 
 
+# the shape class it was measured on: outputs of at most one round of 256 x 256 tiles (the H = 896
+# backbone: 16-152 tiles), where hipBLASLt leaves CUs idle or splits K in batched fp32 GEMMs; larger
+# outputs (the 7B / 8B configs' 1,000+ tiles) keep hipBLASLt
+WGRAD_OWN_MAX_TILES = 256
+
+
 def _own_weight_grad(dy2, x2):
     """dY^T X by va_weight_grad, or None when the operands do not fit it (then hipBLASLt)."""
     T, n_out = dy2.shape
     n_in = x2.shape[1]
+    if -(-n_out // 256) * -(-n_in // 256) > WGRAD_OWN_MAX_TILES:
+        return None
     if (not _OWN_WGRAD or not dy2.is_cuda or dy2.dtype != torch.bfloat16 or x2.dtype != torch.bfloat16
             or T % 32 or n_out % 8 or n_in % 8 or n_out >= WGRAD_SWAP_MIN_OUT or dy2.stride(1) != 1
             or x2.stride(1) != 1 or dy2.stride(0) % 8 or x2.stride(0) % 8 or (dy2.data_ptr() | x2.data_ptr()) % 16):
