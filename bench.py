@@ -161,8 +161,9 @@ def parse(argv=None):
     ap.add_argument("--gemm-table", default="default",
                     help="tuned GEMM solution table (verl_amd/tuned/*.csv, 'default', or 'none')")
     ap.add_argument("--model", default="0.5b")
-    ap.add_argument("--logprob-inplace-bwd", type=int, default=0,
-                    help="1: dlogits over the logits (reference's inplace_backward); 0: fresh buffer (faster stream)")
+    ap.add_argument("--logprob-inplace-bwd", type=int, default=2, choices=[0, 1, 2],
+                    help="1: dlogits over the logits (reference's inplace_backward); 0: fresh buffer (faster stream); "
+                         "2: fresh buffer when it fits in HBM, else over the logits")
     ap.add_argument("--old-noise", type=float, default=0.05,
                     help="old_log_probs = recomputed + N(0, s^2) (SURVEY §8d: ratios straddle the clip band)")
     ap.add_argument("--zero", type=int, default=0, choices=[0, 1],
@@ -179,6 +180,9 @@ def parse(argv=None):
                     help="response tokens per repetition of the CPU baseline's log-prob fwd+bwd sample")
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed repetitions (after 1 warm-up) of the CPU baseline")
     ap.add_argument("--out", default=None, help="also write the JSON line here")
+    ap.add_argument("--dump-state", default=None,
+                    help="rank 0 writes an .npz of the final fp32 masters (every 97th element, bucket order) and "
+                         "metrics: compares runs at different world sizes (tests/test_rehearsal_w8_gpu.py)")
     ap.add_argument("--tune", action="append", default=[],
                     help="KEY=VALUE va_set_tuning override for A/B runs (e.g. 8=0: grid-stride SwiGLU)")
     ap.add_argument("--launcher-check", action="store_true",
@@ -233,10 +237,8 @@ def cpu_baseline(args) -> dict:
     from oracle import reference_ops as ref
 
     affinity = len(os.sched_getaffinity(0))
-    # the box grants a CPU share (OMP_NUM_THREADS=16 there) while affinity lists every host CPU
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity
-    cores = min(cores, affinity)
-    torch.set_num_threads(cores)
+    quota, quota_src = cgroup_cpu_quota()
+    env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
     V = VOCAB
     rows = args.cpu_sample_rows
     g = torch.Generator().manual_seed(0)
@@ -269,23 +271,95 @@ def cpu_baseline(args) -> dict:
         loss.backward()
         return time.perf_counter() - t0
 
-    lp_pass()  # warm-up
-    algo_pass()
-    t_lp = sorted(lp_pass() for _ in range(args.cpu_reps))[args.cpu_reps // 2]
-    t_algo = sorted(algo_pass() for _ in range(args.cpu_reps))[args.cpu_reps // 2]
-    per_token = t_lp / rows + t_algo / (B * R)
+    def measure(threads):
+        torch.set_num_threads(threads)
+        lp_pass()  # warm-up
+        algo_pass()
+        t_lp = sorted(lp_pass() for _ in range(args.cpu_reps))[args.cpu_reps // 2]
+        t_algo = sorted(algo_pass() for _ in range(args.cpu_reps))[args.cpu_reps // 2]
+        return t_lp, t_algo, 1.0 / (t_lp / rows + t_algo / (B * R))
+
+    # thread counts (the affinity count): the CPU quota of the cgroup bounds what
+    # the threads can actually run on; when there is no quota, or one above the box's
+    # OMP_NUM_THREADS share, the affinity count is timed as planned AND that share, both reported
+    if quota is not None and quota <= affinity:
+        plans = [("cgroup_quota", max(1, int(quota)))]
+    else:
+        plans = [("affinity", affinity)]
+        if env_threads and env_threads < affinity:
+            plans.append(("omp_num_threads", env_threads))
+    runs = []
+    for label, threads in plans:
+        t_lp, t_algo, v = measure(threads)
+        runs.append({"threads": threads, "basis": label, "value": round(v, 1),
+                     "median_logprob_s": round(t_lp, 3), "median_algos_s": round(t_algo, 3)})
+    best = max(runs, key=lambda r: r["value"])
     return {
-        "value": round(1.0 / per_token, 1),
+        "value": best["value"],
         "unit": "tokens/s",
-        "cores": cores,
+        "cores": best["threads"],
         "kind": "port",
         "os_cpu_count": os.cpu_count(),
         "affinity_cpus": affinity,
+        "cgroup_cpu_quota": quota,
+        "cgroup_cpu_quota_source": quota_src,
+        "omp_num_threads_env": env_threads,
         "torch_threads": torch.get_num_threads(),
+        "runs": runs,
         "sample": (f"oracle log-prob+entropy fwd+bwd (autograd) of {rows} tokens x V={V} fp32 "
-                   f"(median {t_lp:.2f}s) + GRPO adv + clipped loss + k3 KL fwd/bwd on {B}x{R} "
-                   f"(median {t_algo:.2f}s); 1 warm-up + median of {args.cpu_reps}; model GEMMs excluded"),
+                   f"+ GRPO adv + clipped loss + k3 KL fwd/bwd on {B}x{R}; 1 warm-up + median of {args.cpu_reps} "
+                   f"per thread count; value = the faster thread count (runs lists each); model GEMMs excluded"),
     }
+
+
+def cgroup_cpu_quota():
+    """CPUs the process's cgroup may use (cpu.max quota / period, v2; cfs_quota_us / cfs_period_us,
+    v1), or None without a quota; with the file it came from."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, p = open(path).read().split()[:2]
+            return (None if q == "max" else int(q) / int(p)), f"{path}: {q} {p}"
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return (None if q < 0 else q / p), f"cgroup v1 cfs_quota_us {q} cfs_period_us {p}"
+    except (OSError, ValueError):
+        return None, "no cgroup cpu quota file readable"
+
+
+def master_sample(worker):
+    """Every 97th element of the fp32 master weights over the buckets in bucket order (padding
+    dropped; ZeRO shards all-gathered first, so every rank must call this)."""
+    import torch
+
+    from verl_amd.utils import comm
+
+    mgr = worker.actor.grad_reducer
+    parts = []
+    for i, b in enumerate(mgr.buckets):
+        n_real = sum(p.numel() for p in b.params)
+        if hasattr(mgr, "shards"):
+            full = torch.empty(b.buf.numel(), dtype=torch.float32, device=b.buf.device)
+            comm.all_gather_into(full, mgr.shards[i].detach(), mgr.group)
+        else:
+            full = mgr.master_bufs[i]
+        parts.append(full[:n_real][::97].detach().cpu())
+    return torch.cat(parts)
+
+
+def dump_state(path: str, init, worker, metrics, rank: int):
+    """rank 0 writes the master samples before the first and after the last step, and the final
+    metrics (comparison of world sizes, tests/test_rehearsal_w8_gpu.py)."""
+    import numpy as np
+
+    final = master_sample(worker)
+    if rank == 0:
+        m = metrics.meta_info["metrics"] if metrics is not None else {}
+        np.savez(path, masters_init=init.numpy(), masters=final.numpy(),
+                 **{k.replace("/", "__"): np.asarray(v, dtype=np.float64) for k, v in m.items()
+                    if isinstance(v, (list, float, int))})
 
 
 def shard_batch(args, rank: int, world: int, dev):
@@ -305,9 +379,9 @@ def shard_batch(args, rank: int, world: int, dev):
     dense = args.responses == "dense"
     if args.scaling == "weak":
         return make_grpo_batch(args.prompts, args.n, args.prompt_len, args.response_len, seed=1234 + rank,
-                               device=dev, dense_responses=dense, min_response=128)
+                               device=dev, dense_responses=dense, min_response=128, step_noise=True)
     full = make_grpo_batch(args.prompts, args.n, args.prompt_len, args.response_len, seed=1234,
-                           permute=args.balance, dense_responses=dense, min_response=128)
+                           permute=args.balance, dense_responses=dense, min_response=128, step_noise=True)
     B = len(full)
     if B % world:
         raise SystemExit(f"{B} responses do not split evenly over {world} ranks")
@@ -317,7 +391,6 @@ def shard_batch(args, rank: int, world: int, dev):
     else:
         shard = full.chunk(world)[rank]
         shard.reorder(torch.from_numpy(np.random.RandomState(1234 + rank).permutation(len(shard))))
-    shard.meta_info["global_token_num"] = shard.batch["attention_mask"].sum(-1).tolist()
     return shard.to(dev)
 
 
@@ -370,6 +443,8 @@ def main():
 
     from verl_amd import kernels as K
     from verl_amd.trainer.ppo.core_algos import AdvantageEstimator
+    from verl_amd.trainer.ppo.metric_utils import global_token_num
+    from verl_amd.utils import comm
     from verl_amd.utils.config import AttrDict, actor_config
     from verl_amd.utils.model import build_qwen2
     from verl_amd.workers.dp_workers import ActorWorker
@@ -403,7 +478,7 @@ def main():
             use_dynamic_bsz=args.dynamic_bsz > 0, ppo_max_token_len_per_gpu=args.dynamic_bsz or 16384,
             compute_max_token_len_per_gpu=args.compute_max_tokens or None,
             pack_pad_multiple=args.pad_multiple,
-            logprob_inplace_backward=bool(args.logprob_inplace_bwd),
+            logprob_inplace_backward={0: False, 1: True, 2: "auto"}[args.logprob_inplace_bwd],
             fused_logprob_no_grad=bool(args.fused_no_grad),
             wgrad_side_stream=bool(args.wgrad_stream),
             gemm_tuning_file=None if args.gemm_table in (None, "none") else args.gemm_table,
@@ -417,21 +492,27 @@ def main():
     worker.init_model(model, mixed_precision=not args.no_mixed_precision, zero=bool(args.zero))
     log(rank, f"model ready ({sum(p.numel() for p in model.parameters()) / 1e6:.1f}M params), world={world}, "
               f"{args.scaling} scaling, {B} responses on this rank")
+    init_sample = master_sample(worker) if args.dump_state else None
     batch = shard_batch(args, rank, world, dev)
     assert len(batch) == B, (len(batch), B)
-    # reference-policy log-probs are an input of the step (ref = new + N(0, 0.1^2))
-    gen = torch.Generator(device=dev).manual_seed(99 + rank)
+    # the whole batch's per-sequence token counts (ray_trainer.py:1208), gathered over the ranks
+    batch.meta_info["global_token_num"] = global_token_num(batch.batch["attention_mask"])
+    # reference-policy log-probs are an input of the step (ref = new + N(0, 0.1^2)); the
+    # N(0, 1) draws are per row of the global batch (make_grpo_batch step_noise), so the step's
+    # inputs do not depend on the number of ranks
+    old_noise = batch.batch.pop("old_noise")
+    ref_noise = batch.batch.pop("ref_noise")
     with torch.no_grad():
         lp0 = worker.compute_log_prob(batch).batch["old_log_probs"]
-        batch.batch["ref_log_prob"] = lp0 + 0.1 * torch.randn(lp0.shape, device=dev, generator=gen)
-    del lp0
+        batch.batch["ref_log_prob"] = lp0 + 0.1 * ref_noise
+    del lp0, ref_noise
 
     def step():
         out = worker.compute_log_prob(batch)
         old = out.batch["old_log_probs"]
         if args.old_noise:
             # old = new + N(0, 0.05^2) so the timed step exercises the clip branches
-            old = old + args.old_noise * torch.randn(old.shape, device=dev, generator=gen)
+            old = old + args.old_noise * old_noise
         batch.batch["old_log_probs"] = old
         worker.compute_advantage(batch, AdvantageEstimator.GRPO, norm_adv_by_std_in_grpo=True)
         return worker.update_actor(batch)
@@ -455,6 +536,9 @@ def main():
 
         prof = cProfile.Profile()
         prof.enable()
+    from verl_amd import custom_ops
+
+    fallbacks0 = custom_ops.AUTO_INPLACE_FALLBACKS
     t0 = time.perf_counter()
     metrics = None
     for i in range(args.steps):
@@ -467,9 +551,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    lp_fallbacks = custom_ops.AUTO_INPLACE_FALLBACKS - fallbacks0
     t = torch.tensor([elapsed, -elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    comm.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, fastest = float(t[0].item()), -float(t[1].item())
     ksum = K.TIMER.summary() if K.TIMER is not None else {}
     K.TIMER = None
@@ -477,20 +561,18 @@ def main():
     if world > 1:
         exposed_ms = worker.actor.grad_reducer.stop_timing()
         ex = torch.tensor([exposed_ms / args.steps], dtype=torch.float64, device=dev)
-        dist.all_reduce(ex, op=dist.ReduceOp.MAX)
+        comm.all_reduce(ex, op=dist.ReduceOp.MAX)
         comm = {"exposed_allreduce_ms_per_step": round(float(ex.item()), 3),
                 "isolated_allreduce_ms_per_step": round(worker.actor.grad_reducer.time_isolated_sync(), 3),
                 "grad_bytes": worker.actor.grad_reducer.grad_bytes(),
                 "backend": dist.get_backend()}
     del comm_timer
 
-    resp_tokens = int(batch.batch["response_mask"].sum().item())
-    total_tokens = torch.tensor([resp_tokens, sum(batch.meta_info["global_token_num"])], dtype=torch.float64,
-                                device=dev)
-    if world > 1:
-        dist.all_reduce(total_tokens)
-    tok_s = float(total_tokens[0].item()) * args.steps / elapsed
-    perf_throughput = float(total_tokens[1].item()) * args.steps / elapsed / world  # metric_utils.py:249-257
+    resp_tokens = torch.tensor([int(batch.batch["response_mask"].sum().item())], dtype=torch.float64, device=dev)
+    comm.all_reduce(resp_tokens)
+    tok_s = float(resp_tokens.item()) * args.steps / elapsed
+    # metric_utils.py:249-257: the whole batch's tokens per second per GPU
+    perf_throughput = sum(batch.meta_info["global_token_num"]) * args.steps / elapsed / world
 
     log(rank, f"timed region: {elapsed:.2f}s for {args.steps} steps")
     # after the timed region: every rank must hold the same model (FSDP's by-construction
@@ -501,6 +583,8 @@ def main():
                            metrics.meta_info["metrics"] if metrics is not None else {},
                            ["actor/grad_norm", "actor/lr"], elapsed - fastest)
     log(rank, f"replica check: {rcheck}")
+    if args.dump_state:
+        dump_state(args.dump_state, init_sample, worker, metrics, rank)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N = 1 only
         cpu = cpu_baseline(args)
@@ -515,7 +599,8 @@ def main():
             name, d = max(hbm.items(), key=lambda kv: kv[1]["time_ms_total"])
             traffic, src = pmc_traffic(name, d["avg_bytes"], VOCAB)
             per_row = 2 * 2 * VOCAB + 28 if name.endswith("bwd") else 2 * VOCAB + 20  # bf16 rows
-            ceil, ceil_src = hbm_ceiling(name, round(d["avg_bytes"] / per_row), bool(args.logprob_inplace_bwd))
+            ceil, ceil_src = hbm_ceiling(name, round(d["avg_bytes"] / per_row),
+                                         args.logprob_inplace_bwd == 1 or lp_fallbacks > 0)
             roof = {
                 "kernel": name, "bound": "hbm", "achieved": round(d["gbps"], 1), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(d["gbps"] / HBM_PEAK_GBPS, 4),
@@ -568,8 +653,10 @@ def main():
                                      else f"realistic: U[128, {R}]"),
                 "deviations_from_reference_defaults": (
                     _micro_text(micro, worker.actor._pass_rows("vanilla"), args)
-                    + ("out-of-place log-prob backward (reference: in place)" if not args.logprob_inplace_bwd
-                       else "in-place log-prob backward as the reference")
+                    + {0: "out-of-place log-prob backward (reference: in place)",
+                       1: "in-place log-prob backward as the reference",
+                       2: "out-of-place log-prob backward when its dlogits buffer fits in HBM, else in place as the "
+                          f"reference ({lp_fallbacks} in-place fallbacks in the timed steps)"}[args.logprob_inplace_bwd]
                     + ("; the no-grad old-logp pass runs the fused lm_head + log-prob kernel (the reference's "
                        "use_fused_kernels option, off by default there; same bf16-rounded logits, tests)"
                        if args.fused_no_grad else "")),
@@ -578,7 +665,8 @@ def main():
                 "logprob_max_token_len": (args.logprob_max_tokens or args.dynamic_bsz) if args.dynamic_bsz else None,
                 "peak_hbm_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
                 "pack_pad_multiple": args.pad_multiple,
-                "logprob_inplace_backward": bool(args.logprob_inplace_bwd),
+                "logprob_inplace_backward": {0: False, 1: True, 2: "auto"}[args.logprob_inplace_bwd],
+                "logprob_bwd_inplace_fallbacks": lp_fallbacks,
                 "fused_logprob_no_grad": bool(args.fused_no_grad),
                 "zero_sharded_optimizer": bool(args.zero),
                 "wgrad_side_stream": bool(args.wgrad_stream),

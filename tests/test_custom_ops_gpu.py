@@ -39,7 +39,7 @@ def test_opcheck_logprob_entropy():
     x = logits.clone().requires_grad_(True)
     _check(ops.logprob_entropy_fwd, (x, labels, 1.0, False))
     _check(ops.logprob_entropy_fwd, (logits.float().requires_grad_(True), labels, 0.7, False))
-    logp, ent, lse = ops.logprob_entropy_fwd(logits, labels, 1.0, False)
+    logp, ent, lse = ops.logprob_entropy_fwd(logits, labels, 1.0, 0)
     g = torch.randn_like(logp)
     _check(ops.logprob_entropy_bwd, (g, g, logits, labels, lse, ent, 1.0))
     _check(ops.logprob_entropy_bwd, (g, None, logits, labels, lse, ent, 1.0))

@@ -1,0 +1,26 @@
+"""Host-side argument checks and launch planning of the kernel wrappers (no GPU)."""
+
+import numpy as np
+import pytest
+
+from verl_amd import kernels as K
+
+
+@pytest.mark.parametrize("off", [[1, 4, 8], [0, 4, 4, 8], [0, 5, 3, 8], [0], [0, 4, 7]])
+def test_seg_offsets_rejects_bad_host_offsets(off):
+    """offsets not starting at 0, empty or descending segments, or not ending at the
+    row count would make the loss kernels read rows outside [0, B) and divide by zero."""
+    with pytest.raises(ValueError, match="seg_off"):
+        K.seg_offsets(np.asarray(off), "cpu", rows=8)
+
+
+def test_own_wgrad_splits_respect_k():
+    # H = 896 backbone shapes at the bench's token counts keep their measured plans
+    assert K.own_wgrad_splits(896, 896, 151552) == 16
+    assert K.own_wgrad_splits(9728, 896, 151552) == 5
+    # one 256 x 256 output at 512 tokens (16 K-steps): 2 slices, not 256
+    assert K.own_wgrad_splits(256, 256, 512) == 2
+    assert K.own_wgrad_splits(256, 256, 32) == 1
+    for tokens in (32, 256, 1024, 4096, 65536):
+        s = K.own_wgrad_splits(128, 896, tokens)
+        assert 1 <= s and (s == 1 or -(-tokens // 32) // s >= K.WGRAD_MIN_STEPS_PER_SLICE)

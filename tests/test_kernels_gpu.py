@@ -162,6 +162,46 @@ def test_logprob_inplace_backward(K):
     assert torch.equal(a.grad, leaf.grad)
 
 
+def test_logprob_auto_backward_falls_back_in_place_when_hbm_is_full(K):
+    """"auto" writes dlogits into a fresh buffer when the allocator can provide
+    it and over the logits (the reference's inplace_backward) when it cannot — here forced by
+    reserving all but ~1 GiB of HBM around a 2.4 GB logits tensor. Both give bitwise the in-place
+    result."""
+    from verl_amd import custom_ops
+
+    torch.manual_seed(4)
+    n, V = 8192, 151936  # 2.49 GB of bf16 logits
+    base = torch.randn(n, V, dtype=torch.bfloat16, device=DEV)
+    labels = torch.randint(0, V, (n,), device=DEV)
+    g = torch.randn(n, device=DEV)
+
+    def run(mode):
+        leaf = base.clone().requires_grad_(True)
+        logits = leaf * 1.0
+        lp, ent = K.logprob_entropy(logits, labels, 1.0, inplace_backward=mode)
+        (lp * g + 0.1 * ent).sum().backward()
+        return leaf.grad
+
+    want = run(True)
+    f0 = custom_ops.AUTO_INPLACE_FALLBACKS
+    assert torch.equal(run("auto"), want)  # room for the buffer: out of place
+    assert custom_ops.AUTO_INPLACE_FALLBACKS == f0
+    # the forward keeps base, leaf, logits and (later) leaf.grad: ~4 x 2.49 GB; leave ~1 GiB beyond
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info()
+    need = 3 * base.numel() * base.element_size()  # leaf + logits + leaf.grad
+    hog = torch.empty(max(0, free - need - (1 << 30)), dtype=torch.uint8, device=DEV)
+    try:
+        got = run("auto")
+    finally:
+        del hog
+        torch.cuda.empty_cache()
+    assert custom_ops.AUTO_INPLACE_FALLBACKS == f0 + 1
+    assert torch.equal(got, want)
+    with pytest.raises(ValueError, match="auto"):
+        K.logprob_entropy(base, labels, 1.0, inplace_backward="sometimes")
+
+
 # ------------------------------------------------------------------------------ policy loss
 def _policy_inputs(B, R, seed, mask_dtype=torch.int64, ties=True):
     g = torch.Generator().manual_seed(seed)

@@ -127,10 +127,21 @@ def _as_2d(t: torch.Tensor) -> tuple[int, int]:
 
 
 # =============================================================================== log-prob
-def logprob_entropy(logits, labels, temperature: float = 1.0, inplace_backward: bool = False):
+def _backward_mode(inplace_backward) -> int:
+    """True -> in place, False -> fresh buffer, "auto" -> fresh buffer when it fits, else in place."""
+    if isinstance(inplace_backward, str):
+        if inplace_backward != "auto":
+            raise ValueError(f"inplace_backward must be True, False or 'auto', got {inplace_backward!r}")
+        return 2
+    return 1 if inplace_backward else 0
+
+
+def logprob_entropy(logits, labels, temperature: float = 1.0, inplace_backward=False):
     """(log p[label], entropy) per row of ``logits[..., V]`` after the reference's
     ``logits.div_(temperature)``; one fused HBM pass forward, one backward
-    (torch.ops.verl_amd.logprob_entropy_fwd / _bwd, custom_ops.py)."""
+    (torch.ops.verl_amd.logprob_entropy_fwd / _bwd, custom_ops.py). ``inplace_backward``: True
+    writes dlogits over the logits (flash-attn semantics), False into a fresh buffer, "auto" into a
+    fresh buffer when the allocator can provide it and over the logits otherwise."""
     _require_device(logits, labels)
     V = logits.shape[-1]
     x = logits.reshape(-1, V)
@@ -144,7 +155,7 @@ def logprob_entropy(logits, labels, temperature: float = 1.0, inplace_backward: 
         raise ValueError(f"labels ({lab.shape[0]}) do not match logits rows ({x.shape[0]})")
     if x.dtype not in _DTYPE_CODES:
         raise TypeError(f"unsupported logits dtype {x.dtype}")
-    logp, ent, _ = torch.ops.verl_amd.logprob_entropy_fwd(x, lab, float(temperature), bool(inplace_backward))
+    logp, ent, _ = torch.ops.verl_amd.logprob_entropy_fwd(x, lab, float(temperature), _backward_mode(inplace_backward))
     out_shape = logits.shape[:-1]
     return logp.view(out_shape), ent.view(out_shape)
 
@@ -305,19 +316,29 @@ def fused_policy_loss(
     out, _ = torch.ops.verl_amd.ppo_loss_fwd(
         _f32(old_log_prob), _f32(log_prob), _f32(advantages), m, _f32(ref_log_prob), _f32(entropy), sel,
         1.0 - clip_ratio_low, 1.0 + clip_ratio_high, float(clip_ratio_c), AGG_MODES[loss_agg_mode], kl_type,
-        POLICY_LOSS_MODES[loss_mode], float(mode_coef), int(seg_rows), seg_offsets(seg_off, log_prob.device),
+        POLICY_LOSS_MODES[loss_mode], float(mode_coef), int(seg_rows),
+        seg_offsets(seg_off, log_prob.device, log_prob.shape[0]),
     )
     return out
 
 
-def seg_offsets(seg_off, device):
+def seg_offsets(seg_off, device, rows: int | None = None):
     """Loss micro-batch row offsets as the contiguous int32 device tensor the loss ops take (None
-    stays None). A host list / array goes up asynchronously through pinned memory."""
+    stays None). A host list / array is validated (0 first, strictly increasing, ``rows`` last
+    when given) and goes up asynchronously through pinned memory."""
     if seg_off is None:
         return None
     if isinstance(seg_off, torch.Tensor) and seg_off.is_cuda:
+        # device offsets are trusted (checking them would cost a device->host sync): callers
+        # build them from validated host lists
         return seg_off.to(torch.int32).contiguous()
-    return h2d(np.asarray(seg_off, dtype=np.int32), np.int32, device)
+    off = np.asarray(seg_off.cpu() if isinstance(seg_off, torch.Tensor) else seg_off, dtype=np.int64).reshape(-1)
+    # the kernels binary-search these row ranges and divide by their sizes (ADVICE r3): 0 first,
+    # strictly increasing (no empty micro-batch), the batch's row count last
+    if off.size < 2 or off[0] != 0 or np.any(np.diff(off) <= 0) or (rows is not None and off[-1] != rows):
+        raise ValueError(f"seg_off must run from 0 to the row count{'' if rows is None else f' {rows}'} in strictly "
+                         f"increasing steps (no empty micro-batch): {off.tolist()}")
+    return h2d(off.astype(np.int32), np.int32, device)
 
 
 # =============================================================================== value loss (critic)
@@ -334,7 +355,7 @@ def fused_value_loss(vpreds, values, returns, response_mask, cliprange_value: fl
     m, _ = _mask(response_mask)
     out, _ = torch.ops.verl_amd.value_loss_fwd(_f32(vpreds), _f32(values), _f32(returns), m, float(cliprange_value),
                                                AGG_MODES[loss_agg_mode], int(seg_rows),
-                                               seg_offsets(seg_off, vpreds.device))
+                                               seg_offsets(seg_off, vpreds.device, vpreds.shape[0]))
     return out
 
 
@@ -721,14 +742,26 @@ WGRAD_SWAP_MIN_OUT = 65536  # the lm_head (V = 151,936 outputs)
 _OWN_WGRAD = os.environ.get("VERL_AMD_WGRAD", "own") != "hipblaslt"
 
 
-def own_wgrad_splits(n_out: int, n_in: int) -> int:
+# fewest 32-token K-steps a split-K slice of va_weight_grad gets: its 4-deep LDS ring keeps 3 steps
+# in flight, so shorter slices are mostly prologue / epilogue, and every slice costs an fp32 M x N
+# partial in the workspace that the ordered reduce reads back
+WGRAD_MIN_STEPS_PER_SLICE = 8
+
+
+def own_wgrad_splits(n_out: int, n_in: int, tokens: int | None = None) -> int:
     """K slices of va_weight_grad: one round of workgroups when it fills >= 85 % of the 256 CUs
-    (down 3, q|k|v 12, o 16 at H = 896), else about three full rounds (gate|up: 152 tiles x 5)."""
+    (down 3, q|k|v 12, o 16 at H = 896), else about three full rounds (gate|up: 152 tiles x 5);
+    capped so that every slice keeps >= WGRAD_MIN_STEPS_PER_SLICE K-steps of ``tokens`` (ADVICE
+    r3: 512 tokens = 16 steps no longer get 128-256 mostly empty slices and their workspace)."""
     tiles = -(-n_out // 256) * -(-n_in // 256)
     one = 256 // tiles
     if one >= 1 and tiles * one >= 0.85 * 256:
-        return one
-    return max(1, round(768 / tiles))
+        s = one
+    else:
+        s = max(1, round(768 / tiles))
+    if tokens is not None:
+        s = min(s, max(1, -(-tokens // 32) // WGRAD_MIN_STEPS_PER_SLICE))
+    return s
 
 
 # the shape class it was measured on: outputs of at most one round of 256 x 256 tiles (the H = 896
@@ -747,7 +780,7 @@ def _own_weight_grad(dy2, x2):
             or T % 32 or n_out % 8 or n_in % 8 or n_out >= WGRAD_SWAP_MIN_OUT or dy2.stride(1) != 1
             or x2.stride(1) != 1 or dy2.stride(0) % 8 or x2.stride(0) % 8 or (dy2.data_ptr() | x2.data_ptr()) % 16):
         return None
-    s = own_wgrad_splits(n_out, n_in)
+    s = own_wgrad_splits(n_out, n_in, T)
     out = torch.empty(n_out, n_in, dtype=torch.bfloat16, device=dy2.device)
     nb = L.load().va_weight_grad_workspace_bytes(n_out, n_in, s)
     ws = torch.empty(nb // 4, dtype=torch.float32, device=dy2.device) if nb else None

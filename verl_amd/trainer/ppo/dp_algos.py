@@ -27,11 +27,11 @@ import hashlib
 
 import numpy as np
 import torch
-import torch.distributed as dist
 
 from ... import _lib as L
 from ... import kernels as K
 from ...protocol import DataProto
+from ...utils import comm
 from .core_algos import AdvantageEstimator
 
 _GROUP_ESTIMATORS = {
@@ -45,25 +45,16 @@ _GROUP_ESTIMATORS = {
 
 
 def _world(group) -> int:
-    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    return comm.world(group)
 
 
 def _rank(group) -> int:
-    return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+    return comm.rank(group)
 
 
 def _all_gather(t: torch.Tensor, group=None) -> list[torch.Tensor]:
     """all_gather of equal-shape tensors; gloo moves host tensors, RCCL device tensors."""
-    w = _world(group)
-    if w == 1:
-        return [t]
-    if t.is_cuda and dist.get_backend(group) == "gloo":
-        parts = [torch.empty_like(t, device="cpu") for _ in range(w)]
-        dist.all_gather(parts, t.cpu(), group=group)
-        return [p.to(t.device) for p in parts]
-    parts = [torch.empty_like(t) for _ in range(w)]
-    dist.all_gather(parts, t, group=group)
-    return parts
+    return comm.all_gather(t, group)
 
 
 def uid_keys(index) -> np.ndarray:
@@ -176,7 +167,7 @@ def check_groups_intact(index, group=None) -> bool:
     if w == 1:
         return True
     # RCCL moves device tensors only: stage the exchange on this rank's GPU under nccl
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    dev = comm.comm_device(group)
     keys = torch.from_numpy(np.unique(uid_keys(index))).to(dev)
     n = _all_gather(torch.tensor([keys.numel()], device=dev), group)
     nmax = max(int(x.item()) for x in n)
@@ -210,13 +201,7 @@ def agg_loss_dp(loss_mat: torch.Tensor, loss_mask: torch.Tensor, loss_agg_mode: 
         num, den = x.sum() / loss_mask.shape[-1], torch.ones((), dtype=torch.float64, device=x.device)
     else:
         raise ValueError(f"Invalid loss_agg_mode: {loss_agg_mode}")
-    t = torch.stack([num, den])
-    if t.is_cuda and dist.get_backend(group) == "gloo":
-        h = t.cpu()
-        dist.all_reduce(h, group=group)
-        t = h.to(loss_mat.device)
-    else:
-        dist.all_reduce(t, group=group)
+    t = comm.all_reduce(torch.stack([num, den]), group=group)
     if loss_agg_mode == "token-mean":
         return (t[0] / (t[1] + 1e-8)).float()
     if loss_agg_mode == "seq-mean-token-sum-norm":

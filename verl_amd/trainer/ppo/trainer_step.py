@@ -30,6 +30,7 @@ import torch
 import torch.distributed as dist
 
 from ...protocol import DataProto
+from ...utils import comm
 from . import core_algos
 from .core_algos import AdvantageEstimator
 
@@ -67,11 +68,11 @@ def reduce_metrics(metrics: dict) -> dict:
 
 
 def _world(group=None) -> int:
-    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    return comm.world(group)
 
 
 def _rank(group=None) -> int:
-    return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+    return comm.rank(group)
 
 
 def reduce_metrics_dp(metrics: dict, group=None) -> dict:
@@ -82,7 +83,7 @@ def reduce_metrics_dp(metrics: dict, group=None) -> dict:
     if _world(group) == 1 or not local:
         return local
     keys = sorted(local)
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    dev = comm.comm_device(group)
     out = {}
     for kind, op in (("max", dist.ReduceOp.MAX), ("min", dist.ReduceOp.MIN), ("mean", dist.ReduceOp.SUM)):
         sel = [k for k in keys if (kind == "max" and "max" in k) or (kind == "min" and "min" in k and "max" not in k)
@@ -90,7 +91,7 @@ def reduce_metrics_dp(metrics: dict, group=None) -> dict:
         if not sel:
             continue
         t = torch.tensor([local[k] for k in sel], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=op, group=group)
+        comm.all_reduce(t, op=op, group=group)
         if kind == "mean":
             t /= _world(group)
         out.update(dict(zip(sel, t.tolist(), strict=True)))
@@ -122,13 +123,7 @@ def apply_kl_penalty_dp(data: DataProto, kl_ctrl, kl_penalty: str = "kl", group=
                                          data.batch["ref_log_prob"], response_mask, float(beta), kl_penalty)
     t = torch.stack([row_kl.double().sum(), torch.tensor(float(row_kl.numel()), dtype=torch.float64,
                                                           device=row_kl.device)])
-    if _world(group) > 1:
-        if dist.get_backend(group) == "gloo":
-            h = t.cpu()
-            dist.all_reduce(h, group=group)
-            t = h
-        else:
-            dist.all_reduce(t, group=group)
+    comm.all_reduce(t, group=group)
     batch_size = int(t[1].item())
     current_kl = float((t[0] / t[1]).item())
     kl_ctrl.update(current_kl=current_kl, n_steps=batch_size)
@@ -187,62 +182,85 @@ class PPOTrainerStep:
 
     # ------------------------------------------------------------------ the step
     def step(self, batch: DataProto) -> tuple[DataProto, dict]:
-        """ray_trainer.py:1195-1330 from the rollout output on; returns (batch, metrics)."""
+        """ray_trainer.py:1195-1390 from the rollout output on; returns (batch, metrics): the
+        workers' reduced metric lists plus the driver's data / timing / throughput metrics
+        (metric_utils.py:80-258) over the whole batch of all ranks."""
         from .dp_algos import agg_loss_dp
+        from .metric_utils import (SectionTimer, compute_data_metrics, compute_throughout_metrics,
+                                   compute_timing_metrics, global_token_num)
         from .ray_trainer import compute_response_mask
 
         cfg = self.config
         metrics: dict = {}
+        timer = SectionTimer(self.device)
+        timer.start()
         batch = self.to_device(batch)
         if "response_mask" not in batch.batch.keys():
             batch.batch["response_mask"] = compute_response_mask(batch)
-        batch.meta_info["global_token_num"] = torch.sum(batch.batch["attention_mask"], dim=-1).tolist()
+        # the whole batch's per-sequence token counts, as the reference's driver sets them before
+        # dispatching DP chunks (ray_trainer.py:1208): MFU and throughput divide by the world size
+        batch.meta_info["global_token_num"] = global_token_num(batch.batch["attention_mask"], self.group)
 
         if self.reward_fn is not None:  # :1209-1218
-            res = self.reward_fn(batch)
-            scores, extra = res if isinstance(res, tuple) else (res, {})
-            batch.batch["token_level_scores"] = scores.to(self.device)
-            if extra:
-                batch.non_tensor_batch.update({k: np.array(v) for k, v in extra.items()})
+            with timer.section("reward"):
+                res = self.reward_fn(batch)
+                scores, extra = res if isinstance(res, tuple) else (res, {})
+                batch.batch["token_level_scores"] = scores.to(self.device)
+                if extra:
+                    batch.non_tensor_batch.update({k: np.array(v) for k, v in extra.items()})
 
         # old log-probs (+ entropy metric), :1221-1230
-        old = self.actor.compute_log_prob(batch)
-        entropys = old.batch["entropys"]
-        # over the whole batch as the reference's driver (ray_trainer.py:1224-1228)
-        ent = agg_loss_dp(entropys, batch.batch["response_mask"], cfg.actor_rollout_ref.actor.loss_agg_mode, self.group)
-        metrics["actor/entropy"] = ent.detach()
-        batch.batch["old_log_probs"] = old.batch["old_log_probs"]
+        with timer.section("old_log_prob"):
+            old = self.actor.compute_log_prob(batch)
+            entropys = old.batch["entropys"]
+            # over the whole batch as the reference's driver (ray_trainer.py:1224-1228)
+            ent = agg_loss_dp(entropys, batch.batch["response_mask"], cfg.actor_rollout_ref.actor.loss_agg_mode,
+                              self.group)
+            metrics["actor/entropy"] = ent.detach()
+            batch.batch["old_log_probs"] = old.batch["old_log_probs"]
 
         if self.use_reference_policy:  # :1253-1259
-            ref_out = (self.ref or self.actor).compute_ref_log_prob(batch)
-            batch.batch["ref_log_prob"] = ref_out.batch["ref_log_prob"]
+            with timer.section("ref"):
+                ref_out = (self.ref or self.actor).compute_ref_log_prob(batch)
+                batch.batch["ref_log_prob"] = ref_out.batch["ref_log_prob"]
 
         if self.use_critic:  # :1262-1265
-            batch.batch["values"] = self.critic.compute_values(batch).batch["values"]
+            with timer.section("values"):
+                batch.batch["values"] = self.critic.compute_values(batch).batch["values"]
 
-        # rewards (in-reward KL), :1276-1283
-        if self.kl_ctrl_in_reward is not None:
-            batch, kl_metrics = apply_kl_penalty_dp(batch, self.kl_ctrl_in_reward,
-                                                    cfg.algorithm.get("kl_penalty", "kl"), self.group)
-            metrics.update(kl_metrics)
-        else:
-            batch.batch["token_level_rewards"] = batch.batch["token_level_scores"]
+        with timer.section("adv"):
+            # rewards (in-reward KL), :1276-1283
+            if self.kl_ctrl_in_reward is not None:
+                batch, kl_metrics = apply_kl_penalty_dp(batch, self.kl_ctrl_in_reward,
+                                                        cfg.algorithm.get("kl_penalty", "kl"), self.group)
+                metrics.update(kl_metrics)
+            else:
+                batch.batch["token_level_rewards"] = batch.batch["token_level_scores"]
 
-        # advantages on the workers (the reference: driver CPU, :1285-1305)
-        batch = self.actor.compute_advantage(
-            batch, self.adv_estimator, gamma=cfg.algorithm.get("gamma", 1.0), lam=cfg.algorithm.get("lam", 1.0),
-            num_repeat=cfg.actor_rollout_ref.rollout.n,
-            norm_adv_by_std_in_grpo=cfg.algorithm.get("norm_adv_by_std_in_grpo", True), config=cfg.algorithm)
+            # advantages on the workers (the reference: driver CPU, :1285-1305)
+            batch = self.actor.compute_advantage(
+                batch, self.adv_estimator, gamma=cfg.algorithm.get("gamma", 1.0), lam=cfg.algorithm.get("lam", 1.0),
+                num_repeat=cfg.actor_rollout_ref.rollout.n,
+                norm_adv_by_std_in_grpo=cfg.algorithm.get("norm_adv_by_std_in_grpo", True), config=cfg.algorithm)
 
         step_metrics: dict = {}
         if self.use_critic:  # :1307-1312
-            critic_out = self.critic.update_critic(batch)
+            with timer.section("update_critic"):
+                critic_out = self.critic.update_critic(batch)
             step_metrics.update(critic_out.meta_info["metrics"])
         if cfg.trainer.get("critic_warmup", 0) <= self.global_steps:  # :1314-1320
             batch.meta_info["multi_turn"] = False
-            actor_out = self.actor.update_actor(batch)
+            with timer.section("update_actor"):
+                actor_out = self.actor.update_actor(batch)
             step_metrics.update(actor_out.meta_info["metrics"])
         host = {k: [float(v.item())] if isinstance(v, torch.Tensor) else [v] for k, v in metrics.items()}
         host.update({k: (v if isinstance(v, list) else [v]) for k, v in step_metrics.items()})
+        timing_raw = timer.read()
+        out = reduce_metrics_dp(host, self.group)
+        # the driver's metrics after the step (ray_trainer.py:1380-1390)
+        out["training/global_step"] = self.global_steps
+        out.update(compute_data_metrics(batch, use_critic=self.use_critic, group=self.group))
+        out.update(compute_timing_metrics(batch, timing_raw, group=self.group))
+        out.update(compute_throughout_metrics(batch, timing_raw, n_gpus=_world(self.group)))
         self.global_steps += 1
-        return batch, reduce_metrics_dp(host, self.group)
+        return batch, out

@@ -15,6 +15,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from . import comm
+
 _INT_VIEW = {1: torch.int8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
 _CHUNK = 1 << 24
 
@@ -37,12 +39,6 @@ def bits_checksum(tensors) -> torch.Tensor:
     if acc is None:
         acc = torch.zeros(1, dtype=torch.int64)
     return acc
-
-
-def _comm_device(ref: torch.Tensor, group):
-    if dist.get_backend(group) == "nccl":
-        return torch.device("cuda", torch.cuda.current_device())
-    return torch.device("cpu")
 
 
 def replica_check(module: torch.nn.Module, manager=None, metrics: dict | None = None, metric_keys=(),
@@ -71,15 +67,15 @@ def replica_check(module: torch.nn.Module, manager=None, metrics: dict | None = 
     if world == 1:
         out.update(weights_equal=True, masters_equal=True, metrics_equal=True, replicas_identical=True)
         return out
-    dev = _comm_device(cs, group)
+    dev = comm.comm_device(group)
     hi, lo = cs.to(dev), cs.clone().to(dev)
-    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
-    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    comm.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    comm.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
     m = torch.tensor(vals, dtype=torch.float64)
     mh, ml = m.to(dev), m.clone().to(dev)
     if keys:
-        dist.all_reduce(mh, op=dist.ReduceOp.MAX, group=group)
-        dist.all_reduce(ml, op=dist.ReduceOp.MIN, group=group)
+        comm.all_reduce(mh, op=dist.ReduceOp.MAX, group=group)
+        comm.all_reduce(ml, op=dist.ReduceOp.MIN, group=group)
     hi, lo, mh, ml = hi.cpu(), lo.cpu(), mh.cpu(), ml.cpu()
     w_eq = bool(hi[0] == lo[0])
     m_eq = bool(hi[1] == lo[1])

@@ -23,6 +23,7 @@ import torch.distributed as dist
 
 from .. import _lib as L
 from ..protocol import DataProto, TensorBatch
+from . import comm
 
 __all__ = [
     "karmarkar_karp", "greedy_partition", "get_seqlen_balanced_partitions", "log_seqlen_unbalance", "ceildiv",
@@ -114,7 +115,7 @@ def _num_micro_batches(seq_len_effective: list[int], max_token_len: int, dp_grou
         n = max(min_num_micro_batch, n)
     if dist.is_available() and dist.is_initialized() and same_micro_num_in_dp:
         t = torch.tensor([n], device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=dp_group)
+        comm.all_reduce(t, op=dist.ReduceOp.MAX, group=dp_group)
         n = int(t.cpu().item())
     if num_batches_divided_by is not None:
         n = roundup_divisible(n, num_batches_divided_by)
@@ -124,8 +125,8 @@ def _num_micro_batches(seq_len_effective: list[int], max_token_len: int, dp_grou
 
 def _collective_device(batch):
     am = batch["attention_mask"]
-    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
-        return am.device if am.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    if comm.device_backend():
+        return am.device if am.is_cuda else comm.comm_device()
     return torch.device("cpu")
 
 

@@ -27,7 +27,12 @@ def make_grpo_batch(
     seed: int = 1234,
     device="cpu",
     permute: bool = True,
+    step_noise: bool = False,
 ) -> DataProto:
+    """``step_noise``: also attach ``old_noise`` / ``ref_noise`` [B, R] ~ N(0, 1) drawn per row
+    before the permutation, so the bench's perturbations of the recomputed log-probs (SURVEY §8d:
+    old = new + 0.05 N, ref = new + 0.1 N) travel with their rows and do not depend on how the
+    batch is split over ranks."""
     g = torch.Generator().manual_seed(seed)
     rs = np.random.RandomState(seed)
     B, P, R = n_prompts * n, prompt_len, response_len
@@ -60,6 +65,10 @@ def make_grpo_batch(
         non_tensors=dict(uid=uid),
         meta_info=dict(temperature=1.0),
     )
+    if step_noise:
+        gn = torch.Generator().manual_seed(seed + 7)
+        data.batch["old_noise"] = torch.randn(B, R, generator=gn)
+        data.batch["ref_noise"] = torch.randn(B, R, generator=gn)
     if permute:
         data.reorder(torch.from_numpy(rs.permutation(B)))
     data.meta_info["global_token_num"] = data.batch["attention_mask"].sum(-1).tolist()

@@ -247,8 +247,10 @@ class DataParallelPPOActor(BasePPOActor):
         # the log-prob backward writes dlogits over the logits (flash-attn inplace_backward, as the
         # reference) or into a fresh [N, V] buffer: on MI355X the out-of-place stream runs ~4 %
         # faster (a read+write pass whose writes hit other DRAM pages than its reads) for one more
-        # logits-sized buffer at the backward's peak
-        self.logprob_inplace_backward = bool(self.config.get("logprob_inplace_backward", True))
+        # logits-sized buffer at the backward's peak; "auto" takes the fresh buffer when the
+        # allocator can provide it and the reference's in-place path when it cannot
+        ipb = self.config.get("logprob_inplace_backward", True)
+        self.logprob_inplace_backward = "auto" if ipb == "auto" else bool(ipb)
         # round packed micro-batches up to a multiple of this many tokens (0 = off) and look the
         # model GEMMs up in a tuned solution table (utils/gemm_tuning.py)
         self.pack_pad_multiple = int(self.config.get("pack_pad_multiple", 0) or 0)

@@ -245,16 +245,20 @@ class CriticWorker:
 def perf_metrics(flops_counter, data: DataProto, delta_time: float, ppo_epochs: int, world_size: int,
                  role: str) -> dict:
     """fsdp_workers.py:690-697: MFU of one update (estimated FLOP/s x epochs / promised / world)
-    and the memory high-water marks. global_token_num lists the valid tokens of every sequence
-    of the whole batch (set by the trainer, ray_trainer.py:1207); without it the rank's own
-    attention mask stands in."""
+    and the memory high-water marks. ``global_token_num`` lists the valid tokens of every sequence
+    of the WHOLE batch (the reference's driver sets it before the DP dispatch, ray_trainer.py:1208;
+    PPOTrainerStep and bench.py gather it over the ranks, metric_utils.global_token_num), so the
+    whole batch's FLOPs are divided by the world size. Without it, this rank's own attention mask
+    stands in, and then the FLOPs are already this rank's share: no division."""
     import psutil
 
     tokens = data.meta_info.get("global_token_num")
+    share = world_size
     if tokens is None:
         tokens = data.batch["attention_mask"].sum(-1).tolist()
+        share = 1
     est, promised = flops_counter.estimate_flops(tokens, delta_time)
-    out = {f"perf/mfu/{role}": est * ppo_epochs / promised / world_size}
+    out = {f"perf/mfu/{role}": est * ppo_epochs / promised / share}
     if torch.cuda.is_available():
         out["perf/max_memory_allocated_gb"] = torch.cuda.max_memory_allocated() / (1024**3)
         out["perf/max_memory_reserved_gb"] = torch.cuda.max_memory_reserved() / (1024**3)

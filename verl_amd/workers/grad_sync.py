@@ -30,15 +30,16 @@ import os
 import weakref
 
 import torch
-import torch.distributed as dist
+
+from ..utils import comm
 
 
 def _world_of(group) -> int:
-    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    return comm.world(group)
 
 
 def _rank_of(group) -> int:
-    return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+    return comm.rank(group)
 
 
 def _group_params(params, bucket_bytes: int, elem_bytes: int = 4):
@@ -100,17 +101,15 @@ class _OrderedBuckets:
         self.sync_enabled = False
         self._next = 0
         self._timing = None
-        self._use_avg = self.world > 1 and dist.get_backend(self.group) == "nccl"
+        # RCCL: native AVG in the reduction; gloo: SUM, then 1/W when waited for (utils/comm.py)
+        self._use_avg = self.world > 1 and comm.device_backend(self.group)
 
     def _collective(self, b: _Bucket):
         """Start bucket b's all-reduce (mean over ranks)."""
-        op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
-        return dist.all_reduce(b.buf, op=op, group=self.group, async_op=True)
+        return comm.all_reduce_mean_async(b.buf, self.group)
 
     def _finish_bucket(self, b: _Bucket):
         b.handle.wait()
-        if not self._use_avg:
-            b.buf.mul_(1.0 / self.world)
 
     def _mark_ready(self, b: _Bucket):
         """Bucket b is complete for this pass; launch every consecutive ready bucket in order."""
@@ -170,7 +169,7 @@ class _OrderedBuckets:
         times = []
         for _ in range(reps + 1):
             scratch = [torch.zeros_like(b.buf) for b in self.buckets]
-            dist.barrier(group=self.group)
+            comm.barrier(self.group)
             torch.cuda.synchronize()
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -185,23 +184,14 @@ class _OrderedBuckets:
         return sorted(times[1:])[len(times[1:]) // 2]
 
     def _raw_collective(self, buf):
-        op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
-        return dist.all_reduce(buf, op=op, group=self.group, async_op=True)
+        return comm.all_reduce_mean_async(buf, self.group)
 
 
 @torch.no_grad()
 def _broadcast_from_rank0(tensors, group=None):
     """FSDP sync_module_states: every rank starts from rank 0's values."""
-    if _world_of(group) <= 1:
-        return
-    src = dist.get_global_rank(group, 0) if group is not None else 0
     for t in tensors:
-        if dist.get_backend(group) == "gloo" and t.is_cuda:
-            c = t.detach().cpu()
-            dist.broadcast(c, src=src, group=group)
-            t.copy_(c)
-        else:
-            dist.broadcast(t, src=src, group=group)
+        comm.broadcast(t, 0, group)
 
 
 class GradBucketReducer(_OrderedBuckets):
@@ -495,29 +485,6 @@ class MixedPrecisionParams(_OrderedBuckets):
         self._hooks.clear()
 
 
-def _reduce_scatter_avg(out: torch.Tensor, buf: torch.Tensor, group, use_avg: bool, async_op: bool = True):
-    """out = mean over ranks of buf's shard r (buf.numel() == W * out.numel())."""
-    if use_avg:
-        return dist.reduce_scatter_tensor(out, buf, op=dist.ReduceOp.AVG, group=group, async_op=async_op)
-    return _GlooReduceScatter(out, buf, group)
-
-
-class _GlooReduceScatter:
-    """gloo has no reduce-scatter: all-reduce the bucket and keep this rank's shard (tests only)."""
-
-    def __init__(self, out, buf, group):
-        self.out, self.buf, self.group = out, buf, group
-        self.world = _world_of(group)
-        self.rank = _rank_of(group)
-
-    def wait(self):
-        host = self.buf.detach().cpu() if self.buf.is_cuda else self.buf
-        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
-        n = self.out.numel()
-        self.out.copy_(host[self.rank * n : (self.rank + 1) * n].to(self.out.device))
-        self.out.mul_(1.0 / self.world)
-
-
 class ShardedMixedPrecisionParams(_OrderedBuckets):
     """ZeRO-style data parallelism for the configs whose replicated optimizer state does not fit
     (Llama-3-8B actor + critic, Qwen2.5-7B DAPO; the reference shards with FSDP FULL_SHARD,
@@ -589,14 +556,14 @@ class ShardedMixedPrecisionParams(_OrderedBuckets):
 
     # ------------------------------------------------------------------ collectives
     def _collective(self, b: _Bucket):
-        return _reduce_scatter_avg(self.shards[b.index].grad, b.buf, self.group, self._use_avg)
+        return comm.reduce_scatter_mean_async(self.shards[b.index].grad, b.buf, self.group)
 
     def _finish_bucket(self, b: _Bucket):
         b.handle.wait()
 
     def _raw_collective(self, buf):
         out = torch.empty(buf.numel() // self.world, dtype=buf.dtype, device=buf.device)
-        return _reduce_scatter_avg(out, buf, self.group, self._use_avg)
+        return comm.reduce_scatter_mean_async(out, buf, self.group)
 
     # ------------------------------------------------------------------ hooks (as MixedPrecisionParams)
     def _on_grad(self, p):
@@ -656,13 +623,7 @@ class ShardedMixedPrecisionParams(_OrderedBuckets):
         semantics: coef = max_norm / (norm + 1e-6), clamped to 1; the norm is returned)."""
         grads = [s.grad for s in self.shards]
         local = torch.stack(torch._foreach_norm(grads)).square().sum()
-        if self.world > 1:
-            if dist.get_backend(self.group) == "gloo" and local.is_cuda:
-                h = local.cpu()
-                dist.all_reduce(h, group=self.group)
-                local = h.to(local.device)
-            else:
-                dist.all_reduce(local, group=self.group)
+        comm.all_reduce(local, group=self.group)
         norm = local.sqrt()
         coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
         torch._foreach_mul_(grads, coef)
@@ -674,15 +635,7 @@ class ShardedMixedPrecisionParams(_OrderedBuckets):
         parameter whose storage was re-pointed elsewhere since construction (the fused backbone
         merges q|k|v and gate|up into one buffer, qwen2_fused.py) gets its slice copied over."""
         for s, wbuf in zip(self.shards, self.flat_weights, strict=True):
-            mine = s.detach().to(self.compute_dtype)
-            if self.world == 1:
-                wbuf.copy_(mine)
-            elif dist.get_backend(self.group) == "gloo":
-                parts = [torch.empty_like(mine, device="cpu") for _ in range(self.world)]
-                dist.all_gather(parts, mine.cpu(), group=self.group)
-                wbuf.copy_(torch.cat(parts).to(wbuf.device))
-            else:
-                dist.all_gather_into_tensor(wbuf, mine, group=self.group)
+            comm.all_gather_into(wbuf, s.detach().to(self.compute_dtype), self.group)
         dst, src = [], []
         for p in self.params:
             i, off = self._wslice[id(p)]
