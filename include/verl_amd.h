@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define VA_ABI_VERSION 4
+#define VA_ABI_VERSION 5
 
 /* error codes */
 #define VA_OK 0
@@ -402,6 +402,21 @@ int64_t va_linear_logprob_workspace_bytes(int64_t N, int splits);
 int va_linear_logprob_fwd(const void *hidden, int64_t ldh, const void *weight, int64_t ldw, int dtype,
                           const int64_t *labels, int64_t N, int64_t H, int64_t V, float temperature, int splits,
                           float *logp, float *entropy, float *lse, void *workspace, void *stream);
+
+/* Fused lm_head + log-prob + entropy backward, first half (f1; the reference's
+ * efficient_entropy_backward_kernel_general_d_logits_split_N, utils/kernel/kernels.py:1241-1342,
+ * dispatched at :1491-1548): recomputes the logits tile by tile from hidden / weight exactly as
+ * va_linear_logprob_fwd does (same dtype flags) and writes
+ *   dlogits[i, v] = bf16( ( -p (g_entropy[i] (x - lse_i + H_i) + g_logp[i]) + g_logp[i] [v == labels[i]] ) / T ),
+ *   p = exp(x - lse_i), x the logit as the forward saw it,
+ * i.e. va_logprob_entropy_bwd's arithmetic, without the logits in HBM. lse / entropy: the forward's
+ * outputs; g_logp / g_entropy may be NULL (zero). dlogits [N, V] bf16, row stride ldd >= V (8-byte
+ * aligned, ldd % 4 == 0), V % 4 == 0. The caller runs the lm_head's two backward GEMMs on it
+ * (dhidden = dlogits W, dW = dlogits^T hidden). `splits` vocab ranges per row block as in the forward. */
+int va_linear_logprob_bwd(const void *hidden, int64_t ldh, const void *weight, int64_t ldw, int dtype,
+                          const int64_t *labels, const float *lse, const float *entropy, const float *g_logp,
+                          const float *g_entropy, int64_t N, int64_t H, int64_t V, float temperature, int splits,
+                          void *dlogits, int64_t ldd, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Discounted returns for REINFORCE++ (mode VA_RET_RFPP, gamma) and ReMax (VA_RET_REMAX:

@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_abi_version_and_workspace_queries(lib):
-    assert lib.va_abi_version() == 4
+    assert lib.va_abi_version() == 5
     assert lib.va_ppo_loss_workspace_bytes(10) == 8 * (2 * 10 * 8 + 8)
     assert lib.va_agg_workspace_bytes(10) == 8 * (2 * 10 * 8 + 8)
     assert lib.va_gae_workspace_bytes(7) == 8 * (6 * 7 + 8)
@@ -73,6 +73,12 @@ def test_argument_validation_without_device(lib):
     rc = lib.va_group_coef(1, None, 1, 1, 4, 8, 1e-6, L.VA_ADV_OPO, 1, None)
     assert rc == -1 and b"lengths" in lib.va_last_error()
     assert lib.va_logprob_entropy_fwd(None, 1, 0, 10, 10, None, 1.0, None, None, None, None) == 0  # n_rows 0: no-op
+    # fused lm_head backward: V % 4 != 0 is an argument error; N = 0 is a no-op
+    rc = lib.va_linear_logprob_bwd(None, 64, None, 64, L.VA_BF16, None, None, None, None, None, 4, 64, 130, 1.0, 1,
+                                   None, 130, None)
+    assert rc == -1 and b"V % 4" in lib.va_last_error()
+    assert lib.va_linear_logprob_bwd(None, 64, None, 64, L.VA_BF16, None, None, None, None, None, 0, 64, 128, 1.0, 1,
+                                     None, 128, None) == 0
 
 
 def test_product_path_rejects_cpu_tensors():

@@ -132,3 +132,65 @@ def test_actor_fused_no_grad_logprob_matches_unfused():
     msk = data.batch["response_mask"].bool()
     assert torch.allclose(out[True][0][msk], out[False][0][msk], atol=4e-2)
     assert torch.allclose(out[True][1][msk], out[False][1][msk], atol=5e-3)
+
+
+# ------------------------------------------------------------------ fused backward (va_linear_logprob_bwd)
+@pytest.mark.parametrize("N,H,V", [(300, 64, 1000), (256, 896, 151936), (77, 128, 36), (1, 64, 132)])
+@pytest.mark.parametrize("T", [1.0, 0.7])
+@pytest.mark.parametrize("ent_grad", [False, True])
+def test_fused_backward_dlogits_bitwise_on_exact_logits(N, H, V, T, ent_grad, tile):
+    """the fused backward recomputes the logits inside its MFMA tiles and forms
+    dlogits in registers. On exact-arithmetic data (every GEMM order gives the same logits) its bf16
+    dlogits equal bitwise those of the unfused composition — bf16 logits in HBM, then the streaming
+    va_logprob_entropy_bwd — given the same (lse, entropy) and upstream gradients, including
+    ignore_index / out-of-range labels, rows past a 256-row block and vocab tails."""
+    if tile != 256:
+        pytest.skip("one backward kernel (the forward's tile setting does not apply)")
+    from verl_amd import kernels as K
+
+    h, w = _exact_inputs(N, H, V, seed=N * 3 + V)
+    g = torch.Generator().manual_seed(N + H)
+    labels = torch.randint(0, V, (N,), generator=g)
+    if N > 2:
+        labels[0], labels[1] = -100, V + 3
+    labels[-1] = V - 1
+    logits = (h.float() @ w.float().t()).to(torch.bfloat16).to(DEV)  # exact fp32 sums, one rounding
+    h, w, labels = h.to(DEV), w.to(DEV), labels.to(DEV)
+    _, ent, lse = torch.ops.verl_amd.logprob_entropy_fwd(logits, labels, T, 0)
+    g1 = torch.randn(N, generator=g).to(DEV)
+    g2 = torch.randn(N, generator=g).to(DEV) if ent_grad else None
+    want = torch.ops.verl_amd.logprob_entropy_bwd(g1, g2, logits, labels, lse, ent, T)
+    got = torch.full((N, V + 4), 7.0, dtype=torch.bfloat16, device=DEV)[:, :V]  # row stride > V
+    K._linear_logprob_bwd_raw(h, w, labels, lse, ent, g1, g2, T, False, got)
+    assert torch.equal(torch.isnan(got), torch.isnan(want))
+    assert torch.equal(torch.nan_to_num(got), torch.nan_to_num(want)), (got.float() - want.float()).abs().max()
+
+
+@pytest.mark.parametrize("f32", [False, True])
+def test_fused_backward_equals_composition(f32, tile, monkeypatch):
+    """The autograd backward with the fused dlogits kernel (default) and with the previous
+    composition (VERL_AMD_F1_BWD=compose: hipBLASLt logits recompute + streaming backward) on random
+    Qwen2.5-0.5B-shaped data, several row chunks: d_hidden / d_weight within bf16 rounding of the
+    recomputed logits (the reference's kernel-vs-torch gradient tolerance is 2e-2,
+    tests/utils/test_linear_cross_entropy.py:260-275)."""
+    from verl_amd import kernels as K
+
+    torch.manual_seed(2)
+    N, H, V = 700, 896, 151936
+    h = torch.randn(N, H, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(V, H, device=DEV) * 0.05).to(torch.bfloat16)
+    labels = torch.randint(0, V, (N,), device=DEV)
+    g1, g2 = torch.randn(N, device=DEV), torch.randn(N, device=DEV)
+    monkeypatch.setattr(K._LinearLogprob, "CHUNK_BYTES", 300 * V * 2)  # 3 row chunks
+    grads = {}
+    for mode in ("compose", "fused"):
+        monkeypatch.setenv("VERL_AMD_F1_BWD", mode)
+        ha, wa = h.clone().requires_grad_(True), w.clone().requires_grad_(True)
+        lp, ent = K.linear_logprob_entropy(ha, wa, labels, 0.9, fp32_logits=f32)
+        ((lp * g1).sum() + (ent * g2).sum()).backward()
+        grads[mode] = (ha.grad.float(), wa.grad.float())
+    for i, what in enumerate(("d_hidden", "d_weight")):
+        a, b = grads["fused"][i], grads["compose"][i]
+        err = ((a - b).norm() / b.norm()).item()
+        assert err < 1e-2, f"{what}: relative L2 error {err:.3e}"
+

@@ -1,0 +1,95 @@
+"""Fused lm_head backward (va_linear_logprob_bwd) vs the composition it replaces, at the bench's
+131,072-row update pass (Qwen2.5-0.5B head: H = 896, V = 151,936). Prints one JSON line:
+
+  * kernel level: the fused dlogits kernel (recompute + dlogits, bf16 [N, V] out) vs hipBLASLt's
+    logits recompute + the streaming va_logprob_entropy_bwd in place;
+  * pass level: the whole fused path (f1 forward + fused backward incl. the two lm_head GEMMs) vs the
+    unfused update pass (hipBLASLt logits + logprob_entropy fwd + bwd + the two GEMMs), with the
+    peak HBM of each.
+
+  python tools/f1_bwd_ab.py [--rows 131072] [--iters 3]
+"""
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return sorted(ts)[len(ts) // 2], ts
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=131072)
+    ap.add_argument("--iters", type=int, default=3)
+    args = ap.parse_args()
+    from verl_amd import kernels as K
+
+    dev = torch.device("cuda", 0)
+    H, V, N = 896, 151936, args.rows
+    g = torch.Generator(device=dev).manual_seed(1)
+    w = (torch.randn(V, H, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    h = torch.randn(N, H, device=dev, generator=g).to(torch.bfloat16)
+    lab = torch.randint(0, V, (N,), device=dev, generator=g)
+    g1 = torch.randn(N, device=dev, generator=g)
+    out = {"rows": N, "H": H, "V": V}
+    with torch.no_grad():
+        _, ent, lse = torch.ops.verl_amd.logprob_entropy_fwd(h @ w.t(), lab, 1.0, 0)
+    flops = 2.0 * N * V * H
+
+    # ---- kernel level
+    dlog = torch.empty(N, V, dtype=torch.bfloat16, device=dev)
+    ms, ts = timed(lambda: K._linear_logprob_bwd_raw(h, w, lab, lse, ent, g1, None, 1.0, False, dlog), args.iters)
+    out["fused_dlogits_ms"] = round(ms, 3)
+    out["fused_dlogits_tflops"] = round(flops / ms / 1e9, 1)
+    logits = dlog  # reuse the buffer for the composition
+
+    def compose():
+        torch.matmul(h, w.t(), out=logits)
+        torch.ops.verl_amd.logprob_entropy_bwd_(g1, None, logits, lab, lse, ent, 1.0)
+
+    ms_c, _ = timed(compose, args.iters)
+    out["compose_gemm_plus_stream_bwd_ms"] = round(ms_c, 3)
+    del dlog, logits
+    torch.cuda.empty_cache()
+
+    # ---- pass level (forward + backward of the lm_head + log-prob, with GEMMs)
+    def fused_pass():
+        ha, wa = h.detach().requires_grad_(True), w.detach().requires_grad_(True)
+        lp, _ = K.linear_logprob_entropy(ha, wa, lab, 1.0)
+        (lp * g1).sum().backward()
+
+    def unfused_pass():
+        ha, wa = h.detach().requires_grad_(True), w.detach().requires_grad_(True)
+        lp, _ = K.logprob_entropy(K.linear(ha, wa), lab, 1.0, inplace_backward="auto")
+        (lp * g1).sum().backward()
+
+    for name, fn in (("fused_pass", fused_pass), ("unfused_pass", unfused_pass)):
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats()
+        base = torch.cuda.memory_allocated()
+        ms_p, _ = timed(fn, args.iters)
+        out[f"{name}_ms"] = round(ms_p, 3)
+        out[f"{name}_peak_extra_gb"] = round((torch.cuda.max_memory_allocated() - base) / 1e9, 2)
+    out["fused_chunk_mb"] = K._LinearLogprob.CHUNK_BYTES >> 20
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

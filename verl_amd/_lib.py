@@ -98,6 +98,10 @@ _SIGNATURES: dict[str, tuple] = {
     "va_linear_logprob_fwd": (
         c_int, [_P, c_int64, _P, c_int64, c_int, _P, c_int64, c_int64, c_int64, c_float, c_int, _P, _P, _P, _P, _P]
     ),
+    "va_linear_logprob_bwd": (
+        c_int, [_P, c_int64, _P, c_int64, c_int, _P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_float, c_int, _P,
+                c_int64, _P]
+    ),
     "va_flash_attn_fwd": (
         c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, c_float, _P, _P, _P]
     ),
@@ -137,12 +141,17 @@ def load():
             "(python -m verl_amd.build, or __graft_entry__.build())"
         )
     lib = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+    # VERL_AMD_LIB_AB=1: an older build loaded for an A/B timing run (tools/f1_ab.py) may lack
+    # newer entry points and carry an older ABI version; only what it exports is bound
+    ab = os.environ.get("VERL_AMD_LIB_AB") == "1"
     for name, (res, args) in _SIGNATURES.items():
+        if ab and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.va_abi_version() != 4:
-        raise NativeLibraryError(f"ABI version mismatch: {lib.va_abi_version()} != 4")
+    if lib.va_abi_version() != 5 and not ab:
+        raise NativeLibraryError(f"ABI version mismatch: {lib.va_abi_version()} != 5")
     _lib = lib
     return lib
 

@@ -334,40 +334,18 @@ __device__ __forceinline__ void t_tile_epilogue(const f32x4 (&acc)[8][4], int v0
   }
 }
 
-template <bool SCALE, bool ROUND, bool REMAP>
-__global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
-    const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
-    const int64_t *__restrict__ labels, int64_t N, int K, int64_t V, int splits, int tiles_per_split,
-    float temperature, float *__restrict__ part, float *__restrict__ label_logit) {
-  // ONE LDS array (a second __shared__ object can cost a vmcnt(0) per K-step): 2 staging buffers of
-  // (weight, hidden) images; reused for the final merge of the two vocab wave-rows
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// The persistent transposed sweep shared by the forward and the backward kernels: for each vocab tile
+// of [vt_begin, vt_end) it accumulates S^T = W_tile . H_tile^T (256 vocab x 256 tokens) over K in acc,
+// calls tile(acc, vt) once the tile is complete, and zeroes acc. acc[i][j][e] holds vocab
+// vt * 256 + wr * 128 + (lane >> 4) * 4 + i * 16 + e for token row0 + wc * 64 + j * 16 + (lane & 15).
+template <typename Tile>
+__device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int64_t ldh,
+                                           const uint16_t *__restrict__ w, int64_t ldw, int64_t N, int K, int64_t V,
+                                           int64_t row0, int64_t vt_begin, int64_t vt_end, uint16_t *lds, int wave,
+                                           int lane, Tile &&tile) {
   const int wr = wave >> 2, wc = wave & 3;
-  int64_t L = blockIdx.x;
-  if (REMAP) {  // blocks b, b + 8, ... share an XCD: give each XCD a contiguous run of logical ids
-    const int64_t nl = gridDim.x >> 3;
-    L = (L & 7) * nl + (L >> 3);
-  }
-  const int64_t rb = L / splits, sp = L % splits;
-  const int64_t row0 = rb * TB;
-  const int64_t n_vt = (V + TB - 1) / TB;
-  const int64_t vt_begin = sp * tiles_per_split;
-  const int64_t vt_end = vt_begin + tiles_per_split < n_vt ? vt_begin + tiles_per_split : n_vt;
   const int nk = K / TK;
   const int64_t nsteps = vt_begin < vt_end ? (vt_end - vt_begin) * nk : 0;
-
-  // this lane's 4 tokens (columns of the transposed tile), their labels and online states
-  int lab[4];
-  float m[4], s[4], t[4], ll[4];  // ll: the label's logit, -inf until this lane meets it
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t r = row0 + wc * 64 + j * 16 + (lane & 15);
-    const int64_t lb = r < N ? labels[r] : -1;
-    lab[j] = (lb >= 0 && lb < V) ? static_cast<int>(lb) : -1;
-    m[j] = -INFINITY, s[j] = 0.f, t[j] = 0.f, ll[j] = -INFINITY;
-  }
-
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -408,20 +386,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
     if (kt == nk - 1) {
-      // acc[i][j][e] = logit of vocab v0 + i * 16 + e for token j of this lane
-      const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;  // V < 2^31
-      if (vt * TB + TB > V) {  // uniform: only the last vocab tile has rows past V
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (v0 + i * 16 + e >= V)
-#pragma unroll
-              for (int j = 0; j < 4; ++j) acc[i][j][e] = -INFINITY;
-        t_tile_epilogue<SCALE, ROUND, true>(acc, v0, lab, m, s, t, ll, temperature);
-      } else {
-        t_tile_epilogue<SCALE, ROUND, false>(acc, v0, lab, m, s, t, ll, temperature);
-      }
+      tile(acc, vt);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -430,6 +395,66 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
+}
+
+// this workgroup's (row block, vocab range): blocks b, b + 8, ... share an XCD, so with REMAP each XCD
+// gets a contiguous run of logical ids (split fastest)
+template <bool REMAP>
+__device__ __forceinline__ void t256_block(int splits, int tiles_per_split, int64_t V, int64_t &row0,
+                                           int64_t &sp, int64_t &vt_begin, int64_t &vt_end) {
+  int64_t L = blockIdx.x;
+  if (REMAP) {
+    const int64_t nl = gridDim.x >> 3;
+    L = (L & 7) * nl + (L >> 3);
+  }
+  const int64_t rb = L / splits;
+  sp = L % splits;
+  row0 = rb * TB;
+  const int64_t n_vt = (V + TB - 1) / TB;
+  vt_begin = sp * tiles_per_split;
+  vt_end = vt_begin + tiles_per_split < n_vt ? vt_begin + tiles_per_split : n_vt;
+}
+
+template <bool SCALE, bool ROUND, bool REMAP>
+__global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
+    const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
+    const int64_t *__restrict__ labels, int64_t N, int K, int64_t V, int splits, int tiles_per_split,
+    float temperature, float *__restrict__ part, float *__restrict__ label_logit) {
+  // ONE LDS array (a second __shared__ object can cost a vmcnt(0) per K-step): 2 staging buffers of
+  // (weight, hidden) images; reused for the final merge of the two vocab wave-rows
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  int64_t row0, sp, vt_begin, vt_end;
+  t256_block<REMAP>(splits, tiles_per_split, V, row0, sp, vt_begin, vt_end);
+
+  // this lane's 4 tokens (columns of the transposed tile), their labels and online states
+  int lab[4];
+  float m[4], s[4], t[4], ll[4];  // ll: the label's logit, -inf until this lane meets it
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t r = row0 + wc * 64 + j * 16 + (lane & 15);
+    const int64_t lb = r < N ? labels[r] : -1;
+    lab[j] = (lb >= 0 && lb < V) ? static_cast<int>(lb) : -1;
+    m[j] = -INFINITY, s[j] = 0.f, t[j] = 0.f, ll[j] = -INFINITY;
+  }
+
+  t256_sweep(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
+    // acc[i][j][e] = logit of vocab v0 + i * 16 + e for token j of this lane
+    const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;  // V < 2^31
+    if (vt * TB + TB > V) {  // uniform: only the last vocab tile has rows past V
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (v0 + i * 16 + e >= V)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j][e] = -INFINITY;
+      t_tile_epilogue<SCALE, ROUND, true>(acc, v0, lab, m, s, t, ll, temperature);
+    } else {
+      t_tile_epilogue<SCALE, ROUND, false>(acc, v0, lab, m, s, t, ll, temperature);
+    }
+  });
 
   // merge the 4 lane groups (lanes l, l ^ 16, l ^ 32, l ^ 48 hold the same tokens), then the two
   // vocab wave-rows through LDS (free now: every DMA was waited for), in fixed order
@@ -500,6 +525,82 @@ __global__ __launch_bounds__(256) void linear_logprob_merge_kernel(const float *
   else if (lab < 0 || lab >= V) lp = __builtin_nanf("");
   else lp = label_logit[r] - lse;
   logp[r] = lp;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused backward (f1): the same transposed sweep recomputes each 256 x 256 logits tile and turns it
+// into dlogits in registers, written once as bf16 [N, V] (row stride ldd) for the lm_head's two
+// backward GEMMs; the logits never exist in HBM. Per element the arithmetic is
+// logprob_entropy_bwd's (logprob.hip): with z the logit as the forward saw it (bf16 rounding and
+// div_(T) unless fp32 logits), p = 2^(z L - lse L), dz = -p (gh z + kk) (+ g_lp at the label),
+// kk = gh (H - lse) + g_lp, dx = dz / T, rounded to bf16 (the reference's fused backward,
+// kernels.py:1241-1342, forms the same d_logits per vocab split). Each lane owns 4 consecutive vocab
+// entries of a token per (i, j): one 8-byte store. Rows >= N and vocab >= V are computed, not stored.
+template <bool SCALE, bool ROUND, bool REMAP>
+__global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
+    const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
+    const int64_t *__restrict__ labels, const float *__restrict__ lse_in, const float *__restrict__ ent_in,
+    const float *__restrict__ g_logp, const float *__restrict__ g_ent, int64_t N, int K, int64_t V, int splits,
+    int tiles_per_split, float temperature, uint16_t *__restrict__ dlog, int64_t ldd) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  int64_t row0, sp, vt_begin, vt_end;
+  t256_block<REMAP>(splits, tiles_per_split, V, row0, sp, vt_begin, vt_end);
+
+  // this lane's 4 tokens: label, and the row scalars as logprob_entropy_bwd derives them
+  int lab[4];
+  float glp[4], gh[4], kk[4], nlb[4];
+  uint16_t *drow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t r = row0 + wc * 64 + j * 16 + (lane & 15);
+    const bool ok = r < N;
+    const int64_t lb = ok ? labels[r] : -1;
+    const bool has_lab = lb >= 0 && lb < V;
+    lab[j] = has_lab ? static_cast<int>(lb) : -1;
+    glp[j] = (ok && g_logp != nullptr && has_lab) ? g_logp[r] : 0.f;
+    gh[j] = (ok && g_ent != nullptr) ? g_ent[r] : 0.f;
+    const float lse = ok ? lse_in[r] : 0.f;
+    const float h = (ok && g_ent != nullptr) ? ent_in[r] : 0.f;
+    kk[j] = fmaf(gh[j], h - lse, glp[j]);
+    nlb[j] = -lse * kLog2eF;
+    drow[j] = ok ? dlog + r * ldd : nullptr;
+  }
+
+  t256_sweep(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
+    const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int vb = v0 + i * 16;  // this lane's 4 vocab entries vb .. vb + 3 (V % 4 == 0)
+        float d[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float z = logit_of<SCALE, ROUND>(acc[i][j][e], temperature);
+          const float p = __builtin_amdgcn_exp2f(fmaf(z, kLog2eF, nlb[j]));
+          d[e] = -p * fmaf(gh[j], z, kk[j]);
+        }
+        const int dl = lab[j] - vb;
+        if (dl >= 0 && dl < 4) {  // one lane per token
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (e == dl) d[e] += glp[j];
+        }
+        if constexpr (SCALE) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) d[e] = d[e] / temperature;
+        }
+        if (drow[j] != nullptr && vb < V) {
+          uint2 q;
+          q.x = pack2_bf16(d[0], d[1]);
+          q.y = pack2_bf16(d[2], d[3]);
+          *reinterpret_cast<uint2 *>(drow[j] + vb) = q;
+        }
+      }
+    }
+  });
 }
 
 }  // namespace
@@ -588,4 +689,64 @@ extern "C" int va_linear_logprob_fwd(const void *hidden, int64_t ldh, const void
   hipLaunchKernelGGL(linear_logprob_merge_kernel, dim3(static_cast<unsigned>((N + 255) / 256)), dim3(256), 0, s,
                      part, label_logit, labels, N, V, splits, logp, entropy, lse);
   return check_launch("linear_logprob_fwd");
+}
+
+template <bool SC, bool RD>
+static void launch_bwd_t256(bool remap, dim3 grid, hipStream_t s, const uint16_t *h16, int64_t ldh,
+                            const uint16_t *w16, int64_t ldw, const int64_t *labels, const float *lse,
+                            const float *ent, const float *g_logp, const float *g_ent, int64_t N, int64_t H,
+                            int64_t V, int used, int per, float temperature, uint16_t *dlog, int64_t ldd) {
+  if (remap)
+    hipLaunchKernelGGL((linear_logprob_bwd_t256_kernel<SC, RD, true>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16,
+                       ldw, labels, lse, ent, g_logp, g_ent, N, static_cast<int>(H), V, used, per, temperature, dlog,
+                       ldd);
+  else
+    hipLaunchKernelGGL((linear_logprob_bwd_t256_kernel<SC, RD, false>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16,
+                       ldw, labels, lse, ent, g_logp, g_ent, N, static_cast<int>(H), V, used, per, temperature, dlog,
+                       ldd);
+}
+
+extern "C" int va_linear_logprob_bwd(const void *hidden, int64_t ldh, const void *weight, int64_t ldw, int dtype,
+                                     const int64_t *labels, const float *lse, const float *entropy,
+                                     const float *g_logp, const float *g_entropy, int64_t N, int64_t H, int64_t V,
+                                     float temperature, int splits, void *dlogits, int64_t ldd, void *stream) {
+  const bool fp32_logits = (dtype & VA_LOGITS_F32) != 0;
+  dtype &= ~VA_LOGITS_F32;
+  VA_CHECK_ARG(dtype == VA_BF16, "linear_logprob_bwd: only bf16 hidden / weight are implemented");
+  VA_CHECK_ARG(N >= 0 && H > 0 && V > 0 && H % TK == 0 && H <= (1 << 20) && V % 4 == 0 && V < (int64_t{1} << 31),
+               "linear_logprob_bwd: need H %% 64 == 0 and V %% 4 == 0 (H=%lld, V=%lld)", static_cast<long long>(H),
+               static_cast<long long>(V));
+  VA_CHECK_ARG(ldh >= H && ldw >= H && ldh % 8 == 0 && ldw % 8 == 0 && ldd >= V && ldd % 4 == 0,
+               "linear_logprob_bwd: strides must be >= H (ldd >= V), %% 8 (ldd %% 4)");
+  VA_CHECK_ARG(splits >= 1 && splits <= 64, "linear_logprob_bwd: splits in [1, 64]");
+  VA_CHECK_ARG(temperature > 0.f, "linear_logprob_bwd: temperature must be > 0");
+  if (N == 0) return VA_OK;
+  VA_CHECK_ARG(hidden && weight && labels && lse && dlogits && (g_entropy == nullptr || entropy),
+               "null pointer argument");
+  VA_CHECK_ARG(reinterpret_cast<uintptr_t>(hidden) % 16 == 0 && reinterpret_cast<uintptr_t>(weight) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(dlogits) % 8 == 0,
+               "linear_logprob_bwd: 16-byte aligned hidden / weight and 8-byte aligned dlogits required");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n_vt = (V + TB - 1) / TB;
+  const int per = static_cast<int>((n_vt + splits - 1) / splits);
+  const int used = static_cast<int>((n_vt + per - 1) / per);
+  const int64_t nwg = ((N + TB - 1) / TB) * used;
+  VA_CHECK_ARG(nwg < (int64_t{1} << 31), "linear_logprob_bwd: grid too large");
+  const dim3 grid(static_cast<unsigned>(nwg));
+  const bool remap = nwg % 8 == 0;
+  const auto *h16 = static_cast<const uint16_t *>(hidden);
+  const auto *w16 = static_cast<const uint16_t *>(weight);
+  auto *d16 = static_cast<uint16_t *>(dlogits);
+  if (temperature == 1.0f) {
+    if (fp32_logits) launch_bwd_t256<false, false>(remap, grid, s, h16, ldh, w16, ldw, labels, lse, entropy, g_logp,
+                                                   g_entropy, N, H, V, used, per, temperature, d16, ldd);
+    else launch_bwd_t256<false, true>(remap, grid, s, h16, ldh, w16, ldw, labels, lse, entropy, g_logp, g_entropy, N,
+                                      H, V, used, per, temperature, d16, ldd);
+  } else {
+    if (fp32_logits) launch_bwd_t256<true, false>(remap, grid, s, h16, ldh, w16, ldw, labels, lse, entropy, g_logp,
+                                                  g_entropy, N, H, V, used, per, temperature, d16, ldd);
+    else launch_bwd_t256<true, true>(remap, grid, s, h16, ldh, w16, ldw, labels, lse, entropy, g_logp, g_entropy, N,
+                                     H, V, used, per, temperature, d16, ldd);
+  }
+  return check_launch("linear_logprob_bwd");
 }

@@ -52,7 +52,7 @@ class KernelTimer:
     def __init__(self):
         self.records: list[tuple[str, float, object, object]] = []
 
-    FLOP_KERNELS = frozenset({"linear_logprob_fwd"})
+    FLOP_KERNELS = frozenset({"linear_logprob_fwd", "linear_logprob_bwd"})
 
     def start(self, stream):
         ev = torch.cuda.Event(enable_timing=True)
@@ -194,14 +194,34 @@ def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float, fp32_log
     return logp, ent, lse
 
 
+def _linear_logprob_bwd_raw(hidden, weight, labels, lse, ent, g1, g2, temperature: float, fp32_logits: bool,
+                            dlogits):
+    """dlogits [n, V] bf16 of the rows of ``hidden`` by va_linear_logprob_bwd (no logits in HBM)."""
+    N, H = hidden.shape
+    V = weight.shape[0]
+    ev = TIMER.start(torch.cuda.current_stream(hidden.device)) if TIMER is not None else None
+    dtype = L.VA_BF16 | (L.VA_LOGITS_F32 if fp32_logits else 0)
+    L.call("va_linear_logprob_bwd", _p(hidden), hidden.stride(0), _p(weight), weight.stride(0), dtype, _p(labels),
+           _p(lse), _p(ent), _p(g1), _p(g2), N, H, V, float(temperature), _linear_logprob_splits(N), _p(dlogits),
+           dlogits.stride(0), _stream(hidden))
+    if ev is not None:  # MFMA-bound: the logits recompute, 2 N V H flops (+ 2 B per logit written)
+        TIMER.stop("linear_logprob_bwd", 2 * N * V * H, torch.cuda.current_stream(hidden.device), ev)
+
+
 class _LinearLogprob(torch.autograd.Function):
-    """Forward: one fused MFMA pass (no logits in HBM). Backward: logits are recomputed per row
-    chunk with a hipBLASLt GEMM, turned into dlogits in place by va_logprob_entropy_bwd, and
-    pushed through the two GEMMs of the lm_head (the reference's fused path also recomputes).
+    """Forward: one fused MFMA pass (no logits in HBM). Backward, per row chunk: the fused MFMA
+    kernel va_linear_logprob_bwd recomputes the logits tile by tile and writes bf16 dlogits (the
+    reference's d_logits_split_N kernel, kernels.py:1241-1342), then the lm_head's two GEMMs run on
+    them. ``VERL_AMD_F1_BWD=compose`` keeps the previous composition (hipBLASLt recompute of the
+    logits + va_logprob_entropy_bwd in place) for A/B runs.
     fp32_logits: the logits stay fp32 (no bf16 rounding) in both passes, as in the reference's
     fused kernel; dlogits are rounded to bf16 for the two GEMMs, as its backward's tl.dot inputs."""
 
-    CHUNK_BYTES = 2 << 30
+    # bytes of the per-chunk dlogits buffer (bf16 [rows, V]; the fused path holds no logits, so
+    # this is its whole [rows, V] footprint): by default the bench's 131,072-row pass is ONE chunk,
+    # so the lm_head GEMMs run at full size; a chunk the allocator cannot provide is halved until it
+    # fits (env VERL_AMD_F1_BWD_CHUNK_MB)
+    CHUNK_BYTES = int(os.environ.get("VERL_AMD_F1_BWD_CHUNK_MB", "49152")) << 20
 
     @staticmethod
     def forward(ctx, hidden, weight, labels, temperature, fp32_logits):
@@ -212,30 +232,67 @@ class _LinearLogprob(torch.autograd.Function):
         return logp, ent
 
     @staticmethod
+    def _chunk_buffer(rows: int, V: int, dtype, device):
+        while True:
+            try:
+                return torch.empty(rows, V, dtype=dtype, device=device), rows
+            except torch.OutOfMemoryError:
+                if rows <= 256:
+                    raise
+                rows = max(256, rows // 2)
+
+    @staticmethod
     def backward(ctx, g_logp, g_ent):
         hidden, weight, labels, lse, ent = ctx.saved_tensors
         N, H = hidden.shape
         V = weight.shape[0]
         g1 = None if g_logp is None else _f32(g_logp)
         g2 = None if g_ent is None else _f32(g_ent)
-        d_hidden = torch.empty_like(hidden) if ctx.needs_input_grad[0] else None
-        d_weight = torch.zeros_like(weight, dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        d_hidden = d_weight = None
         f32 = ctx.fp32_logits
-        rows = max(1, int(_LinearLogprob.CHUNK_BYTES // (V * (4 if f32 else hidden.element_size()))))
-        for r0 in range(0, N, rows):
+        fused = os.environ.get("VERL_AMD_F1_BWD", "fused") != "compose" and V % 4 == 0
+        width = 2 if fused else (4 if f32 else hidden.element_size())
+        rows = min(N, max(256, int(_LinearLogprob.CHUNK_BYTES // (V * width))))
+        # the lm_head's two backward GEMMs as the unfused actor runs them: dX over a transposed copy of
+        # W ("TN", input_grad) and dW as the swapped product (weight_grad)
+        wt = (transpose16(weight) if ctx.needs_input_grad[0] and _DGRAD_TN and weight.dtype == torch.bfloat16
+              else None)
+        r0 = 0
+        while r0 < N:
+            if fused:
+                dlog, rows = _LinearLogprob._chunk_buffer(min(rows, N - r0), V, hidden.dtype, hidden.device)
             r1 = min(N, r0 + rows)
             h = hidden[r0:r1]
-            logits = torch.mm(h, weight.t(), out_dtype=torch.float32) if f32 else h @ weight.t()
-            L.call("va_logprob_entropy_bwd", _p(g1[r0:r1] if g1 is not None else None),
-                   _p(g2[r0:r1] if g2 is not None else None), _p(logits), L.VA_F32 if f32 else L.VA_BF16, r1 - r0, V,
-                   logits.stride(0), _p(labels[r0:r1]), _p(lse[r0:r1]), _p(ent[r0:r1]), ctx.temperature, _p(logits),
-                   logits.stride(0), _stream(logits))
-            if f32:
-                logits = logits.to(hidden.dtype)
-            if d_hidden is not None:
-                torch.mm(logits, weight, out=d_hidden[r0:r1])
-            if d_weight is not None:
-                d_weight.add_((logits.t() @ h).float())
+            if fused:
+                dlog = dlog[: r1 - r0]
+                _linear_logprob_bwd_raw(h, weight, labels[r0:r1], lse[r0:r1], ent[r0:r1],
+                                        g1[r0:r1] if g1 is not None else None, g2[r0:r1] if g2 is not None else None,
+                                        ctx.temperature, f32, dlog)
+            else:
+                dlog = torch.mm(h, weight.t(), out_dtype=torch.float32) if f32 else h @ weight.t()
+                L.call("va_logprob_entropy_bwd", _p(g1[r0:r1] if g1 is not None else None),
+                       _p(g2[r0:r1] if g2 is not None else None), _p(dlog), L.VA_F32 if f32 else L.VA_BF16, r1 - r0,
+                       V, dlog.stride(0), _p(labels[r0:r1]), _p(lse[r0:r1]), _p(ent[r0:r1]), ctx.temperature,
+                       _p(dlog), dlog.stride(0), _stream(dlog))
+                if f32:
+                    dlog = dlog.to(hidden.dtype)
+            if ctx.needs_input_grad[0]:
+                dh = torch.nn.functional.linear(dlog, wt) if wt is not None else dlog @ weight
+                if r0 == 0 and r1 == N:
+                    d_hidden = dh
+                else:
+                    if d_hidden is None:
+                        d_hidden = torch.empty_like(hidden)
+                    d_hidden[r0:r1].copy_(dh)
+                del dh
+            if ctx.needs_input_grad[1]:
+                dw = weight_grad(dlog, h)
+                if r0 == 0 and r1 == N:
+                    d_weight = dw
+                else:
+                    d_weight = dw.float() if d_weight is None else d_weight.add_(dw.float())
+            del dlog
+            r0 = r1
         if d_weight is not None:
             d_weight = d_weight.to(weight.dtype)
         return d_hidden, d_weight, None, None, None
