@@ -721,16 +721,6 @@ WGRAD_SWAP_MIN_OUT = 65536  # the lm_head (V = 151,936 outputs)
 _OWN_WGRAD = os.environ.get("VERL_AMD_WGRAD", "own") != "hipblaslt"
 
 
-def own_wgrad_splits(n_out: int, n_in: int) -> int:
-    """K slices of va_weight_grad: one round of workgroups when it fills >= 85 % of the 256 CUs
-    (down 3, q|k|v 12, o 16 at H = 896), else about three full rounds (gate|up: 152 tiles x 5)."""
-    tiles = -(-n_out // 256) * -(-n_in // 256)
-    one = 256 // tiles
-    if one >= 1 and tiles * one >= 0.85 * 256:
-        return one
-    return max(1, round(768 / tiles))
-
-
 # the shape class it was measured on: outputs of at most one round of 256 x 256 tiles (the H = 896
 # backbone: 16-152 tiles), where hipBLASLt leaves CUs idle or splits K in batched fp32 GEMMs; larger
 # outputs (the 7B / 8B configs' 1,000+ tiles) keep hipBLASLt
@@ -747,9 +737,9 @@ def _own_weight_grad(dy2, x2):
             or T % 32 or n_out % 8 or n_in % 8 or n_out >= WGRAD_SWAP_MIN_OUT or dy2.stride(1) != 1
             or x2.stride(1) != 1 or dy2.stride(0) % 8 or x2.stride(0) % 8 or (dy2.data_ptr() | x2.data_ptr()) % 16):
         return None
-    s = own_wgrad_splits(n_out, n_in)
+    s = 0  # automatic: va_weight_grad plans the tiles (remainder tiles for 896 = 3.5 x 256) and slices
     out = torch.empty(n_out, n_in, dtype=torch.bfloat16, device=dy2.device)
-    nb = L.load().va_weight_grad_workspace_bytes(n_out, n_in, s)
+    nb = L.load().va_weight_grad_workspace_bytes(T, n_out, n_in, s)
     ws = torch.empty(nb // 4, dtype=torch.float32, device=dy2.device) if nb else None
     L.call("va_weight_grad", _p(dy2), dy2.stride(0), _p(x2), x2.stride(0), T, n_out, n_in, s, _p(ws), _p(out),
            _stream(dy2))
