@@ -160,6 +160,8 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   VA_TUNE_WHITEN_SLICE_MIN / VA_TUNE_WHITEN_GRID (va_gae_advantage_return): partial count above
  *   which partials are merged in parallel slices first (default 4,096) and the statistics +
  *   whitening launch's grid cap (default 2,048); only the fp64 merge order changes;
+ *   VA_TUNE_WGRAD_REMAINDER (va_weight_grad): 1 (default) = a dimension that is 128 mod 256 gets its
+ *     last 128 rows / columns as 128 x 512 / 512 x 128 tiles; 0 = 256 x 256 tiles throughout.
  *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
  *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
@@ -179,6 +181,7 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_WHITEN_SLICE_MIN 15
 #define VA_TUNE_WHITEN_GRID 16
 #define VA_TUNE_LINEAR_LOGPROB_TILE 17
+#define VA_TUNE_WGRAD_REMAINDER 18
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------
@@ -381,10 +384,10 @@ int va_transpose_16(const void *in, int64_t ld_in, int64_t R, int64_t C, void *o
 /* weight_grad: dW [M, N] bf16 (row-major, contiguous) = dY [K, M]^T X [K, N] (row strides ldy / ldx,
  * bf16, fp32 accumulation), the backward weight gradient of the backbone's linear layers (K = packed
  * tokens; no reference counterpart: torch's linear backward under FSDP, dp_actor.py:465-470). K a
- * multiple of 32; M, N, strides multiples of 8; 16-byte aligned buffers. splits > 1 cuts K into that
- * many slices (fp32 partials in workspace = va_weight_grad_workspace_bytes(M, N, splits), summed in
+ * multiple of 32; M, N, strides multiples of 8; 16-byte aligned buffers. splits: K slices (0 =
+ * automatic; fp32 partials in workspace = va_weight_grad_workspace_bytes(K, M, N, splits), summed in
  * slice order, rounded once). Not a §8 row. */
-int64_t va_weight_grad_workspace_bytes(int64_t M, int64_t N, int splits);
+int64_t va_weight_grad_workspace_bytes(int64_t K, int64_t M, int64_t N, int splits);
 int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_t ldx, int64_t K, int64_t M, int64_t N,
                    int splits, float *workspace, void *out, void *stream);
 

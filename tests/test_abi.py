@@ -69,7 +69,7 @@ def test_argument_validation_without_device(lib):
     # weight gradient: tokens not a multiple of 32
     rc = lib.va_weight_grad(1, 64, 1, 64, 100, 64, 64, 1, None, 1, None)
     assert rc == -1 and b"multiple of 32" in lib.va_last_error()
-    assert lib.va_weight_grad_workspace_bytes(64, 32, 3) == 4 * 3 * 64 * 32
+    assert lib.va_weight_grad_workspace_bytes(4096, 64, 32, 3) == 4 * 3 * 64 * 32
     rc = lib.va_group_coef(1, None, 1, 1, 4, 8, 1e-6, L.VA_ADV_OPO, 1, None)
     assert rc == -1 and b"lengths" in lib.va_last_error()
     assert lib.va_logprob_entropy_fwd(None, 1, 0, 10, 10, None, 1.0, None, None, None, None) == 0  # n_rows 0: no-op

@@ -16,7 +16,7 @@ def _call(dy, x, splits):
     T, M = dy.shape
     N = x.shape[1]
     out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
-    nb = L.load().va_weight_grad_workspace_bytes(M, N, splits)
+    nb = L.load().va_weight_grad_workspace_bytes(T, M, N, splits)
     ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=DEV)
     L.call("va_weight_grad", K._p(dy), dy.stride(0), K._p(x), x.stride(0), T, M, N, splits, K._p(ws), K._p(out),
            K._stream(dy))
@@ -33,9 +33,12 @@ def _check(got, want):
     assert err <= 8e-3 * scale + 1e-6, (err, scale)
 
 
-@pytest.mark.parametrize("T,M,N", [(2048, 1152, 896), (4096, 896, 4864), (1024, 200, 136), (96, 264, 512)])
-@pytest.mark.parametrize("splits", [1, 3, 8])
+@pytest.mark.parametrize("T,M,N", [(2048, 1152, 896), (4096, 896, 4864), (1024, 200, 136), (96, 264, 512),
+                                   (2048, 9728, 896), (1024, 384, 640), (1024, 896, 896)])
+@pytest.mark.parametrize("splits", [0, 1, 3, 8])
 def test_weight_grad_matches_fp32_reference(T, M, N, splits):
+    """splits 0 = automatic (with the 512 x 128 / 128 x 512 remainder tiles when a dimension is 128
+    mod 256: 896, 640, 384); explicit splits run one 256 x 256 launch only when there is no remainder."""
     g = torch.Generator(device=DEV).manual_seed(T + M + N)
     dy = (torch.randn(T, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
     x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
@@ -72,6 +75,26 @@ def test_product_dispatch_uses_it_and_falls_back():
     dy = (torch.randn(4096, 1152, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
     x = torch.randn(4096, 896, device=DEV, generator=g).to(torch.bfloat16)
     got = K.weight_grad(dy, x)
-    assert torch.equal(got, _call(dy, x, K.own_wgrad_splits(1152, 896)))
+    assert torch.equal(got, _call(dy, x, 0))
     odd = K.weight_grad(dy[:4000], x[:4000])  # hipBLASLt path
     _check(odd, _ref(dy[:4000], x[:4000]))
+
+
+@pytest.mark.parametrize("T,M,N", [(4096, 9728, 896), (4096, 896, 4864), (2048, 896, 896)])
+def test_remainder_tiles_match_full_tiles(T, M, N):
+    """VA_TUNE_WGRAD_REMAINDER 0 (256 x 256 tiles throughout) and 1 (remainder tiles) agree to fp32
+    summation order: both within the bf16 tolerance of the reference."""
+    from verl_amd import _lib as L
+
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    dy = (torch.randn(T, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
+    want = _ref(dy, x)
+    try:
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, 0)
+        full = _call(dy, x, 0)
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, 1)
+    rem = _call(dy, x, 0)
+    _check(full, want)
+    _check(rem, want)

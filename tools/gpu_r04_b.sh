@@ -14,3 +14,8 @@ timeout -k 10 400 python bench.py --steps 3 --warmup 1 --out $O/bench_b_default.
 head -c 700 $O/bench_b_default.json; echo
 timeout -k 10 400 python bench.py --steps 3 --warmup 1 --fused-kernels 1 --no-cpu-baseline --out $O/bench_b_fused.json > $O/bench_b_fused.log 2>&1 || { echo "bench fused FAILED"; tail -30 $O/bench_b_fused.log; exit 1; }
 head -c 700 $O/bench_b_fused.json; echo
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 300 python tools/lm_head_gap.py > $O/lm_head_gap.json 2>$O/lm_head_gap.err || { echo "lm_head_gap FAILED"; tail -20 $O/lm_head_gap.err; exit 1; }
+cat $O/lm_head_gap.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_lm_head_gap -o lm_head_gap -- python tools/lm_head_gap.py > $O/lm_head_gap_prof.log 2>&1 || { echo "rocprof lm_head_gap FAILED"; tail -20 $O/lm_head_gap_prof.log; exit 1; }
+find $O/prof_lm_head_gap -name "*kernel_stats.csv" | head -3

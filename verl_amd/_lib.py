@@ -35,6 +35,7 @@ VA_TUNE_FLASH_GROUPED_DKDV, VA_TUNE_GAE_VARIANT, VA_TUNE_BWD_FLAT, VA_TUNE_SWIGL
 VA_TUNE_FLASH_DKDV_QT, VA_TUNE_FLASH_DQ_KB, VA_TUNE_FLASH_FWD_KB, VA_TUNE_GAE_PARTIALS = 9, 10, 11, 12
 VA_TUNE_GAE_NT, VA_TUNE_LOSS_VEC = 13, 14
 VA_TUNE_WHITEN_SLICE_MIN, VA_TUNE_WHITEN_GRID, VA_TUNE_LINEAR_LOGPROB_TILE = 15, 16, 17
+VA_TUNE_WGRAD_REMAINDER = 18
 
 _P = c_void_p
 _SIGNATURES: dict[str, tuple] = {
@@ -113,7 +114,7 @@ _SIGNATURES: dict[str, tuple] = {
     "va_karmarkar_karp": (c_int, [_P, c_int64, c_int64, c_int, _P, _P]),
     "va_rope_qkv_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, c_int64, _P]),
     "va_transpose_16": (c_int, [_P, c_int64, c_int64, c_int64, _P, c_int64, _P]),
-    "va_weight_grad_workspace_bytes": (c_int64, [c_int64, c_int64, c_int]),
+    "va_weight_grad_workspace_bytes": (c_int64, [c_int64, c_int64, c_int64, c_int]),
     "va_weight_grad": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int64, c_int64, c_int, _P, _P, _P]),
 }
 

@@ -27,28 +27,32 @@
 namespace va {
 namespace {
 
-constexpr int WBM = 256, WBN = 256, WBK = 32, WNT = 512, WNSTAGE = 4;
-constexpr int WIMG = WBK * 256;  // bf16 elements of one operand's step image
+constexpr int WBK = 32, WNT = 512;
 
 typedef short wbf16x8 __attribute__((ext_vector_type(8)));
 typedef int wv2i __attribute__((ext_vector_type(2)));
 typedef float wf32x16 __attribute__((ext_vector_type(16)));
 
-// element offset of (row, col) in a [32][256] image with 16-B chunks XOR-swizzled by (row & 3) << 2
+// element offset of (row, col) in a [32][C] image (C = 128, 256 or 512 columns) with 16-B chunks
+// XOR-swizzled by (row & 3) << 2 (every row length is a multiple of the 64 banks' 256 bytes' worth of
+// words, so the swizzle alone spreads a transposed read's 4 rows over all banks)
+template <int C>
 __device__ __forceinline__ int w_off(int row, int col) {
-  return row * 256 + (((col >> 3) ^ ((row & 3) << 2)) << 3) + (col & 7);
+  return row * C + (((col >> 3) ^ ((row & 3) << 2)) << 3) + (col & 7);
 }
 
-// LDS-DMA of one operand's 32 x 256 step image: wave w issues pieces 2w, 2w + 1, piece g = rows 2g,
-// 2g + 1; lane l lands at physical chunk l & 31 of row 2g + (l >> 5) and so fetches the logical
-// chunk the swizzle puts there
+// LDS-DMA of one operand's 32 x C step image: 1 KiB pieces of 512 / C rows, C / 128 per wave; lane l
+// of piece g lands at physical chunk l % (C / 8) of row g (512 / C) + l / (C / 8) and so fetches the
+// logical chunk the swizzle puts there
+template <int C>
 __device__ __forceinline__ void w_stage(const uint16_t *__restrict__ src, int64_t ld, int64_t k0, int col0, int ncols,
                                         uint16_t *img, int wave, int lane) {
+  constexpr int PW = C / 128, RPP = 512 / C, CPR = C / 8;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int g = wave * 2 + i;
-    const int row = 2 * g + (lane >> 5);
-    const int c = (lane & 31) ^ ((row & 3) << 2);
+  for (int i = 0; i < PW; ++i) {
+    const int g = wave * PW + i;
+    const int row = g * RPP + lane / CPR;
+    const int c = (lane % CPR) ^ ((row & 3) << 2);
     int col = col0 + c * 8;
     if (col > ncols - 8) col = ncols - 8;  // clamped: results for these columns are dropped
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + (k0 + row) * ld + col), img + g * 512, 16,
@@ -66,12 +70,24 @@ __device__ __forceinline__ wv2i w_tr_read(const uint16_t *p) {
 
 // 32 columns x 16 k fragment (MFMA A or B operand) by two transposed reads; element j of lane
 // (column col_base + (lane & 31)) = image[16 ss + 8 (j >> 2) + 4 h + (j & 3)][column]
+template <int C>
 __device__ __forceinline__ void w_frag(const uint16_t *img, int ss, int col_base, int lane, wv2i &lo, wv2i &hi) {
   const int h = lane >> 5, g16 = lane >> 4, li = lane & 15;
   const int r0 = 16 * ss + 4 * h + (li >> 2);
   const int col = col_base + 16 * (g16 & 1) + 4 * (li & 3);
-  lo = w_tr_read(img + w_off(r0, col));
-  hi = w_tr_read(img + w_off(r0 + 8, col));
+  lo = w_tr_read(img + w_off<C>(r0, col));
+  hi = w_tr_read(img + w_off<C>(r0 + 8, col));
+}
+
+// retire all but N of this wave's LDS-DMA instructions (N a literal of the counted-wait encoding)
+template <int N>
+__device__ __forceinline__ void w_vm_wait() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else static_assert(N == 0, "unsupported vmcnt");
 }
 
 __device__ __forceinline__ wbf16x8 w_join(wv2i lo, wv2i hi) {
@@ -80,16 +96,22 @@ __device__ __forceinline__ wbf16x8 w_join(wv2i lo, wv2i hi) {
 
 __device__ __forceinline__ int w_crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-template <bool PARTIAL>
+// TM x TN output tile (256 x 256, or 512 x 128 / 128 x 512 for the 128-wide remainder of a
+// dimension that is 128 mod 256): 8 waves of 128 x 64 as (TM / 128) x (TN / 64); NST-deep ring
+template <bool PARTIAL, int TM, int TN, int NST>
 __global__ __launch_bounds__(WNT, 1) void wgrad_kernel(const uint16_t *__restrict__ dy, int64_t ldy,
                                                        const uint16_t *__restrict__ x, int64_t ldx, int64_t K, int M,
                                                        int N, int splits, int64_t kslice, float *__restrict__ part,
-                                                       uint16_t *__restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[WNSTAGE * 2 * WIMG];  // [stage][A | B][32][256]
+                                                       uint16_t *__restrict__ out, int64_t ldo) {
+  constexpr int WN_W = TN / 64;                      // waves along n
+  constexpr int AIMG = WBK * TM, BIMG = WBK * TN;    // step images
+  constexpr int PER = (TM + TN) / 128;               // LDS-DMA instructions per wave per step
+  static_assert((TM / 128) * WN_W == 8, "8 waves of 128 x 64");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[NST * (AIMG + BIMG)];  // [stage][A | B]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int nbn = (N + WBN - 1) / WBN, nbm = (M + WBM - 1) / WBM;
+  const int wm = wave / WN_W, wn = wave % WN_W;
+  const int nbn = (N + TN - 1) / TN, nbm = (M + TM - 1) / TM;
   // XCD-aware bijective remap: hardware ids w, w + 8, ... share an XCD; give them consecutive
   // logical tiles, n-tile fastest, so the n-tiles of one dY tile and K slice share an L2
   const int nwg = nbn * nbm * splits;
@@ -98,7 +120,7 @@ __global__ __launch_bounds__(WNT, 1) void wgrad_kernel(const uint16_t *__restric
   const int bn = logical % nbn;
   const int rest = logical / nbn;
   const int bm = rest % nbm, s = rest / nbm;
-  const int m0 = bm * WBM, n0 = bn * WBN;
+  const int m0 = bm * TM, n0 = bn * TN;
   const int64_t k_beg = static_cast<int64_t>(s) * kslice;
   const int64_t k_end = k_beg + kslice < K ? k_beg + kslice : K;
   const int nsteps = k_end > k_beg ? static_cast<int>((k_end - k_beg) / WBK) : 0;
@@ -111,34 +133,34 @@ __global__ __launch_bounds__(WNT, 1) void wgrad_kernel(const uint16_t *__restric
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  auto issue = [&](int st) {  // 4 LDS-DMA instructions per wave
-    uint16_t *img = lds + (st % WNSTAGE) * 2 * WIMG;
+  auto issue = [&](int st) {  // PER LDS-DMA instructions per wave
+    uint16_t *img = lds + (st % NST) * (AIMG + BIMG);
     const int64_t k0 = k_beg + static_cast<int64_t>(st) * WBK;
-    w_stage(dy, ldy, k0, m0, M, img, wave, lane);
-    w_stage(x, ldx, k0, n0, N, img + WIMG, wave, lane);
+    w_stage<TM>(dy, ldy, k0, m0, M, img, wave, lane);
+    w_stage<TN>(x, ldx, k0, n0, N, img + AIMG, wave, lane);
   };
-  for (int b = 0; b < WNSTAGE - 1; ++b)
+  for (int b = 0; b < NST - 1; ++b)
     if (b < nsteps) issue(b);
   for (int st = 0; st < nsteps; ++st) {
-    const int ahead = nsteps - 1 - st;  // steps issued after st (at most 2 here)
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int ahead = nsteps - 1 - st;  // steps issued after st (at most NST - 2 here)
+    if (NST >= 4 && ahead >= 2) w_vm_wait<2 * PER * (NST >= 4)>();
+    else if (ahead >= 1) w_vm_wait<PER>();
+    else w_vm_wait<0>();
     asm volatile("s_barrier" ::: "memory");
-    if (st + WNSTAGE - 1 < nsteps) issue(st + WNSTAGE - 1);
-    const uint16_t *ia = lds + (st % WNSTAGE) * 2 * WIMG;
-    const uint16_t *ib = ia + WIMG;
+    if (st + NST - 1 < nsteps) issue(st + NST - 1);
+    const uint16_t *ia = lds + (st % NST) * (AIMG + BIMG);
+    const uint16_t *ib = ia + AIMG;
 #pragma unroll
     for (int ss = 0; ss < WBK / 16; ++ss) {
       // issue order A0 B0 B1 A1 A2 A3 (2 reads each); each counted wait releases the fragments it
       // passes through while the later reads stay in flight
       wv2i a0, a1, a2, a3, a4, a5, a6, a7, b0, b1, b2, b3;
-      w_frag(ia, ss, wm * 128 + 0, lane, a0, a1);
-      w_frag(ib, ss, wn * 64 + 0, lane, b0, b1);
-      w_frag(ib, ss, wn * 64 + 32, lane, b2, b3);
-      w_frag(ia, ss, wm * 128 + 32, lane, a2, a3);
-      w_frag(ia, ss, wm * 128 + 64, lane, a4, a5);
-      w_frag(ia, ss, wm * 128 + 96, lane, a6, a7);
+      w_frag<TM>(ia, ss, wm * 128 + 0, lane, a0, a1);
+      w_frag<TN>(ib, ss, wn * 64 + 0, lane, b0, b1);
+      w_frag<TN>(ib, ss, wn * 64 + 32, lane, b2, b3);
+      w_frag<TM>(ia, ss, wm * 128 + 32, lane, a2, a3);
+      w_frag<TM>(ia, ss, wm * 128 + 64, lane, a4, a5);
+      w_frag<TM>(ia, ss, wm * 128 + 96, lane, a6, a7);
       asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1));
       const wbf16x8 fb0 = w_join(b0, b1);
       wbf16x8 fa = w_join(a0, a1);
@@ -174,15 +196,16 @@ __global__ __launch_bounds__(WNT, 1) void wgrad_kernel(const uint16_t *__restric
         const int m = m0 + wm * 128 + i * 32 + w_crow(r, h);
         if (m >= M) continue;
         if constexpr (PARTIAL) part[(static_cast<int64_t>(s) * M + m) * N + n] = acc[i][j][r];
-        else out[static_cast<int64_t>(m) * N + n] = static_cast<uint16_t>(pack2_bf16(acc[i][j][r], 0.f) & 0xffffu);
+        else out[m * ldo + n] = static_cast<uint16_t>(pack2_bf16(acc[i][j][r], 0.f) & 0xffffu);
       }
     }
 }
 
-// out[e] = bf16(sum_s part[s][e]) in slice order; 4 elements per thread (M N % 4 == 0)
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restrict__ part, int splits, int64_t mn,
-                                                           uint16_t *__restrict__ out) {
+// out[m][n] (row stride ldo) = bf16(sum_s part[s][m][n]) in slice order; 4 elements per thread (N % 4 == 0)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restrict__ part, int splits, int64_t M,
+                                                           int64_t N, uint16_t *__restrict__ out, int64_t ldo) {
   const int64_t e = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
+  const int64_t mn = M * N;
   if (e >= mn) return;
   float4 acc = *reinterpret_cast<const float4 *>(part + e);
   for (int s = 1; s < splits; ++s) {
@@ -192,7 +215,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restri
     acc.z += v.z;
     acc.w += v.w;
   }
-  *reinterpret_cast<uint2 *>(out + e) = make_uint2(pack2_bf16(acc.x, acc.y), pack2_bf16(acc.z, acc.w));
+  const int64_t m = e / N, n = e - m * N;
+  *reinterpret_cast<uint2 *>(out + m * ldo + n) = make_uint2(pack2_bf16(acc.x, acc.y), pack2_bf16(acc.z, acc.w));
 }
 
 }  // namespace
@@ -200,8 +224,90 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restri
 
 using namespace va;
 
-extern "C" int64_t va_weight_grad_workspace_bytes(int64_t M, int64_t N, int splits) {
-  return splits > 1 ? static_cast<int64_t>(sizeof(float)) * splits * M * N : 0;
+namespace {
+
+// fewest 32-token steps a slice gets: the 4-deep ring keeps 3 in flight, so a shorter slice is mostly
+// prologue / epilogue, and every slice costs an fp32 M x N partial that the reduce reads back
+constexpr int64_t kMinStepsPerSlice = 8;
+
+// K slices of one launch: one round of workgroups when it fills >= 85 % of the 256 CUs, else about
+// three full rounds; at most one slice per kMinStepsPerSlice steps (kernels.own_wgrad_splits mirrors it)
+int w_auto_splits(int64_t tiles, int64_t steps) {
+  int64_t s = 256 / tiles;
+  if (!(s >= 1 && tiles * s * 100 >= 85 * 256)) s = (768 + tiles / 2) / tiles;
+  const int64_t cap = steps / kMinStepsPerSlice;
+  if (s > cap) s = cap;
+  if (s < 1) s = 1;
+  return static_cast<int>(s > 256 ? 256 : s);
+}
+
+// The launches of one weight gradient: the 256 x 256 tiles, plus, when a dimension is 128 mod 256
+// (896 = 3.5 tiles at H = 896), its last 128 rows / columns as 128 x 512 / 512 x 128 tiles instead
+// of half-empty 256 x 256 ones.
+struct WPart {
+  int kind;  // 0: 256 x 256, 1: 512 x 128 (column remainder), 2: 128 x 512 (row remainder)
+  int64_t m0, n0, M, N;
+  int splits;
+};
+
+int w_plan(int64_t K, int64_t M, int64_t N, int splits, WPart (&p)[2]) {
+  const int64_t steps = K / WBK;
+  int n = 0;
+  if (N % 256 == 128 && N > 128) {
+    p[n++] = WPart{0, 0, 0, M, N - 128, 0};
+    p[n++] = WPart{1, 0, N - 128, M, 128, 0};
+  } else if (M % 256 == 128 && M > 128) {
+    p[n++] = WPart{0, 0, 0, M - 128, N, 0};
+    p[n++] = WPart{2, M - 128, 0, 128, N, 0};
+  } else {
+    p[n++] = WPart{0, 0, 0, M, N, 0};
+  }
+  for (int i = 0; i < n; ++i) {
+    const int tm = p[i].kind == 1 ? 512 : (p[i].kind == 2 ? 128 : 256);
+    const int tn = p[i].kind == 1 ? 128 : (p[i].kind == 2 ? 512 : 256);
+    const int64_t tiles = ((p[i].M + tm - 1) / tm) * ((p[i].N + tn - 1) / tn);
+    p[i].splits = (splits > 0 && n == 1) ? splits : w_auto_splits(tiles, steps);
+  }
+  return n;
+}
+
+int64_t w_part_bytes(const WPart &p) {
+  return p.splits > 1 ? static_cast<int64_t>(sizeof(float)) * p.splits * p.M * p.N : 0;
+}
+
+template <int TM, int TN, int NST>
+void w_launch(const WPart &p, const uint16_t *dy, int64_t ldy, const uint16_t *x, int64_t ldx, int64_t K,
+              float *ws, uint16_t *out, int64_t ldo, hipStream_t st) {
+  const int64_t steps = K / WBK;
+  const int64_t kslice = (steps + p.splits - 1) / p.splits * WBK;
+  const int64_t nwg = ((p.M + TM - 1) / TM) * ((p.N + TN - 1) / TN) * p.splits;
+  const uint16_t *dyp = dy + p.m0, *xp = x + p.n0;  // column offsets of the operands
+  uint16_t *op = out + p.m0 * ldo + p.n0;
+  if (p.splits == 1) {
+    hipLaunchKernelGGL((wgrad_kernel<false, TM, TN, NST>), dim3(static_cast<unsigned>(nwg)), dim3(WNT), 0, st, dyp,
+                       ldy, xp, ldx, K, static_cast<int>(p.M), static_cast<int>(p.N), 1, kslice, nullptr, op, ldo);
+  } else {
+    hipLaunchKernelGGL((wgrad_kernel<true, TM, TN, NST>), dim3(static_cast<unsigned>(nwg)), dim3(WNT), 0, st, dyp,
+                       ldy, xp, ldx, K, static_cast<int>(p.M), static_cast<int>(p.N), p.splits, kslice, ws, nullptr,
+                       ldo);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(static_cast<unsigned>((p.M * p.N / 4 + 255) / 256)), dim3(256), 0,
+                       st, ws, p.splits, p.M, p.N, op, ldo);
+  }
+}
+
+}  // namespace
+
+// va_set_tuning(VA_TUNE_WGRAD_REMAINDER): 1 (default) = the 128-wide remainder tiles above, 0 = every
+// tile 256 x 256 (A/B runs)
+int g_wgrad_remainder = 1;
+
+extern "C" int64_t va_weight_grad_workspace_bytes(int64_t K, int64_t M, int64_t N, int splits) {
+  WPart p[2];
+  const int n = g_wgrad_remainder ? w_plan(K, M, N, splits, p) : (p[0] = WPart{0, 0, 0, M, N, 0}, 1);
+  if (!g_wgrad_remainder) p[0].splits = splits > 0 ? splits : w_auto_splits(((M + 255) / 256) * ((N + 255) / 256), K / WBK);
+  int64_t b = 0;
+  for (int i = 0; i < n; ++i) b += w_part_bytes(p[i]);
+  return b;
 }
 
 extern "C" int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_t ldx, int64_t K, int64_t M, int64_t N,
@@ -212,7 +318,7 @@ extern "C" int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_
                "weight_grad: M, N must be multiples of 8 (M=%lld N=%lld)", static_cast<long long>(M),
                static_cast<long long>(N));
   VA_CHECK_ARG(ldy >= M && ldx >= N && ldy % 8 == 0 && ldx % 8 == 0, "weight_grad: bad leading dimensions");
-  VA_CHECK_ARG(splits >= 1 && splits <= 256, "weight_grad: splits must be in [1, 256]");
+  VA_CHECK_ARG(splits >= 0 && splits <= 256, "weight_grad: splits must be in [0, 256] (0 = automatic)");
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t mn = M * N;
   VA_CHECK_ARG(out != nullptr, "null pointer argument");
@@ -220,24 +326,29 @@ extern "C" int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_
     if (hipMemsetAsync(out, 0, mn * 2, st) != hipSuccess) return check_launch("weight_grad");
     return VA_OK;
   }
-  VA_CHECK_ARG(dy && x && (splits == 1 || workspace), "null pointer argument");
+  WPart p[2];
+  int n;
+  if (g_wgrad_remainder) {
+    n = w_plan(K, M, N, splits, p);
+  } else {
+    n = 1;
+    p[0] = WPart{0, 0, 0, M, N, splits > 0 ? splits : w_auto_splits(((M + 255) / 256) * ((N + 255) / 256), K / WBK)};
+  }
+  bool need_ws = false;
+  for (int i = 0; i < n; ++i) need_ws |= p[i].splits > 1;
+  VA_CHECK_ARG(dy && x && (!need_ws || workspace), "null pointer argument");
   VA_CHECK_ARG(((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) &
                 15) == 0,
                "weight_grad: 16-byte aligned buffers required");
-  const int64_t steps = K / WBK;
-  const int64_t kslice = (steps + splits - 1) / splits * WBK;
-  const int64_t nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN) * splits;
-  VA_CHECK_ARG(nwg < (int64_t{1} << 31), "weight_grad: grid too large");
   const auto *dy16 = static_cast<const uint16_t *>(dy);
   const auto *x16 = static_cast<const uint16_t *>(x);
-  if (splits == 1) {
-    hipLaunchKernelGGL(wgrad_kernel<false>, dim3(static_cast<unsigned>(nwg)), dim3(WNT), 0, st, dy16, ldy, x16, ldx, K,
-                       static_cast<int>(M), static_cast<int>(N), 1, kslice, nullptr, static_cast<uint16_t *>(out));
-  } else {
-    hipLaunchKernelGGL(wgrad_kernel<true>, dim3(static_cast<unsigned>(nwg)), dim3(WNT), 0, st, dy16, ldy, x16, ldx, K,
-                       static_cast<int>(M), static_cast<int>(N), splits, kslice, workspace, nullptr);
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(static_cast<unsigned>((mn / 4 + 255) / 256)), dim3(256), 0, st,
-                       workspace, splits, mn, static_cast<uint16_t *>(out));
+  auto *o16 = static_cast<uint16_t *>(out);
+  float *ws = workspace;
+  for (int i = 0; i < n; ++i) {
+    if (p[i].kind == 0) w_launch<256, 256, 4>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+    else if (p[i].kind == 1) w_launch<512, 128, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+    else w_launch<128, 512, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+    ws += w_part_bytes(p[i]) / static_cast<int64_t>(sizeof(float));
   }
   return check_launch("weight_grad");
 }

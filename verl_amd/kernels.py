@@ -806,18 +806,19 @@ WGRAD_MIN_STEPS_PER_SLICE = 8
 
 
 def own_wgrad_splits(n_out: int, n_in: int, tokens: int | None = None) -> int:
-    """K slices of va_weight_grad: one round of workgroups when it fills >= 85 % of the 256 CUs
+    """Host mirror of va_weight_grad's automatic slice count for one launch of 256 x 256 tiles
+    (w_auto_splits, csrc/wgrad.hip; the product passes splits = 0 and lets the library plan, which
+    also cuts a 128-wide remainder into its own tiles). K slices: one round of workgroups when it fills >= 85 % of the 256 CUs
     (down 3, q|k|v 12, o 16 at H = 896), else about three full rounds (gate|up: 152 tiles x 5);
     capped so that every slice keeps >= WGRAD_MIN_STEPS_PER_SLICE K-steps of ``tokens`` (ADVICE
     r3: 512 tokens = 16 steps no longer get 128-256 mostly empty slices and their workspace)."""
     tiles = -(-n_out // 256) * -(-n_in // 256)
-    one = 256 // tiles
-    if one >= 1 and tiles * one >= 0.85 * 256:
-        s = one
-    else:
-        s = max(1, round(768 / tiles))
+    s = 256 // tiles
+    if not (s >= 1 and tiles * s * 100 >= 85 * 256):
+        s = (768 + tiles // 2) // tiles
     if tokens is not None:
-        s = min(s, max(1, -(-tokens // 32) // WGRAD_MIN_STEPS_PER_SLICE))
+        s = min(s, (tokens // 32) // WGRAD_MIN_STEPS_PER_SLICE)
+    s = min(max(s, 1), 256)
     return s
 
 
@@ -837,9 +838,9 @@ def _own_weight_grad(dy2, x2):
             or T % 32 or n_out % 8 or n_in % 8 or n_out >= WGRAD_SWAP_MIN_OUT or dy2.stride(1) != 1
             or x2.stride(1) != 1 or dy2.stride(0) % 8 or x2.stride(0) % 8 or (dy2.data_ptr() | x2.data_ptr()) % 16):
         return None
-    s = own_wgrad_splits(n_out, n_in, T)
+    s = 0  # automatic: va_weight_grad plans the tiles (remainder tiles for 896 = 3.5 x 256) and slices
     out = torch.empty(n_out, n_in, dtype=torch.bfloat16, device=dy2.device)
-    nb = L.load().va_weight_grad_workspace_bytes(n_out, n_in, s)
+    nb = L.load().va_weight_grad_workspace_bytes(T, n_out, n_in, s)
     ws = torch.empty(nb // 4, dtype=torch.float32, device=dy2.device) if nb else None
     L.call("va_weight_grad", _p(dy2), dy2.stride(0), _p(x2), x2.stride(0), T, n_out, n_in, s, _p(ws), _p(out),
            _stream(dy2))
