@@ -160,8 +160,8 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   VA_TUNE_WHITEN_SLICE_MIN / VA_TUNE_WHITEN_GRID (va_gae_advantage_return): partial count above
  *   which partials are merged in parallel slices first (default 4,096) and the statistics +
  *   whitening launch's grid cap (default 2,048); only the fp64 merge order changes;
- *   VA_TUNE_WGRAD_REMAINDER (va_weight_grad): 1 (default) = a dimension that is 128 mod 256 gets its
- *     last 128 rows / columns as 128 x 512 / 512 x 128 tiles; 0 = 256 x 256 tiles throughout.
+ *   VA_TUNE_WGRAD_REMAINDER (va_weight_grad): 0 (default) = 256 x 256 tiles throughout; 1 = a
+ *     dimension that is 128 mod 256 gets its last 128 rows / columns as 128 x 512 / 512 x 128 tiles.
  *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
  *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1

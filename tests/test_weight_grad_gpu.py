@@ -36,16 +36,25 @@ def _check(got, want):
 @pytest.mark.parametrize("T,M,N", [(2048, 1152, 896), (4096, 896, 4864), (1024, 200, 136), (96, 264, 512),
                                    (2048, 9728, 896), (1024, 384, 640), (1024, 896, 896)])
 @pytest.mark.parametrize("splits", [0, 1, 3, 8])
-def test_weight_grad_matches_fp32_reference(T, M, N, splits):
-    """splits 0 = automatic (with the 512 x 128 / 128 x 512 remainder tiles when a dimension is 128
-    mod 256: 896, 640, 384); explicit splits run one 256 x 256 launch only when there is no remainder."""
+@pytest.mark.parametrize("remainder", [0, 1])
+def test_weight_grad_matches_fp32_reference(T, M, N, splits, remainder):
+    """splits 0 = automatic; with VA_TUNE_WGRAD_REMAINDER = 1 (both settings run here) a dimension that
+    is 128 mod 256 (896, 640, 384) gets 512 x 128 / 128 x 512 remainder tiles, and explicit splits
+    apply only when there is no remainder."""
+    from verl_amd import _lib as L
+
     g = torch.Generator(device=DEV).manual_seed(T + M + N)
     dy = (torch.randn(T, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
     x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
-    got = _call(dy, x, splits)
+    try:
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, remainder)
+        got = _call(dy, x, splits)
+        again = _call(dy, x, splits)
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, 0)
     assert not torch.isnan(got.float()).any()
     _check(got, _ref(dy, x))
-    assert torch.equal(got, _call(dy, x, splits))  # deterministic
+    assert torch.equal(got, again)  # deterministic
 
 
 def test_weight_grad_strided_operands_and_zero_tokens():
@@ -90,11 +99,11 @@ def test_remainder_tiles_match_full_tiles(T, M, N):
     dy = (torch.randn(T, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
     x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
     want = _ref(dy, x)
+    full = _call(dy, x, 0)
     try:
-        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, 0)
-        full = _call(dy, x, 0)
-    finally:
         L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, 1)
-    rem = _call(dy, x, 0)
+        rem = _call(dy, x, 0)
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, 0)
     _check(full, want)
     _check(rem, want)

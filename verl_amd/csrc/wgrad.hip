@@ -297,9 +297,11 @@ void w_launch(const WPart &p, const uint16_t *dy, int64_t ldy, const uint16_t *x
 
 }  // namespace
 
-// va_set_tuning(VA_TUNE_WGRAD_REMAINDER): 1 (default) = the 128-wide remainder tiles above, 0 = every
-// tile 256 x 256 (A/B runs)
-int g_wgrad_remainder = 1;
+// va_set_tuning(VA_TUNE_WGRAD_REMAINDER): 0 (default) = every tile 256 x 256; 1 = the 128-wide
+// remainder tiles above. Interleaved bench A/B on one MI355X: 182.36 / 182.49K tokens/s with 256 x 256
+// tiles vs 182.08 / 181.96K with the remainder tiles (profiles/r04/bench_wgrad_remainder_ab.txt): the
+// half-empty 256-wide tiles cost less than a second launch per weight gradient
+int g_wgrad_remainder = 0;
 
 extern "C" int64_t va_weight_grad_workspace_bytes(int64_t K, int64_t M, int64_t N, int splits) {
   WPart p[2];
