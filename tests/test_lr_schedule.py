@@ -143,3 +143,36 @@ def test_update_actor_and_critic_rpc_metrics_and_scheduler_steps():
         got.append(m["critic/lr"])
         assert "perf/mfu/critic" in m and m["critic/vf_loss"] == [0.25]
     assert got == pytest.approx([0.0, 0.5, 1.0])
+
+
+# the reference's own known answers (tests/utils/test_flops_counter.py:30-139: config, two batches of
+# sequence lengths, expected TFLOPs at delta_time 1); deepseek_v3 (MLA) is outside this path's families
+_FLOPS_KATS = {
+    "llama": (dict(model_type="llama", vocab_size=32000, hidden_size=4096, intermediate_size=11008,
+                   num_hidden_layers=32, num_attention_heads=32, num_key_value_heads=32),
+              (153555818250240 / 1e12, 575955114393600 / 1e12)),
+    "qwen2": (dict(model_type="qwen2", vocab_size=152064, hidden_size=3584, intermediate_size=18944,
+                   num_hidden_layers=28, num_attention_heads=28, num_key_value_heads=4),
+              (170388331954176 / 1e12, 622070178250752 / 1e12)),
+    "qwen3": (dict(model_type="qwen3", vocab_size=151936, hidden_size=4096, intermediate_size=12288,
+                   num_hidden_layers=36, num_attention_heads=32, num_key_value_heads=8, head_dim=128),
+              (185867930959872 / 1e12, 692924253732864 / 1e12)),
+    "qwen3_moe": (dict(model_type="qwen3_moe", hidden_size=2048, vocab_size=151936, num_hidden_layers=48,
+                       num_key_value_heads=4, num_attention_heads=32, head_dim=128, moe_intermediate_size=768,
+                       num_experts_per_tok=8, num_experts=128),
+                  (85087060230144 / 1e12, 365944098521088 / 1e12)),
+}
+
+
+@pytest.mark.parametrize("family", sorted(_FLOPS_KATS))
+def test_flops_counter_reference_known_answers(family):
+    import math
+    from types import SimpleNamespace
+
+    from verl_amd.utils.flops_counter import FlopsCounter
+
+    cfg, expected = _FLOPS_KATS[family]
+    fc = FlopsCounter(SimpleNamespace(**cfg), device_name="AMD Instinct MI355X")
+    for seqlens, want in zip(([512, 1024, 2048], [4096, 4096, 4096]), expected, strict=True):
+        got, _ = fc.estimate_flops(seqlens, 1)
+        assert math.isclose(got, want), (family, got, want)
