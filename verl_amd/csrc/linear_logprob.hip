@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256, 2) void linear_logprob_tiles_kernel(
 // during the current one, across vocab tiles. Grid: row blocks x vocab splits as ONE dimension,
 // remapped so that each XCD gets a contiguous run of (row block, split) ids, split fastest: the few
 // row blocks an XCD works on at a time keep their hidden panels in its L2 while the W tiles stream
-// (tools/f1core/f1t.hip; at 131,072 x 896 x 151,936: 30.1 ms core-only vs 32.3 without the remap).
+// (round-3 dev kernel tools/f1core/f1t.hip, git show 690aed1:tools/f1core/f1t.hip; at 131,072 x 896 x 151,936: 30.1 ms core-only vs 32.3 without the remap).
 constexpr int TB = 256, TK = 64, T_THREADS = 512;
 constexpr int T_TILE = TB * TK;  // bf16 elements of one operand's K-step image
 

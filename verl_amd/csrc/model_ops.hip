@@ -567,7 +567,7 @@ extern "C" int va_swiglu_bwd(const void *dy, const void *gu, int64_t ldgu, int64
   }
   const int64_t total = T * (F / 8);
   if (g_swiglu_variant != 0 && total < (1LL << 31)) {
-    const int u = g_swiglu_variant > 0 ? g_swiglu_variant : 2;  // 2: best bwd (tools/elemwise_ab.py)
+    const int u = g_swiglu_variant > 0 ? g_swiglu_variant : 2;  // 2: best bwd (tools/elemwise_ab.py at 690aed1)
 #define VA_SWB(U)                                                                                                  \
   hipLaunchKernelGGL(swiglu_bwd_stream_kernel<U>, dim3(static_cast<unsigned>((total + 256 * U - 1) / (256 * U))), \
                      dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const uint16_t *>(dy),             \

@@ -2,7 +2,7 @@
 // with fp32 accumulation (K = packed tokens, M = out_features, N = in_features). Not a §8 row: it
 // replaces the hipBLASLt GEMMs of torch's linear backward for this shape class (K in the 10^5 range,
 // an output of a few hundred 256 x 256 tiles; both operands K-outer), which run at 0.69-0.89 PF/s on
-// the bench's shapes (tools/wgrad256_bench.py, profiles/r03/wgrad256_probe.jsonl).
+// the bench's shapes (tools/wgrad256_bench.py at 690aed1, profiles/r03/wgrad256_probe.jsonl).
 //
 // Workgroup = 256 (m) x 256 (n) output tile x one K slice (split-K), 8 waves as 2 (m) x 4 (n), wave
 // tile 128 x 64 = 4 x 2 v_mfma_f32_32x32x16_bf16 accumulators (1.5 transposed fragment reads per

@@ -164,7 +164,7 @@ def logprob_entropy(logits, labels, temperature: float = 1.0, inplace_backward=F
 def _linear_logprob_splits(n_rows: int) -> int:
     """Vocab ranges per row block. The 256-row kernel (default): ~4,096 workgroups (16 per CU, which
     the XCD remap turns into 32 resident (row block, range) pairs per XCD: 4 hidden panels x 8
-    ranges at 131,072 rows; tools/f1t_bench.py: 4 or 8 ranges 33.9 ms, 16: 34.3); the 128-row
+    ranges at 131,072 rows; tools/f1t_bench.py, removed in round 4 — git show 690aed1:tools/f1t_bench.py: 4 or 8 ranges 33.9 ms, 16: 34.3); the 128-row
     kernel: ~1,024 workgroups."""
     env = os.environ.get("VERL_AMD_LINEAR_LOGPROB_SPLITS")
     if env:
@@ -794,7 +794,7 @@ WGRAD_SWAP_MIN_OUT = 65536  # the lm_head (V = 151,936 outputs)
 
 # the backbone weight gradients through va_weight_grad (csrc/wgrad.hip, 256 x 256 tiles, 4-deep LDS-DMA
 # ring) instead of hipBLASLt: at 151,552 tokens gate|up 2,956 -> 2,699 us, down 1,624 -> 1,437, q|k|v
-# 443 -> 376, o 316 -> 305 (tools/wgrad256_bench.py, profiles/r03/wgrad256_probe.jsonl).
+# 443 -> 376, o 316 -> 305 (tools/wgrad256_bench.py at 690aed1, profiles/r03/wgrad256_probe.jsonl).
 # VERL_AMD_WGRAD=hipblaslt keeps hipBLASLt (A/B runs).
 _OWN_WGRAD = os.environ.get("VERL_AMD_WGRAD", "own") != "hipblaslt"
 

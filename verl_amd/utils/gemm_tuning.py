@@ -2,7 +2,7 @@
 
 hipBLASLt's default heuristic picks poorly for the actor's skinny shapes on gfx950 (H = 896
 outputs, tens of thousands of packed tokens): an exhaustive search over the hipBLASLt and rocBLAS
-solutions finds 1.1-1.4x faster kernels (tools/tunableop_probe.py, profiles/r01/). The search is
+solutions finds 1.1-1.4x faster kernels (tools/tunableop_probe.py at 690aed1, profiles/r01/). The search is
 too slow to run inside a training job, so it runs once offline (tools/tune_gemms.py) over the
 shapes a workload produces and the winners are committed as a table under
 ``verl_amd/tuned/``. At run time PyTorch's TunableOp dispatcher looks every GEMM up in that table
