@@ -75,7 +75,46 @@ def test_rmpad_varlen_path_matches_padded_path():
     # both bf16 autocast; different attention kernels -> bf16-level agreement
     assert torch.allclose(lp_pk[m], lp_pad[m], atol=5e-2, rtol=2e-2), (lp_pk[m] - lp_pad[m]).abs().max()
     assert torch.allclose(ent_pk[m], ent_pad[m], atol=5e-2, rtol=2e-2)
-    assert (lp_pk[~m] == 0).all()
+    # masked positions as the reference's rmpad path fills them (dp_actor.py:131-137, 219-237): the
+    # last real token of a short row scores the rolled packed stream's next token (the next row's
+    # first real token in the micro-batch of 4, wrapping), later positions are pad_input zeros
+    with torch.no_grad():
+        want_lp, want_ent = _ref_rmpad_masked(model, data, 1.0, micro=4)
+    assert torch.allclose(lp_pk, want_lp, atol=5e-2, rtol=2e-2), (lp_pk - want_lp).abs().max()
+    assert torch.allclose(ent_pk, want_ent, atol=5e-2, rtol=2e-2), (ent_pk - want_ent).abs().max()
+    tail = (~m) & (want_lp != 0)
+    assert tail.any() and (lp_pk[tail] != 0).all()
+
+
+def _ref_rmpad_masked(model, data, temperature, micro):
+    """The reference's remove-padding log-probs / entropies at EVERY response position
+    (dp_actor.py:99-237): labels = torch.roll(input_ids_rmpad, -1) within each micro-batch of
+    ``micro`` rows, pad_input zeros at padding; logits from the padded forward (same values at real
+    positions up to attention-kernel rounding), fp32 oracle log-softmax / entropy."""
+    b = data.batch
+    ids, am = b["input_ids"], b["attention_mask"].bool()
+    B, S = ids.shape
+    R = b["responses"].shape[1]
+    logits = model(input_ids=ids, attention_mask=b["attention_mask"], position_ids=b["position_ids"],
+                   use_cache=False).logits.float().div(temperature)
+    lp = torch.zeros(B, R, device=ids.device)
+    ent = torch.zeros(B, R, device=ids.device)
+    first = am.long().argmax(dim=1)
+    for r in range(B):
+        g0 = r // micro * micro
+        g1 = min(g0 + micro, B)
+        for t in range(R):
+            p = S - R - 1 + t
+            if not am[r, p]:
+                continue
+            if am[r, p + 1]:
+                lab = ids[r, p + 1]
+            else:
+                nr = r + 1 if r + 1 < g1 else g0
+                lab = ids[nr, first[nr]]
+            lp[r, t] = ref.logprobs_from_logits(logits[r, p][None], lab[None])[0]
+            ent[r, t] = ref.entropy_from_logits(logits[r, p][None])[0]
+    return lp, ent
 
 
 @pytest.mark.parametrize("agg,mb,cmb", [("token-mean", 4, None), ("seq-mean-token-mean", 4, None),

@@ -281,3 +281,34 @@ def test_rewritten_helpers_keep_the_reference_error_surface():
         d.sample_level_repeat({1: 2})
     r = d.sample_level_repeat(np.array([2, 1]))
     assert len(r) == 3 and r.non_tensor_batch["n"].tolist() == [1, 1, 2]
+
+
+def test_plan_packing_masked_tail_labels_follow_the_rolled_stream():
+    """The last real token of a row whose response is shorter than R keeps its log-prob, labelled as
+    the reference's torch.roll(input_ids_rmpad, -1) labels it (dp_actor.py:131-137): the first real
+    token of the next row of the reference's micro-batch, the first row's for the last row."""
+    from verl_amd.workers.actor.dp_actor import _plan_packing
+
+    P, R = 3, 4
+    S = P + R
+    # rows: prompt lengths 2, 3, 1, 2; response lengths 4 (full), 2, 1, 3
+    am = np.zeros((4, S), dtype=np.int64)
+    for r, (pl, rl) in enumerate([(2, 4), (3, 2), (1, 1), (2, 3)]):
+        am[r, P - pl : P + rl] = 1
+    first = am.argmax(axis=1)
+    for groups, nxt in ((None, {1: 2, 2: 3, 3: 0}), ([0, 2, 4], {1: 0, 2: 3, 3: 2})):
+        pk = _plan_packing(am, R, "cpu", groups=groups)
+        sel_out = pk.sel_out.numpy()
+        lab = pk.label_idx.numpy()
+        for o, li in zip(sel_out, lab):
+            r, t = divmod(int(o), R)
+            p = S - R - 1 + t
+            assert am[r, p] == 1
+            if am[r, p + 1]:
+                assert li == r * S + p + 1
+            else:  # the tail: one per short row
+                assert li == nxt[r] * S + first[nxt[r]], (groups, r, t, li)
+        # every real predictor position is kept, padding ones are not
+        kept = {(int(o) // R, int(o) % R) for o in sel_out}
+        want = {(r, t) for r in range(4) for t in range(R) if am[r, S - R - 1 + t]}
+        assert kept == want

@@ -8,7 +8,8 @@ reference. What changes is how the hot path maps onto the GPU:
   * the backbone runs on packed tokens with PyTorch-ROCm flash varlen attention
     (attention.py) and only the hidden states that predict response tokens go through the
     lm_head (the reference materialises logits for prompt tokens too and slices afterwards,
-    dp_actor.py:219-237); log-probs at masked-out positions are 0 here;
+    dp_actor.py:219-237), with the reference's labels, so the returned log-probs and entropies
+    equal its tensors at every position (masked ones included);
   * temperature, log-softmax, label gather and entropy are ONE fused gfx950 kernel pass over
     the logits (va_logprob_entropy_fwd); its backward writes dlogits in place (the reference's
     inplace_backward) or, with logprob_inplace_backward=False (the bench), into a fresh buffer;
@@ -68,8 +69,9 @@ class _Packing:
     token_idx: torch.Tensor  # [nnz] flat indices of real tokens in [B*S]
     cu_seqlens: torch.Tensor  # [B+1] int32
     max_seqlen: int
-    sel_hidden: torch.Tensor  # [n_sel] rows of the packed hidden states that predict a response token
+    sel_hidden: torch.Tensor  # [n_sel] rows of the packed hidden states whose log-prob is kept
     sel_out: torch.Tensor  # [n_sel] flat index into [B*R]
+    label_idx: torch.Tensor  # [n_sel] flat index into input_ids [B*S]: each selected row's label
     attn_blocks: torch.Tensor = None  # [n, 2] int32 (sequence, first query row) for va_flash_attn_fwd
     attn_kblocks: torch.Tensor = None  # [n, 2] int32 (sequence, first key) for va_flash_attn_bwd
     pad: int = 0  # dummy tokens appended as one extra sequence (pad_multiple)
@@ -91,12 +93,20 @@ class _Packing:
         return ids, pos
 
 
-def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device, pad_multiple: int = 0) -> _Packing:
+def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device, pad_multiple: int = 0, groups=None) -> _Packing:
     """Padding removal of one micro-batch. With ``pad_multiple`` > 0 the packed length is rounded
     up to a multiple of it by one extra dummy sequence (token 0, positions 0..pad-1): the model
     GEMMs then see a few fixed token counts, so a tuned GEMM table (utils/gemm_tuning.py) applies.
     The dummy rows are never selected for the loss, so their gradients are exactly zero and they
-    attend only to themselves: the real tokens' results and every weight gradient are unchanged."""
+    attend only to themselves: the real tokens' results and every weight gradient are unchanged.
+
+    Selected rows and labels are the reference's (dp_actor.py:131-137, 219-237): position
+    p = S - R - 1 + t gets log p(input_ids[p + 1]) when p is a real token, and 0 (pad_input) when it
+    is padding. For the last real token of a row whose response is shorter than R, the label is the
+    reference's rolled packed stream (torch.roll(input_ids_rmpad, -1)): the first real token of the
+    next row of the reference's micro-batch, or of its first row for its last row. ``groups``: the
+    row offsets of the reference's micro-batches inside this one ([0, B] when they coincide), e.g.
+    the 8-row loss micro-batches of a 128-row update pass."""
     B, S = attn_mask_cpu.shape
     flat = attn_mask_cpu.reshape(-1).astype(bool)
     token_idx = np.flatnonzero(flat)
@@ -113,9 +123,20 @@ def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device, pad_multiple: int =
     p = (S - R - 1) + t
     pos = (np.arange(B)[:, None] * S + p[None, :]).reshape(-1)
     nxt = pos + 1
-    valid = flat[pos] & flat[nxt]
-    sel_out = np.flatnonzero(valid)
-    sel_hidden = packed_of[pos[valid]]
+    keep = flat[pos]  # real predictor: its log-prob is kept (0 where it is padding)
+    sel_out = np.flatnonzero(keep)
+    sel_hidden = packed_of[pos[keep]]
+    label_idx = nxt[keep]
+    tail = ~flat[nxt[keep]]  # last real token of a short row: label from the rolled packed stream
+    if tail.any():
+        first_real = np.argmax(attn_mask_cpu.astype(bool), axis=1)  # left-padded prompts
+        bounds = np.asarray(groups if groups is not None else [0, B], dtype=np.int64)
+        row = sel_out[tail] // R
+        g = np.searchsorted(bounds, row, side="right") - 1
+        nrow = row + 1
+        wrap = nrow >= bounds[g + 1]
+        nrow[wrap] = bounds[g[wrap]]
+        label_idx[tail] = nrow * S + first_real[nrow]
 
     def dev(a, dt):
         from ... import kernels as K
@@ -128,6 +149,7 @@ def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device, pad_multiple: int =
         max_seqlen=int(seqlens.max()) if B else 0,
         sel_hidden=dev(sel_hidden, np.int64),
         sel_out=dev(sel_out, np.int64),
+        label_idx=dev(label_idx, np.int64),
         attn_blocks=dev(attention.flash_block_table(cu), np.int32),
         attn_kblocks=dev(attention.flash_key_block_table(cu), np.int32),
         pad=int(pad),
@@ -168,17 +190,19 @@ def _multi_modal(mb: DataProto):
     return None if v is None else list(v)
 
 
-def merge_dynamic_passes(config, mini: DataProto, micro_batches: list, idx_lists: list, am, enabled: bool = True):
+def merge_dynamic_passes(config, mini: DataProto, micro_batches: list, idx_lists: list, am, enabled: bool = True,
+                         host_offsets: bool = False):
     """use_dynamic_bsz: consecutive token-budget micro-batches (in the reference's order,
     seqlen_balancing.rearrange_micro_batches) merged into update passes of at most
     ``config.compute_max_token_len_per_gpu`` tokens, for the actor and the critic. Returns (pass
     batches, their row index lists, per pass None or (int32 row offsets of its micro-batches on the
     device, device fp32 rows_s / ppo_mini_batch_size)). Without the key or with ``enabled`` False:
-    the reference's micro-batches, one per pass."""
+    the reference's micro-batches, one per pass. ``host_offsets``: also return, per pass, the host
+    list of its micro-batches' row offsets (None for a single micro-batch)."""
     budget = config.get("compute_max_token_len_per_gpu", None)
     none = [None] * len(micro_batches)
     if not budget or not enabled or len(micro_batches) < 2:
-        return micro_batches, idx_lists, none
+        return (micro_batches, idx_lists, none, none) if host_offsets else (micro_batches, idx_lists, none)
     if am is None:  # padded path: no host copy yet (rearrange_micro_batches has synced already)
         am = mini.batch["attention_mask"].cpu().numpy()
     tokens = [int(am[np.asarray(ix, dtype=np.int64)].sum()) for ix in idx_lists]
@@ -192,20 +216,23 @@ def merge_dynamic_passes(config, mini: DataProto, micro_batches: list, idx_lists
     groups.append(cur)
     dev = mini.batch["input_ids"].device
     mini_rows = float(config.ppo_mini_batch_size)
-    out_mb, out_idx, out_seg = [], [], []
+    out_mb, out_idx, out_seg, out_host = [], [], [], []
     for g in groups:
         if len(g) == 1:
             out_mb.append(micro_batches[g[0]])
             out_idx.append(idx_lists[g[0]])
             out_seg.append(None)
+            out_host.append(None)
             continue
         merged = [r for j in g for r in idx_lists[j]]
         rows = [len(idx_lists[j]) for j in g]
+        offs = np.concatenate([[0], np.cumsum(rows)])
         out_mb.append(mini.select_idxs(np.asarray(merged, dtype=np.int64)))
         out_idx.append(merged)
-        out_seg.append((K.seg_offsets(np.concatenate([[0], np.cumsum(rows)]), dev),
+        out_seg.append((K.seg_offsets(offs, dev, len(merged)),
                         K.h2d(np.asarray(rows, dtype=np.float32) / mini_rows, np.float32, dev)))
-    return out_mb, out_idx, out_seg
+        out_host.append(offs.tolist())
+    return (out_mb, out_idx, out_seg, out_host) if host_offsets else (out_mb, out_idx, out_seg)
 
 
 class DataParallelPPOActor(BasePPOActor):
@@ -321,7 +348,7 @@ class DataParallelPPOActor(BasePPOActor):
                 else:
                     hidden = hf_packed_hidden(self._backbone, ids, pos, packing, multi_modal_inputs)
                 h_sel = hidden.index_select(0, packing.sel_hidden)
-                labels = responses.reshape(-1).index_select(0, packing.sel_out)
+                labels = input_ids.reshape(-1).index_select(0, packing.label_idx)
                 if self._use_fused_lm_head():
                     w = self._lm_head.weight
                     lp_sel, ent_sel = K.linear_logprob_entropy(
@@ -386,9 +413,11 @@ class DataParallelPPOActor(BasePPOActor):
         return am
 
     def _plans(self, data: DataProto, sizes: list[int] = None, idx_lists: list[list[int]] = None,
-               am: np.ndarray = None) -> list:
+               am: np.ndarray = None, group_rows: int = 0, groups: list = None) -> list:
         """Packing plans of consecutive micro-batches of ``sizes`` rows, or of the dynamic
-        micro-batches' row index lists, from one host copy of the attention mask."""
+        micro-batches' row index lists, from one host copy of the attention mask. The reference's
+        micro-batches inside each: runs of ``group_rows`` rows, or per plan the row offsets in
+        ``groups`` (None: the micro-batch itself)."""
         n_mb = len(sizes) if idx_lists is None else len(idx_lists)
         if not self.use_remove_padding:
             return [None] * n_mb
@@ -396,12 +425,16 @@ class DataParallelPPOActor(BasePPOActor):
             am = data.batch["attention_mask"].cpu().numpy()
         R = data.batch["responses"].size(-1)
         dev = data.batch["input_ids"].device
+        if groups is None:
+            groups = [None] * n_mb
         if idx_lists is not None:
-            return [_plan_packing(am[np.asarray(ix, dtype=np.int64)], R, dev, self.pack_pad_multiple)
-                    for ix in idx_lists]
+            return [_plan_packing(am[np.asarray(ix, dtype=np.int64)], R, dev, self.pack_pad_multiple, g)
+                    for ix, g in zip(idx_lists, groups, strict=True)]
         plans, s = [], 0
-        for n in sizes:
-            plans.append(_plan_packing(am[s : s + n], R, dev, self.pack_pad_multiple))
+        for n, g in zip(sizes, groups, strict=True):
+            if g is None and group_rows and n > group_rows:
+                g = list(range(0, n, group_rows)) + [n]
+            plans.append(_plan_packing(am[s : s + n], R, dev, self.pack_pad_multiple, g))
             s += n
         return plans
 
@@ -489,13 +522,13 @@ class DataParallelPPOActor(BasePPOActor):
                     max_token_len = cfg.ppo_max_token_len_per_gpu * self.ulysses_sequence_parallel_size
                     micro_batches, idx_lists = prepare_dynamic_batch(mini, max_token_len=max_token_len)
                     # registered loss variants draw their token selection per micro-batch: never merged
-                    micro_batches, idx_lists, seg_offs = merge_dynamic_passes(cfg, mini, micro_batches, idx_lists, am,
-                                                                              loss_mode == "vanilla")
-                    plans = self._plans(mini, idx_lists=idx_lists, am=am)
+                    micro_batches, idx_lists, seg_offs, seg_rows_h = merge_dynamic_passes(
+                        cfg, mini, micro_batches, idx_lists, am, loss_mode == "vanilla", host_offsets=True)
+                    plans = self._plans(mini, idx_lists=idx_lists, am=am, groups=seg_rows_h)
                 else:
                     seg_mb = int(cfg.ppo_micro_batch_size_per_gpu)
                     micro_batches = mini.split(self._pass_rows(loss_mode))
-                    plans = self._plans(mini, [len(m) for m in micro_batches], am=am)
+                    plans = self._plans(mini, [len(m) for m in micro_batches], am=am, group_rows=seg_mb)
                     seg_offs = [None] * len(micro_batches)
                 self._zero_grad()
                 for i, (mb, plan, seg_off) in enumerate(zip(micro_batches, plans, seg_offs, strict=True)):
