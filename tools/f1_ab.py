@@ -20,12 +20,16 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--rows", type=int, default=131072)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--tune", action="append", default=[], help="KEY=VALUE va_set_tuning before timing")
     ap.add_argument("--unfused", action="store_true",
                     help="also time the unfused path (hipBLASLt lm_head GEMM + logprob_entropy_fwd), e.g. under rocprofv3")
     args = ap.parse_args()
     from verl_amd import _lib as L
     from verl_amd import kernels as K
 
+    for kv in args.tune:
+        key, val = (int(x) for x in kv.split("="))
+        L.call("va_set_tuning", key, val)
     dev = torch.device("cuda", 0)
     H, V, N = 896, 151936, args.rows
     g = torch.Generator(device=dev).manual_seed(1)
