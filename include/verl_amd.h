@@ -162,8 +162,6 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   whitening launch's grid cap (default 2,048); only the fp64 merge order changes;
  *   VA_TUNE_WGRAD_REMAINDER (va_weight_grad): 0 (default) = 256 x 256 tiles throughout; 1 = a
  *     dimension that is 128 mod 256 gets its last 128 rows / columns as 128 x 512 / 512 x 128 tiles.
- *   VA_TUNE_F1_RING (va_linear_logprob_fwd, 256 tiles): 0 (default) = two 64-deep LDS buffers; 4 / 5 = a
- *     4- / 5-deep ring of 32-deep steps (same tiles and results);
  *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
  *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
@@ -184,7 +182,6 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_WHITEN_GRID 16
 #define VA_TUNE_LINEAR_LOGPROB_TILE 17
 #define VA_TUNE_WGRAD_REMAINDER 18
-#define VA_TUNE_F1_RING 19
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

@@ -415,144 +415,14 @@ __device__ __forceinline__ void t256_block(int splits, int tiles_per_split, int6
   vt_end = vt_begin + tiles_per_split < n_vt ? vt_begin + tiles_per_split : n_vt;
 }
 
-// ---- deep-ring variant of the forward sweep (VA_TUNE_F1_RING = 4 or 5; 0 = the sweep above) ----
-// The two-buffer sweep waits for each 64-deep K-step's LDS-DMA at the end of the step before (one
-// step of prefetch): its waves spend ~35 % of their cycles waiting (profiles/r03/pmc_f1_sq.json). Here
-// K moves in 32-deep steps through an NST-deep ring of (weight, hidden) images (NST x 32 KiB), with
-// NST - 1 steps in flight: at the top of step st a counted vmcnt retires this wave's DMA for step st
-// while the later ones stay in flight, one raw s_barrier publishes every wave's pieces and ends every
-// wave's reads of step st - 1, whose buffer the DMA for step st + NST - 1 then refills. The fragment
-// reads are inline-asm ds_read_b128 retired by counted lgkmcnt waits (the compiler would otherwise
-// drain every LDS-DMA in flight before an LDS read). Image row = 32 k (64 B, 4 chunks of 16 B), chunk
-// c of row r at c ^ f((r >> 2) & 3) with f = (0, 2, 3, 1): conflict-free for the 4 x 16-lane groups
-// of ds_read_b128 (MI355X_MICROARCH.md LDS table). Same tiles, same epilogue, same results.
-constexpr int RK = 32;
-constexpr int R_IMG = TB * RK;  // bf16 elements of one operand's 32-deep step image (16 KiB)
-
-__device__ __forceinline__ int r_swz(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
-__device__ __forceinline__ int r_off(int row, int c) { return row * RK + ((c ^ r_swz(row)) << 3); }
-
-// one operand's 256 x 32 step image: 16 pieces of 16 rows (1 KiB), 2 per wave; lane l lands at row
-// 16 g + l / 4, physical chunk l % 4, and fetches the logical chunk the swizzle puts there
-__device__ __forceinline__ void r_stage(const uint16_t *__restrict__ src, int64_t row0, int64_t nrows, int64_t ld,
-                                        int k0, uint16_t *img, int wave, int lane) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int g = wave * 2 + i;
-    const int row = g * 16 + (lane >> 2);
-    const int c = (lane & 3) ^ r_swz(row);
-    int64_t gr = row0 + row;
-    if (gr >= nrows) gr = nrows - 1;
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + gr * ld + k0 + c * 8), img + g * 16 * RK,
-                                     16, 0, 0);
-  }
-}
-
-__device__ __forceinline__ bf16x8 r_read(const uint16_t *p) {
-  bf16x8 r;
-  const uint32_t a =
-      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint16_t *)p));
-  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
-  return r;
-}
-
-template <int N>
-__device__ __forceinline__ void r_vm_wait() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else static_assert(N == 0, "unsupported vmcnt");
-}
-
-template <int NST, typename Tile>
-__device__ __forceinline__ void t256_ring_sweep(const uint16_t *__restrict__ hid, int64_t ldh,
-                                                const uint16_t *__restrict__ w, int64_t ldw, int64_t N, int K, int64_t V,
-                                                int64_t row0, int64_t vt_begin, int64_t vt_end, uint16_t *lds, int wave,
-                                                int lane, Tile &&tile) {
-  const int wr = wave >> 2, wc = wave & 3;
-  const int nk = K / RK;
-  const int64_t nsteps = vt_begin < vt_end ? (vt_end - vt_begin) * nk : 0;
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto issue = [&](int64_t st) {  // 4 LDS-DMA instructions per wave
-    uint16_t *img = lds + (st % NST) * 2 * R_IMG;
-    const int k0 = static_cast<int>(st % nk) * RK;
-    r_stage(w, (vt_begin + st / nk) * TB, V, ldw, k0, img, wave, lane);
-    r_stage(hid, row0, N, ldh, k0, img + R_IMG, wave, lane);
-  };
-  for (int b = 0; b < NST - 1; ++b)
-    if (b < nsteps) issue(b);
-  for (int64_t st = 0; st < nsteps; ++st) {
-    const int64_t ahead = nsteps - 1 - st < NST - 2 ? nsteps - 1 - st : NST - 2;  // issued after st
-    if (ahead >= 3) r_vm_wait<12>();
-    else if (ahead == 2) r_vm_wait<8>();
-    else if (ahead == 1) r_vm_wait<4>();
-    else r_vm_wait<0>();
-    asm volatile("s_barrier" ::: "memory");
-    if (st + NST - 1 < nsteps) issue(st + NST - 1);
-    const uint16_t *la = lds + (st % NST) * 2 * R_IMG;
-    const uint16_t *lb = la + R_IMG;
-    const int c = lane >> 4;
-    bf16x8 fb0 = r_read(lb + r_off(wc * 64 + 0 * 16 + (lane & 15), c));
-    bf16x8 fb1 = r_read(lb + r_off(wc * 64 + 1 * 16 + (lane & 15), c));
-    bf16x8 fb2 = r_read(lb + r_off(wc * 64 + 2 * 16 + (lane & 15), c));
-    bf16x8 fb3 = r_read(lb + r_off(wc * 64 + 3 * 16 + (lane & 15), c));
-    bf16x8 fa0 = r_read(la + r_off(wr * 128 + 0 * 16 + (lane & 15), c));
-    bf16x8 fa1 = r_read(la + r_off(wr * 128 + 1 * 16 + (lane & 15), c));
-    bf16x8 fa2 = r_read(la + r_off(wr * 128 + 2 * 16 + (lane & 15), c));
-    bf16x8 fa3 = r_read(la + r_off(wr * 128 + 3 * 16 + (lane & 15), c));
-    bf16x8 fa4 = r_read(la + r_off(wr * 128 + 4 * 16 + (lane & 15), c));
-    bf16x8 fa5 = r_read(la + r_off(wr * 128 + 5 * 16 + (lane & 15), c));
-    bf16x8 fa6 = r_read(la + r_off(wr * 128 + 6 * 16 + (lane & 15), c));
-    bf16x8 fa7 = r_read(la + r_off(wr * 128 + 7 * 16 + (lane & 15), c));
-    // each counted wait releases the fragments it passes through; later reads stay in flight
-    asm volatile("s_waitcnt lgkmcnt(7)" : "+v"(fb0), "+v"(fb1), "+v"(fb2), "+v"(fb3), "+v"(fa0));
-#define R_ROW(I, FA)                                                                          \
-  acc[I][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA, fb0, acc[I][0], 0, 0, 0);          \
-  acc[I][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA, fb1, acc[I][1], 0, 0, 0);          \
-  acc[I][2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA, fb2, acc[I][2], 0, 0, 0);          \
-  acc[I][3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA, fb3, acc[I][3], 0, 0, 0);
-    R_ROW(0, fa0)
-    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(fa1));
-    R_ROW(1, fa1)
-    asm volatile("s_waitcnt lgkmcnt(5)" : "+v"(fa2));
-    R_ROW(2, fa2)
-    asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(fa3));
-    R_ROW(3, fa3)
-    asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(fa4));
-    R_ROW(4, fa4)
-    asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(fa5));
-    R_ROW(5, fa5)
-    asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(fa6));
-    R_ROW(6, fa6)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa7));
-    R_ROW(7, fa7)
-#undef R_ROW
-    if (static_cast<int>(st % nk) == nk - 1) {
-      tile(acc, vt_begin + st / nk);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  r_vm_wait<0>();
-  asm volatile("s_barrier" ::: "memory");
-}
-
-template <bool SCALE, bool ROUND, bool REMAP, int NST = 0>
+template <bool SCALE, bool ROUND, bool REMAP>
 __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
     const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
     const int64_t *__restrict__ labels, int64_t N, int K, int64_t V, int splits, int tiles_per_split,
     float temperature, float *__restrict__ part, float *__restrict__ label_logit) {
   // ONE LDS array (a second __shared__ object can cost a vmcnt(0) per K-step): 2 staging buffers of
-  // (weight, hidden) images (or the NST-deep ring); reused for the final merge of the two vocab wave-rows
-  constexpr int LDS_ELEMS = NST > 0 ? NST * 2 * R_IMG : 2 * 2 * T_TILE;
-  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
+  // (weight, hidden) images; reused for the final merge of the two vocab wave-rows
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
   int64_t row0, sp, vt_begin, vt_end;
@@ -569,7 +439,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
     m[j] = -INFINITY, s[j] = 0.f, t[j] = 0.f, ll[j] = -INFINITY;
   }
 
-  auto tile = [&](f32x4(&acc)[8][4], int64_t vt) {
+  t256_sweep(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
     // acc[i][j][e] = logit of vocab v0 + i * 16 + e for token j of this lane
     const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;  // V < 2^31
     if (vt * TB + TB > V) {  // uniform: only the last vocab tile has rows past V
@@ -584,9 +454,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
     } else {
       t_tile_epilogue<SCALE, ROUND, false>(acc, v0, lab, m, s, t, ll, temperature);
     }
-  };
-  if constexpr (NST > 0) t256_ring_sweep<NST>(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, tile);
-  else t256_sweep(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, tile);
+  });
 
   // merge the 4 lane groups (lanes l, l ^ 16, l ^ 32, l ^ 48 hold the same tokens), then the two
   // vocab wave-rows through LDS (free now: every DMA was waited for), in fixed order
@@ -744,35 +612,16 @@ using namespace va;
 // (the 256 x 256 LDS-DMA kernel above)
 int g_linear_logprob_tile = 256;
 
-// va_set_tuning(VA_TUNE_F1_RING): 0 (default) = the two-buffer 64-deep sweep; 4 / 5 = the deep-ring
-// variant (32-deep steps, 4 / 5 stages)
-int g_f1_ring = 0;
-
-template <bool SC, bool RD, int NST>
-static void launch_t256_n(bool remap, dim3 grid, hipStream_t s, const uint16_t *h16, int64_t ldh, const uint16_t *w16,
-                          int64_t ldw, const int64_t *labels, int64_t N, int64_t H, int64_t V, int used, int per,
-                          float temperature, float *part, float *label_logit) {
-  if (remap)
-    hipLaunchKernelGGL((linear_logprob_t256_kernel<SC, RD, true, NST>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16,
-                       ldw, labels, N, static_cast<int>(H), V, used, per, temperature, part, label_logit);
-  else
-    hipLaunchKernelGGL((linear_logprob_t256_kernel<SC, RD, false, NST>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16,
-                       ldw, labels, N, static_cast<int>(H), V, used, per, temperature, part, label_logit);
-}
-
 template <bool SC, bool RD>
 static void launch_t256(bool remap, dim3 grid, hipStream_t s, const uint16_t *h16, int64_t ldh, const uint16_t *w16,
                         int64_t ldw, const int64_t *labels, int64_t N, int64_t H, int64_t V, int used, int per,
                         float temperature, float *part, float *label_logit) {
-  if (g_f1_ring == 4)
-    launch_t256_n<SC, RD, 4>(remap, grid, s, h16, ldh, w16, ldw, labels, N, H, V, used, per, temperature, part,
-                             label_logit);
-  else if (g_f1_ring == 5)
-    launch_t256_n<SC, RD, 5>(remap, grid, s, h16, ldh, w16, ldw, labels, N, H, V, used, per, temperature, part,
-                             label_logit);
+  if (remap)
+    hipLaunchKernelGGL((linear_logprob_t256_kernel<SC, RD, true>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16, ldw,
+                       labels, N, static_cast<int>(H), V, used, per, temperature, part, label_logit);
   else
-    launch_t256_n<SC, RD, 0>(remap, grid, s, h16, ldh, w16, ldw, labels, N, H, V, used, per, temperature, part,
-                             label_logit);
+    hipLaunchKernelGGL((linear_logprob_t256_kernel<SC, RD, false>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16, ldw,
+                       labels, N, static_cast<int>(H), V, used, per, temperature, part, label_logit);
 }
 
 extern "C" int64_t va_linear_logprob_workspace_bytes(int64_t N, int splits) {

@@ -714,7 +714,6 @@ extern int g_gae_nt;              // advantage.hip
 extern int g_loss_vec;            // loss.hip
 extern int g_whiten_slice_min;    // advantage.hip
 extern int g_linear_logprob_tile;  // linear_logprob.hip
-extern int g_f1_ring;              // linear_logprob.hip
 extern int g_wgrad_remainder;      // wgrad.hip
 extern int g_whiten_grid;         // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
@@ -740,13 +739,6 @@ extern "C" int va_set_tuning(int key, int value) {
     case VA_TUNE_GAE_NT: g_gae_nt = value & 7; return VA_OK;
     case VA_TUNE_LOSS_VEC: g_loss_vec = value; return VA_OK;
     case VA_TUNE_WGRAD_REMAINDER: g_wgrad_remainder = value; return VA_OK;
-    case VA_TUNE_F1_RING:
-      if (value != 0 && value != 4 && value != 5) {
-        va::set_error("VA_TUNE_F1_RING must be 0, 4 or 5 (got %d)", value);
-        return VA_E_ARG;
-      }
-      g_f1_ring = value;
-      return VA_OK;
     case VA_TUNE_LINEAR_LOGPROB_TILE:
       if (value != 128 && value != 256) {
         va::set_error("VA_TUNE_LINEAR_LOGPROB_TILE must be 128 or 256 (got %d)", value);
