@@ -53,6 +53,8 @@ def all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None) -> torch.Tenso
     if world(group) == 1:
         return t
     avg = op == dist.ReduceOp.AVG
+    if avg and not t.is_floating_point():
+        raise TypeError(f"all_reduce AVG needs a floating-point tensor, got {t.dtype}")
     if device_backend(group):
         dist.all_reduce(t, op=op, group=group)
         return t
