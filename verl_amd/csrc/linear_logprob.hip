@@ -266,23 +266,6 @@ __device__ __forceinline__ void t_stage(const uint16_t *__restrict__ src, int64_
   }
 }
 
-#if defined(VA_F1_SCHED)
-// one 16-byte MFMA fragment from LDS, outside the compiler's wait tracking (see t256_sweep)
-__device__ __forceinline__ bf16x8 t_frag(const uint16_t *p) {
-  bf16x8 r;
-  const uint32_t a =
-      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const uint16_t *)p));
-  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a) : "memory");
-  return r;
-}
-// all but N of this wave's LDS reads retired (vmcnt / expcnt fields at their maxima: not waited)
-template <int N>
-__device__ __forceinline__ void t_lgkm_wait() {
-  __builtin_amdgcn_s_waitcnt(0xC07F | (N << 8));
-  __builtin_amdgcn_sched_barrier(0);
-}
-#endif
-
 // the logit as the unfused path holds it: bf16(acc) (ROUND), then bf16(x / T) (SCALE: div_ in bf16)
 template <bool SCALE, bool ROUND>
 __device__ __forceinline__ float logit_of(float a, float temperature) {
@@ -387,45 +370,6 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
       t_stage(w, (vt_begin + (st + 1) / nk) * TB, V, ldw, k1, na, wave, lane);
       t_stage(hid, row0, N, ldh, k1, na + T_TILE, wave, lane);
     }
-#if defined(VA_F1_SCHED)
-    {
-      // fragment reads issued one 8-MFMA group ahead of their consumers (the second K-half's B
-      // fragments and first A pair under the first half's last group), as inline asm so that the
-      // waits are the counted ones below (LDS returns in order), not the compiler's lgkmcnt(0)
-      const int r16 = lane & 15, cq = lane >> 4;
-      auto rdA = [&](int q, int i) { return t_frag(la + t_img_off(wr * 128 + i * 16 + r16, q * 4 + cq)); };
-      auto rdB = [&](int q, int j) { return t_frag(lb + t_img_off(wc * 64 + j * 16 + r16, q * 4 + cq)); };
-      bf16x8 fb[2][4], fa[2][8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[0][j] = rdB(0, j);
-      fa[0][0] = rdA(0, 0);
-      fa[0][1] = rdA(0, 1);
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          if (g < 3) {
-            fa[q][2 * g + 2] = rdA(q, 2 * g + 2);
-            fa[q][2 * g + 3] = rdA(q, 2 * g + 3);
-            t_lgkm_wait<2>();
-          } else if (q == 0) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) fb[1][j] = rdB(1, j);
-            fa[1][0] = rdA(1, 0);
-            fa[1][1] = rdA(1, 1);
-            t_lgkm_wait<6>();
-          } else {
-            t_lgkm_wait<0>();
-          }
-#pragma unroll
-          for (int i = 2 * g; i < 2 * g + 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q][i], fb[q][j], acc[i][j], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-#else
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int c = q * 4 + (lane >> 4);
@@ -441,7 +385,6 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-#endif
     if (kt == nk - 1) {
       tile(acc, vt);
 #pragma unroll
