@@ -1,0 +1,50 @@
+"""Per-kernel MFMA busy share, clock and wait share from one rocprofv3 --pmc run (csv output) with
+SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
+SQ_ACTIVE_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE. For every kernel-name substring given, the
+dispatches whose name holds it are averaged (MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES over 1,024 SIMDs x
+GRBM_GUI_ACTIVE / 8 XCDs; clock = GRBM_GUI_ACTIVE / 8 / traced duration).
+
+  python tools/sq_summary.py <rocprof dir> <substring> [<substring> ...]
+"""
+
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def main():
+    d, names = sys.argv[1], sys.argv[2:]
+    cc = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)[0]
+    kt = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)[0]
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    kname = {}
+    for r in csv.DictReader(open(cc)):
+        per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+        kname[r["Dispatch_Id"]] = r["Kernel_Name"]
+    dur = {}
+    for r in csv.DictReader(open(kt)):
+        dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    for sub in names:
+        ids = [i for i in per if sub in kname[i] and dur.get(i)]
+        if not ids:
+            print(json.dumps({"kernel": sub, "dispatches": 0}))
+            continue
+        busy = clock = wait = us = 0.0
+        for i in ids:
+            v = per[i]
+            g = v["GRBM_GUI_ACTIVE"] / 8
+            busy += v["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * g)
+            clock += g / dur[i]
+            wait += v["SQ_WAIT_ANY"] / (v["SQ_WAVE_CYCLES"] or 1)
+            us += dur[i] / 1e3
+        n = len(ids)
+        print(json.dumps({"kernel": sub, "dispatches": n, "avg_us": round(us / n, 1),
+                          "mfma_busy": round(busy / n, 3), "clock_ghz": round(clock / n, 3),
+                          "busy_x_clock": round(busy * clock / n / n, 3), "wait_share": round(wait / n, 3),
+                          "name": kname[ids[0]][:90]}))
+
+
+if __name__ == "__main__":
+    main()
