@@ -163,7 +163,10 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   VA_TUNE_WGRAD_REMAINDER (va_weight_grad): 0 (default) = 256 x 256 tiles throughout; 1 = a
  *     dimension that is 128 mod 256 gets its last 128 rows / columns as 128 x 512 / 512 x 128 tiles.
  *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
- *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order). */
+*   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order);
+ *   VA_TUNE_FLASH_DMA (va_flash_attn_fwd / _bwd): bit 1 = forward K / V blocks staged by LDS-DMA
+ *   (64-key blocks), bit 2 = the same for the dQ backward, bit 4 = the dK / dV backward's Q / dO
+ *   tiles; 0 = register-staged (bitwise identical results). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3
@@ -182,6 +185,7 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_WHITEN_GRID 16
 #define VA_TUNE_LINEAR_LOGPROB_TILE 17
 #define VA_TUNE_WGRAD_REMAINDER 18
+#define VA_TUNE_FLASH_DMA 19
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

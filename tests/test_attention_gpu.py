@@ -93,6 +93,34 @@ def test_flash_forward_key_block_128_equals_64(lens):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("lens", [[1, 17, 128, 129, 300], [1184, 1100, 1280, 700], [64] * 9, [65, 191, 257], [3, 5]])
+def test_flash_forward_dma_staging_equals_register_staging(lens):
+    """VA_TUNE_FLASH_DMA bit 1 (K / V blocks by LDS-DMA, rows past a sequence end clamped to its
+    last row instead of zeroed) equals the register-staged forward bitwise: clamped keys are masked
+    to -inf and their P is 0, so the same products and sums are formed."""
+    from verl_amd import _lib as L
+    from verl_amd import kernels as K
+    from verl_amd.workers.actor import attention as A
+
+    q, k, v, cu = _inputs(lens, seed=11 + len(lens))
+    cu_d = torch.tensor(cu, dtype=torch.int32, device=DEV)
+    blocks = torch.tensor(A.flash_block_table(cu), device=DEV)
+    T, mx = q.shape[0], int(max(lens))
+    outs = []
+    try:
+        for dma in (1, 0):
+            L.call("va_set_tuning", L.VA_TUNE_FLASH_DMA, dma)
+            o = torch.empty_like(q)
+            lse = torch.zeros(len(lens), 14, mx, device=DEV)
+            L.call("va_flash_attn_fwd", K._p(q), K._p(k), K._p(v), K._p(cu_d), K._p(blocks), blocks.shape[0], T, 14,
+                   2, 64, mx, 64 ** -0.5, K._p(o), K._p(lse), K._stream(q))
+            outs.append((o, lse))
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_FLASH_DMA, 0)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 def test_flash_forward_matches_torch_flash_and_lse_convention():
     from verl_amd.workers.actor import attention as A
 
@@ -187,6 +215,44 @@ def test_flash_backward_query_tile_64_equals_32(grouped, lens):
         L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, -1)
         L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 128)
         L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, 128)
+    for other in grads[1:]:
+        for a, b in zip(grads[0], other):
+            assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("kblk,qt,grouped", [(64, 64, 1), (128, 128, 1), (128, 128, 0), (128, 32, 0)])
+@pytest.mark.parametrize("lens", [[300, 129, 1000], [1, 33, 64, 65, 128, 129, 200], [1184, 1280], [3, 5]])
+def test_flash_backward_dma_staging_equals_register_staging(kblk, qt, grouped, lens):
+    """VA_TUNE_FLASH_DMA bits 2 / 4 (the dQ kernel's K / V blocks, the dK / dV kernel's Q / dO tiles by
+    LDS-DMA, rows past a sequence end clamped: their P and dS are 0) and bit 1 (the forward) give
+    the register-staged gradients bitwise, grouped and per-query-head dK / dV."""
+    from verl_amd import _lib as L
+    from verl_amd.workers.actor import attention as A
+
+    q, k, v, cu = _inputs(lens, seed=21 + len(lens))
+    cu_d = torch.tensor(cu, dtype=torch.int32, device=DEV)
+    mx = int(max(lens))
+    g = torch.randn_like(q)
+    blocks = torch.tensor(A.flash_block_table(cu), device=DEV)
+    kblocks = torch.tensor(A.flash_key_block_table(cu), device=DEV)
+    grads = []
+    old = A.FLASH_BWD
+    A.FLASH_BWD = "gfx950"
+    L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, kblk)
+    L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, qt)
+    L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, grouped)
+    try:
+        for dma in (7, 4, 2, 0):
+            L.call("va_set_tuning", L.VA_TUNE_FLASH_DMA, dma)
+            qb, kb, vb = (t.clone().requires_grad_(True) for t in (q, k, v))
+            A.flash_attention(qb, kb, vb, cu_d, mx, blocks, kblocks=kblocks).backward(g)
+            grads.append((qb.grad, kb.grad, vb.grad))
+    finally:
+        A.FLASH_BWD = old
+        L.call("va_set_tuning", L.VA_TUNE_FLASH_DMA, 0)
+        L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, 128)
+        L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 128)
+        L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, -1)
     for other in grads[1:]:
         for a, b in zip(grads[0], other):
             assert torch.equal(a, b)

@@ -3,6 +3,7 @@
 (no grad) and forward + backward, HIP-event medians over rounds. One JSON line; run once per build.
 
   VERL_AMD_LIB=scratch/ab/lib_x.so python tools/attn_ab.py --tag x
+  python tools/attn_ab.py --tag dma --tune 19=1
 """
 import argparse
 import json
@@ -37,7 +38,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", default="")
     ap.add_argument("--seqs", type=int, default=128)
+    ap.add_argument("--tune", action="append", default=[], help="KEY=VALUE va_set_tuning before timing")
     args = ap.parse_args()
+    for kv in args.tune:
+        key, val = (int(x) for x in kv.split("="))
+        L.call("va_set_tuning", key, val)
     rng = np.random.default_rng(0)
     lens = (rng.integers(64, 257, args.seqs) + 1024).tolist()
     cu = np.zeros(args.seqs + 1, dtype=np.int64)

@@ -1,6 +1,6 @@
 """Per-kernel MFMA busy share, clock and wait share from one rocprofv3 --pmc run (csv output) with
 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
-SQ_ACTIVE_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE. For every kernel-name substring given, the
+SQ_ACTIVE_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE (or SQ_ACTIVE_INST_VALU: VALU share of wave time). For every kernel-name substring given, the
 dispatches whose name holds it are averaged (MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES over 1,024 SIMDs x
 GRBM_GUI_ACTIVE / 8 XCDs; clock = GRBM_GUI_ACTIVE / 8 / traced duration).
 
@@ -31,18 +31,20 @@ def main():
         if not ids:
             print(json.dumps({"kernel": sub, "dispatches": 0}))
             continue
-        busy = clock = wait = us = 0.0
+        busy = clock = wait = us = valu = 0.0
         for i in ids:
             v = per[i]
             g = v["GRBM_GUI_ACTIVE"] / 8
             busy += v["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * g)
             clock += g / dur[i]
             wait += v["SQ_WAIT_ANY"] / (v["SQ_WAVE_CYCLES"] or 1)
+            valu += v.get("SQ_ACTIVE_INST_VALU", 0.0) / (v["SQ_WAVE_CYCLES"] or 1)
             us += dur[i] / 1e3
         n = len(ids)
         print(json.dumps({"kernel": sub, "dispatches": n, "avg_us": round(us / n, 1),
                           "mfma_busy": round(busy / n, 3), "clock_ghz": round(clock / n, 3),
                           "busy_x_clock": round(busy * clock / n / n, 3), "wait_share": round(wait / n, 3),
+                          "valu_active_share": round(valu / n, 3),
                           "name": kname[ids[0]][:90]}))
 
 

@@ -33,6 +33,15 @@ constexpr int KB = 64;   // keys per staged block
 constexpr float kLog2e_ = 1.4426950408889634f;
 constexpr float kLn2_ = 0.69314718055994531f;
 constexpr float kDeferLog2 = 8.f;  // forward: defer the O rescale until the max grows by 2^8
+#ifndef VA_FLASH_FWD_DMA_OCC
+#define VA_FLASH_FWD_DMA_OCC 2  // waves per SIMD the LDS-DMA forward is compiled for
+#endif
+#ifndef VA_FLASH_DKDV_DMA_OCC
+#define VA_FLASH_DKDV_DMA_OCC 2  // the same for the LDS-DMA dK / dV backward
+#endif
+#ifndef VA_FLASH_DQ_DMA_OCC
+#define VA_FLASH_DQ_DMA_OCC 2  // the same for the LDS-DMA dQ backward
+#endif
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -50,12 +59,13 @@ __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2
 
 // KBF = keys per staged block (64 or 128): 128 halves the barriers (but measures slower: the
 // default is 64); each 64-key sub-block runs the same online-softmax step as a 64-key block
-template <int KBF>
-__global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
+template <int KBF, bool DMA>
+__global__ __launch_bounds__(256, DMA ? VA_FLASH_FWD_DMA_OCC : 2) void flash_fwd_kernel(
     const uint16_t *__restrict__ q, const uint16_t *__restrict__ k, const uint16_t *__restrict__ v,
     const int32_t *__restrict__ cu, const int32_t *__restrict__ blocks, int64_t lse_ld, int Hq, int Hk,
     float scale, uint16_t *__restrict__ o, float *__restrict__ lse) {
   static_assert(KBF == 64 || KBF == 128, "KBF");
+  static_assert(!DMA || KBF == 64, "DMA staging: 64-key blocks");
   constexpr int NCF = KBF * 8 / 256;  // 16-B chunks per thread per operand
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * KBF * D];  // [buf][K | V][KBF keys][64 d]
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, ql = lane & 31;
@@ -87,7 +97,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
   const int wave_last_q = qs + wave * 32 + 31;
 
   // staging: KBF rows x 8 chunks of 16 B per operand, NCF per thread per operand
-  uint4 sk[NCF], sv[NCF];
+  uint4 sk[DMA ? 1 : NCF], sv[DMA ? 1 : NCF];
   auto load_block = [&](int kb) {
 #pragma unroll
     for (int u = 0; u < NCF; ++u) {
@@ -112,13 +122,38 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
     }
   };
 
+  // DMA: the block's K / V rows go global -> LDS by LDS-DMA (16 B per lane, one 1-KiB piece = 8 rows
+  // per wave-instruction, K chunks swizzled through the source address), no staging registers;
+  // rows past the sequence end are clamped (their scores are masked, their P is 0)
+  auto dma_block = [&](int kb, int buf) {
+    uint16_t *lk = lds + buf * 2 * KBF * D;
+    uint16_t *lv = lk + KBF * D;
+#pragma unroll
+    for (int pi = wave; pi < KBF / 8; pi += 4) {
+      const int r = pi * 8 + (lane >> 3), p = lane & 7;
+      const int key = kb * KBF + r;
+      const int64_t base = (s0 + (key < len ? key : len - 1)) * ldk + kvh * D;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(k + base + ((p ^ (r & 7)) << 3)),
+                                       lk + pi * 8 * D, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(v + base + (p << 3)), lv + pi * 8 * D, 16, 0,
+                                       0);
+    }
+  };
+
   if (nkb > 0) {
-    load_block(0);
-    store_block(0);
+    if constexpr (DMA) {
+      dma_block(0, 0);
+    } else {
+      load_block(0);
+      store_block(0);
+    }
   }
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
-    if (kb + 1 < nkb) load_block(kb + 1);
+    if (kb + 1 < nkb) {
+      if constexpr (DMA) dma_block(kb + 1, (kb + 1) & 1);
+      else load_block(kb + 1);
+    }
 #pragma unroll
     for (int sub = 0; sub < KBF / KB; ++sub) {
     const uint16_t *lk = lds + (kb & 1) * 2 * KBF * D + sub * KB * D;
@@ -218,8 +253,10 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(
     }  // sub
     // the other buffer was last read in iteration kb - 1, which every wave finished before the
     // barrier that ended it: store, then one barrier publishes the block for iteration kb + 1
-    if (kb + 1 < nkb) store_block((kb + 1) & 1);
-    __syncthreads();
+    if constexpr (!DMA) {
+      if (kb + 1 < nkb) store_block((kb + 1) & 1);
+    }
+    __syncthreads();  // (DMA: its vmcnt(0) retires this wave's pieces of block kb + 1 first)
   }
 
   // ---- epilogue: O = O^T / l, lane holds O[q][32 dh + crow(r, h)]; lse in natural log
@@ -286,8 +323,8 @@ __device__ __forceinline__ bf16x8 pack_frag(const float *x) {
 // the chip).
 // QT = query rows per staged tile (32 or 64): the 64-row tile halves the barriers per MFMA; the
 // tile's 32-row halves run the same body (a 32-row offset keeps the images' XOR swizzle)
-template <bool GROUPED, int QT>
-__global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
+template <bool GROUPED, int QT, bool DMA>
+__global__ __launch_bounds__(256, DMA ? VA_FLASH_DKDV_DMA_OCC : 2) void flash_bwd_dkdv_kernel(
     const uint16_t *__restrict__ q, const uint16_t *__restrict__ k, const uint16_t *__restrict__ v,
     const uint16_t *__restrict__ dout, const float *__restrict__ lse, const float *__restrict__ delta,
     const int32_t *__restrict__ cu, const int32_t *__restrict__ kblocks, int64_t ld, int64_t T, int Hq, int Hk,
@@ -335,15 +372,28 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   const int n_it = GROUPED ? n_qt * G : n_qt;  // grouped: head-major over the group's query heads
   // staging: one 16-B chunk of the Q tile and one of the dO tile per thread; lse2 / delta by 64 threads
   struct StageQ {
-    uint4 q[NCH], d[NCH];
+    uint4 q[DMA ? 1 : NCH], d[DMA ? 1 : NCH];
     float rc;
   };
   auto load_it = [&](int it) -> StageQ {
     StageQ st;
     const int hj = GROUPED ? it / n_qt : 0;
     const int hq = hq0 + hj, qt0 = qfirst + (it - hj * n_qt) * QT;
+    if constexpr (DMA) {
+      // Q / dO images by LDS-DMA into buffer it & 1 (the buffer read two iterations ago: every wave
+      // passed the barrier that ended that iteration); rows past the sequence end clamped (p = 0)
+      uint16_t *img = lds + (it & 1) * 2 * QT * D;
 #pragma unroll
-    for (int u = 0; u < NCH; ++u) {
+      for (int pi = wave; pi < QT / 8; pi += 4) {
+        const int r = pi * 8 + (lane >> 3), pch = (lane & 7) ^ (r & 7), qp = qt0 + r;
+        const int64_t base = (s0 + (qp < len ? qp : len - 1)) * ldq + hq * D + (pch << 3);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(q + base), img + pi * 8 * D, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(dout + base), img + QT * D + pi * 8 * D, 16,
+                                         0, 0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < (DMA ? 0 : NCH); ++u) {
       const int idx = tid + u * 256, r = idx >> 3, ch = idx & 7, qp = qt0 + r;
       const bool ok = qp < len;
       const int64_t base = (s0 + (ok ? qp : len - 1)) * ldq + hq * D + ch * 8;  // clamped: no branch
@@ -363,7 +413,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dkdv_kernel(
   auto store_it = [&](int buf, const StageQ &st) {
     uint16_t *img = lds + buf * 2 * QT * D;
 #pragma unroll
-    for (int u = 0; u < NCH; ++u) {
+    for (int u = 0; u < (DMA ? 0 : NCH); ++u) {
       const int idx = tid + u * 256, r = idx >> 3, ch = idx & 7;
       *reinterpret_cast<uint4 *>(img + swz(r, ch * 8)) = st.q[u];
       *reinterpret_cast<uint4 *>(img + QT * D + swz(r, ch * 8)) = st.d[u];
@@ -498,8 +548,8 @@ __global__ __launch_bounds__(256) void flash_bwd_group_sum_kernel(const float *_
 // launch that follows: no separate delta pass over O and dO.
 // KBQ = keys per staged block (64 or 128): 128 halves the barriers per MFMA; the block's 32-key
 // tiles run the same body
-template <int KBQ>
-__global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
+template <int KBQ, bool DMA>
+__global__ __launch_bounds__(256, DMA ? VA_FLASH_DQ_DMA_OCC : 2) void flash_bwd_dq_kernel(
     const uint16_t *__restrict__ k, const uint16_t *__restrict__ v, const uint16_t *__restrict__ q,
     const uint16_t *__restrict__ o, const uint16_t *__restrict__ dout, const float *__restrict__ lse,
     float *__restrict__ delta, const int32_t *__restrict__ cu, const int32_t *__restrict__ blocks, int64_t ld,
@@ -554,7 +604,7 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
   const int kv_end = min(len, qs + QB);
   const int nkb = (kv_end + KBQ - 1) / KBQ;
   const int wave_last_q = qs + wave * 32 + 31;
-  uint4 sk[NCK], sv[NCK];
+  uint4 sk[DMA ? 1 : NCK], sv[DMA ? 1 : NCK];
   auto load_block = [&](int kb) {
 #pragma unroll
     for (int u = 0; u < NCK; ++u) {
@@ -578,13 +628,33 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
       *reinterpret_cast<uint4 *>(lv + swz(r, ch * 8)) = sv[u];
     }
   };
+  // DMA: LDS-DMA staging as in the forward (rows past the sequence end clamped: their dS is 0)
+  auto dma_block = [&](int kb, int buf) {
+    uint16_t *lk = lds + buf * 2 * KBQ * D;
+    uint16_t *lv = lk + KBQ * D;
+#pragma unroll
+    for (int pi = wave; pi < KBQ / 8; pi += 4) {
+      const int r = pi * 8 + (lane >> 3), pch = (lane & 7) ^ (r & 7);
+      const int kk = kb * KBQ + r;
+      const int64_t base = (s0 + (kk < len ? kk : len - 1)) * ldk + kvh * D + (pch << 3);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(k + base), lk + pi * 8 * D, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(v + base), lv + pi * 8 * D, 16, 0, 0);
+    }
+  };
   if (nkb > 0) {
-    load_block(0);
-    store_block(0);
+    if constexpr (DMA) {
+      dma_block(0, 0);
+    } else {
+      load_block(0);
+      store_block(0);
+    }
   }
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
-    if (kb + 1 < nkb) load_block(kb + 1);
+    if (kb + 1 < nkb) {
+      if constexpr (DMA) dma_block(kb + 1, (kb + 1) & 1);
+      else load_block(kb + 1);
+    }
     const uint16_t *lk = lds + (kb & 1) * 2 * KBQ * D;
     const uint16_t *lv = lk + KBQ * D;
 #pragma unroll
@@ -624,7 +694,9 @@ __global__ __launch_bounds__(256, 2) void flash_bwd_dq_kernel(
           dqt[dh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(lk, t * 32, s, dh, lane), db, dqt[dh], 0, 0, 0);
       }
     }
-    if (kb + 1 < nkb) store_block((kb + 1) & 1);
+    if constexpr (!DMA) {
+      if (kb + 1 < nkb) store_block((kb + 1) & 1);
+    }
     __syncthreads();
   }
   if (q_ok) {
@@ -654,6 +726,9 @@ int g_flash_dq_kb = 128;
 // va_set_tuning(VA_TUNE_FLASH_FWD_KB): keys per staged forward block, 64 (default) or 128 (slower:
 // 654 vs 573 us at 151,819 tokens, profiles/r01/attn_bwd_staging_ab.log)
 int g_flash_fwd_kb = 64;
+// va_set_tuning(VA_TUNE_FLASH_DMA): bit 1 = forward K / V blocks staged by LDS-DMA (64-key blocks),
+// bit 2 = the same for the dQ backward, bit 4 = the dK / dV backward's Q / dO tiles
+int g_flash_dma = 0;
 
 extern "C" int va_flash_attn_fwd(const void *q, const void *k, const void *v, const int32_t *cu_seqlens,
                                  const int32_t *block_table, int64_t n_blocks, int64_t T, int64_t Hq, int64_t Hk,
@@ -666,12 +741,12 @@ extern "C" int va_flash_attn_fwd(const void *q, const void *k, const void *v, co
   VA_CHECK_ARG(reinterpret_cast<uintptr_t>(q) % 16 == 0 && reinterpret_cast<uintptr_t>(k) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(v) % 16 == 0 && reinterpret_cast<uintptr_t>(o) % 16 == 0,
                "flash_attn_fwd: 16-byte aligned q / k / v / o required");
-#define VA_FWD(KBV)                                                                                             \
-  hipLaunchKernelGGL((flash_fwd_kernel<KBV>), dim3(static_cast<unsigned>(n_blocks), static_cast<unsigned>(Hq)),     \
+#define VA_FWD(KBV, DMAV)                                                                                       \
+  hipLaunchKernelGGL((flash_fwd_kernel<KBV, DMAV>), dim3(static_cast<unsigned>(n_blocks), static_cast<unsigned>(Hq)),     \
                      dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<const uint16_t *>(q),              \
                      static_cast<const uint16_t *>(k), static_cast<const uint16_t *>(v), cu_seqlens, block_table,  \
                      max_len, static_cast<int>(Hq), static_cast<int>(Hk), scale, static_cast<uint16_t *>(o), lse)
-  if (g_flash_fwd_kb == 64) VA_FWD(64); else VA_FWD(128);
+  if (g_flash_dma & 1) VA_FWD(64, true); else if (g_flash_fwd_kb == 64) VA_FWD(64, false); else VA_FWD(128, false);
 #undef VA_FWD
   return check_launch("flash_attn_fwd");
 }
@@ -691,31 +766,50 @@ extern "C" int va_flash_attn_bwd(const void *q, const void *k, const void *v, co
   float *pdk = partial, *pdv = partial + Hq * T * D;
   hipStream_t s = static_cast<hipStream_t>(stream);
   // dQ first: it also produces delta for the dK / dV launch
-#define VA_DQ(KBV)                                                                                               \
-  hipLaunchKernelGGL((flash_bwd_dq_kernel<KBV>), dim3(static_cast<unsigned>(n_q_blocks), static_cast<unsigned>(Hq)), \
+#define VA_DQ(KBV, DMAV)                                                                                         \
+  hipLaunchKernelGGL((flash_bwd_dq_kernel<KBV, DMAV>), dim3(static_cast<unsigned>(n_q_blocks), static_cast<unsigned>(Hq)), \
                      dim3(256), 0, s, static_cast<const uint16_t *>(k), static_cast<const uint16_t *>(v),             \
                      static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(o),                              \
                      static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens, q_blocks, max_len,                  \
                      static_cast<int>(Hq), static_cast<int>(Hk), scale, static_cast<uint16_t *>(dq))
-  if (g_flash_dq_kb == 64) VA_DQ(64); else VA_DQ(128);
+  if (g_flash_dma & 2) {
+    if (g_flash_dq_kb == 64) VA_DQ(64, true); else VA_DQ(128, true);
+  } else {
+    if (g_flash_dq_kb == 64) VA_DQ(64, false); else VA_DQ(128, false);
+  }
 #undef VA_DQ
   // grouped dK / dV (one workgroup per key block x KV head, no partials) once the key blocks alone
   // give >= 2 workgroups per CU; otherwise per query head + the fixed-order group sum
   const bool grouped = g_flash_grouped_dkdv == 1 || (g_flash_grouped_dkdv < 0 && n_k_blocks * Hk >= 512);
   const int qt = g_flash_dkdv_qt;
 #define VA_DKDV(GR, QTV)                                                                                         \
-  hipLaunchKernelGGL((flash_bwd_dkdv_kernel<GR, QTV>),                                                           \
+  if (g_flash_dma & 4) VA_DKDV_L(GR, QTV, true); else VA_DKDV_L(GR, QTV, false)
+#define VA_DKDV_L(GR, QTV, DMAV)                                                                                 \
+  hipLaunchKernelGGL((flash_bwd_dkdv_kernel<GR, QTV, DMAV>),                                                           \
                      dim3(static_cast<unsigned>(n_k_blocks), static_cast<unsigned>(GR ? Hk : Hq)), dim3(256), 0, s, \
                      static_cast<const uint16_t *>(q), static_cast<const uint16_t *>(k),                          \
                      static_cast<const uint16_t *>(v), static_cast<const uint16_t *>(dout), lse, delta, cu_seqlens, \
                      k_blocks, max_len, T, static_cast<int>(Hq), static_cast<int>(Hk), scale, pdk, pdv,            \
                      static_cast<uint16_t *>(dk), static_cast<uint16_t *>(dv))
   if (grouped) {
-    if (qt == 32) VA_DKDV(true, 32); else if (qt == 128) VA_DKDV(true, 128); else VA_DKDV(true, 64);
+    if (qt == 32) {
+      VA_DKDV(true, 32);
+    } else if (qt == 128) {
+      VA_DKDV(true, 128);
+    } else {
+      VA_DKDV(true, 64);
+    }
   } else {
-    if (qt == 32) VA_DKDV(false, 32); else if (qt == 128) VA_DKDV(false, 128); else VA_DKDV(false, 64);
+    if (qt == 32) {
+      VA_DKDV(false, 32);
+    } else if (qt == 128) {
+      VA_DKDV(false, 128);
+    } else {
+      VA_DKDV(false, 64);
+    }
   }
 #undef VA_DKDV
+#undef VA_DKDV_L
   if (!grouped) {
     const int64_t granules = T * Hk * (D / 4);
     int64_t grid = (granules + 255) / 256;

@@ -720,6 +720,7 @@ extern int g_swiglu_variant;      // model_ops.hip
 extern int g_flash_dkdv_qt;       // attention.hip
 extern int g_flash_dq_kb;         // attention.hip
 extern int g_flash_fwd_kb;        // attention.hip
+extern int g_flash_dma;           // attention.hip
 
 extern "C" int va_set_tuning(int key, int value) {
   switch (key) {
@@ -777,6 +778,7 @@ extern "C" int va_set_tuning(int key, int value) {
       }
       g_flash_fwd_kb = value;
       return VA_OK;
+    case VA_TUNE_FLASH_DMA: g_flash_dma = value & 7; return VA_OK;
     default: va::set_error("unknown tuning key %d", key); return VA_E_ARG;
   }
 }
