@@ -143,9 +143,9 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   VA_TUNE_SWIGLU_STREAM (va_swiglu_fwd/bwd): -1 = auto (streaming kernels: 4 / 2 vectors per lane
  *   fwd / bwd, all loads issued first, non-temporal), 2 / 4 / 8 = streaming with that many vectors
  *   per lane, 0 = grid-stride kernels (bitwise identical results);
- *   VA_TUNE_FLASH_DKDV_QT (va_flash_attn_bwd): query rows per staged dK / dV tile, 128 (default), 64
+ *   VA_TUNE_FLASH_DKDV_QT (va_flash_attn_bwd): query rows per staged dK / dV tile, 64 (default), 128
  *   or 32 (bitwise identical results: the same per-32-row products in the same order);
- *   VA_TUNE_FLASH_DQ_KB (va_flash_attn_bwd): keys per staged dQ block, 128 (default) or 64 (bitwise
+ *   VA_TUNE_FLASH_DQ_KB (va_flash_attn_bwd): keys per staged dQ block, 64 (default) or 128 (bitwise
  *   identical results);
  *   VA_TUNE_FLASH_FWD_KB (va_flash_attn_fwd): keys per staged forward block, 64 (default) or 128
  *   (bitwise identical results: the same 64-key online-softmax steps);
@@ -166,7 +166,7 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order);
  *   VA_TUNE_FLASH_DMA (va_flash_attn_fwd / _bwd): bit 1 = forward K / V blocks staged by LDS-DMA
  *   (64-key blocks), bit 2 = the same for the dQ backward, bit 4 = the dK / dV backward's Q / dO
- *   tiles; 0 = register-staged (bitwise identical results). */
+ *   tiles; 7 (default) = all three, 0 = register-staged (bitwise identical results). */
 #define VA_TUNE_FWD_WAVES_PER_ROW 1
 #define VA_TUNE_BWD_WAVES_PER_ROW 2
 #define VA_TUNE_NONTEMPORAL 3

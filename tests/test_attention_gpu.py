@@ -22,6 +22,13 @@ def _inputs(lens, hq=14, hk=2, d=64, seed=0):
     return q, k, v, cu
 
 
+def _restore_flash_defaults():
+    from verl_amd import _lib as L
+
+    for key, val in L.FLASH_TUNING_DEFAULTS.items():
+        L.call("va_set_tuning", key, val)
+
+
 def _ref_fp32(q, k, v, cu, scale):
     """Per-sequence causal SDPA in fp32 (GQA by repeat) -> O [T, Hq, D], LSE [Hq, T]."""
     hq, hk = q.shape[1], k.shape[1]
@@ -88,15 +95,15 @@ def test_flash_forward_key_block_128_equals_64(lens):
                    2, 64, mx, 64 ** -0.5, K._p(o), K._p(lse), K._stream(q))
             outs.append((o, lse))
     finally:
-        L.call("va_set_tuning", L.VA_TUNE_FLASH_FWD_KB, 64)
+        _restore_flash_defaults()
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
 
 
 @pytest.mark.parametrize("lens", [[1, 17, 128, 129, 300], [1184, 1100, 1280, 700], [64] * 9, [65, 191, 257], [3, 5]])
 def test_flash_forward_dma_staging_equals_register_staging(lens):
-    """VA_TUNE_FLASH_DMA bit 1 (K / V blocks by LDS-DMA, rows past a sequence end clamped to its
-    last row instead of zeroed) equals the register-staged forward bitwise: clamped keys are masked
+    """VA_TUNE_FLASH_DMA bit 1 (default; K / V blocks by LDS-DMA, rows past a sequence end clamped to
+    its last row instead of zeroed) equals the register-staged forward bitwise: clamped keys are masked
     to -inf and their P is 0, so the same products and sums are formed."""
     from verl_amd import _lib as L
     from verl_amd import kernels as K
@@ -116,7 +123,7 @@ def test_flash_forward_dma_staging_equals_register_staging(lens):
                    2, 64, mx, 64 ** -0.5, K._p(o), K._p(lse), K._stream(q))
             outs.append((o, lse))
     finally:
-        L.call("va_set_tuning", L.VA_TUNE_FLASH_DMA, 0)
+        _restore_flash_defaults()
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
 
@@ -212,9 +219,7 @@ def test_flash_backward_query_tile_64_equals_32(grouped, lens):
             grads.append((qb.grad, kb.grad, vb.grad))
     finally:
         A.FLASH_BWD = old
-        L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, -1)
-        L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 128)
-        L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, 128)
+        _restore_flash_defaults()
     for other in grads[1:]:
         for a, b in zip(grads[0], other):
             assert torch.equal(a, b)
@@ -249,10 +254,7 @@ def test_flash_backward_dma_staging_equals_register_staging(kblk, qt, grouped, l
             grads.append((qb.grad, kb.grad, vb.grad))
     finally:
         A.FLASH_BWD = old
-        L.call("va_set_tuning", L.VA_TUNE_FLASH_DMA, 0)
-        L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, 128)
-        L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 128)
-        L.call("va_set_tuning", L.VA_TUNE_FLASH_GROUPED_DKDV, -1)
+        _restore_flash_defaults()
     for other in grads[1:]:
         for a, b in zip(grads[0], other):
             assert torch.equal(a, b)

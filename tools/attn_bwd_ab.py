@@ -53,8 +53,8 @@ def main():
             b.record()
             torch.cuda.synchronize()
             times[(qt, kb)].append(a.elapsed_time(b) / 5 * 1e3)
-    L.call("va_set_tuning", L.VA_TUNE_FLASH_DKDV_QT, 128)
-    L.call("va_set_tuning", L.VA_TUNE_FLASH_DQ_KB, 128)
+    for key, val in L.FLASH_TUNING_DEFAULTS.items():
+        L.call("va_set_tuning", key, val)
     fwd_times = {64: [], 128: []}
     with torch.no_grad():
         for _ in range(6):

@@ -718,17 +718,21 @@ using namespace va;
 
 // va_set_tuning(VA_TUNE_FLASH_GROUPED_DKDV): -1 auto, 0 per-query-head partials + group sum, 1 grouped
 int g_flash_grouped_dkdv = -1;
-// va_set_tuning(VA_TUNE_FLASH_DKDV_QT): query rows per staged dK / dV tile, 32, 64 or 128 (default;
-// fwd+bwd 2,485 / 2,421 / 2,383 us at 151,819 tokens, profiles/r01/attn_bwd_staging_ab.log)
-int g_flash_dkdv_qt = 128;
-// va_set_tuning(VA_TUNE_FLASH_DQ_KB): keys per staged dQ block, 64 or 128 (default)
-int g_flash_dq_kb = 128;
+// va_set_tuning(VA_TUNE_FLASH_DKDV_QT): query rows per staged dK / dV tile, 32, 64 (default) or 128
+// (register staging: fwd+bwd 2,485 / 2,421 / 2,383 us at 151,819 tokens, profiles/r01/attn_bwd_staging_ab.log;
+// LDS-DMA staging: 64 2,242-2,248 vs 128 2,255-2,268 us, profiles/r04/attn_dma_ab.jsonl)
+int g_flash_dkdv_qt = 64;
+// va_set_tuning(VA_TUNE_FLASH_DQ_KB): keys per staged dQ block, 64 (default) or 128 (LDS-DMA staging:
+// 64 keys = 32 KiB of LDS lets 3 workgroups share a CU; fwd+bwd 2,288-2,301 vs 2,318-2,325 us)
+int g_flash_dq_kb = 64;
 // va_set_tuning(VA_TUNE_FLASH_FWD_KB): keys per staged forward block, 64 (default) or 128 (slower:
 // 654 vs 573 us at 151,819 tokens, profiles/r01/attn_bwd_staging_ab.log)
 int g_flash_fwd_kb = 64;
 // va_set_tuning(VA_TUNE_FLASH_DMA): bit 1 = forward K / V blocks staged by LDS-DMA (64-key blocks),
-// bit 2 = the same for the dQ backward, bit 4 = the dK / dV backward's Q / dO tiles
-int g_flash_dma = 0;
+// bit 2 = the same for the dQ backward, bit 4 = the dK / dV backward's Q / dO tiles; default 7 (all:
+// forward 541-549 vs 591-597 us, fwd+bwd 2,242-2,248 vs 2,368-2,385 us at 151,819 tokens, bitwise
+// the same results, profiles/r04/attn_dma_ab.jsonl); 0 = register staging through VGPRs
+int g_flash_dma = 7;
 
 extern "C" int va_flash_attn_fwd(const void *q, const void *k, const void *v, const int32_t *cu_seqlens,
                                  const int32_t *block_table, int64_t n_blocks, int64_t T, int64_t Hq, int64_t Hk,
