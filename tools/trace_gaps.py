@@ -13,6 +13,8 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--window", type=float, default=0.0, help="seconds at the end of the trace (0 = all)")
     ap.add_argument("--top", type=int, default=15)
+    ap.add_argument("--timeline", type=float, default=0.0,
+                    help="also list, in time order, every gap >= this many us and each step end (AdamW)")
     a = ap.parse_args()
     ev = []
     for r in csv.DictReader(open(a.trace)):
@@ -21,12 +23,19 @@ def main():
     t_end = max(e[1] for e in ev)
     t0 = t_end - int(a.window * 1e9) if a.window > 0 else ev[0][0]
     ev = [e for e in ev if e[0] >= t0]
-    busy, gaps = 0, []
+    busy, gaps, tl = 0, [], []
     cur_s, cur_e, prev_name = ev[0][0], ev[0][1], ev[0][2]
+    last_opt = None
     for s, e, n in ev[1:]:
+        if a.timeline and "multi_tensor_apply" in n:
+            if last_opt is None or s - last_opt > 20e6:
+                tl.append((s, "---- optimizer step", ""))
+            last_opt = s
         if s > cur_e:
             busy += cur_e - cur_s
             gaps.append((s - cur_e, prev_name, n))
+            if a.timeline and s - cur_e >= a.timeline * 1e3:
+                tl.append((cur_e, f"gap {(s - cur_e) / 1e3:9.1f} us after {prev_name[:45]}", f"before {n[:45]}"))
             cur_s, cur_e = s, e
         else:
             cur_e = max(cur_e, e)
@@ -47,6 +56,8 @@ def main():
         hist[k][1] += g
     for k, (c, t) in hist.items():
         print(f"  {k:6s} {c:6d} gaps {t / 1e6:8.1f} ms")
+    for t, what, nxt in tl:
+        print(f"  {(t - ev[0][0]) / 1e6:9.2f} ms  {what} {nxt}")
 
 
 if __name__ == "__main__":
