@@ -543,12 +543,21 @@ def main():
     from verl_amd import custom_ops
 
     fallbacks0 = custom_ops.AUTO_INPLACE_FALLBACKS
+    tprof_path = os.environ.get("VA_BENCH_TORCH_PROFILE")  # where the step's aten ops come from (diagnostics)
+    tprof = None
+    if tprof_path and rank == 0:
+        tprof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU], with_stack=True)
+        tprof.__enter__()
     t0 = time.perf_counter()
     metrics = None
     for i in range(args.steps):
         metrics = step()
         log(rank, f"timed step {i} issued")
     torch.cuda.synchronize()
+    if tprof is not None:
+        tprof.__exit__(None, None, None)
+        with open(tprof_path, "w") as f:
+            f.write(tprof.key_averages(group_by_stack_n=6).table(sort_by="count", row_limit=40, max_name_column_width=40))
     if prof is not None:
         prof.disable()
         prof.dump_stats(prof_path)
