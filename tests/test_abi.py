@@ -122,6 +122,9 @@ def test_tuning_keys_without_device(lib):
     assert lib.va_set_tuning(L.VA_TUNE_GAE_VARIANT, 0) == 0
     assert lib.va_set_tuning(L.VA_TUNE_BWD_FLAT, -1) == 0
     assert lib.va_set_tuning(L.VA_TUNE_SWIGLU_STREAM, -1) == 0
+    for key, val in L.FLASH_TUNING_DEFAULTS.items():  # the attention staging keys, at their defaults
+        assert lib.va_set_tuning(key, val) == 0, key
+    assert lib.va_set_tuning(L.VA_TUNE_FLASH_DQ_KB, 96) == -1
     assert lib.va_set_tuning(99, 1) == -1
 
 
