@@ -16,9 +16,11 @@
 //                    permuted, guide §3), V^T fragments by ds_read_b64_tr_b16 in the same order;
 //                    O^T keeps the query on the lane, so the rescale by exp2(m_old - m_new) and
 //                    the final 1 / l are lane-local.
-// K / V blocks of 64 keys are staged through double-buffered LDS shared by the 4 waves (the
-// block's next K / V rows are in registers during the current block's MFMAs). K rows are
-// XOR-swizzled for the row-fragment reads; V rows are plain for the transposed reads.
+// K / V blocks of 64 keys are staged through double-buffered LDS shared by the 4 waves: by LDS-DMA
+// (DMA = true, the default: global_load_lds issued at the top of a block for the next one, retired
+// by the block's closing barrier) or through registers (the next block's rows are in VGPRs during
+// the current block's MFMAs). K rows are XOR-swizzled for the row-fragment reads (through the
+// per-lane source address under DMA); V rows are plain for the transposed reads.
 
 #include <math.h>
 
