@@ -24,3 +24,17 @@ def test_own_wgrad_splits_respect_k():
     for tokens in (32, 256, 1024, 4096, 65536):
         s = K.own_wgrad_splits(128, 896, tokens)
         assert 1 <= s and (s == 1 or -(-tokens // 32) // s >= K.WGRAD_MIN_STEPS_PER_SLICE)
+
+
+@pytest.mark.parametrize("lens", [[], [1], [128], [129, 1, 300], [1184, 1100, 1280, 700, 5]])
+def test_flash_block_tables(lens):
+    """Query blocks (heaviest = latest first) and key blocks (earliest first) of every sequence,
+    each (sequence, first row) exactly once, ties broken by sequence."""
+    from verl_amd.workers.actor import attention as A
+
+    cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    want = [(s, r) for s, n in enumerate(lens) for r in range(0, n, 128)]
+    q = [tuple(x) for x in A.flash_block_table(cu).tolist()]
+    k = [tuple(x) for x in A.flash_key_block_table(cu).tolist()]
+    assert q == sorted(want, key=lambda t: (-t[1], t[0]))
+    assert k == sorted(want, key=lambda t: (t[1], t[0]))

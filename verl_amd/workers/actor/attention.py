@@ -47,15 +47,24 @@ def packed_attention(q, k, v, cu, mx, scaling=None):
 FLASH_QB = 128  # query rows per workgroup of va_flash_attn_fwd
 
 
+def _blocks(cu_host, blk: int):
+    """(sequence, first row) of every ``blk``-row block of the packed sequences, in sequence order
+    (host-side, vectorized: it runs on the step's critical path before the first kernel)."""
+    import numpy as np
+
+    lens = np.diff(np.asarray(cu_host, dtype=np.int64))
+    counts = (lens + blk - 1) // blk
+    seqs = np.repeat(np.arange(len(lens)), counts)
+    first = np.repeat(np.cumsum(counts) - counts, counts)
+    return seqs, (np.arange(len(seqs), dtype=np.int64) - first) * blk
+
+
 def flash_block_table(cu_host) -> "np.ndarray":
     """(sequence, first query row) of every 128-row query block, heaviest (latest) blocks first so
     the causal tail of long sequences does not end the launch on a few workgroups."""
     import numpy as np
 
-    cu_host = np.asarray(cu_host, dtype=np.int64)
-    lens = np.diff(cu_host)
-    seqs = np.repeat(np.arange(len(lens)), (lens + FLASH_QB - 1) // FLASH_QB)
-    starts = np.concatenate([np.arange(0, n, FLASH_QB) for n in lens]) if len(lens) else np.zeros(0, np.int64)
+    seqs, starts = _blocks(cu_host, FLASH_QB)
     order = np.lexsort((seqs, -starts))  # by start descending, then sequence
     return np.stack([seqs[order], starts[order]], axis=1).astype(np.int32)
 
@@ -68,10 +77,7 @@ def flash_key_block_table(cu_host) -> "np.ndarray":
     blocks first."""
     import numpy as np
 
-    cu_host = np.asarray(cu_host, dtype=np.int64)
-    lens = np.diff(cu_host)
-    seqs = np.repeat(np.arange(len(lens)), (lens + FLASH_KB - 1) // FLASH_KB)
-    starts = np.concatenate([np.arange(0, n, FLASH_KB) for n in lens]) if len(lens) else np.zeros(0, np.int64)
+    seqs, starts = _blocks(cu_host, FLASH_KB)
     order = np.lexsort((seqs, starts))
     return np.stack([seqs[order], starts[order]], axis=1).astype(np.int32)
 
