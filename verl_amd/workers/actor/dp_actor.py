@@ -110,14 +110,14 @@ def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device, pad_multiple: int =
     B, S = attn_mask_cpu.shape
     flat = attn_mask_cpu.reshape(-1).astype(bool)
     token_idx = np.flatnonzero(flat)
-    seqlens = attn_mask_cpu.astype(bool).sum(axis=1)
+    seqlens = flat.reshape(B, S).sum(axis=1)
     pad = (-len(token_idx)) % pad_multiple if pad_multiple > 0 else 0
     if pad:
         seqlens = np.concatenate([seqlens, [pad]])
     cu = np.zeros(len(seqlens) + 1, dtype=np.int32)
     np.cumsum(seqlens, out=cu[1:])
     # packed index of every padded position (valid only where the mask is 1)
-    packed_of = np.cumsum(flat) - 1
+    packed_of = np.cumsum(flat, dtype=np.int32 if flat.size < 2**31 else np.int64) - 1
     # position p = S - R - 1 + t predicts response token t (dp_actor.py:236-237)
     t = np.arange(R)
     p = (S - R - 1) + t
@@ -138,22 +138,36 @@ def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device, pad_multiple: int =
         nrow[wrap] = bounds[g[wrap]]
         label_idx[tail] = nrow * S + first_real[nrow]
 
-    def dev(a, dt):
-        from ... import kernels as K
+    from ... import kernels as K
 
-        return K.h2d(a, dt, device)
+    # two host->device copies (one int64, one int32 buffer) instead of one per index array: the
+    # plan is on the step's critical path before the first kernel; the tensors are views of them
+    blocks, kblocks = attention.flash_block_table(cu), attention.flash_key_block_table(cu)
+    i64 = [token_idx, sel_hidden, sel_out, label_idx, np.arange(pad)]
+    i32 = [cu, blocks.reshape(-1), kblocks.reshape(-1)]
+    d64 = K.h2d(np.concatenate(i64).astype(np.int64, copy=False), np.int64, device)
+    d32 = K.h2d(np.concatenate(i32).astype(np.int32, copy=False), np.int32, device)
 
+    def views(buf, parts):
+        out, o = [], 0
+        for a in parts:
+            out.append(buf[o:o + len(a)])
+            o += len(a)
+        return out
+
+    t_idx, s_hid, s_out, l_idx, p_pos = views(d64, i64)
+    t_cu, t_blk, t_kblk = views(d32, i32)
     return _Packing(
-        token_idx=dev(token_idx, np.int64),
-        cu_seqlens=dev(cu, np.int32),
+        token_idx=t_idx,
+        cu_seqlens=t_cu,
         max_seqlen=int(seqlens.max()) if B else 0,
-        sel_hidden=dev(sel_hidden, np.int64),
-        sel_out=dev(sel_out, np.int64),
-        label_idx=dev(label_idx, np.int64),
-        attn_blocks=dev(attention.flash_block_table(cu), np.int32),
-        attn_kblocks=dev(attention.flash_key_block_table(cu), np.int32),
+        sel_hidden=s_hid,
+        sel_out=s_out,
+        label_idx=l_idx,
+        attn_blocks=t_blk.view(-1, 2),
+        attn_kblocks=t_kblk.view(-1, 2),
         pad=int(pad),
-        pad_pos=dev(np.arange(pad), np.int64) if pad else None,
+        pad_pos=p_pos if pad else None,
     )
 
 
