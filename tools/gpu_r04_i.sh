@@ -1,3 +1,5 @@
+# NOTE: records the run at commit 44487f4; the ring variant was removed after it and tuning key 19 is
+# now VA_TUNE_FLASH_DMA, so rerun this script only at that commit.
 # f1 forward: the deep-ring variant (VA_TUNE_F1_RING = 19: 0 two 64-deep buffers, 4 / 5 ring stages of
 # 32) interleaved, with its deviation from the unfused path (must stay 0 / within 2e-6), then SQ
 # counters of each (MFMA busy, waits, clock)

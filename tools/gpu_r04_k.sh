@@ -1,3 +1,4 @@
+# NOTE: records the run at commit fdf044b (the VA_F1_SCHED code was removed after it).
 # round 4 GPU pass k: f1 fragment-read pipelining (VA_F1_SCHED build: asm ds_read one MFMA group
 # ahead + counted lgkmcnt) vs the product build; forward and fused backward, alternated; the
 # linear-logprob parity tests on the variant build

@@ -1,3 +1,4 @@
+# NOTE: the VA_F1_PRIO variants were measured from a working-tree patch and not kept.
 # round 4 GPU pass p: f1 forward with s_setprio (VA_F1_PRIO builds: 1 = priority 1 around each
 # step's MFMA cluster, 2 = waves 4-7 at priority 1 for the whole sweep) vs the product build, interleaved
 set -o pipefail
