@@ -376,12 +376,20 @@ __global__ __launch_bounds__(256, DMA ? VA_FLASH_DKDV_DMA_OCC : 2) void flash_bw
   struct StageQ {
     uint4 q[DMA ? 1 : NCH], d[DMA ? 1 : NCH];
     float rc;
+    bool live;
   };
   auto load_it = [&](int it) -> StageQ {
     StageQ st;
     const int hj = GROUPED ? it / n_qt : 0;
     const int hq = hq0 + hj, qt0 = qfirst + (it - hj * n_qt) * QT;
     if constexpr (DMA) {
+      // the row constants first, one unconditional (clamped) load per thread: hipcc waits for it
+      // only where store_it consumes it, and, issued before the DMA below, that wait leaves the DMA
+      // in flight (a conditional load made hipcc drain everything at the top of the iteration)
+      const int rr = tid & (QT - 1), qq = qt0 + rr;
+      const int64_t idx = (static_cast<int64_t>(seq) * Hq + hq) * ld + (qq < len ? qq : len - 1);
+      st.rc = (tid & QT) ? delta[idx] : lse[idx];  // tid < QT: lse, QT <= tid < 2 QT: delta
+      st.live = qq < len;
       // Q / dO images by LDS-DMA into buffer it & 1 (the buffer read two iterations ago: every wave
       // passed the barrier that ended that iteration); rows past the sequence end clamped (p = 0)
       uint16_t *img = lds + (it & 1) * 2 * QT * D;
@@ -404,11 +412,13 @@ __global__ __launch_bounds__(256, DMA ? VA_FLASH_DKDV_DMA_OCC : 2) void flash_bw
       st.q[u] = ok ? a : make_uint4(0, 0, 0, 0);
       st.d[u] = ok ? b : make_uint4(0, 0, 0, 0);
     }
-    st.rc = 0.f;
-    if (tid < 2 * QT) {
-      const int rr = tid & (QT - 1), qq = qt0 + rr;
-      const int64_t idx = (static_cast<int64_t>(seq) * Hq + hq) * ld + qq;
-      if (qq < len) st.rc = tid < QT ? lse[idx] * kLog2e_ : delta[idx];
+    if constexpr (!DMA) {
+      st.rc = 0.f;
+      if (tid < 2 * QT) {
+        const int rr = tid & (QT - 1), qq = qt0 + rr;
+        const int64_t idx = (static_cast<int64_t>(seq) * Hq + hq) * ld + qq;
+        if (qq < len) st.rc = tid < QT ? lse[idx] * kLog2e_ : delta[idx];
+      }
     }
     return st;
   };
@@ -420,7 +430,11 @@ __global__ __launch_bounds__(256, DMA ? VA_FLASH_DKDV_DMA_OCC : 2) void flash_bw
       *reinterpret_cast<uint4 *>(img + swz(r, ch * 8)) = st.q[u];
       *reinterpret_cast<uint4 *>(img + QT * D + swz(r, ch * 8)) = st.d[u];
     }
-    if (tid < 2 * QT) rowc[buf * 2 * QT + tid] = st.rc;
+    if constexpr (DMA) {
+      if (tid < 2 * QT) rowc[buf * 2 * QT + tid] = st.live ? (tid < QT ? st.rc * kLog2e_ : st.rc) : 0.f;
+    } else {
+      if (tid < 2 * QT) rowc[buf * 2 * QT + tid] = st.rc;
+    }
   };
   StageQ stq;
   if (n_it > 0) {
