@@ -4,6 +4,10 @@ projections (forward, with / without bias) and their input gradients (dY against
 weight). Relative error of both against an fp32 product; HIP-event medians; one JSON line each.
 
   python tools/linear_tn_ab.py [--tokens 153600] [--per 0]
+
+The probe kernel (va_linear_tn: t256_sweep with a bf16 store epilogue, ABI 6) was measured with this
+script (profiles/r04/linear_tn_ab.jsonl) and not kept, so at HEAD the script stops at its first call;
+it records the method.
 """
 
 import argparse
