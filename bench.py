@@ -315,6 +315,25 @@ def cpu_baseline(args) -> dict:
     }
 
 
+def clipped_tokens(step_metrics: list, batch, micro: int, dynamic: bool):
+    """Tokens on the clipped branches over the timed steps: sum over every loss micro-batch of
+    pg_clipfrac (and pg_clipfrac_lower) x its response tokens. The update walks the rank's rows in
+    order in micro-batches of ``micro`` rows (dp_actor.update_policy: one mini-batch per rank), so
+    the k-th entry of a metric list is rows [k micro, (k+1) micro). None with dynamic micro-batches."""
+    if dynamic or not step_metrics:
+        return None
+    rm = batch.batch["response_mask"]
+    B = rm.shape[0]
+    per_mb = [float(rm[r:r + micro].sum()) for r in range(0, B, micro)]  # one host sync, after the timed region
+    out = {"pg_clipfrac": 0.0, "pg_clipfrac_lower": 0.0}
+    for m in step_metrics:
+        for key in out:
+            vals = m.get(f"actor/{key}", [])
+            out[key] += sum(v * per_mb[k % len(per_mb)] for k, v in enumerate(vals))
+    return {"clipped_tokens": round(out["pg_clipfrac"]), "clipped_lower_tokens": round(out["pg_clipfrac_lower"]),
+            "response_tokens": round(sum(per_mb)) * len(step_metrics)}
+
+
 def cgroup_cpu_quota():
     """CPUs the process's cgroup may use (cpu.max quota / period, v2; cfs_quota_us / cfs_period_us,
     v1), or None without a quota; with the file it came from."""
@@ -550,8 +569,10 @@ def main():
         tprof.__enter__()
     t0 = time.perf_counter()
     metrics = None
+    step_metrics = []  # each timed step's metric lists (host values: update_actor returns them)
     for i in range(args.steps):
         metrics = step()
+        step_metrics.append(metrics.meta_info["metrics"])
         log(rank, f"timed step {i} issued")
     torch.cuda.synchronize()
     if tprof is not None:
@@ -588,6 +609,17 @@ def main():
     perf_throughput = sum(batch.meta_info["global_token_num"]) * args.steps / elapsed / world
 
     log(rank, f"timed region: {elapsed:.2f}s for {args.steps} steps")
+    # the reference's reduction of the last step's metric lists (utils/metric/utils.py:23-50: mean,
+    # max / min by key name), then over the ranks as its DP collect does; and the clipped-branch
+    # token counts of all timed steps, summed over the ranks
+    from verl_amd.trainer.ppo.trainer_step import reduce_metrics_dp
+
+    final_metrics = reduce_metrics_dp(dict(metrics.meta_info["metrics"])) if metrics is not None else {}
+    clip = clipped_tokens(step_metrics, batch, micro, args.dynamic_bsz > 0)
+    if clip is not None and world > 1:
+        ct = torch.tensor([clip[k] for k in sorted(clip)], dtype=torch.float64, device=dev)
+        vcomm.all_reduce(ct)
+        clip = {k: round(float(v)) for k, v in zip(sorted(clip), ct.tolist())}
     # after the timed region: every rank must hold the same model (FSDP's by-construction
     # consistency, fsdp_workers.py:370-405) and the same globally-reduced metrics
     from verl_amd.utils.replica_check import replica_check
@@ -707,8 +739,10 @@ def main():
             "cpu_baseline": cpu,
             "replicas_identical": rcheck["replicas_identical"],
             "replica_check": rcheck,
-            "final_metrics": {k: (v[-1] if isinstance(v, list) else v)
-                              for k, v in (metrics.meta_info["metrics"].items() if metrics is not None else [])},
+            "final_metrics": final_metrics,
+            "final_metrics_reduction": "reduce_metrics (utils/metric/utils.py:23-50) of the last timed step, "
+                                       "mean over the ranks",
+            "clip_branch_tokens_timed_steps": clip,
         }
         s = json.dumps(line)
         print(s, flush=True)

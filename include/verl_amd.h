@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define VA_ABI_VERSION 5
+#define VA_ABI_VERSION 6
 
 /* error codes */
 #define VA_OK 0
@@ -390,10 +390,13 @@ int va_transpose_16(const void *in, int64_t ld_in, int64_t R, int64_t C, void *o
  * tokens; no reference counterpart: torch's linear backward under FSDP, dp_actor.py:465-470). K a
  * multiple of 32; M, N, strides multiples of 8; 16-byte aligned buffers. splits: K slices (0 =
  * automatic; fp32 partials in workspace = va_weight_grad_workspace_bytes(K, M, N, splits), summed in
- * slice order, rounded once). Not a §8 row. */
+ * slice order, rounded once). workspace_bytes: the size of the buffer passed (ABI 6): the launch
+ * plans its tiles and slices once and fails with VA_E_ARG when that plan needs more than this (the
+ * plan depends on VA_TUNE_WGRAD_REMAINDER, which may change between the size query and the launch).
+ * Not a §8 row. */
 int64_t va_weight_grad_workspace_bytes(int64_t K, int64_t M, int64_t N, int splits);
 int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_t ldx, int64_t K, int64_t M, int64_t N,
-                   int splits, float *workspace, void *out, void *stream);
+                   int splits, float *workspace, int64_t workspace_bytes, void *out, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Fused lm_head + log-prob + entropy forward (the reference's use_fused_kernels
@@ -417,13 +420,17 @@ int va_linear_logprob_fwd(const void *hidden, int64_t ldh, const void *weight, i
  *   dlogits[i, v] = bf16( ( -p (g_entropy[i] (x - lse_i + H_i) + g_logp[i]) + g_logp[i] [v == labels[i]] ) / T ),
  *   p = exp(x - lse_i), x the logit as the forward saw it,
  * i.e. va_logprob_entropy_bwd's arithmetic, without the logits in HBM. lse / entropy: the forward's
- * outputs; g_logp / g_entropy may be NULL (zero). dlogits [N, V] bf16, row stride ldd >= V (8-byte
- * aligned, ldd % 4 == 0), V % 4 == 0. The caller runs the lm_head's two backward GEMMs on it
- * (dhidden = dlogits W, dW = dlogits^T hidden). `splits` vocab ranges per row block as in the forward. */
+ * outputs; g_logp / g_entropy may be NULL (zero). Only the vocab range [v_begin, v_end) of the V
+ * entries is computed (ABI 6; [0, V) for all of it): dlogits [N, v_end - v_begin] bf16, column 0 =
+ * vocab v_begin, row stride ldd >= v_end - v_begin (8-byte aligned, ldd % 4 == 0), (v_end - v_begin)
+ * % 4 == 0 — the reference's vocab_per_split loop (kernels.py:1491-1548), so that only one range of
+ * dlogits exists at a time; labels are valid against the whole V. The caller runs the lm_head's two
+ * backward GEMMs on it (dhidden += dlogits W[v_begin:v_end], dW[v_begin:v_end] = dlogits^T hidden).
+ * `splits` vocab sub-ranges per row block as in the forward. */
 int va_linear_logprob_bwd(const void *hidden, int64_t ldh, const void *weight, int64_t ldw, int dtype,
                           const int64_t *labels, const float *lse, const float *entropy, const float *g_logp,
-                          const float *g_entropy, int64_t N, int64_t H, int64_t V, float temperature, int splits,
-                          void *dlogits, int64_t ldd, void *stream);
+                          const float *g_entropy, int64_t N, int64_t H, int64_t V, int64_t v_begin, int64_t v_end,
+                          float temperature, int splits, void *dlogits, int64_t ldd, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Discounted returns for REINFORCE++ (mode VA_RET_RFPP, gamma) and ReMax (VA_RET_REMAX:

@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_abi_version_and_workspace_queries(lib):
-    assert lib.va_abi_version() == 5
+    assert lib.va_abi_version() == 6
     assert lib.va_ppo_loss_workspace_bytes(10) == 8 * (2 * 10 * 8 + 8)
     assert lib.va_agg_workspace_bytes(10) == 8 * (2 * 10 * 8 + 8)
     assert lib.va_gae_workspace_bytes(7) == 8 * (6 * 7 + 8)
@@ -67,18 +67,27 @@ def test_argument_validation_without_device(lib):
     assert rc == -1 and b"bad segments" in lib.va_last_error()
     assert lib.va_outcome_workspace_bytes(10) == 4 * 3 * 10
     # weight gradient: tokens not a multiple of 32
-    rc = lib.va_weight_grad(1, 64, 1, 64, 100, 64, 64, 1, None, 1, None)
+    rc = lib.va_weight_grad(1, 64, 1, 64, 100, 64, 64, 1, None, 0, 1, None)
     assert rc == -1 and b"multiple of 32" in lib.va_last_error()
+    # the launch's own plan needs more workspace than the caller passed
+    rc = lib.va_weight_grad(16, 64, 16, 32, 4096, 64, 32, 3, 16, 4 * 3 * 64 * 32 - 4, 16, None)
+    assert rc == -1 and b"workspace bytes" in lib.va_last_error()
     assert lib.va_weight_grad_workspace_bytes(4096, 64, 32, 3) == 4 * 3 * 64 * 32
     rc = lib.va_group_coef(1, None, 1, 1, 4, 8, 1e-6, L.VA_ADV_OPO, 1, None)
     assert rc == -1 and b"lengths" in lib.va_last_error()
     assert lib.va_logprob_entropy_fwd(None, 1, 0, 10, 10, None, 1.0, None, None, None, None) == 0  # n_rows 0: no-op
     # fused lm_head backward: V % 4 != 0 is an argument error; N = 0 is a no-op
-    rc = lib.va_linear_logprob_bwd(None, 64, None, 64, L.VA_BF16, None, None, None, None, None, 4, 64, 130, 1.0, 1,
-                                   None, 130, None)
+    rc = lib.va_linear_logprob_bwd(None, 64, None, 64, L.VA_BF16, None, None, None, None, None, 4, 64, 130, 0, 130,
+                                   1.0, 1, None, 130, None)
     assert rc == -1 and b"V % 4" in lib.va_last_error()
-    assert lib.va_linear_logprob_bwd(None, 64, None, 64, L.VA_BF16, None, None, None, None, None, 0, 64, 128, 1.0, 1,
-                                     None, 128, None) == 0
+    assert lib.va_linear_logprob_bwd(None, 64, None, 64, L.VA_BF16, None, None, None, None, None, 0, 64, 128, 0, 128,
+                                     1.0, 1, None, 128, None) == 0
+    # vocab ranges (ABI 6): inside [0, V), a multiple of 4 wide (V itself need not be)
+    rc = lib.va_linear_logprob_bwd(None, 64, None, 64, L.VA_BF16, None, None, None, None, None, 4, 64, 128, 64, 132,
+                                   1.0, 1, None, 68, None)
+    assert rc == -1 and b"vocab range" in lib.va_last_error()
+    assert lib.va_linear_logprob_bwd(None, 64, None, 64, L.VA_BF16, None, None, None, None, None, 0, 64, 130, 2, 130,
+                                     1.0, 1, None, 128, None) == 0
 
 
 def test_product_path_rejects_cpu_tensors():

@@ -192,3 +192,43 @@ def test_whole_batch_metrics_match_reference_formulas():
     assert m["critic/score/mean"] == pytest.approx(float(score.mean()), rel=1e-6)
     rl = b.batch["attention_mask"][:, -5:].sum(-1).float()
     assert m["response_length/clip_ratio"] == pytest.approx(float(torch.eq(rl, 5).float().mean()))
+
+
+def test_explained_var_without_cancellation_at_large_means():
+    """the variances behind vf_explained_var are second moments about the merged mean,
+    so returns / values of mean 1e8 and unit spread keep their variance (sumsq - n mean^2 in fp64
+    would leave only a few bits of it)."""
+    b = _batch(B=8, R=16, seed=5)
+    g = torch.Generator().manual_seed(11)
+    b.batch["returns"] = 1e8 + torch.randn(8, 16, generator=g, dtype=torch.float64)
+    b.batch["values"] = 1e8 + 0.5 * torch.randn(8, 16, generator=g, dtype=torch.float64)
+    m = compute_data_metrics(b, use_critic=True)
+    rm = b.batch["response_mask"].bool()
+    ret = torch.masked_select(b.batch["returns"], rm)
+    val = torch.masked_select(b.batch["values"], rm)
+    ev = 1.0 - torch.var(ret - val) / (torch.var(ret) + 1e-5)
+    assert m["critic/vf_explained_var"] == pytest.approx(float(ev), rel=1e-9)
+
+
+def test_bench_final_metrics_are_the_reference_reduction():
+    """bench.py reports reduce_metrics of the last step's lists (utils/metric/utils.py:23-50: the
+    mean, max / min by key name; W = 1 here) and counts the clipped-branch tokens of the timed
+    steps as pg_clipfrac x each loss micro-batch's response tokens."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from verl_amd.trainer.ppo.trainer_step import reduce_metrics_dp
+
+    m = {"actor/pg_loss": [0.5, 0.1, 0.3], "actor/pg_clipfrac": [0.0, 0.25, 0.5], "actor/pg_clipfrac_lower": [0.0, 0.0, 0.1],
+         "perf/max_memory_allocated_gb": 3.0, "actor/lr": 1e-6}
+    got = reduce_metrics_dp(dict(m))
+    assert got == reduce_metrics(dict(m))
+    assert got["actor/pg_loss"] == pytest.approx(0.3) and got["perf/max_memory_allocated_gb"] == 3.0
+    rm = torch.ones(6, 4, dtype=torch.long)
+    rm[2:4, 2:] = 0  # micro-batch 1 (rows 2-3) holds 4 tokens, the others 8
+    batch = DataProto.from_dict(tensors={"response_mask": rm})
+    clip = bench.clipped_tokens([m, m], batch, micro=2, dynamic=False)
+    assert clip == {"clipped_tokens": round(2 * (0.25 * 4 + 0.5 * 8)), "clipped_lower_tokens": round(2 * 0.1 * 8),
+                    "response_tokens": 2 * 20}
+    assert bench.clipped_tokens([m], batch, micro=2, dynamic=True) is None

@@ -18,8 +18,8 @@ def _call(dy, x, splits):
     out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
     nb = L.load().va_weight_grad_workspace_bytes(T, M, N, splits)
     ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=DEV)
-    L.call("va_weight_grad", K._p(dy), dy.stride(0), K._p(x), x.stride(0), T, M, N, splits, K._p(ws), K._p(out),
-           K._stream(dy))
+    L.call("va_weight_grad", K._p(dy), dy.stride(0), K._p(x), x.stride(0), T, M, N, splits, K._p(ws), ws.numel() * 4,
+           K._p(out), K._stream(dy))
     return out
 
 

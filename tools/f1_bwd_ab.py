@@ -3,11 +3,12 @@
 
   * kernel level: the fused dlogits kernel (recompute + dlogits, bf16 [N, V] out) vs hipBLASLt's
     logits recompute + the streaming va_logprob_entropy_bwd in place;
-  * pass level: the whole fused path (f1 forward + fused backward incl. the two lm_head GEMMs) vs the
-    unfused update pass (hipBLASLt logits + logprob_entropy fwd + bwd + the two GEMMs), with the
-    peak HBM of each.
+  * pass level: the whole fused path (f1 forward + fused backward incl. the two lm_head GEMMs, per
+    vocab range of --vocab-splits columns: the reference's _Split_Dlogits_N loop) vs the unfused
+    update pass (hipBLASLt logits + logprob_entropy fwd + bwd + the two GEMMs), with the peak HBM
+    of each.
 
-  python tools/f1_bwd_ab.py [--rows 131072] [--iters 3]
+  python tools/f1_bwd_ab.py [--rows 131072] [--iters 3] [--vocab-splits 9504,37984,151936]
 """
 
 import argparse
@@ -38,6 +39,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=131072)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--vocab-splits", default="9504", help="comma-separated vocab range widths of the fused pass")
+    ap.add_argument("--skip-kernel", action="store_true", help="pass level only")
     args = ap.parse_args()
     from verl_amd import kernels as K
 
@@ -54,6 +57,8 @@ def main():
     flops = 2.0 * N * V * H
 
     # ---- kernel level
+    if args.skip_kernel:
+        return pass_level(args, K, h, w, lab, g1, out)
     dlog = torch.empty(N, V, dtype=torch.bfloat16, device=dev)
     ms, ts = timed(lambda: K._linear_logprob_bwd_raw(h, w, lab, lse, ent, g1, None, 1.0, False, dlog), args.iters)
     out["fused_dlogits_ms"] = round(ms, 3)
@@ -68,8 +73,12 @@ def main():
     out["compose_gemm_plus_stream_bwd_ms"] = round(ms_c, 3)
     del dlog, logits
     torch.cuda.empty_cache()
+    pass_level(args, K, h, w, lab, g1, out)
 
-    # ---- pass level (forward + backward of the lm_head + log-prob, with GEMMs)
+
+def pass_level(args, K, h, w, lab, g1, out):
+    """forward + backward of the lm_head + log-prob, with GEMMs"""
+
     def fused_pass():
         ha, wa = h.detach().requires_grad_(True), w.detach().requires_grad_(True)
         lp, _ = K.linear_logprob_entropy(ha, wa, lab, 1.0)
@@ -80,14 +89,16 @@ def main():
         lp, _ = K.logprob_entropy(K.linear(ha, wa), lab, 1.0, inplace_backward="auto")
         (lp * g1).sum().backward()
 
-    for name, fn in (("fused_pass", fused_pass), ("unfused_pass", unfused_pass)):
+    runs = [(f"fused_pass_split{int(s)}", fused_pass, int(s)) for s in args.vocab_splits.split(",")]
+    for name, fn, split in runs + [("unfused_pass", unfused_pass, None)]:
+        if split is not None:
+            K._LinearLogprob.VOCAB_PER_SPLIT = split
         torch.cuda.empty_cache()
         torch.cuda.reset_peak_memory_stats()
         base = torch.cuda.memory_allocated()
         ms_p, _ = timed(fn, args.iters)
         out[f"{name}_ms"] = round(ms_p, 3)
         out[f"{name}_peak_extra_gb"] = round((torch.cuda.max_memory_allocated() - base) / 1e9, 2)
-    out["fused_chunk_mb"] = K._LinearLogprob.CHUNK_BYTES >> 20
     print(json.dumps(out), flush=True)
 
 

@@ -52,7 +52,7 @@ def main():
         o = torch.empty(V, H, dtype=torch.bfloat16, device=dev)
         nb = L.load().va_weight_grad_workspace_bytes(T, V, H, 0)
         ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=dev) if nb else None
-        L.call("va_weight_grad", K._p(dy), dy.stride(0), K._p(x), x.stride(0), T, V, H, 0, K._p(ws), K._p(o),
+        L.call("va_weight_grad", K._p(dy), dy.stride(0), K._p(x), x.stride(0), T, V, H, 0, K._p(ws), nb, K._p(o),
                K._stream(dy))
         return o
 

@@ -15,6 +15,10 @@ def main():
     ap.add_argument("--top", type=int, default=15)
     ap.add_argument("--timeline", type=float, default=0.0,
                     help="also list, in time order, every gap >= this many us and each step end (AdamW)")
+    ap.add_argument("--steps", type=int, default=0,
+                    help="per-step idle over the last N steps (a step = from the end of one optimizer step's "
+                         "AdamW launches to the end of the next), and the gaps of those steps summed by the "
+                         "kernel pair around them")
     a = ap.parse_args()
     ev = []
     for r in csv.DictReader(open(a.trace)):
@@ -58,6 +62,50 @@ def main():
         print(f"  {k:6s} {c:6d} gaps {t / 1e6:8.1f} ms")
     for t, what, nxt in tl:
         print(f"  {(t - ev[0][0]) / 1e6:9.2f} ms  {what} {nxt}")
+    if a.steps:
+        per_step(ev, a.steps, a.top)
+
+
+def per_step(ev, n_steps, top):
+    """Idle time of each of the last ``n_steps`` steps, bounded by the optimizer (AdamW
+    multi_tensor_apply) launch groups, and their gaps summed by (kernel before, kernel after)."""
+    groups, last = [], None
+    for s, e, n in ev:
+        if "multi_tensor_apply" in n:
+            if last is None or s - last > 20e6:
+                groups.append([s, e])
+            else:
+                groups[-1][1] = max(groups[-1][1], e)
+            last = s
+    if len(groups) < n_steps + 1:
+        print(f"per-step: only {len(groups)} optimizer steps in the trace")
+        return
+    pairs, tot_idle, tot_span = {}, 0, 0
+    for i in range(len(groups) - n_steps, len(groups)):
+        lo, hi = groups[i - 1][1], groups[i][1]
+        sev = [x for x in ev if x[0] >= lo and x[1] <= hi]
+        cur_e, prev = lo, "(previous optimizer step)"
+        idle, big, cnt = 0, (0, "", ""), 0
+        for s, e, n in sev:
+            if s > cur_e:
+                g = s - cur_e
+                idle += g
+                cnt += 1
+                big = max(big, (g, prev, n))
+                k = (prev[:40], n[:40])
+                pairs.setdefault(k, [0, 0])
+                pairs[k][0] += 1
+                pairs[k][1] += g
+            if e >= cur_e:
+                cur_e, prev = e, n
+        span = hi - lo
+        tot_idle += idle
+        tot_span += span
+        print(f"step {i}: span {span / 1e6:8.2f} ms, idle {idle / 1e6:7.2f} ms ({100 * idle / span:.2f}%) in {cnt} "
+              f"gaps; largest {big[0] / 1e3:.1f} us after {big[1][:40]} before {big[2][:40]}")
+    print(f"last {n_steps} steps: idle {tot_idle / 1e6:.2f} of {tot_span / 1e6:.2f} ms ({100 * tot_idle / tot_span:.2f}%)")
+    for (p, n), (c, g) in sorted(pairs.items(), key=lambda kv: -kv[1][1])[:top]:
+        print(f"  {g / 1e6 / n_steps:7.3f} ms/step {c / n_steps:6.1f} gaps/step  after {p:40s} before {n}")
 
 
 if __name__ == "__main__":

@@ -41,6 +41,8 @@ VA_TUNE_WGRAD_REMAINDER, VA_TUNE_FLASH_DMA = 18, 19
 FLASH_TUNING_DEFAULTS = {VA_TUNE_FLASH_DMA: 7, VA_TUNE_FLASH_DQ_KB: 64, VA_TUNE_FLASH_DKDV_QT: 64,
                          VA_TUNE_FLASH_FWD_KB: 64, VA_TUNE_FLASH_GROUPED_DKDV: -1}
 
+ABI_VERSION = 6  # include/verl_amd.h VA_ABI_VERSION
+
 _P = c_void_p
 _SIGNATURES: dict[str, tuple] = {
     "va_abi_version": (c_int, []),
@@ -104,8 +106,8 @@ _SIGNATURES: dict[str, tuple] = {
         c_int, [_P, c_int64, _P, c_int64, c_int, _P, c_int64, c_int64, c_int64, c_float, c_int, _P, _P, _P, _P, _P]
     ),
     "va_linear_logprob_bwd": (
-        c_int, [_P, c_int64, _P, c_int64, c_int, _P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_float, c_int, _P,
-                c_int64, _P]
+        c_int, [_P, c_int64, _P, c_int64, c_int, _P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int64, c_int64,
+                c_float, c_int, _P, c_int64, _P]
     ),
     "va_flash_attn_fwd": (
         c_int, [_P, _P, _P, _P, _P, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, c_float, _P, _P, _P]
@@ -119,7 +121,7 @@ _SIGNATURES: dict[str, tuple] = {
     "va_rope_qkv_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, c_int64, _P]),
     "va_transpose_16": (c_int, [_P, c_int64, c_int64, c_int64, _P, c_int64, _P]),
     "va_weight_grad_workspace_bytes": (c_int64, [c_int64, c_int64, c_int64, c_int]),
-    "va_weight_grad": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int64, c_int64, c_int, _P, _P, _P]),
+    "va_weight_grad": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int64, c_int64, c_int, _P, c_int64, _P, _P]),
 }
 
 _lib = None
@@ -155,8 +157,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.va_abi_version() != 5 and not ab:
-        raise NativeLibraryError(f"ABI version mismatch: {lib.va_abi_version()} != 5")
+    if lib.va_abi_version() != ABI_VERSION and not ab:
+        raise NativeLibraryError(f"ABI version mismatch: {lib.va_abi_version()} != {ABI_VERSION}")
     _lib = lib
     return lib
 

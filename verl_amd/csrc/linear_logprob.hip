@@ -536,12 +536,16 @@ __global__ __launch_bounds__(256) void linear_logprob_merge_kernel(const float *
 // kk = gh (H - lse) + g_lp, dx = dz / T, rounded to bf16 (the reference's fused backward,
 // kernels.py:1241-1342, forms the same d_logits per vocab split). Each lane owns 4 consecutive vocab
 // entries of a token per (i, j): one 8-byte store. Rows >= N and vocab >= V are computed, not stored.
+// One launch covers the vocab range [vbase, vbase + V) of a V_full vocabulary (w points at row vbase,
+// dlog column 0 is vocab vbase): the reference's _Split_Dlogits_N loop (kernels.py:1491-1548) runs it
+// per range so that only [N, range] dlogits exist at a time. A label counts as valid against V_full
+// (its g_lp term enters kk for every range); its own +g_lp lands only in the range that holds it.
 template <bool SCALE, bool ROUND, bool REMAP>
 __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
     const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
     const int64_t *__restrict__ labels, const float *__restrict__ lse_in, const float *__restrict__ ent_in,
-    const float *__restrict__ g_logp, const float *__restrict__ g_ent, int64_t N, int K, int64_t V, int splits,
-    int tiles_per_split, float temperature, uint16_t *__restrict__ dlog, int64_t ldd) {
+    const float *__restrict__ g_logp, const float *__restrict__ g_ent, int64_t N, int K, int64_t V, int64_t V_full,
+    int64_t vbase, int splits, int tiles_per_split, float temperature, uint16_t *__restrict__ dlog, int64_t ldd) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
@@ -557,8 +561,9 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
     const int64_t r = row0 + wc * 64 + j * 16 + (lane & 15);
     const bool ok = r < N;
     const int64_t lb = ok ? labels[r] : -1;
-    const bool has_lab = lb >= 0 && lb < V;
-    lab[j] = has_lab ? static_cast<int>(lb) : -1;
+    const bool has_lab = lb >= 0 && lb < V_full;
+    // the label's column in this range (outside [0, V): never matched below)
+    lab[j] = (has_lab && lb >= vbase && lb < vbase + V) ? static_cast<int>(lb - vbase) : -1;
     glp[j] = (ok && g_logp != nullptr && has_lab) ? g_logp[r] : 0.f;
     gh[j] = (ok && g_ent != nullptr) ? g_ent[r] : 0.f;
     const float lse = ok ? lse_in[r] : 0.f;
@@ -695,29 +700,35 @@ template <bool SC, bool RD>
 static void launch_bwd_t256(bool remap, dim3 grid, hipStream_t s, const uint16_t *h16, int64_t ldh,
                             const uint16_t *w16, int64_t ldw, const int64_t *labels, const float *lse,
                             const float *ent, const float *g_logp, const float *g_ent, int64_t N, int64_t H,
-                            int64_t V, int used, int per, float temperature, uint16_t *dlog, int64_t ldd) {
+                            int64_t V, int64_t V_full, int64_t vbase, int used, int per, float temperature,
+                            uint16_t *dlog, int64_t ldd) {
   if (remap)
     hipLaunchKernelGGL((linear_logprob_bwd_t256_kernel<SC, RD, true>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16,
-                       ldw, labels, lse, ent, g_logp, g_ent, N, static_cast<int>(H), V, used, per, temperature, dlog,
-                       ldd);
+                       ldw, labels, lse, ent, g_logp, g_ent, N, static_cast<int>(H), V, V_full, vbase, used, per,
+                       temperature, dlog, ldd);
   else
     hipLaunchKernelGGL((linear_logprob_bwd_t256_kernel<SC, RD, false>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16,
-                       ldw, labels, lse, ent, g_logp, g_ent, N, static_cast<int>(H), V, used, per, temperature, dlog,
-                       ldd);
+                       ldw, labels, lse, ent, g_logp, g_ent, N, static_cast<int>(H), V, V_full, vbase, used, per,
+                       temperature, dlog, ldd);
 }
 
 extern "C" int va_linear_logprob_bwd(const void *hidden, int64_t ldh, const void *weight, int64_t ldw, int dtype,
                                      const int64_t *labels, const float *lse, const float *entropy,
                                      const float *g_logp, const float *g_entropy, int64_t N, int64_t H, int64_t V,
-                                     float temperature, int splits, void *dlogits, int64_t ldd, void *stream) {
+                                     int64_t v_begin, int64_t v_end, float temperature, int splits, void *dlogits,
+                                     int64_t ldd, void *stream) {
   const bool fp32_logits = (dtype & VA_LOGITS_F32) != 0;
   dtype &= ~VA_LOGITS_F32;
   VA_CHECK_ARG(dtype == VA_BF16, "linear_logprob_bwd: only bf16 hidden / weight are implemented");
-  VA_CHECK_ARG(N >= 0 && H > 0 && V > 0 && H % TK == 0 && H <= (1 << 20) && V % 4 == 0 && V < (int64_t{1} << 31),
-               "linear_logprob_bwd: need H %% 64 == 0 and V %% 4 == 0 (H=%lld, V=%lld)", static_cast<long long>(H),
-               static_cast<long long>(V));
-  VA_CHECK_ARG(ldh >= H && ldw >= H && ldh % 8 == 0 && ldw % 8 == 0 && ldd >= V && ldd % 4 == 0,
-               "linear_logprob_bwd: strides must be >= H (ldd >= V), %% 8 (ldd %% 4)");
+  VA_CHECK_ARG(v_begin >= 0 && v_end > v_begin && v_end <= V,
+               "linear_logprob_bwd: vocab range [%lld, %lld) must lie in [0, V=%lld)", static_cast<long long>(v_begin),
+               static_cast<long long>(v_end), static_cast<long long>(V));
+  const int64_t Vr = v_end - v_begin;  // the range's width: dlogits columns
+  VA_CHECK_ARG(N >= 0 && H > 0 && H % TK == 0 && H <= (1 << 20) && Vr % 4 == 0 && V < (int64_t{1} << 31),
+               "linear_logprob_bwd: need H %% 64 == 0 and V %% 4 == 0 over the range (H=%lld, V=%lld)",
+               static_cast<long long>(H), static_cast<long long>(Vr));
+  VA_CHECK_ARG(ldh >= H && ldw >= H && ldh % 8 == 0 && ldw % 8 == 0 && ldd >= Vr && ldd % 4 == 0,
+               "linear_logprob_bwd: strides must be >= H (ldd >= the range), %% 8 (ldd %% 4)");
   VA_CHECK_ARG(splits >= 1 && splits <= 64, "linear_logprob_bwd: splits in [1, 64]");
   VA_CHECK_ARG(temperature > 0.f, "linear_logprob_bwd: temperature must be > 0");
   if (N == 0) return VA_OK;
@@ -727,7 +738,7 @@ extern "C" int va_linear_logprob_bwd(const void *hidden, int64_t ldh, const void
                    reinterpret_cast<uintptr_t>(dlogits) % 8 == 0,
                "linear_logprob_bwd: 16-byte aligned hidden / weight and 8-byte aligned dlogits required");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const int64_t n_vt = (V + TB - 1) / TB;
+  const int64_t n_vt = (Vr + TB - 1) / TB;
   const int per = static_cast<int>((n_vt + splits - 1) / splits);
   const int used = static_cast<int>((n_vt + per - 1) / per);
   const int64_t nwg = ((N + TB - 1) / TB) * used;
@@ -735,18 +746,18 @@ extern "C" int va_linear_logprob_bwd(const void *hidden, int64_t ldh, const void
   const dim3 grid(static_cast<unsigned>(nwg));
   const bool remap = nwg % 8 == 0;
   const auto *h16 = static_cast<const uint16_t *>(hidden);
-  const auto *w16 = static_cast<const uint16_t *>(weight);
+  const auto *w16 = static_cast<const uint16_t *>(weight) + v_begin * ldw;  // the range's first weight row
   auto *d16 = static_cast<uint16_t *>(dlogits);
   if (temperature == 1.0f) {
     if (fp32_logits) launch_bwd_t256<false, false>(remap, grid, s, h16, ldh, w16, ldw, labels, lse, entropy, g_logp,
-                                                   g_entropy, N, H, V, used, per, temperature, d16, ldd);
+                                                   g_entropy, N, H, Vr, V, v_begin, used, per, temperature, d16, ldd);
     else launch_bwd_t256<false, true>(remap, grid, s, h16, ldh, w16, ldw, labels, lse, entropy, g_logp, g_entropy, N,
-                                      H, V, used, per, temperature, d16, ldd);
+                                      H, Vr, V, v_begin, used, per, temperature, d16, ldd);
   } else {
     if (fp32_logits) launch_bwd_t256<true, false>(remap, grid, s, h16, ldh, w16, ldw, labels, lse, entropy, g_logp,
-                                                  g_entropy, N, H, V, used, per, temperature, d16, ldd);
+                                                  g_entropy, N, H, Vr, V, v_begin, used, per, temperature, d16, ldd);
     else launch_bwd_t256<true, true>(remap, grid, s, h16, ldh, w16, ldw, labels, lse, entropy, g_logp, g_entropy, N,
-                                     H, V, used, per, temperature, d16, ldd);
+                                     H, Vr, V, v_begin, used, per, temperature, d16, ldd);
   }
   return check_launch("linear_logprob_bwd");
 }

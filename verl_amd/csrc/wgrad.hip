@@ -276,13 +276,15 @@ int64_t w_part_bytes(const WPart &p) {
 }
 
 template <int TM, int TN, int NST>
-void w_launch(const WPart &p, const uint16_t *dy, int64_t ldy, const uint16_t *x, int64_t ldx, int64_t K,
+int w_launch(const WPart &p, const uint16_t *dy, int64_t ldy, const uint16_t *x, int64_t ldx, int64_t K,
               float *ws, uint16_t *out, int64_t ldo, hipStream_t st) {
   const int64_t steps = K / WBK;
   const int64_t kslice = (steps + p.splits - 1) / p.splits * WBK;
   const int64_t nwg = ((p.M + TM - 1) / TM) * ((p.N + TN - 1) / TN) * p.splits;
   const uint16_t *dyp = dy + p.m0, *xp = x + p.n0;  // column offsets of the operands
   uint16_t *op = out + p.m0 * ldo + p.n0;
+  VA_CHECK_ARG(nwg < (int64_t{1} << 31) && (p.M * p.N / 4 + 255) / 256 < (int64_t{1} << 31),
+               "weight_grad: grid too large (%lld workgroups)", static_cast<long long>(nwg));
   if (p.splits == 1) {
     hipLaunchKernelGGL((wgrad_kernel<false, TM, TN, NST>), dim3(static_cast<unsigned>(nwg)), dim3(WNT), 0, st, dyp,
                        ldy, xp, ldx, K, static_cast<int>(p.M), static_cast<int>(p.N), 1, kslice, nullptr, op, ldo);
@@ -293,6 +295,15 @@ void w_launch(const WPart &p, const uint16_t *dy, int64_t ldy, const uint16_t *x
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(static_cast<unsigned>((p.M * p.N / 4 + 255) / 256)), dim3(256), 0,
                        st, ws, p.splits, p.M, p.N, op, ldo);
   }
+  return VA_OK;
+}
+
+// The launches of one weight gradient under one reading of the remainder setting (the size query
+// and the launch each plan once; the launch checks its plan against the caller's buffer size)
+int w_plan_all(int64_t K, int64_t M, int64_t N, int splits, int remainder, WPart (&p)[2]) {
+  if (remainder) return w_plan(K, M, N, splits, p);
+  p[0] = WPart{0, 0, 0, M, N, splits > 0 ? splits : w_auto_splits(((M + 255) / 256) * ((N + 255) / 256), K / WBK)};
+  return 1;
 }
 
 }  // namespace
@@ -305,15 +316,14 @@ int g_wgrad_remainder = 0;
 
 extern "C" int64_t va_weight_grad_workspace_bytes(int64_t K, int64_t M, int64_t N, int splits) {
   WPart p[2];
-  const int n = g_wgrad_remainder ? w_plan(K, M, N, splits, p) : (p[0] = WPart{0, 0, 0, M, N, 0}, 1);
-  if (!g_wgrad_remainder) p[0].splits = splits > 0 ? splits : w_auto_splits(((M + 255) / 256) * ((N + 255) / 256), K / WBK);
+  const int n = w_plan_all(K, M, N, splits, g_wgrad_remainder, p);
   int64_t b = 0;
   for (int i = 0; i < n; ++i) b += w_part_bytes(p[i]);
   return b;
 }
 
 extern "C" int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_t ldx, int64_t K, int64_t M, int64_t N,
-                              int splits, float *workspace, void *out, void *stream) {
+                              int splits, float *workspace, int64_t workspace_bytes, void *out, void *stream) {
   VA_CHECK_ARG(K >= 0 && K % WBK == 0, "weight_grad: K (tokens) must be a multiple of 32 (K=%lld)",
                static_cast<long long>(K));
   VA_CHECK_ARG(M >= 8 && N >= 8 && M % 8 == 0 && N % 8 == 0 && M < (1 << 30) && N < (1 << 30),
@@ -329,16 +339,12 @@ extern "C" int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_
     return VA_OK;
   }
   WPart p[2];
-  int n;
-  if (g_wgrad_remainder) {
-    n = w_plan(K, M, N, splits, p);
-  } else {
-    n = 1;
-    p[0] = WPart{0, 0, 0, M, N, splits > 0 ? splits : w_auto_splits(((M + 255) / 256) * ((N + 255) / 256), K / WBK)};
-  }
-  bool need_ws = false;
-  for (int i = 0; i < n; ++i) need_ws |= p[i].splits > 1;
-  VA_CHECK_ARG(dy && x && (!need_ws || workspace), "null pointer argument");
+  const int n = w_plan_all(K, M, N, splits, g_wgrad_remainder, p);
+  int64_t need = 0;
+  for (int i = 0; i < n; ++i) need += w_part_bytes(p[i]);
+  VA_CHECK_ARG(dy && x && (need == 0 || workspace), "null pointer argument");
+  VA_CHECK_ARG(need <= workspace_bytes, "weight_grad: the plan needs %lld workspace bytes, %lld given",
+               static_cast<long long>(need), static_cast<long long>(workspace_bytes));
   VA_CHECK_ARG(((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) &
                 15) == 0,
                "weight_grad: 16-byte aligned buffers required");
@@ -347,9 +353,11 @@ extern "C" int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_
   auto *o16 = static_cast<uint16_t *>(out);
   float *ws = workspace;
   for (int i = 0; i < n; ++i) {
-    if (p[i].kind == 0) w_launch<256, 256, 4>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
-    else if (p[i].kind == 1) w_launch<512, 128, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
-    else w_launch<128, 512, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+    int rc;
+    if (p[i].kind == 0) rc = w_launch<256, 256, 4>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+    else if (p[i].kind == 1) rc = w_launch<512, 128, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+    else rc = w_launch<128, 512, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+    if (rc != VA_OK) return rc;
     ws += w_part_bytes(p[i]) / static_cast<int64_t>(sizeof(float));
   }
   return check_launch("weight_grad");

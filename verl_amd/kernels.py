@@ -161,19 +161,21 @@ def logprob_entropy(logits, labels, temperature: float = 1.0, inplace_backward=F
 
 
 # =============================================================================== fused lm_head + log-prob
-def _linear_logprob_splits(n_rows: int) -> int:
+def _linear_logprob_splits(n_rows: int, vocab: int | None = None) -> int:
     """Vocab ranges per row block. The 256-row kernel (default): ~4,096 workgroups (16 per CU, which
     the XCD remap turns into 32 resident (row block, range) pairs per XCD: 4 hidden panels x 8
     ranges at 131,072 rows; tools/f1t_bench.py, removed in round 4 — git show 690aed1:tools/f1t_bench.py: 4 or 8 ranges 33.9 ms, 16: 34.3); the 128-row
-    kernel: ~1,024 workgroups."""
+    kernel: ~1,024 workgroups. ``vocab``: at most one range per 256-wide vocab tile."""
     env = os.environ.get("VERL_AMD_LINEAR_LOGPROB_SPLITS")
     if env:
-        return int(env)
-    if L.TUNING.get(L.VA_TUNE_LINEAR_LOGPROB_TILE, 256) == 256:
+        s = int(env)
+    elif L.TUNING.get(L.VA_TUNE_LINEAR_LOGPROB_TILE, 256) == 256:
         blocks = max(1, (n_rows + 255) // 256)
-        return int(min(64, max(1, -(-4096 // blocks))))
-    blocks = max(1, (n_rows + 127) // 128)
-    return int(min(64, max(1, -(-1024 // blocks))))
+        s = int(min(64, max(1, -(-4096 // blocks))))
+    else:
+        blocks = max(1, (n_rows + 127) // 128)
+        s = int(min(64, max(1, -(-1024 // blocks))))
+    return s if vocab is None else max(1, min(s, -(-vocab // 256)))
 
 
 def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float, fp32_logits: bool = False):
@@ -195,33 +197,40 @@ def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float, fp32_log
 
 
 def _linear_logprob_bwd_raw(hidden, weight, labels, lse, ent, g1, g2, temperature: float, fp32_logits: bool,
-                            dlogits):
-    """dlogits [n, V] bf16 of the rows of ``hidden`` by va_linear_logprob_bwd (no logits in HBM)."""
+                            dlogits, v_begin: int = 0, v_end: int | None = None):
+    """dlogits [n, v_end - v_begin] bf16 of the rows of ``hidden`` over the vocab range [v_begin,
+    v_end) (default: all of it) by va_linear_logprob_bwd (no logits in HBM)."""
     N, H = hidden.shape
     V = weight.shape[0]
+    v_end = V if v_end is None else int(v_end)
     ev = TIMER.start(torch.cuda.current_stream(hidden.device)) if TIMER is not None else None
     dtype = L.VA_BF16 | (L.VA_LOGITS_F32 if fp32_logits else 0)
     L.call("va_linear_logprob_bwd", _p(hidden), hidden.stride(0), _p(weight), weight.stride(0), dtype, _p(labels),
-           _p(lse), _p(ent), _p(g1), _p(g2), N, H, V, float(temperature), _linear_logprob_splits(N), _p(dlogits),
-           dlogits.stride(0), _stream(hidden))
-    if ev is not None:  # MFMA-bound: the logits recompute, 2 N V H flops (+ 2 B per logit written)
-        TIMER.stop("linear_logprob_bwd", 2 * N * V * H, torch.cuda.current_stream(hidden.device), ev)
+           _p(lse), _p(ent), _p(g1), _p(g2), N, H, V, int(v_begin), v_end, float(temperature),
+           _linear_logprob_splits(N, v_end - v_begin), _p(dlogits), dlogits.stride(0), _stream(hidden))
+    if ev is not None:  # MFMA-bound: the logits recompute, 2 N Vr H flops (+ 2 B per logit written)
+        TIMER.stop("linear_logprob_bwd", 2 * N * (v_end - v_begin) * H, torch.cuda.current_stream(hidden.device), ev)
 
 
 class _LinearLogprob(torch.autograd.Function):
-    """Forward: one fused MFMA pass (no logits in HBM). Backward, per row chunk: the fused MFMA
-    kernel va_linear_logprob_bwd recomputes the logits tile by tile and writes bf16 dlogits (the
-    reference's d_logits_split_N kernel, kernels.py:1241-1342), then the lm_head's two GEMMs run on
-    them. ``VERL_AMD_F1_BWD=compose`` keeps the previous composition (hipBLASLt recompute of the
-    logits + va_logprob_entropy_bwd in place) for A/B runs.
-    fp32_logits: the logits stay fp32 (no bf16 rounding) in both passes, as in the reference's
-    fused kernel; dlogits are rounded to bf16 for the two GEMMs, as its backward's tl.dot inputs."""
+    """Forward: one fused MFMA pass (no logits in HBM). Backward: the reference's default
+    _Split_Dlogits_N (utils/kernel/kernels.py:1491-1548) — per vocab range of VOCAB_PER_SPLIT
+    columns, the fused MFMA kernel va_linear_logprob_bwd recomputes that range's logits tile by tile
+    and writes its bf16 dlogits [N, range] (kernels.py:1241-1342), then d_hidden += dlogits_s W_s
+    (fp32 accumulation) and d_weight[s] = dlogits_s^T hidden: no [N, V] buffer exists in either
+    pass. ``VERL_AMD_F1_BWD=compose`` (and a vocabulary not a multiple of 4) runs the previous
+    composition instead, in row chunks: hipBLASLt recompute of the logits + va_logprob_entropy_bwd
+    in place. fp32_logits: the logits stay fp32 (no bf16 rounding) in both passes, as in the
+    reference's fused kernel; dlogits are rounded to bf16 for the two GEMMs, as its backward's
+    tl.dot inputs."""
 
-    # bytes of the per-chunk dlogits buffer (bf16 [rows, V]; the fused path holds no logits, so
-    # this is its whole [rows, V] footprint): by default the bench's 131,072-row pass is ONE chunk,
-    # so the lm_head GEMMs run at full size; a chunk the allocator cannot provide is halved until it
-    # fits (env VERL_AMD_F1_BWD_CHUNK_MB)
-    CHUNK_BYTES = int(os.environ.get("VERL_AMD_F1_BWD_CHUNK_MB", "49152")) << 20
+    # vocab columns per range of the fused backward (the reference's vocab_per_split, 9504: 16
+    # ranges at V = 151,936, a 2.5 GB bf16 range at the bench's 131,072 rows); a range the allocator
+    # cannot provide is halved until it fits (env VERL_AMD_F1_BWD_VOCAB_SPLIT)
+    VOCAB_PER_SPLIT = int(os.environ.get("VERL_AMD_F1_BWD_VOCAB_SPLIT", "9504"))
+    # bytes of the compose path's per-chunk logits buffer ([rows, V] in the logits dtype; ADVICE r4:
+    # the pre-round-4 2 GiB, env VERL_AMD_F1_BWD_CHUNK_MB)
+    COMPOSE_CHUNK_BYTES = int(os.environ.get("VERL_AMD_F1_BWD_CHUNK_MB", "2048")) << 20
 
     @staticmethod
     def forward(ctx, hidden, weight, labels, temperature, fp32_logits):
@@ -232,51 +241,63 @@ class _LinearLogprob(torch.autograd.Function):
         return logp, ent
 
     @staticmethod
-    def _chunk_buffer(rows: int, V: int, dtype, device):
+    def _range_buffer(N: int, width: int, dtype, device):
+        """[N, width] dlogits buffer, width halved (in multiples of 8) until the allocator has it."""
         while True:
             try:
-                return torch.empty(rows, V, dtype=dtype, device=device), rows
+                return torch.empty(N, width, dtype=dtype, device=device), width
             except torch.OutOfMemoryError:
-                if rows <= 256:
+                if width <= 256:
                     raise
-                rows = max(256, rows // 2)
+                width = max(256, width // 2 // 8 * 8)
 
     @staticmethod
-    def backward(ctx, g_logp, g_ent):
-        hidden, weight, labels, lse, ent = ctx.saved_tensors
+    def _vocab_split_backward(ctx, hidden, weight, labels, lse, ent, g1, g2):
         N, H = hidden.shape
         V = weight.shape[0]
-        g1 = None if g_logp is None else _f32(g_logp)
-        g2 = None if g_ent is None else _f32(g_ent)
-        d_hidden = d_weight = None
+        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        width = min(V, max(256, _LinearLogprob.VOCAB_PER_SPLIT // 8 * 8))
+        buf, width = _LinearLogprob._range_buffer(N, width, hidden.dtype, hidden.device)
+        # dX over a transposed copy of W ("TN", as input_grad); each range is a column slice of it
+        wt = transpose16(weight) if need_h and _DGRAD_TN and weight.dtype == torch.bfloat16 else None
+        dh32 = None
+        d_weight = torch.empty_like(weight) if need_w else None
+        for v0 in range(0, V, width):
+            v1 = min(V, v0 + width)
+            dlog = buf[:, : v1 - v0]
+            _linear_logprob_bwd_raw(hidden, weight, labels, lse, ent, g1, g2, ctx.temperature, ctx.fp32_logits, dlog,
+                                    v0, v1)
+            if need_h:
+                w_s = wt[:, v0:v1].t() if wt is not None else weight[v0:v1]
+                if dh32 is None:
+                    dh32 = torch.mm(dlog, w_s, out_dtype=torch.float32)
+                else:
+                    torch.addmm(dh32, dlog, w_s, out_dtype=torch.float32, out=dh32)
+            if need_w:
+                d_weight[v0:v1].copy_(weight_grad(dlog, hidden))
+        return (dh32.to(hidden.dtype) if need_h else None), d_weight
+
+    @staticmethod
+    def _compose_backward(ctx, hidden, weight, labels, lse, ent, g1, g2):
+        N, H = hidden.shape
+        V = weight.shape[0]
         f32 = ctx.fp32_logits
-        fused = os.environ.get("VERL_AMD_F1_BWD", "fused") != "compose" and V % 4 == 0
-        width = 2 if fused else (4 if f32 else hidden.element_size())
-        rows = min(N, max(256, int(_LinearLogprob.CHUNK_BYTES // (V * width))))
-        # the lm_head's two backward GEMMs as the unfused actor runs them: dX over a transposed copy of
-        # W ("TN", input_grad) and dW as the swapped product (weight_grad)
-        wt = (transpose16(weight) if ctx.needs_input_grad[0] and _DGRAD_TN and weight.dtype == torch.bfloat16
-              else None)
-        r0 = 0
-        while r0 < N:
-            if fused:
-                dlog, rows = _LinearLogprob._chunk_buffer(min(rows, N - r0), V, hidden.dtype, hidden.device)
+        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        width = 4 if f32 else hidden.element_size()
+        rows = min(N, max(256, int(_LinearLogprob.COMPOSE_CHUNK_BYTES // (V * width))))
+        wt = transpose16(weight) if need_h and _DGRAD_TN and weight.dtype == torch.bfloat16 else None
+        d_hidden = d_weight = None
+        for r0 in range(0, N, rows):
             r1 = min(N, r0 + rows)
             h = hidden[r0:r1]
-            if fused:
-                dlog = dlog[: r1 - r0]
-                _linear_logprob_bwd_raw(h, weight, labels[r0:r1], lse[r0:r1], ent[r0:r1],
-                                        g1[r0:r1] if g1 is not None else None, g2[r0:r1] if g2 is not None else None,
-                                        ctx.temperature, f32, dlog)
-            else:
-                dlog = torch.mm(h, weight.t(), out_dtype=torch.float32) if f32 else h @ weight.t()
-                L.call("va_logprob_entropy_bwd", _p(g1[r0:r1] if g1 is not None else None),
-                       _p(g2[r0:r1] if g2 is not None else None), _p(dlog), L.VA_F32 if f32 else L.VA_BF16, r1 - r0,
-                       V, dlog.stride(0), _p(labels[r0:r1]), _p(lse[r0:r1]), _p(ent[r0:r1]), ctx.temperature,
-                       _p(dlog), dlog.stride(0), _stream(dlog))
-                if f32:
-                    dlog = dlog.to(hidden.dtype)
-            if ctx.needs_input_grad[0]:
+            dlog = torch.mm(h, weight.t(), out_dtype=torch.float32) if f32 else h @ weight.t()
+            L.call("va_logprob_entropy_bwd", _p(g1[r0:r1] if g1 is not None else None),
+                   _p(g2[r0:r1] if g2 is not None else None), _p(dlog), L.VA_F32 if f32 else L.VA_BF16, r1 - r0,
+                   V, dlog.stride(0), _p(labels[r0:r1]), _p(lse[r0:r1]), _p(ent[r0:r1]), ctx.temperature,
+                   _p(dlog), dlog.stride(0), _stream(dlog))
+            if f32:
+                dlog = dlog.to(hidden.dtype)
+            if need_h:
                 dh = torch.nn.functional.linear(dlog, wt) if wt is not None else dlog @ weight
                 if r0 == 0 and r1 == N:
                     d_hidden = dh
@@ -285,16 +306,33 @@ class _LinearLogprob(torch.autograd.Function):
                         d_hidden = torch.empty_like(hidden)
                     d_hidden[r0:r1].copy_(dh)
                 del dh
-            if ctx.needs_input_grad[1]:
+            if need_w:
                 dw = weight_grad(dlog, h)
                 if r0 == 0 and r1 == N:
                     d_weight = dw
                 else:
                     d_weight = dw.float() if d_weight is None else d_weight.add_(dw.float())
             del dlog
-            r0 = r1
         if d_weight is not None:
             d_weight = d_weight.to(weight.dtype)
+        return d_hidden, d_weight
+
+    @staticmethod
+    def backward(ctx, g_logp, g_ent):
+        hidden, weight, labels, lse, ent = ctx.saved_tensors
+        N = hidden.shape[0]
+        V = weight.shape[0]
+        need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if N == 0:
+            # zero gradients rather than None: a DP rank's lm_head gradient hook must
+            # still fire so that its all-reduce bucket becomes ready
+            return (torch.zeros_like(hidden) if need_h else None, torch.zeros_like(weight) if need_w else None,
+                    None, None, None)
+        g1 = None if g_logp is None else _f32(g_logp)
+        g2 = None if g_ent is None else _f32(g_ent)
+        fused = os.environ.get("VERL_AMD_F1_BWD", "fused") != "compose" and V % 4 == 0
+        run = _LinearLogprob._vocab_split_backward if fused else _LinearLogprob._compose_backward
+        d_hidden, d_weight = run(ctx, hidden, weight, labels, lse, ent, g1, g2)
         return d_hidden, d_weight, None, None, None
 
 
@@ -842,7 +880,7 @@ def _own_weight_grad(dy2, x2):
     out = torch.empty(n_out, n_in, dtype=torch.bfloat16, device=dy2.device)
     nb = L.load().va_weight_grad_workspace_bytes(T, n_out, n_in, s)
     ws = torch.empty(nb // 4, dtype=torch.float32, device=dy2.device) if nb else None
-    L.call("va_weight_grad", _p(dy2), dy2.stride(0), _p(x2), x2.stride(0), T, n_out, n_in, s, _p(ws), _p(out),
+    L.call("va_weight_grad", _p(dy2), dy2.stride(0), _p(x2), x2.stride(0), T, n_out, n_in, s, _p(ws), nb, _p(out),
            _stream(dy2))
     return out
 

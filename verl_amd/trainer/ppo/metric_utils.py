@@ -38,7 +38,8 @@ def _compute_response_info(batch: DataProto) -> dict[str, Any]:
 
 
 class _Stats:
-    """Named per-rank partial statistics merged in two all-reduces (SUM, MAX)."""
+    """Named per-rank partial statistics merged in all-reduces (SUM, MAX; then one SUM of the
+    second moments about the merged means)."""
 
     def __init__(self, device):
         self.device = device
@@ -46,6 +47,7 @@ class _Stats:
         self.maxs: list[torch.Tensor] = []
         self.sum_idx: dict[str, int] = {}
         self.max_idx: dict[str, int] = {}
+        self.moments: list[tuple[str, torch.Tensor]] = []
 
     def _f64(self, v):
         return v.to(torch.float64).reshape(()) if isinstance(v, torch.Tensor) else \
@@ -69,22 +71,37 @@ class _Stats:
         self.maxs.append((-lo).to(self.device))
 
     def add_moments(self, name, x: torch.Tensor):
-        """count, sum, sum of squares (fp64) and extrema of x."""
+        """count, sum and extrema of x (fp64); its second moment about the merged mean is formed
+        in reduce() (M2 = sum (x - mean)^2, not sumsq - n mean^2: no cancellation when the mean
+        is large against the spread)."""
         x = x.to(torch.float64).reshape(-1)
         self.add_sum(name + "/n", x.numel())
         self.add_sum(name + "/sum", x.sum())
-        self.add_sum(name + "/sumsq", (x * x).sum())
+        self.moments.append((name, x))
         self.add_extrema(name, x)
 
     def reduce(self, group=None) -> tuple[dict, dict]:
         dev = comm.comm_device(group) if comm.world(group) > 1 else self.device
+        multi = comm.world(group) > 1
         s = torch.stack(self.sums).to(dev) if self.sums else torch.zeros(0, dtype=torch.float64, device=dev)
         m = torch.stack(self.maxs).to(dev) if self.maxs else torch.zeros(0, dtype=torch.float64, device=dev)
-        if comm.world(group) > 1:
+        if multi:
             comm.all_reduce(s, group=group)
             comm.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
-        host = torch.cat([s, m]).cpu().tolist()  # the one device->host copy
+        # second moments about the batch-global means (still on the device: no host round trip)
+        m2 = []
+        for name, x in self.moments:
+            n = s[self.sum_idx[name + "/n"]]
+            mu = s[self.sum_idx[name + "/sum"]] / n.clamp_min(1)
+            m2.append(((x.to(dev) - mu) ** 2).sum())
+        m2 = torch.stack(m2) if m2 else torch.zeros(0, dtype=torch.float64, device=dev)
+        if multi and m2.numel():
+            comm.all_reduce(m2, group=group)
+        host = torch.cat([s, m, m2]).cpu().tolist()  # the one device->host copy
         sums = {k: host[i] for k, i in self.sum_idx.items()}
+        base = len(self.sums) + len(self.maxs)
+        for j, (name, _) in enumerate(self.moments):
+            sums[name + "/m2"] = host[base + j]
         ext = {}
         for k, i in self.max_idx.items():
             v = host[len(self.sums) + i]
@@ -98,12 +115,11 @@ def _mean(s, name):
 
 
 def _var(s, name):
-    """torch.var (unbiased) from the merged count / sum / sum of squares."""
+    """torch.var (unbiased) from the merged count and second moment about the merged mean."""
     n = s[name + "/n"]
     if n < 2:
         return float("nan")
-    mu = s[name + "/sum"] / n
-    return max(s[name + "/sumsq"] - n * mu * mu, 0.0) / (n - 1)
+    return s[name + "/m2"] / (n - 1)
 
 
 def compute_data_metrics(batch: DataProto, use_critic: bool = True, group=None) -> dict[str, Any]:
