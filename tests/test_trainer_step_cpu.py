@@ -153,3 +153,50 @@ def test_attention_mask_host_copy_reuse_and_invalidation():
     a3 = DataParallelPPOActor._mask_host(me, other, refresh=False)
     assert a3 is not a2 and a3.sum() == 0
     assert DataParallelPPOActor._mask_host(me, other, refresh=True) is not a3  # refresh copies
+
+
+def test_attention_mask_host_mirror_is_used_until_either_tensor_is_written():
+    """DataProto.to(cuda) keeps the host tensor the mask came from (protocol.HOST_MIRRORED_KEY);
+    _mask_host plans from it instead of a device->host copy, but not once either side was
+    written in place (emulated here on host tensors: the mirror attribute is what .to sets)."""
+    from types import SimpleNamespace
+
+    from verl_amd.workers.actor.dp_actor import DataParallelPPOActor
+
+    me = SimpleNamespace(_am_cache=None)
+    src = torch.ones(3, 5, dtype=torch.int64)
+    dev = torch.ones(3, 5, dtype=torch.int64)  # stands in for the device copy
+    dev._va_host_mirror = (src, src._version, dev._version)
+    src_np = src.numpy()
+    got = DataParallelPPOActor._mask_host(me, dev)
+    assert np.shares_memory(got, src_np)  # the mirror itself, no copy
+    me._am_cache = None
+    dev[0, 0] = 0  # the device side changed: the mirror is stale
+    got = DataParallelPPOActor._mask_host(me, dev)
+    assert not np.shares_memory(got, src_np) and got[0, 0] == 0
+    me._am_cache = None
+    dev2 = torch.ones(3, 5, dtype=torch.int64)
+    dev2._va_host_mirror = (src, src._version, dev2._version)
+    src[1, 1] = 0  # the host side changed after the move
+    got = DataParallelPPOActor._mask_host(me, dev2)
+    assert not np.shares_memory(got, src.numpy()) and got[1, 1] == 1
+
+
+def test_device_metrics_mapping_and_callbacks(capsys):
+    """dp_actor.DeviceMetrics (the update's metrics, read back asynchronously): tensor and host
+    values in list order, scalars kept, keys set before the first read kept, on_ready callbacks
+    run once after the values are in, and the non-finite grad_norm warning."""
+    from verl_amd.workers.actor.dp_actor import DeviceMetrics
+
+    m = DeviceMetrics({"actor/pg_loss": [torch.tensor(0.5), 0.25, torch.tensor([1.5])],
+                       "actor/grad_norm": [torch.tensor(float("inf"))], "actor/kl_coef": [0.001], "perf/x": 3.0})
+    m["actor/lr"] = 1e-6
+    seen = []
+    m.add_on_ready(lambda mm: seen.append(mm["actor/pg_loss"][0]))
+    m.add_on_ready(lambda mm: mm.__setitem__("perf/mfu/actor", 0.4))
+    assert m["actor/pg_loss"] == [0.5, 0.25, 1.5] and m["perf/x"] == 3.0 and m["actor/lr"] == 1e-6
+    assert seen == [0.5] and m["perf/mfu/actor"] == 0.4
+    assert set(m) == {"actor/pg_loss", "actor/grad_norm", "actor/kl_coef", "perf/x", "actor/lr", "perf/mfu/actor"}
+    assert "not finite" in capsys.readouterr().out
+    m.add_on_ready(lambda mm: seen.append(1))  # already resolved: runs at once
+    assert seen == [0.5, 1] and dict(m)["actor/kl_coef"] == [0.001]

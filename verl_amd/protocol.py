@@ -26,6 +26,10 @@ __all__ = ["DataProto", "DataProtoItem", "TensorBatch", "union_tensor_dict", "pa
            "unpad_dataproto", "DataProtoConfig", "collate_fn"]
 
 
+
+# DataProto.to(cuda) of a host batch keeps the host tensor of this key next to the device one
+HOST_MIRRORED_KEY = "attention_mask"
+
 class _TypedSwitches(type):
     """Class-level boolean switches: ``DataProtoConfig.auto_padding = True`` is type-checked on
     assignment (the reference's metaclass property, protocol.py:33-45; same message)."""
@@ -319,8 +323,15 @@ class DataProto:
     # ------------------------------------------------------------------ moves and views
     def to(self, device, non_blocking: bool = False) -> "DataProto":
         if self.batch is not None:
-            self.batch = TensorBatch({k: v.to(device, non_blocking=non_blocking) for k, v in self.batch.items()},
-                                     batch_size=self.batch.batch_size)
+            moved = {}
+            for k, v in self.batch.items():
+                t = v.to(device, non_blocking=non_blocking)
+                if k == HOST_MIRRORED_KEY and t is not v and v.device.type == "cpu" and t.is_cuda:
+                    # the host copy the mask arrived with: the actor plans padding removal from it
+                    # instead of a device->host copy that would drain the stream (dp_actor._mask_host)
+                    t._va_host_mirror = (v, v._version, t._version)
+                moved[k] = t
+            self.batch = TensorBatch(moved, batch_size=self.batch.batch_size)
         return self
 
     def select(self, batch_keys=None, non_tensor_batch_keys=None, meta_info_keys=None, deepcopy=False) -> "DataProto":

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import logging
 import os
+from collections.abc import MutableMapping
 from dataclasses import dataclass
 
 import numpy as np
@@ -405,24 +406,33 @@ class DataParallelPPOActor(BasePPOActor):
             return False
         return bool(self.use_fused_kernels or (self.fused_logprob_no_grad and not torch.is_grad_enabled()))
 
-    def _mask_host(self, am_t: torch.Tensor, refresh: bool) -> np.ndarray:
-        """Host copy of the attention mask. compute_log_prob (the step's first pass over the
-        batch) always copies it (refresh=True: the GPU is idle there anyway); update_policy reuses
-        that copy while the tensor is the same unmodified one (same storage, shape and version):
-        a second D2H copy at the start of the update would drain the queued old-logp pass and
-        advantage work and leave the GPU idle while the host plans the update.
+    def _mask_host(self, am_t: torch.Tensor, refresh: bool = False) -> np.ndarray:
+        """Host copy of the attention mask, which plans padding removal. A device->host copy drains
+        the stream: at the start of a step it would leave the GPU idle while the host plans, and at
+        the start of the update it would wait for the queued old-logp pass and advantage work. So,
+        in this order:
+          * the host tensor the mask arrived with (DataProto.to of a host batch keeps it,
+            protocol.HOST_MIRRORED_KEY), while neither tensor has been written since;
+          * the copy taken last, while the tensor is the same unmodified one (same storage, shape
+            and in-place version: the step's compute_log_prob and update_policy, or the same batch
+            again);
+          * else one device->host copy (also with ``refresh``).
 
-        Contract: the attention mask must not change between compute_log_prob and update_policy
-        of one step other than through ordinary in-place tensor writes (which bump the version);
-        writes through ``.data`` or through another tensor sharing the storage are not seen and
-        would leave the update planned from the stale copy. The step driver
-        (trainer_step.PPOTrainerStep) never writes the mask."""
+        Contract: the mask must not change other than through ordinary in-place tensor writes
+        (which bump the version); writes through ``.data`` or through another tensor sharing the
+        storage are not seen and would leave the passes planned from the stale copy. The step
+        driver (trainer_step.PPOTrainerStep) never writes the mask."""
         # the cache holds the device tensor itself, so its storage cannot be freed and reused by
         # another batch's mask while the key (pointer, shape, in-place version) is compared
         key = (am_t.data_ptr(), tuple(am_t.shape), am_t._version, am_t.device)
         if not refresh and self._am_cache is not None and self._am_cache[0] == key:
             return self._am_cache[2]
-        am = am_t.cpu().numpy()
+        mirror = getattr(am_t, "_va_host_mirror", None)
+        if (not refresh and mirror is not None and mirror[0]._version == mirror[1] and am_t._version == mirror[2]
+                and tuple(mirror[0].shape) == tuple(am_t.shape)):
+            am = mirror[0].numpy()
+        else:
+            am = am_t.cpu().numpy()
         self._am_cache = (key, am_t, am)
         return am
 
@@ -478,7 +488,7 @@ class DataParallelPPOActor(BasePPOActor):
         has_mm = "multi_modal_inputs" in data.non_tensor_batch.keys()
         data = data.select(batch_keys=["responses", "input_ids", "attention_mask", "position_ids"],
                            non_tensor_batch_keys=["multi_modal_inputs"] if has_mm else [])
-        am = self._mask_host(data.batch["attention_mask"], refresh=True) if self.use_remove_padding else None
+        am = self._mask_host(data.batch["attention_mask"]) if self.use_remove_padding else None
         if use_dynamic_bsz:
             # dp_actor.py:321-323: micro-batches cut by a token budget, restored afterwards
             max_token_len = data.meta_info["max_token_len"] * self.ulysses_sequence_parallel_size
@@ -513,7 +523,7 @@ class DataParallelPPOActor(BasePPOActor):
             keys.append("ref_log_prob")
         has_mm = "multi_modal_inputs" in data.non_tensor_batch.keys()
         data = data.select(batch_keys=keys, non_tensor_batch_keys=["multi_modal_inputs"] if has_mm else [])
-        am_full = self._mask_host(data.batch["attention_mask"], refresh=False) if self.use_remove_padding else None
+        am_full = self._mask_host(data.batch["attention_mask"]) if self.use_remove_padding else None
         mini_batches = data.split(cfg.ppo_mini_batch_size)
         if not cfg.use_dynamic_bsz:
             self.gradient_accumulation = cfg.ppo_mini_batch_size // cfg.ppo_micro_batch_size_per_gpu
@@ -673,29 +683,96 @@ def step_unless_nonfinite(optimizer, grad_norm: torch.Tensor, zero_grad, after_s
     return grad_norm
 
 
-def _to_host(dev_metrics: dict) -> dict:
-    """One device->host transfer for every metric of the update (the reference calls .item()
-    per micro-batch, dp_actor.py:462-483); host values (e.g. kl_coef) never go to the device."""
-    dev_keys, dev_vals, out_pos = [], [], []
-    out: dict[str, list] = {}
-    for k, lst in dev_metrics.items():
-        dst = out.setdefault(k, [])
-        for v in lst:
-            if isinstance(v, torch.Tensor):
-                dev_keys.append(k)
-                out_pos.append(len(dst))
-                dev_vals.append(v.detach().float().reshape(()))
-                dst.append(None)
-            else:
-                dst.append(float(v))
-    if dev_vals:
-        devs = {v.device for v in dev_vals}
-        flat = torch.stack([v.to(dev_vals[0].device) for v in dev_vals]).cpu().tolist() if len(devs) == 1 else \
-            [float(v.cpu()) for v in dev_vals]
-        for k, i, v in zip(dev_keys, out_pos, flat, strict=True):
-            out[k][i] = v
-    for k, lst in out.items():
-        if k.endswith("grad_norm") and not all(np.isfinite(g) for g in lst):
-            rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
-            print(f"WARN: rank {rank} {k} is not finite: {lst} (optimizer step skipped)")
-    return out
+class DeviceMetrics(MutableMapping):
+    """The metric lists of one update, read back without blocking the host (the reference calls
+    .item() per micro-batch, dp_actor.py:462-483, a host sync each): every device value goes into
+    ONE pinned host buffer by an asynchronous copy at the end of the update, and the first read
+    waits for that copy's event. Until then the host runs on — into the next step's planning
+    while the GPU finishes the optimizer step — so the GPU is not left idle at the step boundary.
+    Host values (e.g. kl_coef) never go to the device. Keys set before the first read are kept;
+    ``on_ready`` callbacks (e.g. the update's MFU from its device time) run once, after the copy."""
+
+    def __init__(self, dev_metrics: dict, on_ready=()):
+        dev_keys, dev_vals, out_pos = [], [], []
+        out: dict[str, list] = {}
+        for k, lst in dev_metrics.items():
+            if not isinstance(lst, (list, tuple)):  # a scalar entry stays as it is
+                out[k] = lst.item() if isinstance(lst, torch.Tensor) else lst
+                continue
+            dst = out.setdefault(k, [])
+            for v in lst:
+                if isinstance(v, torch.Tensor):
+                    dev_keys.append(k)
+                    out_pos.append(len(dst))
+                    dev_vals.append(v.detach().float().reshape(()))
+                    dst.append(None)
+                else:
+                    dst.append(float(v))
+        self._data = out
+        self._slots = list(zip(dev_keys, out_pos, strict=True))
+        self._host = self._event = None
+        self._on_ready = list(on_ready)
+        if dev_vals:
+            devs = {v.device for v in dev_vals}
+            if len(devs) == 1 and dev_vals[0].is_cuda:
+                flat = torch.stack(dev_vals)
+                self._host = torch.empty(flat.shape, dtype=flat.dtype, pin_memory=True)
+                self._host.copy_(flat, non_blocking=True)
+                self._event = torch.cuda.Event()
+                self._event.record(torch.cuda.current_stream(flat.device))
+            else:  # host tensors, or several devices: read now
+                self._host = torch.stack([v.cpu() for v in dev_vals])
+        if self._host is None:
+            self._finish()
+
+    def add_on_ready(self, fn):
+        """Run ``fn(self)`` once the device values are in (now, if they already are)."""
+        if self._slots is None:
+            fn(self)
+        else:
+            self._on_ready.append(fn)
+
+    def _finish(self):
+        if self._slots is None:
+            return
+        if self._event is not None:
+            self._event.synchronize()
+        if self._host is not None:
+            for (k, i), v in zip(self._slots, self._host.tolist(), strict=True):
+                self._data[k][i] = v
+        self._slots, self._host, self._event = None, None, None
+        for k, lst in self._data.items():
+            if k.endswith("grad_norm") and isinstance(lst, list) and not all(np.isfinite(g) for g in lst):
+                rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+                print(f"WARN: rank {rank} {k} is not finite: {lst} (optimizer step skipped)")
+        fns, self._on_ready = self._on_ready, []
+        for fn in fns:
+            fn(self)
+
+    def __getitem__(self, k):
+        self._finish()
+        return self._data[k]
+
+    def __setitem__(self, k, v):
+        self._data[k] = v
+
+    def __delitem__(self, k):
+        self._finish()
+        del self._data[k]
+
+    def __iter__(self):
+        self._finish()
+        return iter(dict(self._data))
+
+    def __len__(self):
+        self._finish()
+        return len(self._data)
+
+    def __repr__(self):
+        self._finish()
+        return f"DeviceMetrics({self._data!r})"
+
+
+def _to_host(dev_metrics: dict) -> DeviceMetrics:
+    """The update's metrics as a DeviceMetrics (one asynchronous device->host copy)."""
+    return DeviceMetrics(dev_metrics)

@@ -21,6 +21,7 @@ from ..protocol import DataProto
 from ..utils.flops_counter import FlopsCounter
 from ..utils.torch_functional import build_lr_scheduler
 from .actor import DataParallelPPOActor
+from .actor.dp_actor import DeviceMetrics
 from .grad_sync import GradBucketReducer, MixedPrecisionParams, ShardedMixedPrecisionParams
 
 
@@ -167,13 +168,16 @@ class ActorWorker:
         additions: perf/mfu/actor (model FLOPs of the whole batch's tokens, meta_info
         global_token_num, over the update's wall time and the device peak, / world size),
         perf/max_memory_* and perf/cpu_memory_used_gb, actor/lr (the rate this update used),
-        then one LR-scheduler step. update_policy returns its metrics through one device->host
-        copy, so the host clock here spans the device work of the update."""
-        t0 = time.perf_counter()
-        metrics = self.actor.update_policy(data)
-        delta_time = time.perf_counter() - t0
-        metrics.update(perf_metrics(self.flops_counter, data, delta_time, self.config.actor.get("ppo_epochs", 1),
-                                    self.world_size, "actor"))
+        then one LR-scheduler step. update_policy's metrics arrive by an asynchronous device->host
+        copy (dp_actor.DeviceMetrics: the host does not wait for the update here), so the update's
+        time for the MFU is its device span between two stream events, read with the metrics."""
+        span = _UpdateSpan(self.module)
+        metrics = as_device_metrics(self.actor.update_policy(data))
+        span.stop()
+        epochs = self.config.actor.get("ppo_epochs", 1)
+        metrics.update(perf_metrics(self.flops_counter, data, span.host_seconds(), epochs, self.world_size, "actor"))
+        metrics.add_on_ready(lambda m: m.__setitem__("perf/mfu/actor", perf_metrics(
+            self.flops_counter, data, span.seconds(), epochs, self.world_size, "actor", memory=False)["perf/mfu/actor"]))
         metrics["actor/lr"] = self.actor_lr_scheduler.get_last_lr()[0]
         self.actor_lr_scheduler.step()
         return DataProto(meta_info={"metrics": metrics})
@@ -231,19 +235,55 @@ class CriticWorker:
     def update_critic(self, data: DataProto) -> DataProto:
         """fsdp_workers.py:1231-1264: metrics + perf/mfu/critic + critic/lr, then one LR-scheduler
         step."""
-        t0 = time.perf_counter()
-        metrics = self.critic.update_critic(data=data)
-        delta_time = time.perf_counter() - t0
-        mfu = perf_metrics(self.flops_counter, data, delta_time, self.config.get("ppo_epochs", 1), self.world_size,
-                           "critic")
-        metrics["perf/mfu/critic"] = mfu["perf/mfu/critic"]
+        span = _UpdateSpan(getattr(self.critic, "critic_module", None))
+        metrics = as_device_metrics(self.critic.update_critic(data=data))
+        span.stop()
+        epochs = self.config.get("ppo_epochs", 1)
+        metrics["perf/mfu/critic"] = perf_metrics(self.flops_counter, data, span.host_seconds(), epochs,
+                                                  self.world_size, "critic", memory=False)["perf/mfu/critic"]
+        metrics.add_on_ready(lambda m: m.__setitem__("perf/mfu/critic", perf_metrics(
+            self.flops_counter, data, span.seconds(), epochs, self.world_size, "critic", memory=False)["perf/mfu/critic"]))
         metrics["critic/lr"] = self.critic_lr_scheduler.get_last_lr()[0]
         self.critic_lr_scheduler.step()
         return DataProto(meta_info={"metrics": metrics})
 
 
+def as_device_metrics(metrics) -> DeviceMetrics:
+    return metrics if isinstance(metrics, DeviceMetrics) else DeviceMetrics(metrics)
+
+
+class _UpdateSpan:
+    """Time of one update: its device span between two events on the current stream (the host
+    does not wait for the update to finish), the host clock for a module off the GPU."""
+
+    def __init__(self, module):
+        p = next(module.parameters(), None) if module is not None else None
+        self.cuda = p is not None and p.is_cuda
+        self.t0 = time.perf_counter()
+        self.t1 = None
+        self.ev = None
+        if self.cuda:
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self.ev[0].record()
+
+    def stop(self):
+        self.t1 = time.perf_counter()
+        if self.ev is not None:
+            self.ev[1].record()
+
+    def host_seconds(self) -> float:
+        return self.t1 - self.t0
+
+    def seconds(self) -> float:
+        """The device span (waits for the end event), or the host time off the GPU."""
+        if self.ev is None:
+            return self.host_seconds()
+        self.ev[1].synchronize()
+        return self.ev[0].elapsed_time(self.ev[1]) / 1e3
+
+
 def perf_metrics(flops_counter, data: DataProto, delta_time: float, ppo_epochs: int, world_size: int,
-                 role: str) -> dict:
+                 role: str, memory: bool = True) -> dict:
     """fsdp_workers.py:690-697: MFU of one update (estimated FLOP/s x epochs / promised / world)
     and the memory high-water marks. ``global_token_num`` lists the valid tokens of every sequence
     of the WHOLE batch (the reference's driver sets it before the DP dispatch, ray_trainer.py:1208;
@@ -259,6 +299,8 @@ def perf_metrics(flops_counter, data: DataProto, delta_time: float, ppo_epochs: 
         share = 1
     est, promised = flops_counter.estimate_flops(tokens, delta_time)
     out = {f"perf/mfu/{role}": est * ppo_epochs / promised / share}
+    if not memory:
+        return out
     if torch.cuda.is_available():
         out["perf/max_memory_allocated_gb"] = torch.cuda.max_memory_allocated() / (1024**3)
         out["perf/max_memory_reserved_gb"] = torch.cuda.max_memory_reserved() / (1024**3)
