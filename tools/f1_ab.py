@@ -3,6 +3,10 @@ libverl_amd.so: run once per build with VERL_AMD_LIB pointing at it; prints one 
 of 5 timed blocks of --iters launches, and the largest deviation from the unfused path).
 
   VERL_AMD_LIB=scratch/ab/libverl_amd_old.so python tools/f1_ab.py --tag old
+
+--pre-gemm-ms X runs X ms of back-to-back hipBLASLt GEMMs (the backbone's gate|up forward shape)
+right before each timed block, with no host sync in between: the f1 launches then start in the
+power / clock state the bench step leaves them in (the in-step penalty question).
 """
 
 import argparse
@@ -23,6 +27,8 @@ def main():
     ap.add_argument("--tune", action="append", default=[], help="KEY=VALUE va_set_tuning before timing")
     ap.add_argument("--unfused", action="store_true",
                     help="also time the unfused path (hipBLASLt lm_head GEMM + logprob_entropy_fwd), e.g. under rocprofv3")
+    ap.add_argument("--pre-gemm-ms", type=float, default=0.0,
+                    help="back-to-back GEMM load (ms) right before each timed block")
     args = ap.parse_args()
     from verl_amd import _lib as L
     from verl_amd import kernels as K
@@ -44,8 +50,17 @@ def main():
         for _ in range(3):
             K.linear_logprob_entropy(h, w, lab, 1.0)
         torch.cuda.synchronize()
+        pre = None
+        if args.pre_gemm_ms > 0:  # ~2.0 ms per gate|up forward GEMM at 163,840 tokens
+            xa = torch.randn(163840, 896, device=dev).to(torch.bfloat16)
+            wa = torch.randn(9728, 896, device=dev).to(torch.bfloat16)
+            ya = torch.empty(163840, 9728, dtype=torch.bfloat16, device=dev)
+            pre = (xa, wa, ya, max(1, int(args.pre_gemm_ms / 2.0)))
         times = []
         for _ in range(5):
+            if pre is not None:
+                for _ in range(pre[3]):
+                    torch.matmul(pre[0], pre[1].t(), out=pre[2])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(args.iters):
@@ -73,7 +88,8 @@ def main():
                 ut.append(e0.elapsed_time(e1) / args.iters)
         unfused_ms = round(sorted(ut)[2], 3)
         del logits
-    print(json.dumps({"tag": args.tag, "lib": str(L.LIB_PATH), "rows": N, "ms_median": round(ms, 3),
+    print(json.dumps({"tag": args.tag, "lib": str(L.LIB_PATH), "rows": N, "pre_gemm_ms": args.pre_gemm_ms,
+                      "iters": args.iters, "ms_median": round(ms, 3),
                       "ms_all": [round(t, 3) for t in times], "tflops": round(2.0 * N * V * H / ms / 1e9, 1),
                       "max_dlp_vs_unfused": dlp, "max_dent_vs_unfused": dent, "unfused_ms": unfused_ms}), flush=True)
 

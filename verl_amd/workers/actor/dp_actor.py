@@ -488,7 +488,8 @@ class DataParallelPPOActor(BasePPOActor):
         has_mm = "multi_modal_inputs" in data.non_tensor_batch.keys()
         data = data.select(batch_keys=["responses", "input_ids", "attention_mask", "position_ids"],
                            non_tensor_batch_keys=["multi_modal_inputs"] if has_mm else [])
-        am = self._mask_host(data.batch["attention_mask"]) if self.use_remove_padding else None
+        am = (self._mask_host(data.batch["attention_mask"], refresh=BLOCKING_STEP_BOUNDARY)
+              if self.use_remove_padding else None)
         if use_dynamic_bsz:
             # dp_actor.py:321-323: micro-batches cut by a token budget, restored afterwards
             max_token_len = data.meta_info["max_token_len"] * self.ulysses_sequence_parallel_size
@@ -773,6 +774,15 @@ class DeviceMetrics(MutableMapping):
         return f"DeviceMetrics({self._data!r})"
 
 
+# VERL_AMD_BLOCKING_STEP_BOUNDARY=1 restores the round-4 step boundary for A/B runs: the update's
+# metrics are read back before update_policy returns (a host sync), and compute_log_prob always
+# copies the attention mask device->host
+BLOCKING_STEP_BOUNDARY = os.environ.get("VERL_AMD_BLOCKING_STEP_BOUNDARY", "0") == "1"
+
+
 def _to_host(dev_metrics: dict) -> DeviceMetrics:
     """The update's metrics as a DeviceMetrics (one asynchronous device->host copy)."""
-    return DeviceMetrics(dev_metrics)
+    m = DeviceMetrics(dev_metrics)
+    if BLOCKING_STEP_BOUNDARY:
+        len(m)  # waits for the copy here
+    return m
