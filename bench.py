@@ -172,6 +172,9 @@ def parse(argv=None):
                     help="1: backbone weight gradients + fp32 accumulation on a side stream (wgrad_side_stream)")
     ap.add_argument("--fused-no-grad", type=int, default=1, choices=[0, 1],
                     help="1: the no-grad old-logp pass runs the fused lm_head + log-prob kernel (f1, fused_logprob_no_grad)")
+    ap.add_argument("--f1-after-backbone", type=int, default=1, choices=[0, 1],
+                    help="1: the no-grad pass runs every micro-batch's backbone, then the fused lm_head launches back "
+                         "to back (fused_lm_head_after_backbone); 0: backbone + lm_head per micro-batch")
     ap.add_argument("--fused-kernels", type=int, default=0, choices=[0, 1],
                     help="1: use_fused_kernels for every pass (the update pass too: fused f1 forward + the fused "
                          "dlogits backward, no [N, V] logits in HBM)")
@@ -502,6 +505,7 @@ def main():
             pack_pad_multiple=args.pad_multiple,
             logprob_inplace_backward={0: False, 1: True, 2: "auto"}[args.logprob_inplace_bwd],
             fused_logprob_no_grad=bool(args.fused_no_grad),
+            fused_lm_head_after_backbone=bool(args.f1_after_backbone),
             use_fused_kernels=bool(args.fused_kernels),
             wgrad_side_stream=bool(args.wgrad_stream),
             gemm_tuning_file=None if args.gemm_table in (None, "none") else args.gemm_table,
@@ -718,6 +722,7 @@ def main():
                 "logprob_inplace_backward": {0: False, 1: True, 2: "auto"}[args.logprob_inplace_bwd],
                 "logprob_bwd_inplace_fallbacks": lp_fallbacks,
                 "fused_logprob_no_grad": bool(args.fused_no_grad),
+                "fused_lm_head_after_backbone": bool(args.f1_after_backbone),
                 "use_fused_kernels": bool(args.fused_kernels),
                 "zero_sharded_optimizer": bool(args.zero),
                 "wgrad_side_stream": bool(args.wgrad_stream),

@@ -107,7 +107,9 @@ def test_fused_backward_matches_unfused():
 
 
 def test_actor_fused_no_grad_logprob_matches_unfused():
-    """compute_log_prob with fused_logprob_no_grad on / off (packed bf16 actor)."""
+    """compute_log_prob with fused_logprob_no_grad on / off (packed bf16 actor); with it on, the
+    lm_head launches after all micro-batches' backbones (default) give the same bits as one
+    backbone + lm_head per micro-batch."""
     import copy
 
     from verl_amd.utils.config import actor_config
@@ -124,14 +126,16 @@ def test_actor_fused_no_grad_logprob_matches_unfused():
                            dense_responses=False, min_response=5, seed=4, device=DEV)
     data.meta_info.update(micro_batch_size=4, temperature=0.9, use_dynamic_bsz=False)
     out = {}
-    for fused in (False, True):
+    for fused, after in ((False, True), (True, True), (True, False)):
         m = copy.deepcopy(base)
-        a = DataParallelPPOActor(actor_config(use_remove_padding=True, fused_logprob_no_grad=fused), m,
+        a = DataParallelPPOActor(actor_config(use_remove_padding=True, fused_logprob_no_grad=fused,
+                                              fused_lm_head_after_backbone=after), m,
                                  torch.optim.SGD(m.parameters(), lr=0.0))
-        out[fused] = a.compute_log_prob(data, calculate_entropy=True)
+        out[fused, after] = a.compute_log_prob(data, calculate_entropy=True)
     msk = data.batch["response_mask"].bool()
-    assert torch.allclose(out[True][0][msk], out[False][0][msk], atol=4e-2)
-    assert torch.allclose(out[True][1][msk], out[False][1][msk], atol=5e-3)
+    assert torch.allclose(out[True, True][0][msk], out[False, True][0][msk], atol=4e-2)
+    assert torch.allclose(out[True, True][1][msk], out[False, True][1][msk], atol=5e-3)
+    assert torch.equal(out[True, True][0], out[True, False][0]) and torch.equal(out[True, True][1], out[True, False][1])
 
 
 # ------------------------------------------------------------------ fused backward (va_linear_logprob_bwd)

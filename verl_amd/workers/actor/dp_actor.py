@@ -172,6 +172,15 @@ def _plan_packing(attn_mask_cpu: np.ndarray, R: int, device, pad_multiple: int =
     )
 
 
+def _scatter_rows(lp_sel, ent_sel, packing: _Packing, B: int, R: int, calculate_entropy: bool):
+    """(entropy or None, log_probs) [B, R] from the selected rows' values (pad_input: 0 elsewhere)."""
+    log_probs = lp_sel.new_zeros(B * R).index_copy(0, packing.sel_out, lp_sel).view(B, R)
+    entropy = None
+    if calculate_entropy:
+        entropy = ent_sel.new_zeros(B * R).index_copy(0, packing.sel_out, ent_sel).view(B, R)
+    return entropy, log_probs
+
+
 def _mm_kwargs(multi_modal_inputs, device=None) -> dict:
     """dp_actor.py:94-98: the rows' multi-modal tensors concatenated along dim 0, on ``device``
     (the reference's FSDP module moves forward inputs to its device)."""
@@ -283,6 +292,9 @@ class DataParallelPPOActor(BasePPOActor):
         # gfx950 flash-attention forward (attention.hip) inside the fused packed backbone
         self.fused_attention = self.config.get("fused_attention", True)
         self.fused_logprob_no_grad = self.config.get("fused_logprob_no_grad", False)
+        # no-grad passes with the fused lm_head: run all micro-batches' backbones, then the lm_head
+        # launches back to back (compute_log_prob)
+        self.fused_lm_head_after_backbone = bool(self.config.get("fused_lm_head_after_backbone", True))
         # the fused kernel's logits: bf16-rounded like the unfused autocast path (default: fused and
         # unfused agree) or fp32 like the reference's own fused kernel
         self.fused_kernel_fp32_logits = bool(self.config.get("fused_kernel_fp32_logits", False))
@@ -347,28 +359,9 @@ class DataParallelPPOActor(BasePPOActor):
                 if packing is None:
                     packing = _plan_packing(micro_batch["attention_mask"].cpu().numpy(), R, input_ids.device,
                                             self.pack_pad_multiple)
-                ids, pos = packing.gather(input_ids, micro_batch["position_ids"])
-                if self._fused_backbone is None:
-                    from . import qwen2_fused
-
-                    self._fused_backbone = self.fused_model_ops and qwen2_fused.supports(self._backbone)
-                if self._fused_backbone:
-                    from .qwen2_fused import packed_forward
-
-                    fa = self.fused_attention
-                    hidden = packed_forward(self._backbone, ids, pos, packing.cu_seqlens, packing.max_seqlen,
-                                            attn_blocks=packing.attn_blocks if fa else None,
-                                            attn_kblocks=packing.attn_kblocks if fa else None,
-                                            multi_modal_inputs=multi_modal_inputs)
-                else:
-                    hidden = hf_packed_hidden(self._backbone, ids, pos, packing, multi_modal_inputs)
-                h_sel = hidden.index_select(0, packing.sel_hidden)
-                labels = input_ids.reshape(-1).index_select(0, packing.label_idx)
+                h_sel, labels = self._selected_hidden(micro_batch, packing, multi_modal_inputs)
                 if self._use_fused_lm_head():
-                    w = self._lm_head.weight
-                    lp_sel, ent_sel = K.linear_logprob_entropy(
-                        h_sel.to(torch.bfloat16), w if w.dtype == torch.bfloat16 else w.to(torch.bfloat16), labels,
-                        temperature, fp32_logits=self.fused_kernel_fp32_logits)
+                    lp_sel, ent_sel = self._fused_lm_head_logprob(h_sel, labels, temperature)
                 else:
                     head = self._lm_head
                     if (isinstance(head, nn.Linear) and head.bias is None and h_sel.is_cuda
@@ -381,10 +374,7 @@ class DataParallelPPOActor(BasePPOActor):
                         logits = head(h_sel)
                     lp_sel, ent_sel = verl_F.logprobs_and_entropy_from_logits(
                         logits, labels, temperature, inplace_backward=self.logprob_inplace_backward)
-                log_probs = lp_sel.new_zeros(B * R).index_copy(0, packing.sel_out, lp_sel).view(B, R)
-                entropy = None
-                if calculate_entropy:
-                    entropy = ent_sel.new_zeros(B * R).index_copy(0, packing.sel_out, ent_sel).view(B, R)
+                entropy, log_probs = _scatter_rows(lp_sel, ent_sel, packing, B, R, calculate_entropy)
             else:
                 pos_ids = micro_batch["position_ids"]
                 if pos_ids.dim() == 3:  # qwen2vl mrope (bsz, 3, seqlen) -> (3, bsz, seqlen), dp_actor.py:106-107
@@ -399,6 +389,34 @@ class DataParallelPPOActor(BasePPOActor):
                     logits, responses, temperature, inplace_backward=self.logprob_inplace_backward)
                 entropy = ent if calculate_entropy else None
         return entropy, log_probs
+
+    def _selected_hidden(self, micro_batch, packing: _Packing, multi_modal_inputs=None):
+        """The packed backbone over one micro-batch -> (hidden states of the rows whose log-prob is
+        kept [n_sel, H], their labels [n_sel]) (dp_actor.py:167-190 up to the lm_head)."""
+        input_ids = micro_batch["input_ids"]
+        ids, pos = packing.gather(input_ids, micro_batch["position_ids"])
+        if self._fused_backbone is None:
+            from . import qwen2_fused
+
+            self._fused_backbone = self.fused_model_ops and qwen2_fused.supports(self._backbone)
+        if self._fused_backbone:
+            from .qwen2_fused import packed_forward
+
+            fa = self.fused_attention
+            hidden = packed_forward(self._backbone, ids, pos, packing.cu_seqlens, packing.max_seqlen,
+                                    attn_blocks=packing.attn_blocks if fa else None,
+                                    attn_kblocks=packing.attn_kblocks if fa else None,
+                                    multi_modal_inputs=multi_modal_inputs)
+        else:
+            hidden = hf_packed_hidden(self._backbone, ids, pos, packing, multi_modal_inputs)
+        h_sel = hidden.index_select(0, packing.sel_hidden)
+        labels = input_ids.reshape(-1).index_select(0, packing.label_idx)
+        return h_sel, labels
+
+    def _fused_lm_head_logprob(self, h_sel, labels, temperature):
+        w = self._lm_head.weight
+        return K.linear_logprob_entropy(h_sel.to(torch.bfloat16), w if w.dtype == torch.bfloat16 else w.to(torch.bfloat16),
+                                        labels, temperature, fp32_logits=self.fused_kernel_fp32_logits)
 
     def _use_fused_lm_head(self) -> bool:
         head = self._lm_head
@@ -499,11 +517,30 @@ class DataParallelPPOActor(BasePPOActor):
             micro_batches = data.split(micro_batch_size)
             plans = self._plans(data, [len(m) for m in micro_batches], am=am)
         lps, ents = [], []
-        for mb, plan in zip(micro_batches, plans, strict=True):
-            ent, lp = self._forward_micro_batch(mb.batch, temperature, calculate_entropy, plan, _multi_modal(mb))
-            lps.append(lp)
-            if calculate_entropy:
-                ents.append(ent)
+        if self.use_remove_padding and self._use_fused_lm_head() and self.fused_lm_head_after_backbone:
+            # every micro-batch's backbone first, then their fused lm_head launches back to back: f1
+            # right after the backbone's power-capped GEMMs starts clocked down (33.1 ms alone, 34.9 ms
+            # right after GEMM load, 33.4 ms per launch over 4 in a row; profiles/r05/f1_pre_gemm_load.jsonl),
+            # so consecutive launches recover the clock. Per-row results are the same bits.
+            sel = []
+            with torch.autocast(device_type=self.device_name, dtype=self.autocast_dtype or torch.bfloat16,
+                                enabled=self.autocast_dtype is not None):
+                for mb, plan in zip(micro_batches, plans, strict=True):
+                    sel.append(self._selected_hidden(mb.batch, plan, _multi_modal(mb)))
+                for mb, plan, (h_sel, labels) in zip(micro_batches, plans, sel, strict=True):
+                    lp_sel, ent_sel = self._fused_lm_head_logprob(h_sel, labels, temperature)
+                    B, R = mb.batch["responses"].shape
+                    ent, lp = _scatter_rows(lp_sel, ent_sel, plan, B, R, calculate_entropy)
+                    lps.append(lp)
+                    if calculate_entropy:
+                        ents.append(ent)
+            del sel
+        else:
+            for mb, plan in zip(micro_batches, plans, strict=True):
+                ent, lp = self._forward_micro_batch(mb.batch, temperature, calculate_entropy, plan, _multi_modal(mb))
+                lps.append(lp)
+                if calculate_entropy:
+                    ents.append(ent)
         log_probs = torch.concat(lps, dim=0)
         entropys = torch.concat(ents, dim=0) if calculate_entropy else None
         if use_dynamic_bsz:
