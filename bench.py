@@ -175,6 +175,8 @@ def parse(argv=None):
     ap.add_argument("--f1-after-backbone", type=int, default=1, choices=[0, 1],
                     help="1: the no-grad pass runs every micro-batch's backbone, then the fused lm_head launches back "
                          "to back (fused_lm_head_after_backbone); 0: backbone + lm_head per micro-batch")
+    ap.add_argument("--f1-concat", type=int, default=0, choices=[0, 1],
+                    help="with --f1-after-backbone 1: one fused lm_head launch over all micro-batches' rows")
     ap.add_argument("--fused-kernels", type=int, default=0, choices=[0, 1],
                     help="1: use_fused_kernels for every pass (the update pass too: fused f1 forward + the fused "
                          "dlogits backward, no [N, V] logits in HBM)")
@@ -506,6 +508,7 @@ def main():
             logprob_inplace_backward={0: False, 1: True, 2: "auto"}[args.logprob_inplace_bwd],
             fused_logprob_no_grad=bool(args.fused_no_grad),
             fused_lm_head_after_backbone=bool(args.f1_after_backbone),
+            fused_lm_head_concat=bool(args.f1_concat),
             use_fused_kernels=bool(args.fused_kernels),
             wgrad_side_stream=bool(args.wgrad_stream),
             gemm_tuning_file=None if args.gemm_table in (None, "none") else args.gemm_table,
@@ -723,6 +726,7 @@ def main():
                 "logprob_bwd_inplace_fallbacks": lp_fallbacks,
                 "fused_logprob_no_grad": bool(args.fused_no_grad),
                 "fused_lm_head_after_backbone": bool(args.f1_after_backbone),
+                "fused_lm_head_concat": bool(args.f1_concat),
                 "use_fused_kernels": bool(args.fused_kernels),
                 "zero_sharded_optimizer": bool(args.zero),
                 "wgrad_side_stream": bool(args.wgrad_stream),

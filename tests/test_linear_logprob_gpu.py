@@ -126,16 +126,22 @@ def test_actor_fused_no_grad_logprob_matches_unfused():
                            dense_responses=False, min_response=5, seed=4, device=DEV)
     data.meta_info.update(micro_batch_size=4, temperature=0.9, use_dynamic_bsz=False)
     out = {}
-    for fused, after in ((False, True), (True, True), (True, False)):
+    for fused, after, concat in ((False, True, False), (True, True, False), (True, False, False), (True, True, True)):
         m = copy.deepcopy(base)
         a = DataParallelPPOActor(actor_config(use_remove_padding=True, fused_logprob_no_grad=fused,
-                                              fused_lm_head_after_backbone=after), m,
+                                              fused_lm_head_after_backbone=after, fused_lm_head_concat=concat), m,
                                  torch.optim.SGD(m.parameters(), lr=0.0))
-        out[fused, after] = a.compute_log_prob(data, calculate_entropy=True)
+        out[fused, after, concat] = a.compute_log_prob(data, calculate_entropy=True)
+        if not concat:
+            out[fused, after] = out[fused, after, concat]
     msk = data.batch["response_mask"].bool()
     assert torch.allclose(out[True, True][0][msk], out[False, True][0][msk], atol=4e-2)
     assert torch.allclose(out[True, True][1][msk], out[False, True][1][msk], atol=5e-3)
     assert torch.equal(out[True, True][0], out[True, False][0]) and torch.equal(out[True, True][1], out[True, False][1])
+    # one launch over both micro-batches' rows: within fp32 rounding of the vocab-range merge
+    for i in range(2):
+        a, b = out[True, True, True][i][msk], out[True, True, False][i][msk]
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-5), (a - b).abs().max()
 
 
 # ------------------------------------------------------------------ fused backward (va_linear_logprob_bwd)

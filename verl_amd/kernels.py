@@ -178,10 +178,11 @@ def _linear_logprob_splits(n_rows: int, vocab: int | None = None) -> int:
     return s if vocab is None else max(1, min(s, -(-vocab // 256)))
 
 
-def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float, fp32_logits: bool = False):
+def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float, fp32_logits: bool = False,
+                            splits: int | None = None):
     N, H = hidden.shape
     V = weight.shape[0]
-    splits = _linear_logprob_splits(N)
+    splits = _linear_logprob_splits(N) if splits is None else int(splits)
     logp = torch.empty(N, dtype=torch.float32, device=hidden.device)
     ent = torch.empty(N, dtype=torch.float32, device=hidden.device)
     lse = torch.empty(N, dtype=torch.float32, device=hidden.device)
@@ -233,8 +234,8 @@ class _LinearLogprob(torch.autograd.Function):
     COMPOSE_CHUNK_BYTES = int(os.environ.get("VERL_AMD_F1_BWD_CHUNK_MB", "2048")) << 20
 
     @staticmethod
-    def forward(ctx, hidden, weight, labels, temperature, fp32_logits):
-        logp, ent, lse = _linear_logprob_fwd_raw(hidden, weight, labels, temperature, fp32_logits)
+    def forward(ctx, hidden, weight, labels, temperature, fp32_logits, splits=None):
+        logp, ent, lse = _linear_logprob_fwd_raw(hidden, weight, labels, temperature, fp32_logits, splits)
         ctx.save_for_backward(hidden, weight, labels, lse, ent)
         ctx.temperature = float(temperature)
         ctx.fp32_logits = bool(fp32_logits)
@@ -327,21 +328,24 @@ class _LinearLogprob(torch.autograd.Function):
             # zero gradients rather than None: a DP rank's lm_head gradient hook must
             # still fire so that its all-reduce bucket becomes ready
             return (torch.zeros_like(hidden) if need_h else None, torch.zeros_like(weight) if need_w else None,
-                    None, None, None)
+                    None, None, None, None)
         g1 = None if g_logp is None else _f32(g_logp)
         g2 = None if g_ent is None else _f32(g_ent)
         fused = os.environ.get("VERL_AMD_F1_BWD", "fused") != "compose" and V % 4 == 0
         run = _LinearLogprob._vocab_split_backward if fused else _LinearLogprob._compose_backward
         d_hidden, d_weight = run(ctx, hidden, weight, labels, lse, ent, g1, g2)
-        return d_hidden, d_weight, None, None, None
+        return d_hidden, d_weight, None, None, None, None
 
 
-def linear_logprob_entropy(hidden, weight, labels, temperature: float = 1.0, fp32_logits: bool = False):
+def linear_logprob_entropy(hidden, weight, labels, temperature: float = 1.0, fp32_logits: bool = False,
+                           splits: int | None = None):
     """(log p[label], entropy) of ``hidden @ weight.T`` (the lm_head) after ``div_(temperature)``,
     computed by the fused MFMA kernel without materialising the [N, V] logits. bf16 only.
     fp32_logits=False rounds the logits to bf16 as the unfused autocast path does (fused and
     unfused agree); True keeps them fp32, the numerics of the reference's fused kernel
-    (utils/kernel/kernels.py:120-663, tests/utils/test_linear_cross_entropy.py tolerances)."""
+    (utils/kernel/kernels.py:120-663, tests/utils/test_linear_cross_entropy.py tolerances).
+    ``splits``: vocab ranges per row block (default: by the row count, _linear_logprob_splits); the
+    per-row results depend on it only through the fixed-order merge of the ranges."""
     _require_device(hidden, weight, labels)
     _bf16_only(hidden, weight)
     if hidden.dim() != 2 or weight.dim() != 2 or hidden.shape[1] != weight.shape[1]:
@@ -353,7 +357,9 @@ def linear_logprob_entropy(hidden, weight, labels, temperature: float = 1.0, fp3
     lab = labels.reshape(-1).long().contiguous()
     if lab.shape[0] != hidden.shape[0]:
         raise ValueError(f"labels ({lab.shape[0]}) do not match hidden rows ({hidden.shape[0]})")
-    return _LinearLogprob.apply(hidden, weight, lab, float(temperature), bool(fp32_logits))
+    if splits is not None and not 1 <= int(splits) <= 64:
+        raise ValueError(f"linear_logprob: splits must be in [1, 64], got {splits}")
+    return _LinearLogprob.apply(hidden, weight, lab, float(temperature), bool(fp32_logits), splits)
 
 
 # =============================================================================== policy loss

@@ -295,6 +295,8 @@ class DataParallelPPOActor(BasePPOActor):
         # no-grad passes with the fused lm_head: run all micro-batches' backbones, then the lm_head
         # launches back to back (compute_log_prob)
         self.fused_lm_head_after_backbone = bool(self.config.get("fused_lm_head_after_backbone", True))
+        # ... and as ONE launch over the concatenated rows
+        self.fused_lm_head_concat = bool(self.config.get("fused_lm_head_concat", False))
         # the fused kernel's logits: bf16-rounded like the unfused autocast path (default: fused and
         # unfused agree) or fp32 like the reference's own fused kernel
         self.fused_kernel_fp32_logits = bool(self.config.get("fused_kernel_fp32_logits", False))
@@ -413,10 +415,10 @@ class DataParallelPPOActor(BasePPOActor):
         labels = input_ids.reshape(-1).index_select(0, packing.label_idx)
         return h_sel, labels
 
-    def _fused_lm_head_logprob(self, h_sel, labels, temperature):
+    def _fused_lm_head_logprob(self, h_sel, labels, temperature, splits=None):
         w = self._lm_head.weight
         return K.linear_logprob_entropy(h_sel.to(torch.bfloat16), w if w.dtype == torch.bfloat16 else w.to(torch.bfloat16),
-                                        labels, temperature, fp32_logits=self.fused_kernel_fp32_logits)
+                                        labels, temperature, fp32_logits=self.fused_kernel_fp32_logits, splits=splits)
 
     def _use_fused_lm_head(self) -> bool:
         head = self._lm_head
@@ -527,8 +529,17 @@ class DataParallelPPOActor(BasePPOActor):
                                 enabled=self.autocast_dtype is not None):
                 for mb, plan in zip(micro_batches, plans, strict=True):
                     sel.append(self._selected_hidden(mb.batch, plan, _multi_modal(mb)))
-                for mb, plan, (h_sel, labels) in zip(micro_batches, plans, sel, strict=True):
-                    lp_sel, ent_sel = self._fused_lm_head_logprob(h_sel, labels, temperature)
+                if self.fused_lm_head_concat and len(sel) > 1:
+                    # ONE launch over every micro-batch's rows, with the vocab ranges a micro-batch's
+                    # own launch would use (the same per-row bits for equal-sized micro-batches)
+                    sizes = [h.shape[0] for h, _ in sel]
+                    lp_all, ent_all = self._fused_lm_head_logprob(
+                        torch.cat([h for h, _ in sel]), torch.cat([lab for _, lab in sel]), temperature,
+                        splits=K._linear_logprob_splits(max(sizes)))
+                    outs = list(zip(lp_all.split(sizes), ent_all.split(sizes), strict=True))
+                else:
+                    outs = [self._fused_lm_head_logprob(h_sel, labels, temperature) for h_sel, labels in sel]
+                for mb, plan, (lp_sel, ent_sel) in zip(micro_batches, plans, outs, strict=True):
                     B, R = mb.batch["responses"].shape
                     ent, lp = _scatter_rows(lp_sel, ent_sel, plan, B, R, calculate_entropy)
                     lps.append(lp)
