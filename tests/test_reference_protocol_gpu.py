@@ -11,7 +11,9 @@ and the reference's own tolerances:
   * the fused lm_head kernel (no logits in HBM) in its fp32-logits mode — the reference's fused
     kernel keeps the logits fp32; the default mode rounds them to bf16 like the unfused autocast
     path — 1e-3 / 2e-4 log-probs, 5e-3 / 5e-4 entropy (:217-218), 2e-2 / 4e-2 gradients (:267-268).
-This pins the log-prob / entropy restatement to torch itself, independently of the oracle.
+This pins the log-prob / entropy restatement to torch itself, independently of the oracle; the
+fused kernel's default (bf16-logits) mode is pinned to an fp32 torch reference with the same two
+bf16 roundings (test_fused_lm_head_default_mode_against_torch).
 """
 
 import pytest
@@ -86,3 +88,37 @@ def _fused_case(K, N, H, V):
     dh_g, dw_g = _grads(got, (hidden, weight), g_ent, g_lp)
     torch.testing.assert_close(dh_g, dh_w, atol=2e-2, rtol=4e-2)
     torch.testing.assert_close(dw_g, dw_w, atol=2e-2, rtol=4e-2)
+
+
+def _st_round(x):
+    """bf16 rounding with an identity gradient: the autocast path's bf16 logits and div_(T)
+    (dp_actor.py:182) as torch autograd sees them (the rounding is not differentiated)."""
+    return x + (x.to(torch.bfloat16).float() - x).detach()
+
+
+@pytest.mark.parametrize("N,H,V", [(2169, 896, 151936)])
+def test_fused_lm_head_default_mode_against_torch(N, H, V):
+    """The fused lm_head kernel in its DEFAULT mode (logits rounded to bf16, then bf16(x / T), as
+    the unfused autocast path holds them) pinned to torch itself: an fp32 reference with the same
+    two roundings (straight-through in the backward), on the reference protocol's inputs. What
+    remains is the accumulation order of the fp32 dot products before rounding (MFMA tiles vs
+    torch's GEMM), which can move a logit by one bf16 unit: bounds of one unit at |x| < 8 (2^-5)
+    for a row's log-prob, 1e-3 on entropy, and 1e-2 relative L2 on both gradients (dlogits are
+    bf16 for the lm_head GEMMs, as under autocast)."""
+    from verl_amd import kernels as K
+
+    hidden, weight, labels, g_ent, g_lp = _inputs(N, H, V, seed=N + 7)
+    h32 = hidden.detach().float().requires_grad_(True)
+    w32 = weight.detach().float().requires_grad_(True)
+    x = _st_round(_st_round(h32 @ w32.t()) / TEMPERATURE)
+    want = (torch.log_softmax(x, dim=-1).gather(-1, labels[:, None])[:, 0],
+            torch.logsumexp(x, dim=-1) - (torch.softmax(x, dim=-1) * x).sum(-1))
+    got = K.linear_logprob_entropy(hidden, weight, labels, TEMPERATURE)
+    dlp = (got[0] - want[0]).abs()
+    assert dlp.max().item() <= 2 ** -5 and dlp.mean().item() < 1e-4, (dlp.max().item(), dlp.mean().item())
+    assert (got[1] - want[1]).abs().max().item() < 1e-3
+    dh_w, dw_w = torch.autograd.grad((want[1], want[0]), (h32, w32), (g_ent.float(), g_lp.float()))
+    dh_g, dw_g = _grads(got, (hidden, weight), g_ent, g_lp)
+    for g, w, what in ((dh_g, dh_w, "d_hidden"), (dw_g, dw_w, "d_weight")):
+        err = ((g.float() - w).norm() / w.norm()).item()
+        assert err < 1e-2, f"{what}: relative L2 error {err:.3e}"

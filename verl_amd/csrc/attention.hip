@@ -182,7 +182,11 @@ __global__ __launch_bounds__(256, DMA ? VA_FLASH_FWD_DMA_OCC : 2) void flash_fwd
       // ---- online softmax over the block (base 2); masks only on diagonal / sequence-end blocks.
       // The running max m is kept on the RAW scores (c > 0), p = exp2(fma(S, c, -m c)) is one FMA
       // + one exp per score, and O / l are rescaled only when the max grows by more than
-      // kDeferLog2 / c (p <= 2^kDeferLog2 meanwhile; l and O see the same factor: exact).
+      // kDeferLog2 / c (p <= 2^kDeferLog2 meanwhile; l and O see the same factor: exact). Cross-lane
+      // work is kept off the steady state (round 5: 547-549 vs 565 us per 151,819-token micro-batch,
+      // profiles/r05/attn_fwd_shuffle_skip_ab.jsonl): the row max over both lanes of a query is
+      // exchanged only when some lane's own half passes the bound, and each lane sums its half of the
+      // row sum, the halves added once at the end.
       const bool need_mask = (key0 + KB - 1 > qs + wave * 32) || (key0 + KB - 1 >= len);
       float x[32];
 #pragma unroll
@@ -204,15 +208,19 @@ __global__ __launch_bounds__(256, DMA ? VA_FLASH_FWD_DMA_OCC : 2) void flash_fwd
         tm1 = fmaxf(tm1, x[r + 1]);
       }
       float tm = fmaxf(tm0, tm1);
-      tm = fmaxf(tm, __shfl_xor(tm, 32, kWave));
-      if (tm > m + kDeferLog2 / c) {  // per-lane; O / l rescaled only on these rows
-        const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - tm) * c);
-        l *= alpha;
+      // the rescale decision needs the max over both halves of the row (this lane and lane ^ 32),
+      // but only when some lane's own half passes the bound: the exchange is skipped otherwise
+      if (__builtin_amdgcn_ballot_w64(tm > m + kDeferLog2 / c) != 0) {  // wave-uniform
+        tm = fmaxf(tm, __shfl_xor(tm, 32, kWave));
+        if (tm > m + kDeferLog2 / c) {  // per-lane; O / l rescaled only on these rows
+          const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - tm) * c);
+          l *= alpha;
 #pragma unroll
-        for (int dh = 0; dh < 2; ++dh)
+          for (int dh = 0; dh < 2; ++dh)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) oacc[dh][r] *= alpha;
-        m = tm;
+            for (int r = 0; r < 16; ++r) oacc[dh][r] *= alpha;
+          m = tm;
+        }
       }
       const float nmc = m == -INFINITY ? 0.f : -m * c;
       float rs0 = 0.f, rs1 = 0.f;
@@ -223,9 +231,7 @@ __global__ __launch_bounds__(256, DMA ? VA_FLASH_FWD_DMA_OCC : 2) void flash_fwd
         rs0 += x[r];
         rs1 += x[r + 1];
       }
-      float rs = rs0 + rs1;
-      rs += __shfl_xor(rs, 32, kWave);
-      l += rs;
+      l += rs0 + rs1;  // this lane's half of the row sum (the halves are added once, at the end)
       // ---- O^T += V^T P^T over 4 k-steps of 16 keys; P^T = S^T registers 8s..8s+7 as bf16
       //      (k order permuted, guide §3); V^T fragment element j <-> key 16 s + 8 (j >> 2) + 4 h + (j & 3)
       const int g16 = lane >> 4, li = lane & 15;
@@ -262,6 +268,7 @@ __global__ __launch_bounds__(256, DMA ? VA_FLASH_FWD_DMA_OCC : 2) void flash_fwd
   }
 
   // ---- epilogue: O = O^T / l, lane holds O[q][32 dh + crow(r, h)]; lse in natural log
+  l += __shfl_xor(l, 32, kWave);  // the two lanes of a query hold the two halves of its row sum
   if (q_ok) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     uint16_t *orow = o + (s0 + q_pos) * ldq + head * D;
