@@ -395,6 +395,14 @@ int va_transpose_16(const void *in, int64_t ld_in, int64_t R, int64_t C, void *o
  * plan depends on VA_TUNE_WGRAD_REMAINDER, which may change between the size query and the launch).
  * Not a §8 row. */
 int64_t va_weight_grad_workspace_bytes(int64_t K, int64_t M, int64_t N, int splits);
+/* column_sum: out [C] bf16 = sum over the T rows of x [T, C] bf16 (row stride ld), fp32 accumulation in
+ * a fixed order (row slabs, then their partials): the bias gradient of the merged q|k|v projection
+ * (no reference counterpart: torch's dy.sum(0) in the linear backward under FSDP, dp_actor.py:465-470).
+ * C % 8 == 0, C <= 2048, 16-byte aligned x / out; workspace of va_column_sum_workspace_bytes(T, C)
+ * bytes, its size passed as workspace_bytes. Not a §8 row. */
+int64_t va_column_sum_workspace_bytes(int64_t T, int64_t C);
+int va_column_sum(const void *x, int64_t ld, int dtype, int64_t T, int64_t C, float *workspace,
+                  int64_t workspace_bytes, void *out, void *stream);
 int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_t ldx, int64_t K, int64_t M, int64_t N,
                    int splits, float *workspace, int64_t workspace_bytes, void *out, void *stream);
 

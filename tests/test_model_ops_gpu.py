@@ -295,3 +295,36 @@ def test_splitk_weight_grad(n_out, n_in, T):
     _grad_close(got, want, "split-K dW", rtol=5e-3)
     base = (dy.t() @ x).float()
     assert (got.float() - want).norm() <= 1.5 * (base - want).norm() + 1e-3
+
+
+@pytest.mark.parametrize("T,C", [(163840, 1152), (1000, 64), (4099, 2048), (1, 8), (0, 1152)])
+def test_column_sum_matches_fp32_sum(T, C):
+    """va_column_sum (the q|k|v bias gradient, kernels.column_sum): an fp32-accumulated column sum
+    rounded once to bf16 — within one bf16 unit of torch's fp64 sum of the same bf16 values — on
+    contiguous and row-strided inputs, deterministic run to run; zero rows give zeros."""
+    from verl_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(T + C)
+    base = torch.randn(T, C + 16, device=DEV, generator=g).to(torch.bfloat16)
+    for x in (base[:, :C].contiguous(), base[:, :C]):
+        got = K.column_sum(x)
+        want = x.double().sum(0)
+        assert got.dtype == torch.bfloat16 and got.shape == (C,)
+        tol = want.abs().to(torch.float32) * 2 ** -8 + 1e-3 * (T ** 0.5 + 1)
+        assert torch.all((got.double() - want).abs() <= tol.double()), (got.double() - want).abs().max()
+        assert torch.equal(got, K.column_sum(x))
+
+
+def test_merged_linear_bias_gradient_uses_column_sum():
+    """The merged q|k|v linear's bias gradient (kernels._MergedLinear) is the column sum of dY."""
+    from verl_amd import kernels as K
+
+    torch.manual_seed(0)
+    x = torch.randn(300, 64, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    w = torch.randn(96, 64, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    b = torch.randn(96, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    y = K.merged_linear(x, w, b, [w], [b])
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    assert torch.equal(b.grad, K.column_sum(dy))
+    assert (b.grad.double() - dy.double().sum(0)).abs().max().item() < 0.1

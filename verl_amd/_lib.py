@@ -121,6 +121,8 @@ _SIGNATURES: dict[str, tuple] = {
     "va_rope_qkv_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, c_int64, _P]),
     "va_transpose_16": (c_int, [_P, c_int64, c_int64, c_int64, _P, c_int64, _P]),
     "va_weight_grad_workspace_bytes": (c_int64, [c_int64, c_int64, c_int64, c_int]),
+    "va_column_sum_workspace_bytes": (c_int64, [c_int64, c_int64]),
+    "va_column_sum": (c_int, [_P, c_int64, c_int, c_int64, c_int64, _P, c_int64, _P, _P]),
     "va_weight_grad": (c_int, [_P, c_int64, _P, c_int64, c_int64, c_int64, c_int64, c_int, _P, c_int64, _P, _P]),
 }
 

@@ -748,7 +748,7 @@ class _MergedLinear(torch.autograd.Function):
         dw = weight_grad(dy2, x2)
         grads = list(torch.split(dw, ctx.w_rows, dim=0))
         if ctx.has_b:
-            db = dy2.sum(0)
+            db = column_sum(dy2)
             grads += list(torch.split(db, ctx.w_rows, dim=0))
         return grads
 
@@ -924,6 +924,25 @@ def weight_grad(dy2, x2):
             acc += torch.mm(dy2[main:].t(), x2[main:], out_dtype=torch.float32)
         return acc.to(dy2.dtype)
     return dy2.t() @ x2
+
+
+# VERL_AMD_BIAS_SUM=torch keeps torch's reduction for the bias gradients (A/B runs)
+_OWN_COLSUM = os.environ.get("VERL_AMD_BIAS_SUM", "own") != "torch"
+
+
+def column_sum(x2):
+    """x2.sum(0) for a [T, C] matrix: va_column_sum (fp32 accumulation in a fixed order, bf16 out)
+    for bf16 HIP tensors with C % 8 == 0 and C <= 2048 (the q|k|v bias gradient: 1,152 columns at
+    Qwen2.5-0.5B), torch's reduction otherwise."""
+    T, C = x2.shape
+    if not (_OWN_COLSUM and x2.is_cuda and x2.dtype == torch.bfloat16 and C % 8 == 0 and C <= 2048 and x2.stride(1) == 1
+            and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0):
+        return x2.sum(0)
+    out = torch.empty(C, dtype=torch.bfloat16, device=x2.device)
+    nb = L.load().va_column_sum_workspace_bytes(T, C)
+    ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=x2.device)
+    L.call("va_column_sum", _p(x2), x2.stride(0), L.VA_BF16, T, C, _p(ws), nb, _p(out), _stream(x2))
+    return out
 
 
 def linear(x, weight):
