@@ -200,3 +200,7 @@ def test_device_metrics_mapping_and_callbacks(capsys):
     assert "not finite" in capsys.readouterr().out
     m.add_on_ready(lambda mm: seen.append(1))  # already resolved: runs at once
     assert seen == [0.5, 1] and dict(m)["actor/kl_coef"] == [0.001]
+    import pickle
+
+    back = pickle.loads(pickle.dumps(m))
+    assert type(back) is dict and back == dict(m)

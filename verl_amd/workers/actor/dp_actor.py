@@ -821,6 +821,12 @@ class DeviceMetrics(MutableMapping):
         self._finish()
         return f"DeviceMetrics({self._data!r})"
 
+    def __reduce__(self):
+        # pickled (e.g. in a DataProto's meta_info across a process boundary) as the plain dict of
+        # host values: the pinned buffer and the event stay behind
+        self._finish()
+        return (dict, (dict(self._data),))
+
 
 # VERL_AMD_BLOCKING_STEP_BOUNDARY=1 restores the round-4 step boundary for A/B runs: the update's
 # metrics are read back before update_policy returns (a host sync), and compute_log_prob always
