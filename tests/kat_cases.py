@@ -1,0 +1,80 @@
+"""Known answers derived by hand from the reference source (no oracle, no reference run): each case
+states the inputs, the expected outputs worked out from the cited lines, and the working. Used twice:
+tests/test_oracle_kats.py pins the CPU oracle to them, tests/test_kats_gpu.py pins the HIP kernels
+to them directly, so neither side rests only on the other.
+"""
+
+import math
+
+E = math.e
+
+# ---- dual-clip PPO, core_algos.py:722-794 (cliprange 0.2, clip_ratio_c 3.0, one token per case) ----
+# ratio = exp(clamp(lp - old, -20, 20)); l1 = -A r; l2 = -A clamp(r, 0.8, 1.2); lmax = max(l1, l2)
+# A >= 0: per-token lmax; A < 0: min(lmax, -A c). clipfrac counts l2 > l1, clipfrac_lower counts
+# lmax > -A c with A < 0.
+#   (A, lp - old)   r        l1        l2     per-token   clip  lower
+#   (+1, 0.5)      e^0.5    -1.6487   -1.2    -1.2        1     0     (upper clip, A > 0)
+#   (-1, 1.5)      e^1.5    +4.4817   +1.2    +3.0        0     1     (dual clip: min(4.4817, 3))
+#   (-1, -0.5)     e^-0.5   +0.6065   +0.8    +0.8        1     0     (lower clip, A < 0)
+#   (+2, 0)        1        -2        -2      -2          0     0     (inside the trust region)
+# Every mean is masked_mean = masked sum / (mask count + 1e-8) (torch_functional.py:171-185).
+_N4 = 4 + 1e-8
+POLICY_CASE = dict(
+    adv=[1.0, -1.0, -1.0, 2.0],
+    d_lp=[0.5, 1.5, -0.5, 0.0],
+    per_token=[-1.2, 3.0, 0.8, -2.0],
+    pg_loss=(-1.2 + 3.0 + 0.8 - 2.0) / _N4,  # token-mean: 0.15
+    clipfrac=2 / _N4,
+    clipfrac_lower=1 / _N4,
+    ppo_kl=-(0.5 + 1.5 - 0.5 + 0.0) / _N4,  # masked_mean(-(lp - old)): -0.375
+    # d pg_loss / d lp (token-mean over 4): only the unclipped branches carry the ratio's gradient:
+    # case 1 clipped (0), case 2 the constant dual bound (0), case 3 clipped (0), case 4 -A r / 4
+    # (at r = 1 l1 == l2: torch.maximum splits the gradient, both halves -A r)
+    dlp=[0.0, 0.0, 0.0, -2.0 * 1.0 / _N4],
+)
+
+# lp - old is clamped to [-20, 20] before exp AND before the KL metric (core_algos.py:766-770):
+# lp - old = 25 with A = -1 gives r = e^20, l1 = e^20 > 3, so the dual clip yields 3, clipfrac_lower 1,
+# and ppo_kl = masked_mean(-clamped) = -20, not -25
+_N1 = 1 + 1e-8
+CLAMP_CASE = dict(adv=[-1.0], d_lp=[25.0], pg_loss=3.0 / _N1, clipfrac=0.0, clipfrac_lower=1.0 / _N1,
+                  ppo_kl=-20.0 / _N1)
+
+# ---- agg_loss, core_algos.py:686-719 ----
+AGG_LOSS = [[1.0, 2.0, 3.0], [4.0, 5.0, 6.0]]
+AGG_MASK = [[1, 1, 0], [1, 0, 0]]
+AGG_WANT = {
+    "token-mean": (1 + 2 + 4) / (3 + 1e-8),  # masked_mean
+    "seq-mean-token-sum": (3 + 4) / 2,  # mean over rows of the row sums
+    "seq-mean-token-mean": (3 / 2 + 4 / 1) / 2,  # mean over rows of the row means
+    "seq-mean-token-sum-norm": (3 + 4) / 3,  # total / the mask's last dim (3)
+}
+
+# ---- kl_penalty, core_algos.py:1034-1069 (logprob, ref_logprob) -> value ----
+#   k1 = lp - ref; abs = |lp - ref|; k2 = (lp - ref)^2 / 2; k3: k = clamp(ref - lp, -20, 20),
+#   clamp(e^k - k - 1, -10, 10)
+KL_LP = [0.0, -1.0, 0.0, -30.0]
+KL_REF = [-1.0, 0.0, 0.0, 0.0]
+KL_WANT = {
+    "kl": [1.0, -1.0, 0.0, -30.0],
+    "abs": [1.0, 1.0, 0.0, 30.0],
+    "mse": [0.5, 0.5, 0.0, 450.0],
+    "low_var_kl": [1 / E, E - 2.0, 0.0, 10.0],  # k = -1: e^-1; k = 1: e - 2; k = 20 (clamped): 10
+}
+
+# ---- masked_whiten, torch_functional.py:206-223: unbiased variance, rsqrt(var + 1e-8) ----
+WHITEN_X = [1.0, 2.0, 3.0, 4.0, 100.0]
+WHITEN_MASK = [1, 1, 1, 1, 0]
+# mean 2.5; unbiased var = (2.25 + 0.25 + 0.25 + 2.25) / 3 = 5 / 3
+# (masked_mean's 1e-8: mean = 10 / (4 + 1e-8); masked_var's own bias correction n / (n - 1))
+_MU = 10 / (4 + 1e-8)
+_VAR = sum((x - _MU) ** 2 for x in WHITEN_X[:4]) / (4 + 1e-8) * 4 / 3
+WHITEN_WANT = [(x - _MU) / math.sqrt(_VAR + 1e-8) for x in WHITEN_X]
+
+# ---- GRPO outcome advantage, core_algos.py:246-308 (epsilon 1e-6) ----
+# group "a": scores 1, 0, 0, 1 -> mean 0.5, unbiased std sqrt(1/3); group "b": singleton -> (0, 1)
+GRPO_SCORES = [1.0, 0.0, 0.0, 1.0, 5.0]
+GRPO_UID = ["a", "a", "a", "a", "b"]
+_S = math.sqrt(1 / 3)
+GRPO_WANT = [0.5 / (_S + 1e-6), -0.5 / (_S + 1e-6), -0.5 / (_S + 1e-6), 0.5 / (_S + 1e-6), 5.0 / (1.0 + 1e-6)]
+GRPO_NOSTD_WANT = [0.5, -0.5, -0.5, 0.5, 5.0]  # Dr.GRPO: scores - mean (singleton mean 0)

@@ -167,3 +167,51 @@ def test_value_loss_kats():
     loss, frac = ref.compute_value_loss(vp, ret, vp.clone(), torch.ones(3, 5), 0.2)
     assert frac.item() == 0.0
     assert torch.allclose(loss, 0.5 * ((vp - ret) ** 2).mean(), atol=1e-6)
+
+
+# --- hand-derived known answers (tests/kat_cases.py): the oracle against values worked out by hand -
+def _kt(x, dtype=torch.float64):
+    return torch.tensor(x, dtype=dtype)
+
+
+@pytest.mark.parametrize("shape", [(1, 4), (4, 1), (2, 2)])
+def test_dual_clip_policy_loss_hand_kat(shape):
+    from tests import kat_cases as C
+
+    c = C.POLICY_CASE
+    old = torch.zeros(4, dtype=torch.float64)
+    lp = _kt(c["d_lp"]).requires_grad_(True)
+    adv = _kt(c["adv"])
+    m = torch.ones(4, dtype=torch.float64)
+    pg, cf, kl, cfl = ref.compute_policy_loss(old.view(shape), lp.view(shape), adv.view(shape), m.view(shape),
+                                              cliprange=0.2, clip_ratio_c=3.0)
+    assert abs(pg.item() - c["pg_loss"]) < 1e-12
+    assert abs(cf.item() - c["clipfrac"]) < 1e-12 and abs(cfl.item() - c["clipfrac_lower"]) < 1e-12
+    assert abs(kl.item() - c["ppo_kl"]) < 1e-12
+    pg.backward()
+    assert torch.allclose(lp.grad, _kt(c["dlp"]), atol=1e-12)
+    c = C.CLAMP_CASE
+    pg, cf, kl, cfl = ref.compute_policy_loss(torch.zeros(1, 1, dtype=torch.float64), _kt([c["d_lp"]]),
+                                              _kt([c["adv"]]), torch.ones(1, 1, dtype=torch.float64), cliprange=0.2)
+    got = (pg.item(), cf.item(), cfl.item(), kl.item())
+    assert np.allclose(got, (c["pg_loss"], c["clipfrac"], c["clipfrac_lower"], c["ppo_kl"]), rtol=1e-14, atol=0)
+
+
+def test_agg_kl_whiten_grpo_hand_kats():
+    from tests import kat_cases as C
+
+    for mode, want in C.AGG_WANT.items():
+        assert abs(ref.agg_loss(_kt(C.AGG_LOSS), _kt(C.AGG_MASK), mode).item() - want) < 1e-12, mode
+    for kt, want in C.KL_WANT.items():
+        got = ref.kl_penalty(_kt(C.KL_LP), _kt(C.KL_REF), kt)
+        assert torch.allclose(got, _kt(want), atol=1e-12, rtol=1e-12), kt
+    got = ref.masked_whiten(_kt(C.WHITEN_X), _kt(C.WHITEN_MASK))
+    assert torch.allclose(got, _kt(C.WHITEN_WANT), atol=1e-12)
+    rew = torch.zeros(5, 3, dtype=torch.float32)
+    rew[:, 1] = torch.tensor(C.GRPO_SCORES)
+    mask = torch.ones(5, 3)
+    adv, _ = ref.compute_grpo_outcome_advantage(rew.clone(), mask, np.array(C.GRPO_UID, dtype=object))
+    assert torch.allclose(adv[:, 0], torch.tensor(C.GRPO_WANT), atol=1e-6)
+    adv, _ = ref.compute_grpo_outcome_advantage(rew.clone(), mask, np.array(C.GRPO_UID, dtype=object),
+                                                norm_adv_by_std_in_grpo=False)
+    assert torch.allclose(adv[:, 0], torch.tensor(C.GRPO_NOSTD_WANT), atol=1e-7)
