@@ -172,6 +172,8 @@ def parse(argv=None):
                     help="1: backbone weight gradients + fp32 accumulation on a side stream (wgrad_side_stream)")
     ap.add_argument("--fused-no-grad", type=int, default=1, choices=[0, 1],
                     help="1: the no-grad old-logp pass runs the fused lm_head + log-prob kernel (f1, fused_logprob_no_grad)")
+    ap.add_argument("--fused-mlp-no-grad", type=int, default=0, choices=[0, 1],
+                    help="1: the no-grad old-logp pass runs gate|up + SwiGLU as one kernel (fused_mlp_no_grad)")
     ap.add_argument("--f1-after-backbone", type=int, default=1, choices=[0, 1],
                     help="1: the no-grad pass runs every micro-batch's backbone, then the fused lm_head launches back "
                          "to back (fused_lm_head_after_backbone); 0: backbone + lm_head per micro-batch")
@@ -507,6 +509,7 @@ def main():
             pack_pad_multiple=args.pad_multiple,
             logprob_inplace_backward={0: False, 1: True, 2: "auto"}[args.logprob_inplace_bwd],
             fused_logprob_no_grad=bool(args.fused_no_grad),
+            fused_mlp_no_grad=bool(args.fused_mlp_no_grad),
             fused_lm_head_after_backbone=bool(args.f1_after_backbone),
             fused_lm_head_concat=bool(args.f1_concat),
             use_fused_kernels=bool(args.fused_kernels),
@@ -716,7 +719,9 @@ def main():
                           f"reference ({lp_fallbacks} in-place fallbacks in the timed steps)"}[args.logprob_inplace_bwd]
                     + ("; the no-grad old-logp pass runs the fused lm_head + log-prob kernel (the reference's "
                        "use_fused_kernels option, off by default there; same bf16-rounded logits, tests)"
-                       if args.fused_no_grad else "")),
+                       if args.fused_no_grad else "")
+                    + ("; the no-grad pass runs gate|up + SwiGLU as one kernel (own GEMM summation order: hidden "
+                       "states equal the unfused forward to bf16 rounding, tests)" if args.fused_mlp_no_grad else "")),
                 "dynamic_bsz_max_token_len": args.dynamic_bsz or None,
                 "compute_max_token_len": args.compute_max_tokens or None,
                 "logprob_max_token_len": (args.logprob_max_tokens or args.dynamic_bsz) if args.dynamic_bsz else None,
@@ -725,6 +730,7 @@ def main():
                 "logprob_inplace_backward": {0: False, 1: True, 2: "auto"}[args.logprob_inplace_bwd],
                 "logprob_bwd_inplace_fallbacks": lp_fallbacks,
                 "fused_logprob_no_grad": bool(args.fused_no_grad),
+                "fused_mlp_no_grad": bool(args.fused_mlp_no_grad),
                 "fused_lm_head_after_backbone": bool(args.f1_after_backbone),
                 "fused_lm_head_concat": bool(args.f1_concat),
                 "use_fused_kernels": bool(args.fused_kernels),

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define VA_ABI_VERSION 6
+#define VA_ABI_VERSION 7
 
 /* error codes */
 #define VA_OK 0
@@ -374,6 +374,15 @@ int va_swiglu_fwd(const void *gu, int64_t ldgu, int64_t uoff, int dtype, int64_t
                   void *stream);
 int va_swiglu_bwd(const void *dy, const void *gu, int64_t ldgu, int64_t uoff, int dtype, int64_t T, int64_t F,
                   void *dgu, int64_t lddgu, int64_t duoff, void *stream);
+/* gate_up_swiglu (ABI 7): y [T, F] (row stride ldy >= F, % 4, 8-byte aligned) = swiglu of the merged
+ * gate|up projection x [T, H] . w_gate_up [2F, H]^T (gate rows 0..F-1, up rows F..2F-1; row strides ldx /
+ * ldw, 16-byte aligned) without writing the [T, 2F] projection: g / u rounded to bf16 as the GEMM's
+ * output, then swiglu_fwd's arithmetic. H % 64 == 0, F % 128 == 0; `splits` feature ranges per 256-token
+ * block (1..64). For the no-grad forward (nothing keeps the projection for a backward); no reference
+ * counterpart: HF Qwen2MLP's act_fn(gate_proj(x)) * up_proj(x) under the actor's no-grad old-logp pass,
+ * dp_actor.py:331-333 (compute_log_prob's torch.no_grad forward). Not a §8 row. */
+int va_gate_up_swiglu(const void *x, int64_t ldx, const void *w_gate_up, int64_t ldw, int dtype, int64_t T,
+                      int64_t H, int64_t F, int splits, void *y, int64_t ldy, void *stream);
 int va_rope_qkv_fwd(const void *qkv, int64_t ld, const void *cos, const void *sin, int dtype, int64_t T,
                     int64_t Hq, int64_t Hk, int64_t D, void *q, void *k, void *v, void *stream);
 int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *cos, const void *sin, int dtype,

@@ -328,3 +328,112 @@ def test_merged_linear_bias_gradient_uses_column_sum():
     y.backward(dy)
     assert torch.equal(b.grad, K.column_sum(dy))
     assert (b.grad.double() - dy.double().sum(0)).abs().max().item() < 0.1
+
+
+def _exact_operands(T, H, F_, ldx=None, seed=0):
+    """Integer-valued x and w / 8: every partial sum of x w^T is exact in fp32, so any summation order
+    gives the same projection (and the same bf16 rounding of it)."""
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    xs = torch.randint(-2, 3, (T, ldx or H), device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randint(-3, 4, (2 * F_, H), device=DEV, generator=g).float() / 8).to(torch.bfloat16)
+    return xs[:, :H], w
+
+
+@pytest.mark.parametrize("T,H,F_,ldx,splits", [(1000, 896, 4864, None, None), (256, 64, 128, None, 1),
+                                                (517, 256, 512, 320, 3), (3, 128, 256, None, 64),
+                                                (4096, 896, 4864, None, 19)])
+def test_gate_up_swiglu_bitwise_on_exact_data(T, H, F_, ldx, splits):
+    """va_gate_up_swiglu == merged GEMM (hipBLASLt) + swiglu_merged, bit for bit, when the projection is
+    exact: the same bf16 rounding points and per-element arithmetic; ragged token tails, a strided x,
+    feature ranges per token block from 1 to the tile count."""
+    from verl_amd import kernels as K
+
+    x, w = _exact_operands(T, H, F_, ldx, seed=T + F_)
+    with torch.no_grad():
+        want = K.swiglu_merged(x @ w.t())
+        got = K.gate_up_swiglu(x, w, splits=splits)
+    assert got.shape == (T, F_)
+    assert torch.equal(got, want)
+
+
+def test_gate_up_swiglu_random_vs_fp32():
+    """Random operands: within bf16 rounding of silu(g) * u from an fp32 GEMM (tolerance: 2 bf16 ulp on
+    all but 1e-3 of the elements, i.e. the product's own rounding points)."""
+    from verl_amd import kernels as K
+
+    torch.manual_seed(11)
+    T, H, F_ = 3000, 896, 4864
+    x = torch.randn(T, H, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(2 * F_, H, device=DEV) * 0.05).to(torch.bfloat16)
+    with torch.no_grad():
+        gu = x.float() @ w.float().t()
+        ref = F.silu(gu[:, :F_].to(torch.bfloat16).float()).to(torch.bfloat16).float() * gu[:, F_:].to(torch.bfloat16).float()
+        got = K.gate_up_swiglu(x, w)
+        unfused = K.swiglu_merged(x @ w.t())
+    _ulp_close(got, ref, n_ulp=4, what="gate_up_swiglu vs fp32")
+    _ulp_close(got, unfused, n_ulp=4, what="gate_up_swiglu vs unfused")
+
+
+def test_gate_up_swiglu_contract():
+    from verl_amd import kernels as K
+
+    x = torch.randn(64, 128, device=DEV).to(torch.bfloat16)
+    w = torch.randn(2 * 256, 128, device=DEV).to(torch.bfloat16)
+    with torch.no_grad():
+        assert K.gate_up_swiglu(x[:0], w).shape == (0, 256)
+        with pytest.raises(ValueError, match="unsupported"):
+            K.gate_up_swiglu(x, w[: 2 * 192])  # F % 128 != 0
+    with pytest.raises(RuntimeError, match="forward-only"):
+        K.gate_up_swiglu(x.requires_grad_(True), w)
+    assert not K.gate_up_swiglu_supported(x[:, :96], w[:, :96])
+
+
+@pytest.mark.parametrize("family", ["qwen2", "llama"])
+def test_fused_mlp_no_grad_pass(family):
+    """fused_mlp_no_grad: compute_log_prob's packed forward runs va_gate_up_swiglu (and only there:
+    the update pass keeps the merged GEMM + swiglu for its backward); log-probs match the unfused
+    no-grad pass to bf16 rounding."""
+    from verl_amd import kernels as K
+    from verl_amd.utils.config import actor_config
+    from verl_amd.utils.model import build_llama, build_qwen2
+    from verl_amd.utils.synthetic import make_grpo_batch
+    from verl_amd.workers.actor import DataParallelPPOActor, attention
+
+    if not attention.varlen_available(DEV):
+        pytest.skip("flash varlen unavailable")
+    if family == "qwen2":
+        base = build_qwen2("tiny", device=DEV, attn_implementation="sdpa", seed=5, intermediate_size=384)
+    else:
+        base = build_llama("tiny", device=DEV, attn_implementation="sdpa", seed=5)
+    for p in base.parameters():
+        p.data = p.data.to(torch.bfloat16)
+    data = make_grpo_batch(n_prompts=2, n=4, prompt_len=20, response_len=30, vocab=4096, min_prompt=3,
+                           dense_responses=False, min_response=5, seed=6, device=DEV)
+    data.meta_info.update(micro_batch_size=4, temperature=1.0, use_dynamic_bsz=False)
+    calls = []
+    orig = K.gate_up_swiglu
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    out = {}
+    try:
+        K.gate_up_swiglu = spy
+        for fused in (False, True):
+            m = copy.deepcopy(base)
+            a = DataParallelPPOActor(actor_config(use_remove_padding=True, fused_mlp_no_grad=fused), m,
+                                     torch.optim.SGD(m.parameters(), lr=0.0))
+            n0 = len(calls)
+            lp, ent = a.compute_log_prob(data, calculate_entropy=True)
+            n_nograd = len(calls) - n0
+            e, lp2 = a._forward_micro_batch(data.batch, 1.0, calculate_entropy=False)
+            (lp2 * data.batch["response_mask"]).sum().backward()
+            assert len(calls) - n0 == n_nograd, "the fused MLP ran under autograd"
+            assert (n_nograd > 0) == fused, n_nograd
+            out[fused] = (lp, ent)
+    finally:
+        K.gate_up_swiglu = orig
+    msk = data.batch["response_mask"].bool()
+    assert torch.allclose(out[True][0][msk], out[False][0][msk], atol=3e-2, rtol=2e-2)
+    assert torch.allclose(out[True][1][msk], out[False][1][msk], atol=3e-2, rtol=2e-2)

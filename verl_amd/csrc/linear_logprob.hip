@@ -252,8 +252,15 @@ constexpr int T_TILE = TB * TK;  // bf16 elements of one operand's K-step image
 
 __device__ __forceinline__ int t_img_off(int row, int c) { return row * TK + ((c ^ ((row >> 1) & 7)) << 3); }
 
+// image row -> source row of the streamed (weight) operand: the identity for the lm_head; the gate|up
+// pairing (GateUpRows below) for the fused SwiGLU projection
+struct IdentityRows {
+  __device__ __forceinline__ int64_t operator()(int64_t r) const { return r; }
+};
+
+template <typename RowMap = IdentityRows>
 __device__ __forceinline__ void t_stage(const uint16_t *__restrict__ src, int64_t row0, int64_t nrows, int64_t ld,
-                                        int k0, uint16_t *img, int wave, int lane) {
+                                        int k0, uint16_t *img, int wave, int lane, const RowMap &rmap = RowMap{}) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int g = wave * 4 + i;  // 32 groups of 8 rows (1 KB each)
@@ -261,6 +268,7 @@ __device__ __forceinline__ void t_stage(const uint16_t *__restrict__ src, int64_
     const int lc = (lane & 7) ^ ((row >> 1) & 7);
     int64_t gr = row0 + row;
     if (gr >= nrows) gr = nrows - 1;  // clamped rows / columns are computed and discarded
+    gr = rmap(gr);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + gr * ld + k0 + lc * 8), img + g * 8 * TK,
                                      16, 0, 0);
   }
@@ -338,11 +346,11 @@ __device__ __forceinline__ void t_tile_epilogue(const f32x4 (&acc)[8][4], int v0
 // of [vt_begin, vt_end) it accumulates S^T = W_tile . H_tile^T (256 vocab x 256 tokens) over K in acc,
 // calls tile(acc, vt) once the tile is complete, and zeroes acc. acc[i][j][e] holds vocab
 // vt * 256 + wr * 128 + (lane >> 4) * 4 + i * 16 + e for token row0 + wc * 64 + j * 16 + (lane & 15).
-template <typename Tile>
+template <typename Tile, typename WMap = IdentityRows>
 __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int64_t ldh,
                                            const uint16_t *__restrict__ w, int64_t ldw, int64_t N, int K, int64_t V,
                                            int64_t row0, int64_t vt_begin, int64_t vt_end, uint16_t *lds, int wave,
-                                           int lane, Tile &&tile) {
+                                           int lane, Tile &&tile, const WMap &wmap = WMap{}) {
   const int wr = wave >> 2, wc = wave & 3;
   const int nk = K / TK;
   const int64_t nsteps = vt_begin < vt_end ? (vt_end - vt_begin) * nk : 0;
@@ -353,7 +361,7 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (nsteps > 0) {
-    t_stage(w, vt_begin * TB, V, ldw, 0, lds, wave, lane);
+    t_stage(w, vt_begin * TB, V, ldw, 0, lds, wave, lane, wmap);
     t_stage(hid, row0, N, ldh, 0, lds + T_TILE, wave, lane);
   }
   __builtin_amdgcn_s_waitcnt(0);
@@ -367,7 +375,7 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
     if (st + 1 < nsteps) {
       uint16_t *na = lds + (buf ^ 1) * 2 * T_TILE;
       const int k1 = static_cast<int>((st + 1) % nk) * TK;
-      t_stage(w, (vt_begin + (st + 1) / nk) * TB, V, ldw, k1, na, wave, lane);
+      t_stage(w, (vt_begin + (st + 1) / nk) * TB, V, ldw, k1, na, wave, lane, wmap);
       t_stage(hid, row0, N, ldh, k1, na + T_TILE, wave, lane);
     }
 #pragma unroll
@@ -608,6 +616,66 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
   });
 }
 
+// ------------------------------------------------------------------ gate|up projection + SwiGLU
+// The merged gate|up GEMM of a SiLU MLP with its SwiGLU applied in the epilogue: y = bf16(bf16(silu(g))
+// * u), g / u = bf16 of the [T, 2F] projection x . W^T (W = [gate rows F | up rows F]), so the [T, 2F]
+// projection never reaches HBM (the no-grad pass of the actor's old-logp forward, where nothing keeps
+// it for a backward). The same transposed sweep as f1 with the feature index as the MFMA row: a
+// 256-row weight image of tile t holds, per wave-row wr, gate features t 128 + wr 64 + [0, 64) in its
+// blocks i = 0..3 and the SAME features' up rows in blocks 4..7, so acc[i][j][e] and acc[i + 4][j][e]
+// are the gate and up of one (feature, token) in one lane: the epilogue is elementwise, each lane
+// storing 4 consecutive features of a token (8 bytes) per (i, j). Per element the arithmetic of
+// swiglu_fwd (model_ops.hip), so on exact-arithmetic data the output equals GEMM + swiglu bitwise.
+struct GateUpRows {
+  int64_t F;
+  __device__ __forceinline__ int64_t operator()(int64_t r) const {
+    const int64_t t = r >> 8;  // 256 image rows per 128 features
+    const int q = static_cast<int>(r & 127), blk = q >> 4;
+    const int64_t f = t * 128 + ((r >> 7) & 1) * 64 + (blk & 3) * 16 + (q & 15);
+    return blk >= 4 ? F + f : f;
+  }
+};
+
+template <bool REMAP>
+__global__ __launch_bounds__(T_THREADS, 1) void gate_up_swiglu_t256_kernel(
+    const uint16_t *__restrict__ x, int64_t ldx, const uint16_t *__restrict__ w, int64_t ldw, int64_t T, int K,
+    int64_t F, int splits, int tiles_per_split, uint16_t *__restrict__ y, int64_t ldy) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  int64_t row0, sp, vt_begin, vt_end;
+  t256_block<REMAP>(splits, tiles_per_split, 2 * F, row0, sp, vt_begin, vt_end);
+  uint16_t *yrow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t r = row0 + wc * 64 + j * 16 + (lane & 15);
+    yrow[j] = r < T ? y + r * ldy : nullptr;
+  }
+  t256_sweep(
+      x, ldx, w, ldw, T, K, 2 * F, row0, vt_begin, vt_end, lds, wave, lane,
+      [&](f32x4(&acc)[8][4], int64_t vt) {
+        const int64_t f0 = vt * 128 + wr * 64 + (lane >> 4) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (yrow[j] == nullptr) continue;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float g = round_bf16(acc[i][j][e]), u = round_bf16(acc[i + 4][j][e]);
+              o[e] = round_bf16(va_silu(g)) * u;
+            }
+            uint2 q;
+            q.x = pack2_bf16(o[0], o[1]);
+            q.y = pack2_bf16(o[2], o[3]);
+            *reinterpret_cast<uint2 *>(yrow[j] + f0 + i * 16) = q;
+          }
+        }
+      },
+      GateUpRows{F});
+}
+
 }  // namespace
 }  // namespace va
 
@@ -760,4 +828,36 @@ extern "C" int va_linear_logprob_bwd(const void *hidden, int64_t ldh, const void
                                      H, Vr, V, v_begin, used, per, temperature, d16, ldd);
   }
   return check_launch("linear_logprob_bwd");
+}
+
+extern "C" int va_gate_up_swiglu(const void *x, int64_t ldx, const void *w_gate_up, int64_t ldw, int dtype, int64_t T,
+                                 int64_t H, int64_t F, int splits, void *y, int64_t ldy, void *stream) {
+  VA_CHECK_ARG(dtype == VA_BF16, "gate_up_swiglu: only bf16 is implemented");
+  VA_CHECK_ARG(T >= 0 && H > 0 && H % TK == 0 && H <= (1 << 20) && F > 0 && F % 128 == 0 && F < (int64_t{1} << 30),
+               "gate_up_swiglu: need H %% 64 == 0 and F %% 128 == 0 (H=%lld, F=%lld)", static_cast<long long>(H),
+               static_cast<long long>(F));
+  VA_CHECK_ARG(ldx >= H && ldw >= H && ldx % 8 == 0 && ldw % 8 == 0 && ldy >= F && ldy % 4 == 0,
+               "gate_up_swiglu: strides must be >= H (ldy >= F), %% 8 (ldy %% 4)");
+  VA_CHECK_ARG(splits >= 1 && splits <= 64, "gate_up_swiglu: splits in [1, 64]");
+  if (T == 0) return VA_OK;
+  VA_CHECK_ARG(x && w_gate_up && y, "null pointer argument");
+  VA_CHECK_ARG(reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(w_gate_up) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(y) % 8 == 0,
+               "gate_up_swiglu: 16-byte aligned x / weight and 8-byte aligned y required");
+  const int64_t n_vt = F / 128;  // 256 image rows (128 gate + 128 up) per tile
+  const int per = static_cast<int>((n_vt + splits - 1) / splits);
+  const int used = static_cast<int>((n_vt + per - 1) / per);
+  const int64_t nwg = ((T + TB - 1) / TB) * used;
+  VA_CHECK_ARG(nwg < (int64_t{1} << 31), "gate_up_swiglu: grid too large");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const auto *x16 = static_cast<const uint16_t *>(x);
+  const auto *w16 = static_cast<const uint16_t *>(w_gate_up);
+  auto *y16 = static_cast<uint16_t *>(y);
+  if (nwg % 8 == 0)
+    hipLaunchKernelGGL(gate_up_swiglu_t256_kernel<true>, dim3(static_cast<unsigned>(nwg)), dim3(T_THREADS), 0, s, x16,
+                       ldx, w16, ldw, T, static_cast<int>(H), F, used, per, y16, ldy);
+  else
+    hipLaunchKernelGGL(gate_up_swiglu_t256_kernel<false>, dim3(static_cast<unsigned>(nwg)), dim3(T_THREADS), 0, s,
+                       x16, ldx, w16, ldw, T, static_cast<int>(H), F, used, per, y16, ldy);
+  return check_launch("gate_up_swiglu");
 }

@@ -236,7 +236,7 @@ __global__ __launch_bounds__(256) void colsum_rows_kernel(const uint16_t *__rest
 // gate / up are rows of a merged [T, ldgu] projection output (u at column offset `uoff`, so the
 // plain two-tensor case is ldgu = F, uoff = u - g); y is [T, F].  Backward writes dg / du into the
 // same merged layout (the gradient of the merged gate|up GEMM).
-__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+__device__ __forceinline__ float silu(float g) { return va_silu(g); }  // va_common.h
 
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const uint16_t *__restrict__ gu, int64_t ldgu,
                                                          int64_t uoff, int64_t T, int F,
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const uint16_t *__restr
     unpack8(ld16(gr + uoff), u8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float s = 1.f / (1.f + __expf(-g8[e]));
+      const float s = va_sigmoid(g8[e]);
       ru[e] = d8[e] * rbf(g8[e] * s);
       rg[e] = d8[e] * u8[e] * (s * (1.f + g8[e] * (1.f - s)));
     }
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_stream_kernel(const uint16_t *
     unpack8(ru[u], u8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float s = 1.f / (1.f + __expf(-g8[e]));
+      const float s = va_sigmoid(g8[e]);
       ou[e] = d8[e] * rbf(g8[e] * s);
       og[e] = d8[e] * u8[e] * (s * (1.f + g8[e] * (1.f - s)));
     }

@@ -34,6 +34,12 @@ __device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(va_f32x2{a, b}, va_bf16x2));
 }
 __device__ __forceinline__ float round_to_bf16(float x) { return __uint_as_float(pack2_bf16(x, 0.f) << 16); }
+// logistic sigmoid and SiLU as every SwiGLU kernel computes them (forward, backward, the fused gate|up
+// epilogue: one definition, so they agree bitwise): v_exp_f32 (__expf) and the hardware reciprocal
+// v_rcp_f32 (1 ulp) instead of an IEEE division, whose div_scale / div_fmas / div_fixup expansion costs
+// ~6 VALU slots more per element (hidden in the streaming kernels, not in an MFMA epilogue)
+__device__ __forceinline__ float va_sigmoid(float g) { return __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
+__device__ __forceinline__ float va_silu(float g) { return g * va_sigmoid(g); }
 __device__ __forceinline__ float f16_to_f32(uint16_t h) {
   return static_cast<float>(__builtin_bit_cast(_Float16, h));
 }

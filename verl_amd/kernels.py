@@ -719,6 +719,48 @@ def swiglu_merged(gu):
     return _SwiGLU.apply(gu, gu.shape[1] // 2)
 
 
+def _gate_up_swiglu_splits(n_rows: int, n_tiles: int) -> int:
+    """Feature ranges per 256-token block of va_gate_up_swiglu (n_tiles = F / 128): as f1's heuristic,
+    ~4,096 workgroups; VERL_AMD_GATE_UP_SPLITS overrides."""
+    env = os.environ.get("VERL_AMD_GATE_UP_SPLITS")
+    if env:
+        s = int(env)
+    else:
+        blocks = max(1, (n_rows + 255) // 256)
+        s = -(-4096 // blocks)
+    return int(max(1, min(64, n_tiles, s)))
+
+
+def gate_up_swiglu_supported(x, w_gate_up) -> bool:
+    """Shapes / layouts va_gate_up_swiglu takes: bf16 on the device, H % 64 == 0, F % 128 == 0."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w_gate_up.dtype == torch.bfloat16 and x.dim() == 2
+            and w_gate_up.dim() == 2 and x.shape[1] == w_gate_up.shape[1] and x.shape[1] % 64 == 0
+            and w_gate_up.shape[0] % 256 == 0 and x.stride(-1) == 1 and w_gate_up.stride(-1) == 1
+            and x.stride(0) % 8 == 0 and w_gate_up.stride(0) % 8 == 0
+            and x.data_ptr() % 16 == 0 and w_gate_up.data_ptr() % 16 == 0)
+
+
+def gate_up_swiglu(x, w_gate_up, splits: int | None = None):
+    """silu(x W_g^T) * (x W_u^T) for the merged gate|up weight [2F, H] in ONE kernel (no [T, 2F]
+    projection in HBM): the no-grad forward only (raises under autograd: the backward needs the
+    projection). Same bf16 rounding points as merged_linear + swiglu_merged; the GEMM's summation
+    order is its own (tests/test_model_ops_gpu.py: bitwise on exact-arithmetic data)."""
+    _require_device(x, w_gate_up)
+    _bf16_only(x, w_gate_up)
+    if torch.is_grad_enabled() and (x.requires_grad or w_gate_up.requires_grad):
+        raise RuntimeError("gate_up_swiglu is forward-only: use merged_linear + swiglu_merged under autograd")
+    if not gate_up_swiglu_supported(x, w_gate_up):
+        raise ValueError(f"gate_up_swiglu: unsupported operands x {tuple(x.shape)} / w {tuple(w_gate_up.shape)} "
+                         "(need bf16, H % 64 == 0, F % 128 == 0, unit inner stride, 16-byte alignment)")
+    T, H = x.shape
+    F = w_gate_up.shape[0] // 2
+    y = torch.empty(T, F, dtype=x.dtype, device=x.device)
+    s = _gate_up_swiglu_splits(T, F // 128) if splits is None else int(splits)
+    L.call("va_gate_up_swiglu", _p(x), x.stride(0), _p(w_gate_up), w_gate_up.stride(0), L.VA_BF16, T, H, F, s, _p(y),
+           F, _stream(x))
+    return y
+
+
 def swiglu(gate, up):
     """silu(gate) * up for separate gate / up tensors of the same shape (bf16)."""
     _require_device(gate, up)

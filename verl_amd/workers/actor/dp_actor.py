@@ -292,6 +292,8 @@ class DataParallelPPOActor(BasePPOActor):
         # gfx950 flash-attention forward (attention.hip) inside the fused packed backbone
         self.fused_attention = self.config.get("fused_attention", True)
         self.fused_logprob_no_grad = self.config.get("fused_logprob_no_grad", False)
+        # no-grad passes: gate|up GEMM + SwiGLU as one kernel (qwen2_fused.packed_forward fuse_mlp)
+        self.fused_mlp_no_grad = bool(self.config.get("fused_mlp_no_grad", False))
         # no-grad passes with the fused lm_head: run all micro-batches' backbones, then the lm_head
         # launches back to back (compute_log_prob)
         self.fused_lm_head_after_backbone = bool(self.config.get("fused_lm_head_after_backbone", True))
@@ -408,7 +410,8 @@ class DataParallelPPOActor(BasePPOActor):
             hidden = packed_forward(self._backbone, ids, pos, packing.cu_seqlens, packing.max_seqlen,
                                     attn_blocks=packing.attn_blocks if fa else None,
                                     attn_kblocks=packing.attn_kblocks if fa else None,
-                                    multi_modal_inputs=multi_modal_inputs)
+                                    multi_modal_inputs=multi_modal_inputs,
+                                    fuse_mlp=self.fused_mlp_no_grad and not torch.is_grad_enabled())
         else:
             hidden = hf_packed_hidden(self._backbone, ids, pos, packing, multi_modal_inputs)
         h_sel = hidden.index_select(0, packing.sel_hidden)

@@ -9,7 +9,8 @@ through one function that owns the layer loop, so that per decoder layer the wor
   rope_qkv   (split q/k/v into flash varlen's [T, H, D] layout + rotary, one kernel)
   flash varlen attention, o_proj GEMM
   add_rmsnorm (residual add + post_attention_layernorm)
-  gate|up as ONE GEMM, swiglu on the merged output (one kernel), down GEMM
+  gate|up as ONE GEMM, swiglu on the merged output (one kernel), down GEMM — in a no-grad forward
+  (the old-logp pass) gate|up + swiglu are ONE kernel (va_gate_up_swiglu: no [T, 2F] projection)
 
 instead of the ~45 PyTorch kernels HF issues (norm chains, adds, transposes, rotary, bias
 reductions x3). Forward numerics keep HF's bf16 rounding points (see csrc/model_ops.hip), so
@@ -201,12 +202,25 @@ def _attention(attn, y, cos, sin, cu, max_len, hq, hk, d, attn_blocks=None, attn
     return o(out.reshape(T, hq * d))
 
 
+def _mlp_activation(mlp, y, fuse: bool):
+    """silu(gate_proj(y)) * up_proj(y): one fused kernel in the no-grad forward when the shapes allow
+    (and the projections carry no bias), else the merged GEMM + the SwiGLU kernel."""
+    lins = [mlp.gate_proj, mlp.up_proj]
+    if fuse and lins[0].bias is None:
+        w_all = _merged(mlp, "gate_up.w", [lin.weight for lin in lins])
+        if K.gate_up_swiglu_supported(y, w_all):
+            return K.gate_up_swiglu(y, w_all)
+    return K.swiglu_merged(_merged_linear(mlp, "gate_up", y, lins))
+
+
 def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor, cu_seqlens: torch.Tensor,
                    max_seqlen: int, attn_blocks: torch.Tensor = None, attn_kblocks: torch.Tensor = None,
-                   multi_modal_inputs: list = None) -> torch.Tensor:
+                   multi_modal_inputs: list = None, fuse_mlp: bool = False) -> torch.Tensor:
     """input_ids [T] and position_ids [T] (or [3, T], mrope) packed, cu_seqlens [B+1] int32 -> last
     hidden state [T, H] bf16 (after the final norm), i.e. Qwen2Model(...).last_hidden_state[0] on
-    the same packing."""
+    the same packing. ``fuse_mlp``: outside autograd, gate|up + SwiGLU run as one kernel
+    (va_gate_up_swiglu; its GEMM sums in its own order, so the hidden states match the unfused
+    forward to bf16 rounding, not bitwise)."""
     stack = text_backbone(backbone)
     cfg = stack.config
     hq = cfg.num_attention_heads
@@ -215,6 +229,7 @@ def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor
     x = input_embeddings(backbone, input_ids, multi_modal_inputs)  # [T, H]
     cos, sin = rotary(stack, x, position_ids)  # [1, T, D] bf16
     residual = x
+    fuse_mlp = bool(fuse_mlp) and not torch.is_grad_enabled()
     layers = stack.layers[: cfg.num_hidden_layers]
     h = None
     for i, layer in enumerate(layers):
@@ -227,9 +242,8 @@ def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor
         ln = layer.post_attention_layernorm
         residual, y = K.add_rmsnorm(a, residual, ln.weight, ln.variance_epsilon)
         mlp = layer.mlp
-        gu = _merged_linear(mlp, "gate_up", y, [mlp.gate_proj, mlp.up_proj])
         dp = mlp.down_proj
-        a = K.swiglu_merged(gu)
+        a = _mlp_activation(mlp, y, fuse_mlp)
         h = K.linear(a, dp.weight) if dp.bias is None else dp(a)
     norm = stack.norm
     if h is None:
