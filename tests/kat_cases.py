@@ -78,3 +78,44 @@ GRPO_UID = ["a", "a", "a", "a", "b"]
 _S = math.sqrt(1 / 3)
 GRPO_WANT = [0.5 / (_S + 1e-6), -0.5 / (_S + 1e-6), -0.5 / (_S + 1e-6), 0.5 / (_S + 1e-6), 5.0 / (1.0 + 1e-6)]
 GRPO_NOSTD_WANT = [0.5, -0.5, -0.5, 0.5, 5.0]  # Dr.GRPO: scores - mean (singleton mean 0)
+
+# ---- log-softmax gather + entropy in closed form (torch_functional.py:64-160; dp_actor.py:182-201) ----
+# Row r has k_r logits at the value c_r and V - k_r at 0 (the "hot" entries are the first k_r), so
+#   Z = k e^c + (V - k), lse = ln Z, logp(label) = c [label < k] - lse,
+#   H = lse - sum p x = ln Z - k c e^c / Z,
+# and the gradients d logp / d x_j = [j = label] - p_j, d H / d x_j = -p_j (x_j - lse + H)
+# (p_j = e^{x_j} / Z); with a temperature T the logits are x / T and the gradients gain a 1 / T.
+LS_V = 1000
+LS_ROWS = [  # (k, c, label): c and c / 2 are exact in bf16
+    (0, 0.0, 7),  # uniform: logp = -ln V, H = ln V
+    (1, 2.0, 0),  # one hot entry, label on it
+    (10, 3.0, 500),  # label on a cold entry
+    (500, -1.0, 3),  # half the row below zero, label hot
+    (999, 4.0, 999),  # all but the last entry hot, label the cold tail entry
+]
+
+
+def ls_logits(temperature=1.0):
+    """[rows, V] logits (before the division by T) and labels of LS_ROWS, as nested lists."""
+    rows = [[c if j < k else 0.0 for j in range(LS_V)] for k, c, _ in LS_ROWS]
+    return rows, [lab for _, _, lab in LS_ROWS]
+
+
+def ls_expected(temperature=1.0, g_logp=1.0, g_ent=0.5):
+    """(logp, entropy, dlogits) of LS_ROWS in closed form (floats; dlogits the gradient of
+    g_logp * logp + g_ent * H with respect to the UNDIVIDED logits)."""
+    logp, ent, grads = [], [], []
+    for k, c, lab in LS_ROWS:
+        z = c / temperature
+        Z = k * math.exp(z) + (LS_V - k)
+        lse = math.log(Z)
+        H = lse - k * z * math.exp(z) / Z
+        logp.append((z if lab < k else 0.0) - lse)
+        ent.append(H)
+        g = []
+        for j in range(LS_V):
+            x = z if j < k else 0.0
+            p = math.exp(x) / Z
+            g.append((g_logp * ((1.0 if j == lab else 0.0) - p) + g_ent * (-p * (x - lse + H))) / temperature)
+        grads.append(g)
+    return logp, ent, grads

@@ -60,3 +60,56 @@ def test_agg_kl_whiten_grpo_kernel_hand_kats():
     assert torch.allclose(adv[:, 0].cpu(), torch.tensor(C.GRPO_WANT), atol=1e-5)
     adv, _ = core_algos.compute_grpo_outcome_advantage(rew, mask, uid, norm_adv_by_std_in_grpo=False)
     assert torch.allclose(adv[:, 0].cpu(), torch.tensor(C.GRPO_NOSTD_WANT), atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("temperature", [1.0, 2.0])
+def test_logprob_entropy_kernel_closed_form(dtype, temperature):
+    """va_logprob_entropy_fwd / _bwd against the closed forms of tests/kat_cases.py (two-level rows,
+    exact in bf16): logp and entropy to fp32 rounding; dlogits to 1e-5 relative (fp32 logits) or to
+    one bf16 rounding (bf16 logits: the gradient is written in the logits' dtype)."""
+    from verl_amd import kernels as K
+
+    rows, labels = C.ls_logits()
+    x = torch.tensor(rows, dtype=dtype, device=DEV).requires_grad_(True)
+    lab = torch.tensor(labels, device=DEV)
+    lp, ent = K.logprob_entropy(x, lab, temperature, inplace_backward=False)
+    want_lp, want_ent, want_g = C.ls_expected(temperature, g_logp=1.0, g_ent=0.5)
+    assert torch.allclose(lp.cpu().double(), torch.tensor(want_lp, dtype=torch.float64), atol=2e-6, rtol=0)
+    assert torch.allclose(ent.cpu().double(), torch.tensor(want_ent, dtype=torch.float64), atol=2e-6, rtol=0)
+    (lp.sum() + 0.5 * ent.sum()).backward()
+    g = torch.tensor(want_g, dtype=torch.float64)
+    tol = 1e-5 if dtype == torch.float32 else 2.0 ** -8  # fp32: v_exp_f32 (1 ulp) inside p
+    assert torch.allclose(x.grad.cpu().double(), g, atol=1e-9, rtol=tol)
+
+
+@pytest.mark.parametrize("fp32_logits", [False, True])
+@pytest.mark.parametrize("temperature", [1.0, 2.0])
+def test_fused_lm_head_kernel_closed_form(fp32_logits, temperature):
+    """f1 (va_linear_logprob_fwd and the fused vocab-range backward) on a hidden / weight pair whose
+    product is exactly the two-level rows of tests/kat_cases.py: hidden row r = c_r e_r, weight[j, r] =
+    [j < k_r]. logp / entropy to fp32 rounding; d hidden = dlogits W and d weight = dlogits^T hidden from
+    the closed-form dlogits rounded to bf16 (the dtype the fused backward writes them in)."""
+    from verl_amd import kernels as K
+
+    n, H = len(C.LS_ROWS), 64
+    hid = torch.zeros(n, H, dtype=torch.float64)
+    w = torch.zeros(C.LS_V, H, dtype=torch.float64)
+    for r, (k, c, _) in enumerate(C.LS_ROWS):
+        hid[r, r] = c
+        w[:k, r] = 1.0
+    labels = torch.tensor([lab for _, _, lab in C.LS_ROWS], device=DEV)
+    hb = hid.to(torch.bfloat16).to(DEV).requires_grad_(True)
+    wb = w.to(torch.bfloat16).to(DEV).requires_grad_(True)
+    lp, ent = K.linear_logprob_entropy(hb, wb, labels, temperature, fp32_logits=fp32_logits)
+    want_lp, want_ent, want_g = C.ls_expected(temperature, g_logp=1.0, g_ent=0.5)
+    assert torch.allclose(lp.detach().cpu().double(), torch.tensor(want_lp, dtype=torch.float64), atol=2e-6, rtol=0)
+    assert torch.allclose(ent.detach().cpu().double(), torch.tensor(want_ent, dtype=torch.float64), atol=2e-6, rtol=0)
+    (lp.sum() + 0.5 * ent.sum()).backward()
+    g = torch.tensor(want_g, dtype=torch.float64).to(torch.bfloat16).double()  # the fused backward's dlogits are bf16
+    want_dh, want_dw = g @ w, g.t() @ hid
+    # the two GEMMs run in bf16 with fp32 accumulation and a bf16 result
+    for got, want, what in ((hb.grad, want_dh, "d hidden"), (wb.grad, want_dw, "d weight")):
+        got = got.cpu().double()
+        err = ((got - want).abs() - 2.0 ** -7 * want.abs()).max().item()
+        assert err <= 1e-6, f"{what}: {err:.3e} beyond one bf16 rounding"

@@ -215,3 +215,22 @@ def test_agg_kl_whiten_grpo_hand_kats():
     adv, _ = ref.compute_grpo_outcome_advantage(rew.clone(), mask, np.array(C.GRPO_UID, dtype=object),
                                                 norm_adv_by_std_in_grpo=False)
     assert torch.allclose(adv[:, 0], torch.tensor(C.GRPO_NOSTD_WANT), atol=1e-7)
+
+
+@pytest.mark.parametrize("temperature", [1.0, 2.0])
+def test_logprob_entropy_closed_form_kats(temperature):
+    """The oracle's log-prob / entropy (fp64) and their autograd gradient against the closed forms of
+    tests/kat_cases.py (LS_ROWS: two-level rows)."""
+    from tests import kat_cases as C
+
+    rows, labels = C.ls_logits()
+    x = torch.tensor(rows, dtype=torch.float64, requires_grad=True)
+    lab = torch.tensor(labels)
+    z = ref.apply_temperature(x, temperature)
+    lp = ref.logprobs_from_logits(z, lab)
+    ent = ref.entropy_from_logits(z)
+    want_lp, want_ent, want_g = C.ls_expected(temperature, g_logp=1.0, g_ent=0.5)
+    assert torch.allclose(lp, torch.tensor(want_lp, dtype=torch.float64), atol=1e-12, rtol=0)
+    assert torch.allclose(ent, torch.tensor(want_ent, dtype=torch.float64), atol=1e-12, rtol=0)
+    (lp.sum() + 0.5 * ent.sum()).backward()
+    assert torch.allclose(x.grad, torch.tensor(want_g, dtype=torch.float64), atol=1e-12, rtol=0)
