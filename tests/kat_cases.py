@@ -119,3 +119,49 @@ def ls_expected(temperature=1.0, g_logp=1.0, g_ent=0.5):
             g.append((g_logp * ((1.0 if j == lab else 0.0) - p) + g_ent * (-p * (x - lse + H))) / temperature)
         grads.append(g)
     return logp, ent, grads
+
+
+# ---- outcome estimators (core_algos.py:311-605), worked by hand ----
+def _masked_whiten(vals, mask):
+    """torch_functional.py:171-223 on flat lists: masked_mean with its + 1e-8, unbiased variance
+    (masked_mean of the squared deviations times n / (n - 1)), rsqrt(var + 1e-8)."""
+    n = sum(mask)
+    mu = sum(v * m for v, m in zip(vals, mask)) / (n + 1e-8)
+    var = sum((v - mu) ** 2 * m for v, m in zip(vals, mask)) / (n + 1e-8) * n / (n - 1)
+    return [(v - mu) / math.sqrt(var + 1e-8) for v in vals]
+
+
+# RLOO (core_algos.py:428-476): a_i = (s_i - mean) n / (n - 1) within a group; a singleton keeps s
+RLOO_SCORES, RLOO_UID = [1.0, 0.0, 0.0, 1.0, 5.0], ["a", "a", "a", "a", "b"]
+RLOO_WANT = [2 / 3, -2 / 3, -2 / 3, 2 / 3, 5.0]
+
+# OPO (core_algos.py:479-530): baseline sum(len s) / sum(len) per group (singleton: 0), len = mask sum
+OPO_SCORES, OPO_UID, OPO_LEN = [1.0, 0.0, 1.0, 7.0], ["a", "a", "a", "b"], [2, 1, 1, 3]
+OPO_WANT = [0.25, -0.75, 0.25, 7.0]  # group a: (2 * 1 + 1 * 0 + 1 * 1) / 4 = 0.75
+
+# pass@k (core_algos.py:311-370): only the group's best gets (r_max - r_2nd) / (std + eps)
+PASSK_SCORES, PASSK_UID = [1.0, 3.0, 2.0], ["a", "a", "a"]
+PASSK_WANT = [0.0, 1.0 / (1.0 + 1e-6), 0.0]  # unbiased std of (1, 3, 2) = 1
+PASSK_NOSTD_WANT = [0.0, 1.0, 0.0]
+
+# REINFORCE++ (core_algos.py:533-569), gamma 0.5: running = r_t + gamma running, stored, then reset
+# by the mask. Row 0 [0, 0, 1] all valid -> [0.25, 0.5, 1]; row 1 [1, 0, 2] with mask [1, 1, 0] ->
+# t = 2: 2 (stored, then reset to 0), t = 1: 0, t = 0: 1 -> [1, 0, 2]; advantages = masked_whiten of
+# the returns over the 5 valid entries, times the mask
+RFPP_REWARDS = [[0.0, 0.0, 1.0], [1.0, 0.0, 2.0]]
+RFPP_MASK = [[1, 1, 1], [1, 1, 0]]
+RFPP_RETURNS = [[0.25, 0.5, 1.0], [1.0, 0.0, 2.0]]
+_w = _masked_whiten([0.25, 0.5, 1.0, 1.0, 0.0, 2.0], [1, 1, 1, 1, 1, 0])
+RFPP_ADV = [_w[:3], [_w[3], _w[4], 0.0]]
+
+# ReMax (core_algos.py:572-605): returns = reverse cumsum of r * mask; adv = returns - b * mask
+REMAX_REWARDS, REMAX_MASK, REMAX_BASE = [[0.0, 0.0, 1.0, 5.0]], [[1, 1, 1, 0]], [0.25]
+REMAX_RETURNS = [[1.0, 1.0, 1.0, 0.0]]
+REMAX_ADV = [[0.75, 0.75, 0.75, 0.0]]
+
+# GAE (core_algos.py:193-241), gamma = lam = 0.5, values [0.1, 0.2, 0.3], reward 1 at the end:
+# delta_2 = 1 - 0.3 = 0.7, delta_1 = 0.5 * 0.3 - 0.2 = -0.05, delta_0 = 0.5 * 0.2 - 0.1 = 0
+# A_2 = 0.7, A_1 = -0.05 + 0.25 * 0.7 = 0.125, A_0 = 0 + 0.25 * 0.125 = 0.03125; returns = A + V
+GAE_REWARDS, GAE_VALUES, GAE_MASK = [[0.0, 0.0, 1.0]], [[0.1, 0.2, 0.3]], [[1, 1, 1]]
+GAE_RETURNS = [[0.13125, 0.325, 1.0]]
+GAE_ADV = [_masked_whiten([0.03125, 0.125, 0.7], [1, 1, 1])]

@@ -113,3 +113,53 @@ def test_fused_lm_head_kernel_closed_form(fp32_logits, temperature):
         got = got.cpu().double()
         err = ((got - want).abs() - 2.0 ** -7 * want.abs()).max().item()
         assert err <= 1e-6, f"{what}: {err:.3e} beyond one bf16 rounding"
+
+
+@pytest.mark.parametrize("R", [3, 8])
+def test_estimator_kernels_hand_kats(R):
+    """RLOO / OPO / pass@k / REINFORCE++ / ReMax / GAE kernels against tests/kat_cases.py (R = 3: the
+    unaligned-row kernels; R = 8: the 16-byte quad kernels, the extra columns masked out)."""
+    from verl_amd.trainer.ppo import core_algos
+    from verl_amd.utils.config import AttrDict
+
+    def col(scores, lengths=None):
+        rew = torch.zeros(len(scores), R, device=DEV)
+        rew[:, 0] = _t(scores)
+        mask = torch.ones(len(scores), R, dtype=torch.int64, device=DEV)
+        if lengths is not None:
+            for i, n in enumerate(lengths):
+                mask[i, n:] = 0
+        return rew, mask
+
+    def pad(rows, fill=0.0):
+        return _t([list(r) + [fill] * (R - len(r)) for r in rows])
+
+    uid = lambda u: np.array(u, dtype=object)  # noqa: E731
+    rew, mask = col(C.RLOO_SCORES)
+    adv, _ = core_algos.compute_rloo_outcome_advantage(rew, mask, uid(C.RLOO_UID))
+    assert torch.allclose(adv[:, 0].cpu(), torch.tensor(C.RLOO_WANT), atol=1e-6)
+    rew, mask = col(C.OPO_SCORES, lengths=C.OPO_LEN)
+    adv, _ = core_algos.compute_opo_outcome_advantage(rew, mask, uid(C.OPO_UID))
+    assert torch.allclose(adv[:, 0].cpu(), torch.tensor(C.OPO_WANT), atol=1e-6)
+    assert torch.count_nonzero(adv[mask == 0]).item() == 0
+    rew, mask = col(C.PASSK_SCORES)
+    for norm, want in ((True, C.PASSK_WANT), (False, C.PASSK_NOSTD_WANT)):
+        adv, _ = core_algos.compute_grpo_passk_outcome_advantage(
+            rew, mask, uid(C.PASSK_UID), config=AttrDict(norm_adv_by_std_in_grpo=norm))
+        assert torch.allclose(adv[:, 0].cpu(), torch.tensor(want), atol=1e-6), norm
+    m = pad(C.RFPP_MASK).to(torch.int64)
+    adv, ret = core_algos.compute_reinforce_plus_plus_outcome_advantage(pad(C.RFPP_REWARDS), m,
+                                                                        config=AttrDict(gamma=0.5))
+    assert torch.allclose(ret[:, :3].cpu(), torch.tensor(C.RFPP_RETURNS), atol=1e-6)
+    assert torch.allclose(adv[:, :3].cpu(), torch.tensor(C.RFPP_ADV), atol=1e-5)
+    assert torch.count_nonzero(adv[m == 0]).item() == 0
+    if R >= 4:
+        m = pad(C.REMAX_MASK).to(torch.int64)
+        adv, ret = core_algos.compute_remax_outcome_advantage(pad(C.REMAX_REWARDS), _t(C.REMAX_BASE), m,
+                                                              config=AttrDict(gamma=1.0))
+        assert torch.allclose(ret[:, :4].cpu(), torch.tensor(C.REMAX_RETURNS), atol=1e-7)
+        assert torch.allclose(adv[:, :4].cpu(), torch.tensor(C.REMAX_ADV), atol=1e-7)
+    adv, ret = core_algos.compute_gae_advantage_return(pad(C.GAE_REWARDS), pad(C.GAE_VALUES),
+                                                       pad(C.GAE_MASK).to(torch.int64), 0.5, 0.5)
+    assert torch.allclose(ret[:, :3].cpu(), torch.tensor(C.GAE_RETURNS), atol=1e-6)
+    assert torch.allclose(adv[:, :3].cpu(), torch.tensor(C.GAE_ADV), atol=1e-5)

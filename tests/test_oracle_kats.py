@@ -234,3 +234,43 @@ def test_logprob_entropy_closed_form_kats(temperature):
     assert torch.allclose(ent, torch.tensor(want_ent, dtype=torch.float64), atol=1e-12, rtol=0)
     (lp.sum() + 0.5 * ent.sum()).backward()
     assert torch.allclose(x.grad, torch.tensor(want_g, dtype=torch.float64), atol=1e-12, rtol=0)
+
+
+def test_estimator_hand_kats():
+    """RLOO, OPO, pass@k, REINFORCE++, ReMax and GAE on the oracle against tests/kat_cases.py."""
+    from tests import kat_cases as C
+
+    def col(scores, R=3, lengths=None):
+        rew = torch.zeros(len(scores), R)
+        rew[:, 0] = torch.tensor(scores)
+        mask = torch.ones(len(scores), R)
+        if lengths is not None:
+            for i, n in enumerate(lengths):
+                mask[i, n:] = 0
+        return rew, mask
+
+    rew, mask = col(C.RLOO_SCORES)
+    adv, _ = ref.compute_rloo_outcome_advantage(rew, mask, np.array(C.RLOO_UID, dtype=object))
+    assert torch.allclose(adv[:, 0], torch.tensor(C.RLOO_WANT), atol=1e-6)
+    rew, mask = col(C.OPO_SCORES, lengths=C.OPO_LEN)
+    adv, _ = ref.compute_opo_outcome_advantage(rew, mask, np.array(C.OPO_UID, dtype=object))
+    assert torch.allclose(adv[:, 0], torch.tensor(C.OPO_WANT), atol=1e-6)
+    assert torch.equal(adv[mask == 0], torch.zeros(int((mask == 0).sum())))
+    rew, mask = col(C.PASSK_SCORES)
+    adv, _ = ref.compute_grpo_passk_outcome_advantage(rew, mask, np.array(C.PASSK_UID, dtype=object))
+    assert torch.allclose(adv[:, 0], torch.tensor(C.PASSK_WANT), atol=1e-6)
+    adv, _ = ref.compute_grpo_passk_outcome_advantage(rew, mask, np.array(C.PASSK_UID, dtype=object), norm=False)
+    assert torch.allclose(adv[:, 0], torch.tensor(C.PASSK_NOSTD_WANT), atol=1e-7)
+    d = torch.float64
+    adv, ret = ref.compute_reinforce_plus_plus_outcome_advantage(torch.tensor(C.RFPP_REWARDS, dtype=d),
+                                                                 torch.tensor(C.RFPP_MASK, dtype=d), 0.5)
+    assert torch.allclose(ret, torch.tensor(C.RFPP_RETURNS, dtype=d), atol=1e-12)
+    assert torch.allclose(adv, torch.tensor(C.RFPP_ADV, dtype=d), atol=1e-9)
+    adv, ret = ref.compute_remax_outcome_advantage(torch.tensor(C.REMAX_REWARDS, dtype=d),
+                                                   torch.tensor(C.REMAX_BASE, dtype=d),
+                                                   torch.tensor(C.REMAX_MASK, dtype=d))
+    assert torch.allclose(ret, torch.tensor(C.REMAX_RETURNS, dtype=d)) and torch.allclose(adv, torch.tensor(C.REMAX_ADV, dtype=d))
+    adv, ret = ref.compute_gae_advantage_return(torch.tensor(C.GAE_REWARDS, dtype=d), torch.tensor(C.GAE_VALUES, dtype=d),
+                                                torch.tensor(C.GAE_MASK, dtype=d), 0.5, 0.5)
+    assert torch.allclose(ret, torch.tensor(C.GAE_RETURNS, dtype=d), atol=1e-12)
+    assert torch.allclose(adv, torch.tensor(C.GAE_ADV, dtype=d), atol=1e-9)
