@@ -443,7 +443,10 @@ int va_linear_logprob_fwd(const void *hidden, int64_t ldh, const void *weight, i
  * % 4 == 0 — the reference's vocab_per_split loop (kernels.py:1491-1548), so that only one range of
  * dlogits exists at a time; labels are valid against the whole V. The caller runs the lm_head's two
  * backward GEMMs on it (dhidden += dlogits W[v_begin:v_end], dW[v_begin:v_end] = dlogits^T hidden).
- * `splits` vocab sub-ranges per row block as in the forward. */
+ * `splits` vocab sub-ranges per row block as in the forward. Only rows [v_begin, v_end) of weight are
+ * read, so a vocabulary shard of a tensor-parallel lm_head (the reference's dist_process_group path,
+ * kernels.py:1345-1553 with its rank offset) passes the address its full matrix's row 0 would have
+ * (shard - v_begin * ldw), V = the whole vocabulary and the shard's range, with global label ids. */
 int va_linear_logprob_bwd(const void *hidden, int64_t ldh, const void *weight, int64_t ldw, int dtype,
                           const int64_t *labels, const float *lse, const float *entropy, const float *g_logp,
                           const float *g_entropy, int64_t N, int64_t H, int64_t V, int64_t v_begin, int64_t v_end,

@@ -198,16 +198,26 @@ def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float, fp32_log
 
 
 def _linear_logprob_bwd_raw(hidden, weight, labels, lse, ent, g1, g2, temperature: float, fp32_logits: bool,
-                            dlogits, v_begin: int = 0, v_end: int | None = None):
+                            dlogits, v_begin: int = 0, v_end: int | None = None, vocab_offset: int = 0,
+                            vocab_total: int | None = None):
     """dlogits [n, v_end - v_begin] bf16 of the rows of ``hidden`` over the vocab range [v_begin,
-    v_end) (default: all of it) by va_linear_logprob_bwd (no logits in HBM)."""
+    v_end) (default: all of it) of ``weight`` by va_linear_logprob_bwd (no logits in HBM).
+    ``weight`` may be a vocabulary shard (tensor parallel): its row 0 is vocab ``vocab_offset`` of a
+    ``vocab_total``-row vocabulary, and the labels are global ids. The C call then gets the address the
+    full matrix's row 0 would have and the global range (only the shard's rows are read), so the
+    g_logp term of a row enters every shard and its own +g_logp only the shard holding the label."""
     N, H = hidden.shape
     V = weight.shape[0]
     v_end = V if v_end is None else int(v_end)
+    off = int(vocab_offset)
+    v_tot = V if vocab_total is None else int(vocab_total)
+    if not (0 <= off and off + V <= v_tot):
+        raise ValueError(f"linear_logprob_bwd: shard [{off}, {off + V}) outside the vocabulary of {v_tot}")
+    w_base = _vp(weight.data_ptr() - off * weight.stride(0) * weight.element_size())
     ev = TIMER.start(torch.cuda.current_stream(hidden.device)) if TIMER is not None else None
     dtype = L.VA_BF16 | (L.VA_LOGITS_F32 if fp32_logits else 0)
-    L.call("va_linear_logprob_bwd", _p(hidden), hidden.stride(0), _p(weight), weight.stride(0), dtype, _p(labels),
-           _p(lse), _p(ent), _p(g1), _p(g2), N, H, V, int(v_begin), v_end, float(temperature),
+    L.call("va_linear_logprob_bwd", _p(hidden), hidden.stride(0), w_base, weight.stride(0), dtype, _p(labels),
+           _p(lse), _p(ent), _p(g1), _p(g2), N, H, v_tot, off + int(v_begin), off + v_end, float(temperature),
            _linear_logprob_splits(N, v_end - v_begin), _p(dlogits), dlogits.stride(0), _stream(hidden))
     if ev is not None:  # MFMA-bound: the logits recompute, 2 N Vr H flops (+ 2 B per logit written)
         TIMER.stop("linear_logprob_bwd", 2 * N * (v_end - v_begin) * H, torch.cuda.current_stream(hidden.device), ev)
@@ -267,7 +277,7 @@ class _LinearLogprob(torch.autograd.Function):
             v1 = min(V, v0 + width)
             dlog = buf[:, : v1 - v0]
             _linear_logprob_bwd_raw(hidden, weight, labels, lse, ent, g1, g2, ctx.temperature, ctx.fp32_logits, dlog,
-                                    v0, v1)
+                                    v0, v1, getattr(ctx, "vocab_offset", 0), getattr(ctx, "vocab_total", None))
             if need_h:
                 w_s = wt[:, v0:v1].t() if wt is not None else weight[v0:v1]
                 if dh32 is None:
