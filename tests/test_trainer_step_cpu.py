@@ -204,3 +204,19 @@ def test_device_metrics_mapping_and_callbacks(capsys):
 
     back = pickle.loads(pickle.dumps(m))
     assert type(back) is dict and back == dict(m)
+
+
+def test_fused_kernel_impl_backend_selects_the_logits_precision():
+    """actor_rollout_ref.model.fused_kernel_options.impl_backend (ppo_trainer.yaml:91-94): "torch" (the
+    default) is FusedLinearForPPO's bf16 logits, "triton" the Triton kernel's fp32 logits
+    (fsdp_workers.py:298-309); an explicit fused_kernel_fp32_logits wins."""
+    from verl_amd.utils.config import actor_config
+    from verl_amd.utils.model import build_qwen2
+    from verl_amd.workers.actor import DataParallelPPOActor
+
+    m = build_qwen2("tiny", device="cpu")
+    for kw, want in (({}, False), ({"fused_kernel_options": {"impl_backend": "torch"}}, False),
+                     ({"fused_kernel_options": {"impl_backend": "triton"}}, True),
+                     ({"fused_kernel_options": {"impl_backend": "triton"}, "fused_kernel_fp32_logits": False}, False)):
+        a = DataParallelPPOActor(actor_config(**kw), m, torch.optim.SGD(m.parameters(), lr=0.0))
+        assert a.fused_kernel_fp32_logits is want, kw

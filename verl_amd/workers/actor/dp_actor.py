@@ -299,9 +299,13 @@ class DataParallelPPOActor(BasePPOActor):
         self.fused_lm_head_after_backbone = bool(self.config.get("fused_lm_head_after_backbone", True))
         # ... and as ONE launch over the concatenated rows
         self.fused_lm_head_concat = bool(self.config.get("fused_lm_head_concat", False))
-        # the fused kernel's logits: bf16-rounded like the unfused autocast path (default: fused and
-        # unfused agree) or fp32 like the reference's own fused kernel
-        self.fused_kernel_fp32_logits = bool(self.config.get("fused_kernel_fp32_logits", False))
+        # the fused kernel's logits: bf16-rounded like the unfused autocast path and the reference's
+        # default fused backend (fused_kernel_options.impl_backend "torch", ppo_trainer.yaml:91-94,
+        # utils/experimental/torch_functional.py:20-37), or fp32 like its "triton" backend
+        # (utils/kernel/kernels.py:120-346; fsdp_workers.py:298-309 selects it)
+        fko = self.config.get("fused_kernel_options", None) or {}
+        backend = fko.get("impl_backend", None) if hasattr(fko, "get") else None
+        self.fused_kernel_fp32_logits = bool(self.config.get("fused_kernel_fp32_logits", backend == "triton"))
         # the log-prob backward writes dlogits over the logits (flash-attn inplace_backward, as the
         # reference) or into a fresh [N, V] buffer: on MI355X the out-of-place stream runs ~4 %
         # faster (a read+write pass whose writes hit other DRAM pages than its reads) for one more
