@@ -17,7 +17,10 @@ __all__ = [
     "entropy_from_logits", "entropy_from_logits_with_chunking", "masked_sum", "masked_mean", "masked_var",
     "masked_whiten", "clip_by_value", "get_response_mask", "distributed_mean_max_min_std",
     "distributed_masked_mean", "allgather_dict_tensors", "broadcast_dict_tensor",
-    "get_constant_schedule_with_warmup", "get_cosine_schedule_with_warmup",
+    "get_constant_schedule_with_warmup", "get_cosine_schedule_with_warmup", "get_wsd_schedule_with_warmup",
+    "logprobs_from_logits_naive", "logprobs_from_logits_flash_attn", "log_probs_from_logits_response",
+    "log_probs_from_logits_response_rmpad", "log_probs_from_logits_all_rmpad", "post_process_logits",
+    "compute_grad_norm", "get_unpad_data", "remove_pad_token", "pad_sequence_to_length", "pad_2d_list_to_length",
 ]
 
 
@@ -34,6 +37,65 @@ def logprobs_from_logits(logits, labels, inplace_backward=True):
     """
     logp, _ = K.logprob_entropy(logits, labels, 1.0, inplace_backward)
     return logp
+
+
+def logprobs_from_logits_naive(logits, labels):
+    """torch_functional.py:110-113 (log_softmax + gather): the same values from the one-pass kernel."""
+    return logprobs_from_logits(logits, labels, inplace_backward=False)
+
+
+def logprobs_from_logits_flash_attn(logits, labels, inplace_backward=True):
+    """torch_functional.py:95-100 (flash-attn's cross_entropy_loss with inplace_backward): the
+    kernel pair this module's logprobs_from_logits runs."""
+    return logprobs_from_logits(logits, labels, inplace_backward=inplace_backward)
+
+
+def _unpad_indices(attention_mask):
+    return torch.nonzero(attention_mask.flatten(), as_tuple=False).flatten()
+
+
+def _pad_rows(values, indices, batch: int, seqlen: int):
+    """flash_attn.bert_padding.pad_input for a [nnz] vector: zeros at the padded positions."""
+    out = torch.zeros(batch * seqlen, dtype=values.dtype, device=values.device)
+    out[indices] = values
+    return out.view(batch, seqlen)
+
+
+def log_probs_from_logits_response(input_ids, logits, response_length):
+    """torch_functional.py:422-435: log-probs of the response tokens from the full [B, S, V] logits
+    (logits at position t predict token t + 1)."""
+    response_logits = logits[:, -response_length - 1 : -1]
+    response = input_ids[:, -response_length:]
+    return logprobs_from_logits(logits=response_logits, labels=response)
+
+
+def log_probs_from_logits_response_rmpad(input_ids, attention_mask, logits_rmpad, response_length):
+    """torch_functional.py:438-462: log-probs from remove-padding logits [nnz, V] of the padded
+    input_ids [B, S]: labels are the packed ids rolled by one (torch.roll over the whole packed
+    stream, as the reference), scattered back to [B, S] and cut to the response."""
+    batch_size, seqlen = input_ids.shape
+    indices = _unpad_indices(attention_mask)
+    ids_rmpad = input_ids.flatten()[indices]
+    rolled = torch.roll(ids_rmpad, shifts=-1, dims=0)
+    full = logprobs_from_logits(logits=logits_rmpad, labels=rolled)
+    return _pad_rows(full, indices, batch_size, seqlen)[:, -response_length - 1 : -1]
+
+
+def log_probs_from_logits_all_rmpad(input_ids_rmpad, logits_rmpad, indices, batch_size, seqlen, response_length):
+    """torch_functional.py:465-490: as log_probs_from_logits_response_rmpad with the packed ids
+    [1, nnz] and their unpad indices given."""
+    ids = input_ids_rmpad.transpose(0, 1).squeeze(-1)
+    rolled = torch.roll(ids, shifts=-1, dims=0)
+    full = logprobs_from_logits(logits=logits_rmpad, labels=rolled)
+    return _pad_rows(full, indices, batch_size, seqlen)[:, -response_length - 1 : -1]
+
+
+def post_process_logits(input_ids, logits, temperature, top_k, top_p):
+    """torch_functional.py:493-500: logits.div_(temperature) in place (top-k / top-p are disabled
+    there too)."""
+    if temperature != 1.0:
+        logits = logits.div_(temperature)
+    return logits
 
 
 def logprobs_from_logits_v2(logits, labels):
@@ -157,6 +219,45 @@ def distributed_masked_mean(local_tensor, local_mask):
     return packed[0] / packed[1]
 
 
+def compute_grad_norm(model: torch.nn.Module):
+    """torch_functional.py:249-254: the SUM OF SQUARES of all gradients (no square root), a host
+    float. One device reduction over all gradients instead of a host sync per parameter."""
+    grads = [p.grad.detach() for p in model.parameters() if p.grad is not None]
+    if not grads:
+        return 0
+    sq = torch._foreach_norm(grads, 2.0)
+    return float(torch.sum(torch.stack([g.double() for g in sq]) ** 2).item())
+
+
+def get_unpad_data(attention_mask):
+    """torch_functional.py:629-638: (indices of the valid tokens, cu_seqlens int32, max seqlen)."""
+    seqlens = attention_mask.sum(dim=-1, dtype=torch.int32)
+    indices = _unpad_indices(attention_mask)
+    cu = torch.nn.functional.pad(torch.cumsum(seqlens, dim=0, dtype=torch.int32), (1, 0))
+    return indices, cu, int(seqlens.max().item())
+
+
+def remove_pad_token(input_ids: torch.Tensor, attention_mask: torch.Tensor):
+    """torch_functional.py:407-419: per row, the last mask.sum() ids (left padding removed), as lists."""
+    return [ids[len(ids) - int(mask.sum()):].cpu().numpy().tolist()
+            for ids, mask in zip(input_ids, attention_mask, strict=True)]
+
+
+def pad_sequence_to_length(tensors, max_seq_len, pad_token_id, left_pad=False):
+    """torch_functional.py:318-328: pad the last dim to max_seq_len (unchanged when already longer)."""
+    if tensors.shape[-1] >= max_seq_len:
+        return tensors
+    n = max_seq_len - tensors.shape[-1]
+    return torch.nn.functional.pad(tensors, (n, 0) if left_pad else (0, n), "constant", pad_token_id)
+
+
+def pad_2d_list_to_length(response, pad_token_id, max_length=None):
+    """torch_functional.py:307-315: a ragged 2-D list right-padded into a tensor."""
+    longest = max(len(r) for r in response)
+    target = max_length if max_length is not None and max_length > longest else longest
+    return torch.tensor([tuple(r) + (pad_token_id,) * (target - len(r)) for r in response])
+
+
 def broadcast_dict_tensor(tensors, src, group):
     for key in sorted(tensors.keys()):
         torch.distributed.broadcast(tensors[key], src=src, group=group, async_op=False)
@@ -204,6 +305,33 @@ def get_constant_schedule_with_warmup(optimizer, num_warmup_steps: int, last_epo
 
     def factor(step: int) -> float:
         return float(step) / float(max(1.0, warm)) if step < warm else 1.0
+
+    return LambdaLR(optimizer, factor, last_epoch)
+
+
+def get_wsd_schedule_with_warmup(optimizer, num_warmup_steps: int, num_training_steps: int,
+                                 min_lr_ratio: float = 0.0, num_cycles: float = 0.5, last_epoch: int = -1,
+                                 stable_ratio: float = 0.9):
+    """torch_functional.py:641-694: warmup (linear from 0), stable (1), then cosine decay to
+    min_lr_ratio over the last (1 - stable_ratio) of the post-warmup steps, min_lr_ratio after."""
+    import math
+
+    from torch.optim.lr_scheduler import LambdaLR
+
+    remaining = max(0, num_training_steps - num_warmup_steps)
+    stable = int(remaining * stable_ratio)
+    decay = remaining - stable
+
+    def factor(step: int) -> float:
+        if step < num_warmup_steps:
+            return float(step) / float(max(1, num_warmup_steps))
+        if step < num_warmup_steps + stable:
+            return 1.0
+        if step < num_training_steps:
+            progress = float(step - num_warmup_steps - stable) / float(max(1, decay))
+            value = max(0.0, 0.5 * (1.0 + math.cos(math.pi * float(num_cycles) * 2.0 * progress)))
+            return (1.0 - min_lr_ratio) * value + min_lr_ratio
+        return min_lr_ratio
 
     return LambdaLR(optimizer, factor, last_epoch)
 
