@@ -232,3 +232,30 @@ def test_bench_final_metrics_are_the_reference_reduction():
     assert clip == {"clipped_tokens": round(2 * (0.25 * 4 + 0.5 * 8)), "clipped_lower_tokens": round(2 * 0.1 * 8),
                     "response_tokens": 2 * 20}
     assert bench.clipped_tokens([m], batch, micro=2, dynamic=True) is None
+
+
+def test_validation_metrics_reference_answers():
+    """tests/trainer/ppo/test_metric_utils_on_cpu.py:213-318 (bootstrap_metric, calc_maj_val,
+    process_validation_metrics) with the reference's own expectations, and the draws equal to the
+    reference's global-RNG sequence for the same seed."""
+    import numpy as np
+
+    from verl_amd.trainer.ppo.metric_utils import bootstrap_metric, calc_maj_val, process_validation_metrics
+
+    res = bootstrap_metric([1, 2, 3, 4, 5], subset_size=3, reduce_fns=[np.mean, np.max], n_bootstrap=100, seed=42)
+    assert len(res) == 2 and abs(res[0][0] - 3.0) <= 0.3 and 3.5 < res[1][0] < 5.0
+    np.random.seed(42)  # the reference's draws (np.random.seed + np.random.choice)
+    want = [np.max([[1, 2, 3, 4, 5][i] for i in np.random.choice(5, size=3, replace=True)]) for _ in range(100)]
+    assert res[1] == (np.mean(want), np.std(want))
+    with pytest.raises(ValueError):
+        bootstrap_metric([], subset_size=1, reduce_fns=[np.mean])
+    assert calc_maj_val([{"pred": "A", "val": 0.9}, {"pred": "B", "val": 0.8}, {"pred": "A", "val": 0.7}],
+                        vote_key="pred", val_key="val") == 0.9
+    assert calc_maj_val([{"pred": "A", "val": 0.9}, {"pred": "B", "val": 0.8}, {"pred": "B", "val": 0.7},
+                         {"pred": "A", "val": 0.6}], vote_key="pred", val_key="val") in (0.9, 0.8)
+    r = process_validation_metrics(["source1", "source1", "source2"], ["prompt1", "prompt1", "prompt2"],
+                                   {"score": [0.8, 0.9, 0.7]}, seed=42)
+    assert "source1" in r and "source2" in r and abs(r["source1"]["score"]["mean@2"] - 0.85) < 1e-12
+    r = process_validation_metrics(["source1"] * 3, ["prompt1"] * 3, {"score": [0.8, 0.9, 0.7], "pred": ["A", "B", "A"]},
+                                   seed=42)
+    assert "maj@2/mean" in r["source1"]["score"] and "maj@3/mean" in r["source1"]["score"]

@@ -312,3 +312,38 @@ def test_plan_packing_masked_tail_labels_follow_the_rolled_stream():
         kept = {(int(o) // R, int(o) % R) for o in sel_out}
         want = {(r, t) for r in range(4) for t in range(R) if am[r, S - R - 1 + t]}
         assert kept == want
+
+
+def test_unfold_column_chunks_and_future_and_env_padding(monkeypatch):
+    """protocol.py:816-853 (unfold_column_chunks), :905-950 (DataProtoFuture, here over
+    concurrent.futures instead of Ray object refs), :52-55 (VERL_AUTO_PADDING)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from verl_amd.protocol import DataProto, DataProtoFuture
+
+    d = DataProto.from_dict({"x": torch.arange(12).view(2, 6), "y": torch.tensor([10, 20])},
+                            non_tensors={"z": np.array([[1, 2, 3, 4], [5, 6, 7, 8]], dtype=object),
+                                         "w": np.array(["a", "b"], dtype=object)})
+    u = d.unfold_column_chunks(2, split_keys=["x", "z"])
+    assert len(u) == 4
+    assert u.batch["x"].tolist() == [[0, 1, 2], [3, 4, 5], [6, 7, 8], [9, 10, 11]]
+    assert u.batch["y"].tolist() == [10, 10, 20, 20]
+    assert u.non_tensor_batch["z"].tolist() == [[1, 2], [3, 4], [5, 6], [7, 8]]
+    assert u.non_tensor_batch["w"].tolist() == ["a", "a", "b", "b"]
+    r = d.unfold_column_chunks(3)  # no split keys: every key repeated
+    assert r.batch["x"].shape == (6, 6) and r.non_tensor_batch["w"].tolist() == ["a"] * 3 + ["b"] * 3
+
+    with ThreadPoolExecutor(2) as ex:
+        futs = [ex.submit(lambda i=i: d.select_idxs([i])) for i in range(2)]
+        fut = DataProtoFuture.concat(futs)
+        whole = fut.get()
+        assert whole.batch["y"].tolist() == [10, 20]
+        parts = fut.chunk(2)
+        assert [p.get().batch["y"].tolist() for p in parts] == [[10], [20]]
+
+    three = DataProto.from_dict({"a": torch.arange(3)})
+    with pytest.raises(AssertionError, match="only support equal chunk"):
+        three.chunk(2)
+    monkeypatch.setenv("VERL_AUTO_PADDING", "1")
+    assert three.is_padding_enabled()
+    assert [len(c) for c in three.chunk(2)] == [2, 1]

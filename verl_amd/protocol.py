@@ -15,7 +15,7 @@ import io
 import logging
 import pathlib
 import pickle
-from collections.abc import Iterator
+from collections.abc import Callable, Iterator
 from dataclasses import dataclass, field
 from typing import Any, Optional
 
@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 __all__ = ["DataProto", "DataProtoItem", "TensorBatch", "union_tensor_dict", "pad_dataproto_to_divisor",
-           "unpad_dataproto", "DataProtoConfig", "collate_fn"]
+           "unpad_dataproto", "DataProtoConfig", "collate_fn", "DataProtoFuture"]
 
 
 
@@ -424,7 +424,12 @@ class DataProto:
 
     # ------------------------------------------------------------------ padding / chunking
     def is_padding_enabled(self) -> bool:
-        return self.meta_info.get(DataProtoConfig.auto_padding_key, False) or DataProtoConfig.auto_padding
+        """protocol.py:52-55 / 681-687: the batch's meta_info flag, the class switch, or the
+        VERL_AUTO_PADDING environment variable (TRUE / 1)."""
+        import os
+
+        env = os.getenv("VERL_AUTO_PADDING", "FALSE").upper() in ("TRUE", "1")
+        return bool(self.meta_info.get(DataProtoConfig.auto_padding_key, False) or DataProtoConfig.auto_padding or env)
 
     def padding(self, padding_size, padding_candidate=""):
         if padding_size == 0:
@@ -487,6 +492,26 @@ class DataProto:
                 val, (repeat_times,) + (1,) * (val.ndim - 1))
         return type(self)(batch=batch, non_tensor_batch=non_tensor, meta_info=self.meta_info)
 
+    def unfold_column_chunks(self, n_split: int, split_keys: Optional[list] = None) -> "DataProto":
+        """protocol.py:816-853: the keys in ``split_keys`` are split along dim 1 into n_split parts
+        unfolded into the batch dim ([B, n k, ...] -> [B n, k, ...], row-major); every other key
+        (tensor and non-tensor) is repeated n_split times per row (repeat_interleave)."""
+        keys = set(split_keys) if split_keys is not None else set()
+
+        def unfold(x):
+            shape = list(x.shape)
+            shape[0], shape[1] = x.shape[0] * n_split, x.shape[1] // n_split
+            return x.reshape(*shape)
+
+        batch = None
+        if self.batch is not None:
+            src = {k: (unfold(v) if k in keys else torch.repeat_interleave(v, n_split, dim=0))
+                   for k, v in self.batch.items()}
+            batch = TensorBatch(src, batch_size=(len(self) * n_split,))
+        non_tensor = {k: (unfold(v) if k in keys else np.repeat(v, n_split, axis=0))
+                      for k, v in self.non_tensor_batch.items()}
+        return type(self)(batch=batch, non_tensor_batch=non_tensor, meta_info=self.meta_info)
+
     def sample_level_repeat(self, repeat_times) -> "DataProto":
         """protocol.py:855-901 — per-sample repeat counts (list / tuple / 1-D tensor or array)."""
         if isinstance(repeat_times, torch.Tensor | np.ndarray):
@@ -546,6 +571,40 @@ def unfold_batch_dim(data: DataProto, batch_dims=2):
     out.batch = TensorBatch(tensors) if tensors else None
     out.non_tensor_batch = non_tensor
     return out
+
+
+@dataclass
+class DataProtoFuture:
+    """protocol.py:905-950 without Ray: a list of per-worker results to be collected (collect_fn,
+    DataProto.concat by default) and optionally re-partitioned (dispatch_fn) on get(). A future is
+    anything with .result() (concurrent.futures) or an already computed DataProto; this process runs
+    no Ray object store, so ray.get becomes .result()."""
+
+    collect_fn: Callable
+    futures: list
+    dispatch_fn: Optional[Callable] = None
+
+    @staticmethod
+    def concat(data: list) -> "DataProtoFuture":
+        return DataProtoFuture(collect_fn=DataProto.concat, futures=data)
+
+    def chunk(self, chunks: int) -> list["DataProtoFuture"]:
+        from functools import partial
+
+        def dispatch_fn(x, i, chunks):
+            return x.chunk(chunks=chunks)[i]
+
+        return [DataProtoFuture(collect_fn=self.collect_fn, futures=self.futures,
+                                dispatch_fn=partial(dispatch_fn, i=i, chunks=chunks)) for i in range(chunks)]
+
+    def get(self):
+        output = [f.result() if hasattr(f, "result") else f for f in self.futures]
+        for o in output:
+            assert isinstance(o, DataProto)
+        output = self.collect_fn(output)
+        if self.dispatch_fn is not None:
+            output = self.dispatch_fn(output)
+        return output
 
 
 def all_gather_data_proto(data: DataProto, process_group) -> None:

@@ -269,3 +269,76 @@ def global_token_num(attention_mask: torch.Tensor, group=None) -> list[int]:
     pad[: local.numel()] = local
     parts = comm.all_gather(pad, group)
     return torch.cat([p[:n] for p, n in zip(parts, sizes, strict=True)]).tolist()
+
+
+# ------------------------------------------------------------------ validation metrics (host)
+def bootstrap_metric(data: list, subset_size: int, reduce_fns: list, n_bootstrap: int = 1000,
+                     seed: int = 42) -> list[tuple[float, float]]:
+    """metric_utils.py:261-299: (mean, std) of each reduce_fn over n_bootstrap resamples of
+    subset_size items drawn with replacement. The draws are the reference's (MT19937 seeded with
+    ``seed``, one choice() per resample), from a local generator instead of the global one."""
+    rng = np.random.RandomState(seed)
+    per_fn = [[] for _ in reduce_fns]
+    for _ in range(n_bootstrap):
+        idx = rng.choice(len(data), size=subset_size, replace=True)
+        sample = [data[i] for i in idx]
+        for out, fn in zip(per_fn, reduce_fns):
+            out.append(fn(sample))
+    return [(np.mean(v), np.std(v)) for v in per_fn]
+
+
+def calc_maj_val(data: list[dict], vote_key: str, val_key: str) -> float:
+    """metric_utils.py:302-335: the first val_key value of the most frequent vote_key value (ties:
+    the vote seen first)."""
+    counts, first = {}, {}
+    for d in data:
+        v = d[vote_key]
+        counts[v] = counts.get(v, 0) + 1
+        first.setdefault(v, d[val_key])
+    return first[max(counts, key=counts.get)]
+
+
+def process_validation_metrics(data_sources: list[str], sample_inputs: list[str], infos_dict: dict[str, list],
+                               seed: int = 42) -> dict:
+    """metric_utils.py:338-446: per data source and variable, the mean over prompts of mean@N,
+    std@N and, at N = 2, 4, ..., n, the bootstrap best@N / worst@N (and maj@N when a "pred" variable
+    exists) of each prompt's responses; string-valued variables are skipped."""
+    from collections import defaultdict
+    from functools import partial
+
+    groups = defaultdict(lambda: defaultdict(lambda: defaultdict(list)))
+    for i, src in enumerate(data_sources):
+        for var, vals in infos_dict.items():
+            groups[src][sample_inputs[i]][var].append(vals[i])
+    collected = defaultdict(lambda: defaultdict(lambda: defaultdict(list)))
+    for src, prompts in groups.items():
+        for var2vals in prompts.values():
+            for var, vals in var2vals.items():
+                if isinstance(vals[0], str):
+                    continue
+                n_resp = len(vals)
+                m = {f"mean@{n_resp}": np.mean(vals)}
+                if n_resp > 1:
+                    m[f"std@{n_resp}"] = np.std(vals)
+                    sizes, n = [], 2
+                    while n < n_resp:
+                        sizes.append(n)
+                        n *= 2
+                    sizes.append(n_resp)
+                    for n in sizes:
+                        (b_mean, b_std), (w_mean, w_std) = bootstrap_metric(vals, n, [np.max, np.min], seed=seed)
+                        m[f"best@{n}/mean"], m[f"best@{n}/std"] = b_mean, b_std
+                        m[f"worst@{n}/mean"], m[f"worst@{n}/std"] = w_mean, w_std
+                        if var2vals.get("pred") is not None:
+                            votes = [{"val": v, "pred": p} for v, p in zip(vals, var2vals["pred"], strict=True)]
+                            [(mj_mean, mj_std)] = bootstrap_metric(
+                                votes, n, [partial(calc_maj_val, vote_key="pred", val_key="val")], seed=seed)
+                            m[f"maj@{n}/mean"], m[f"maj@{n}/std"] = mj_mean, mj_std
+                for name, val in m.items():
+                    collected[src][var][name].append(val)
+    out = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
+    for src, var2 in collected.items():
+        for var, name2 in var2.items():
+            for name, vals in name2.items():
+                out[src][var][name] = np.mean(vals)
+    return out

@@ -10,6 +10,7 @@ driver CPU.
 
 from __future__ import annotations
 
+from enum import Enum
 from typing import Optional
 
 import torch
@@ -125,6 +126,19 @@ def filter_groups(batch: DataProto, metric: str = "acc"):
     kept = {uid for uid, vs in vals.items() if np.std(vs) > 0 or len(vs) == 1}
     idx = [i for i, uid in enumerate(uids) if uid in kept]
     return batch[idx], len(kept)
+
+
+class Role(Enum):
+    """ray_trainer.py:67-78: the worker roles a trainer maps to resource pools (subclass to add
+    roles). Here one process per GPU plays the actor (and critic / ref) roles of its DP rank."""
+
+    Actor = 0
+    Rollout = 1
+    ActorRollout = 2
+    Critic = 3
+    RefPolicy = 4
+    RewardModel = 5
+    ActorRolloutRef = 6
 
 
 class ResourcePoolManager:
