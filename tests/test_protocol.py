@@ -347,3 +347,29 @@ def test_unfold_column_chunks_and_future_and_env_padding(monkeypatch):
     monkeypatch.setenv("VERL_AUTO_PADDING", "1")
     assert three.is_padding_enabled()
     assert [len(c) for c in three.chunk(2)] == [2, 1]
+
+
+@pytest.mark.parametrize("case", ["2d", "2d_nested_labels", "3d"])
+def test_unfold_column_chunks_reference_cases(case):
+    """The three cases of tests/test_protocol_on_cpu.py:416-480 (inputs and expected outputs)."""
+    from verl_amd.protocol import DataProto
+
+    rows = torch.arange(1, 13).view(3, 4)
+    if case == "3d":
+        obs1 = torch.stack([rows, rows], dim=-1)  # [[[1, 1], [2, 2], ...], ...]
+        obs2 = obs1[:, :2]
+    else:
+        obs1, obs2 = rows, rows[:, :2]
+    labels = [["a1", "a2"], ["b1", "b2"], ["c1", "c2"]] if case == "2d_nested_labels" else ["a", "b", "c"]
+    d = DataProto.from_dict(tensors={"obs1": obs1, "obs2": obs2}, non_tensors={"labels": labels},
+                            meta_info={"name": "abc"})
+    keys = ["obs1", "labels"] if case == "2d_nested_labels" else ["obs1"]
+    u = d.unfold_column_chunks(2, split_keys=keys)
+    want1 = torch.arange(1, 13).view(6, 2)
+    if case == "3d":
+        want1 = torch.stack([want1, want1], dim=-1)
+    assert torch.equal(u.batch["obs1"], want1)
+    assert torch.equal(u.batch["obs2"], torch.repeat_interleave(obs2, 2, dim=0))
+    want_l = [["a1"], ["a2"], ["b1"], ["b2"], ["c1"], ["c2"]] if case == "2d_nested_labels" else list("aabbcc")
+    assert (u.non_tensor_batch["labels"] == np.array(want_l, dtype=object)).all()
+    assert u.meta_info == {"name": "abc"}
