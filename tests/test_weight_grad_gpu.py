@@ -107,3 +107,43 @@ def test_remainder_tiles_match_full_tiles(T, M, N):
         L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, 0)
     _check(full, want)
     _check(rem, want)
+
+
+@pytest.mark.parametrize("T,M,N", [(2048, 1152, 896), (4096, 896, 4864), (1024, 200, 136), (96, 264, 512),
+                                   (2048, 9728, 896)])
+@pytest.mark.parametrize("splits", [0, 1, 3])
+@pytest.mark.parametrize("remainder", [0, 1])
+def test_weight_grad_16x16x32_form(T, M, N, splits, remainder):
+    """VA_TUNE_WGRAD_MFMA = 16 (8 x 4 v_mfma_f32_16x16x32_bf16 blocks per wave, the 8-row image
+    swizzle): the fp32 reference's tolerance, deterministic, and on exact-arithmetic operands (small
+    integers: every partial sum exact) bitwise equal to the 32x32x16 form."""
+    from verl_amd import _lib as L
+
+    g = torch.Generator(device=DEV).manual_seed(T + M + N + 1)
+    dy = (torch.randn(T, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
+    dyi = torch.randint(-3, 4, (T, M), device=DEV, generator=g).to(torch.bfloat16)
+    xi = torch.randint(-3, 4, (T, N), device=DEV, generator=g).to(torch.bfloat16)
+    try:
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, remainder)
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_MFMA, 16)
+        got = _call(dy, x, splits)
+        again = _call(dy, x, splits)
+        exact16 = _call(dyi, xi, splits)
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_MFMA, 32)
+        exact32 = _call(dyi, xi, splits)
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, 0)
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_MFMA, 32)
+    assert not torch.isnan(got.float()).any()
+    _check(got, _ref(dy, x))
+    assert torch.equal(got, again)
+    assert torch.equal(exact16, exact32)
+    assert torch.equal(exact16.float(), _ref(dyi, xi).to(torch.bfloat16).float())
+
+
+def test_weight_grad_mfma_setting_is_checked():
+    from verl_amd import _lib as L
+
+    with pytest.raises(RuntimeError, match="16 or 32"):
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_MFMA, 8)

@@ -715,6 +715,7 @@ extern int g_loss_vec;            // loss.hip
 extern int g_whiten_slice_min;    // advantage.hip
 extern int g_linear_logprob_tile;  // linear_logprob.hip
 extern int g_wgrad_remainder;      // wgrad.hip
+extern int g_wgrad_mfma;           // wgrad.hip
 extern int g_whiten_grid;         // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
 extern int g_flash_dkdv_qt;       // attention.hip
@@ -740,6 +741,13 @@ extern "C" int va_set_tuning(int key, int value) {
     case VA_TUNE_GAE_NT: g_gae_nt = value & 7; return VA_OK;
     case VA_TUNE_LOSS_VEC: g_loss_vec = value; return VA_OK;
     case VA_TUNE_WGRAD_REMAINDER: g_wgrad_remainder = value; return VA_OK;
+    case VA_TUNE_WGRAD_MFMA:
+      if (value != 16 && value != 32) {
+        va::set_error("va_set_tuning: VA_TUNE_WGRAD_MFMA must be 16 or 32");
+        return VA_E_ARG;
+      }
+      g_wgrad_mfma = value;
+      return VA_OK;
     case VA_TUNE_LINEAR_LOGPROB_TILE:
       if (value != 128 && value != 256) {
         va::set_error("VA_TUNE_LINEAR_LOGPROB_TILE must be 128 or 256 (got %d)", value);

@@ -32,19 +32,38 @@ constexpr int WBK = 32, WNT = 512;
 typedef short wbf16x8 __attribute__((ext_vector_type(8)));
 typedef int wv2i __attribute__((ext_vector_type(2)));
 typedef float wf32x16 __attribute__((ext_vector_type(16)));
+typedef float wf32x4 __attribute__((ext_vector_type(4)));
+
+// the wave tile's accumulators: 4 x 2 32x32 blocks (16 fp32 each) or 8 x 4 16x16 blocks (4 each)
+template <bool MF16>
+struct WAcc {
+  wf32x16 v[4][2];
+};
+template <>
+struct WAcc<true> {
+  wf32x4 v[8][4];
+};
 
 // element offset of (row, col) in a [32][C] image (C = 128, 256 or 512 columns) with 16-B chunks
 // XOR-swizzled by (row & 3) << 2 (every row length is a multiple of the 64 banks' 256 bytes' worth of
 // words, so the swizzle alone spreads a transposed read's 4 rows over all banks)
-template <int C>
+// SW16 (the 16x16x32 kernel's images): chunks XOR-swizzled by (row & 7) << 1 instead, since its
+// transposed reads cover 2 chunks of 8 consecutive rows per 32 lanes (the 4-row swizzle would put rows
+// r and r + 4 on the same banks)
+template <int C, bool SW16 = false>
+__device__ __forceinline__ int w_swz(int row) {
+  return SW16 ? ((row & 7) << 1) : ((row & 3) << 2);
+}
+
+template <int C, bool SW16 = false>
 __device__ __forceinline__ int w_off(int row, int col) {
-  return row * C + (((col >> 3) ^ ((row & 3) << 2)) << 3) + (col & 7);
+  return row * C + (((col >> 3) ^ w_swz<C, SW16>(row)) << 3) + (col & 7);
 }
 
 // LDS-DMA of one operand's 32 x C step image: 1 KiB pieces of 512 / C rows, C / 128 per wave; lane l
 // of piece g lands at physical chunk l % (C / 8) of row g (512 / C) + l / (C / 8) and so fetches the
 // logical chunk the swizzle puts there
-template <int C>
+template <int C, bool SW16 = false>
 __device__ __forceinline__ void w_stage(const uint16_t *__restrict__ src, int64_t ld, int64_t k0, int col0, int ncols,
                                         uint16_t *img, int wave, int lane) {
   constexpr int PW = C / 128, RPP = 512 / C, CPR = C / 8;
@@ -52,7 +71,7 @@ __device__ __forceinline__ void w_stage(const uint16_t *__restrict__ src, int64_
   for (int i = 0; i < PW; ++i) {
     const int g = wave * PW + i;
     const int row = g * RPP + lane / CPR;
-    const int c = (lane % CPR) ^ ((row & 3) << 2);
+    const int c = (lane % CPR) ^ w_swz<C, SW16>(row);
     int col = col0 + c * 8;
     if (col > ncols - 8) col = ncols - 8;  // clamped: results for these columns are dropped
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + (k0 + row) * ld + col), img + g * 512, 16,
@@ -79,6 +98,19 @@ __device__ __forceinline__ void w_frag(const uint16_t *img, int ss, int col_base
   hi = w_tr_read(img + w_off<C>(r0 + 8, col));
 }
 
+// 16 columns x 32 k fragment (v_mfma_f32_16x16x32_bf16 A or B operand) by two transposed reads: the
+// 16-lane group g = lane >> 4 reads rows 4 g .. 4 g + 3 and 16 + 4 g .. 16 + 4 g + 3 of its 16
+// columns, so element j of lane (column col_base + (lane & 15)) = image[16 (j >> 2) + 4 g + (j & 3)]
+// [column] (A and B in the same k order); each 32-lane half reads 8 distinct rows per instruction
+template <int C>
+__device__ __forceinline__ void w_frag16(const uint16_t *img, int col_base, int lane, wv2i &lo, wv2i &hi) {
+  const int g = lane >> 4, li = lane & 15;
+  const int r0 = 4 * g + (li >> 2);
+  const int col = col_base + 4 * (li & 3);
+  lo = w_tr_read(img + w_off<C, true>(r0, col));
+  hi = w_tr_read(img + w_off<C, true>(r0 + 16, col));
+}
+
 // retire all but N of this wave's LDS-DMA instructions (N a literal of the counted-wait encoding)
 template <int N>
 __device__ __forceinline__ void w_vm_wait() {
@@ -90,15 +122,67 @@ __device__ __forceinline__ void w_vm_wait() {
   else static_assert(N == 0, "unsupported vmcnt");
 }
 
+// retire all but N of this wave's LDS reads, naming the fragment registers those reads produced
+template <int N>
+__device__ __forceinline__ void w_lgkm_wait(wv2i &lo, wv2i &hi) {
+  if constexpr (N == 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo), "+v"(hi));
+  else if constexpr (N == 2) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(lo), "+v"(hi));
+  else if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(lo), "+v"(hi));
+  else if constexpr (N == 6) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(lo), "+v"(hi));
+  else if constexpr (N == 8) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(lo), "+v"(hi));
+  else if constexpr (N == 10) asm volatile("s_waitcnt lgkmcnt(10)" : "+v"(lo), "+v"(hi));
+  else if constexpr (N == 12) asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(lo), "+v"(hi));
+  else if constexpr (N == 14) asm volatile("s_waitcnt lgkmcnt(14)" : "+v"(lo), "+v"(hi));
+  else static_assert(N == 0, "unsupported lgkmcnt");
+}
+
 __device__ __forceinline__ wbf16x8 w_join(wv2i lo, wv2i hi) {
   return __builtin_bit_cast(wbf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3));
 }
 
 __device__ __forceinline__ int w_crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// one 32-token step of the 16x16x32 form: 24 transposed reads issued A0 B0..B3 A1..A7, each counted
+// wait releasing the next A fragment while the later reads stay in flight; 32 MFMAs
+template <int TM, int TN, int I>
+__device__ __forceinline__ void w_step16_row(const uint16_t *ia, int wm, int lane, wv2i (&a)[8][2],
+                                             const wbf16x8 (&fb)[4], wf32x4 (&acc)[8][4]) {
+  w_lgkm_wait<14 - 2 * I>(a[I][0], a[I][1]);
+  const wbf16x8 fa = w_join(a[I][0], a[I][1]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[I][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[j], acc[I][j], 0, 0, 0);
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void w_step16(const uint16_t *ia, const uint16_t *ib, int wm, int wn, int lane,
+                                         wf32x4 (&acc)[8][4]) {
+  wv2i a[8][2], b[4][2];
+  w_frag16<TM>(ia, wm * 128, lane, a[0][0], a[0][1]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w_frag16<TN>(ib, wn * 64 + j * 16, lane, b[j][0], b[j][1]);
+#pragma unroll
+  for (int i = 1; i < 8; ++i) w_frag16<TM>(ia, wm * 128 + i * 16, lane, a[i][0], a[i][1]);
+  // A0 and B0..B3 are the first 10 reads: 14 may stay outstanding
+  asm volatile("s_waitcnt lgkmcnt(14)" : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]),
+               "+v"(b[2][1]), "+v"(b[3][0]), "+v"(b[3][1]));
+  wbf16x8 fb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb[j] = w_join(b[j][0], b[j][1]);
+  w_step16_row<TM, TN, 0>(ia, wm, lane, a, fb, acc);
+  w_step16_row<TM, TN, 1>(ia, wm, lane, a, fb, acc);
+  w_step16_row<TM, TN, 2>(ia, wm, lane, a, fb, acc);
+  w_step16_row<TM, TN, 3>(ia, wm, lane, a, fb, acc);
+  w_step16_row<TM, TN, 4>(ia, wm, lane, a, fb, acc);
+  w_step16_row<TM, TN, 5>(ia, wm, lane, a, fb, acc);
+  w_step16_row<TM, TN, 6>(ia, wm, lane, a, fb, acc);
+  w_step16_row<TM, TN, 7>(ia, wm, lane, a, fb, acc);
+}
+
 // TM x TN output tile (256 x 256, or 512 x 128 / 128 x 512 for the 128-wide remainder of a
-// dimension that is 128 mod 256): 8 waves of 128 x 64 as (TM / 128) x (TN / 64); NST-deep ring
-template <bool PARTIAL, int TM, int TN, int NST>
+// dimension that is 128 mod 256): 8 waves of 128 x 64 as (TM / 128) x (TN / 64); NST-deep ring.
+// MF16: the wave tile as 8 x 4 v_mfma_f32_16x16x32_bf16 blocks (one MFMA depth per 32-token step,
+// 16-column fragments, the 8-row image swizzle) instead of 4 x 2 32x32x16 blocks.
+template <bool PARTIAL, int TM, int TN, int NST, bool MF16 = false>
 __global__ __launch_bounds__(WNT, 1) void wgrad_kernel(const uint16_t *__restrict__ dy, int64_t ldy,
                                                        const uint16_t *__restrict__ x, int64_t ldx, int64_t K, int M,
                                                        int N, int splits, int64_t kslice, float *__restrict__ part,
@@ -125,19 +209,27 @@ __global__ __launch_bounds__(WNT, 1) void wgrad_kernel(const uint16_t *__restric
   const int64_t k_end = k_beg + kslice < K ? k_beg + kslice : K;
   const int nsteps = k_end > k_beg ? static_cast<int>((k_end - k_beg) / WBK) : 0;
 
-  wf32x16 acc[4][2];
+  WAcc<MF16> accs;
+  auto &acc = accs.v;
+  if constexpr (MF16) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 4; ++j) acc[i][j] = wf32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  }
 
   auto issue = [&](int st) {  // PER LDS-DMA instructions per wave
     uint16_t *img = lds + (st % NST) * (AIMG + BIMG);
     const int64_t k0 = k_beg + static_cast<int64_t>(st) * WBK;
-    w_stage<TM>(dy, ldy, k0, m0, M, img, wave, lane);
-    w_stage<TN>(x, ldx, k0, n0, N, img + AIMG, wave, lane);
+    w_stage<TM, MF16>(dy, ldy, k0, m0, M, img, wave, lane);
+    w_stage<TN, MF16>(x, ldx, k0, n0, N, img + AIMG, wave, lane);
   };
   for (int b = 0; b < NST - 1; ++b)
     if (b < nsteps) issue(b);
@@ -150,6 +242,9 @@ __global__ __launch_bounds__(WNT, 1) void wgrad_kernel(const uint16_t *__restric
     if (st + NST - 1 < nsteps) issue(st + NST - 1);
     const uint16_t *ia = lds + (st % NST) * (AIMG + BIMG);
     const uint16_t *ib = ia + AIMG;
+    if constexpr (MF16) {
+      w_step16<TM, TN>(ia, ib, wm, wn, lane, acc);
+    } else {
 #pragma unroll
     for (int ss = 0; ss < WBK / 16; ++ss) {
       // issue order A0 B0 B1 A1 A2 A3 (2 reads each); each counted wait releases the fragments it
@@ -181,24 +276,43 @@ __global__ __launch_bounds__(WNT, 1) void wgrad_kernel(const uint16_t *__restric
       acc[3][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb0, acc[3][0], 0, 0, 0);
       acc[3][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb1, acc[3][1], 0, 0, 0);
     }
+    }  // MF16
   }
 
-  // lane holds C[m = m0 + wm 128 + i 32 + w_crow(r, h)][n = n0 + wn 64 + j 32 + (lane & 31)]
-  const int h = lane >> 5, nl = lane & 31;
+  if constexpr (MF16) {
+    // lane holds C[m = m0 + wm 128 + i 16 + 4 (lane >> 4) + e][n = n0 + wn 64 + j 16 + (lane & 15)]
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + nl;
-      if (n >= N) continue;
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+        if (n >= N) continue;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 128 + i * 32 + w_crow(r, h);
-        if (m >= M) continue;
-        if constexpr (PARTIAL) part[(static_cast<int64_t>(s) * M + m) * N + n] = acc[i][j][r];
-        else out[m * ldo + n] = static_cast<uint16_t>(pack2_bf16(acc[i][j][r], 0.f) & 0xffffu);
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wm * 128 + i * 16 + 4 * (lane >> 4) + e;
+          if (m >= M) continue;
+          if constexpr (PARTIAL) part[(static_cast<int64_t>(s) * M + m) * N + n] = acc[i][j][e];
+          else out[m * ldo + n] = static_cast<uint16_t>(pack2_bf16(acc[i][j][e], 0.f) & 0xffffu);
+        }
       }
-    }
+  } else {
+    // lane holds C[m = m0 + wm 128 + i 32 + w_crow(r, h)][n = n0 + wn 64 + j 32 + (lane & 31)]
+    const int h = lane >> 5, nl = lane & 31;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wn * 64 + j * 32 + nl;
+        if (n >= N) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * 128 + i * 32 + w_crow(r, h);
+          if (m >= M) continue;
+          if constexpr (PARTIAL) part[(static_cast<int64_t>(s) * M + m) * N + n] = acc[i][j][r];
+          else out[m * ldo + n] = static_cast<uint16_t>(pack2_bf16(acc[i][j][r], 0.f) & 0xffffu);
+        }
+      }
+  }
 }
 
 // out[m][n] (row stride ldo) = bf16(sum_s part[s][m][n]) in slice order; 4 elements per thread (N % 4 == 0)
@@ -275,7 +389,7 @@ int64_t w_part_bytes(const WPart &p) {
   return p.splits > 1 ? static_cast<int64_t>(sizeof(float)) * p.splits * p.M * p.N : 0;
 }
 
-template <int TM, int TN, int NST>
+template <int TM, int TN, int NST, bool MF16>
 int w_launch(const WPart &p, const uint16_t *dy, int64_t ldy, const uint16_t *x, int64_t ldx, int64_t K,
               float *ws, uint16_t *out, int64_t ldo, hipStream_t st) {
   const int64_t steps = K / WBK;
@@ -286,10 +400,10 @@ int w_launch(const WPart &p, const uint16_t *dy, int64_t ldy, const uint16_t *x,
   VA_CHECK_ARG(nwg < (int64_t{1} << 31) && (p.M * p.N / 4 + 255) / 256 < (int64_t{1} << 31),
                "weight_grad: grid too large (%lld workgroups)", static_cast<long long>(nwg));
   if (p.splits == 1) {
-    hipLaunchKernelGGL((wgrad_kernel<false, TM, TN, NST>), dim3(static_cast<unsigned>(nwg)), dim3(WNT), 0, st, dyp,
+    hipLaunchKernelGGL((wgrad_kernel<false, TM, TN, NST, MF16>), dim3(static_cast<unsigned>(nwg)), dim3(WNT), 0, st, dyp,
                        ldy, xp, ldx, K, static_cast<int>(p.M), static_cast<int>(p.N), 1, kslice, nullptr, op, ldo);
   } else {
-    hipLaunchKernelGGL((wgrad_kernel<true, TM, TN, NST>), dim3(static_cast<unsigned>(nwg)), dim3(WNT), 0, st, dyp,
+    hipLaunchKernelGGL((wgrad_kernel<true, TM, TN, NST, MF16>), dim3(static_cast<unsigned>(nwg)), dim3(WNT), 0, st, dyp,
                        ldy, xp, ldx, K, static_cast<int>(p.M), static_cast<int>(p.N), p.splits, kslice, ws, nullptr,
                        ldo);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(static_cast<unsigned>((p.M * p.N / 4 + 255) / 256)), dim3(256), 0,
@@ -313,6 +427,9 @@ int w_plan_all(int64_t K, int64_t M, int64_t N, int splits, int remainder, WPart
 // tiles vs 182.08 / 181.96K with the remainder tiles (profiles/r04/bench_wgrad_remainder_ab.txt): the
 // half-empty 256-wide tiles cost less than a second launch per weight gradient
 int g_wgrad_remainder = 0;
+// va_set_tuning(VA_TUNE_WGRAD_MFMA): 32 (default) = 4 x 2 v_mfma_f32_32x32x16_bf16 blocks per wave,
+// 16 = 8 x 4 v_mfma_f32_16x16x32_bf16 blocks (the MFMA form of f1's sweep)
+int g_wgrad_mfma = 32;
 
 extern "C" int64_t va_weight_grad_workspace_bytes(int64_t K, int64_t M, int64_t N, int splits) {
   WPart p[2];
@@ -354,9 +471,16 @@ extern "C" int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_
   float *ws = workspace;
   for (int i = 0; i < n; ++i) {
     int rc;
-    if (p[i].kind == 0) rc = w_launch<256, 256, 4>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
-    else if (p[i].kind == 1) rc = w_launch<512, 128, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
-    else rc = w_launch<128, 512, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+    const bool mf16 = g_wgrad_mfma == 16;
+    if (p[i].kind == 0)
+      rc = mf16 ? w_launch<256, 256, 4, true>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+                : w_launch<256, 256, 4, false>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+    else if (p[i].kind == 1)
+      rc = mf16 ? w_launch<512, 128, 3, true>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+                : w_launch<512, 128, 3, false>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+    else
+      rc = mf16 ? w_launch<128, 512, 3, true>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+                : w_launch<128, 512, 3, false>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
     if (rc != VA_OK) return rc;
     ws += w_part_bytes(p[i]) / static_cast<int64_t>(sizeof(float));
   }
