@@ -165,3 +165,27 @@ REMAX_ADV = [[0.75, 0.75, 0.75, 0.0]]
 GAE_REWARDS, GAE_VALUES, GAE_MASK = [[0.0, 0.0, 1.0]], [[0.1, 0.2, 0.3]], [[1, 1, 1]]
 GAE_RETURNS = [[0.13125, 0.325, 1.0]]
 GAE_ADV = [_masked_whiten([0.03125, 0.125, 0.7], [1, 1, 1])]
+
+
+# ---- registered loss variants (core_algos.py:797-972), one row of 4 tokens, mask 1, token-mean ----
+# gpg: -lp A aggregated; metrics 0. lp = [0.1, -0.2, 0.4, 0], A = [1, -1, 2, 0]:
+#   losses [-0.1, -0.2, -0.8, 0] -> -1.1 / 4; d/dlp = -A / 4
+GPG_LP, GPG_ADV = [0.1, -0.2, 0.4, 0.0], [1.0, -1.0, 2.0, 0.0]
+GPG_LOSS = -1.1 / _N4
+GPG_DLP = [-1.0 / _N4, 1.0 / _N4, -2.0 / _N4, 0.0]
+# kl_cov (kl_cov_ratio 0.25 -> k = max(1, int(4 * 0.25)) = 1 token, ppo_kl_coef 1), old = 0: cov =
+# (A - 0.5)(lp - 0.075) = [0.0125, 0.4125, 0.4875, 0.0375] -> token 2 gets + |lp - old| = 0.4:
+#   losses [-e^0.1, e^-0.2, -2 e^0.4 + 0.4, 0]; ppo_kl (slot 2) = masked_mean |lp - old| = 0.7 / 4;
+#   d/dlp = [-e^0.1, e^-0.2, -2 e^0.4 + 1, 0] / 4
+KLCOV_LOSS = (-math.exp(0.1) + math.exp(-0.2) - 2 * math.exp(0.4) + 0.4) / _N4
+KLCOV_PPO_KL = 0.7 / _N4
+KLCOV_DLP = [-math.exp(0.1) / _N4, math.exp(-0.2) / _N4, (-2 * math.exp(0.4) + 1.0) / _N4, 0.0]
+# clip_cov (clip_cov_ratio 0.25 -> 1 token, bounds (1, 5)), lp = old = [1, -0.3, -0.7, 0] (ratio 1,
+# nothing clipped by the ratio), A = [2, -2, 0, 0]: cov = A (lp - 0) = [2, 0.6, 0, 0], only token 0 lies
+# in (1, 5), so the random draw has one candidate: corr = [0, 1, 1, 1];
+#   losses max(l1, l2) corr = [0, 2, 0, 0] -> 2 / 4; clipfrac = 1 / 4; ppo_kl 0;
+#   d/dlp: token 1 at the l1 == l2 tie, torch.maximum's halves both -A r = 2 -> 2 / 4
+CLIPCOV_LP, CLIPCOV_ADV = [1.0, -0.3, -0.7, 0.0], [2.0, -2.0, 0.0, 0.0]
+CLIPCOV_LOSS = 2.0 / _N4
+CLIPCOV_CLIPFRAC = 1.0 / _N4
+CLIPCOV_DLP = [0.0, 2.0 / _N4, 0.0, 0.0]

@@ -163,3 +163,35 @@ def test_estimator_kernels_hand_kats(R):
                                                        pad(C.GAE_MASK).to(torch.int64), 0.5, 0.5)
     assert torch.allclose(ret[:, :3].cpu(), torch.tensor(C.GAE_RETURNS), atol=1e-6)
     assert torch.allclose(adv[:, :3].cpu(), torch.tensor(C.GAE_ADV), atol=1e-5)
+
+
+def test_loss_variant_kernels_hand_kats():
+    """gpg / kl_cov / clip_cov through the registered loss functions (selection on the host, loss and
+    gradient in the fused kernel) against tests/kat_cases.py."""
+    from verl_amd.trainer.ppo import core_algos
+    from verl_amd.utils.config import actor_config
+
+    cfg = actor_config()
+    cfg.policy_loss.kl_cov_ratio = 0.25
+    cfg.policy_loss.ppo_kl_coef = 1.0
+    cfg.policy_loss.clip_cov_ratio = 0.25
+    cfg.policy_loss.clip_cov_lb = 1.0
+    cfg.policy_loss.clip_cov_ub = 5.0
+    m = torch.ones(1, 4, dtype=torch.int64, device=DEV)
+    adv = _t([C.GPG_ADV])
+
+    def run(name, old, lp_vals, a):
+        lp = _t([lp_vals]).requires_grad_(True)
+        out = core_algos.get_policy_loss_fn(name)(old, lp, a, m, "token-mean", cfg)
+        out[0].backward()
+        return [o.item() for o in out], lp.grad[0].cpu()
+
+    (loss, cf, kl, cfl), g = run("gpg", torch.zeros(1, 4, device=DEV), C.GPG_LP, adv)
+    assert abs(loss - C.GPG_LOSS) < 1e-6 and (cf, kl, cfl) == (0.0, 0.0, 0.0)
+    assert torch.allclose(g, torch.tensor(C.GPG_DLP), atol=1e-7)
+    (loss, cf, kl, cfl), g = run("kl_cov", torch.zeros(1, 4, device=DEV), C.GPG_LP, adv)
+    assert abs(loss - C.KLCOV_LOSS) < 1e-6 and abs(kl - C.KLCOV_PPO_KL) < 1e-6
+    assert torch.allclose(g, torch.tensor(C.KLCOV_DLP), atol=1e-6)
+    (loss, cf, kl, cfl), g = run("clip_cov", _t([C.CLIPCOV_LP]), C.CLIPCOV_LP, _t([C.CLIPCOV_ADV]))
+    assert abs(loss - C.CLIPCOV_LOSS) < 1e-6 and abs(cf - C.CLIPCOV_CLIPFRAC) < 1e-6 and kl == 0.0
+    assert torch.allclose(g, torch.tensor(C.CLIPCOV_DLP), atol=1e-7)

@@ -274,3 +274,22 @@ def test_estimator_hand_kats():
                                                 torch.tensor(C.GAE_MASK, dtype=d), 0.5, 0.5)
     assert torch.allclose(ret, torch.tensor(C.GAE_RETURNS, dtype=d), atol=1e-12)
     assert torch.allclose(adv, torch.tensor(C.GAE_ADV, dtype=d), atol=1e-9)
+
+
+def test_loss_variant_hand_kats():
+    """gpg / kl_cov on the oracle against tests/kat_cases.py (clip_cov's random draw is pinned on the
+    kernels, tests/test_kats_gpu.py, where the selection has one candidate)."""
+    from tests import kat_cases as C
+
+    d = torch.float64
+    m = torch.ones(1, 4, dtype=d)
+    lp = torch.tensor([C.GPG_LP], dtype=d, requires_grad=True)
+    loss = ref.compute_policy_loss_gpg(lp, torch.tensor([C.GPG_ADV], dtype=d), m)
+    loss.backward()
+    assert abs(loss.item() - C.GPG_LOSS) < 1e-12 and torch.allclose(lp.grad[0], torch.tensor(C.GPG_DLP, dtype=d))
+    lp = torch.tensor([C.GPG_LP], dtype=d, requires_grad=True)
+    loss, kl = ref.compute_policy_loss_kl_cov(torch.zeros(1, 4, dtype=d), lp, torch.tensor([C.GPG_ADV], dtype=d), m,
+                                              kl_cov_ratio=0.25, ppo_kl_coef=1.0)
+    loss.backward()
+    assert abs(loss.item() - C.KLCOV_LOSS) < 1e-12 and abs(kl.item() - C.KLCOV_PPO_KL) < 1e-12
+    assert torch.allclose(lp.grad[0], torch.tensor(C.KLCOV_DLP, dtype=d), atol=1e-12)
