@@ -195,3 +195,19 @@ def test_loss_variant_kernels_hand_kats():
     (loss, cf, kl, cfl), g = run("clip_cov", _t([C.CLIPCOV_LP]), C.CLIPCOV_LP, _t([C.CLIPCOV_ADV]))
     assert abs(loss - C.CLIPCOV_LOSS) < 1e-6 and abs(cf - C.CLIPCOV_CLIPFRAC) < 1e-6 and kl == 0.0
     assert torch.allclose(g, torch.tensor(C.CLIPCOV_DLP), atol=1e-7)
+
+
+def test_value_loss_kernel_hand_kat():
+    """core_algos.py:992-1031 by hand (the oracle's test_value_loss_kats): values 0, cliprange 0.5,
+    vpreds 2 -> clipped 0.5; returns 0: (2 - 0)^2 = 4 vs (0.5 - 0)^2 = 0.25 -> 4 (unclipped wins);
+    returns 3: 1 vs 6.25 -> 6.25 (clipped wins). loss = 0.5 mean = 0.5 (4 + 6.25) / 2, clipfrac 1/2;
+    d loss / d vpreds = 0.5 * 2 (2 - 0) / 2 for token 0 and 0 for token 1 (the clipped branch is flat)."""
+    from verl_amd.trainer.ppo import core_algos
+
+    vp = _t([[2.0, 2.0]]).requires_grad_(True)
+    loss, frac = core_algos.compute_value_loss(vp, _t([[0.0, 3.0]]), _t([[0.0, 0.0]]),
+                                               torch.ones(1, 2, dtype=torch.int64, device=DEV), 0.5)
+    loss.backward()
+    assert abs(loss.item() - 0.5 * (4.0 + 6.25) / (2 + 1e-8)) < 1e-6
+    assert abs(frac.item() - 1 / (2 + 1e-8)) < 1e-7
+    assert torch.allclose(vp.grad.cpu(), torch.tensor([[2.0 / (2 + 1e-8), 0.0]]), atol=1e-6)

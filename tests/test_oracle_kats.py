@@ -293,3 +293,23 @@ def test_loss_variant_hand_kats():
     loss.backward()
     assert abs(loss.item() - C.KLCOV_LOSS) < 1e-12 and abs(kl.item() - C.KLCOV_PPO_KL) < 1e-12
     assert torch.allclose(lp.grad[0], torch.tensor(C.KLCOV_DLP, dtype=d), atol=1e-12)
+
+
+def test_kl_controllers_hand_kats():
+    """core_algos.py:131-190 on the product's host classes: adaptive value *= 1 + clip(kl/target - 1,
+    +-0.2) n/horizon; fixed never moves; the horizon assertion and unknown types."""
+    from verl_amd.trainer.ppo.core_algos import get_kl_controller
+    from verl_amd.utils.config import AttrDict
+
+    c = get_kl_controller(AttrDict(type="adaptive", kl_coef=0.1, target_kl=6.0, horizon=10000))
+    c.update(current_kl=12.0, n_steps=100)  # error clipped to 0.2: x 1.002
+    assert c.value == pytest.approx(0.1002, rel=1e-12)
+    c.update(current_kl=5.4, n_steps=500)  # error -0.1: x 0.995
+    assert c.value == pytest.approx(0.1002 * 0.995, rel=1e-12)
+    f = get_kl_controller(AttrDict(type="fixed", kl_coef=0.3))
+    f.update(current_kl=100.0, n_steps=10)
+    assert f.value == 0.3
+    with pytest.raises(AssertionError, match="horizon must be larger than 0"):
+        get_kl_controller(AttrDict(type="adaptive", kl_coef=0.1, target_kl=6.0, horizon=0))
+    with pytest.raises(NotImplementedError):
+        get_kl_controller(AttrDict(type="pid", kl_coef=0.1))
