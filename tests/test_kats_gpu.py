@@ -211,3 +211,43 @@ def test_value_loss_kernel_hand_kat():
     assert abs(loss.item() - 0.5 * (4.0 + 6.25) / (2 + 1e-8)) < 1e-6
     assert abs(frac.item() - 1 / (2 + 1e-8)) < 1e-7
     assert torch.allclose(vp.grad.cpu(), torch.tensor([[2.0 / (2 + 1e-8), 0.0]]), atol=1e-6)
+
+
+def test_group_estimators_on_an_empty_batch():
+    """B = 0: the reference's group loops do not run (core_algos.py:282-308, 311-370, 428-667), so
+    GRPO / Dr.GRPO / pass@k / RLOO / OPO / GPG / ReMax return empty [0, R] advantages; RF++-baseline,
+    RF++ and GAE reach masked_whiten with an all-zero mask and raise its ValueError."""
+    from verl_amd.trainer.ppo import core_algos
+    from verl_amd.utils.config import AttrDict
+
+    r = torch.zeros(0, 8, device=DEV)
+    m = torch.zeros(0, 8, dtype=torch.int64, device=DEV)
+    idx = np.array([], dtype=object)
+    outs = [core_algos.compute_grpo_outcome_advantage(r, m, idx),
+            core_algos.compute_grpo_outcome_advantage(r, m, idx, norm_adv_by_std_in_grpo=False),
+            core_algos.compute_grpo_passk_outcome_advantage(r, m, idx, config=AttrDict(norm_adv_by_std_in_grpo=True)),
+            core_algos.compute_rloo_outcome_advantage(r, m, idx),
+            core_algos.compute_opo_outcome_advantage(r, m, idx),
+            core_algos.compute_gpg_outcome_advantage(r, m, idx)]
+    for adv, ret in outs:
+        assert adv.shape == (0, 8) and ret.shape == (0, 8) and adv.dtype == torch.float32
+    adv, ret = core_algos.compute_remax_outcome_advantage(r, torch.zeros(0, device=DEV), m, config=AttrDict(gamma=1.0))
+    assert adv.shape == (0, 8) and ret.shape == (0, 8)
+    for fn in (lambda: core_algos.compute_reinforce_plus_plus_baseline_outcome_advantage(r, m, idx),
+               lambda: core_algos.compute_reinforce_plus_plus_outcome_advantage(r, m, config=AttrDict(gamma=1.0)),
+               lambda: core_algos.compute_gae_advantage_return(r, r, m, 1.0, 1.0)):
+        with pytest.raises(ValueError, match="At least one element in the mask has to be 1"):
+            fn()
+
+
+def test_agg_loss_fully_masked_row():
+    """agg_loss with a row whose mask is all 0 (core_algos.py:686-719): token-mean and the sum modes
+    ignore it, seq-mean-token-mean divides 0 by 0 for it and returns NaN, as torch does."""
+    from verl_amd.trainer.ppo import core_algos
+
+    x = _t([[1.0, 2.0, 3.0], [4.0, 5.0, 6.0]])
+    m = _t([[1, 1, 0], [0, 0, 0]], torch.int64)
+    assert abs(core_algos.agg_loss(x, m, "token-mean").item() - 3.0 / (2 + 1e-8)) < 1e-6
+    assert core_algos.agg_loss(x, m, "seq-mean-token-sum").item() == 1.5
+    assert core_algos.agg_loss(x, m, "seq-mean-token-sum-norm").item() == 1.0
+    assert torch.isnan(core_algos.agg_loss(x, m, "seq-mean-token-mean")).item()

@@ -132,13 +132,20 @@ def get_kl_controller(kl_ctrl):
 @register_adv_est(AdvantageEstimator.GAE)
 def compute_gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam):
     """core_algos.py:193-241 — returns (whitened advantages, returns)."""
+    if token_level_rewards.shape[0] == 0:  # masked_whiten over an empty mask: the reference's ValueError
+        raise ValueError("At least one element in the mask has to be 1.")
     with torch.no_grad():
         return K.gae_advantage_return(token_level_rewards, values, response_mask, float(gamma), float(lam))
 
 
-def _no_empty_group(index):
-    if len(index) == 0:
-        raise ValueError("no score in prompt index: <empty batch>")
+def _empty_batch(token_level_rewards, response_mask):
+    """An empty batch (B = 0): the reference's group loops do not run and it returns the empty
+    [0, R] scores x mask (core_algos.py:282-308, 428-530, 311-370), so these estimators return it too
+    (the group kernels need B > 0)."""
+    if token_level_rewards.shape[0] != 0:
+        return None
+    empty = torch.zeros(token_level_rewards.shape, dtype=torch.float32, device=token_level_rewards.device)
+    return empty * response_mask
 
 
 @register_adv_est(AdvantageEstimator.GRPO)
@@ -151,7 +158,9 @@ def compute_grpo_outcome_advantage(
     config=None,
 ) -> tuple[torch.Tensor, torch.Tensor]:
     """core_algos.py:246-308 — GRPO (or Dr.GRPO when norm_adv_by_std_in_grpo is False)."""
-    _no_empty_group(index)
+    empty = _empty_batch(token_level_rewards, response_mask)
+    if empty is not None:
+        return empty, empty
     est = L.VA_ADV_GRPO if norm_adv_by_std_in_grpo else L.VA_ADV_GRPO_NOSTD
     with torch.no_grad():
         scores = K.outcome_advantage(token_level_rewards, response_mask, index, epsilon, est)
@@ -169,6 +178,9 @@ def compute_grpo_passk_outcome_advantage(token_level_rewards, response_mask, ind
     if len(counts) and counts.min() < 2:
         bad = uids[int(np.argmin(counts))]
         raise ValueError(f"Pass@k requires at least 2 samples per group. Got {int(counts.min())} for group {bad}.")
+    empty = _empty_batch(token_level_rewards, response_mask)
+    if empty is not None:
+        return empty, empty
     est = L.VA_ADV_PASSK if norm else L.VA_ADV_PASSK_NOSTD
     with torch.no_grad():
         adv = K.outcome_advantage(token_level_rewards, response_mask, index, epsilon, est)
@@ -178,8 +190,10 @@ def compute_grpo_passk_outcome_advantage(token_level_rewards, response_mask, ind
 @register_adv_est(AdvantageEstimator.REINFORCE_PLUS_PLUS_BASELINE)
 def compute_reinforce_plus_plus_baseline_outcome_advantage(token_level_rewards, response_mask, index, epsilon=1e-6,
                                                            config=None, **kwargs):
-    """core_algos.py:376-424: group-mean baseline, then masked whitening, times the mask."""
-    _no_empty_group(index)
+    """core_algos.py:376-424: group-mean baseline, then masked whitening, times the mask (an empty
+    batch reaches masked_whiten with an all-zero mask: the reference's ValueError)."""
+    if token_level_rewards.shape[0] == 0:
+        raise ValueError("At least one element in the mask has to be 1.")
     with torch.no_grad():
         # the reference tiles the (s - mean) scalar over all columns before masking: same values
         ones = torch.ones_like(token_level_rewards, dtype=torch.float32)
@@ -194,7 +208,9 @@ def compute_reinforce_plus_plus_baseline_outcome_advantage(token_level_rewards, 
 @register_adv_est(AdvantageEstimator.RLOO)
 def compute_rloo_outcome_advantage(token_level_rewards, response_mask, index, epsilon=1e-6, config=None, **kwargs):
     """core_algos.py:428-476 — leave-one-out baseline."""
-    _no_empty_group(index)
+    empty = _empty_batch(token_level_rewards, response_mask)
+    if empty is not None:
+        return empty, empty
     with torch.no_grad():
         scores = K.outcome_advantage(token_level_rewards, response_mask, index, epsilon, L.VA_ADV_RLOO)
     return scores, scores
@@ -204,7 +220,9 @@ def compute_rloo_outcome_advantage(token_level_rewards, response_mask, index, ep
 def compute_opo_outcome_advantage(token_level_rewards, response_mask, index, epsilon=1e-6, config=None, **kwargs):
     """core_algos.py:479-530 — length-weighted group baseline sum(len*s)/sum(len) (singleton
     groups: baseline 0); one group kernel."""
-    _no_empty_group(index)
+    empty = _empty_batch(token_level_rewards, response_mask)
+    if empty is not None:
+        return empty, empty
     with torch.no_grad():
         scores = K.outcome_advantage(token_level_rewards, response_mask, index, epsilon, L.VA_ADV_OPO)
     return scores, scores
@@ -216,6 +234,8 @@ def compute_reinforce_plus_plus_outcome_advantage(token_level_rewards, response_
     masked whitening (whiten kernels; the reference's ValueErrors), times the mask."""
     assert config is not None
     gamma = config.gamma
+    if token_level_rewards.shape[0] == 0:  # masked_whiten over an empty mask: the reference's ValueError
+        raise ValueError("At least one element in the mask has to be 1.")
     with torch.no_grad():
         returns = K.discounted_returns(token_level_rewards, response_mask, gamma, L.VA_RET_RFPP)
         stats, _ = K.whiten_stats(returns, response_mask)
@@ -228,6 +248,9 @@ def compute_reinforce_plus_plus_outcome_advantage(token_level_rewards, response_
 def compute_remax_outcome_advantage(token_level_rewards, reward_baselines, response_mask, config=None, **kwargs):
     """core_algos.py:572-605 — reverse cumulative sum of r * mask (scan kernel) minus the
     per-response baseline on valid tokens."""
+    empty = _empty_batch(token_level_rewards, response_mask)
+    if empty is not None:
+        return empty, empty
     with torch.no_grad():
         returns, advantages = K.discounted_returns(token_level_rewards, response_mask, 1.0, L.VA_RET_REMAX,
                                                    baselines=reward_baselines)
@@ -238,6 +261,9 @@ def compute_remax_outcome_advantage(token_level_rewards, reward_baselines, respo
 def compute_gpg_outcome_advantage(token_level_rewards, response_mask, index, epsilon=1e-6, f_norm=1.0, alpha=1.0,
                                   config=None, **kwargs):
     """core_algos.py:608-667: alpha = B / max(#nonzero scores, 1); (s - mean) * alpha / f_norm."""
+    empty = _empty_batch(token_level_rewards, response_mask)
+    if empty is not None:
+        return empty, empty
     scores = token_level_rewards.sum(dim=-1)
     with torch.no_grad():
         alpha = scores.shape[0] / torch.count_nonzero(scores).clamp(min=1)
