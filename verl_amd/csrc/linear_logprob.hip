@@ -346,14 +346,24 @@ __device__ __forceinline__ void t_tile_epilogue(const f32x4 (&acc)[8][4], int v0
 // of [vt_begin, vt_end) it accumulates S^T = W_tile . H_tile^T (256 vocab x 256 tokens) over K in acc,
 // calls tile(acc, vt) once the tile is complete, and zeroes acc. acc[i][j][e] holds vocab
 // vt * 256 + wr * 128 + (lane >> 4) * 4 + i * 16 + e for token row0 + wc * 64 + j * 16 + (lane & 15).
-template <typename Tile, typename WMap = IdentityRows>
+// SKEW: wave-row 1 runs nk / 2 K-steps behind wave-row 0, so the two waves that share a SIMD (w and
+// w + 4) reach their tile epilogues half a tile apart and one's exp / sum work issues under the
+// other's MFMAs instead of both stalling the matrix core at once. The hidden image is shared, so
+// wave-row 1 takes each tile's K-chunks in the rotated order nk / 2, ..., nk - 1, 0, ..., nk / 2 - 1
+// (its fp32 sums differ from wave-row 0's order only in rounding); each wave stages its own half of
+// the weight image (t_stage: wave w loads image rows 32 w .. 32 w + 31, i.e. its wave-row's half)
+// from its own tile. The sweep takes nk / 2 extra steps, in which one wave-row idles.
+template <bool SKEW = false, typename Tile, typename WMap = IdentityRows>
 __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int64_t ldh,
                                            const uint16_t *__restrict__ w, int64_t ldw, int64_t N, int K, int64_t V,
                                            int64_t row0, int64_t vt_begin, int64_t vt_end, uint16_t *lds, int wave,
                                            int lane, Tile &&tile, const WMap &wmap = WMap{}) {
   const int wr = wave >> 2, wc = wave & 3;
   const int nk = K / TK;
-  const int64_t nsteps = vt_begin < vt_end ? (vt_end - vt_begin) * nk : 0;
+  const int64_t nmine = vt_begin < vt_end ? (vt_end - vt_begin) * nk : 0;  // K-steps of each wave-row
+  // this wave-row's lag (wave-uniform: read from lane 0 so the branches below are scalar)
+  const int lag = SKEW ? (__builtin_amdgcn_readfirstlane(wave) >> 2) * (nk >> 1) : 0;
+  const int64_t nsteps = nmine > 0 ? nmine + (SKEW ? (nk >> 1) : 0) : 0;
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -366,17 +376,33 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+  // step counters kept incrementally: a 64-bit division per step is ~130 scalar instructions (the
+  // loop's SALU count before this, per wave and K-step, next to 64 MFMAs)
+  int64_t ls = -lag;     // this wave-row's own step at loop step st (negative: not started)
+  int kt = 0;            // ls mod nk once ls >= 0: the K-chunks of the current tile done so far
+  int64_t vt = vt_begin; // vt_begin + ls / nk: the tile being accumulated
+  int hk = 0;            // st mod nk: the K-chunk in the staged images (shared by both wave-rows)
   for (int64_t st = 0; st < nsteps; ++st) {
     const int buf = static_cast<int>(st & 1);
-    const int kt = static_cast<int>(st % nk);
-    const int64_t vt = vt_begin + st / nk;
+    const bool active = !SKEW || (ls >= 0 && ls < nmine);
+    const int hk1 = hk + 1 == nk ? 0 : hk + 1;
     const uint16_t *la = lds + buf * 2 * T_TILE;
     const uint16_t *lb = la + T_TILE;
     if (st + 1 < nsteps) {
+      // the tile of own step ls + 1, clamped into the range (a wave-row's idle steps stage a valid
+      // tile that nobody reads)
+      int64_t vs = ls + 1 <= 0 ? vt_begin : (kt + 1 == nk ? vt + 1 : vt);
+      if (SKEW && vs >= vt_end) vs = vt_end - 1;
       uint16_t *na = lds + (buf ^ 1) * 2 * T_TILE;
-      const int k1 = static_cast<int>((st + 1) % nk) * TK;
-      t_stage(w, (vt_begin + (st + 1) / nk) * TB, V, ldw, k1, na, wave, lane, wmap);
-      t_stage(hid, row0, N, ldh, k1, na + T_TILE, wave, lane);
+      t_stage(w, vs * TB, V, ldw, hk1 * TK, na, wave, lane, wmap);
+      t_stage(hid, row0, N, ldh, hk1 * TK, na + T_TILE, wave, lane);
+    }
+    hk = hk1;
+    if (!active) {
+      ++ls;
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      continue;
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -399,7 +425,12 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      kt = 0;
+      ++vt;
+    } else {
+      ++kt;
     }
+    ++ls;
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
@@ -423,7 +454,7 @@ __device__ __forceinline__ void t256_block(int splits, int tiles_per_split, int6
   vt_end = vt_begin + tiles_per_split < n_vt ? vt_begin + tiles_per_split : n_vt;
 }
 
-template <bool SCALE, bool ROUND, bool REMAP>
+template <bool SCALE, bool ROUND, bool REMAP, bool SKEW>
 __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
     const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
     const int64_t *__restrict__ labels, int64_t N, int K, int64_t V, int splits, int tiles_per_split,
@@ -447,7 +478,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
     m[j] = -INFINITY, s[j] = 0.f, t[j] = 0.f, ll[j] = -INFINITY;
   }
 
-  t256_sweep(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
+  t256_sweep<SKEW>(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
     // acc[i][j][e] = logit of vocab v0 + i * 16 + e for token j of this lane
     const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;  // V < 2^31
     if (vt * TB + TB > V) {  // uniform: only the last vocab tile has rows past V
@@ -684,17 +715,20 @@ using namespace va;
 // va_set_tuning(VA_TUNE_LINEAR_LOGPROB_TILE): 128 (the 128 x 128 register-staged kernel) or 256
 // (the 256 x 256 LDS-DMA kernel above)
 int g_linear_logprob_tile = 256;
+// va_set_tuning(VA_TUNE_F1_SKEW): 1 = the forward sweep's wave-row 1 runs half a tile behind
+// (t256_sweep SKEW), 0 = both wave-rows in step
+int g_f1_skew = 0;
 
 template <bool SC, bool RD>
 static void launch_t256(bool remap, dim3 grid, hipStream_t s, const uint16_t *h16, int64_t ldh, const uint16_t *w16,
                         int64_t ldw, const int64_t *labels, int64_t N, int64_t H, int64_t V, int used, int per,
                         float temperature, float *part, float *label_logit) {
-  if (remap)
-    hipLaunchKernelGGL((linear_logprob_t256_kernel<SC, RD, true>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16, ldw,
-                       labels, N, static_cast<int>(H), V, used, per, temperature, part, label_logit);
-  else
-    hipLaunchKernelGGL((linear_logprob_t256_kernel<SC, RD, false>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16, ldw,
-                       labels, N, static_cast<int>(H), V, used, per, temperature, part, label_logit);
+  const auto kern = remap ? (g_f1_skew ? linear_logprob_t256_kernel<SC, RD, true, true>
+                                        : linear_logprob_t256_kernel<SC, RD, true, false>)
+                          : (g_f1_skew ? linear_logprob_t256_kernel<SC, RD, false, true>
+                                       : linear_logprob_t256_kernel<SC, RD, false, false>);
+  hipLaunchKernelGGL(kern, grid, dim3(T_THREADS), 0, s, h16, ldh, w16, ldw, labels, N, static_cast<int>(H), V, used,
+                     per, temperature, part, label_logit);
 }
 
 extern "C" int64_t va_linear_logprob_workspace_bytes(int64_t N, int splits) {
