@@ -164,10 +164,6 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *     dimension that is 128 mod 256 gets its last 128 rows / columns as 128 x 512 / 512 x 128 tiles.
  *   VA_TUNE_WGRAD_MFMA (va_weight_grad): 32 (default) = 32x32x16 MFMA blocks; 16 = 16x16x32 blocks
  *     (same tiles and staging; results differ only in the MFMA's internal summation order).
- *   VA_TUNE_F1_SKEW (va_linear_logprob_fwd, 256 tiles): 1 = the second vocab wave-row runs half a
- *     tile of K-steps behind the first, so the two waves of a SIMD reach their softmax epilogues at
- *     different times (its logits summed over K in a rotated chunk order: fp32 rounding only);
- *     0 = both wave-rows in step.
  *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
 *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order);
  *   VA_TUNE_FLASH_DMA (va_flash_attn_fwd / _bwd): bit 1 = forward K / V blocks staged by LDS-DMA
@@ -193,7 +189,6 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_WGRAD_REMAINDER 18
 #define VA_TUNE_FLASH_DMA 19
 #define VA_TUNE_WGRAD_MFMA 20
-#define VA_TUNE_F1_SKEW 21
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

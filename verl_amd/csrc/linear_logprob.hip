@@ -253,8 +253,11 @@ constexpr int T_TILE = TB * TK;  // bf16 elements of one operand's K-step image
 __device__ __forceinline__ int t_img_off(int row, int c) { return row * TK + ((c ^ ((row >> 1) & 7)) << 3); }
 
 // image row -> source row of the streamed (weight) operand: the identity for the lm_head; the gate|up
-// pairing (GateUpRows below) for the fused SwiGLU projection
+// pairing (GateUpRows below) for the fused SwiGLU projection. kTileStep: source rows one 256-row
+// image tile advances, so that map(t * 256 + r) = map(r) + t * kTileStep (the sweep's per-lane
+// staging offsets are computed once from map(r)).
 struct IdentityRows {
+  static constexpr int64_t kTileStep = 256;
   __device__ __forceinline__ int64_t operator()(int64_t r) const { return r; }
 };
 
@@ -346,63 +349,67 @@ __device__ __forceinline__ void t_tile_epilogue(const f32x4 (&acc)[8][4], int v0
 // of [vt_begin, vt_end) it accumulates S^T = W_tile . H_tile^T (256 vocab x 256 tokens) over K in acc,
 // calls tile(acc, vt) once the tile is complete, and zeroes acc. acc[i][j][e] holds vocab
 // vt * 256 + wr * 128 + (lane >> 4) * 4 + i * 16 + e for token row0 + wc * 64 + j * 16 + (lane & 15).
-// SKEW: wave-row 1 runs nk / 2 K-steps behind wave-row 0, so the two waves that share a SIMD (w and
-// w + 4) reach their tile epilogues half a tile apart and one's exp / sum work issues under the
-// other's MFMAs instead of both stalling the matrix core at once. The hidden image is shared, so
-// wave-row 1 takes each tile's K-chunks in the rotated order nk / 2, ..., nk - 1, 0, ..., nk / 2 - 1
-// (its fp32 sums differ from wave-row 0's order only in rounding); each wave stages its own half of
-// the weight image (t_stage: wave w loads image rows 32 w .. 32 w + 31, i.e. its wave-row's half)
-// from its own tile. The sweep takes nk / 2 extra steps, in which one wave-row idles.
-template <bool SKEW = false, typename Tile, typename WMap = IdentityRows>
+// Staging addresses: each lane's 4 hidden rows (clamped at N) and its 4 weight-image rows' offsets
+// within a tile are fixed for the sweep and computed once; per K-step only the scalar tile / chunk
+// base moves (the last vocab tile, whose rows pass V, takes the clamped per-lane path).
+template <typename Tile, typename WMap = IdentityRows>
 __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int64_t ldh,
                                            const uint16_t *__restrict__ w, int64_t ldw, int64_t N, int K, int64_t V,
                                            int64_t row0, int64_t vt_begin, int64_t vt_end, uint16_t *lds, int wave,
                                            int lane, Tile &&tile, const WMap &wmap = WMap{}) {
   const int wr = wave >> 2, wc = wave & 3;
   const int nk = K / TK;
-  const int64_t nmine = vt_begin < vt_end ? (vt_end - vt_begin) * nk : 0;  // K-steps of each wave-row
-  // this wave-row's lag (wave-uniform: read from lane 0 so the branches below are scalar)
-  const int lag = SKEW ? (__builtin_amdgcn_readfirstlane(wave) >> 2) * (nk >> 1) : 0;
-  const int64_t nsteps = nmine > 0 ? nmine + (SKEW ? (nk >> 1) : 0) : 0;
+  const int64_t nsteps = vt_begin < vt_end ? (vt_end - vt_begin) * nk : 0;
+  const uint16_t *hsrc[4];
+  int64_t woff[4];
+  int ldsoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int g = wave * 4 + i;  // 32 groups of 8 rows (1 KB each)
+    const int row = g * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((row >> 1) & 7);
+    int64_t hr = row0 + row;
+    if (hr >= N) hr = N - 1;  // clamped rows are computed and discarded
+    hsrc[i] = hid + hr * ldh + lc * 8;
+    woff[i] = wmap(row) * ldw + lc * 8;
+    ldsoff[i] = g * 8 * TK;
+  }
+  // stage K-chunk kc of vocab tile vs (weight) and of the row block (hidden) into image pair img
+  auto stage = [&](int64_t vs, int kc, uint16_t *img) {
+    const int k0 = kc * TK;
+    if (vs * TB + TB <= V) {
+      const uint16_t *wb = w + vs * WMap::kTileStep * ldw + k0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(wb + woff[i]), img + ldsoff[i], 16, 0, 0);
+    } else {
+      t_stage(w, vs * TB, V, ldw, k0, img, wave, lane, wmap);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(hsrc[i] + k0), img + T_TILE + ldsoff[i], 16, 0,
+                                       0);
+  };
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nsteps > 0) {
-    t_stage(w, vt_begin * TB, V, ldw, 0, lds, wave, lane, wmap);
-    t_stage(hid, row0, N, ldh, 0, lds + T_TILE, wave, lane);
-  }
+  if (nsteps > 0) stage(vt_begin, 0, lds);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  // step counters kept incrementally: a 64-bit division per step is ~130 scalar instructions (the
-  // loop's SALU count before this, per wave and K-step, next to 64 MFMAs)
-  int64_t ls = -lag;     // this wave-row's own step at loop step st (negative: not started)
-  int kt = 0;            // ls mod nk once ls >= 0: the K-chunks of the current tile done so far
-  int64_t vt = vt_begin; // vt_begin + ls / nk: the tile being accumulated
-  int hk = 0;            // st mod nk: the K-chunk in the staged images (shared by both wave-rows)
+  // step counters kept incrementally: a 64-bit division per step is ~130 scalar instructions (two
+  // of them per K-step before round 5: 33.08 -> 32.17 ms at the bench shape, f1_counter_ab.jsonl)
+  int kt = 0;             // K-chunks of the current tile done so far
+  int64_t vt = vt_begin;  // the tile being accumulated
   for (int64_t st = 0; st < nsteps; ++st) {
     const int buf = static_cast<int>(st & 1);
-    const bool active = !SKEW || (ls >= 0 && ls < nmine);
-    const int hk1 = hk + 1 == nk ? 0 : hk + 1;
     const uint16_t *la = lds + buf * 2 * T_TILE;
     const uint16_t *lb = la + T_TILE;
     if (st + 1 < nsteps) {
-      // the tile of own step ls + 1, clamped into the range (a wave-row's idle steps stage a valid
-      // tile that nobody reads)
-      int64_t vs = ls + 1 <= 0 ? vt_begin : (kt + 1 == nk ? vt + 1 : vt);
-      if (SKEW && vs >= vt_end) vs = vt_end - 1;
-      uint16_t *na = lds + (buf ^ 1) * 2 * T_TILE;
-      t_stage(w, vs * TB, V, ldw, hk1 * TK, na, wave, lane, wmap);
-      t_stage(hid, row0, N, ldh, hk1 * TK, na + T_TILE, wave, lane);
-    }
-    hk = hk1;
-    if (!active) {
-      ++ls;
-      __builtin_amdgcn_s_waitcnt(0);
-      __syncthreads();
-      continue;
+      const bool last = kt + 1 == nk;
+      stage(last ? vt + 1 : vt, last ? 0 : kt + 1, lds + (buf ^ 1) * 2 * T_TILE);
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -430,7 +437,6 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
     } else {
       ++kt;
     }
-    ++ls;
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
@@ -454,7 +460,7 @@ __device__ __forceinline__ void t256_block(int splits, int tiles_per_split, int6
   vt_end = vt_begin + tiles_per_split < n_vt ? vt_begin + tiles_per_split : n_vt;
 }
 
-template <bool SCALE, bool ROUND, bool REMAP, bool SKEW>
+template <bool SCALE, bool ROUND, bool REMAP>
 __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
     const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
     const int64_t *__restrict__ labels, int64_t N, int K, int64_t V, int splits, int tiles_per_split,
@@ -478,7 +484,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
     m[j] = -INFINITY, s[j] = 0.f, t[j] = 0.f, ll[j] = -INFINITY;
   }
 
-  t256_sweep<SKEW>(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
+  t256_sweep(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
     // acc[i][j][e] = logit of vocab v0 + i * 16 + e for token j of this lane
     const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;  // V < 2^31
     if (vt * TB + TB > V) {  // uniform: only the last vocab tile has rows past V
@@ -658,6 +664,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
 // storing 4 consecutive features of a token (8 bytes) per (i, j). Per element the arithmetic of
 // swiglu_fwd (model_ops.hip), so on exact-arithmetic data the output equals GEMM + swiglu bitwise.
 struct GateUpRows {
+  static constexpr int64_t kTileStep = 128;
   int64_t F;
   __device__ __forceinline__ int64_t operator()(int64_t r) const {
     const int64_t t = r >> 8;  // 256 image rows per 128 features
@@ -715,18 +722,12 @@ using namespace va;
 // va_set_tuning(VA_TUNE_LINEAR_LOGPROB_TILE): 128 (the 128 x 128 register-staged kernel) or 256
 // (the 256 x 256 LDS-DMA kernel above)
 int g_linear_logprob_tile = 256;
-// va_set_tuning(VA_TUNE_F1_SKEW): 1 = the forward sweep's wave-row 1 runs half a tile behind
-// (t256_sweep SKEW), 0 = both wave-rows in step
-int g_f1_skew = 0;
 
 template <bool SC, bool RD>
 static void launch_t256(bool remap, dim3 grid, hipStream_t s, const uint16_t *h16, int64_t ldh, const uint16_t *w16,
                         int64_t ldw, const int64_t *labels, int64_t N, int64_t H, int64_t V, int used, int per,
                         float temperature, float *part, float *label_logit) {
-  const auto kern = remap ? (g_f1_skew ? linear_logprob_t256_kernel<SC, RD, true, true>
-                                        : linear_logprob_t256_kernel<SC, RD, true, false>)
-                          : (g_f1_skew ? linear_logprob_t256_kernel<SC, RD, false, true>
-                                       : linear_logprob_t256_kernel<SC, RD, false, false>);
+  const auto kern = remap ? linear_logprob_t256_kernel<SC, RD, true> : linear_logprob_t256_kernel<SC, RD, false>;
   hipLaunchKernelGGL(kern, grid, dim3(T_THREADS), 0, s, h16, ldh, w16, ldw, labels, N, static_cast<int>(H), V, used,
                      per, temperature, part, label_logit);
 }

@@ -716,7 +716,6 @@ extern int g_whiten_slice_min;    // advantage.hip
 extern int g_linear_logprob_tile;  // linear_logprob.hip
 extern int g_wgrad_remainder;      // wgrad.hip
 extern int g_wgrad_mfma;           // wgrad.hip
-extern int g_f1_skew;              // linear_logprob.hip
 extern int g_whiten_grid;         // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
 extern int g_flash_dkdv_qt;       // attention.hip
@@ -748,13 +747,6 @@ extern "C" int va_set_tuning(int key, int value) {
         return VA_E_ARG;
       }
       g_wgrad_mfma = value;
-      return VA_OK;
-    case VA_TUNE_F1_SKEW:
-      if (value != 0 && value != 1) {
-        va::set_error("va_set_tuning: VA_TUNE_F1_SKEW must be 0 or 1 (got %d)", value);
-        return VA_E_ARG;
-      }
-      g_f1_skew = value;
       return VA_OK;
     case VA_TUNE_LINEAR_LOGPROB_TILE:
       if (value != 128 && value != 256) {
