@@ -468,7 +468,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
   // ONE LDS array (a second __shared__ object can cost a vmcnt(0) per K-step): 2 staging buffers of
   // (weight, hidden) images; reused for the final merge of the two vocab wave-rows
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar LDS-DMA bases
   const int wr = wave >> 2, wc = wave & 3;
   int64_t row0, sp, vt_begin, vt_end;
   t256_block<REMAP>(splits, tiles_per_split, V, row0, sp, vt_begin, vt_end);
@@ -592,7 +592,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
     const float *__restrict__ g_logp, const float *__restrict__ g_ent, int64_t N, int K, int64_t V, int64_t V_full,
     int64_t vbase, int splits, int tiles_per_split, float temperature, uint16_t *__restrict__ dlog, int64_t ldd) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar LDS-DMA bases
   const int wr = wave >> 2, wc = wave & 3;
   int64_t row0, sp, vt_begin, vt_end;
   t256_block<REMAP>(splits, tiles_per_split, V, row0, sp, vt_begin, vt_end);
@@ -679,7 +679,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void gate_up_swiglu_t256_kernel(
     const uint16_t *__restrict__ x, int64_t ldx, const uint16_t *__restrict__ w, int64_t ldw, int64_t T, int K,
     int64_t F, int splits, int tiles_per_split, uint16_t *__restrict__ y, int64_t ldy) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar LDS-DMA bases
   const int wr = wave >> 2, wc = wave & 3;
   int64_t row0, sp, vt_begin, vt_end;
   t256_block<REMAP>(splits, tiles_per_split, 2 * F, row0, sp, vt_begin, vt_end);
