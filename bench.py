@@ -674,6 +674,7 @@ def main():
                 "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(f1["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4),
                 "traffic": round(f1_traffic) if f1_traffic else None, "traffic_source": f1_src,
                 "algo_flops_per_launch": f1["avg_flops"], "avg_launch_us": round(f1["avg_us"], 2),
+                "launch_us_min_median_max": [round(f1["min_us"], 1), round(f1["median_us"], 1), round(f1["max_us"], 1)],
                 "launches": f1["launches"], "time_ms_total": round(f1["time_ms_total"], 2),
             }
         # `roofline`: the §8 kernel that takes the most time in the timed steps (the fused

@@ -67,13 +67,19 @@ class KernelTimer:
     def summary(self) -> dict:
         """{name: {launches, algo_bytes_total, time_ms_total, avg_us, gbps}} (after a sync)."""
         out: dict[str, dict] = {}
+        per: dict[str, list[float]] = {}
         for name, nb, e0, e1 in self.records:
             d = out.setdefault(name, {"launches": 0, "algo_bytes_total": 0.0, "time_ms_total": 0.0})
+            ms = e0.elapsed_time(e1)
             d["launches"] += 1
             d["algo_bytes_total"] += nb
-            d["time_ms_total"] += e0.elapsed_time(e1)
+            d["time_ms_total"] += ms
+            per.setdefault(name, []).append(ms)
         for name, d in out.items():
             d["avg_us"] = 1e3 * d["time_ms_total"] / d["launches"]
+            t = sorted(per[name])  # the spread shows a slow launch (clock / power state) next to the mean
+            d["min_us"], d["max_us"] = 1e3 * t[0], 1e3 * t[-1]
+            d["median_us"] = 1e3 * t[len(t) // 2]
             if name in self.FLOP_KERNELS:  # MFMA-bound: the recorded amount is algorithmic flops
                 d["algo_flops_total"] = d.pop("algo_bytes_total")
                 d["avg_flops"] = d["algo_flops_total"] / d["launches"]
