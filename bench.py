@@ -172,7 +172,7 @@ def parse(argv=None):
                     help="1: backbone weight gradients + fp32 accumulation on a side stream (wgrad_side_stream)")
     ap.add_argument("--fused-no-grad", type=int, default=1, choices=[0, 1],
                     help="1: the no-grad old-logp pass runs the fused lm_head + log-prob kernel (f1, fused_logprob_no_grad)")
-    ap.add_argument("--fused-mlp-no-grad", type=int, default=0, choices=[0, 1],
+    ap.add_argument("--fused-mlp-no-grad", type=int, default=1, choices=[0, 1],
                     help="1: the no-grad old-logp pass runs gate|up + SwiGLU as one kernel (fused_mlp_no_grad)")
     ap.add_argument("--f1-after-backbone", type=int, default=1, choices=[0, 1],
                     help="1: the no-grad pass runs every micro-batch's backbone, then the fused lm_head launches back "
@@ -721,8 +721,9 @@ def main():
                     + ("; the no-grad old-logp pass runs the fused lm_head + log-prob kernel (the reference's "
                        "use_fused_kernels option, off by default there; same bf16-rounded logits, tests)"
                        if args.fused_no_grad else "")
-                    + ("; the no-grad pass runs gate|up + SwiGLU as one kernel (own GEMM summation order: hidden "
-                       "states equal the unfused forward to bf16 rounding, tests)" if args.fused_mlp_no_grad else "")),
+                    + ("; the no-grad pass runs gate|up + SwiGLU as one kernel (the [T, 2F] projection never "
+                       "reaches HBM; the same bits as the merged GEMM + SwiGLU on exact-arithmetic data, tests, and "
+                       "on the bench's data, relative L2 0.0)" if args.fused_mlp_no_grad else "")),
                 "dynamic_bsz_max_token_len": args.dynamic_bsz or None,
                 "compute_max_token_len": args.compute_max_tokens or None,
                 "logprob_max_token_len": (args.logprob_max_tokens or args.dynamic_bsz) if args.dynamic_bsz else None,

@@ -258,24 +258,9 @@ __device__ __forceinline__ int t_img_off(int row, int c) { return row * TK + ((c
 // staging offsets are computed once from map(r)).
 struct IdentityRows {
   static constexpr int64_t kTileStep = 256;
+  static constexpr bool kMayClip = true;  // the last vocab tile may pass V
   __device__ __forceinline__ int64_t operator()(int64_t r) const { return r; }
 };
-
-template <typename RowMap = IdentityRows>
-__device__ __forceinline__ void t_stage(const uint16_t *__restrict__ src, int64_t row0, int64_t nrows, int64_t ld,
-                                        int k0, uint16_t *img, int wave, int lane, const RowMap &rmap = RowMap{}) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int g = wave * 4 + i;  // 32 groups of 8 rows (1 KB each)
-    const int row = g * 8 + (lane >> 3);
-    const int lc = (lane & 7) ^ ((row >> 1) & 7);
-    int64_t gr = row0 + row;
-    if (gr >= nrows) gr = nrows - 1;  // clamped rows / columns are computed and discarded
-    gr = rmap(gr);
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + gr * ld + k0 + lc * 8), img + g * 8 * TK,
-                                     16, 0, 0);
-  }
-}
 
 // the logit as the unfused path holds it: bf16(acc) (ROUND), then bf16(x / T) (SCALE: div_ in bf16)
 template <bool SCALE, bool ROUND>
@@ -351,7 +336,7 @@ __device__ __forceinline__ void t_tile_epilogue(const f32x4 (&acc)[8][4], int v0
 // vt * 256 + wr * 128 + (lane >> 4) * 4 + i * 16 + e for token row0 + wc * 64 + j * 16 + (lane & 15).
 // Staging addresses: each lane's 4 hidden rows (clamped at N) and its 4 weight-image rows' offsets
 // within a tile are fixed for the sweep and computed once; per K-step only the scalar tile / chunk
-// base moves (the last vocab tile, whose rows pass V, takes the clamped per-lane path).
+// base moves (in the last vocab tile, rows past V select row V - 1's address instead).
 template <typename Tile, typename WMap = IdentityRows>
 __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int64_t ldh,
                                            const uint16_t *__restrict__ w, int64_t ldw, int64_t N, int K, int64_t V,
@@ -374,16 +359,25 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
     woff[i] = wmap(row) * ldw + lc * 8;
     ldsoff[i] = g * 8 * TK;
   }
-  // stage K-chunk kc of vocab tile vs (weight) and of the row block (hidden) into image pair img
+  // rows past V (identity map, last vocab tile only) read row V - 1 instead: computed, then discarded
+  const uint16_t *wlast[4];
+  int rowi[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    rowi[i] = (wave * 4 + i) * 8 + (lane >> 3);
+    wlast[i] = w + (V - 1) * ldw + (((lane & 7) ^ ((rowi[i] >> 1) & 7)) * 8);
+  }
+  // stage K-chunk kc of vocab tile vs (weight) and of the row block (hidden) into image pair img;
+  // branch-free, so that it shares one scheduling region with the step's MFMAs
   auto stage = [&](int64_t vs, int kc, uint16_t *img) {
     const int k0 = kc * TK;
-    if (vs * TB + TB <= V) {
-      const uint16_t *wb = w + vs * WMap::kTileStep * ldw + k0;
+    const int64_t tb = vs * TB;
+    const uint16_t *wb = w + vs * WMap::kTileStep * ldw + k0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(wb + woff[i]), img + ldsoff[i], 16, 0, 0);
-    } else {
-      t_stage(w, vs * TB, V, ldw, k0, img, wave, lane, wmap);
+    for (int i = 0; i < 4; ++i) {
+      const uint16_t *p = wb + woff[i];
+      if constexpr (WMap::kMayClip) p = tb + rowi[i] >= V ? wlast[i] + k0 : p;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(p), img + ldsoff[i], 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -407,12 +401,18 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
     const int buf = static_cast<int>(st & 1);
     const uint16_t *la = lds + buf * 2 * T_TILE;
     const uint16_t *lb = la + T_TILE;
-    if (st + 1 < nsteps) {
-      const bool last = kt + 1 == nk;
-      stage(last ? vt + 1 : vt, last ? 0 : kt + 1, lds + (buf ^ 1) * 2 * T_TILE);
-    }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
+      // the next step's images, issued between the two K-halves: hipcc then spreads the address, M0
+      // and DMA issue over the second half's MFMAs instead of running them ahead of the first (30.1 vs
+      // 31.5 ms issued before the step's MFMAs, f1_stage_at_ab.jsonl); the last step re-stages a valid
+      // tile into the free buffer, unread
+      if (q == 1) {
+        const bool last = kt + 1 == nk;
+        int64_t vs = last ? vt + 1 : vt;
+        if (vs >= vt_end) vs = vt_end - 1;
+        stage(vs, last ? 0 : kt + 1, lds + (buf ^ 1) * 2 * T_TILE);
+      }
       const int c = q * 4 + (lane >> 4);
       bf16x8 fa[8], fb[4];
 #pragma unroll
@@ -665,6 +665,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
 // swiglu_fwd (model_ops.hip), so on exact-arithmetic data the output equals GEMM + swiglu bitwise.
 struct GateUpRows {
   static constexpr int64_t kTileStep = 128;
+  static constexpr bool kMayClip = false;  // F % 128 == 0: every tile is whole
   int64_t F;
   __device__ __forceinline__ int64_t operator()(int64_t r) const {
     const int64_t t = r >> 8;  // 256 image rows per 128 features
