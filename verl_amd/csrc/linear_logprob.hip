@@ -248,6 +248,7 @@ __global__ __launch_bounds__(256, 2) void linear_logprob_tiles_kernel(
 // row blocks an XCD works on at a time keep their hidden panels in its L2 while the W tiles stream
 // (round-3 dev kernel tools/f1core/f1t.hip, git show 690aed1:tools/f1core/f1t.hip; at 131,072 x 896 x 151,936: 30.1 ms core-only vs 32.3 without the remap).
 constexpr int TB = 256, TK = 64, T_THREADS = 512;
+
 constexpr int T_TILE = TB * TK;  // bf16 elements of one operand's K-step image
 
 __device__ __forceinline__ int t_img_off(int row, int c) { return row * TK + ((c ^ ((row >> 1) & 7)) << 3); }
@@ -258,8 +259,11 @@ __device__ __forceinline__ int t_img_off(int row, int c) { return row * TK + ((c
 // staging offsets are computed once from map(r)).
 struct IdentityRows {
   static constexpr int64_t kTileStep = 256;
-  static constexpr bool kMayClip = true;  // the last vocab tile may pass V
   __device__ __forceinline__ int64_t operator()(int64_t r) const { return r; }
+  // rows of tile vs's weight window that exist (the last vocab tile may pass V)
+  __device__ __forceinline__ int64_t window_rows(int64_t vs, int64_t V) const {
+    return V - vs * 256 < 256 ? V - vs * 256 : 256;
+  }
 };
 
 // the logit as the unfused path holds it: bf16(acc) (ROUND), then bf16(x / T) (SCALE: div_ in bf16)
@@ -274,17 +278,11 @@ __device__ __forceinline__ float logit_of(float a, float temperature) {
 // T > 0) is monotonic, so the tile max of the logits is the map of the raw accumulators' max: one
 // max pass over acc, then ONE pass of map -> exp2 -> sums. TAIL: the last vocab tile, whose rows
 // past V are -inf (weight 0, kept out of the x-weighted sum: 0 * -inf is NaN).
-template <bool SCALE, bool ROUND, bool TAIL>
-__device__ __forceinline__ void t_tile_epilogue(const f32x4 (&acc)[8][4], int v0, const int (&lab)[4], float (&m)[4],
-                                                float (&s)[4], float (&t)[4], float (&ll)[4], float temperature) {
+template <bool SCALE, bool ROUND>
+__device__ __forceinline__ void t_tile_labels(const f32x4 (&acc)[8][4], int v0, const int (&lab)[4], float (&ll)[4],
+                                              float temperature) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float rm = acc[0][j][0];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) rm = fmaxf(rm, acc[i][j][e]);
-    const float lm = logit_of<SCALE, ROUND>(rm, temperature);
     const int d = lab[j] - v0;  // the label sits at (i, e) = (d >> 4, d & 3) when d in [0, 128), d & 12 == 0
     if (d >= 0 && d < 128 && (d & 12) == 0) {
       const int uu = (d >> 4) * 4 + (d & 3);
@@ -295,40 +293,103 @@ __device__ __forceinline__ void t_tile_epilogue(const f32x4 (&acc)[8][4], int v0
         for (int e = 0; e < 4; ++e) v = (i * 4 + e) == uu ? acc[i][j][e] : v;
       ll[j] = logit_of<SCALE, ROUND>(v, temperature);
     }
-    const float nm = fmaxf(m[j], lm);
-    const float nb = base_of(nm);
-    const float alpha = __builtin_amdgcn_exp2f(base_of(m[j]) - nb);
-    // pairs of logits in packed fp32 (v_pk_fma_f32 / v_pk_add_f32): ~3 VALU slots + 1 exp per logit
-    // instead of ~5 + 1, the halves of ss / tt summed once per tile (33.1-33.2 vs 33.6-33.8 ms at
-    // 131,072 x 896 x 151,936, tools/f1_ab.py; profiles/r03/f1_packed_epilogue_ab.log)
-    const va_f32x2 l2e = {kLog2eF, kLog2eF}, nnb = {-nb, -nb};
-    va_f32x2 ss = {0.f, 0.f}, tt = {0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; e += 2) {
-        va_f32x2 x;
-        if constexpr (ROUND && !SCALE) {  // both roundings in one v_cvt_pk_bf16_f32
-          const uint32_t p = pack2_bf16(acc[i][j][e], acc[i][j][e + 1]);
-          x = va_f32x2{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
-        } else {
-          x = va_f32x2{logit_of<SCALE, ROUND>(acc[i][j][e], temperature),
-                       logit_of<SCALE, ROUND>(acc[i][j][e + 1], temperature)};
-        }
-        const va_f32x2 arg = __builtin_elementwise_fma(x, l2e, nnb);
-        const va_f32x2 ex = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
-        ss = ss + ex;
-        if constexpr (TAIL) {
-          x.x = x.x == -INFINITY ? 0.f : x.x;
-          x.y = x.y == -INFINITY ? 0.f : x.y;
-        }
-        tt = __builtin_elementwise_fma(ex, x, tt);
-      }
-    s[j] = fmaf(s[j], alpha, ss.x + ss.y);
-    t[j] = fmaf(t[j], alpha, tt.x + tt.y);
-    m[j] = nm;
   }
 }
+
+// Fold token column j of a finished tile into the lane's state; branch-free (it shares a scheduling
+// region with the next tile's MFMAs). TAIL: vocab rows v0 + 16 i + e >= V are -inf. In three parts
+// (the deferred sweep interleaves them with MFMA halves): the max pass (col_begin), the exp / sum
+// pass over blocks i in [I0, I1) (col_blocks), and the merge into the running state (col_end).
+struct ColState {
+  float nm, nb, alpha;
+  va_f32x2 ss, tt;
+};
+
+template <bool SCALE, bool ROUND, bool TAIL>
+__device__ __forceinline__ float col_val(const f32x4 (&acc)[8][4], int i, int j, int e, int v0, int64_t V) {
+  return (TAIL && v0 + i * 16 + e >= V) ? -INFINITY : acc[i][j][e];
+}
+
+template <bool SCALE, bool ROUND, bool TAIL>
+__device__ __forceinline__ ColState col_begin(const f32x4 (&acc)[8][4], int j, int v0, int64_t V, float m,
+                                              float temperature) {
+  float rm = col_val<SCALE, ROUND, TAIL>(acc, 0, j, 0, v0, V);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rm = fmaxf(rm, col_val<SCALE, ROUND, TAIL>(acc, i, j, e, v0, V));
+  ColState c;
+  c.nm = fmaxf(m, logit_of<SCALE, ROUND>(rm, temperature));
+  c.nb = base_of(c.nm);
+  c.alpha = __builtin_amdgcn_exp2f(base_of(m) - c.nb);
+  c.ss = va_f32x2{0.f, 0.f}, c.tt = va_f32x2{0.f, 0.f};
+  return c;
+}
+
+// pairs of logits in packed fp32 (v_pk_fma_f32 / v_pk_add_f32): ~3 VALU slots + 1 exp per logit
+// instead of ~5 + 1, the halves of ss / tt summed once per tile (33.1-33.2 vs 33.6-33.8 ms at
+// 131,072 x 896 x 151,936, tools/f1_ab.py; profiles/r03/f1_packed_epilogue_ab.log)
+template <bool SCALE, bool ROUND, bool TAIL, int I0, int I1>
+__device__ __forceinline__ void col_blocks(const f32x4 (&acc)[8][4], int j, int v0, int64_t V, float temperature,
+                                           ColState &c) {
+  const va_f32x2 l2e = {kLog2eF, kLog2eF}, nnb = {-c.nb, -c.nb};
+#pragma unroll
+  for (int i = I0; i < I1; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; e += 2) {
+      const float a0 = col_val<SCALE, ROUND, TAIL>(acc, i, j, e, v0, V);
+      const float a1 = col_val<SCALE, ROUND, TAIL>(acc, i, j, e + 1, v0, V);
+      va_f32x2 x;
+      if constexpr (ROUND && !SCALE) {  // both roundings in one v_cvt_pk_bf16_f32
+        const uint32_t p = pack2_bf16(a0, a1);
+        x = va_f32x2{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+      } else {
+        x = va_f32x2{logit_of<SCALE, ROUND>(a0, temperature), logit_of<SCALE, ROUND>(a1, temperature)};
+      }
+      const va_f32x2 arg = __builtin_elementwise_fma(x, l2e, nnb);
+      const va_f32x2 ex = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+      c.ss = c.ss + ex;
+      if constexpr (TAIL) {
+        x.x = x.x == -INFINITY ? 0.f : x.x;
+        x.y = x.y == -INFINITY ? 0.f : x.y;
+      }
+      c.tt = __builtin_elementwise_fma(ex, x, c.tt);
+    }
+}
+
+__device__ __forceinline__ void col_end(const ColState &c, float &m, float &s, float &t) {
+  s = fmaf(s, c.alpha, c.ss.x + c.ss.y);
+  t = fmaf(t, c.alpha, c.tt.x + c.tt.y);
+  m = c.nm;
+}
+
+template <bool SCALE, bool ROUND, bool TAIL>
+__device__ __forceinline__ void t_col_epilogue(const f32x4 (&acc)[8][4], int j, int v0, int64_t V, float (&m)[4],
+                                               float (&s)[4], float (&t)[4], float temperature) {
+  ColState c = col_begin<SCALE, ROUND, TAIL>(acc, j, v0, V, m[j], temperature);
+  col_blocks<SCALE, ROUND, TAIL, 0, 8>(acc, j, v0, V, temperature, c);
+  col_end(c, m[j], s[j], t[j]);
+}
+
+// The forward's tile epilogue as the deferred sweep calls it: labels (rare, branchy) first, then one
+// token column at a time, each ahead of that column's first MFMAs of the next tile.
+template <bool SCALE, bool ROUND>
+struct FwdEpilogue {
+  int lab[4];
+  float m[4], s[4], t[4], ll[4];  // ll: the label's logit, -inf until this lane meets it
+  float temperature;
+  int64_t V;
+  int vbase;  // wr * 128 + (lane >> 4) * 4: this lane's first vocab row within a tile
+  __device__ __forceinline__ int v0(int64_t vt) const { return static_cast<int>(vt * TB) + vbase; }  // V < 2^31
+  __device__ __forceinline__ bool tail(int64_t vt) const { return vt * TB + TB > V; }
+  __device__ __forceinline__ void pre(const f32x4 (&acc)[8][4], int64_t vt) {
+    t_tile_labels<SCALE, ROUND>(acc, v0(vt), lab, ll, temperature);
+  }
+  template <bool TAIL>
+  __device__ __forceinline__ void col(const f32x4 (&acc)[8][4], int64_t vt, int j) {
+    t_col_epilogue<SCALE, ROUND, TAIL>(acc, j, v0(vt), V, m, s, t, temperature);
+  }
+};
 
 // The persistent transposed sweep shared by the forward and the backward kernels: for each vocab tile
 // of [vt_begin, vt_end) it accumulates S^T = W_tile . H_tile^T (256 vocab x 256 tokens) over K in acc,
@@ -345,44 +406,36 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
   const int wr = wave >> 2, wc = wave & 3;
   const int nk = K / TK;
   const int64_t nsteps = vt_begin < vt_end ? (vt_end - vt_begin) * nk : 0;
-  const uint16_t *hsrc[4];
-  int64_t woff[4];
+  // LDS-DMA through buffer resources: per lane a fixed 32-bit byte offset per staged row, the K-chunk
+  // as the scalar offset, and the resource's record count as the bound — rows past N (hidden) or past
+  // V (weight, last vocab tile) read 0 (computed, then discarded) with no per-lane clamping
+  uint32_t hoff[4], woff[4];
   int ldsoff[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int g = wave * 4 + i;  // 32 groups of 8 rows (1 KB each)
     const int row = g * 8 + (lane >> 3);
     const int lc = (lane & 7) ^ ((row >> 1) & 7);
-    int64_t hr = row0 + row;
-    if (hr >= N) hr = N - 1;  // clamped rows are computed and discarded
-    hsrc[i] = hid + hr * ldh + lc * 8;
-    woff[i] = wmap(row) * ldw + lc * 8;
+    hoff[i] = static_cast<uint32_t>((row * ldh + lc * 8) * 2);
+    woff[i] = static_cast<uint32_t>((wmap(row) * ldw + lc * 8) * 2);
     ldsoff[i] = g * 8 * TK;
   }
-  // rows past V (identity map, last vocab tile only) read row V - 1 instead: computed, then discarded
-  const uint16_t *wlast[4];
-  int rowi[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    rowi[i] = (wave * 4 + i) * 8 + (lane >> 3);
-    wlast[i] = w + (V - 1) * ldw + (((lane & 7) ^ ((rowi[i] >> 1) & 7)) * 8);
-  }
+  const int64_t hrows = N - row0 < TB ? N - row0 : TB;
+  const __amdgpu_buffer_rsrc_t hres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t *>(hid + row0 * ldh), 0, static_cast<int>(hrows * ldh * 2), 0x00020000);
   // stage K-chunk kc of vocab tile vs (weight) and of the row block (hidden) into image pair img;
   // branch-free, so that it shares one scheduling region with the step's MFMAs
   auto stage = [&](int64_t vs, int kc, uint16_t *img) {
-    const int k0 = kc * TK;
-    const int64_t tb = vs * TB;
-    const uint16_t *wb = w + vs * WMap::kTileStep * ldw + k0;
+    const int kb = kc * TK * 2;
+    const int64_t wbytes = wmap.window_rows(vs, V) * ldw * 2;
+    const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t *>(w + vs * WMap::kTileStep * ldw), 0,
+        static_cast<int>(wbytes < 0x7fffffff ? wbytes : 0x7fffffff), 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint16_t *p = wb + woff[i];
-      if constexpr (WMap::kMayClip) p = tb + rowi[i] >= V ? wlast[i] + k0 : p;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(p), img + ldsoff[i], 16, 0, 0);
-    }
+    for (int i = 0; i < 4; ++i) __builtin_amdgcn_raw_ptr_buffer_load_lds(wres, img + ldsoff[i], 16, woff[i], kb, 0, 0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(hsrc[i] + k0), img + T_TILE + ldsoff[i], 16, 0,
-                                       0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(hres, img + T_TILE + ldsoff[i], 16, hoff[i], kb, 0, 0);
   };
   f32x4 acc[8][4];
 #pragma unroll
@@ -414,13 +467,17 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
         stage(vs, last ? 0 : kt + 1, lds + (buf ^ 1) * 2 * T_TILE);
       }
       const int c = q * 4 + (lane >> 4);
+      auto frag_a = [&](int i) {
+        return *reinterpret_cast<const bf16x8 *>(la + t_img_off(wr * 128 + i * 16 + (lane & 15), c));
+      };
+      auto frag_b = [&](int j) {
+        return *reinterpret_cast<const bf16x8 *>(lb + t_img_off(wc * 64 + j * 16 + (lane & 15), c));
+      };
       bf16x8 fa[8], fb[4];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        fa[i] = *reinterpret_cast<const bf16x8 *>(la + t_img_off(wr * 128 + i * 16 + (lane & 15), c));
+      for (int i = 0; i < 8; ++i) fa[i] = frag_a(i);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        fb[j] = *reinterpret_cast<const bf16x8 *>(lb + t_img_off(wc * 64 + j * 16 + (lane & 15), c));
+      for (int j = 0; j < 4; ++j) fb[j] = frag_b(j);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -474,33 +531,30 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_t256_kernel(
   t256_block<REMAP>(splits, tiles_per_split, V, row0, sp, vt_begin, vt_end);
 
   // this lane's 4 tokens (columns of the transposed tile), their labels and online states
-  int lab[4];
-  float m[4], s[4], t[4], ll[4];  // ll: the label's logit, -inf until this lane meets it
+  FwdEpilogue<SCALE, ROUND> epi;
+  epi.temperature = temperature, epi.V = V, epi.vbase = wr * 128 + (lane >> 4) * 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t r = row0 + wc * 64 + j * 16 + (lane & 15);
     const int64_t lb = r < N ? labels[r] : -1;
-    lab[j] = (lb >= 0 && lb < V) ? static_cast<int>(lb) : -1;
-    m[j] = -INFINITY, s[j] = 0.f, t[j] = 0.f, ll[j] = -INFINITY;
+    epi.lab[j] = (lb >= 0 && lb < V) ? static_cast<int>(lb) : -1;
+    epi.m[j] = -INFINITY, epi.s[j] = 0.f, epi.t[j] = 0.f, epi.ll[j] = -INFINITY;
   }
 
+  // acc[i][j][e] = logit of vocab v0 + i * 16 + e for token j of this lane; only the last vocab
+  // tile has rows past V (TAIL)
   t256_sweep(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
-    // acc[i][j][e] = logit of vocab v0 + i * 16 + e for token j of this lane
-    const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;  // V < 2^31
-    if (vt * TB + TB > V) {  // uniform: only the last vocab tile has rows past V
+    epi.pre(acc, vt);
+    if (epi.tail(vt)) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (v0 + i * 16 + e >= V)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j][e] = -INFINITY;
-      t_tile_epilogue<SCALE, ROUND, true>(acc, v0, lab, m, s, t, ll, temperature);
+      for (int j = 0; j < 4; ++j) epi.template col<true>(acc, vt, j);
     } else {
-      t_tile_epilogue<SCALE, ROUND, false>(acc, v0, lab, m, s, t, ll, temperature);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) epi.template col<false>(acc, vt, j);
     }
   });
 
+  float(&m)[4] = epi.m, (&s)[4] = epi.s, (&t)[4] = epi.t, (&ll)[4] = epi.ll;
   // merge the 4 lane groups (lanes l, l ^ 16, l ^ 32, l ^ 48 hold the same tokens), then the two
   // vocab wave-rows through LDS (free now: every DMA was waited for), in fixed order
 #pragma unroll
@@ -665,8 +719,9 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
 // swiglu_fwd (model_ops.hip), so on exact-arithmetic data the output equals GEMM + swiglu bitwise.
 struct GateUpRows {
   static constexpr int64_t kTileStep = 128;
-  static constexpr bool kMayClip = false;  // F % 128 == 0: every tile is whole
   int64_t F;
+  // tile vs's window reaches its up rows at F + vs * 128 + [0, 128) (F % 128 == 0: every tile whole)
+  __device__ __forceinline__ int64_t window_rows(int64_t, int64_t) const { return F + 128; }
   __device__ __forceinline__ int64_t operator()(int64_t r) const {
     const int64_t t = r >> 8;  // 256 image rows per 128 features
     const int q = static_cast<int>(r & 127), blk = q >> 4;
@@ -746,7 +801,8 @@ extern "C" int va_linear_logprob_fwd(const void *hidden, int64_t ldh, const void
   VA_CHECK_ARG(dtype == VA_BF16, "linear_logprob: only bf16 hidden / weight are implemented");
   VA_CHECK_ARG(N >= 0 && H > 0 && V > 0 && H % BK == 0 && H <= (1 << 20),
                "linear_logprob: need H %% 64 == 0 (H=%lld)", static_cast<long long>(H));
-  VA_CHECK_ARG(ldh >= H && ldw >= H && ldh % 8 == 0 && ldw % 8 == 0, "linear_logprob: strides must be >= H, %% 8");
+  VA_CHECK_ARG(ldh >= H && ldw >= H && ldh % 8 == 0 && ldw % 8 == 0 && ldh < (1 << 22) && ldw < (1 << 22),
+               "linear_logprob: strides must be >= H, %% 8, < 2^22 (32-bit buffer offsets of a 256-row tile)");
   VA_CHECK_ARG(splits >= 1 && splits <= 64, "linear_logprob: splits in [1, 64]");
   VA_CHECK_ARG(temperature > 0.f, "linear_logprob: temperature must be > 0");
   if (N == 0) return VA_OK;
@@ -831,8 +887,9 @@ extern "C" int va_linear_logprob_bwd(const void *hidden, int64_t ldh, const void
   VA_CHECK_ARG(N >= 0 && H > 0 && H % TK == 0 && H <= (1 << 20) && Vr % 4 == 0 && V < (int64_t{1} << 31),
                "linear_logprob_bwd: need H %% 64 == 0 and V %% 4 == 0 over the range (H=%lld, V=%lld)",
                static_cast<long long>(H), static_cast<long long>(Vr));
-  VA_CHECK_ARG(ldh >= H && ldw >= H && ldh % 8 == 0 && ldw % 8 == 0 && ldd >= Vr && ldd % 4 == 0,
-               "linear_logprob_bwd: strides must be >= H (ldd >= the range), %% 8 (ldd %% 4)");
+  VA_CHECK_ARG(ldh >= H && ldw >= H && ldh % 8 == 0 && ldw % 8 == 0 && ldh < (1 << 22) && ldw < (1 << 22) &&
+                   ldd >= Vr && ldd % 4 == 0,
+               "linear_logprob_bwd: strides must be >= H (ldd >= the range), %% 8 (ldd %% 4), < 2^22");
   VA_CHECK_ARG(splits >= 1 && splits <= 64, "linear_logprob_bwd: splits in [1, 64]");
   VA_CHECK_ARG(temperature > 0.f, "linear_logprob_bwd: temperature must be > 0");
   if (N == 0) return VA_OK;
@@ -872,8 +929,10 @@ extern "C" int va_gate_up_swiglu(const void *x, int64_t ldx, const void *w_gate_
   VA_CHECK_ARG(T >= 0 && H > 0 && H % TK == 0 && H <= (1 << 20) && F > 0 && F % 128 == 0 && F < (int64_t{1} << 30),
                "gate_up_swiglu: need H %% 64 == 0 and F %% 128 == 0 (H=%lld, F=%lld)", static_cast<long long>(H),
                static_cast<long long>(F));
-  VA_CHECK_ARG(ldx >= H && ldw >= H && ldx % 8 == 0 && ldw % 8 == 0 && ldy >= F && ldy % 4 == 0,
-               "gate_up_swiglu: strides must be >= H (ldy >= F), %% 8 (ldy %% 4)");
+  VA_CHECK_ARG(ldx >= H && ldw >= H && ldx % 8 == 0 && ldw % 8 == 0 && ldy >= F && ldy % 4 == 0 && ldx < (1 << 22) &&
+                   (F + 128) * ldw * 2 < (int64_t{1} << 31),
+               "gate_up_swiglu: strides must be >= H (ldy >= F), %% 8 (ldy %% 4); (F + 128) ldw 2 < 2^31 (32-bit "
+               "buffer offsets)");
   VA_CHECK_ARG(splits >= 1 && splits <= 64, "gate_up_swiglu: splits in [1, 64]");
   if (T == 0) return VA_OK;
   VA_CHECK_ARG(x && w_gate_up && y, "null pointer argument");
