@@ -753,7 +753,9 @@ def gate_up_swiglu_supported(x, w_gate_up) -> bool:
             and w_gate_up.dim() == 2 and x.shape[1] == w_gate_up.shape[1] and x.shape[1] % 64 == 0
             and w_gate_up.shape[0] % 256 == 0 and x.stride(-1) == 1 and w_gate_up.stride(-1) == 1
             and x.stride(0) % 8 == 0 and w_gate_up.stride(0) % 8 == 0
-            and x.data_ptr() % 16 == 0 and w_gate_up.data_ptr() % 16 == 0)
+            and x.data_ptr() % 16 == 0 and w_gate_up.data_ptr() % 16 == 0
+            # the sweep's 32-bit buffer offsets (va_gate_up_swiglu's checks)
+            and x.stride(0) < (1 << 22) and (w_gate_up.shape[0] // 2 + 128) * w_gate_up.stride(0) * 2 < (1 << 31))
 
 
 def gate_up_swiglu(x, w_gate_up, splits: int | None = None):
