@@ -174,6 +174,9 @@ def parse(argv=None):
                     help="1: the no-grad old-logp pass runs the fused lm_head + log-prob kernel (f1, fused_logprob_no_grad)")
     ap.add_argument("--fused-mlp-no-grad", type=int, default=1, choices=[0, 1],
                     help="1: the no-grad old-logp pass runs gate|up + SwiGLU as one kernel (fused_mlp_no_grad)")
+    ap.add_argument("--fused-mlp-train", type=int, default=0, choices=[0, 1],
+                    help="1: update passes run gate|up + SwiGLU as one kernel that also writes the projection for "
+                         "the backward (fused_mlp_train)")
     ap.add_argument("--f1-after-backbone", type=int, default=1, choices=[0, 1],
                     help="1: the no-grad pass runs every micro-batch's backbone, then the fused lm_head launches back "
                          "to back (fused_lm_head_after_backbone); 0: backbone + lm_head per micro-batch")
@@ -510,6 +513,7 @@ def main():
             logprob_inplace_backward={0: False, 1: True, 2: "auto"}[args.logprob_inplace_bwd],
             fused_logprob_no_grad=bool(args.fused_no_grad),
             fused_mlp_no_grad=bool(args.fused_mlp_no_grad),
+            fused_mlp_train=bool(args.fused_mlp_train),
             fused_lm_head_after_backbone=bool(args.f1_after_backbone),
             fused_lm_head_concat=bool(args.f1_concat),
             use_fused_kernels=bool(args.fused_kernels),
@@ -733,6 +737,7 @@ def main():
                 "logprob_bwd_inplace_fallbacks": lp_fallbacks,
                 "fused_logprob_no_grad": bool(args.fused_no_grad),
                 "fused_mlp_no_grad": bool(args.fused_mlp_no_grad),
+                "fused_mlp_train": bool(args.fused_mlp_train),
                 "fused_lm_head_after_backbone": bool(args.f1_after_backbone),
                 "fused_lm_head_concat": bool(args.f1_concat),
                 "use_fused_kernels": bool(args.fused_kernels),

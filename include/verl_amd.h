@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define VA_ABI_VERSION 7
+#define VA_ABI_VERSION 8
 
 /* error codes */
 #define VA_OK 0
@@ -386,6 +386,13 @@ int va_swiglu_bwd(const void *dy, const void *gu, int64_t ldgu, int64_t uoff, in
  * dp_actor.py:331-333 (compute_log_prob's torch.no_grad forward). Not a §8 row. */
 int va_gate_up_swiglu(const void *x, int64_t ldx, const void *w_gate_up, int64_t ldw, int dtype, int64_t T,
                       int64_t H, int64_t F, int splits, void *y, int64_t ldy, void *stream);
+/* gate_up_swiglu_save (ABI 8): as va_gate_up_swiglu, and also the projection's g | u (bf16, exactly
+ * the merged GEMM's output) into gu [T, 2F] (row stride ldgu >= 2F, % 4, 8-byte aligned): the
+ * training forward's gate|up GEMM + swiglu_fwd in one kernel, gu kept for va_swiglu_bwd (HF
+ * Qwen2MLP under autograd, dp_actor.py:331-333 in update_policy's forward). Not a §8 row. */
+int va_gate_up_swiglu_save(const void *x, int64_t ldx, const void *w_gate_up, int64_t ldw, int dtype, int64_t T,
+                           int64_t H, int64_t F, int splits, void *y, int64_t ldy, void *gu, int64_t ldgu,
+                           void *stream);
 int va_rope_qkv_fwd(const void *qkv, int64_t ld, const void *cos, const void *sin, int dtype, int64_t T,
                     int64_t Hq, int64_t Hk, int64_t D, void *q, void *k, void *v, void *stream);
 int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *cos, const void *sin, int dtype,

@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_abi_version_and_workspace_queries(lib):
-    assert lib.va_abi_version() == 7
+    assert lib.va_abi_version() == 8
     assert lib.va_ppo_loss_workspace_bytes(10) == 8 * (2 * 10 * 8 + 8)
     assert lib.va_agg_workspace_bytes(10) == 8 * (2 * 10 * 8 + 8)
     assert lib.va_gae_workspace_bytes(7) == 8 * (6 * 7 + 8)
@@ -135,6 +135,15 @@ def test_tuning_keys_without_device(lib):
         assert lib.va_set_tuning(key, val) == 0, key
     assert lib.va_set_tuning(L.VA_TUNE_FLASH_DQ_KB, 96) == -1
     assert lib.va_set_tuning(99, 1) == -1
+
+
+def test_gate_up_swiglu_save_validation_without_device(lib):
+    # ABI 8: the projection buffer is required and must hold 2F columns
+    rc = lib.va_gate_up_swiglu_save(1, 64, 1, 64, L.VA_BF16, 4, 64, 128, 1, 1, 128, None, 256, None)
+    assert rc == -1 and b"null projection" in lib.va_last_error()
+    rc = lib.va_gate_up_swiglu_save(16, 64, 16, 64, L.VA_BF16, 4, 64, 128, 1, 16, 128, 16, 200, None)
+    assert rc == -1 and b"2F" in lib.va_last_error()
+    assert lib.va_gate_up_swiglu_save(None, 64, None, 64, L.VA_BF16, 0, 64, 128, 1, None, 128, None, 256, None) == 0
 
 
 def test_transpose_validation_without_device(lib):

@@ -356,6 +356,48 @@ def test_gate_up_swiglu_bitwise_on_exact_data(T, H, F_, ldx, splits):
     assert torch.equal(got, want)
 
 
+@pytest.mark.parametrize("T,H,F_,ldx", [(1000, 896, 4864, None), (517, 256, 512, 320), (3, 128, 256, None)])
+def test_gate_up_swiglu_save_bitwise_on_exact_data(T, H, F_, ldx):
+    """va_gate_up_swiglu_save (ABI 8): y as va_gate_up_swiglu and the saved projection equal to the
+    merged GEMM's bf16 output, bit for bit, on exact data (ragged tails, strided x)."""
+    from verl_amd import kernels as K
+
+    x, w = _exact_operands(T, H, F_, ldx, seed=3 * T + F_)
+    with torch.no_grad():
+        gu_want = x @ w.t()
+        y_want = K.swiglu_merged(gu_want)
+        y, gu = K._gate_up_swiglu_raw(x, w, None, save=True)
+    assert torch.equal(gu, gu_want)
+    assert torch.equal(y, y_want)
+
+
+@pytest.mark.parametrize("T,H,F_", [(1000, 896, 4864), (300, 128, 256)])
+def test_fused_mlp_train_forward_backward_bitwise_on_exact_data(T, H, F_):
+    """gate_up_swiglu_train (fused_mlp_train): the activation and the gradients of x and of the gate /
+    up weights equal merged_linear + swiglu_merged's bit for bit on exact data (the backward runs the
+    same swiglu_bwd / dgrad / weight-gradient kernels on the same saved projection)."""
+    from verl_amd import kernels as K
+
+    x0, w0 = _exact_operands(T, H, F_, None, seed=T + 7)
+    g = torch.Generator(device=DEV).manual_seed(T)
+    dy = (torch.randint(-2, 3, (T, F_), device=DEV, generator=g).float() / 4).to(torch.bfloat16)
+    res = {}
+    for fused in (False, True):
+        x = x0.clone().requires_grad_(True)
+        w_all = w0.clone()
+        gate = torch.nn.Parameter(w_all[:F_])
+        up = torch.nn.Parameter(w_all[F_:])
+        gate.data, up.data = w_all[:F_], w_all[F_:]  # views into the merged buffer, as qwen2_fused._merged
+        if fused:
+            y = K.gate_up_swiglu_train(x, w_all, [gate, up])
+        else:
+            y = K.swiglu_merged(K.merged_linear(x, w_all, None, [gate, up]))
+        y.backward(dy)
+        res[fused] = (y.detach(), x.grad, gate.grad, up.grad)
+    for a, b, what in zip(res[True], res[False], ("y", "dx", "d_gate", "d_up")):
+        assert torch.equal(a, b), what
+
+
 def test_gate_up_swiglu_random_vs_fp32():
     """Random operands: within bf16 rounding of silu(g) * u from an fp32 GEMM (tolerance: 2 bf16 ulp on
     all but 1e-3 of the elements, i.e. the product's own rounding points)."""

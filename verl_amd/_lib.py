@@ -41,7 +41,7 @@ VA_TUNE_WGRAD_REMAINDER, VA_TUNE_FLASH_DMA, VA_TUNE_WGRAD_MFMA = 18, 19, 20
 FLASH_TUNING_DEFAULTS = {VA_TUNE_FLASH_DMA: 7, VA_TUNE_FLASH_DQ_KB: 64, VA_TUNE_FLASH_DKDV_QT: 64,
                          VA_TUNE_FLASH_FWD_KB: 64, VA_TUNE_FLASH_GROUPED_DKDV: -1}
 
-ABI_VERSION = 7  # include/verl_amd.h VA_ABI_VERSION
+ABI_VERSION = 8  # include/verl_amd.h VA_ABI_VERSION
 
 _P = c_void_p
 _SIGNATURES: dict[str, tuple] = {
@@ -96,6 +96,8 @@ _SIGNATURES: dict[str, tuple] = {
     "va_swiglu_fwd": (c_int, [_P, c_int64, c_int64, c_int, c_int64, c_int64, _P, _P]),
     "va_swiglu_bwd": (c_int, [_P, _P, c_int64, c_int64, c_int, c_int64, c_int64, _P, c_int64, c_int64, _P]),
     "va_gate_up_swiglu": (c_int, [_P, c_int64, _P, c_int64, c_int, c_int64, c_int64, c_int64, c_int, _P, c_int64, _P]),
+    "va_gate_up_swiglu_save": (c_int, [_P, c_int64, _P, c_int64, c_int, c_int64, c_int64, c_int64, c_int, _P, c_int64,
+                                       _P, c_int64, _P]),
     "va_rope_qkv_fwd": (c_int, [_P, c_int64, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, _P, _P, _P]),
     "va_value_loss_fwd": (c_int, [_P, _P, _P, _P, c_int, c_int64, c_int64, c_float, c_int, c_int64, _P, c_int64, _P,
                                   _P, _P]),

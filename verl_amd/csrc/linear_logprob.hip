@@ -730,20 +730,25 @@ struct GateUpRows {
   }
 };
 
-template <bool REMAP>
+// SAVE: also store the projection's g / u (bf16, as the merged GEMM writes them) into gu [T, 2F] for
+// the training forward, whose SwiGLU backward needs them: the GEMM + swiglu_fwd pair without the
+// swiglu_fwd's re-read of the projection.
+template <bool REMAP, bool SAVE>
 __global__ __launch_bounds__(T_THREADS, 1) void gate_up_swiglu_t256_kernel(
     const uint16_t *__restrict__ x, int64_t ldx, const uint16_t *__restrict__ w, int64_t ldw, int64_t T, int K,
-    int64_t F, int splits, int tiles_per_split, uint16_t *__restrict__ y, int64_t ldy) {
+    int64_t F, int splits, int tiles_per_split, uint16_t *__restrict__ y, int64_t ldy, uint16_t *__restrict__ gu,
+    int64_t ldgu) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar LDS-DMA bases
   const int wr = wave >> 2, wc = wave & 3;
   int64_t row0, sp, vt_begin, vt_end;
   t256_block<REMAP>(splits, tiles_per_split, 2 * F, row0, sp, vt_begin, vt_end);
-  uint16_t *yrow[4];
+  uint16_t *yrow[4], *grow[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t r = row0 + wc * 64 + j * 16 + (lane & 15);
     yrow[j] = r < T ? y + r * ldy : nullptr;
+    if constexpr (SAVE) grow[j] = r < T ? gu + r * ldgu : nullptr;
   }
   t256_sweep(
       x, ldx, w, ldw, T, K, 2 * F, row0, vt_begin, vt_end, lds, wave, lane,
@@ -754,16 +759,23 @@ __global__ __launch_bounds__(T_THREADS, 1) void gate_up_swiglu_t256_kernel(
           if (yrow[j] == nullptr) continue;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float o[4];
+            float o[4], gg[4], uu[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float g = round_bf16(acc[i][j][e]), u = round_bf16(acc[i + 4][j][e]);
-              o[e] = round_bf16(va_silu(g)) * u;
+              gg[e] = round_bf16(acc[i][j][e]), uu[e] = round_bf16(acc[i + 4][j][e]);
+              o[e] = round_bf16(va_silu(gg[e])) * uu[e];
             }
             uint2 q;
             q.x = pack2_bf16(o[0], o[1]);
             q.y = pack2_bf16(o[2], o[3]);
             *reinterpret_cast<uint2 *>(yrow[j] + f0 + i * 16) = q;
+            if constexpr (SAVE) {
+              uint2 qg, qu;
+              qg.x = pack2_bf16(gg[0], gg[1]), qg.y = pack2_bf16(gg[2], gg[3]);
+              qu.x = pack2_bf16(uu[0], uu[1]), qu.y = pack2_bf16(uu[2], uu[3]);
+              *reinterpret_cast<uint2 *>(grow[j] + f0 + i * 16) = qg;
+              *reinterpret_cast<uint2 *>(grow[j] + F + f0 + i * 16) = qu;
+            }
           }
         }
       },
@@ -923,8 +935,9 @@ extern "C" int va_linear_logprob_bwd(const void *hidden, int64_t ldh, const void
   return check_launch("linear_logprob_bwd");
 }
 
-extern "C" int va_gate_up_swiglu(const void *x, int64_t ldx, const void *w_gate_up, int64_t ldw, int dtype, int64_t T,
-                                 int64_t H, int64_t F, int splits, void *y, int64_t ldy, void *stream) {
+static int gate_up_swiglu_impl(const void *x, int64_t ldx, const void *w_gate_up, int64_t ldw, int dtype, int64_t T,
+                               int64_t H, int64_t F, int splits, void *y, int64_t ldy, void *gu, int64_t ldgu,
+                               void *stream) {
   VA_CHECK_ARG(dtype == VA_BF16, "gate_up_swiglu: only bf16 is implemented");
   VA_CHECK_ARG(T >= 0 && H > 0 && H % TK == 0 && H <= (1 << 20) && F > 0 && F % 128 == 0 && F < (int64_t{1} << 30),
                "gate_up_swiglu: need H %% 64 == 0 and F %% 128 == 0 (H=%lld, F=%lld)", static_cast<long long>(H),
@@ -933,6 +946,8 @@ extern "C" int va_gate_up_swiglu(const void *x, int64_t ldx, const void *w_gate_
                    (F + 128) * ldw * 2 < (int64_t{1} << 31),
                "gate_up_swiglu: strides must be >= H (ldy >= F), %% 8 (ldy %% 4); (F + 128) ldw 2 < 2^31 (32-bit "
                "buffer offsets)");
+  VA_CHECK_ARG(gu == nullptr || (ldgu >= 2 * F && ldgu % 4 == 0 && reinterpret_cast<uintptr_t>(gu) % 8 == 0),
+               "gate_up_swiglu: the saved projection needs ldgu >= 2F, %% 4, 8-byte alignment");
   VA_CHECK_ARG(splits >= 1 && splits <= 64, "gate_up_swiglu: splits in [1, 64]");
   if (T == 0) return VA_OK;
   VA_CHECK_ARG(x && w_gate_up && y, "null pointer argument");
@@ -948,11 +963,24 @@ extern "C" int va_gate_up_swiglu(const void *x, int64_t ldx, const void *w_gate_
   const auto *x16 = static_cast<const uint16_t *>(x);
   const auto *w16 = static_cast<const uint16_t *>(w_gate_up);
   auto *y16 = static_cast<uint16_t *>(y);
-  if (nwg % 8 == 0)
-    hipLaunchKernelGGL(gate_up_swiglu_t256_kernel<true>, dim3(static_cast<unsigned>(nwg)), dim3(T_THREADS), 0, s, x16,
-                       ldx, w16, ldw, T, static_cast<int>(H), F, used, per, y16, ldy);
-  else
-    hipLaunchKernelGGL(gate_up_swiglu_t256_kernel<false>, dim3(static_cast<unsigned>(nwg)), dim3(T_THREADS), 0, s,
-                       x16, ldx, w16, ldw, T, static_cast<int>(H), F, used, per, y16, ldy);
+  auto *g16 = static_cast<uint16_t *>(gu);
+  const bool remap = nwg % 8 == 0;
+  const auto kern = gu != nullptr ? (remap ? gate_up_swiglu_t256_kernel<true, true> : gate_up_swiglu_t256_kernel<false, true>)
+                                  : (remap ? gate_up_swiglu_t256_kernel<true, false>
+                                           : gate_up_swiglu_t256_kernel<false, false>);
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nwg)), dim3(T_THREADS), 0, s, x16, ldx, w16, ldw, T,
+                     static_cast<int>(H), F, used, per, y16, ldy, g16, ldgu);
   return check_launch("gate_up_swiglu");
+}
+
+extern "C" int va_gate_up_swiglu(const void *x, int64_t ldx, const void *w_gate_up, int64_t ldw, int dtype, int64_t T,
+                                 int64_t H, int64_t F, int splits, void *y, int64_t ldy, void *stream) {
+  return gate_up_swiglu_impl(x, ldx, w_gate_up, ldw, dtype, T, H, F, splits, y, ldy, nullptr, 0, stream);
+}
+
+extern "C" int va_gate_up_swiglu_save(const void *x, int64_t ldx, const void *w_gate_up, int64_t ldw, int dtype,
+                                      int64_t T, int64_t H, int64_t F, int splits, void *y, int64_t ldy, void *gu,
+                                      int64_t ldgu, void *stream) {
+  VA_CHECK_ARG(T == 0 || gu != nullptr, "gate_up_swiglu_save: null projection buffer");
+  return gate_up_swiglu_impl(x, ldx, w_gate_up, ldw, dtype, T, H, F, splits, y, ldy, gu, ldgu, stream);
 }

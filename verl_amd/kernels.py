@@ -770,13 +770,74 @@ def gate_up_swiglu(x, w_gate_up, splits: int | None = None):
     if not gate_up_swiglu_supported(x, w_gate_up):
         raise ValueError(f"gate_up_swiglu: unsupported operands x {tuple(x.shape)} / w {tuple(w_gate_up.shape)} "
                          "(need bf16, H % 64 == 0, F % 128 == 0, unit inner stride, 16-byte alignment)")
+    return _gate_up_swiglu_raw(x, w_gate_up, splits, save=False)[0]
+
+
+def _gate_up_swiglu_raw(x, w_gate_up, splits, save: bool):
+    """(y, gu or None): va_gate_up_swiglu, or va_gate_up_swiglu_save which also writes the
+    projection gu [T, 2F] (the merged GEMM's bf16 output) for a backward."""
     T, H = x.shape
     F = w_gate_up.shape[0] // 2
     y = torch.empty(T, F, dtype=x.dtype, device=x.device)
     s = _gate_up_swiglu_splits(T, F // 128) if splits is None else int(splits)
-    L.call("va_gate_up_swiglu", _p(x), x.stride(0), _p(w_gate_up), w_gate_up.stride(0), L.VA_BF16, T, H, F, s, _p(y),
-           F, _stream(x))
-    return y
+    if not save:
+        L.call("va_gate_up_swiglu", _p(x), x.stride(0), _p(w_gate_up), w_gate_up.stride(0), L.VA_BF16, T, H, F, s,
+               _p(y), F, _stream(x))
+        return y, None
+    gu = torch.empty(T, 2 * F, dtype=x.dtype, device=x.device)
+    L.call("va_gate_up_swiglu_save", _p(x), x.stride(0), _p(w_gate_up), w_gate_up.stride(0), L.VA_BF16, T, H, F, s,
+           _p(y), F, _p(gu), 2 * F, _stream(x))
+    return y, gu
+
+
+class _GateUpSwiGLU(torch.autograd.Function):
+    """y = swiglu(x W^T) for the merged gate|up weight W = [gate | up] (views of ``params``) with the
+    GEMM and the activation in ONE forward kernel that also writes the projection gu for the
+    backward (va_gate_up_swiglu_save): the forward of merged_linear + swiglu_merged without the
+    activation's re-read of gu. Backward: va_swiglu_bwd on (dy, gu), then _MergedLinear's dgrad /
+    weight-gradient path (incl. the side-stream weight gradients)."""
+
+    @staticmethod
+    def forward(ctx, x, w_all, n_w, *params):
+        y, gu = _gate_up_swiglu_raw(x, w_all, None, save=True)
+        ctx.save_for_backward(x, w_all, gu)
+        ctx.w_rows = [p.shape[0] for p in params[:n_w]]
+        ctx.has_b = False
+        ctx.params = params
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w_all, gu = ctx.saved_tensors
+        T, F2 = gu.shape
+        F = F2 // 2
+        dy2 = dy.contiguous()
+        dgu = torch.empty(T, F2, dtype=gu.dtype, device=gu.device)
+        L.call("va_swiglu_bwd", _p(dy2), _p(gu), gu.stride(0), F, L.VA_BF16, T, F, _p(dgu), F2, F, _stream(gu))
+        del gu
+        params = ctx.params
+        sink = WGRAD_SINK
+        if sink is not None and dgu.is_cuda and sink.owns_exclusively(params):
+            side = sink.wgrad_stream
+            main = torch.cuda.current_stream(dgu.device)
+            side.wait_stream(main)
+            dx = input_grad(dgu, w_all)
+            with torch.cuda.stream(side):
+                sink.deliver(params, _MergedLinear._param_grads(ctx, dgu, x))
+            sink.throttle(main, keep=(dgu, x))
+            return (dx, None, None, *([None] * len(params)))
+        dx = input_grad(dgu, w_all)
+        return (dx, None, None, *_MergedLinear._param_grads(ctx, dgu, x))
+
+
+def gate_up_swiglu_train(x, w_all, weights: list):
+    """swiglu(x [gate|up]^T) under autograd with the fused forward (_GateUpSwiGLU); ``weights`` are
+    the gate / up parameters (views into ``w_all``) that receive the gradients."""
+    _require_device(x, w_all)
+    _bf16_only(x, w_all)
+    if not gate_up_swiglu_supported(x, w_all):
+        raise ValueError(f"gate_up_swiglu_train: unsupported operands x {tuple(x.shape)} / w {tuple(w_all.shape)}")
+    return _GateUpSwiGLU.apply(x, w_all, len(weights), *weights)
 
 
 def swiglu(gate, up):

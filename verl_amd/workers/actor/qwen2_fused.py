@@ -202,25 +202,31 @@ def _attention(attn, y, cos, sin, cu, max_len, hq, hk, d, attn_blocks=None, attn
     return o(out.reshape(T, hq * d))
 
 
-def _mlp_activation(mlp, y, fuse: bool):
-    """silu(gate_proj(y)) * up_proj(y): one fused kernel in the no-grad forward when the shapes allow
-    (and the projections carry no bias), else the merged GEMM + the SwiGLU kernel."""
+def _mlp_activation(mlp, y, fuse: bool, fuse_train: bool = False):
+    """silu(gate_proj(y)) * up_proj(y): one fused kernel when the shapes allow (and the projections
+    carry no bias) — in the no-grad forward (``fuse``: no projection written) and, with
+    ``fuse_train``, under autograd (the kernel also writes the projection for the backward) — else
+    the merged GEMM + the SwiGLU kernel."""
     lins = [mlp.gate_proj, mlp.up_proj]
-    if fuse and lins[0].bias is None:
-        w_all = _merged(mlp, "gate_up.w", [lin.weight for lin in lins])
+    training = torch.is_grad_enabled() and (y.requires_grad or lins[0].weight.requires_grad)
+    if (fuse_train if training else fuse) and lins[0].bias is None:
+        ws = [lin.weight for lin in lins]
+        w_all = _merged(mlp, "gate_up.w", ws)
         if K.gate_up_swiglu_supported(y, w_all):
-            return K.gate_up_swiglu(y, w_all)
+            return K.gate_up_swiglu_train(y, w_all, ws) if training else K.gate_up_swiglu(y, w_all)
     return K.swiglu_merged(_merged_linear(mlp, "gate_up", y, lins))
 
 
 def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor, cu_seqlens: torch.Tensor,
                    max_seqlen: int, attn_blocks: torch.Tensor = None, attn_kblocks: torch.Tensor = None,
-                   multi_modal_inputs: list = None, fuse_mlp: bool = False) -> torch.Tensor:
+                   multi_modal_inputs: list = None, fuse_mlp: bool = False,
+                   fuse_mlp_train: bool = False) -> torch.Tensor:
     """input_ids [T] and position_ids [T] (or [3, T], mrope) packed, cu_seqlens [B+1] int32 -> last
     hidden state [T, H] bf16 (after the final norm), i.e. Qwen2Model(...).last_hidden_state[0] on
     the same packing. ``fuse_mlp``: outside autograd, gate|up + SwiGLU run as one kernel
     (va_gate_up_swiglu; its GEMM sums in its own order, so the hidden states match the unfused
-    forward to bf16 rounding, not bitwise)."""
+    forward to bf16 rounding, not bitwise). ``fuse_mlp_train``: under autograd, the same kernel also
+    writes the projection for the SwiGLU backward (va_gate_up_swiglu_save)."""
     stack = text_backbone(backbone)
     cfg = stack.config
     hq = cfg.num_attention_heads
@@ -243,7 +249,7 @@ def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor
         residual, y = K.add_rmsnorm(a, residual, ln.weight, ln.variance_epsilon)
         mlp = layer.mlp
         dp = mlp.down_proj
-        a = _mlp_activation(mlp, y, fuse_mlp)
+        a = _mlp_activation(mlp, y, fuse_mlp, fuse_mlp_train)
         h = K.linear(a, dp.weight) if dp.bias is None else dp(a)
     norm = stack.norm
     if h is None:
