@@ -727,7 +727,9 @@ def main():
                        if args.fused_no_grad else "")
                     + ("; the no-grad pass runs gate|up + SwiGLU as one kernel (the [T, 2F] projection never "
                        "reaches HBM; the same bits as the merged GEMM + SwiGLU on exact-arithmetic data, tests, and "
-                       "on the bench's data, relative L2 0.0)" if args.fused_mlp_no_grad else "")),
+                       "on the bench's data, relative L2 0.0)" if args.fused_mlp_no_grad else "")
+                    + ("; the update pass runs gate|up + SwiGLU as one kernel that also writes the projection "
+                       "(the same bits, tests)" if args.fused_mlp_train else "")),
                 "dynamic_bsz_max_token_len": args.dynamic_bsz or None,
                 "compute_max_token_len": args.compute_max_tokens or None,
                 "logprob_max_token_len": (args.logprob_max_tokens or args.dynamic_bsz) if args.dynamic_bsz else None,
