@@ -377,7 +377,7 @@ int va_swiglu_fwd(const void *gu, int64_t ldgu, int64_t uoff, int dtype, int64_t
                   void *stream);
 int va_swiglu_bwd(const void *dy, const void *gu, int64_t ldgu, int64_t uoff, int dtype, int64_t T, int64_t F,
                   void *dgu, int64_t lddgu, int64_t duoff, void *stream);
-/* gate_up_swiglu (ABI 7): y [T, F] (row stride ldy >= F, % 4, 8-byte aligned) = swiglu of the merged
+/* gate_up_swiglu (ABI 7): y [T, F] (row stride ldy >= F, % 8, 16-byte aligned) = swiglu of the merged
  * gate|up projection x [T, H] . w_gate_up [2F, H]^T (gate rows 0..F-1, up rows F..2F-1; row strides ldx /
  * ldw, 16-byte aligned) without writing the [T, 2F] projection: g / u rounded to bf16 as the GEMM's
  * output, then swiglu_fwd's arithmetic. H % 64 == 0, F % 128 == 0; `splits` feature ranges per 256-token
@@ -387,7 +387,7 @@ int va_swiglu_bwd(const void *dy, const void *gu, int64_t ldgu, int64_t uoff, in
 int va_gate_up_swiglu(const void *x, int64_t ldx, const void *w_gate_up, int64_t ldw, int dtype, int64_t T,
                       int64_t H, int64_t F, int splits, void *y, int64_t ldy, void *stream);
 /* gate_up_swiglu_save (ABI 8): as va_gate_up_swiglu, and also the projection's g | u (bf16, exactly
- * the merged GEMM's output) into gu [T, 2F] (row stride ldgu >= 2F, % 4, 8-byte aligned): the
+ * the merged GEMM's output) into gu [T, 2F] (row stride ldgu >= 2F, % 8, 16-byte aligned): the
  * training forward's gate|up GEMM + swiglu_fwd in one kernel, gu kept for va_swiglu_bwd (HF
  * Qwen2MLP under autograd, dp_actor.py:331-333 in update_policy's forward). Not a §8 row. */
 int va_gate_up_swiglu_save(const void *x, int64_t ldx, const void *w_gate_up, int64_t ldw, int dtype, int64_t T,

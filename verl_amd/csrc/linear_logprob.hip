@@ -248,6 +248,7 @@ __global__ __launch_bounds__(256, 2) void linear_logprob_tiles_kernel(
 // row blocks an XCD works on at a time keep their hidden panels in its L2 while the W tiles stream
 // (round-3 dev kernel tools/f1core/f1t.hip, git show 690aed1:tools/f1core/f1t.hip; at 131,072 x 896 x 151,936: 30.1 ms core-only vs 32.3 without the remap).
 constexpr int TB = 256, TK = 64, T_THREADS = 512;
+constexpr int GU_SROW = 72;  // gate_up_swiglu's store scratch row: 64 features + 16 B (bank spread, 16-B reads)
 
 constexpr int T_TILE = TB * TK;  // bf16 elements of one operand's K-step image
 
@@ -738,44 +739,55 @@ __global__ __launch_bounds__(T_THREADS, 1) void gate_up_swiglu_t256_kernel(
     const uint16_t *__restrict__ x, int64_t ldx, const uint16_t *__restrict__ w, int64_t ldw, int64_t T, int K,
     int64_t F, int splits, int tiles_per_split, uint16_t *__restrict__ y, int64_t ldy, uint16_t *__restrict__ gu,
     int64_t ldgu) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
+  // the staging images, then a wave-private 16 x GU_SROW scratch per wave for the epilogue's stores
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE + 8 * 16 * GU_SROW];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar LDS-DMA bases
   const int wr = wave >> 2, wc = wave & 3;
   int64_t row0, sp, vt_begin, vt_end;
   t256_block<REMAP>(splits, tiles_per_split, 2 * F, row0, sp, vt_begin, vt_end);
-  uint16_t *yrow[4], *grow[4];
+  // Stores through LDS: each lane holds 4 consecutive features of one token per (i, j), i.e. 16 rows x
+  // 32 B per wave-instruction; the wave writes its 16-token x 64-feature block of one output into its
+  // scratch and reads it back as whole 128-B row segments (8 lanes x 16 B per token row), so every
+  // global store writes full cache lines. Wave-private: no barrier (a wave's LDS ops stay in order).
+  uint16_t *scr = lds + 2 * 2 * T_TILE + wave * 16 * GU_SROW;
+  auto put = [&](int i, float a, float b, float c, float d) {
+    uint2 q;
+    q.x = pack2_bf16(a, b), q.y = pack2_bf16(c, d);
+    *reinterpret_cast<uint2 *>(scr + (lane & 15) * GU_SROW + (lane >> 4) * 4 + i * 16) = q;
+  };
+  auto flush = [&](int j, uint16_t *out, int64_t ld, int64_t col0) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t r = row0 + wc * 64 + j * 16 + (lane & 15);
-    yrow[j] = r < T ? y + r * ldy : nullptr;
-    if constexpr (SAVE) grow[j] = r < T ? gu + r * ldgu : nullptr;
-  }
+    for (int h = 0; h < 2; ++h) {
+      const int r = h * 8 + (lane >> 3);
+      const uint4 v = *reinterpret_cast<const uint4 *>(scr + r * GU_SROW + (lane & 7) * 8);
+      const int64_t t = row0 + wc * 64 + j * 16 + r;
+      if (t < T) *reinterpret_cast<uint4 *>(out + t * ld + col0 + (lane & 7) * 8) = v;
+    }
+  };
   t256_sweep(
       x, ldx, w, ldw, T, K, 2 * F, row0, vt_begin, vt_end, lds, wave, lane,
       [&](f32x4(&acc)[8][4], int64_t vt) {
-        const int64_t f0 = vt * 128 + wr * 64 + (lane >> 4) * 4;
+        const int64_t c0 = vt * 128 + wr * 64;  // this wave's 64 output features
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if (yrow[j] == nullptr) continue;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float o[4], gg[4], uu[4];
+            float o[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              gg[e] = round_bf16(acc[i][j][e]), uu[e] = round_bf16(acc[i + 4][j][e]);
-              o[e] = round_bf16(va_silu(gg[e])) * uu[e];
-            }
-            uint2 q;
-            q.x = pack2_bf16(o[0], o[1]);
-            q.y = pack2_bf16(o[2], o[3]);
-            *reinterpret_cast<uint2 *>(yrow[j] + f0 + i * 16) = q;
-            if constexpr (SAVE) {
-              uint2 qg, qu;
-              qg.x = pack2_bf16(gg[0], gg[1]), qg.y = pack2_bf16(gg[2], gg[3]);
-              qu.x = pack2_bf16(uu[0], uu[1]), qu.y = pack2_bf16(uu[2], uu[3]);
-              *reinterpret_cast<uint2 *>(grow[j] + f0 + i * 16) = qg;
-              *reinterpret_cast<uint2 *>(grow[j] + F + f0 + i * 16) = qu;
-            }
+            for (int e = 0; e < 4; ++e)
+              o[e] = round_bf16(va_silu(round_bf16(acc[i][j][e]))) * round_bf16(acc[i + 4][j][e]);
+            put(i, o[0], o[1], o[2], o[3]);
+          }
+          flush(j, y, ldy, c0);
+          if constexpr (SAVE) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              put(i, acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);  // g: bf16 of the GEMM output
+            flush(j, gu, ldgu, c0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              put(i, acc[i + 4][j][0], acc[i + 4][j][1], acc[i + 4][j][2], acc[i + 4][j][3]);  // u
+            flush(j, gu, ldgu, F + c0);
           }
         }
       },
@@ -942,18 +954,18 @@ static int gate_up_swiglu_impl(const void *x, int64_t ldx, const void *w_gate_up
   VA_CHECK_ARG(T >= 0 && H > 0 && H % TK == 0 && H <= (1 << 20) && F > 0 && F % 128 == 0 && F < (int64_t{1} << 30),
                "gate_up_swiglu: need H %% 64 == 0 and F %% 128 == 0 (H=%lld, F=%lld)", static_cast<long long>(H),
                static_cast<long long>(F));
-  VA_CHECK_ARG(ldx >= H && ldw >= H && ldx % 8 == 0 && ldw % 8 == 0 && ldy >= F && ldy % 4 == 0 && ldx < (1 << 22) &&
+  VA_CHECK_ARG(ldx >= H && ldw >= H && ldx % 8 == 0 && ldw % 8 == 0 && ldy >= F && ldy % 8 == 0 && ldx < (1 << 22) &&
                    (F + 128) * ldw * 2 < (int64_t{1} << 31),
-               "gate_up_swiglu: strides must be >= H (ldy >= F), %% 8 (ldy %% 4); (F + 128) ldw 2 < 2^31 (32-bit "
-               "buffer offsets)");
-  VA_CHECK_ARG(gu == nullptr || (ldgu >= 2 * F && ldgu % 4 == 0 && reinterpret_cast<uintptr_t>(gu) % 8 == 0),
-               "gate_up_swiglu: the saved projection needs ldgu >= 2F, %% 4, 8-byte alignment");
+               "gate_up_swiglu: strides must be >= H (ldy >= F), %% 8; (F + 128) ldw 2 < 2^31 (32-bit buffer "
+               "offsets)");
+  VA_CHECK_ARG(gu == nullptr || (ldgu >= 2 * F && ldgu % 8 == 0 && reinterpret_cast<uintptr_t>(gu) % 16 == 0),
+               "gate_up_swiglu: the saved projection needs ldgu >= 2F, %% 8, 16-byte alignment");
   VA_CHECK_ARG(splits >= 1 && splits <= 64, "gate_up_swiglu: splits in [1, 64]");
   if (T == 0) return VA_OK;
   VA_CHECK_ARG(x && w_gate_up && y, "null pointer argument");
   VA_CHECK_ARG(reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(w_gate_up) % 16 == 0 &&
-                   reinterpret_cast<uintptr_t>(y) % 8 == 0,
-               "gate_up_swiglu: 16-byte aligned x / weight and 8-byte aligned y required");
+                   reinterpret_cast<uintptr_t>(y) % 16 == 0,
+               "gate_up_swiglu: 16-byte aligned x / weight / y required (whole-line 16-B stores)");
   const int64_t n_vt = F / 128;  // 256 image rows (128 gate + 128 up) per tile
   const int per = static_cast<int>((n_vt + splits - 1) / splits);
   const int used = static_cast<int>((n_vt + per - 1) / per);
