@@ -640,13 +640,16 @@ __global__ __launch_bounds__(256) void linear_logprob_merge_kernel(const float *
 // dlog column 0 is vocab vbase): the reference's _Split_Dlogits_N loop (kernels.py:1491-1548) runs it
 // per range so that only [N, range] dlogits exist at a time. A label counts as valid against V_full
 // (its g_lp term enters kk for every range); its own +g_lp lands only in the range that holds it.
-template <bool SCALE, bool ROUND, bool REMAP>
+// WIDE (dlogits 16-byte aligned, ldd % 8 == 0): the stores go through a wave-private LDS scratch as
+// whole row segments (8 lanes x 16 B per token row, 64 vocab columns at a time), as the fused SwiGLU's;
+// otherwise each lane stores its 4 columns (8 B) directly.
+template <bool SCALE, bool ROUND, bool REMAP, bool WIDE>
 __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
     const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
     const int64_t *__restrict__ labels, const float *__restrict__ lse_in, const float *__restrict__ ent_in,
     const float *__restrict__ g_logp, const float *__restrict__ g_ent, int64_t N, int K, int64_t V, int64_t V_full,
     int64_t vbase, int splits, int tiles_per_split, float temperature, uint16_t *__restrict__ dlog, int64_t ldd) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE];
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE + (WIDE ? 8 * 16 * GU_SROW : 0)];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar LDS-DMA bases
   const int wr = wave >> 2, wc = wave & 3;
   int64_t row0, sp, vt_begin, vt_end;
@@ -673,6 +676,23 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
     drow[j] = ok ? dlog + r * ldd : nullptr;
   }
 
+  uint16_t *scr = lds + 2 * 2 * T_TILE + wave * 16 * GU_SROW;  // WIDE only
+  // scratch (16 token rows x 64 columns) -> dlogits columns [c0, c0 + 64) of this wave's token rows j:
+  // whole 16-B pieces, the range's last piece (V % 8 == 4) as 8 B
+  auto flush = [&](int j, int64_t c0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = h * 8 + (lane >> 3);
+      const uint4 v = *reinterpret_cast<const uint4 *>(scr + r * GU_SROW + (lane & 7) * 8);
+      const int64_t t = row0 + wc * 64 + j * 16 + r;
+      const int64_t col = c0 + (lane & 7) * 8;
+      if (t < N && col < V) {
+        uint16_t *dst = dlog + t * ldd + col;
+        if (col + 8 <= V) *reinterpret_cast<uint4 *>(dst) = v;
+        else *reinterpret_cast<uint2 *>(dst) = make_uint2(v.x, v.y);
+      }
+    }
+  };
   t256_sweep(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
     const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;
 #pragma unroll
@@ -697,10 +717,13 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
 #pragma unroll
           for (int e = 0; e < 4; ++e) d[e] = d[e] / temperature;
         }
-        if (drow[j] != nullptr && vb < V) {
-          uint2 q;
-          q.x = pack2_bf16(d[0], d[1]);
-          q.y = pack2_bf16(d[2], d[3]);
+        uint2 q;
+        q.x = pack2_bf16(d[0], d[1]);
+        q.y = pack2_bf16(d[2], d[3]);
+        if constexpr (WIDE) {
+          *reinterpret_cast<uint2 *>(scr + (lane & 15) * GU_SROW + (lane >> 4) * 4 + (i & 3) * 16) = q;
+          if ((i & 3) == 3) flush(j, static_cast<int64_t>(vt) * TB + wr * 128 + (i >> 2) * 64);
+        } else if (drow[j] != nullptr && vb < V) {
           *reinterpret_cast<uint2 *>(drow[j] + vb) = q;
         }
       }
@@ -886,14 +909,13 @@ static void launch_bwd_t256(bool remap, dim3 grid, hipStream_t s, const uint16_t
                             const float *ent, const float *g_logp, const float *g_ent, int64_t N, int64_t H,
                             int64_t V, int64_t V_full, int64_t vbase, int used, int per, float temperature,
                             uint16_t *dlog, int64_t ldd) {
-  if (remap)
-    hipLaunchKernelGGL((linear_logprob_bwd_t256_kernel<SC, RD, true>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16,
-                       ldw, labels, lse, ent, g_logp, g_ent, N, static_cast<int>(H), V, V_full, vbase, used, per,
-                       temperature, dlog, ldd);
-  else
-    hipLaunchKernelGGL((linear_logprob_bwd_t256_kernel<SC, RD, false>), grid, dim3(T_THREADS), 0, s, h16, ldh, w16,
-                       ldw, labels, lse, ent, g_logp, g_ent, N, static_cast<int>(H), V, V_full, vbase, used, per,
-                       temperature, dlog, ldd);
+  const bool wide = ldd % 8 == 0 && reinterpret_cast<uintptr_t>(dlog) % 16 == 0;
+  const auto kern = remap ? (wide ? linear_logprob_bwd_t256_kernel<SC, RD, true, true>
+                                  : linear_logprob_bwd_t256_kernel<SC, RD, true, false>)
+                          : (wide ? linear_logprob_bwd_t256_kernel<SC, RD, false, true>
+                                  : linear_logprob_bwd_t256_kernel<SC, RD, false, false>);
+  hipLaunchKernelGGL(kern, grid, dim3(T_THREADS), 0, s, h16, ldh, w16, ldw, labels, lse, ent, g_logp, g_ent, N,
+                     static_cast<int>(H), V, V_full, vbase, used, per, temperature, dlog, ldd);
 }
 
 extern "C" int va_linear_logprob_bwd(const void *hidden, int64_t ldh, const void *weight, int64_t ldw, int dtype,
