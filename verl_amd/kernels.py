@@ -817,7 +817,7 @@ class _GateUpSwiGLU(torch.autograd.Function):
         del gu
         params = ctx.params
         sink = WGRAD_SINK
-        if sink is not None and dgu.is_cuda and sink.owns_exclusively(params):
+        if sink is not None and dgu.is_cuda and w_all.shape[0] < WGRAD_SWAP_MIN_OUT and sink.owns_exclusively(params):
             side = sink.wgrad_stream
             main = torch.cuda.current_stream(dgu.device)
             side.wait_stream(main)
