@@ -248,7 +248,7 @@ __global__ __launch_bounds__(256, 2) void linear_logprob_tiles_kernel(
 // row blocks an XCD works on at a time keep their hidden panels in its L2 while the W tiles stream
 // (round-3 dev kernel tools/f1core/f1t.hip, git show 690aed1:tools/f1core/f1t.hip; at 131,072 x 896 x 151,936: 30.1 ms core-only vs 32.3 without the remap).
 constexpr int TB = 256, TK = 64, T_THREADS = 512;
-constexpr int GU_SROW = 72;  // gate_up_swiglu's store scratch row: 64 features + 16 B (bank spread, 16-B reads)
+constexpr int GU_SROW = 72;  // epilogue store scratch row (fused SwiGLU, dlogits): 64 columns + 16 B (bank spread, 16-B reads)
 
 constexpr int T_TILE = TB * TK;  // bf16 elements of one operand's K-step image
 
