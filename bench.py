@@ -177,6 +177,8 @@ def parse(argv=None):
     ap.add_argument("--fused-mlp-train", type=int, default=0, choices=[0, 1],
                     help="1: update passes run gate|up + SwiGLU as one kernel that also writes the projection for "
                          "the backward (fused_mlp_train)")
+    ap.add_argument("--fused-qkv", type=int, default=0, choices=[0, 1],
+                    help="1: the q|k|v GEMM + bias + RoPE as one kernel in every pass (fused_qkv)")
     ap.add_argument("--f1-after-backbone", type=int, default=1, choices=[0, 1],
                     help="1: the no-grad pass runs every micro-batch's backbone, then the fused lm_head launches back "
                          "to back (fused_lm_head_after_backbone); 0: backbone + lm_head per micro-batch")
@@ -514,6 +516,7 @@ def main():
             fused_logprob_no_grad=bool(args.fused_no_grad),
             fused_mlp_no_grad=bool(args.fused_mlp_no_grad),
             fused_mlp_train=bool(args.fused_mlp_train),
+            fused_qkv=bool(args.fused_qkv),
             fused_lm_head_after_backbone=bool(args.f1_after_backbone),
             fused_lm_head_concat=bool(args.f1_concat),
             use_fused_kernels=bool(args.fused_kernels),
@@ -729,7 +732,8 @@ def main():
                        "reaches HBM; the same bits as the merged GEMM + SwiGLU on exact-arithmetic data, tests, and "
                        "on the bench's data, relative L2 0.0)" if args.fused_mlp_no_grad else "")
                     + ("; the update pass runs gate|up + SwiGLU as one kernel that also writes the projection "
-                       "(the same bits, tests)" if args.fused_mlp_train else "")),
+                       "(the same bits, tests)" if args.fused_mlp_train else "")
+                    + ("; the q|k|v GEMM, bias and RoPE run as one kernel (tests)" if args.fused_qkv else "")),
                 "dynamic_bsz_max_token_len": args.dynamic_bsz or None,
                 "compute_max_token_len": args.compute_max_tokens or None,
                 "logprob_max_token_len": (args.logprob_max_tokens or args.dynamic_bsz) if args.dynamic_bsz else None,
@@ -740,6 +744,7 @@ def main():
                 "fused_logprob_no_grad": bool(args.fused_no_grad),
                 "fused_mlp_no_grad": bool(args.fused_mlp_no_grad),
                 "fused_mlp_train": bool(args.fused_mlp_train),
+                "fused_qkv": bool(args.fused_qkv),
                 "fused_lm_head_after_backbone": bool(args.f1_after_backbone),
                 "fused_lm_head_concat": bool(args.f1_concat),
                 "use_fused_kernels": bool(args.fused_kernels),

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define VA_ABI_VERSION 8
+#define VA_ABI_VERSION 9
 
 /* error codes */
 #define VA_OK 0
@@ -393,6 +393,15 @@ int va_gate_up_swiglu(const void *x, int64_t ldx, const void *w_gate_up, int64_t
 int va_gate_up_swiglu_save(const void *x, int64_t ldx, const void *w_gate_up, int64_t ldw, int dtype, int64_t T,
                            int64_t H, int64_t F, int splits, void *y, int64_t ldy, void *gu, int64_t ldgu,
                            void *stream);
+/* qkv_rope (ABI 9): q [T, Hq D], k / v [T, Hk D] (contiguous, 16-byte aligned) from x [T, H] and the merged
+ * q|k|v weight w_qkv [(Hq + 2 Hk) D, H] (row strides ldx / ldw, 16-byte aligned) plus its bias [(Hq + 2 Hk) D]
+ * (nullable): bf16(x w^T + b), then rope_qkv_fwd's rotate-half RoPE on q and k with cos / sin [T, D] (row
+ * stride D) — the GEMM + rope_qkv_fwd pair without the [T, (Hq + 2 Hk) D] projection in HBM. D == 64,
+ * H % 64 == 0; `splits` feature ranges per 256-token block (1..64). Qwen2Attention's q/k/v_proj +
+ * apply_rotary_pos_emb under the actor's forwards (dp_actor.py:331-333). Not a §8 row. */
+int va_qkv_rope(const void *x, int64_t ldx, const void *w_qkv, int64_t ldw, const void *bias, const void *cos,
+                const void *sin, int dtype, int64_t T, int64_t H, int Hq, int Hk, int D, int splits, void *q, void *k,
+                void *v, void *stream);
 int va_rope_qkv_fwd(const void *qkv, int64_t ld, const void *cos, const void *sin, int dtype, int64_t T,
                     int64_t Hq, int64_t Hk, int64_t D, void *q, void *k, void *v, void *stream);
 int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *cos, const void *sin, int dtype,

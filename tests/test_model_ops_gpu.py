@@ -398,6 +398,66 @@ def test_fused_mlp_train_forward_backward_bitwise_on_exact_data(T, H, F_):
         assert torch.equal(a, b), what
 
 
+def _qkv_case(T, H, hq, hk, seed, bias=True):
+    """Exact operands for the fused q|k|v: integer x, w / 8, bias / 8 (the projection and bias sum are
+    exact in fp32), and real rotary tables of packed positions."""
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    nf = (hq + 2 * hk) * 64
+    x = torch.randint(-2, 3, (T, H), device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randint(-3, 4, (nf, H), device=DEV, generator=g).float() / 8).to(torch.bfloat16)
+    b = (torch.randint(-4, 5, (nf,), device=DEV, generator=g).float() / 8).to(torch.bfloat16) if bias else None
+    pos = torch.randint(0, 4096, (T,), device=DEV, generator=g).float()
+    inv = 1.0 / (1e6 ** (torch.arange(0, 64, 2, device=DEV).float() / 64))
+    fr = pos[:, None] * inv[None]
+    emb = torch.cat([fr, fr], -1)
+    return x, w, b, emb.cos().to(torch.bfloat16)[None], emb.sin().to(torch.bfloat16)[None]
+
+
+@pytest.mark.parametrize("T,H,hq,hk,bias", [(1000, 896, 14, 2, True), (300, 128, 4, 2, True), (37, 64, 2, 1, False),
+                                            (2048, 896, 14, 2, True)])
+def test_qkv_rope_bitwise_on_exact_data(T, H, hq, hk, bias):
+    """va_qkv_rope (ABI 9) == merged q|k|v GEMM with bias (hipBLASLt) + rope_qkv, bit for bit, on exact
+    projections: q / k rotated, v passed through, ragged token tails, a last tile half past the heads."""
+    from verl_amd import kernels as K
+
+    x, w, b, cos, sin = _qkv_case(T, H, hq, hk, seed=T + hq)
+    with torch.no_grad():
+        want = K.rope_qkv(torch.nn.functional.linear(x, w, b), cos, sin, hq, hk, 64)
+        got = K.qkv_rope(x, w, b, cos, sin, hq, hk, 64, [w], [b] if bias else None)
+    for a, e, what in zip(got, want, "qkv"):
+        assert torch.equal(a, e), what
+
+
+def test_qkv_rope_gradients_equal_the_unfused_path():
+    """Under autograd the fused q|k|v gives the unfused path's gradients of x, the q/k/v weights and
+    biases bit for bit on exact data (the backward runs the same rope_qkv_bwd / dgrad / weight and
+    bias-gradient kernels)."""
+    from verl_amd import kernels as K
+
+    T, H, hq, hk = 512, 128, 4, 2
+    x0, w0, b0, cos, sin = _qkv_case(T, H, hq, hk, seed=5)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    dq, dk, dv = ((torch.randint(-2, 3, (T, n, 64), device=DEV, generator=g).float() / 4).to(torch.bfloat16)
+                  for n in (hq, hk, hk))
+    sizes = [hq * 64, hk * 64, hk * 64]
+    res = {}
+    for fused in (False, True):
+        x = x0.clone().requires_grad_(True)
+        w_all, b_all = w0.clone(), b0.clone()
+        ws = [torch.nn.Parameter(t) for t in torch.split(w_all, sizes)]
+        bs = [torch.nn.Parameter(t) for t in torch.split(b_all, sizes)]
+        for p_, t in zip(ws + bs, list(torch.split(w_all, sizes)) + list(torch.split(b_all, sizes))):
+            p_.data = t
+        if fused:
+            q, k, v = K.qkv_rope(x, w_all, b_all, cos, sin, hq, hk, 64, ws, bs)
+        else:
+            q, k, v = K.rope_qkv(K.merged_linear(x, w_all, b_all, ws, bs), cos, sin, hq, hk, 64)
+        torch.autograd.backward([q, k, v], [dq, dk, dv])
+        res[fused] = [q.detach(), k.detach(), v.detach(), x.grad] + [p_.grad for p_ in ws + bs]
+    for i, (a, e) in enumerate(zip(res[True], res[False])):
+        assert torch.equal(a, e), i
+
+
 def test_gate_up_swiglu_random_vs_fp32():
     """Random operands: within bf16 rounding of silu(g) * u from an fp32 GEMM (tolerance: 2 bf16 ulp on
     all but 1e-3 of the elements, i.e. the product's own rounding points)."""

@@ -41,7 +41,7 @@ VA_TUNE_WGRAD_REMAINDER, VA_TUNE_FLASH_DMA, VA_TUNE_WGRAD_MFMA = 18, 19, 20
 FLASH_TUNING_DEFAULTS = {VA_TUNE_FLASH_DMA: 7, VA_TUNE_FLASH_DQ_KB: 64, VA_TUNE_FLASH_DKDV_QT: 64,
                          VA_TUNE_FLASH_FWD_KB: 64, VA_TUNE_FLASH_GROUPED_DKDV: -1}
 
-ABI_VERSION = 8  # include/verl_amd.h VA_ABI_VERSION
+ABI_VERSION = 9  # include/verl_amd.h VA_ABI_VERSION
 
 _P = c_void_p
 _SIGNATURES: dict[str, tuple] = {
@@ -121,6 +121,8 @@ _SIGNATURES: dict[str, tuple] = {
          _P, _P, _P, _P, _P, _P],
     ),
     "va_karmarkar_karp": (c_int, [_P, c_int64, c_int64, c_int, _P, _P]),
+    "va_qkv_rope": (c_int, [_P, c_int64, _P, c_int64, _P, _P, _P, c_int, c_int64, c_int64, c_int, c_int, c_int, c_int,
+                            _P, _P, _P, _P]),
     "va_rope_qkv_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, c_int64, _P]),
     "va_transpose_16": (c_int, [_P, c_int64, c_int64, c_int64, _P, c_int64, _P]),
     "va_weight_grad_workspace_bytes": (c_int64, [c_int64, c_int64, c_int64, c_int]),

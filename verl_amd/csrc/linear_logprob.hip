@@ -817,6 +817,98 @@ __global__ __launch_bounds__(T_THREADS, 1) void gate_up_swiglu_t256_kernel(
       GateUpRows{F});
 }
 
+// ------------------------------------------------------------------ q|k|v projection + bias + RoPE
+// The attention block's merged q|k|v GEMM with its bias and rotate-half RoPE in the epilogue, writing
+// q [T, Hq D], k / v [T, Hk D] directly (head_dim D = 64): the unfused path's [T, (Hq + 2 Hk) D]
+// projection and its rope_qkv_fwd pass disappear. A wave-row's 128 features are two whole heads, and
+// a lane's features 16 i + 4 (lane >> 4) + e of a head pair d with d + 32 in blocks i and i + 2, so
+// RoPE is lane-local; per element the arithmetic of F.linear's bias epilogue (bf16(acc + b)) and of
+// rope_qkv_fwd (model_ops.hip: bf16 after each product, then the sum rounded). Stores through the
+// wave-private LDS scratch as whole 128-B head rows. cos / sin [T, D] bf16 (row stride D).
+template <bool REMAP>
+__global__ __launch_bounds__(T_THREADS, 1) void qkv_rope_t256_kernel(
+    const uint16_t *__restrict__ x, int64_t ldx, const uint16_t *__restrict__ w, int64_t ldw,
+    const uint16_t *__restrict__ bias, const uint16_t *__restrict__ cs, const uint16_t *__restrict__ sn, int64_t T,
+    int K, int Hq, int Hk, int splits, int tiles_per_split, uint16_t *__restrict__ q, uint16_t *__restrict__ k,
+    uint16_t *__restrict__ v) {
+  constexpr int D = 64;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * T_TILE + 8 * 16 * GU_SROW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3, g4 = (lane >> 4) * 4;
+  const int nh = Hq + 2 * Hk;
+  const int64_t NF = static_cast<int64_t>(nh) * D;
+  int64_t row0, sp, vt_begin, vt_end;
+  t256_block<REMAP>(splits, tiles_per_split, NF, row0, sp, vt_begin, vt_end);
+  uint16_t *scr = lds + 2 * 2 * T_TILE + wave * 16 * GU_SROW;
+  auto put = [&](int i, const float (&o)[4]) {
+    uint2 u;
+    u.x = pack2_bf16(o[0], o[1]), u.y = pack2_bf16(o[2], o[3]);
+    *reinterpret_cast<uint2 *>(scr + (lane & 15) * GU_SROW + g4 + i * 16) = u;
+  };
+  auto flush = [&](int j, uint16_t *out, int64_t ld, int64_t col0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = h * 8 + (lane >> 3);
+      const uint4 val = *reinterpret_cast<const uint4 *>(scr + r * GU_SROW + (lane & 7) * 8);
+      const int64_t t = row0 + wc * 64 + j * 16 + r;
+      if (t < T) *reinterpret_cast<uint4 *>(out + t * ld + col0 + (lane & 7) * 8) = val;
+    }
+  };
+  // bf16 lanes of a packed pair, as fp32
+  auto lo = [](uint32_t u) { return __uint_as_float(u << 16); };
+  auto hi = [](uint32_t u) { return __uint_as_float(u & 0xffff0000u); };
+  auto el = [&](const uint2 &u, int e) { return e == 0 ? lo(u.x) : e == 1 ? hi(u.x) : e == 2 ? lo(u.y) : hi(u.y); };
+  t256_sweep(x, ldx, w, ldw, T, K, NF, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
+    const int hb = static_cast<int>(vt * 4) + wr * 2;  // this wave-row's two heads
+    uint2 bb[8];  // bias of features 16 i + g4 + 0..3 of the two heads (packed bf16)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t f = static_cast<int64_t>(hb) * D + i * 16 + g4;
+      bb[i] = (bias != nullptr && f < NF) ? *reinterpret_cast<const uint2 *>(bias + f) : make_uint2(0u, 0u);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int64_t t = row0 + wc * 64 + j * 16 + (lane & 15);
+      if (t >= T) t = T - 1;  // rows past T: computed, not stored
+      uint2 cc[4], ss[4];  // cos / sin at d = 16 i + g4 + 0..3 (i >= 2: the second half), packed bf16
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        cc[i] = *reinterpret_cast<const uint2 *>(cs + t * D + i * 16 + g4);
+        ss[i] = *reinterpret_cast<const uint2 *>(sn + t * D + i * 16 + g4);
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int head = hb + hh;
+        if (head >= nh) continue;  // wave-uniform: the last tile's unused half
+        auto xv = [&](int i, int e) { return round_bf16(acc[4 * hh + i][j][e] + el(bb[4 * hh + i], e)); };
+        if (head < Hq + Hk) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            float o1[4], o2[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float x1 = xv(i, e), x2 = xv(i + 2, e);
+              o1[e] = round_bf16(x1 * el(cc[i], e)) + round_bf16(-x2 * el(ss[i], e));
+              o2[e] = round_bf16(x2 * el(cc[i + 2], e)) + round_bf16(x1 * el(ss[i + 2], e));
+            }
+            put(i, o1);
+            put(i + 2, o2);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float o[4] = {xv(i, 0), xv(i, 1), xv(i, 2), xv(i, 3)};
+            put(i, o);
+          }
+        }
+        if (head < Hq) flush(j, q, static_cast<int64_t>(Hq) * D, static_cast<int64_t>(head) * D);
+        else if (head < Hq + Hk) flush(j, k, static_cast<int64_t>(Hk) * D, static_cast<int64_t>(head - Hq) * D);
+        else flush(j, v, static_cast<int64_t>(Hk) * D, static_cast<int64_t>(head - Hq - Hk) * D);
+      }
+    }
+  });
+}
+
 }  // namespace
 }  // namespace va
 
@@ -1017,4 +1109,36 @@ extern "C" int va_gate_up_swiglu_save(const void *x, int64_t ldx, const void *w_
                                       int64_t ldgu, void *stream) {
   VA_CHECK_ARG(T == 0 || gu != nullptr, "gate_up_swiglu_save: null projection buffer");
   return gate_up_swiglu_impl(x, ldx, w_gate_up, ldw, dtype, T, H, F, splits, y, ldy, gu, ldgu, stream);
+}
+
+extern "C" int va_qkv_rope(const void *x, int64_t ldx, const void *w_qkv, int64_t ldw, const void *bias,
+                           const void *cos, const void *sin, int dtype, int64_t T, int64_t H, int Hq, int Hk, int D,
+                           int splits, void *q, void *k, void *v, void *stream) {
+  VA_CHECK_ARG(dtype == VA_BF16, "qkv_rope: only bf16 is implemented");
+  VA_CHECK_ARG(D == 64, "qkv_rope: head_dim 64 only (got %d)", D);
+  VA_CHECK_ARG(T >= 0 && H > 0 && H % TK == 0 && H <= (1 << 20) && Hq > 0 && Hk > 0 && Hq % Hk == 0,
+               "qkv_rope: need H %% 64 == 0 and Hq a multiple of Hk");
+  const int64_t NF = static_cast<int64_t>(Hq + 2 * Hk) * D;
+  VA_CHECK_ARG(ldx >= H && ldw >= H && ldx % 8 == 0 && ldw % 8 == 0 && ldx < (1 << 22) && ldw < (1 << 22),
+               "qkv_rope: strides must be >= H, %% 8, < 2^22");
+  VA_CHECK_ARG(splits >= 1 && splits <= 64, "qkv_rope: splits in [1, 64]");
+  if (T == 0) return VA_OK;
+  VA_CHECK_ARG(x && w_qkv && cos && sin && q && k && v, "null pointer argument");
+  VA_CHECK_ARG(reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(w_qkv) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(q) % 16 == 0 && reinterpret_cast<uintptr_t>(k) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(v) % 16 == 0 && reinterpret_cast<uintptr_t>(cos) % 8 == 0 &&
+                   reinterpret_cast<uintptr_t>(sin) % 8 == 0 && reinterpret_cast<uintptr_t>(bias) % 8 == 0,
+               "qkv_rope: 16-byte aligned x / w / q / k / v and 8-byte aligned cos / sin / bias required");
+  const int64_t n_vt = (NF + TB - 1) / TB;
+  const int per = static_cast<int>((n_vt + splits - 1) / splits);
+  const int used = static_cast<int>((n_vt + per - 1) / per);
+  const int64_t nwg = ((T + TB - 1) / TB) * used;
+  VA_CHECK_ARG(nwg < (int64_t{1} << 31), "qkv_rope: grid too large");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const auto kern = nwg % 8 == 0 ? qkv_rope_t256_kernel<true> : qkv_rope_t256_kernel<false>;
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nwg)), dim3(T_THREADS), 0, s, static_cast<const uint16_t *>(x),
+                     ldx, static_cast<const uint16_t *>(w_qkv), ldw, static_cast<const uint16_t *>(bias),
+                     static_cast<const uint16_t *>(cos), static_cast<const uint16_t *>(sin), T, static_cast<int>(H), Hq,
+                     Hk, used, per, static_cast<uint16_t *>(q), static_cast<uint16_t *>(k), static_cast<uint16_t *>(v));
+  return check_launch("qkv_rope");
 }

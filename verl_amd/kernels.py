@@ -1108,6 +1108,82 @@ class _RoPEQKV(torch.autograd.Function):
         return dqkv, None, None, None, None, None
 
 
+def qkv_rope_supported(x, w_all, b_all, cos, head_dim: int) -> bool:
+    """Shapes / layouts va_qkv_rope takes (bf16 on the device, head_dim 64, H % 64 == 0)."""
+    return (head_dim == 64 and x.is_cuda and x.dtype == w_all.dtype == torch.bfloat16 and x.dim() == 2
+            and x.shape[1] % 64 == 0 and x.stride(-1) == 1 and w_all.stride(-1) == 1 and x.stride(0) % 8 == 0
+            and w_all.stride(0) % 8 == 0 and x.stride(0) < (1 << 22) and w_all.stride(0) < (1 << 22)
+            and x.data_ptr() % 16 == 0 and w_all.data_ptr() % 16 == 0
+            and (b_all is None or (b_all.dtype == torch.bfloat16 and b_all.is_contiguous() and b_all.data_ptr() % 8 == 0))
+            and cos.dtype == torch.bfloat16)
+
+
+def _qkv_rope_raw(x, w_all, b_all, c, s, hq: int, hk: int, d: int):
+    T, H = x.shape
+    q = torch.empty(T, hq, d, dtype=x.dtype, device=x.device)
+    k = torch.empty(T, hk, d, dtype=x.dtype, device=x.device)
+    v = torch.empty(T, hk, d, dtype=x.dtype, device=x.device)
+    n_vt = -(-((hq + 2 * hk) * d) // 256)
+    splits = int(min(64, max(1, -(-4096 // max(1, (T + 255) // 256)), 1), n_vt))
+    L.call("va_qkv_rope", _p(x), x.stride(0), _p(w_all), w_all.stride(0), _p(b_all) if b_all is not None else None,
+           _p(c), _p(s), L.VA_BF16, T, H, hq, hk, d, splits, _p(q), _p(k), _p(v), _stream(x))
+    return q, k, v
+
+
+class _QKVRoPE(torch.autograd.Function):
+    """q, k, v = rope(split(x W^T + b)) with the GEMM, bias and RoPE in ONE forward kernel (va_qkv_rope,
+    no [T, (Hq + 2 Hk) D] projection in HBM). Backward: rope_qkv_bwd into dqkv, then _MergedLinear's
+    dgrad / weight / bias-gradient path (incl. the side-stream weight gradients)."""
+
+    @staticmethod
+    def forward(ctx, x, w_all, b_all, c, s, hq, hk, d, n_w, *params):
+        q, k, v = _qkv_rope_raw(x, w_all, b_all, c, s, hq, hk, d)
+        ctx.save_for_backward(x, w_all, c, s)
+        ctx.dims = (hq, hk, d)
+        ctx.w_rows = [p.shape[0] for p in params[:n_w]]
+        ctx.has_b = b_all is not None
+        ctx.params = params
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        x, w_all, c, s = ctx.saved_tensors
+        hq, hk, d = ctx.dims
+        T = x.shape[0]
+        dq = dq.contiguous() if dq is not None else torch.zeros(T, hq, d, dtype=x.dtype, device=x.device)
+        dk = dk.contiguous() if dk is not None else torch.zeros(T, hk, d, dtype=x.dtype, device=x.device)
+        dv = dv.contiguous() if dv is not None else torch.zeros(T, hk, d, dtype=x.dtype, device=x.device)
+        width = (hq + 2 * hk) * d
+        dqkv = torch.empty(T, width, dtype=x.dtype, device=x.device)
+        L.call("va_rope_qkv_bwd", _p(dq), _p(dk), _p(dv), _p(c), _p(s), L.VA_BF16, T, hq, hk, d, _p(dqkv), width,
+               _stream(dqkv))
+        params = ctx.params
+        nones = (None,) * 8
+        sink = WGRAD_SINK
+        if sink is not None and dqkv.is_cuda and sink.owns_exclusively(params):
+            side = sink.wgrad_stream
+            main = torch.cuda.current_stream(dqkv.device)
+            side.wait_stream(main)
+            dx = input_grad(dqkv, w_all)
+            with torch.cuda.stream(side):
+                sink.deliver(params, _MergedLinear._param_grads(ctx, dqkv, x))
+            sink.throttle(main, keep=(dqkv, x))
+            return (dx, *nones, *([None] * len(params)))
+        return (input_grad(dqkv, w_all), *nones, *_MergedLinear._param_grads(ctx, dqkv, x))
+
+
+def qkv_rope(x, w_all, b_all, cos, sin, num_q_heads: int, num_kv_heads: int, head_dim: int, weights: list,
+             biases: list | None = None):
+    """(q, k, v) [T, H, D] = rope_qkv(merged_linear(x, w_all, b_all)) with the GEMM, bias and RoPE in one
+    kernel (va_qkv_rope); gradients to ``weights`` / ``biases`` (views into w_all / b_all) under autograd."""
+    _require_device(x, w_all, cos, sin)
+    _bf16_only(x, w_all, cos, sin)
+    T = x.shape[0]
+    c, s = cos.reshape(T, head_dim).contiguous(), sin.reshape(T, head_dim).contiguous()
+    params = list(weights) + (list(biases) if biases else [])
+    return _QKVRoPE.apply(x, w_all, b_all, c, s, num_q_heads, num_kv_heads, head_dim, len(weights), *params)
+
+
 def rope_qkv(qkv, cos, sin, num_q_heads: int, num_kv_heads: int, head_dim: int):
     """Split the merged q|k|v projection [T, (Hq+2Hk)*D] into flash varlen's [T, H, D] tensors and
     apply apply_rotary_pos_emb (rotate_half form) to q and k, in one kernel (bf16)."""

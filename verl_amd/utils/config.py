@@ -62,6 +62,7 @@ def actor_config(**overrides) -> AttrDict:
         fused_logprob_no_grad=False,
         fused_mlp_no_grad=False,
         fused_mlp_train=False,
+        fused_qkv=False,
         # (verl_amd) responses per update forward/backward pass; None = ppo_micro_batch_size_per_gpu
         compute_micro_batch_size_per_gpu=None,
         # (verl_amd) use_dynamic_bsz: tokens per update pass holding several token-budget micro-batches

@@ -296,6 +296,8 @@ class DataParallelPPOActor(BasePPOActor):
         self.fused_mlp_no_grad = bool(self.config.get("fused_mlp_no_grad", False))
         # update passes: the same kernel under autograd, also writing the projection for the backward
         self.fused_mlp_train = bool(self.config.get("fused_mlp_train", False))
+        # all passes: the q|k|v GEMM + bias + RoPE as one kernel (qwen2_fused._qkv)
+        self.fused_qkv = bool(self.config.get("fused_qkv", False))
         # no-grad passes with the fused lm_head: run all micro-batches' backbones, then the lm_head
         # launches back to back (compute_log_prob)
         self.fused_lm_head_after_backbone = bool(self.config.get("fused_lm_head_after_backbone", True))
@@ -418,7 +420,7 @@ class DataParallelPPOActor(BasePPOActor):
                                     attn_kblocks=packing.attn_kblocks if fa else None,
                                     multi_modal_inputs=multi_modal_inputs,
                                     fuse_mlp=self.fused_mlp_no_grad and not torch.is_grad_enabled(),
-                                    fuse_mlp_train=self.fused_mlp_train)
+                                    fuse_mlp_train=self.fused_mlp_train, fuse_qkv=self.fused_qkv)
         else:
             hidden = hf_packed_hidden(self._backbone, ids, pos, packing, multi_modal_inputs)
         h_sel = hidden.index_select(0, packing.sel_hidden)

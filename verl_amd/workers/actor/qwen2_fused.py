@@ -188,10 +188,24 @@ def _merged_linear(module, key: str, x, linears: list):
     return K.merged_linear(x, w_all, b_all, ws, bs)
 
 
-def _attention(attn, y, cos, sin, cu, max_len, hq, hk, d, attn_blocks=None, attn_kblocks=None):
+def _qkv(attn, y, cos, sin, hq, hk, d, fuse: bool):
+    """q, k, v [T, H, D] after RoPE: the merged q|k|v GEMM + the RoPE kernel, or (``fuse``) one kernel
+    with the bias and RoPE in the GEMM's epilogue (va_qkv_rope)."""
+    lins = [attn.q_proj, attn.k_proj, attn.v_proj]
+    if fuse:
+        ws = [lin.weight for lin in lins]
+        w_all = _merged(attn, "qkv.w", ws)
+        bs = [lin.bias for lin in lins] if lins[0].bias is not None else None
+        b_all = _merged(attn, "qkv.b", bs) if bs else None
+        if K.qkv_rope_supported(y, w_all, b_all, cos, d):
+            return K.qkv_rope(y, w_all, b_all, cos, sin, hq, hk, d, ws, bs)
+    qkv = _merged_linear(attn, "qkv", y, lins)
+    return K.rope_qkv(qkv, cos, sin, hq, hk, d)
+
+
+def _attention(attn, y, cos, sin, cu, max_len, hq, hk, d, attn_blocks=None, attn_kblocks=None, fuse_qkv=False):
     T = y.shape[0]
-    qkv = _merged_linear(attn, "qkv", y, [attn.q_proj, attn.k_proj, attn.v_proj])
-    q, k, v = K.rope_qkv(qkv, cos, sin, hq, hk, d)
+    q, k, v = _qkv(attn, y, cos, sin, hq, hk, d, fuse_qkv)
     if attn_blocks is not None and attention.flash_supported(q, k):
         out = attention.flash_attention(q, k, v, cu, max_len, attn_blocks, scaling=attn.scaling, kblocks=attn_kblocks)
     else:
@@ -220,13 +234,14 @@ def _mlp_activation(mlp, y, fuse: bool, fuse_train: bool = False):
 def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor, cu_seqlens: torch.Tensor,
                    max_seqlen: int, attn_blocks: torch.Tensor = None, attn_kblocks: torch.Tensor = None,
                    multi_modal_inputs: list = None, fuse_mlp: bool = False,
-                   fuse_mlp_train: bool = False) -> torch.Tensor:
+                   fuse_mlp_train: bool = False, fuse_qkv: bool = False) -> torch.Tensor:
     """input_ids [T] and position_ids [T] (or [3, T], mrope) packed, cu_seqlens [B+1] int32 -> last
     hidden state [T, H] bf16 (after the final norm), i.e. Qwen2Model(...).last_hidden_state[0] on
     the same packing. ``fuse_mlp``: outside autograd, gate|up + SwiGLU run as one kernel
     (va_gate_up_swiglu; its GEMM sums in its own order, so the hidden states match the unfused
     forward to bf16 rounding, not bitwise). ``fuse_mlp_train``: under autograd, the same kernel also
-    writes the projection for the SwiGLU backward (va_gate_up_swiglu_save)."""
+    writes the projection for the SwiGLU backward (va_gate_up_swiglu_save). ``fuse_qkv``: the q|k|v
+    GEMM, its bias and RoPE as one kernel (va_qkv_rope), in both passes."""
     stack = text_backbone(backbone)
     cfg = stack.config
     hq = cfg.num_attention_heads
@@ -244,7 +259,8 @@ def packed_forward(backbone, input_ids: torch.Tensor, position_ids: torch.Tensor
             y = K.rmsnorm(residual, ln.weight, ln.variance_epsilon)
         else:
             residual, y = K.add_rmsnorm(h, residual, ln.weight, ln.variance_epsilon)
-        a = _attention(layer.self_attn, y, cos, sin, cu_seqlens, max_seqlen, hq, hk, d, attn_blocks, attn_kblocks)
+        a = _attention(layer.self_attn, y, cos, sin, cu_seqlens, max_seqlen, hq, hk, d, attn_blocks, attn_kblocks,
+                       fuse_qkv=fuse_qkv)
         ln = layer.post_attention_layernorm
         residual, y = K.add_rmsnorm(a, residual, ln.weight, ln.variance_epsilon)
         mlp = layer.mlp
