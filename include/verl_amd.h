@@ -164,6 +164,13 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *     dimension that is 128 mod 256 gets its last 128 rows / columns as 128 x 512 / 512 x 128 tiles.
  *   VA_TUNE_WGRAD_MFMA (va_weight_grad): 32 (default) = 32x32x16 MFMA blocks; 16 = 16x16x32 blocks
  *     (same tiles and staging; results differ only in the MFMA's internal summation order).
+ *   VA_TUNE_WGRAD_TILES (va_weight_grad): 3 (default), 2, 1 = one launch whose tile shape (256 x 256,
+ *     or 256 x 224 / 224 x 256 / 128 x 448 / 448 x 128, which divide 896 exactly) and K-slice count
+ *     are chosen by a cost model (rounds of 256 workgroups x tile area x steps + the split-K reduce),
+ *     16x16x32 MFMA blocks; 2 / 3 read each step's fragments one step ahead (two register sets),
+ *     3 also spreads the LDS-DMA between the MFMAs; 0 = 256 x 256 tiles (+ VA_TUNE_WGRAD_REMAINDER)
+ *     with the round-4 slice rule. Results differ only in the fp32 summation order of the slices
+ *     and the MFMA blocks.
  *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
 *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order);
  *   VA_TUNE_FLASH_DMA (va_flash_attn_fwd / _bwd): bit 1 = forward K / V blocks staged by LDS-DMA
@@ -189,6 +196,7 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_WGRAD_REMAINDER 18
 #define VA_TUNE_FLASH_DMA 19
 #define VA_TUNE_WGRAD_MFMA 20
+#define VA_TUNE_WGRAD_TILES 21
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------
@@ -420,7 +428,7 @@ int va_transpose_16(const void *in, int64_t ld_in, int64_t R, int64_t C, void *o
  * automatic; fp32 partials in workspace = va_weight_grad_workspace_bytes(K, M, N, splits), summed in
  * slice order, rounded once). workspace_bytes: the size of the buffer passed (ABI 6): the launch
  * plans its tiles and slices once and fails with VA_E_ARG when that plan needs more than this (the
- * plan depends on VA_TUNE_WGRAD_REMAINDER, which may change between the size query and the launch).
+ * plan depends on VA_TUNE_WGRAD_TILES / _REMAINDER, which may change between the size query and the launch).
  * Not a §8 row. */
 int64_t va_weight_grad_workspace_bytes(int64_t K, int64_t M, int64_t N, int splits);
 /* column_sum: out [C] bf16 = sum over the T rows of x [T, C] bf16 (row stride ld), fp32 accumulation in

@@ -38,3 +38,28 @@ def test_flash_block_tables(lens):
     k = [tuple(x) for x in A.flash_key_block_table(cu).tolist()]
     assert q == sorted(want, key=lambda t: (-t[1], t[0]))
     assert k == sorted(want, key=lambda t: (t[1], t[0]))
+
+
+@pytest.mark.parametrize("M,N,T", [(9728, 896, 151552), (896, 4864, 151552), (1152, 896, 151552), (896, 896, 151552),
+                                   (151936, 896, 131072), (9504, 896, 131072), (200, 136, 1024), (264, 512, 96),
+                                   (37888, 3584, 65536), (256, 256, 32)])
+@pytest.mark.parametrize("splits", [0, 3])
+def test_own_wgrad_plan_mirrors_the_library(M, N, T, splits):
+    """kernels.own_wgrad_plan (host mirror of w_plan_tiles) gives the slice count the library plans:
+    its workspace query (host code, no GPU) is 4 B x slices x M x N when slices > 1."""
+    from verl_amd import _lib as L
+
+    kind, s = K.own_wgrad_plan(M, N, T, splits)
+    assert kind in K.WGRAD_TILE_KINDS and 1 <= s
+    if splits:
+        assert s == splits
+    nb = L.load().va_weight_grad_workspace_bytes(T, M, N, splits)
+    assert nb == (4 * s * M * N if s > 1 else 0)
+
+
+def test_own_wgrad_plan_uses_896_dividing_tiles():
+    """The bench's backbone and lm_head shapes (H = 896) get tiles with no padded MFMA work."""
+    for M, N in [(9728, 896), (896, 4864), (1152, 896), (896, 896), (151936, 896)]:
+        kind, s = K.own_wgrad_plan(M, N, 151552 if M < 100000 else 131072)
+        tm, tn = K.WGRAD_TILE_KINDS[kind]
+        assert (-(-M // tm) * tm) * (-(-N // tn) * tn) <= M * N * 1.01, (M, N, kind)

@@ -126,11 +126,17 @@ def test_actor_fused_no_grad_logprob_matches_unfused():
                            dense_responses=False, min_response=5, seed=4, device=DEV)
     data.meta_info.update(micro_batch_size=4, temperature=0.9, use_dynamic_bsz=False)
     out = {}
-    for fused, after, concat in ((False, True, False), (True, True, False), (True, False, False), (True, True, True)):
+    for fused, after, concat, group_bytes in ((False, True, False, 2 << 30), (True, True, False, 2 << 30),
+                                              (True, False, False, 2 << 30), (True, True, True, 2 << 30),
+                                              (True, True, False, 1)):
         m = copy.deepcopy(base)
         a = DataParallelPPOActor(actor_config(use_remove_padding=True, fused_logprob_no_grad=fused,
-                                              fused_lm_head_after_backbone=after, fused_lm_head_concat=concat), m,
+                                              fused_lm_head_after_backbone=after, fused_lm_head_concat=concat,
+                                              fused_lm_head_group_bytes=group_bytes), m,
                                  torch.optim.SGD(m.parameters(), lr=0.0))
+        if group_bytes == 1:  # every micro-batch its own group (hidden states freed per group)
+            out["per_group"] = a.compute_log_prob(data, calculate_entropy=True)
+            continue
         out[fused, after, concat] = a.compute_log_prob(data, calculate_entropy=True)
         if not concat:
             out[fused, after] = out[fused, after, concat]
@@ -138,6 +144,7 @@ def test_actor_fused_no_grad_logprob_matches_unfused():
     assert torch.allclose(out[True, True][0][msk], out[False, True][0][msk], atol=4e-2)
     assert torch.allclose(out[True, True][1][msk], out[False, True][1][msk], atol=5e-3)
     assert torch.equal(out[True, True][0], out[True, False][0]) and torch.equal(out[True, True][1], out[True, False][1])
+    assert torch.equal(out[True, True][0], out["per_group"][0]) and torch.equal(out[True, True][1], out["per_group"][1])
     # one launch over both micro-batches' rows: within fp32 rounding of the vocab-range merge
     for i in range(2):
         a, b = out[True, True, True][i][msk], out[True, True, False][i][msk]

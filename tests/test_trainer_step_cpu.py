@@ -155,31 +155,36 @@ def test_attention_mask_host_copy_reuse_and_invalidation():
     assert DataParallelPPOActor._mask_host(me, other, refresh=True) is not a3  # refresh copies
 
 
-def test_attention_mask_host_mirror_is_used_until_either_tensor_is_written():
-    """DataProto.to(cuda) keeps the host tensor the mask came from (protocol.HOST_MIRRORED_KEY);
-    _mask_host plans from it instead of a device->host copy, but not once either side was
-    written in place (emulated here on host tensors: the mirror attribute is what .to sets)."""
+def test_attention_mask_host_mirror_is_used_until_the_device_tensor_is_written():
+    """DataProto.to(cuda) keeps a private host clone of the mask it moved (protocol.HOST_MIRRORED_KEY);
+    _mask_host plans from it instead of a device->host copy, but not once the device tensor was
+    written in place. Writes to the caller's host tensor after the move (through numpy views or a
+    reused loader buffer, which bump no version) cannot reach the clone. Emulated on host
+    tensors: the mirror attribute is what .to sets."""
     from types import SimpleNamespace
 
+    from verl_amd.protocol import HOST_MIRRORED_KEY, DataProto
     from verl_amd.workers.actor.dp_actor import DataParallelPPOActor
 
     me = SimpleNamespace(_am_cache=None)
     src = torch.ones(3, 5, dtype=torch.int64)
     dev = torch.ones(3, 5, dtype=torch.int64)  # stands in for the device copy
-    dev._va_host_mirror = (src, src._version, dev._version)
-    src_np = src.numpy()
+    mirror = src.clone()
+    dev._va_host_mirror = (mirror, dev._version)
     got = DataParallelPPOActor._mask_host(me, dev)
-    assert np.shares_memory(got, src_np)  # the mirror itself, no copy
+    assert np.shares_memory(got, mirror.numpy())  # the mirror itself, no copy
+    src.numpy()[1, 1] = 0  # the caller's buffer reused after the move: the clone still holds the moved mask
+    me._am_cache = None
+    got = DataParallelPPOActor._mask_host(me, dev)
+    assert got[1, 1] == 1
     me._am_cache = None
     dev[0, 0] = 0  # the device side changed: the mirror is stale
     got = DataParallelPPOActor._mask_host(me, dev)
-    assert not np.shares_memory(got, src_np) and got[0, 0] == 0
-    me._am_cache = None
-    dev2 = torch.ones(3, 5, dtype=torch.int64)
-    dev2._va_host_mirror = (src, src._version, dev2._version)
-    src[1, 1] = 0  # the host side changed after the move
-    got = DataParallelPPOActor._mask_host(me, dev2)
-    assert not np.shares_memory(got, src.numpy()) and got[1, 1] == 1
+    assert not np.shares_memory(got, mirror.numpy()) and got[0, 0] == 0
+    # DataProto.to only mirrors a host -> device move, and then as a clone
+    d = DataProto.from_dict({HOST_MIRRORED_KEY: torch.ones(2, 4, dtype=torch.int64)})
+    d.to("cpu")
+    assert getattr(d.batch[HOST_MIRRORED_KEY], "_va_host_mirror", None) is None
 
 
 def test_device_metrics_mapping_and_callbacks(capsys):

@@ -23,6 +23,27 @@ def _call(dy, x, splits):
     return out
 
 
+class _tuning:
+    """va_set_tuning values for the body of a with-block, restored to the library defaults after."""
+
+    DEFAULTS = {"VA_TUNE_WGRAD_TILES": 3, "VA_TUNE_WGRAD_REMAINDER": 0, "VA_TUNE_WGRAD_MFMA": 32}
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        from verl_amd import _lib as L
+
+        for k, v in self.kw.items():
+            L.call("va_set_tuning", getattr(L, k), v)
+
+    def __exit__(self, *exc):
+        from verl_amd import _lib as L
+
+        for k in self.kw:
+            L.call("va_set_tuning", getattr(L, k), self.DEFAULTS[k])
+
+
 def _ref(dy, x):
     return torch.mm(dy.t().float(), x.float())
 
@@ -36,22 +57,19 @@ def _check(got, want):
 @pytest.mark.parametrize("T,M,N", [(2048, 1152, 896), (4096, 896, 4864), (1024, 200, 136), (96, 264, 512),
                                    (2048, 9728, 896), (1024, 384, 640), (1024, 896, 896)])
 @pytest.mark.parametrize("splits", [0, 1, 3, 8])
-@pytest.mark.parametrize("remainder", [0, 1])
-def test_weight_grad_matches_fp32_reference(T, M, N, splits, remainder):
-    """splits 0 = automatic; with VA_TUNE_WGRAD_REMAINDER = 1 (both settings run here) a dimension that
-    is 128 mod 256 (896, 640, 384) gets 512 x 128 / 128 x 512 remainder tiles, and explicit splits
-    apply only when there is no remainder."""
-    from verl_amd import _lib as L
-
+@pytest.mark.parametrize("tiles,remainder", [(0, 0), (0, 1), (1, 0), (2, 0), (3, 0)])
+def test_weight_grad_matches_fp32_reference(T, M, N, splits, tiles, remainder):
+    """splits 0 = automatic. VA_TUNE_WGRAD_TILES 0: 256 x 256 tiles, and with VA_TUNE_WGRAD_REMAINDER
+    = 1 a dimension that is 128 mod 256 (896, 640, 384) gets 512 x 128 / 128 x 512 remainder tiles
+    (explicit splits apply only when there is no remainder); 1 / 2: the cost-model planner's tile
+    kinds (256 x 224, 224 x 256, 128 x 448, 448 x 128 for dimensions that are multiples of 224),
+    without / with the cross-step fragment pipeline (3: its LDS-DMA spread between the MFMAs)."""
     g = torch.Generator(device=DEV).manual_seed(T + M + N)
     dy = (torch.randn(T, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
     x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
-    try:
-        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, remainder)
+    with _tuning(VA_TUNE_WGRAD_TILES=tiles, VA_TUNE_WGRAD_REMAINDER=remainder):
         got = _call(dy, x, splits)
         again = _call(dy, x, splits)
-    finally:
-        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, 0)
     assert not torch.isnan(got.float()).any()
     _check(got, _ref(dy, x))
     assert torch.equal(got, again)  # deterministic
@@ -93,18 +111,14 @@ def test_product_dispatch_uses_it_and_falls_back():
 def test_remainder_tiles_match_full_tiles(T, M, N):
     """VA_TUNE_WGRAD_REMAINDER 0 (256 x 256 tiles throughout) and 1 (remainder tiles) agree to fp32
     summation order: both within the bf16 tolerance of the reference."""
-    from verl_amd import _lib as L
-
     g = torch.Generator(device=DEV).manual_seed(M + N)
     dy = (torch.randn(T, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
     x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
     want = _ref(dy, x)
-    full = _call(dy, x, 0)
-    try:
-        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, 1)
+    with _tuning(VA_TUNE_WGRAD_TILES=0):
+        full = _call(dy, x, 0)
+    with _tuning(VA_TUNE_WGRAD_TILES=0, VA_TUNE_WGRAD_REMAINDER=1):
         rem = _call(dy, x, 0)
-    finally:
-        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, 0)
     _check(full, want)
     _check(rem, want)
 
@@ -117,24 +131,17 @@ def test_weight_grad_16x16x32_form(T, M, N, splits, remainder):
     """VA_TUNE_WGRAD_MFMA = 16 (8 x 4 v_mfma_f32_16x16x32_bf16 blocks per wave, the 8-row image
     swizzle): the fp32 reference's tolerance, deterministic, and on exact-arithmetic operands (small
     integers: every partial sum exact) bitwise equal to the 32x32x16 form."""
-    from verl_amd import _lib as L
-
     g = torch.Generator(device=DEV).manual_seed(T + M + N + 1)
     dy = (torch.randn(T, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
     x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
     dyi = torch.randint(-3, 4, (T, M), device=DEV, generator=g).to(torch.bfloat16)
     xi = torch.randint(-3, 4, (T, N), device=DEV, generator=g).to(torch.bfloat16)
-    try:
-        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, remainder)
-        L.call("va_set_tuning", L.VA_TUNE_WGRAD_MFMA, 16)
+    with _tuning(VA_TUNE_WGRAD_TILES=0, VA_TUNE_WGRAD_REMAINDER=remainder, VA_TUNE_WGRAD_MFMA=16):
         got = _call(dy, x, splits)
         again = _call(dy, x, splits)
         exact16 = _call(dyi, xi, splits)
-        L.call("va_set_tuning", L.VA_TUNE_WGRAD_MFMA, 32)
+    with _tuning(VA_TUNE_WGRAD_TILES=0, VA_TUNE_WGRAD_REMAINDER=remainder):
         exact32 = _call(dyi, xi, splits)
-    finally:
-        L.call("va_set_tuning", L.VA_TUNE_WGRAD_REMAINDER, 0)
-        L.call("va_set_tuning", L.VA_TUNE_WGRAD_MFMA, 32)
     assert not torch.isnan(got.float()).any()
     _check(got, _ref(dy, x))
     assert torch.equal(got, again)
@@ -147,3 +154,52 @@ def test_weight_grad_mfma_setting_is_checked():
 
     with pytest.raises(RuntimeError, match="16 or 32"):
         L.call("va_set_tuning", L.VA_TUNE_WGRAD_MFMA, 8)
+
+
+@pytest.mark.parametrize("T,M,N", [(2048, 9728, 896), (2048, 896, 4864), (4096, 1152, 896), (4096, 896, 896),
+                                   (1024, 9504, 896), (1024, 448, 224), (1024, 200, 136), (512, 3584, 3584)])
+@pytest.mark.parametrize("splits", [0, 1, 2, 5])
+def test_tile_kinds_bitwise_on_exact_operands(T, M, N, splits):
+    """On exact-arithmetic operands (small integers: every partial and slice sum is exact in fp32) the
+    planner's tile kinds with and without the fragment pipeline (both DMA placements) give the same bits as the 256 x 256
+    tiles of the 32x32x16 form and as the fp32 reference rounded once; on random operands every
+    setting meets the reference's tolerance and repeats bitwise."""
+    g = torch.Generator(device=DEV).manual_seed(T * 7 + M + N)
+    dyi = torch.randint(-3, 4, (T, M), device=DEV, generator=g).to(torch.bfloat16)
+    xi = torch.randint(-3, 4, (T, N), device=DEV, generator=g).to(torch.bfloat16)
+    dy = (torch.randn(T, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
+    want = _ref(dy, x)
+    exact = {}
+    for tiles in (0, 1, 2, 3):
+        with _tuning(VA_TUNE_WGRAD_TILES=tiles):
+            exact[tiles] = _call(dyi, xi, splits)
+            got = _call(dy, x, splits)
+            assert torch.equal(got, _call(dy, x, splits))
+        _check(got, want)
+    assert all(torch.equal(exact[0], exact[t]) for t in (1, 2, 3))
+    assert torch.equal(exact[3].float(), _ref(dyi, xi).to(torch.bfloat16).float())
+
+
+def test_lm_head_weight_gradient_on_the_own_kernel():
+    """The lm_head's dW [V, H] = dlogits^T h (V = 151,936 > the backbone's tile cap) goes through
+    va_weight_grad in the product dispatch (256 x 224 tiles, K split by the cost model), within the
+    fp32 reference's tolerance, with a row stride > V (a [:, :V] view of a padded buffer)."""
+    from verl_amd import kernels as K
+
+    T, V, H = 1024, 151936, 896
+    g = torch.Generator(device=DEV).manual_seed(11)
+    buf = (torch.randn(T, V + 64, device=DEV, generator=g) * 1e-2).to(torch.bfloat16)
+    dy = buf[:, :V]
+    x = torch.randn(T, H, device=DEV, generator=g).to(torch.bfloat16)
+    assert K._OWN_LMHEAD_WGRAD
+    got = K.weight_grad(dy, x)
+    assert torch.equal(got, _call(dy, x, 0))
+    _check(got, _ref(dy, x))
+
+
+def test_weight_grad_tiles_setting_is_checked():
+    from verl_amd import _lib as L
+
+    with pytest.raises(RuntimeError, match="0, 1, 2 or 3"):
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_TILES, 4)

@@ -716,6 +716,7 @@ extern int g_whiten_slice_min;    // advantage.hip
 extern int g_linear_logprob_tile;  // linear_logprob.hip
 extern int g_wgrad_remainder;      // wgrad.hip
 extern int g_wgrad_mfma;           // wgrad.hip
+extern int g_wgrad_tiles;          // wgrad.hip
 extern int g_whiten_grid;         // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
 extern int g_flash_dkdv_qt;       // attention.hip
@@ -747,6 +748,13 @@ extern "C" int va_set_tuning(int key, int value) {
         return VA_E_ARG;
       }
       g_wgrad_mfma = value;
+      return VA_OK;
+    case VA_TUNE_WGRAD_TILES:
+      if (value < 0 || value > 3) {
+        va::set_error("va_set_tuning: VA_TUNE_WGRAD_TILES must be 0, 1, 2 or 3");
+        return VA_E_ARG;
+      }
+      g_wgrad_tiles = value;
       return VA_OK;
     case VA_TUNE_LINEAR_LOGPROB_TILE:
       if (value != 128 && value != 256) {

@@ -987,23 +987,55 @@ def own_wgrad_splits(n_out: int, n_in: int, tokens: int | None = None) -> int:
     return s
 
 
+# va_weight_grad's tile kinds (csrc/wgrad.hip, VA_TUNE_WGRAD_TILES >= 1): kind -> (rows, cols) of one
+# workgroup's output tile; 3-6 divide 896 = 4 x 224 = 2 x 448 exactly
+WGRAD_TILE_KINDS = {0: (256, 256), 3: (256, 224), 4: (224, 256), 5: (128, 448), 6: (448, 128)}
+
+
+def own_wgrad_plan(n_out: int, n_in: int, tokens: int, splits: int = 0) -> tuple:
+    """Host mirror of w_plan_tiles (csrc/wgrad.hip): the (kind, splits) with the least estimated time,
+    rounds of 256 workgroups x tile area x (steps per slice + 8) + 0.11 per output element and slice
+    + 2e5 for the split-K reduce; ties keep the earlier kind / fewer slices (1e-3 relative margin)."""
+    steps = tokens // 32
+    cap = min(max(steps // WGRAD_MIN_STEPS_PER_SLICE, 1), 256)
+    best, plan = None, None
+    for kind, (tm, tn) in WGRAD_TILE_KINDS.items():
+        lo, hi = (splits, splits) if splits > 0 else (1, min(cap, 64))
+        tiles = -(-n_out // tm) * -(-n_in // tn)
+        for sv in range(lo, hi + 1):
+            c = float(-(-tiles * sv // 256)) * float(tm * tn) * (float(-(-steps // sv)) + 8.0)
+            if sv > 1:
+                c += 0.11 * sv * float(n_out * n_in) + 2.0e5
+            if best is None or c < best * 0.999:
+                best, plan = c, (kind, sv)
+    return plan
+
+
 # the shape class it was measured on: outputs of at most one round of 256 x 256 tiles (the H = 896
 # backbone: 16-152 tiles), where hipBLASLt leaves CUs idle or splits K in batched fp32 GEMMs; larger
-# outputs (the 7B / 8B configs' 1,000+ tiles) keep hipBLASLt
+# backbone outputs (the 7B / 8B configs' 1,000+ tiles) keep hipBLASLt
 WGRAD_OWN_MAX_TILES = 256
+
+# the lm_head weight gradient (dW [V, H] = dlogits^T h, K = update-pass rows) through va_weight_grad:
+# its 256 x 224 / 128 x 448 tiles divide H = 896 exactly and the cost model splits K to even out the
+# last round of workgroups. VERL_AMD_LMHEAD_WGRAD=hipblaslt keeps the swapped hipBLASLt product (A/B)
+_OWN_LMHEAD_WGRAD = os.environ.get("VERL_AMD_LMHEAD_WGRAD", "own") != "hipblaslt"
 
 
 def _own_weight_grad(dy2, x2):
     """dY^T X by va_weight_grad, or None when the operands do not fit it (then hipBLASLt)."""
     T, n_out = dy2.shape
     n_in = x2.shape[1]
-    if -(-n_out // 256) * -(-n_in // 256) > WGRAD_OWN_MAX_TILES:
+    lm_head = n_out >= WGRAD_SWAP_MIN_OUT
+    if lm_head and not _OWN_LMHEAD_WGRAD:
+        return None
+    if not lm_head and -(-n_out // 256) * -(-n_in // 256) > WGRAD_OWN_MAX_TILES:
         return None
     if (not _OWN_WGRAD or not dy2.is_cuda or dy2.dtype != torch.bfloat16 or x2.dtype != torch.bfloat16
-            or T % 32 or n_out % 8 or n_in % 8 or n_out >= WGRAD_SWAP_MIN_OUT or dy2.stride(1) != 1
+            or T % 32 or n_out % 8 or n_in % 8 or n_out >= 2**30 or n_in >= 2**30 or dy2.stride(1) != 1
             or x2.stride(1) != 1 or dy2.stride(0) % 8 or x2.stride(0) % 8 or (dy2.data_ptr() | x2.data_ptr()) % 16):
         return None
-    s = 0  # automatic: va_weight_grad plans the tiles (remainder tiles for 896 = 3.5 x 256) and slices
+    s = 0  # automatic: va_weight_grad plans the tile shape and the K slices
     out = torch.empty(n_out, n_in, dtype=torch.bfloat16, device=dy2.device)
     nb = L.load().va_weight_grad_workspace_bytes(T, n_out, n_in, s)
     ws = torch.empty(nb // 4, dtype=torch.float32, device=dy2.device) if nb else None

@@ -327,9 +327,11 @@ class DataProto:
             for k, v in self.batch.items():
                 t = v.to(device, non_blocking=non_blocking)
                 if k == HOST_MIRRORED_KEY and t is not v and v.device.type == "cpu" and t.is_cuda:
-                    # the host copy the mask arrived with: the actor plans padding removal from it
-                    # instead of a device->host copy that would drain the stream (dp_actor._mask_host)
-                    t._va_host_mirror = (v, v._version, t._version)
+                    # a private host copy of the mask as it was moved: the actor plans padding removal
+                    # from it instead of a device->host copy that would drain the stream
+                    # (dp_actor._mask_host). A clone, not the caller's tensor: writes to that through
+                    # numpy views or a reused loader buffer do not bump its version
+                    t._va_host_mirror = (v.clone(), t._version)
                 moved[k] = t
             self.batch = TensorBatch(moved, batch_size=self.batch.batch_size)
         return self

@@ -301,6 +301,12 @@ class DataParallelPPOActor(BasePPOActor):
         # no-grad passes with the fused lm_head: run all micro-batches' backbones, then the lm_head
         # launches back to back (compute_log_prob)
         self.fused_lm_head_after_backbone = bool(self.config.get("fused_lm_head_after_backbone", True))
+        # ... in groups of micro-batches whose selected hidden states [n_sel, H] take at most this many
+        # bytes together (each group's lm_heads run once its backbones have, and its hidden states are
+        # freed then), so the pass holds a bounded amount beside the micro-batch being computed, as the
+        # reference's log_prob_micro_batch_size bounds it; the bench's 4 x 131,072 x 896
+        # bf16 rows (0.94 GB) are one group
+        self.fused_lm_head_group_bytes = int(self.config.get("fused_lm_head_group_bytes", 2 << 30))
         # ... and as ONE launch over the concatenated rows
         self.fused_lm_head_concat = bool(self.config.get("fused_lm_head_concat", False))
         # the fused kernel's logits: bf16-rounded like the unfused autocast path and the reference's
@@ -432,6 +438,33 @@ class DataParallelPPOActor(BasePPOActor):
         return K.linear_logprob_entropy(h_sel.to(torch.bfloat16), w if w.dtype == torch.bfloat16 else w.to(torch.bfloat16),
                                         labels, temperature, fp32_logits=self.fused_kernel_fp32_logits, splits=splits)
 
+    def _fused_lm_head_group(self, group: list, temperature, calculate_entropy: bool, lps: list, ents: list):
+        """The fused lm_head launches of a group of micro-batches whose backbones have run (``group``
+        = [(micro-batch, plan, h_sel, labels)], emptied here: each h_sel is released once its launch
+        is queued), back to back, or as one launch over the concatenated rows (fused_lm_head_concat,
+        with the vocab ranges a micro-batch's own launch would use: the same per-row bits for
+        equal-sized micro-batches); per-response log-probs / entropies appended to lps / ents."""
+        if self.fused_lm_head_concat and len(group) > 1:
+            sizes = [g[2].shape[0] for g in group]
+            lp_all, ent_all = self._fused_lm_head_logprob(
+                torch.cat([g[2] for g in group]), torch.cat([g[3] for g in group]), temperature,
+                splits=K._linear_logprob_splits(max(sizes)))
+            outs = list(zip(lp_all.split(sizes), ent_all.split(sizes), strict=True))
+            for g in group:
+                g[2] = None
+        else:
+            outs = []
+            for g in group:
+                outs.append(self._fused_lm_head_logprob(g[2], g[3], temperature))
+                g[2] = None
+        for (mb, plan, _, _), (lp_sel, ent_sel) in zip(group, outs, strict=True):
+            B, R = mb.batch["responses"].shape
+            ent, lp = _scatter_rows(lp_sel, ent_sel, plan, B, R, calculate_entropy)
+            lps.append(lp)
+            if calculate_entropy:
+                ents.append(ent)
+        group.clear()
+
     def _use_fused_lm_head(self) -> bool:
         head = self._lm_head
         if not isinstance(head, nn.Linear) or head.bias is not None:
@@ -443,8 +476,8 @@ class DataParallelPPOActor(BasePPOActor):
         the stream: at the start of a step it would leave the GPU idle while the host plans, and at
         the start of the update it would wait for the queued old-logp pass and advantage work. So,
         in this order:
-          * the host tensor the mask arrived with (DataProto.to of a host batch keeps it,
-            protocol.HOST_MIRRORED_KEY), while neither tensor has been written since;
+          * the host copy DataProto.to took of a host batch's mask (protocol.HOST_MIRRORED_KEY: a
+            clone only it holds), while the device tensor has not been written since;
           * the copy taken last, while the tensor is the same unmodified one (same storage, shape
             and in-place version: the step's compute_log_prob and update_policy, or the same batch
             again);
@@ -460,7 +493,7 @@ class DataParallelPPOActor(BasePPOActor):
         if not refresh and self._am_cache is not None and self._am_cache[0] == key:
             return self._am_cache[2]
         mirror = getattr(am_t, "_va_host_mirror", None)
-        if (not refresh and mirror is not None and mirror[0]._version == mirror[1] and am_t._version == mirror[2]
+        if (not refresh and mirror is not None and am_t._version == mirror[1]
                 and tuple(mirror[0].shape) == tuple(am_t.shape)):
             am = mirror[0].numpy()
         else:
@@ -536,28 +569,17 @@ class DataParallelPPOActor(BasePPOActor):
             # right after the backbone's power-capped GEMMs starts clocked down (33.1 ms alone, 34.9 ms
             # right after GEMM load, 33.4 ms per launch over 4 in a row; profiles/r05/f1_pre_gemm_load.jsonl),
             # so consecutive launches recover the clock. Per-row results are the same bits.
-            sel = []
             with torch.autocast(device_type=self.device_name, dtype=self.autocast_dtype or torch.bfloat16,
                                 enabled=self.autocast_dtype is not None):
-                for mb, plan in zip(micro_batches, plans, strict=True):
-                    sel.append(self._selected_hidden(mb.batch, plan, _multi_modal(mb)))
-                if self.fused_lm_head_concat and len(sel) > 1:
-                    # ONE launch over every micro-batch's rows, with the vocab ranges a micro-batch's
-                    # own launch would use (the same per-row bits for equal-sized micro-batches)
-                    sizes = [h.shape[0] for h, _ in sel]
-                    lp_all, ent_all = self._fused_lm_head_logprob(
-                        torch.cat([h for h, _ in sel]), torch.cat([lab for _, lab in sel]), temperature,
-                        splits=K._linear_logprob_splits(max(sizes)))
-                    outs = list(zip(lp_all.split(sizes), ent_all.split(sizes), strict=True))
-                else:
-                    outs = [self._fused_lm_head_logprob(h_sel, labels, temperature) for h_sel, labels in sel]
-                for mb, plan, (lp_sel, ent_sel) in zip(micro_batches, plans, outs, strict=True):
-                    B, R = mb.batch["responses"].shape
-                    ent, lp = _scatter_rows(lp_sel, ent_sel, plan, B, R, calculate_entropy)
-                    lps.append(lp)
-                    if calculate_entropy:
-                        ents.append(ent)
-            del sel
+                group, held = [], 0
+                for i, (mb, plan) in enumerate(zip(micro_batches, plans, strict=True)):
+                    h_sel, labels = self._selected_hidden(mb.batch, plan, _multi_modal(mb))
+                    held += h_sel.numel() * h_sel.element_size()
+                    group.append([mb, plan, h_sel, labels])
+                    h_sel = labels = None
+                    if held >= self.fused_lm_head_group_bytes or i == len(micro_batches) - 1:
+                        self._fused_lm_head_group(group, temperature, calculate_entropy, lps, ents)
+                        group, held = [], 0
         else:
             for mb, plan in zip(micro_batches, plans, strict=True):
                 ent, lp = self._forward_micro_batch(mb.batch, temperature, calculate_entropy, plan, _multi_modal(mb))
