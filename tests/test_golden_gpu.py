@@ -114,6 +114,61 @@ def test_headline_core_algos_512x1024():
     close(nd.grad, newr.grad.numpy(), 1e-6 * gm, 1e-4, "dlp 512x1024")
 
 
+def test_headline_dual_clip_lower_branch_512x1024_loss_micro_batches():
+    """the timed bench step (old = recomputed + N(0, 0.05^2)) fires the
+    dual-clip lower branch 0 times in 10.49M tokens, so here the bench's batch shape and loss
+    micro-batching (512 x 1,024, GRPO advantages of groups of 8, 64 segments of the reference's
+    ppo_micro_batch_size_per_gpu = 8 rows, token-mean each, k3 KL) with old = new + 0.5 N(0, 1): the
+    ratio passes clip_ratio_c = 3 on negative advantages (core_algos.py:785-791) for a few percent of
+    the tokens. Every segment's pg_loss, clipfrac, ppo_kl, clipfrac_lower and kl_loss and the
+    accumulated gradient d(sum_s loss_s / 64) / d log_prob against the oracle's 64 separate
+    micro-batch losses (dp_actor.py:419-470)."""
+    from verl_amd import kernels as K
+    from verl_amd.trainer.ppo import core_algos
+
+    g = torch.Generator().manual_seed(606)
+    B, R, S = 512, 1024, 8
+    lens = torch.randint(128, R + 1, (B,), generator=g)
+    mask = (torch.arange(R)[None, :] < lens[:, None]).long()
+    rewards = torch.zeros(B, R)
+    rewards[torch.arange(B), lens - 1] = torch.bernoulli(torch.full((B,), 0.5), generator=g)
+    uid = np.array([f"p{i // 8}" for i in range(B)], dtype=object)
+    adv, _ = ref.compute_grpo_outcome_advantage(rewards.clone(), mask, uid)
+    new = -torch.rand(B, R, generator=g) * 3
+    old = new + 0.5 * torch.randn(B, R, generator=g)
+    refl = new + 0.1 * torch.randn(B, R, generator=g)
+    nseg = B // S
+    newr = new.clone().requires_grad_(True)
+    want = []
+    total = 0.0
+    for i in range(nseg):
+        sl = slice(i * S, (i + 1) * S)
+        loss, met = ref.actor_loss(old[sl], newr[sl], adv[sl], mask[sl], clip_ratio=0.2, clip_ratio_c=3.0,
+                                   ref_log_prob=refl[sl], kl_loss_type="low_var_kl", kl_loss_coef=0.001,
+                                   grad_scale=1.0 / nseg)
+        total = total + loss
+        want.append([met["pg_loss"].item(), met["pg_clipfrac"].item(), met["ppo_kl"].item(),
+                     met["pg_clipfrac_lower"].item(), met["kl_loss"].item()])
+    total.backward()
+    want = np.asarray(want)
+    assert (want[:, 3] > 0).sum() >= nseg // 2, "the lower branch must fire in most segments"
+    nd = new.to(DEV).requires_grad_(True)
+    out = K.fused_policy_loss(old.to(DEV), nd, adv.to(DEV), mask.to(DEV), 0.2, 0.2, 3.0, "token-mean",
+                              ref_log_prob=refl.to(DEV), kl_loss_type="low_var_kl", seg_rows=S)
+    assert tuple(out.shape) == (nseg, 8)
+    ((out[:, 0] + 0.001 * out[:, 4]).sum() / nseg).backward()
+    got = out[:, [0, 1, 2, 3, 4]].detach().cpu().double().numpy()
+    clipped_lower_tokens = (got[:, 3] * out[:, 6].detach().cpu().double().numpy()).sum()
+    assert clipped_lower_tokens > 1000, clipped_lower_tokens
+    np.testing.assert_allclose(got[:, 0], want[:, 0], atol=1e-5, rtol=1e-4, err_msg="pg_loss per segment")
+    np.testing.assert_allclose(got[:, 1], want[:, 1], atol=1e-6, rtol=1e-6, err_msg="clipfrac")
+    np.testing.assert_allclose(got[:, 3], want[:, 3], atol=1e-6, rtol=1e-6, err_msg="clipfrac_lower")
+    np.testing.assert_allclose(got[:, 2], want[:, 2], atol=1e-6, rtol=1e-4, err_msg="ppo_kl")
+    np.testing.assert_allclose(got[:, 4], want[:, 4], atol=1e-6, rtol=1e-4, err_msg="kl_loss")
+    gm = newr.grad.abs().max().item()
+    close(nd.grad, newr.grad.numpy(), 1e-6 * gm, 1e-4, "accumulated dlp with the lower branch")
+
+
 def test_headline_logprob_micro_batch_8x1024x151936():
     """A full update micro-batch of logits (8 x 1024 rows x 151,936 bf16 = 2.5 GB): oracle on 64
     sampled rows; on all rows the size-independent invariants logp <= 0, 0 <= H <= log V, and

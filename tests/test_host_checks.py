@@ -63,3 +63,21 @@ def test_own_wgrad_plan_uses_896_dividing_tiles():
         kind, s = K.own_wgrad_plan(M, N, 151552 if M < 100000 else 131072)
         tm, tn = K.WGRAD_TILE_KINDS[kind]
         assert (-(-M // tm) * tm) * (-(-N // tn) * tn) <= M * N * 1.01, (M, N, kind)
+
+
+def test_qkv_rope_rejects_mismatched_operands():
+    """va_qkv_rope takes H from x and its rows from the head counts, so the wrappers check
+    that the weight, bias and cos / sin tables describe one merged projection (host-side, no GPU)."""
+    import torch
+
+    T, H, hq, hk, d = 32, 128, 2, 1, 64
+    x = torch.zeros(T, H, dtype=torch.bfloat16)
+    w = torch.zeros((hq + 2 * hk) * d, H, dtype=torch.bfloat16)
+    b = torch.zeros((hq + 2 * hk) * d, dtype=torch.bfloat16)
+    c = torch.zeros(T, d, dtype=torch.bfloat16)
+    assert K._qkv_rope_shape_error(x, w, b, c, c, hq, hk, d) is None
+    assert "input dimension" in K._qkv_rope_shape_error(x, w[:, :64], b, c, c, hq, hk, d)
+    assert "rows" in K._qkv_rope_shape_error(x, w[:-64], b, c, c, hq, hk, d)
+    assert "b_all" in K._qkv_rope_shape_error(x, w, b[:-1], c, c, hq, hk, d)
+    assert "sin" in K._qkv_rope_shape_error(x, w, b, c, c[:-1], hq, hk, d)
+    assert not K.qkv_rope_supported(x, w[:-64], b, c, d, hq, hk, c)

@@ -1140,8 +1140,28 @@ class _RoPEQKV(torch.autograd.Function):
         return dqkv, None, None, None, None, None
 
 
-def qkv_rope_supported(x, w_all, b_all, cos, head_dim: int) -> bool:
-    """Shapes / layouts va_qkv_rope takes (bf16 on the device, head_dim 64, H % 64 == 0)."""
+def _qkv_rope_shape_error(x, w_all, b_all, cos, sin, num_q_heads, num_kv_heads, head_dim: int):
+    """Why the operands do not describe one merged q|k|v projection (None if they do): the kernel takes
+    H from x and its output rows from the head counts, so a mismatched weight, bias or cos / sin table
+    would be read out of bounds."""
+    if x.dim() != 2 or w_all.dim() != 2 or w_all.shape[1] != x.shape[1]:
+        return f"x {tuple(x.shape)} and w_all {tuple(w_all.shape)} do not share the input dimension"
+    if num_q_heads is not None and w_all.shape[0] != (num_q_heads + 2 * num_kv_heads) * head_dim:
+        return f"w_all has {w_all.shape[0]} rows, not ({num_q_heads} + 2 x {num_kv_heads}) x {head_dim}"
+    if b_all is not None and b_all.numel() != w_all.shape[0]:
+        return f"b_all has {b_all.numel()} elements for {w_all.shape[0]} rows"
+    for name, t in (("cos", cos), ("sin", sin)):
+        if t is not None and t.numel() != x.shape[0] * head_dim:
+            return f"{name} has {t.numel()} elements, not T x head_dim = {x.shape[0]} x {head_dim}"
+    return None
+
+
+def qkv_rope_supported(x, w_all, b_all, cos, head_dim: int, num_q_heads: int | None = None,
+                       num_kv_heads: int | None = None, sin=None) -> bool:
+    """Shapes / layouts va_qkv_rope takes (bf16 on the device, head_dim 64, H % 64 == 0, the operands of
+    one merged projection: _qkv_rope_shape_error)."""
+    if _qkv_rope_shape_error(x, w_all, b_all, cos, sin, num_q_heads, num_kv_heads, head_dim) is not None:
+        return False
     return (head_dim == 64 and x.is_cuda and x.dtype == w_all.dtype == torch.bfloat16 and x.dim() == 2
             and x.shape[1] % 64 == 0 and x.stride(-1) == 1 and w_all.stride(-1) == 1 and x.stride(0) % 8 == 0
             and w_all.stride(0) % 8 == 0 and x.stride(0) < (1 << 22) and w_all.stride(0) < (1 << 22)
@@ -1210,6 +1230,9 @@ def qkv_rope(x, w_all, b_all, cos, sin, num_q_heads: int, num_kv_heads: int, hea
     kernel (va_qkv_rope); gradients to ``weights`` / ``biases`` (views into w_all / b_all) under autograd."""
     _require_device(x, w_all, cos, sin)
     _bf16_only(x, w_all, cos, sin)
+    err = _qkv_rope_shape_error(x, w_all, b_all, cos, sin, num_q_heads, num_kv_heads, head_dim)
+    if err is not None:
+        raise ValueError(f"qkv_rope: {err}")
     T = x.shape[0]
     c, s = cos.reshape(T, head_dim).contiguous(), sin.reshape(T, head_dim).contiguous()
     params = list(weights) + (list(biases) if biases else [])

@@ -243,18 +243,22 @@ class PPOTrainerStep:
                 num_repeat=cfg.actor_rollout_ref.rollout.n,
                 norm_adv_by_std_in_grpo=cfg.algorithm.get("norm_adv_by_std_in_grpo", True), config=cfg.algorithm)
 
-        step_metrics: dict = {}
+        # the updates' metrics (dp_actor.DeviceMetrics: an asynchronous device -> host copy) stay unread
+        # until both updates are queued, so reading the critic's does not hold back the actor update
+        # (ADVICE r5); they are read below, before the step's one metric reduction
+        pending = []
         if self.use_critic:  # :1307-1312
             with timer.section("update_critic"):
                 critic_out = self.critic.update_critic(batch)
-            step_metrics.update(critic_out.meta_info["metrics"])
+            pending.append(critic_out.meta_info["metrics"])
         if cfg.trainer.get("critic_warmup", 0) <= self.global_steps:  # :1314-1320
             batch.meta_info["multi_turn"] = False
             with timer.section("update_actor"):
                 actor_out = self.actor.update_actor(batch)
-            step_metrics.update(actor_out.meta_info["metrics"])
+            pending.append(actor_out.meta_info["metrics"])
         host = {k: [float(v.item())] if isinstance(v, torch.Tensor) else [v] for k, v in metrics.items()}
-        host.update({k: (v if isinstance(v, list) else [v]) for k, v in step_metrics.items()})
+        for step_metrics in pending:
+            host.update({k: (v if isinstance(v, list) else [v]) for k, v in step_metrics.items()})
         timing_raw = timer.read()
         out = reduce_metrics_dp(host, self.group)
         # the driver's metrics after the step (ray_trainer.py:1380-1390)

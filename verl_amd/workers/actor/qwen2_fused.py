@@ -197,7 +197,7 @@ def _qkv(attn, y, cos, sin, hq, hk, d, fuse: bool):
         w_all = _merged(attn, "qkv.w", ws)
         bs = [lin.bias for lin in lins] if lins[0].bias is not None else None
         b_all = _merged(attn, "qkv.b", bs) if bs else None
-        if K.qkv_rope_supported(y, w_all, b_all, cos, d):
+        if K.qkv_rope_supported(y, w_all, b_all, cos, d, hq, hk, sin):
             return K.qkv_rope(y, w_all, b_all, cos, sin, hq, hk, d, ws, bs)
     qkv = _merged_linear(attn, "qkv", y, lins)
     return K.rope_qkv(qkv, cos, sin, hq, hk, d)

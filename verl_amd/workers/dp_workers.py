@@ -176,8 +176,10 @@ class ActorWorker:
         span.stop()
         epochs = self.config.actor.get("ppo_epochs", 1)
         metrics.update(perf_metrics(self.flops_counter, data, span.host_seconds(), epochs, self.world_size, "actor"))
-        metrics.add_on_ready(lambda m: m.__setitem__("perf/mfu/actor", perf_metrics(
-            self.flops_counter, data, span.seconds(), epochs, self.world_size, "actor", memory=False)["perf/mfu/actor"]))
+        # the callback holds the token counts only, not the batch
+        tokens, share = token_share(data, self.world_size)
+        fc = self.flops_counter
+        metrics.add_on_ready(lambda m: m.__setitem__("perf/mfu/actor", mfu(fc, tokens, share, span.seconds(), epochs)))
         metrics["actor/lr"] = self.actor_lr_scheduler.get_last_lr()[0]
         self.actor_lr_scheduler.step()
         return DataProto(meta_info={"metrics": metrics})
@@ -241,8 +243,9 @@ class CriticWorker:
         epochs = self.config.get("ppo_epochs", 1)
         metrics["perf/mfu/critic"] = perf_metrics(self.flops_counter, data, span.host_seconds(), epochs,
                                                   self.world_size, "critic", memory=False)["perf/mfu/critic"]
-        metrics.add_on_ready(lambda m: m.__setitem__("perf/mfu/critic", perf_metrics(
-            self.flops_counter, data, span.seconds(), epochs, self.world_size, "critic", memory=False)["perf/mfu/critic"]))
+        tokens, share = token_share(data, self.world_size)
+        fc = self.flops_counter
+        metrics.add_on_ready(lambda m: m.__setitem__("perf/mfu/critic", mfu(fc, tokens, share, span.seconds(), epochs)))
         metrics["critic/lr"] = self.critic_lr_scheduler.get_last_lr()[0]
         self.critic_lr_scheduler.step()
         return DataProto(meta_info={"metrics": metrics})
@@ -282,6 +285,20 @@ class _UpdateSpan:
         return self.ev[0].elapsed_time(self.ev[1]) / 1e3
 
 
+def token_share(data: DataProto, world_size: int) -> tuple:
+    """(per-sequence valid token counts, divisor) for the MFU: the whole batch's ``global_token_num``
+    over the world size, or this rank's own attention mask undivided (see perf_metrics)."""
+    tokens = data.meta_info.get("global_token_num")
+    if tokens is None:
+        return data.batch["attention_mask"].sum(-1).tolist(), 1
+    return tokens, world_size
+
+
+def mfu(flops_counter, tokens, share: int, delta_time: float, ppo_epochs: int) -> float:
+    est, promised = flops_counter.estimate_flops(tokens, delta_time)
+    return est * ppo_epochs / promised / share
+
+
 def perf_metrics(flops_counter, data: DataProto, delta_time: float, ppo_epochs: int, world_size: int,
                  role: str, memory: bool = True) -> dict:
     """fsdp_workers.py:690-697: MFU of one update (estimated FLOP/s x epochs / promised / world)
@@ -292,13 +309,8 @@ def perf_metrics(flops_counter, data: DataProto, delta_time: float, ppo_epochs: 
     stands in, and then the FLOPs are already this rank's share: no division."""
     import psutil
 
-    tokens = data.meta_info.get("global_token_num")
-    share = world_size
-    if tokens is None:
-        tokens = data.batch["attention_mask"].sum(-1).tolist()
-        share = 1
-    est, promised = flops_counter.estimate_flops(tokens, delta_time)
-    out = {f"perf/mfu/{role}": est * ppo_epochs / promised / share}
+    tokens, share = token_share(data, world_size)
+    out = {f"perf/mfu/{role}": mfu(flops_counter, tokens, share, delta_time, ppo_epochs)}
     if not memory:
         return out
     if torch.cuda.is_available():
