@@ -57,13 +57,14 @@ def _check(got, want):
 @pytest.mark.parametrize("T,M,N", [(2048, 1152, 896), (4096, 896, 4864), (1024, 200, 136), (96, 264, 512),
                                    (2048, 9728, 896), (1024, 384, 640), (1024, 896, 896)])
 @pytest.mark.parametrize("splits", [0, 1, 3, 8])
-@pytest.mark.parametrize("tiles,remainder", [(0, 0), (0, 1), (1, 0), (2, 0), (3, 0)])
+@pytest.mark.parametrize("tiles,remainder", [(0, 0), (0, 1), (1, 0), (2, 0), (3, 0), (4, 0)])
 def test_weight_grad_matches_fp32_reference(T, M, N, splits, tiles, remainder):
     """splits 0 = automatic. VA_TUNE_WGRAD_TILES 0: 256 x 256 tiles, and with VA_TUNE_WGRAD_REMAINDER
     = 1 a dimension that is 128 mod 256 (896, 640, 384) gets 512 x 128 / 128 x 512 remainder tiles
     (explicit splits apply only when there is no remainder); 1 / 2: the cost-model planner's tile
     kinds (256 x 224, 224 x 256, 128 x 448, 448 x 128 for dimensions that are multiples of 224),
-    without / with the cross-step fragment pipeline (3: its LDS-DMA spread between the MFMAs)."""
+    without / with the cross-step fragment pipeline (3: its LDS-DMA spread between the MFMAs; 4: its
+    fragment reads too)."""
     g = torch.Generator(device=DEV).manual_seed(T + M + N)
     dy = (torch.randn(T, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
     x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
@@ -171,13 +172,13 @@ def test_tile_kinds_bitwise_on_exact_operands(T, M, N, splits):
     x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
     want = _ref(dy, x)
     exact = {}
-    for tiles in (0, 1, 2, 3):
+    for tiles in (0, 1, 2, 3, 4):
         with _tuning(VA_TUNE_WGRAD_TILES=tiles):
             exact[tiles] = _call(dyi, xi, splits)
             got = _call(dy, x, splits)
             assert torch.equal(got, _call(dy, x, splits))
         _check(got, want)
-    assert all(torch.equal(exact[0], exact[t]) for t in (1, 2, 3))
+    assert all(torch.equal(exact[0], exact[t]) for t in (1, 2, 3, 4))
     assert torch.equal(exact[3].float(), _ref(dyi, xi).to(torch.bfloat16).float())
 
 
@@ -201,5 +202,5 @@ def test_lm_head_weight_gradient_on_the_own_kernel():
 def test_weight_grad_tiles_setting_is_checked():
     from verl_amd import _lib as L
 
-    with pytest.raises(RuntimeError, match="0, 1, 2 or 3"):
-        L.call("va_set_tuning", L.VA_TUNE_WGRAD_TILES, 4)
+    with pytest.raises(RuntimeError, match="0 .. 4"):
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_TILES, 5)

@@ -10,7 +10,7 @@
 #   tests:<pytest args>   a subset, e.g. "tests:tests/test_weight_grad_gpu.py -k tile" -> pytest_<n>.log
 #   smoke                 __graft_entry__.smoke()          -> smoke.log
 #   bench[:<tag>[:<args>]] bench.py as the driver runs it (+ args) -> bench_<tag>.json / .log
-#   rocprof[:<tag>]       the bench command under rocprofv3 --kernel-trace --stats -> kernel_stats_<tag>*,
+#   rocprof[:<tag>[:<args>]] the bench command (+ args) under rocprofv3 --kernel-trace --stats -> kernel_stats_<tag>*,
 #                         trace_gaps_<tag>.txt, bench_under_rocprof_<tag>.json
 #   pmc_f1                tools/f1_pmc.sh                  -> pmc_f1_product.json
 #   tool:<script> <args>  python tools/<script> <args>     -> <script stem>[_<n>].jsonl
@@ -55,8 +55,9 @@ for step in "$@"; do
       echo "# cmd: python bench.py --out $O/bench_$tag.json $args" > "$O/bench_$tag.json.cmd"
       python -c "import json;d=json.load(open('$O/bench_$tag.json'));r=d['roofline'];print('bench $tag', d['value'], d['ms_per_step'], r['kernel'], r['frac'], d.get('config',{}).get('peak_hbm_gb'))" ;;
     rocprof*)
-      tag=${step#rocprof}; tag=${tag#:}; tag=${tag:-headline}
-      run 600 "$O/bench_prof_$tag.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$tag" -o "$tag" -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --out "$O/bench_under_rocprof_$tag.json"
+      IFS=: read -r _ tag args <<< "$step"; tag=${tag:-headline}
+      # shellcheck disable=SC2086
+      run 600 "$O/bench_prof_$tag.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$tag" -o "$tag" -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --out "$O/bench_under_rocprof_$tag.json" $args
       st=$(find "$O/prof_$tag" -name "*kernel_stats.csv" | head -1)
       kt=$(find "$O/prof_$tag" -name "*kernel_trace.csv" | head -1)
       { echo "# cmd: rocprofv3 --kernel-trace --stats -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline; python tools/prof_summary.py"; python tools/prof_summary.py "$st"; } > "$O/kernel_stats_${tag}_summary.txt"

@@ -750,8 +750,8 @@ extern "C" int va_set_tuning(int key, int value) {
       g_wgrad_mfma = value;
       return VA_OK;
     case VA_TUNE_WGRAD_TILES:
-      if (value < 0 || value > 3) {
-        va::set_error("va_set_tuning: VA_TUNE_WGRAD_TILES must be 0, 1, 2 or 3");
+      if (value < 0 || value > 4) {
+        va::set_error("va_set_tuning: VA_TUNE_WGRAD_TILES must be 0 .. 4");
         return VA_E_ARG;
       }
       g_wgrad_tiles = value;

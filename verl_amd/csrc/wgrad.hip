@@ -424,17 +424,43 @@ __global__ __launch_bounds__(WNT, 1) void wgrad_kernel(const uint16_t *__restric
     constexpr int NM = NA * NB, G = NM / (PER + 1);
     // PIPE 1: the DMA right after the barrier, ahead of the reads (its own scheduling region);
     // PIPE 2: between the MFMAs, PER pieces in gaps of G MFMAs (sched_group_barrier)
+    // PIPE 3: the fragment reads of step st + 1 between the MFMAs too (one per MFMA), so no burst of
+    // LDS reads sits between the barrier and the first MFMA
+    constexpr int NR = 2 * (NA + NB);  // transposed reads per step
     auto body = [&](int st, WFrags<NA, NB> &cur, WFrags<NA, NB> &nxt) {
       w_frags_ready(cur);
       const bool more = st + 1 < nsteps;
       // the last iteration has passed no barrier that ends the other waves' reads of step st's
       // buffer, so its (unneeded) DMA goes to buffer st + 1, which holds no step that is read
       const int buf = (more ? st : st + 1) % NST, src = st + NST < nsteps ? st + NST : nsteps - 1;
+      const uint16_t *im = lds + ((st + 1) % NST) * (AIMG + BIMG);
+      if constexpr (PIPE == 3) {
+        // (the last iteration's reads land in registers nobody uses; no barrier is needed for them)
+        if (more) {
+          w_vm_wait<(NST - 2) * PER>();
+          asm volatile("s_barrier" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        issue_to(buf, src);
+        w_read16g<IA, IB, NA, NB>(im, im + AIMG, wm * WM, wn * WN, lane, nxt);
+        w_mma16g<NA, NB>(cur, acc);
+        int p = 0;
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+          if (i < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one fragment read
+          if (i % G == G - 1 && p < PER) {
+            __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // one LDS-DMA piece
+            ++p;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        return;
+      }
       if (more) {
         w_vm_wait<(NST - 2) * PER>();
         asm volatile("s_barrier" ::: "memory");
         if constexpr (PIPE == 1) issue_to(buf, src);
-        const uint16_t *im = lds + ((st + 1) % NST) * (AIMG + BIMG);
         w_read16g<IA, IB, NA, NB>(im, im + AIMG, wm * WM, wn * WN, lane, nxt);
       } else if constexpr (PIPE == 1) {
         issue_to(buf, src);
@@ -459,6 +485,7 @@ __global__ __launch_bounds__(WNT, 1) void wgrad_kernel(const uint16_t *__restric
     }
     if (st < nsteps) body(st, f0, f1);
     w_vm_wait<0>();  // no LDS-DMA outlives the workgroup's LDS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   } else {
   for (int b = 0; b < NST - 1; ++b)
       if (b < nsteps) issue(b);
@@ -701,7 +728,8 @@ int g_wgrad_mfma = 32;
 // va_set_tuning(VA_TUNE_WGRAD_TILES): 1-3 = the cost-model planner over the 256 x 256 and the
 // 896-dividing tile kinds (w_plan_tiles), every kind in the 16x16x32 form; 2 = with the cross-step
 // fragment pipeline (buffer-resource LDS-DMA after the barrier), 3 = the pipeline with the LDS-DMA
-// spread between the MFMAs; 1 = no pipeline; 0 = kind 0 (+ the remainder setting) with w_auto_splits
+// spread between the MFMAs, 4 = also the fragment reads spread between the MFMAs; 1 = no pipeline;
+// 0 = kind 0 (+ the remainder setting) with w_auto_splits
 int g_wgrad_tiles = 3;
 
 namespace {
@@ -758,8 +786,9 @@ extern "C" int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_
     const bool mf16 = g_wgrad_mfma == 16;
     const int pipe = g_wgrad_tiles >= 2 ? g_wgrad_tiles - 1 : 0;  // PIPE form of the kernels
     if (p[i].kind == 0 && pipe)
-      rc = pipe == 1 ? w_launch<256, 256, 4, true, 128, 64, 1>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
-                     : w_launch<256, 256, 4, true, 128, 64, 2>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+      rc = pipe == 1   ? w_launch<256, 256, 4, true, 128, 64, 1>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+           : pipe == 2 ? w_launch<256, 256, 4, true, 128, 64, 2>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+                       : w_launch<256, 256, 4, true, 128, 64, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
     else if (p[i].kind == 0)
       rc = mf16 ? w_launch<256, 256, 4, true>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
                 : w_launch<256, 256, 4, false>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
@@ -770,19 +799,23 @@ extern "C" int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_
       rc = mf16 ? w_launch<128, 512, 3, true>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
                 : w_launch<128, 512, 3, false>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
     else if (p[i].kind == 3)
-      rc = pipe == 2   ? w_launch<256, 224, 4, true, 64, 112, 2>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+      rc = pipe == 3   ? w_launch<256, 224, 4, true, 64, 112, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+           : pipe == 2 ? w_launch<256, 224, 4, true, 64, 112, 2>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
            : pipe == 1 ? w_launch<256, 224, 4, true, 64, 112, 1>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
                        : w_launch<256, 224, 4, true, 64, 112>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
     else if (p[i].kind == 4)
-      rc = pipe == 2   ? w_launch<224, 256, 4, true, 112, 64, 2>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+      rc = pipe == 3   ? w_launch<224, 256, 4, true, 112, 64, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+           : pipe == 2 ? w_launch<224, 256, 4, true, 112, 64, 2>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
            : pipe == 1 ? w_launch<224, 256, 4, true, 112, 64, 1>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
                        : w_launch<224, 256, 4, true, 112, 64>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
     else if (p[i].kind == 5)
-      rc = pipe == 2   ? w_launch<128, 448, 4, true, 64, 112, 2>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+      rc = pipe == 3   ? w_launch<128, 448, 4, true, 64, 112, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+           : pipe == 2 ? w_launch<128, 448, 4, true, 64, 112, 2>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
            : pipe == 1 ? w_launch<128, 448, 4, true, 64, 112, 1>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
                        : w_launch<128, 448, 3, true, 64, 112>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
     else
-      rc = pipe == 2   ? w_launch<448, 128, 4, true, 112, 64, 2>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+      rc = pipe == 3   ? w_launch<448, 128, 4, true, 112, 64, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+           : pipe == 2 ? w_launch<448, 128, 4, true, 112, 64, 2>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
            : pipe == 1 ? w_launch<448, 128, 4, true, 112, 64, 1>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
                        : w_launch<448, 128, 3, true, 112, 64>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
     if (rc != VA_OK) return rc;
