@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define VA_ABI_VERSION 9
+#define VA_ABI_VERSION 10
 
 /* error codes */
 #define VA_OK 0
@@ -164,11 +164,11 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *     dimension that is 128 mod 256 gets its last 128 rows / columns as 128 x 512 / 512 x 128 tiles.
  *   VA_TUNE_WGRAD_MFMA (va_weight_grad): 32 (default) = 32x32x16 MFMA blocks; 16 = 16x16x32 blocks
  *     (same tiles and staging; results differ only in the MFMA's internal summation order).
- *   VA_TUNE_WGRAD_TILES (va_weight_grad): 3 (default), 2, 1 = one launch whose tile shape (256 x 256,
+ *   VA_TUNE_WGRAD_TILES (va_weight_grad): 4 (default), 3, 2, 1 = one launch whose tile shape (256 x 256,
  *     or 256 x 224 / 224 x 256 / 128 x 448 / 448 x 128, which divide 896 exactly) and K-slice count
  *     are chosen by a cost model (rounds of 256 workgroups x tile area x steps + the split-K reduce),
  *     16x16x32 MFMA blocks; 2 / 3 read each step's fragments one step ahead (two register sets),
- *     3 also spreads the LDS-DMA between the MFMAs; 0 = 256 x 256 tiles (+ VA_TUNE_WGRAD_REMAINDER)
+ *     3 also spreads the LDS-DMA between the MFMAs, 4 the fragment reads too; 0 = 256 x 256 tiles (+ VA_TUNE_WGRAD_REMAINDER)
  *     with the round-4 slice rule. Results differ only in the fp32 summation order of the slices
  *     and the MFMA blocks.
  *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
@@ -360,6 +360,19 @@ int va_apply_kl_penalty(const float *scores, const float *old_lp, const float *r
  * ------------------------------------------------------------------------------------ */
 int va_accumulate_grads(int n_tensors, const void *const *src, const int64_t *numel,
                         int src_dtype, float *const *dst, float scale, void *stream);
+
+/* adamw_flat (ABI 10): one AdamW step over n fp32 elements of flat buffers (a parameter manager's
+ * master-weight / gradient bucket and its moments), torch's fused AdamW arithmetic (ADAMW mode, no
+ * amsgrad / maximize, its double-precision intermediates). Replaces: actor_optimizer.step() of the
+ * reference's _optimizer_step (dp_actor.py:272-288; torch.optim.AdamW, fsdp_workers.py:418-423) over
+ * the masters' per-parameter views. step: device fp32 step count, already advanced (bias corrections
+ * 1 - beta^step); grad_scale: device fp32 scalar the gradients are multiplied by first (the
+ * clip_grad_norm_ coefficient, folded; NULL = 1); found_inf: device fp32 flag (NULL = never), != 0
+ * leaves parameters and moments untouched; zero_grad != 0 also writes 0 to the gradients (then also
+ * when skipped). 16-byte aligned buffers. */
+int va_adamw_flat(float *param, float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, double lr,
+                  double beta1, double beta2, double eps, double weight_decay, const float *step,
+                  const float *grad_scale, const float *found_inf, int zero_grad, void *stream);
 
 /* ---------------------------------------------------------------------------------------
  * Fused bf16 model ops for the actor backbone. Not the reference's hot path: they replace the

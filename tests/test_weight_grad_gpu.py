@@ -26,7 +26,7 @@ def _call(dy, x, splits):
 class _tuning:
     """va_set_tuning values for the body of a with-block, restored to the library defaults after."""
 
-    DEFAULTS = {"VA_TUNE_WGRAD_TILES": 3, "VA_TUNE_WGRAD_REMAINDER": 0, "VA_TUNE_WGRAD_MFMA": 32}
+    DEFAULTS = {"VA_TUNE_WGRAD_TILES": 4, "VA_TUNE_WGRAD_REMAINDER": 0, "VA_TUNE_WGRAD_MFMA": 32}
 
     def __init__(self, **kw):
         self.kw = kw

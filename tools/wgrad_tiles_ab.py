@@ -1,7 +1,7 @@
 """va_weight_grad's tile planners, interleaved on one GPU (VA_TUNE_WGRAD_TILES = 0: 256 x 256 tiles
 in the 32x32x16 form with the round-4 slice rule; 1: the cost-model planner's 896-dividing tiles,
 16x16x32; 2: the same with the cross-step fragment pipeline; 3: the pipeline with its LDS-DMA spread
-between the MFMAs) at the bench's backbone shapes (dW =
+between the MFMAs; 4: the fragment reads in the MFMAs' scheduling region too) at the bench's backbone shapes (dW =
 dY^T X, K = 151,552 packed tokens) and the lm_head's (V = 151,936 x H = 896, K = 131,072 rows; also
 hipBLASLt's swapped product + transpose, the previous default). HIP-event medians of `--reps`
 interleaved rounds of `--iters` launches; one JSON line per shape, then the per-step totals (x 96
@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--rows", type=int, default=131072)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--modes", default="0,1,2,3")
+    ap.add_argument("--modes", default="0,3,4")
     ap.add_argument("--no-lm-head", action="store_true")
     args = ap.parse_args()
     from verl_amd import _lib as L
@@ -74,7 +74,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 res[arm].append(round(e0.elapsed_time(e1) / iters * 1e3, 1))
-        L.call("va_set_tuning", L.VA_TUNE_WGRAD_TILES, 3)
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_TILES, 4)
         med = {a: sorted(v)[len(v) // 2] for a, v in res.items()}
         per_step = 4 if name == "lm_head" else 96
         for a, v in med.items():

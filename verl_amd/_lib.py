@@ -41,7 +41,7 @@ VA_TUNE_WGRAD_REMAINDER, VA_TUNE_FLASH_DMA, VA_TUNE_WGRAD_MFMA, VA_TUNE_WGRAD_TI
 FLASH_TUNING_DEFAULTS = {VA_TUNE_FLASH_DMA: 7, VA_TUNE_FLASH_DQ_KB: 64, VA_TUNE_FLASH_DKDV_QT: 64,
                          VA_TUNE_FLASH_FWD_KB: 64, VA_TUNE_FLASH_GROUPED_DKDV: -1}
 
-ABI_VERSION = 9  # include/verl_amd.h VA_ABI_VERSION
+ABI_VERSION = 10  # include/verl_amd.h VA_ABI_VERSION
 
 _P = c_void_p
 _SIGNATURES: dict[str, tuple] = {
@@ -90,6 +90,8 @@ _SIGNATURES: dict[str, tuple] = {
     ),
     "va_apply_kl_penalty": (c_int, [_P, _P, _P, _P, c_int, c_int64, c_int64, c_int, c_float, _P, _P, _P]),
     "va_accumulate_grads": (c_int, [c_int, _P, _P, c_int, _P, c_float, _P]),
+    "va_adamw_flat": (c_int, [_P, _P, _P, _P, c_int64, c_double, c_double, c_double, c_double, c_double, _P, _P, _P,
+                              c_int, _P]),
     "va_rmsnorm_workspace_bytes": (c_int64, [c_int64, c_int64]),
     "va_rmsnorm_fwd": (c_int, [_P, _P, _P, c_int, c_int64, c_int64, c_float, _P, _P, _P, _P]),
     "va_rmsnorm_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, _P, _P, _P, _P]),

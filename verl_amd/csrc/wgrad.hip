@@ -725,12 +725,14 @@ int g_wgrad_remainder = 0;
 // va_set_tuning(VA_TUNE_WGRAD_MFMA): 32 (default) = 4 x 2 v_mfma_f32_32x32x16_bf16 blocks per wave,
 // 16 = 8 x 4 v_mfma_f32_16x16x32_bf16 blocks (the MFMA form of f1's sweep)
 int g_wgrad_mfma = 32;
-// va_set_tuning(VA_TUNE_WGRAD_TILES): 1-3 = the cost-model planner over the 256 x 256 and the
+// va_set_tuning(VA_TUNE_WGRAD_TILES): 1-4 = the cost-model planner over the 256 x 256 and the
 // 896-dividing tile kinds (w_plan_tiles), every kind in the 16x16x32 form; 2 = with the cross-step
 // fragment pipeline (buffer-resource LDS-DMA after the barrier), 3 = the pipeline with the LDS-DMA
-// spread between the MFMAs, 4 = also the fragment reads spread between the MFMAs; 1 = no pipeline;
-// 0 = kind 0 (+ the remainder setting) with w_auto_splits
-int g_wgrad_tiles = 3;
+// spread between the MFMAs, 4 (default) = the fragment reads in the MFMAs' scheduling region too
+// (profiles/r06/e/wgrad_tiles_ab_2.jsonl: backbone 395.8 ms per step vs 413.3 for 3 and 463.8 for
+// the round-5 kernel (0), lm_head 33.5 ms vs 36.1 for hipBLASLt); 1 = no pipeline; 0 = kind 0 (+ the
+// remainder setting) with w_auto_splits
+int g_wgrad_tiles = 4;
 
 namespace {
 // The launches of one weight gradient under the current tile settings (the size query and the

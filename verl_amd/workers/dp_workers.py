@@ -22,7 +22,7 @@ from ..utils.flops_counter import FlopsCounter
 from ..utils.torch_functional import build_lr_scheduler
 from .actor import DataParallelPPOActor
 from .actor.dp_actor import DeviceMetrics
-from .grad_sync import GradBucketReducer, MixedPrecisionParams, ShardedMixedPrecisionParams
+from .grad_sync import FlatAdamW, GradBucketReducer, MixedPrecisionParams, ShardedMixedPrecisionParams
 
 
 def init_distributed(backend: str | None = None) -> tuple[int, int]:
@@ -71,6 +71,20 @@ def make_param_manager(module: torch.nn.Module, bucket_mb: int, mixed_precision:
     return GradBucketReducer(module.parameters(), bucket_bytes=bucket_mb << 20)
 
 
+# VERL_AMD_FLAT_ADAMW=0: torch.optim.AdamW(fused=True) over the masters instead of grad_sync.FlatAdamW
+_FLAT_ADAMW = os.environ.get("VERL_AMD_FLAT_ADAMW", "1") != "0"
+
+
+def make_optimizer(manager, optim, fused: bool):
+    """AdamW with the role's optim config (fsdp_workers.py:418-423): FlatAdamW over the replicated
+    mixed-precision manager's flat buckets on the GPU, torch's AdamW otherwise (fused on the GPU)."""
+    betas = tuple(optim.get("betas", (0.9, 0.999)))
+    wd = optim.get("weight_decay", 0.01)
+    if fused and _FLAT_ADAMW and isinstance(manager, MixedPrecisionParams):
+        return FlatAdamW(manager, lr=optim.lr, betas=betas, weight_decay=wd)
+    return torch.optim.AdamW(manager.optimizer_params(), lr=optim.lr, betas=betas, weight_decay=wd, fused=fused)
+
+
 class ActorWorker:
     """update_actor / compute_log_prob of the actor role, one per GPU."""
 
@@ -106,9 +120,7 @@ class ActorWorker:
         optim = self.config.actor.optim
         fused = next(module.parameters()).is_cuda
         manager = make_param_manager(module, bucket_mb, mixed_precision, zero)
-        opt = torch.optim.AdamW(manager.optimizer_params(), lr=optim.lr,
-                                betas=tuple(optim.get("betas", (0.9, 0.999))),
-                                weight_decay=optim.get("weight_decay", 0.01), fused=fused)
+        opt = make_optimizer(manager, optim, fused)
         self.actor = DataParallelPPOActor(self.config.actor, module, opt, grad_reducer=manager)
         self.actor_optimizer = opt
         self.actor_lr_scheduler = build_lr_scheduler(opt, optim, role="actor", rank=self.rank)
@@ -218,9 +230,7 @@ class CriticWorker:
         optim = self.config.optim
         fused = next(module.parameters()).is_cuda
         manager = make_param_manager(module, bucket_mb, mixed_precision, zero)
-        opt = torch.optim.AdamW(manager.optimizer_params(), lr=optim.lr,
-                                betas=tuple(optim.get("betas", (0.9, 0.999))),
-                                weight_decay=optim.get("weight_decay", 0.01), fused=fused)
+        opt = make_optimizer(manager, optim, fused)
         self.critic = DataParallelPPOCritic(self.config, module, opt, grad_reducer=manager)
         self.critic_lr_scheduler = build_lr_scheduler(opt, optim, role="critic", rank=self.rank)
         self.flops_counter = FlopsCounter(module.config)

@@ -296,6 +296,11 @@ class MixedPrecisionParams(_OrderedBuckets):
         self._master_of = {}
         self._gview = {}
         self._bucket_of = {}
+        self._flat_of = {}  # id(master) -> (bucket index, element offset in its flat buffer)
+        # FlatAdamW folds the clip's multiply and the next zero_grad into its step (see there)
+        self.fold_clip = False
+        self.clip_coef = None
+        self._grads_zero = True
         for i, g in enumerate(groups):
             n = sum(p.numel() for p in g)
             dev = g[0].device
@@ -308,6 +313,7 @@ class MixedPrecisionParams(_OrderedBuckets):
                 mv.copy_(p.detach().float())
                 master = torch.nn.Parameter(mv, requires_grad=True)
                 master.grad = gbuf[off : off + k].view_as(p)
+                self._flat_of[id(master)] = (i, off)
                 self._master_of[id(p)] = master
                 self._gview[id(p)] = master.grad
                 off += k
@@ -409,6 +415,7 @@ class MixedPrecisionParams(_OrderedBuckets):
         launch) and, on a syncing micro-batch, mark it ready for its (ordered) collective."""
         ready = self._ready.pop(id(b), [])
         if ready:
+            self._grads_zero = False
             if ready[0].is_cuda:
                 from .. import kernels as K
 
@@ -438,11 +445,30 @@ class MixedPrecisionParams(_OrderedBuckets):
     # same interface as GradBucketReducer
     def zero_grad(self):
         self._join_wgrad_stream()
-        for b in self.buckets:
-            b.buf.zero_()
+        if not self._grads_zero:  # FlatAdamW's step already wrote the zeros
+            for b in self.buckets:
+                b.buf.zero_()
+            self._grads_zero = True
         for p in self.params:
             p.grad = None
         self._ready = {}
+
+    def flat_buckets(self) -> list:
+        """(flat fp32 master buffer, flat fp32 gradient buffer) per bucket, in bucket order."""
+        return [(m, b.buf) for m, b in zip(self.master_bufs, self.buckets, strict=True)]
+
+    def flat_index(self, master) -> tuple:
+        """(bucket index, element offset) of a master parameter inside flat_buckets()."""
+        return self._flat_of[id(master)]
+
+    def take_clip_coef(self):
+        """The folded clip's coefficient (device scalar) once, or None."""
+        c, self.clip_coef = self.clip_coef, None
+        return c
+
+    def grads_zeroed(self):
+        """The optimizer step wrote zeros to every gradient bucket (FlatAdamW, zero_grad folded)."""
+        self._grads_zero = True
 
     def begin_sync(self):
         self.sync_enabled = self.world > 1
@@ -471,7 +497,11 @@ class MixedPrecisionParams(_OrderedBuckets):
             return torch.zeros(())
         total = torch.linalg.vector_norm(torch.stack(torch._foreach_norm(bufs)))
         coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
-        torch._foreach_mul_(bufs, coef)
+        if self.fold_clip:
+            # FlatAdamW multiplies the gradients by coef as it reads them (the same fp32 product)
+            self.clip_coef = coef
+        else:
+            torch._foreach_mul_(bufs, coef)
         return total
 
     @torch.no_grad()
@@ -483,6 +513,63 @@ class MixedPrecisionParams(_OrderedBuckets):
         for h in self._hooks:
             h.remove()
         self._hooks.clear()
+
+
+class FlatAdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW(fused=True) over a MixedPrecisionParams manager's fp32 masters, stepped as
+    ONE streaming launch per flat bucket (va_adamw_flat, csrc/optim.hip) instead of torch's ~100
+    multi-tensor launches over the ~290 per-parameter views (5.7 ms per step at ~2.4 TB/s,
+    profiles/r06/d/kernel_stats_p8_summary.txt). The reference's _optimizer_step (dp_actor.py:272-288:
+    clip_grad_norm_, a non-finite skip, optimizer.step(); AdamW from fsdp_workers.py:418-423):
+      * torch's fused ADAMW arithmetic (its double-precision intermediates; tests/test_flat_adamw_gpu.py
+        compares the masters and moments with torch.optim.AdamW(fused=True) bit for bit);
+      * the gradient clip's in-place multiply is folded into the step (the manager keeps the
+        coefficient, fold_clip), and so is the next zero_grad (the step writes zeros; the
+        manager's zero_grad skips the buckets while nothing was accumulated since);
+      * ``found_inf`` (a device flag, set by dp_actor.step_unless_nonfinite as for torch's fused
+        AdamW) skips the update on the device: parameters, moments and the step count unchanged.
+    The per-parameter state (exp_avg / exp_avg_sq / step) is exposed as views of the flat moments, in
+    torch.optim.AdamW's layout. VERL_AMD_FLAT_ADAMW=0 keeps torch's AdamW (A/B runs)."""
+
+    def __init__(self, manager, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 1e-2):
+        params = manager.optimizer_params()
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False, maximize=False,
+                        foreach=None, capturable=False, differentiable=False, fused=True)
+        super().__init__(params, defaults)
+        if len(self.param_groups) != 1:
+            raise ValueError("FlatAdamW takes one parameter group (the manager's masters)")
+        self.manager = manager
+        self._flat = manager.flat_buckets()
+        self._m = [torch.zeros_like(mf) for mf, _ in self._flat]
+        self._v = [torch.zeros_like(mf) for mf, _ in self._flat]
+        self._step = torch.zeros((), dtype=torch.float32, device=self._flat[0][0].device)
+        for p in params:
+            i, off = manager.flat_index(p)
+            n = p.numel()
+            self.state[p] = {"step": self._step, "exp_avg": self._m[i][off : off + n].view_as(p),
+                             "exp_avg_sq": self._v[i][off : off + n].view_as(p)}
+        self.found_inf = None
+        manager.fold_clip = True
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        from .. import _lib as L
+        from .. import kernels as K
+
+        loss = closure() if closure is not None else None
+        g = self.param_groups[0]
+        lr, (b1, b2), eps, wd = float(g["lr"]), g["betas"], float(g["eps"]), float(g["weight_decay"])
+        fi = self.found_inf
+        # torch's fused AdamW: step += 1, and -= found_inf after a skipped step
+        self._step.add_(1.0) if fi is None else self._step.add_(1.0 - fi)
+        coef = self.manager.take_clip_coef()
+        st = K._stream(self._step)
+        for (mf, gf), m, v in zip(self._flat, self._m, self._v, strict=True):
+            L.call("va_adamw_flat", K._p(mf), K._p(gf), K._p(m), K._p(v), mf.numel(), lr, float(b1), float(b2), eps,
+                   wd, K._p(self._step), K._p(coef) if coef is not None else None,
+                   K._p(fi) if fi is not None else None, 1, st)
+        self.manager.grads_zeroed()
+        return loss
 
 
 class ShardedMixedPrecisionParams(_OrderedBuckets):
@@ -575,6 +662,7 @@ class ShardedMixedPrecisionParams(_OrderedBuckets):
     def _flush(self, b, complete: bool = True):
         ready = self._ready.pop(id(b), [])
         if ready:
+            self._grads_zero = False
             if ready[0].is_cuda:
                 from .. import kernels as K
 
