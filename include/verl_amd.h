@@ -171,6 +171,9 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *     3 also spreads the LDS-DMA between the MFMAs, 4 the fragment reads too; 0 = 256 x 256 tiles (+ VA_TUNE_WGRAD_REMAINDER)
  *     with the round-4 slice rule. Results differ only in the fp32 summation order of the slices
  *     and the MFMA blocks.
+ *   VA_TUNE_ADAMW_MATH (va_adamw_flat): rounding flavour of the step's square root / divisions / double
+ *     multiply-adds (bit 1 hardware sqrt, bit 2 reciprocal-based division, bit 4 FMA contraction),
+ *     to match a given torch build's fused AdamW bit for bit.
  *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
 *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order);
  *   VA_TUNE_FLASH_DMA (va_flash_attn_fwd / _bwd): bit 1 = forward K / V blocks staged by LDS-DMA
@@ -197,6 +200,7 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_FLASH_DMA 19
 #define VA_TUNE_WGRAD_MFMA 20
 #define VA_TUNE_WGRAD_TILES 21
+#define VA_TUNE_ADAMW_MATH 22
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

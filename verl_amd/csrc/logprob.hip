@@ -717,6 +717,7 @@ extern int g_linear_logprob_tile;  // linear_logprob.hip
 extern int g_wgrad_remainder;      // wgrad.hip
 extern int g_wgrad_mfma;           // wgrad.hip
 extern int g_wgrad_tiles;          // wgrad.hip
+extern int g_adamw_math;           // optim.hip
 extern int g_whiten_grid;         // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
 extern int g_flash_dkdv_qt;       // attention.hip
@@ -748,6 +749,13 @@ extern "C" int va_set_tuning(int key, int value) {
         return VA_E_ARG;
       }
       g_wgrad_mfma = value;
+      return VA_OK;
+    case VA_TUNE_ADAMW_MATH:
+      if (value < 0 || value > 7) {
+        va::set_error("va_set_tuning: VA_TUNE_ADAMW_MATH must be 0 .. 7");
+        return VA_E_ARG;
+      }
+      g_adamw_math = value;
       return VA_OK;
     case VA_TUNE_WGRAD_TILES:
       if (value < 0 || value > 4) {
