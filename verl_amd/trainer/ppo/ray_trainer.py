@@ -10,7 +10,6 @@ driver CPU.
 
 from __future__ import annotations
 
-from enum import Enum
 from typing import Optional
 
 import torch
@@ -19,6 +18,7 @@ from ... import kernels as K
 from ...protocol import DataProto
 from . import core_algos
 from .core_algos import AdvantageEstimator
+from .trainer_step import Role  # ray_trainer.py:67-78; one enum for the mapping keys and the step
 
 
 def apply_kl_penalty(data: DataProto, kl_ctrl, kl_penalty="kl"):
@@ -128,19 +128,6 @@ def filter_groups(batch: DataProto, metric: str = "acc"):
     return batch[idx], len(kept)
 
 
-class Role(Enum):
-    """ray_trainer.py:67-78: the worker roles a trainer maps to resource pools (subclass to add
-    roles). Here one process per GPU plays the actor (and critic / ref) roles of its DP rank."""
-
-    Actor = 0
-    Rollout = 1
-    ActorRollout = 2
-    Critic = 3
-    RefPolicy = 4
-    RewardModel = 5
-    ActorRolloutRef = 6
-
-
 class ResourcePoolManager:
     """ray_trainer.py:81-126 without Ray: the GPUs are the torch.distributed ranks of this job, so
     the spec is recorded for reference and the pools are this process group."""
@@ -171,7 +158,6 @@ class RayPPOTrainer:
     def __init__(self, config, tokenizer=None, role_worker_mapping: Optional[dict] = None, resource_pool_manager=None,
                  ray_worker_group_cls=None, processor=None, reward_fn=None, val_reward_fn=None, train_dataset=None,
                  val_dataset=None, collate_fn=None, train_sampler=None, device_name="cuda"):
-        from .trainer_step import Role
 
         self.config = config
         self.tokenizer = tokenizer
@@ -190,7 +176,7 @@ class RayPPOTrainer:
 
     def init_workers(self):
         """ray_trainer.py:823-907: build the role workers (here: call the factories)."""
-        from .trainer_step import PPOTrainerStep, Role
+        from .trainer_step import PPOTrainerStep
 
         self.actor_rollout_wg = self.role_worker_mapping[Role.ActorRollout]()
         self.critic_wg = self.role_worker_mapping[Role.Critic]() if self.use_critic else None

@@ -36,7 +36,9 @@ from .core_algos import AdvantageEstimator
 
 
 class Role(Enum):
-    """ray_trainer.py:67-78."""
+    """ray_trainer.py:67-78: the worker roles a trainer maps to resource pools (subclass to add
+    roles); here one process per GPU plays the actor (and critic / ref) roles of its DP rank.
+    verl_amd.trainer.ppo.ray_trainer re-exports this enum."""
 
     Actor = 0
     Rollout = 1
