@@ -171,6 +171,9 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *     3 also spreads the LDS-DMA between the MFMAs, 4 the fragment reads too; 0 = 256 x 256 tiles (+ VA_TUNE_WGRAD_REMAINDER)
  *     with the round-4 slice rule. Results differ only in the fp32 summation order of the slices
  *     and the MFMA blocks.
+ *   VA_TUNE_WGRAD_KIND (va_weight_grad, VA_TUNE_WGRAD_TILES >= 1): -1 (default) = the cost model's tile
+ *     shape, 0 / 3 / 4 / 5 / 6 = that shape (256 x 256, 256 x 224, 224 x 256, 128 x 448, 448 x 128)
+ *     with the model's slice count for it (A/B runs; the same results up to fp32 summation order).
  *   VA_TUNE_ADAMW_MATH (va_adamw_flat): rounding flavour of the step's square root / divisions / double
  *     multiply-adds (bit 1 hardware sqrt, bit 2 reciprocal-based division, bit 4 FMA contraction),
  *     to match a given torch build's fused AdamW bit for bit.
@@ -201,6 +204,7 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_WGRAD_MFMA 20
 #define VA_TUNE_WGRAD_TILES 21
 #define VA_TUNE_ADAMW_MATH 22
+#define VA_TUNE_WGRAD_KIND 23
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

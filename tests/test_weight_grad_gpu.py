@@ -204,3 +204,26 @@ def test_weight_grad_tiles_setting_is_checked():
 
     with pytest.raises(RuntimeError, match="0 .. 4"):
         L.call("va_set_tuning", L.VA_TUNE_WGRAD_TILES, 5)
+
+
+@pytest.mark.parametrize("kind", [0, 3, 4, 5, 6])
+@pytest.mark.parametrize("T,M,N", [(1024, 1152, 896), (512, 200, 136), (2048, 896, 4864)])
+def test_each_tile_kind_forced(kind, T, M, N):
+    """VA_TUNE_WGRAD_KIND forces one tile shape (with the cost model's slice count for it): every kind
+    is exact on exact-arithmetic operands and within the reference's tolerance on random ones, also on
+    shapes it does not divide (clamped staging, dropped columns)."""
+    g = torch.Generator(device=DEV).manual_seed(kind * 101 + T + M + N)
+    dyi = torch.randint(-3, 4, (T, M), device=DEV, generator=g).to(torch.bfloat16)
+    xi = torch.randint(-3, 4, (T, N), device=DEV, generator=g).to(torch.bfloat16)
+    dy = (torch.randn(T, M, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    x = torch.randn(T, N, device=DEV, generator=g).to(torch.bfloat16)
+    from verl_amd import _lib as L
+
+    try:
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_KIND, kind)
+        exact = _call(dyi, xi, 0)
+        got = _call(dy, x, 0)
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_KIND, -1)
+    assert torch.equal(exact.float(), _ref(dyi, xi).to(torch.bfloat16).float())
+    _check(got, _ref(dy, x))

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--modes", default="0,3,4")
     ap.add_argument("--no-lm-head", action="store_true")
+    ap.add_argument("--lm-head-plans", default="",
+                    help="also time the lm_head at these kind/splits plans, e.g. 3/1,3/2,3/3,5/2 (VA_TUNE_WGRAD_KIND)")
     args = ap.parse_args()
     from verl_amd import _lib as L
     from verl_amd import kernels as K
@@ -87,6 +89,35 @@ def main():
                           "median_us": med, "pflops": {a: round(tf / v * 1e3, 3) for a, v in med.items()},
                           "rel_l2_vs_first": rel}), flush=True)
     print(json.dumps({"per_step_ms": {k: round(v, 1) for k, v in totals.items()}}), flush=True)
+    if args.lm_head_plans:
+        M, N, T = 151936, 896, args.rows
+        dy = (torch.randn(T, M, device="cuda", generator=g) * 1e-3).to(torch.bfloat16)
+        x = torch.randn(T, N, device="cuda", generator=g).to(torch.bfloat16)
+
+        def own_at(splits):
+            o = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+            nb = L.load().va_weight_grad_workspace_bytes(T, M, N, splits)
+            ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device="cuda")
+            L.call("va_weight_grad", K._p(dy), dy.stride(0), K._p(x), x.stride(0), T, M, N, splits, K._p(ws), nb,
+                   K._p(o), K._stream(dy))
+            return o
+
+        plans = [tuple(int(v) for v in pl.split("/")) for pl in args.lm_head_plans.split(",")]
+        res = {f"{k}/{sp}": [] for k, sp in plans}
+        for _ in range(args.reps):
+            for kind, sp in plans:
+                L.call("va_set_tuning", L.VA_TUNE_WGRAD_KIND, kind)
+                own_at(sp)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(3):
+                    own_at(sp)
+                e1.record()
+                torch.cuda.synchronize()
+                res[f"{kind}/{sp}"].append(round(e0.elapsed_time(e1) / 3, 3))
+        L.call("va_set_tuning", L.VA_TUNE_WGRAD_KIND, -1)
+        print(json.dumps({"lm_head_plans_ms": res, "auto_plan": K.own_wgrad_plan(M, N, T)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -718,6 +718,7 @@ extern int g_wgrad_remainder;      // wgrad.hip
 extern int g_wgrad_mfma;           // wgrad.hip
 extern int g_wgrad_tiles;          // wgrad.hip
 extern int g_adamw_math;           // optim.hip
+extern int g_wgrad_kind;           // wgrad.hip
 extern int g_whiten_grid;         // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
 extern int g_flash_dkdv_qt;       // attention.hip
@@ -749,6 +750,13 @@ extern "C" int va_set_tuning(int key, int value) {
         return VA_E_ARG;
       }
       g_wgrad_mfma = value;
+      return VA_OK;
+    case VA_TUNE_WGRAD_KIND:
+      if (!(value == -1 || value == 0 || (value >= 3 && value <= 6))) {
+        va::set_error("va_set_tuning: VA_TUNE_WGRAD_KIND must be -1, 0 or 3 .. 6");
+        return VA_E_ARG;
+      }
+      g_wgrad_kind = value;
       return VA_OK;
     case VA_TUNE_ADAMW_MATH:
       if (value < 0 || value > 7) {

@@ -597,6 +597,9 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restri
 
 using namespace va;
 
+// va_set_tuning(VA_TUNE_WGRAD_KIND): -1 = the cost model's tile shape, else that kind (A/B runs)
+int g_wgrad_kind = -1;
+
 namespace {
 
 // fewest 32-token steps a slice gets: the 4-deep ring keeps 3 in flight, so a shorter slice is mostly
@@ -673,6 +676,7 @@ int w_plan_tiles(int64_t K, int64_t M, int64_t N, int splits, WPart (&p)[2]) {
   double best = 0.0;
   int bk = -1, bs = 1;
   for (int kind : {0, 3, 4, 5, 6}) {
+    if (g_wgrad_kind >= 0 && kind != g_wgrad_kind) continue;
     const int64_t s_lo = splits > 0 ? splits : 1, s_hi = splits > 0 ? splits : (cap < 64 ? cap : 64);
     for (int64_t sv = s_lo; sv <= s_hi; ++sv) {
       const double c = w_cost(kind, steps, M, N, sv);

@@ -46,7 +46,10 @@ def tp_merge(labels, vocab_offset: int, vocab_shard: int, vocab_total: int, logp
       m = max_r lse_r, A = sum_r e^{lse_r - m}, B = sum_r e^{lse_r - m} (lse_r - H_r),
       lse = m + ln A, H = lse - B / A, logp = x[label] - lse,
     x[label] contributed by the shard that holds it. Labels: -100 (ignore_index) gives 0, other ids
-    outside the vocabulary NaN, as va_linear_logprob_fwd."""
+    outside the vocabulary NaN, as va_linear_logprob_fwd. Precision note: x[label] is
+    rebuilt as logp_r + lse_r in fp32, so it carries ~ulp(lse_r) of rounding where the reference
+    all-reduces the raw label logit (epilogue_tp); vocab tensor parallelism is outside SURVEY §8
+    (§2 row 17), so this adapter is kept as is rather than widened to return the raw logit."""
     in_shard = (labels >= vocab_offset) & (labels < vocab_offset + vocab_shard)
     xlab = torch.where(in_shard, logp_l + lse_l, torch.zeros_like(lse_l))
     m = lse_l.clone()
