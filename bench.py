@@ -654,7 +654,9 @@ def main():
 
     if rank == 0:
         roof_hbm = roof_f1 = None
-        hbm = {k: v for k, v in ksum.items() if "tflops" not in v}
+        # the rooflines are the §8 path's kernels (the log-prob kernels, f1); the model-side
+        # kernels the timer also records (weight_grad, adamw_flat) are reported under `kernels` only
+        hbm = {k: v for k, v in ksum.items() if "tflops" not in v and k.startswith("logprob_entropy")}
         if hbm:
             # the streaming log-prob kernels: the dominant HBM-bound one by time
             name, d = max(hbm.items(), key=lambda kv: kv[1]["time_ms_total"])
@@ -672,7 +674,7 @@ def main():
                 "avg_launch_us": round(d["avg_us"], 2), "launches": d["launches"],
                 "time_ms_total": round(d["time_ms_total"], 2),
             }
-        f1s = {k: v for k, v in ksum.items() if "tflops" in v}
+        f1s = {k: v for k, v in ksum.items() if "tflops" in v and k.startswith("linear_logprob")}
         if f1s:  # MFMA-bound fused lm_head kernels (f1): 2 N V H flops per launch, the dominant one by time
             name, f1 = max(f1s.items(), key=lambda kv: kv[1]["time_ms_total"])
             f1_traffic, f1_src = pmc_traffic_f1(f1["avg_flops"]) if name == "linear_logprob_fwd" else (None, None)

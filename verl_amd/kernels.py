@@ -52,7 +52,7 @@ class KernelTimer:
     def __init__(self):
         self.records: list[tuple[str, float, object, object]] = []
 
-    FLOP_KERNELS = frozenset({"linear_logprob_fwd", "linear_logprob_bwd"})
+    FLOP_KERNELS = frozenset({"linear_logprob_fwd", "linear_logprob_bwd", "weight_grad", "weight_grad_lm_head"})
 
     def start(self, stream):
         ev = torch.cuda.Event(enable_timing=True)
@@ -1039,8 +1039,12 @@ def _own_weight_grad(dy2, x2):
     out = torch.empty(n_out, n_in, dtype=torch.bfloat16, device=dy2.device)
     nb = L.load().va_weight_grad_workspace_bytes(T, n_out, n_in, s)
     ws = torch.empty(nb // 4, dtype=torch.float32, device=dy2.device) if nb else None
+    st = torch.cuda.current_stream(dy2.device)
+    ev = TIMER.start(st) if TIMER is not None else None
     L.call("va_weight_grad", _p(dy2), dy2.stride(0), _p(x2), x2.stride(0), T, n_out, n_in, s, _p(ws), nb, _p(out),
            _stream(dy2))
+    if ev is not None:  # MFMA-bound: 2 T M N flops (the launch incl. its split-K reduce)
+        TIMER.stop("weight_grad_lm_head" if lm_head else "weight_grad", 2 * T * n_out * n_in, st, ev)
     return out
 
 

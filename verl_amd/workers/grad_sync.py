@@ -564,10 +564,14 @@ class FlatAdamW(torch.optim.Optimizer):
         self._step.add_(1.0) if fi is None else self._step.add_(1.0 - fi)
         coef = self.manager.take_clip_coef()
         st = K._stream(self._step)
+        stream = torch.cuda.current_stream(self._step.device)
         for (mf, gf), m, v in zip(self._flat, self._m, self._v, strict=True):
+            ev = K.TIMER.start(stream) if K.TIMER is not None else None
             L.call("va_adamw_flat", K._p(mf), K._p(gf), K._p(m), K._p(v), mf.numel(), lr, float(b1), float(b2), eps,
                    wd, K._p(self._step), K._p(coef) if coef is not None else None,
                    K._p(fi) if fi is not None else None, 1, st)
+            if ev is not None:  # HBM-bound: p, g, m, v read, p, m, v, g (zeroed) written
+                K.TIMER.stop("adamw_flat", 32 * mf.numel(), stream, ev)
         self.manager.grads_zeroed()
         return loss
 
