@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--modes", default="0,3,4")
     ap.add_argument("--no-lm-head", action="store_true")
+    ap.add_argument("--kind-sweep", action="store_true",
+                    help="per shape: every tile kind forced (VA_TUNE_WGRAD_KIND, the model's slices for it) vs auto")
     ap.add_argument("--lm-head-plans", default="",
                     help="also time the lm_head at these kind/splits plans, e.g. 3/1,3/2,3/3,5/2 (VA_TUNE_WGRAD_KIND)")
     args = ap.parse_args()
@@ -89,6 +91,30 @@ def main():
                           "median_us": med, "pflops": {a: round(tf / v * 1e3, 3) for a, v in med.items()},
                           "rel_l2_vs_first": rel}), flush=True)
     print(json.dumps({"per_step_ms": {k: round(v, 1) for k, v in totals.items()}}), flush=True)
+    if args.kind_sweep:
+        for name, (M, N, T) in shapes.items():
+            dy = (torch.randn(T, M, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+            x = torch.randn(T, N, device="cuda", generator=g).to(torch.bfloat16)
+            kinds = [-1, 0, 3, 4, 5, 6]
+            res = {k: [] for k in kinds}
+            iters = 2 if name == "lm_head" else args.iters
+            for _ in range(args.reps):
+                for kind in kinds:
+                    L.call("va_set_tuning", L.VA_TUNE_WGRAD_KIND, kind)
+                    own(dy, x)
+                    torch.cuda.synchronize()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(iters):
+                        own(dy, x)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    res[kind].append(round(e0.elapsed_time(e1) / iters * 1e3, 1))
+            L.call("va_set_tuning", L.VA_TUNE_WGRAD_KIND, -1)
+            print(json.dumps({"kind_sweep": name, "M": M, "N": N, "K": T, "auto_plan": K.own_wgrad_plan(M, N, T),
+                              "us": {str(k): v for k, v in res.items()},
+                              "median_us": {str(k): sorted(v)[len(v) // 2] for k, v in res.items()}}), flush=True)
+            del dy, x
     if args.lm_head_plans:
         M, N, T = 151936, 896, args.rows
         dy = (torch.randn(T, M, device="cuda", generator=g) * 1e-3).to(torch.bfloat16)
