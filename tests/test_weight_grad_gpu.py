@@ -206,7 +206,7 @@ def test_weight_grad_tiles_setting_is_checked():
         L.call("va_set_tuning", L.VA_TUNE_WGRAD_TILES, 5)
 
 
-@pytest.mark.parametrize("kind", [0, 3, 4, 5, 6])
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("T,M,N", [(1024, 1152, 896), (512, 200, 136), (2048, 896, 4864)])
 def test_each_tile_kind_forced(kind, T, M, N):
     """VA_TUNE_WGRAD_KIND forces one tile shape (with the cost model's slice count for it): every kind

@@ -95,7 +95,7 @@ def main():
         for name, (M, N, T) in shapes.items():
             dy = (torch.randn(T, M, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
             x = torch.randn(T, N, device="cuda", generator=g).to(torch.bfloat16)
-            kinds = [-1, 0, 3, 4, 5, 6]
+            kinds = [-1, 0, 1, 2, 3, 4, 5, 6]
             res = {k: [] for k in kinds}
             iters = 2 if name == "lm_head" else args.iters
             for _ in range(args.reps):

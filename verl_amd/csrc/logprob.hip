@@ -752,8 +752,8 @@ extern "C" int va_set_tuning(int key, int value) {
       g_wgrad_mfma = value;
       return VA_OK;
     case VA_TUNE_WGRAD_KIND:
-      if (!(value == -1 || value == 0 || (value >= 3 && value <= 6))) {
-        va::set_error("va_set_tuning: VA_TUNE_WGRAD_KIND must be -1, 0 or 3 .. 6");
+      if (value < -1 || value > 6) {
+        va::set_error("va_set_tuning: VA_TUNE_WGRAD_KIND must be -1 .. 6");
         return VA_E_ARG;
       }
       g_wgrad_kind = value;

@@ -619,8 +619,10 @@ int w_auto_splits(int64_t tiles, int64_t steps) {
 
 // The launches of one weight gradient. Tile kinds (all 8 waves, 1 workgroup per CU):
 //   0: 256 x 256, wave tile 128 x 64 (32x32x16 or, with VA_TUNE_WGRAD_MFMA = 16, 16x16x32 blocks)
-//   1: 512 x 128 / 2: 128 x 512, the 128-wide remainder of a dimension that is 128 mod 256
-//      (VA_TUNE_WGRAD_REMAINDER = 1, as a second launch beside kind 0)
+//   1: 512 x 128 / 2: 128 x 512 (wave tile 128 x 64): with VA_TUNE_WGRAD_TILES = 0 the 128-wide
+//      remainder of a dimension that is 128 mod 256 (VA_TUNE_WGRAD_REMAINDER = 1, a second launch
+//      beside kind 0); with the planner (>= 1) whole-launch candidates like the kinds below (896 =
+//      7 x 128)
 //   3: 256 x 224 / 4: 224 x 256 / 5: 128 x 448 / 6: 448 x 128 (VA_TUNE_WGRAD_TILES = 1): tiles that
 //      divide 896 = 4 x 224 = 2 x 448 (Qwen2.5-0.5B's hidden size) exactly, wave tiles 64 x 112 /
 //      112 x 64 of 16x16x32 blocks, so none of the MFMA work is spent on padding (256 x 256 tiles
@@ -675,7 +677,7 @@ int w_plan_tiles(int64_t K, int64_t M, int64_t N, int splits, WPart (&p)[2]) {
   const int64_t cap = steps / kMinStepsPerSlice < 1 ? 1 : (steps / kMinStepsPerSlice > 256 ? 256 : steps / kMinStepsPerSlice);
   double best = 0.0;
   int bk = -1, bs = 1;
-  for (int kind : {0, 3, 4, 5, 6}) {
+  for (int kind : {0, 1, 2, 3, 4, 5, 6}) {
     if (g_wgrad_kind >= 0 && kind != g_wgrad_kind) continue;
     const int64_t s_lo = splits > 0 ? splits : 1, s_hi = splits > 0 ? splits : (cap < 64 ? cap : 64);
     for (int64_t sv = s_lo; sv <= s_hi; ++sv) {
@@ -798,6 +800,14 @@ extern "C" int va_weight_grad(const void *dy, int64_t ldy, const void *x, int64_
     else if (p[i].kind == 0)
       rc = mf16 ? w_launch<256, 256, 4, true>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
                 : w_launch<256, 256, 4, false>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+    else if (p[i].kind == 1 && pipe)
+      rc = pipe == 3   ? w_launch<512, 128, 4, true, 128, 64, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+           : pipe == 2 ? w_launch<512, 128, 4, true, 128, 64, 2>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+                       : w_launch<512, 128, 4, true, 128, 64, 1>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
+    else if (p[i].kind == 2 && pipe)
+      rc = pipe == 3   ? w_launch<128, 512, 4, true, 128, 64, 3>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+           : pipe == 2 ? w_launch<128, 512, 4, true, 128, 64, 2>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
+                       : w_launch<128, 512, 4, true, 128, 64, 1>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);
     else if (p[i].kind == 1)
       rc = mf16 ? w_launch<512, 128, 3, true>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st)
                 : w_launch<512, 128, 3, false>(p[i], dy16, ldy, x16, ldx, K, ws, o16, N, st);

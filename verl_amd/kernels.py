@@ -989,7 +989,8 @@ def own_wgrad_splits(n_out: int, n_in: int, tokens: int | None = None) -> int:
 
 # va_weight_grad's tile kinds (csrc/wgrad.hip, VA_TUNE_WGRAD_TILES >= 1): kind -> (rows, cols) of one
 # workgroup's output tile; 3-6 divide 896 = 4 x 224 = 2 x 448 exactly
-WGRAD_TILE_KINDS = {0: (256, 256), 3: (256, 224), 4: (224, 256), 5: (128, 448), 6: (448, 128)}
+WGRAD_TILE_KINDS = {0: (256, 256), 1: (512, 128), 2: (128, 512), 3: (256, 224), 4: (224, 256), 5: (128, 448),
+                    6: (448, 128)}
 
 
 def own_wgrad_plan(n_out: int, n_in: int, tokens: int, splits: int = 0) -> tuple:
