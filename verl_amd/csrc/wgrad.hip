@@ -658,14 +658,21 @@ int w_plan(int64_t K, int64_t M, int64_t N, int splits, WPart (&p)[2]) {
 
 // Estimated time of one launch of `kind` with s K slices, in units of one workgroup-step of one
 // output element (a 32-token step of a 256 x 256 tile = 65,536 units = ~1 us at ~1.1 PF/s over 256
-// CUs): rounds of 256 workgroups x tile area x (steps per slice + 8 steps of ring fill and epilogue),
-// plus the split-K reduce (8 B per output element and slice at ~5 TB/s = 0.11 units, + one launch)
+// CUs): rounds of 256 workgroups x tile area x (steps per slice + 8 steps of ring fill and epilogue)
+// x the kind's measured efficiency factor, plus the split-K reduce (8 B per output element and slice
+// at ~5 TB/s = 0.11 units, + one launch)
+// measured issue efficiency per unit of tile area (profiles/r06/i/wgrad_tiles_ab_2.jsonl, every kind
+// forced on the bench's five shapes): the 128 x 64 wave tile (kinds 0-2: 24 fragment reads per 32
+// MFMAs) runs ~6-8 % more flops per cycle than 64 x 112 / 112 x 64 (22 per 28), and the 448-wide
+// shapes (5, 6) ~4 % more than 256 x 224 / 224 x 256 (3, 4)
+constexpr double w_kind_factor(int k) { return k == 0 ? 0.92 : (k <= 2 ? 0.94 : (k <= 4 ? 1.0 : 0.96)); }
+
 double w_cost(int kind, int64_t steps, int64_t M, int64_t N, int64_t s) {
   const int64_t tm = w_kind_tm(kind), tn = w_kind_tn(kind);
   const int64_t tiles = ((M + tm - 1) / tm) * ((N + tn - 1) / tn);
   const int64_t rounds = (tiles * s + 255) / 256;
   const double per_slice = static_cast<double>((steps + s - 1) / s) + 8.0;
-  double c = static_cast<double>(rounds) * static_cast<double>(tm * tn) * per_slice;
+  double c = static_cast<double>(rounds) * static_cast<double>(tm * tn) * per_slice * w_kind_factor(kind);
   if (s > 1) c += 0.11 * static_cast<double>(s) * static_cast<double>(M * N) + 2.0e5;
   return c;
 }

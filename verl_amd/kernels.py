@@ -991,12 +991,15 @@ def own_wgrad_splits(n_out: int, n_in: int, tokens: int | None = None) -> int:
 # workgroup's output tile; 3-6 divide 896 = 4 x 224 = 2 x 448 exactly
 WGRAD_TILE_KINDS = {0: (256, 256), 1: (512, 128), 2: (128, 512), 3: (256, 224), 4: (224, 256), 5: (128, 448),
                     6: (448, 128)}
+# w_kind_factor: measured flops per cycle per unit of tile area (profiles/r06/i/wgrad_tiles_ab_2.jsonl)
+WGRAD_KIND_FACTOR = {0: 0.92, 1: 0.94, 2: 0.94, 3: 1.0, 4: 1.0, 5: 0.96, 6: 0.96}
 
 
 def own_wgrad_plan(n_out: int, n_in: int, tokens: int, splits: int = 0) -> tuple:
     """Host mirror of w_plan_tiles (csrc/wgrad.hip): the (kind, splits) with the least estimated time,
-    rounds of 256 workgroups x tile area x (steps per slice + 8) + 0.11 per output element and slice
-    + 2e5 for the split-K reduce; ties keep the earlier kind / fewer slices (1e-3 relative margin)."""
+    rounds of 256 workgroups x tile area x (steps per slice + 8) x the kind's efficiency factor + 0.11
+    per output element and slice + 2e5 for the split-K reduce; ties keep the earlier kind / fewer
+    slices (1e-3 relative margin)."""
     steps = tokens // 32
     cap = min(max(steps // WGRAD_MIN_STEPS_PER_SLICE, 1), 256)
     best, plan = None, None
@@ -1004,7 +1007,7 @@ def own_wgrad_plan(n_out: int, n_in: int, tokens: int, splits: int = 0) -> tuple
         lo, hi = (splits, splits) if splits > 0 else (1, min(cap, 64))
         tiles = -(-n_out // tm) * -(-n_in // tn)
         for sv in range(lo, hi + 1):
-            c = float(-(-tiles * sv // 256)) * float(tm * tn) * (float(-(-steps // sv)) + 8.0)
+            c = float(-(-tiles * sv // 256)) * float(tm * tn) * (float(-(-steps // sv)) + 8.0) * WGRAD_KIND_FACTOR[kind]
             if sv > 1:
                 c += 0.11 * sv * float(n_out * n_in) + 2.0e5
             if best is None or c < best * 0.999:
