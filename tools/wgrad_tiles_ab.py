@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--modes", default="0,3,4")
     ap.add_argument("--no-lm-head", action="store_true")
+    ap.add_argument("--shapes", default="",
+                    help="instead of the bench's shapes: name=MxNxK,... (e.g. gate_up7b=37888x3584x16384); adds "
+                         "hipBLASLt's dY^T @ X as an arm")
     ap.add_argument("--kind-sweep", action="store_true",
                     help="per shape: every tile kind forced (VA_TUNE_WGRAD_KIND, the model's slices for it) vs auto")
     ap.add_argument("--lm-head-plans", default="",
@@ -41,6 +44,12 @@ def main():
               "down": (896, 4864, args.tokens)}
     if not args.no_lm_head:
         shapes["lm_head"] = (151936, 896, args.rows)
+    custom = bool(args.shapes)
+    if custom:
+        shapes = {}
+        for item in args.shapes.split(","):
+            name, dims = item.split("=")
+            shapes[name] = tuple(int(v) for v in dims.split("x"))
     g = torch.Generator(device="cuda").manual_seed(0)
     totals = {}
 
@@ -54,13 +63,15 @@ def main():
         return o
 
     def hipblaslt(dy, x):
-        return K.transpose16(x.t() @ dy)
+        if dy.shape[1] >= K.WGRAD_SWAP_MIN_OUT:
+            return K.transpose16(x.t() @ dy)
+        return dy.t() @ x
 
     for name, (M, N, T) in shapes.items():
         scale = 1e-3 if name == "lm_head" else 0.1
         dy = (torch.randn(T, M, device="cuda", generator=g) * scale).to(torch.bfloat16)
         x = torch.randn(T, N, device="cuda", generator=g).to(torch.bfloat16)
-        arms = [(f"tiles{m}", m) for m in modes] + ([("hipblaslt", None)] if name == "lm_head" else [])
+        arms = [(f"tiles{m}", m) for m in modes] + ([("hipblaslt", None)] if name == "lm_head" or custom else [])
         res = {a: [] for a, _ in arms}
         outs = {}
         iters = max(2, args.iters // 4) if name == "lm_head" else args.iters
