@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define VA_ABI_VERSION 10
+#define VA_ABI_VERSION 11
 
 /* error codes */
 #define VA_OK 0
@@ -177,6 +177,9 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   VA_TUNE_ADAMW_MATH (va_adamw_flat): rounding flavour of the step's square root / divisions / double
  *     multiply-adds (bit 1 hardware sqrt, bit 2 reciprocal-based division, bit 4 FMA contraction),
  *     to match a given torch build's fused AdamW bit for bit.
+ *   VA_TUNE_LINEAR_TN (va_linear_tn): 1 (default) = each workgroup keeps one feature tile and runs a range
+ *     of token blocks, the workgroups of one token range side by side on one XCD; 0 = consecutive tiles of
+ *     the (token block, feature tile) list per workgroup (bitwise identical results).
  *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
 *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order);
  *   VA_TUNE_FLASH_DMA (va_flash_attn_fwd / _bwd): bit 1 = forward K / V blocks staged by LDS-DMA
@@ -205,6 +208,7 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_WGRAD_TILES 21
 #define VA_TUNE_ADAMW_MATH 22
 #define VA_TUNE_WGRAD_KIND 23
+#define VA_TUNE_LINEAR_TN 24
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------
@@ -435,6 +439,18 @@ int va_rope_qkv_fwd(const void *qkv, int64_t ld, const void *cos, const void *si
                     int64_t Hq, int64_t Hk, int64_t D, void *q, void *k, void *v, void *stream);
 int va_rope_qkv_bwd(const void *dq, const void *dk, const void *dv, const void *cos, const void *sin, int dtype,
                     int64_t T, int64_t Hq, int64_t Hk, int64_t D, void *dqkv, int64_t ld, void *stream);
+
+/* linear_tn (ABI 11): y [M, N] (row stride ldy >= N, % 4, 8-byte aligned) = bf16(x [M, K] . w [N, K]^T (+ bias
+ * [N])), fp32 accumulation — F.linear's layout, both operands contiguous along K (row strides ldx / ldw, % 8,
+ * 16-byte aligned), the bias added to the fp32 sum before the one rounding (nullable, 8-byte aligned). Output
+ * tiles of 256 rows x tile_n columns, tile_n in {192, 224, 256, 288} dividing N (0 = the first of 224, 288,
+ * 256, 192 that does: va_linear_tn_tile(N), 0 when none does); K % 64 == 0; `per` tiles per persistent
+ * workgroup (0 = automatic: one round of 256 workgroups). The backbone's projections (forward, and the input
+ * gradients over a transposed weight copy) whose widths 896 / 1,152 are not multiples of 256: torch's
+ * nn.Linear under FSDP in the reference (dp_actor.py:331-333, :465-470). Not a §8 row. */
+int va_linear_tn_tile(int64_t N);
+int va_linear_tn(const void *x, int64_t ldx, const void *w, int64_t ldw, const void *bias, int dtype, int64_t M,
+                 int64_t N, int64_t K, int tile_n, int per, void *y, int64_t ldy, void *stream);
 
 /* transpose_16: out [C, R] (row stride ld_out) = in [R, C] (row stride ld_in)^T for any 16-bit
  * element type; R, C, strides multiples of 8, 16-byte aligned buffers. The layout step of the

@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_abi_version_and_workspace_queries(lib):
-    assert lib.va_abi_version() == 10
+    assert lib.va_abi_version() == 11
     assert lib.va_ppo_loss_workspace_bytes(10) == 8 * (2 * 10 * 8 + 8)
     assert lib.va_agg_workspace_bytes(10) == 8 * (2 * 10 * 8 + 8)
     assert lib.va_gae_workspace_bytes(7) == 8 * (6 * 7 + 8)

@@ -17,6 +17,8 @@
 #   ab:<name>:<reps>:<v1>|<v2>[|...][:<common args>]   tools/gpu_ab.sh (interleaved bench variants) -> ab_<name>.txt
 #   sq:<name>:<kernel substrings>:<command>   one rocprofv3 --pmc pass of the SQ / GRBM counters over
 #                         <command> (no other trace domains), summarised by tools/sq_summary.py -> sq_<name>.jsonl
+#   pmc:<name>:<counters, comma-separated>:<kernel substrings>:<command>   the same with other counters
+#                         (at most 8 SQ_ per pass) -> sq_<name>.jsonl ("extra": per-dispatch averages)
 #   cmd:<name>:<command>  any other command                -> <name>.txt
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -84,6 +86,15 @@ for step in "$@"; do
     sq:*)
       IFS=: read -r _ name subs cmd <<< "$step"
       C="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE"
+      # shellcheck disable=SC2086
+      run 200 "$O/sq_$name.log" timeout -s KILL 180 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$O/sq_$name" -o run -- $cmd
+      # shellcheck disable=SC2086
+      { echo "# cmd: rocprofv3 --pmc $C --kernel-trace -- $cmd; python tools/sq_summary.py <dir> $subs"; python tools/sq_summary.py "$O/sq_$name" $subs; } > "$O/sq_$name.jsonl"
+      rm -rf "$O/sq_$name"
+      cat "$O/sq_$name.jsonl" ;;
+    pmc:*)
+      IFS=: read -r _ name cnt subs cmd <<< "$step"
+      C=${cnt//,/ }
       # shellcheck disable=SC2086
       run 200 "$O/sq_$name.log" timeout -s KILL 180 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$O/sq_$name" -o run -- $cmd
       # shellcheck disable=SC2086

@@ -14,6 +14,10 @@ import json
 import sys
 
 
+FIXED = {"SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+         "SQ_ACTIVE_INST_ANY", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_ACTIVE_INST_VALU"}
+
+
 def main():
     d, names = sys.argv[1], sys.argv[2:]
     cc = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)[0]
@@ -32,20 +36,24 @@ def main():
             print(json.dumps({"kernel": sub, "dispatches": 0}))
             continue
         busy = clock = wait = us = valu = 0.0
+        extra = collections.defaultdict(float)
         for i in ids:
             v = per[i]
-            g = v["GRBM_GUI_ACTIVE"] / 8
-            busy += v["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * g)
+            g = v.get("GRBM_GUI_ACTIVE", 0.0) / 8
+            busy += v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024 * g) if g else 0.0
             clock += g / dur[i]
-            wait += v["SQ_WAIT_ANY"] / (v["SQ_WAVE_CYCLES"] or 1)
-            valu += v.get("SQ_ACTIVE_INST_VALU", 0.0) / (v["SQ_WAVE_CYCLES"] or 1)
+            wait += v.get("SQ_WAIT_ANY", 0.0) / (v.get("SQ_WAVE_CYCLES") or 1)
+            valu += v.get("SQ_ACTIVE_INST_VALU", 0.0) / (v.get("SQ_WAVE_CYCLES") or 1)
             us += dur[i] / 1e3
+            for c, x in v.items():
+                if c not in FIXED:
+                    extra[c] += x
         n = len(ids)
         print(json.dumps({"kernel": sub, "dispatches": n, "avg_us": round(us / n, 1),
                           "mfma_busy": round(busy / n, 3), "clock_ghz": round(clock / n, 3),
                           "busy_x_clock": round(busy * clock / n / n, 3), "wait_share": round(wait / n, 3),
                           "valu_active_share": round(valu / n, 3),
-                          "name": kname[ids[0]][:90]}))
+                          "extra": {c: round(x / n) for c, x in extra.items()}, "name": kname[ids[0]][:90]}))
 
 
 if __name__ == "__main__":

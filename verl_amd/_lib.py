@@ -36,13 +36,13 @@ VA_TUNE_FLASH_DKDV_QT, VA_TUNE_FLASH_DQ_KB, VA_TUNE_FLASH_FWD_KB, VA_TUNE_GAE_PA
 VA_TUNE_GAE_NT, VA_TUNE_LOSS_VEC = 13, 14
 VA_TUNE_WHITEN_SLICE_MIN, VA_TUNE_WHITEN_GRID, VA_TUNE_LINEAR_LOGPROB_TILE = 15, 16, 17
 VA_TUNE_WGRAD_REMAINDER, VA_TUNE_FLASH_DMA, VA_TUNE_WGRAD_MFMA, VA_TUNE_WGRAD_TILES = 18, 19, 20, 21
-VA_TUNE_ADAMW_MATH, VA_TUNE_WGRAD_KIND = 22, 23
+VA_TUNE_ADAMW_MATH, VA_TUNE_WGRAD_KIND, VA_TUNE_LINEAR_TN = 22, 23, 24
 # the library's compiled-in flash-attention staging defaults (csrc/attention.hip), for code that
 # changes a setting and restores it
 FLASH_TUNING_DEFAULTS = {VA_TUNE_FLASH_DMA: 7, VA_TUNE_FLASH_DQ_KB: 64, VA_TUNE_FLASH_DKDV_QT: 64,
                          VA_TUNE_FLASH_FWD_KB: 64, VA_TUNE_FLASH_GROUPED_DKDV: -1}
 
-ABI_VERSION = 10  # include/verl_amd.h VA_ABI_VERSION
+ABI_VERSION = 11  # include/verl_amd.h VA_ABI_VERSION
 
 _P = c_void_p
 _SIGNATURES: dict[str, tuple] = {
@@ -128,6 +128,9 @@ _SIGNATURES: dict[str, tuple] = {
                             _P, _P, _P, _P]),
     "va_rope_qkv_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int64, c_int64, c_int64, c_int64, _P, c_int64, _P]),
     "va_transpose_16": (c_int, [_P, c_int64, c_int64, c_int64, _P, c_int64, _P]),
+    "va_linear_tn_tile": (c_int, [c_int64]),
+    "va_linear_tn": (c_int, [_P, c_int64, _P, c_int64, _P, c_int, c_int64, c_int64, c_int64, c_int, c_int, _P, c_int64,
+                             _P]),
     "va_weight_grad_workspace_bytes": (c_int64, [c_int64, c_int64, c_int64, c_int]),
     "va_column_sum_workspace_bytes": (c_int64, [c_int64, c_int64]),
     "va_column_sum": (c_int, [_P, c_int64, c_int, c_int64, c_int64, _P, c_int64, _P, _P]),

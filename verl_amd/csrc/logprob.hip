@@ -719,6 +719,7 @@ extern int g_wgrad_mfma;           // wgrad.hip
 extern int g_wgrad_tiles;          // wgrad.hip
 extern int g_adamw_math;           // optim.hip
 extern int g_wgrad_kind;           // wgrad.hip
+extern int g_linear_tn;            // gemm_tn.hip
 extern int g_whiten_grid;         // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
 extern int g_flash_dkdv_qt;       // attention.hip
@@ -757,6 +758,13 @@ extern "C" int va_set_tuning(int key, int value) {
         return VA_E_ARG;
       }
       g_wgrad_kind = value;
+      return VA_OK;
+    case VA_TUNE_LINEAR_TN:
+      if (value < 0 || value > 8) {
+        va::set_error("va_set_tuning: VA_TUNE_LINEAR_TN must be 0 .. 8");
+        return VA_E_ARG;
+      }
+      g_linear_tn = value;
       return VA_OK;
     case VA_TUNE_ADAMW_MATH:
       if (value < 0 || value > 7) {
