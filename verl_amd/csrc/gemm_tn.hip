@@ -596,6 +596,430 @@ __device__ __forceinline__ void linear_tn_pp_body(const uint16_t *__restrict__ x
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// The ping-pong form over 64-deep K-steps (VA_TUNE_LINEAR_TN = 9): every DMA piece reads 8 rows x 128 B
+// (whole cache lines: half the L1 -> L2 requests of the 32-deep steps' 64-B row pieces, whose texture-data
+// path was the measured limit), the token operand through a 3-stage ring and the weight operand (read
+// by the XCD's 8 workgroups of its feature tile in step, mostly L2 hits) through 2 stages: 152 KB of LDS
+// for 224-wide tiles. Load phase st issues W(st + 2), then X(st + 3), then (a tile end) the epilogue's
+// stores, reads step st + 1's fragments and retires W(st + 2) (and with it X(st + 2)) leaving X(st + 3)
+// and the stores in flight.
+constexpr int Q_TK = 64;
+
+__device__ __forceinline__ int q_swz(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int q_img_off(int row, int c) { return row * Q_TK + ((c ^ q_swz(row)) << 3); }
+
+template <int I, bool BIAS>
+__device__ __forceinline__ void linear_tn_pp64_body(const uint16_t *__restrict__ x, int64_t ldx,
+                                                    const uint16_t *__restrict__ w, int64_t ldw,
+                                                    const uint16_t *__restrict__ bias, int64_t M, int K, int64_t N,
+                                                    int per, uint16_t *__restrict__ y, int64_t ldy) {
+  constexpr int WR = 32 * I;
+  constexpr int WIMG = WR * Q_TK, XIMG = G_TM * Q_TK;  // bf16 elements of one stage
+  constexpr int NXB = 3, NWB = 2;                      // ring depths
+  constexpr int XBASE = 0, WBASE = NXB * XIMG, IDLE = WBASE + NWB * WIMG, BIASO = IDLE + 512;
+  constexpr int WG8 = WR / 8;                          // 8-row DMA groups of the weight image
+  constexpr int NWS = (WG8 + 7) / 8, NXS = 4;          // pieces per wave and step
+  constexpr int S = I * 4;
+  constexpr int VM = NXS, VM_EPI = NXS + S < 63 ? NXS + S : 63;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[BIASO + WR];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int64_t n_nt = N / WR, n_mt = (M + G_TM - 1) / G_TM;
+  int64_t L = blockIdx.x;
+  {
+    const int64_t nl = gridDim.x >> 3;
+    L = (L & 7) * nl + (L >> 3);
+  }
+  const int64_t nt = L % n_nt, mt0 = (L / n_nt) * per;
+  const int64_t ntiles = n_mt - mt0 < per ? n_mt - mt0 : per;
+  if (ntiles <= 0) return;
+  const int nk = K / Q_TK;
+  const int nsteps = static_cast<int>(ntiles) * nk;
+
+  uint32_t xoff[NXS], woff[NWS];
+  int xdst[NXS], wdst[NWS];
+#pragma unroll
+  for (int s2 = 0; s2 < NXS; ++s2) {
+    const int g = s2 * 8 + wave, row = g * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ q_swz(row);
+    xoff[s2] = static_cast<uint32_t>((row * ldx + lc * 8) * 2);
+    xdst[s2] = g * 8 * Q_TK;
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < NWS; ++s2) {
+    const int g = s2 * 8 + wave;
+    const bool ok = g < WG8;
+    const int row = (ok ? g * 8 : 0) + (lane >> 3);
+    const int lc = (lane & 7) ^ q_swz(row);
+    woff[s2] = static_cast<uint32_t>((row * ldw + lc * 8) * 2);
+    wdst[s2] = ok ? g * 8 * Q_TK : -1;
+  }
+  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t *>(w + nt * WR * ldw), 0, static_cast<int>(WR * ldw * 2), 0x00020000);
+  auto issue_w = [&](int buf, int kc) {
+    uint16_t *img = lds + WBASE + buf * WIMG;
+    const int kb = kc * Q_TK * 2;
+#pragma unroll
+    for (int s2 = 0; s2 < NWS; ++s2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wres, wdst[s2] >= 0 ? img + wdst[s2] : lds + IDLE, 16, woff[s2], kb, 0,
+                                               0);
+  };
+  auto issue_x = [&](int buf, int tl, int kc) {
+    const int64_t m0 = (mt0 + tl) * G_TM;
+    const int64_t rows = M - m0 < G_TM ? M - m0 : G_TM;
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t *>(x + m0 * ldx), 0, static_cast<int>(rows * ldx * 2), 0x00020000);
+    uint16_t *img = lds + XBASE + buf * XIMG;
+    const int kb = kc * Q_TK * 2;
+#pragma unroll
+    for (int s2 = 0; s2 < NXS; ++s2) __builtin_amdgcn_raw_ptr_buffer_load_lds(xres, img + xdst[s2], 16, xoff[s2], kb, 0, 0);
+  };
+  bf16x8 fa[2][I], fbb[2][4];
+  auto read = [&](int step) {
+    const uint16_t *iw = lds + WBASE + (step % NWB) * WIMG, *ix = lds + XBASE + (step % NXB) * XIMG;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = q * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+        fa[q][i] = *reinterpret_cast<const bf16x8 *>(iw + q_img_off(wr * (WR / 2) + i * 16 + (lane & 15), c));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        fbb[q][j] = *reinterpret_cast<const bf16x8 *>(ix + q_img_off(wc * 64 + j * 16 + (lane & 15), c));
+    }
+  };
+  auto ready = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[0][0]));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int i = 0; i < I; ++i) asm volatile("" : "+v"(fa[q][i]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(fbb[q][j]));
+    }
+  };
+
+  f32x4 acc[I][4];
+#pragma unroll
+  for (int i = 0; i < I; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int64_t mt = mt0;
+  int kt = 0;
+  int st_epi = -8;
+  // DMA cursors: W(st + 2) (K-step only: the weight tile is the workgroup's for every tile) and
+  // X(st + 3) (tile, K-step)
+  int w_kc = 2 % nk, x_tl = 3 / nk, x_kc = 3 % nk;
+  const int fl = wr * (WR / 2) + (lane >> 4) * 4, fb = static_cast<int>(nt * WR) + fl;
+  if constexpr (BIAS) {
+    for (int q = tid; q < WR; q += G_THREADS) lds[BIASO + q] = bias[nt * WR + q];
+    __syncthreads();
+  }
+  auto epilogue = [&]() {
+    const int64_t m0 = mt * G_TM;
+    const int64_t rows = M - m0 < G_TM ? M - m0 : G_TM;
+    const __amdgpu_buffer_rsrc_t yres = __builtin_amdgcn_make_buffer_rsrc(
+        y + m0 * ldy, 0, static_cast<int>(rows * ldy * 2), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int tok = wc * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+        if constexpr (BIAS) {
+          const uint2 bb = *reinterpret_cast<const uint2 *>(lds + BIASO + fl + i * 16);
+          v0 += bf16_lo(bb.x), v1 += bf16_hi(bb.x), v2 += bf16_lo(bb.y), v3 += bf16_hi(bb.y);
+        }
+        typedef int v2i __attribute__((ext_vector_type(2)));
+        const v2i qv = {static_cast<int>(pack2_bf16(v0, v1)), static_cast<int>(pack2_bf16(v2, v3))};
+        __builtin_amdgcn_raw_buffer_store_b64(qv, yres, (tok * static_cast<int>(ldy) + fb + i * 16) * 2, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto clampx = [&](int step, int &tl, int &kc) {  // step -> (tile, K-step); past the end: the last step
+    const int st2 = step < nsteps ? step : nsteps - 1;
+    tl = st2 / nk, kc = st2 % nk;
+  };
+
+  // prologue: W(0) X(0) W(1) X(1) X(2) issued; all but X(2) retired; step 0's fragments in registers
+  {
+    int tl, kc;
+    issue_w(0, 0);
+    clampx(0, tl, kc), issue_x(0, tl, kc);
+    issue_w(1, 1 % nk);
+    clampx(1, tl, kc), issue_x(1, tl, kc);
+    clampx(2, tl, kc), issue_x(2, tl, kc);
+  }
+  p_vm_wait<NXS>();
+  asm volatile("s_barrier" ::: "memory");
+  read(0);
+  ready();
+  if (wr == 1) asm volatile("s_barrier" ::: "memory");  // the stagger
+  for (int st = 0; st < nsteps; ++st) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q][i], fbb[q][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    // load phase st
+    const bool w_in = st + 2 < nsteps, x_in = st + 3 < nsteps;
+    issue_w(st % NWB, w_in ? w_kc : nk - 1);
+    if (++w_kc == nk) w_kc = 0;
+    issue_x(st % NXB, x_in ? x_tl : static_cast<int>(ntiles) - 1, x_in ? x_kc : nk - 1);
+    if (++x_kc == nk) x_kc = 0, ++x_tl;
+    if (++kt == nk) {
+      epilogue();
+      st_epi = st;
+      kt = 0;
+      ++mt;
+    }
+    if (st + 1 < nsteps) read(st + 1);
+    if (st_epi == st) p_vm_wait<VM_EPI>();
+    else p_vm_wait<VM>();
+    ready();
+    asm volatile("s_barrier" ::: "memory");
+  }
+  if (wr == 0) asm volatile("s_barrier" ::: "memory");
+  p_vm_wait<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <int I, bool BIAS>
+__device__ __forceinline__ void linear_tn_pp64s_body(const uint16_t *__restrict__ x, int64_t ldx,
+                                                    const uint16_t *__restrict__ w, int64_t ldw,
+                                                    const uint16_t *__restrict__ bias, int64_t M, int K, int64_t N,
+                                                    int per, uint16_t *__restrict__ y, int64_t ldy) {
+  constexpr int WR = 32 * I;
+  constexpr int WIMG = WR * Q_TK, XIMG = G_TM * Q_TK;  // bf16 elements of one stage
+  constexpr int NXB = 3, NWB = 2;                      // ring depths
+  constexpr int XBASE = 0, WBASE = NXB * XIMG, IDLE = WBASE + NWB * WIMG, BIASO = IDLE + 512;
+  constexpr int WG8 = WR / 8;                          // 8-row DMA groups of the weight image
+  constexpr int NWS = WG8 / 4, NXS = 8;                // pieces per loader wave and step
+  static_assert(WG8 % 4 == 0, "whole weight groups per loader wave");
+  constexpr int S = I * 4;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[BIASO + WR];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int64_t n_nt = N / WR, n_mt = (M + G_TM - 1) / G_TM;
+  int64_t L = blockIdx.x;
+  {
+    const int64_t nl = gridDim.x >> 3;
+    L = (L & 7) * nl + (L >> 3);
+  }
+  const int64_t nt = L % n_nt, mt0 = (L / n_nt) * per;
+  const int64_t ntiles = n_mt - mt0 < per ? n_mt - mt0 : per;
+  if (ntiles <= 0) return;
+  const int nk = K / Q_TK;
+  const int nsteps = static_cast<int>(ntiles) * nk;
+
+  uint32_t xoff[NXS], woff[NWS];
+  int xdst[NXS], wdst[NWS];
+  const int lw = wave & 3;  // the wave's index among its group's four loaders
+#pragma unroll
+  for (int s2 = 0; s2 < NXS; ++s2) {
+    const int g = s2 * 4 + lw, row = g * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ q_swz(row);
+    xoff[s2] = static_cast<uint32_t>((row * ldx + lc * 8) * 2);
+    xdst[s2] = g * 8 * Q_TK;
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < NWS; ++s2) {
+    const int g = s2 * 4 + lw;
+    const int row = g * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ q_swz(row);
+    woff[s2] = static_cast<uint32_t>((row * ldw + lc * 8) * 2);
+    wdst[s2] = g * 8 * Q_TK;
+  }
+  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t *>(w + nt * WR * ldw), 0, static_cast<int>(WR * ldw * 2), 0x00020000);
+  auto issue_w = [&](int buf, int kc) {
+    uint16_t *img = lds + WBASE + buf * WIMG;
+    const int kb = kc * Q_TK * 2;
+#pragma unroll
+    for (int s2 = 0; s2 < NWS; ++s2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wres, img + wdst[s2], 16, woff[s2], kb, 0, 0);
+  };
+  auto issue_x = [&](int buf, int tl, int kc) {
+    const int64_t m0 = (mt0 + tl) * G_TM;
+    const int64_t rows = M - m0 < G_TM ? M - m0 : G_TM;
+    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t *>(x + m0 * ldx), 0, static_cast<int>(rows * ldx * 2), 0x00020000);
+    uint16_t *img = lds + XBASE + buf * XIMG;
+    const int kb = kc * Q_TK * 2;
+#pragma unroll
+    for (int s2 = 0; s2 < NXS; ++s2) __builtin_amdgcn_raw_ptr_buffer_load_lds(xres, img + xdst[s2], 16, xoff[s2], kb, 0, 0);
+  };
+  bf16x8 fa[2][I], fbb[2][4];
+  auto read = [&](int step) {
+    const uint16_t *iw = lds + WBASE + (step % NWB) * WIMG, *ix = lds + XBASE + (step % NXB) * XIMG;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = q * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+        fa[q][i] = *reinterpret_cast<const bf16x8 *>(iw + q_img_off(wr * (WR / 2) + i * 16 + (lane & 15), c));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        fbb[q][j] = *reinterpret_cast<const bf16x8 *>(ix + q_img_off(wc * 64 + j * 16 + (lane & 15), c));
+    }
+  };
+  auto ready = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[0][0]));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int i = 0; i < I; ++i) asm volatile("" : "+v"(fa[q][i]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(fbb[q][j]));
+    }
+  };
+
+  f32x4 acc[I][4];
+#pragma unroll
+  for (int i = 0; i < I; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int64_t mt = mt0;
+  int kt = 0;
+  // DMA cursors: W(st + 2) (K-step only: the weight tile is the workgroup's for every tile) and
+  // X(st + 3) (tile, K-step)
+  int w_kc = 2 % nk, x_tl = 3 / nk, x_kc = 3 % nk;
+  const int fl = wr * (WR / 2) + (lane >> 4) * 4, fb = static_cast<int>(nt * WR) + fl;
+  if constexpr (BIAS) {
+    for (int q = tid; q < WR; q += G_THREADS) lds[BIASO + q] = bias[nt * WR + q];
+    __syncthreads();
+  }
+  auto epilogue = [&]() {
+    const int64_t m0 = mt * G_TM;
+    const int64_t rows = M - m0 < G_TM ? M - m0 : G_TM;
+    const __amdgpu_buffer_rsrc_t yres = __builtin_amdgcn_make_buffer_rsrc(
+        y + m0 * ldy, 0, static_cast<int>(rows * ldy * 2), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int tok = wc * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+        if constexpr (BIAS) {
+          const uint2 bb = *reinterpret_cast<const uint2 *>(lds + BIASO + fl + i * 16);
+          v0 += bf16_lo(bb.x), v1 += bf16_hi(bb.x), v2 += bf16_lo(bb.y), v3 += bf16_hi(bb.y);
+        }
+        typedef int v2i __attribute__((ext_vector_type(2)));
+        const v2i qv = {static_cast<int>(pack2_bf16(v0, v1)), static_cast<int>(pack2_bf16(v2, v3))};
+        __builtin_amdgcn_raw_buffer_store_b64(qv, yres, (tok * static_cast<int>(ldy) + fb + i * 16) * 2, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto clampx = [&](int step, int &tl, int &kc) {  // step -> (tile, K-step); past the end: the last step
+    const int st2 = step < nsteps ? step : nsteps - 1;
+    tl = st2 / nk, kc = st2 % nk;
+  };
+
+  // prologue: the weight loaders (waves 4-7) issue W(0), W(1) and retire both; the token loaders (waves
+  // 0-3) X(0), X(1), X(2) and retire all but X(2); step 0's fragments in registers
+  const bool wload = wr == 1;
+  if (wload) {
+    issue_w(0, 0);
+    issue_w(1, 1 % nk);
+    p_vm_wait<0>();
+  } else {
+    int tl, kc;
+    clampx(0, tl, kc), issue_x(0, tl, kc);
+    clampx(1, tl, kc), issue_x(1, tl, kc);
+    clampx(2, tl, kc), issue_x(2, tl, kc);
+    p_vm_wait<NXS>();
+  }
+  asm volatile("s_barrier" ::: "memory");
+  read(0);
+  ready();
+  if (wload) asm volatile("s_barrier" ::: "memory");  // the stagger
+  for (int st = 0; st < nsteps; ++st) {
+    __builtin_amdgcn_sched_barrier(0);
+    // MFMA phase; a weight loader first issues W(st + 2) into step st's weight buffer, free since every
+    // wave's load phase st - 1 (see above)
+    if (wload) {
+      issue_w(st % NWB, st + 2 < nsteps ? w_kc : nk - 1);
+      if (++w_kc == nk) w_kc = 0;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q][i], fbb[q][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    // load phase st: a token loader issues X(st + 3); the epilogue at a tile's end; step st + 1's
+    // fragments; then the token loaders retire X(st + 2) (X(st + 3) and the stores stay in flight), the
+    // weight loaders W(st + 2) (the stores stay in flight)
+    if (!wload) {
+      const bool x_in = st + 3 < nsteps;
+      issue_x(st % NXB, x_in ? x_tl : static_cast<int>(ntiles) - 1, x_in ? x_kc : nk - 1);
+      if (++x_kc == nk) x_kc = 0, ++x_tl;
+    }
+    const bool epi = ++kt == nk;
+    if (epi) {
+      epilogue();
+      kt = 0;
+      ++mt;
+    }
+    if (st + 1 < nsteps) read(st + 1);
+    if (wload) {
+      if (epi) p_vm_wait<S>();
+      else p_vm_wait<0>();
+    } else {
+      if (epi) p_vm_wait<NXS + S>();
+      else p_vm_wait<NXS>();
+    }
+    ready();
+    asm volatile("s_barrier" ::: "memory");
+  }
+  if (!wload) asm volatile("s_barrier" ::: "memory");
+  p_vm_wait<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <int I, bool BIAS>
+__global__ __launch_bounds__(G_THREADS, 1) void linear_tn_pp64s_kernel(const uint16_t *__restrict__ x, int64_t ldx,
+                                                                       const uint16_t *__restrict__ w, int64_t ldw,
+                                                                       const uint16_t *__restrict__ bias, int64_t M,
+                                                                       int K, int64_t N, int per,
+                                                                       uint16_t *__restrict__ y, int64_t ldy) {
+  linear_tn_pp64s_body<I, BIAS>(x, ldx, w, ldw, bias, M, K, N, per, y, ldy);
+}
+
+template <int I, bool BIAS>
+__global__ __launch_bounds__(G_THREADS, 1) void linear_tn_pp64_kernel(const uint16_t *__restrict__ x, int64_t ldx,
+                                                                      const uint16_t *__restrict__ w, int64_t ldw,
+                                                                      const uint16_t *__restrict__ bias, int64_t M,
+                                                                      int K, int64_t N, int per,
+                                                                      uint16_t *__restrict__ y, int64_t ldy) {
+  linear_tn_pp64_body<I, BIAS>(x, ldx, w, ldw, bias, M, K, N, per, y, ldy);
+}
+
 template <int I, int NST, bool BIAS, int PROBE = 0>
 __global__ __launch_bounds__(G_THREADS, 1) void linear_tn_pp_kernel(const uint16_t *__restrict__ x, int64_t ldx,
                                                                     const uint16_t *__restrict__ w, int64_t ldw,
@@ -705,7 +1129,8 @@ extern "C" int va_linear_tn(const void *x, int64_t ldx, const void *w, int64_t l
   const int64_t n_nt = N / tile_n, n_mt = (M + G_TM - 1) / G_TM;
   const bool lock = g_linear_tn >= 1 && n_nt <= 32;  // (wider outputs: list order, two-buffer form)
   // the pipelined form needs a K of at least its ring (4 / 5 steps of 32); shorter: the two-buffer form
-  const bool pipe = g_linear_tn >= 2 && lock && K >= (g_linear_tn == 3 || g_linear_tn == 8 ? 5 : 4) * P_TK;  // (ping-pong: 4)
+  const bool pipe = g_linear_tn >= 2 && lock && K >= (g_linear_tn == 3 || g_linear_tn == 8 ? 5 : 4) * P_TK &&
+                    (g_linear_tn < 9 || K >= 3 * Q_TK);  // (ping-pong: 4)
   // automatic: one round of the 256 CUs (one 512-thread workgroup per CU), tiles spread evenly; in LOCK
   // order whole groups of 8 token ranges (the grid is padded to multiples of 8 n_nt workgroups)
   if (per == 0) {
@@ -735,7 +1160,17 @@ extern "C" int va_linear_tn(const void *x, int64_t ldx, const void *w, int64_t l
   const auto *b16 = static_cast<const uint16_t *>(bias);
   auto *y16 = static_cast<uint16_t *>(y);
   if (pipe && (tile_n == 192 || tile_n == 224)) {  // the two register sets fit these wave tiles only
-    if (g_linear_tn == 8) {  // ping-pong, 5-stage ring
+    if (g_linear_tn == 10) {  // ping-pong, 64-deep steps, split loaders
+      const auto kern = tile_n == 192 ? (has_b ? linear_tn_pp64s_kernel<6, true> : linear_tn_pp64s_kernel<6, false>)
+                                      : (has_b ? linear_tn_pp64s_kernel<7, true> : linear_tn_pp64s_kernel<7, false>);
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nwg)), dim3(G_THREADS), 0, s, x16, ldx, w16, ldw, b16, M,
+                         static_cast<int>(K), N, per, y16, ldy);
+    } else if (g_linear_tn == 9) {  // ping-pong, 64-deep steps
+      const auto kern = tile_n == 192 ? (has_b ? linear_tn_pp64_kernel<6, true> : linear_tn_pp64_kernel<6, false>)
+                                      : (has_b ? linear_tn_pp64_kernel<7, true> : linear_tn_pp64_kernel<7, false>);
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nwg)), dim3(G_THREADS), 0, s, x16, ldx, w16, ldw, b16, M,
+                         static_cast<int>(K), N, per, y16, ldy);
+    } else if (g_linear_tn == 8) {  // ping-pong, 5-stage ring
       if (tile_n == 192) launch_tn_pp<6, 5>(has_b, nwg, s, x16, ldx, w16, ldw, b16, M, N, K, per, y16, ldy);
       else launch_tn_pp<7, 5>(has_b, nwg, s, x16, ldx, w16, ldw, b16, M, N, K, per, y16, ldy);
     } else if (g_linear_tn >= 5) {  // timing probes (wrong results): 5 no operand traffic, 6 one token block, 7 no stagger
