@@ -177,9 +177,10 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *   VA_TUNE_ADAMW_MATH (va_adamw_flat): rounding flavour of the step's square root / divisions / double
  *     multiply-adds (bit 1 hardware sqrt, bit 2 reciprocal-based division, bit 4 FMA contraction),
  *     to match a given torch build's fused AdamW bit for bit.
- *   VA_TUNE_LINEAR_TN (va_linear_tn): 1 (default) = each workgroup keeps one feature tile and runs a range
- *     of token blocks, the workgroups of one token range side by side on one XCD; 0 = consecutive tiles of
- *     the (token block, feature tile) list per workgroup (bitwise identical results).
+ *   VA_TUNE_LINEAR_TN (va_linear_tn): 2 (default) = the ping-pong form for 192 / 224-wide tiles at K >= 192
+ *     (else 1); 1 = the two-buffer form, each workgroup keeping one feature tile over a range of token blocks,
+ *     the workgroups of one token range side by side on one XCD; 0 = the two-buffer form over consecutive
+ *     tiles of the (token block, feature tile) list (all bitwise identical).
  *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
 *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order);
  *   VA_TUNE_FLASH_DMA (va_flash_attn_fwd / _bwd): bit 1 = forward K / V blocks staged by LDS-DMA

@@ -42,11 +42,11 @@ def test_exact_operands_bitwise_equal_to_f_linear(M, N, K, tile, bias):
     assert torch.equal(y, ref)
 
 
-@pytest.mark.parametrize("mode", [10, 9, 4, 3, 2, 1])
+@pytest.mark.parametrize("mode", [2, 1])
 @pytest.mark.parametrize("M,N,K,bias", [(257, 896, 128, True), (1000, 1152, 1152, True), (3000, 896, 4864, False),
-                                         (2560, 896, 896, False)])
+                                         (2560, 896, 896, False), (600, 896, 192, False), (513, 1152, 256, True)])
 def test_forms_bitwise_equal_on_exact_data(mode, M, N, K, bias):
-    """The pipelined form (K >= 128: its 4-stage ring spans tiles) and the two-buffer form, per tile
+    """The ping-pong form (K >= 192: its rings run on across tiles) and the two-buffer form, per tile
     boundary / row tail / per-workgroup tile count."""
     from verl_amd import _lib as L
 
@@ -87,7 +87,7 @@ def test_strided_operands_tiles_per_workgroup_and_row_stride():
     from verl_amd import _lib as L
 
     try:
-        for order in (10, 9, 4, 3, 2, 1, 0):  # VA_TUNE_LINEAR_TN: the pipelined form, the two-buffer form's two tile orders
+        for order in (2, 1, 0):  # VA_TUNE_LINEAR_TN: the ping-pong form, the two-buffer form's two tile orders
             L.call("va_set_tuning", L.VA_TUNE_LINEAR_TN, order)
             for per in (0, 1, 3, 7, 100):
                 y, buf = _run(xs, ws, per=per, ldy=904)
@@ -125,6 +125,6 @@ def test_tile_query_and_argument_checks():
     with pytest.raises(RuntimeError, match="aligned"):
         L.call("va_linear_tn", K._p(x[:, 4:]), 128, K._p(w), 128, None, L.VA_BF16, 64, 224, 64, 0, 0, K._p(y), 224, s)
     with pytest.raises(RuntimeError, match="VA_TUNE_LINEAR_TN"):
-        L.call("va_set_tuning", L.VA_TUNE_LINEAR_TN, 11)
+        L.call("va_set_tuning", L.VA_TUNE_LINEAR_TN, 3)
     with pytest.raises(RuntimeError, match="strides"):
         L.call("va_linear_tn", K._p(x), 64, K._p(w), 128, None, L.VA_BF16, 64, 224, 128, 0, 0, K._p(y), 224, s)

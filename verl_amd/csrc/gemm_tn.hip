@@ -11,14 +11,19 @@
 //
 // Core: 8 waves = 2 (feature halves of WR / 2 = I blocks of 16) x 4 (token quarters of 64 = 4 blocks),
 // v_mfma_f32_16x16x32_bf16 with the weight rows as the MFMA rows, so a lane holds 4 consecutive output
-// features of one token per block (one 8-byte store). Both operands stream through two LDS images per
-// 64-deep K-step by LDS-DMA (buffer_load ... lds, 16 B per lane) whose 16-byte chunk c of row r sits at
-// c ^ ((r >> 1) & 7) (swizzled on the global source address: conflict-free fragment reads), the next
-// step's images issued between the current step's two K-halves. Persistent: a workgroup runs `per`
-// consecutive tiles of the (token block, feature tile) list, feature tile fastest, staging the next
-// tile's first K-step during the current tile's last (no prologue between tiles); workgroups b, b + 8,
-// ... share an XCD and get contiguous runs of tiles (the token panels they share stay in its L2).
-// Rows past M read 0 through the buffer resource's bound and are not stored.
+// features of one token per block (one 8-byte store). Operands by LDS-DMA (buffer_load ... lds, 16 B per
+// lane, 8 rows x 128 B per piece) into images whose 16-byte chunk c of row r sits at c ^ ((r >> 1) & 7)
+// (swizzled on the global source address: conflict-free fragment reads). Persistent: each workgroup keeps
+// one feature tile over a range of token blocks, the workgroups of one token range side by side on one
+// XCD (each token K-step is read from HBM / the Infinity Cache once per XCD, then from its L2). Two forms:
+// the two-buffer form below (the next step's images issued between the current step's two K-halves) and
+// the ping-pong form further down (the default where it applies). Rows past M read 0 through the buffer
+// resource's bound and are not stored.
+//
+// Measured against hipBLASLt at the bench's shapes (151,552 tokens, profiles/r06/z): 0.85-1.20 PF/s vs
+// 0.96-1.30 — hipBLASLt's 256 x 256 tiles keep its MFMA pipe 78 % busy at a power-limited clock where
+// these reach 55 %, more than the 12.5 % of padding the 224-wide tiles save — so the product keeps
+// hipBLASLt for these GEMMs; the kernel stays as the measured alternative.
 //
 // Bound: MFMA, 2 M N K flops per launch.
 
@@ -193,416 +198,28 @@ __device__ __forceinline__ void linear_tn_body(const uint16_t *__restrict__ x, i
 }
 
 // ---------------------------------------------------------------------------------------------
-// The pipelined form (VA_TUNE_LINEAR_TN = 2): 32-deep K-steps through a 4-stage LDS-DMA ring, the DMA of
-// step st + 4 issued while step st computes (2 steps stay in flight across every barrier: counted
-// vmcnt, raw s_barrier), and each wave's fragments of step st + 1 read from LDS between the MFMAs of
-// step st (two register sets), the DMA pieces spread between them too — the schedule of the weight
-// gradients' pipelined tiles (wgrad.hip PIPE 3) on F.linear's K-contiguous operands, whose fragments are
-// plain ds_read_b128 of 8 consecutive K of one row. Image rows are 64 B (32 K); 16-byte chunk c of row r
-// sits at c ^ ((r >> 2) & 2) (swizzled on the DMA source: conflict-free fragment reads). The tile order
-// is LOCK's (one feature tile per workgroup, the workgroups of a token range side by side on one XCD)
-// and the ring runs on across the workgroup's tiles; a tile's epilogue stores by buffer stores (rows
-// past M dropped by the resource bound), a fixed count per lane that the next NST - 1 waits leave in
-// flight behind the DMA pieces issued before them.
-constexpr int P_TK = 32;
-
-// chunk c of row r at c ^ ((r >> 2) & 2): conflict-free for ds_read_b128's four 16-lane groups
-// ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31} and the same + 32) over 16 rows x 4 chunks
-__device__ __forceinline__ int p_swz(int row) { return (row >> 2) & 2; }
-__device__ __forceinline__ int p_img_off(int row, int c) { return row * P_TK + ((c ^ p_swz(row)) << 3); }
-
+// retire all but N of this wave's vector-memory operations (LDS-DMA pieces and buffer stores, in issue order)
 template <int N>
 __device__ __forceinline__ void p_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int NA, int NB>
-struct PFrags {
-  bf16x8 a[NA], b[NB];
-};
-
-// WC: token wave-columns — 4 (8 waves, two per SIMD, 64 tokens x I blocks each) or 2 (4 waves, one per
-// SIMD, 128 tokens each: twice the MFMAs per fragment read and per barrier, the accumulators in AGPRs)
-template <int I, int WC, int NST, bool BIAS>
-__device__ __forceinline__ void linear_tn_pipe_body(const uint16_t *__restrict__ x, int64_t ldx,
-                                                    const uint16_t *__restrict__ w, int64_t ldw,
-                                                    const uint16_t *__restrict__ bias, int64_t M, int K, int64_t N,
-                                                    int per, uint16_t *__restrict__ y, int64_t ldy) {
-  constexpr int WR = 32 * I;                   // output features per tile
-  constexpr int WIMG = WR * P_TK, XIMG = G_TM * P_TK;
-  constexpr int BUF = WIMG + XIMG;             // bf16 elements of one ring stage
-  constexpr int NW = 2 * WC, NT = 64 * NW;    // waves, threads
-  constexpr int NB = 16 / WC;                  // token blocks per wave (256 tokens over WC columns)
-  constexpr int WG16 = WR / 16;                // 16-row DMA groups of the weight image
-  constexpr int NWS = (WG16 + NW - 1) / NW;    // weight pieces per wave and step
-  constexpr int NXS = 16 / NW;                 // token pieces per wave and step
-  constexpr int PER = NWS + NXS;               // LDS-DMA pieces per wave and step
-  constexpr int S = I * NB;                    // epilogue stores per lane
-  constexpr int NM = I * NB, NR = I + NB;      // MFMAs and fragment reads per wave and step
-  constexpr int G = NM / (PER + 1);
-  // the wait after an epilogue keeps its stores in flight (capped at the 6-bit count: waiting for a
-  // few of them too is only slower)
-  constexpr int VM_EPI = (NST - 2) * PER + S < 63 ? (NST - 2) * PER + S : 63;
-  // the ring, 1 KB for the weight pieces without a group, then the tile's bias (WR bf16)
-  __shared__ __attribute__((aligned(16))) uint16_t lds[NST * BUF + 512 + WR];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave / WC, wc = wave % WC;
-
-  const int64_t n_nt = N / WR, n_mt = (M + G_TM - 1) / G_TM;
-  int64_t L = blockIdx.x;
-  {
-    const int64_t nl = gridDim.x >> 3;  // the host pads the grid to a multiple of 8 n_nt
-    L = (L & 7) * nl + (L >> 3);
-  }
-  const int64_t nt = L % n_nt, mt0 = (L / n_nt) * per;
-  const int64_t ntiles = n_mt - mt0 < per ? n_mt - mt0 : per;
-  if (ntiles <= 0) return;
-  const int nk = K / P_TK;  // >= NST (K >= 128)
-  const int nsteps = static_cast<int>(ntiles) * nk;
-
-  // DMA pieces: lane offsets within a 16-row group (row l >> 2, source chunk (l & 3) ^ swizzle)
-  uint32_t xoff[NXS], woff[NWS];
-  int xdst[NXS], wdst[NWS];
-#pragma unroll
-  for (int s2 = 0; s2 < NXS; ++s2) {
-    const int g = s2 * NW + wave, row = g * 16 + (lane >> 2);
-    const int lc = (lane & 3) ^ p_swz(row);
-    xoff[s2] = static_cast<uint32_t>((row * ldx + lc * 8) * 2);
-    xdst[s2] = WIMG + g * 16 * P_TK;
-  }
-#pragma unroll
-  for (int s2 = 0; s2 < NWS; ++s2) {
-    const int g = s2 * NW + wave;
-    const bool ok = g < WG16;
-    const int row = (ok ? g * 16 : 0) + (lane >> 2);
-    const int lc = (lane & 3) ^ p_swz(row);
-    woff[s2] = static_cast<uint32_t>((row * ldw + lc * 8) * 2);
-    wdst[s2] = ok ? g * 16 * P_TK : -1;
-  }
-  uint16_t *const idle = lds + NST * BUF;
-  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t *>(w + nt * WR * ldw), 0, static_cast<int>(WR * ldw * 2), 0x00020000);
-  // step src (of this workgroup's nsteps) into ring buffer buf; branch-free
-  auto issue_to = [&](int buf, int tl, int kc) {
-    const int64_t m0 = (mt0 + tl) * G_TM;
-    const int64_t rows = M - m0 < G_TM ? M - m0 : G_TM;
-    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t *>(x + m0 * ldx), 0, static_cast<int>(rows * ldx * 2), 0x00020000);
-    uint16_t *img = lds + buf * BUF;
-    const int kb = kc * P_TK * 2;
-#pragma unroll
-    for (int s2 = 0; s2 < NWS; ++s2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wres, wdst[s2] >= 0 ? img + wdst[s2] : idle, 16, woff[s2], kb, 0, 0);
-#pragma unroll
-    for (int s2 = 0; s2 < NXS; ++s2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xres, img + xdst[s2], 16, xoff[s2], kb, 0, 0);
-  };
-  auto read = [&](const uint16_t *img, PFrags<I, NB> &f) {
-    const int c = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < I; ++i)
-      f.a[i] = *reinterpret_cast<const bf16x8 *>(img + p_img_off(wr * (WR / 2) + i * 16 + (lane & 15), c));
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-      f.b[j] = *reinterpret_cast<const bf16x8 *>(img + WIMG + p_img_off(wc * 16 * NB + j * 16 + (lane & 15), c));
-  };
-  auto ready = [&](PFrags<I, NB> &f) {  // every LDS read of this wave retired; no MFMA above the wait
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f.a[0]));
-#pragma unroll
-    for (int i = 1; i < I; ++i) asm volatile("" : "+v"(f.a[i]));
-#pragma unroll
-    for (int j = 0; j < NB; ++j) asm volatile("" : "+v"(f.b[j]));
-  };
-
-  f32x4 acc[I][NB];
-#pragma unroll
-  for (int i = 0; i < I; ++i)
-#pragma unroll
-    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  int64_t mt = mt0;  // the tile being accumulated
-  int kt = 0;
-  int st_epi = -NST;  // the last iteration that stored a tile
-  int d_tl = NST / nk, d_kc = NST % nk;  // tile and K-step of the DMA source step st + NST
-  // the epilogue: acc[i][j][e] = Y[token mt 256 + wc 64 + 16 j + (lane & 15)][feature fb + 16 i + e]
-  const int fl = wr * (WR / 2) + (lane >> 4) * 4, fb = static_cast<int>(nt * WR) + fl;
-  // the bias through LDS (an ordinary global load in the loop would make hipcc drain the DMA ring)
-  const uint16_t *lbias = lds + NST * BUF + 512;
-  if constexpr (BIAS) {
-    for (int f = tid; f < WR; f += NT) lds[NST * BUF + 512 + f] = bias[nt * WR + f];
-    __syncthreads();
-  }
-  auto epilogue = [&]() {
-    const int64_t m0 = mt * G_TM;
-    const int64_t rows = M - m0 < G_TM ? M - m0 : G_TM;
-    const __amdgpu_buffer_rsrc_t yres = __builtin_amdgcn_make_buffer_rsrc(
-        y + m0 * ldy, 0, static_cast<int>(rows * ldy * 2), 0x00020000);
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int tok = wc * 16 * NB + j * 16 + (lane & 15);
-#pragma unroll
-      for (int i = 0; i < I; ++i) {
-        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-        if constexpr (BIAS) {  // F.linear's bias epilogue: bf16(acc + b)
-          const uint2 bb = *reinterpret_cast<const uint2 *>(lbias + fl + i * 16);
-          v0 += bf16_lo(bb.x), v1 += bf16_hi(bb.x), v2 += bf16_lo(bb.y), v3 += bf16_hi(bb.y);
-        }
-        typedef int v2i __attribute__((ext_vector_type(2)));
-        const v2i q = {static_cast<int>(pack2_bf16(v0, v1)), static_cast<int>(pack2_bf16(v2, v3))};
-        __builtin_amdgcn_raw_buffer_store_b64(q, yres, (tok * static_cast<int>(ldy) + fb + i * 16) * 2, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < I; ++i)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
-
-  // iteration st: fragments of step st ready; publish step st + 1 (steps through st + NST - 1 issued,
-  // NST - 2 of them stay in flight, plus a recent epilogue's stores issued after them), read its
-  // fragments, MFMAs of step st with the DMA of step st + NST into step st's buffer between them
-  auto body = [&](int st, PFrags<I, NB> &cur, PFrags<I, NB> &nxt) {
-    ready(cur);
-    const bool more = st + 1 < nsteps;
-    const int buf = (more ? st : st + 1) % NST;
-    // the source step st + NST from the incremental cursor (past the last step: the last step again)
-    const bool in_range = st + NST < nsteps;
-    const int tl = in_range ? d_tl : static_cast<int>(ntiles) - 1, kc = in_range ? d_kc : nk - 1;
-    if (more) {
-      if (st - st_epi < NST) p_vm_wait<VM_EPI>();
-      else p_vm_wait<(NST - 2) * PER>();
-      asm volatile("s_barrier" ::: "memory");
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    issue_to(buf, tl, kc);
-    if (++d_kc == nk) d_kc = 0, ++d_tl;
-    read(lds + ((st + 1) % NST) * BUF, nxt);
-#pragma unroll
-    for (int i = 0; i < I; ++i)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.a[i], cur.b[j], acc[i][j], 0, 0, 0);
-    int p = 0;
-#pragma unroll
-    for (int m = 0; m < NM; ++m) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);               // one MFMA
-      if (m < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one fragment read
-      if (m % G == G - 1 && p < PER) {
-        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // one LDS-DMA piece
-        ++p;
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (++kt == nk) {
-      epilogue();
-      st_epi = st;
-      kt = 0;
-      ++mt;
-    }
-  };
-
-  PFrags<I, NB> f0, f1;
-  for (int b = 0; b < NST; ++b) {
-    const int src = b < nsteps ? b : nsteps - 1;
-    issue_to(b, src / nk, src % nk);
-  }
-  p_vm_wait<(NST - 1) * PER>();
-  asm volatile("s_barrier" ::: "memory");
-  read(lds, f0);
-  int st = 0;
-  for (; st + 1 < nsteps; st += 2) {
-    body(st, f0, f1);
-    body(st + 1, f1, f0);
-  }
-  if (st < nsteps) body(st, f0, f1);
-  p_vm_wait<0>();  // no LDS-DMA outlives the workgroup's LDS
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-// The ping-pong form (VA_TUNE_LINEAR_TN = 4): per 32-deep K-step each wave alternates an MFMA phase (the
-// step's 28 MFMAs on fragments already in registers) and a load phase (the tile epilogue when one ends,
-// the DMA of step st + NST into step st's ring buffer, the fragments of step st + 1 into the same
-// registers, the waits that retire them and step st + 2's DMA), a barrier after each; waves 4-7 (the
-// partners of waves 0-3 on the four SIMDs) run one barrier behind, so each SIMD's matrix pipe alternates
-// between one wave's MFMA phase while its partner loads (cdna_hip_programming.md, the 8-phase template's
-// stagger). Ordering, with the stagger: every wave retires DMA(st + 2) at the end of its load phase st,
-// before the barrier that its partner group passes into load phase st + 1, which reads it; a ring buffer
-// is re-filled in load phase st only after every wave's reads of it (load phase st - 1, retired by the
-// lgkmcnt wait before that phase's closing barrier) — both groups' phases pair up so.
-template <int I, int NST, bool BIAS, int PROBE = 0>
-__device__ __forceinline__ void linear_tn_pp_body(const uint16_t *__restrict__ x, int64_t ldx,
-                                                  const uint16_t *__restrict__ w, int64_t ldw,
-                                                  const uint16_t *__restrict__ bias, int64_t M, int K, int64_t N,
-                                                  int per, uint16_t *__restrict__ y, int64_t ldy) {
-  constexpr int WR = 32 * I;
-  constexpr int WIMG = WR * P_TK, XIMG = G_TM * P_TK;
-  constexpr int BUF = WIMG + XIMG;
-  constexpr int WG16 = WR / 16;
-  constexpr int NWS = (WG16 + 7) / 8;
-  constexpr int PER = NWS + 2;
-  constexpr int S = I * 4;
-  constexpr int VM = (NST - 2) * PER, VM_EPI = VM + S < 63 ? VM + S : 63;
-  __shared__ __attribute__((aligned(16))) uint16_t lds[NST * BUF + 512 + WR];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-
-  const int64_t n_nt = N / WR, n_mt = (M + G_TM - 1) / G_TM;
-  int64_t L = blockIdx.x;
-  {
-    const int64_t nl = gridDim.x >> 3;
-    L = (L & 7) * nl + (L >> 3);
-  }
-  const int64_t nt = L % n_nt, mt0 = (L / n_nt) * per;
-  const int64_t ntiles = n_mt - mt0 < per ? n_mt - mt0 : per;
-  if (ntiles <= 0) return;
-  const int nk = K / P_TK;
-  const int nsteps = static_cast<int>(ntiles) * nk;
-
-  uint32_t xoff[2], woff[NWS];
-  int xdst[2], wdst[NWS];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-    const int g = s2 * 8 + wave, row = g * 16 + (lane >> 2);
-    const int lc = (lane & 3) ^ p_swz(row);
-    xoff[s2] = static_cast<uint32_t>((row * ldx + lc * 8) * 2);
-    xdst[s2] = WIMG + g * 16 * P_TK;
-  }
-#pragma unroll
-  for (int s2 = 0; s2 < NWS; ++s2) {
-    const int g = s2 * 8 + wave;
-    const bool ok = g < WG16;
-    const int row = (ok ? g * 16 : 0) + (lane >> 2);
-    const int lc = (lane & 3) ^ p_swz(row);
-    woff[s2] = static_cast<uint32_t>((row * ldw + lc * 8) * 2);
-    wdst[s2] = ok ? g * 16 * P_TK : -1;
-  }
-  uint16_t *const idle = lds + NST * BUF;
-  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t *>(w + nt * WR * ldw), 0, static_cast<int>(WR * ldw * 2), 0x00020000);
-  auto issue_to = [&](int buf, int tl, int kc) {
-    if constexpr (PROBE == 1) return;  // (timing probe: no operand traffic)
-    const int64_t m0 = (PROBE == 2 ? 0 : mt0 + tl) * G_TM;  // (probe 2: every workgroup one token block)
-    const int64_t rows = M - m0 < G_TM ? M - m0 : G_TM;
-    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t *>(x + m0 * ldx), 0, static_cast<int>(rows * ldx * 2), 0x00020000);
-    uint16_t *img = lds + buf * BUF;
-    const int kb = kc * P_TK * 2;
-#pragma unroll
-    for (int s2 = 0; s2 < NWS; ++s2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wres, wdst[s2] >= 0 ? img + wdst[s2] : idle, 16, woff[s2], kb, 0, 0);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) __builtin_amdgcn_raw_ptr_buffer_load_lds(xres, img + xdst[s2], 16, xoff[s2], kb, 0, 0);
-  };
-  PFrags<I, 4> f;
-  auto read = [&](const uint16_t *img) {
-    const int c = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < I; ++i)
-      f.a[i] = *reinterpret_cast<const bf16x8 *>(img + p_img_off(wr * (WR / 2) + i * 16 + (lane & 15), c));
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      f.b[j] = *reinterpret_cast<const bf16x8 *>(img + WIMG + p_img_off(wc * 64 + j * 16 + (lane & 15), c));
-  };
-  auto ready = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f.a[0]));
-#pragma unroll
-    for (int i = 1; i < I; ++i) asm volatile("" : "+v"(f.a[i]));
-#pragma unroll
-    for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(f.b[j]));
-  };
-
-  f32x4 acc[I][4];
-#pragma unroll
-  for (int i = 0; i < I; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  int64_t mt = mt0;
-  int kt = 0;
-  int st_epi = -NST;
-  int d_tl = NST / nk, d_kc = NST % nk;
-  const int fl = wr * (WR / 2) + (lane >> 4) * 4, fb = static_cast<int>(nt * WR) + fl;
-  const uint16_t *lbias = lds + NST * BUF + 512;
-  if constexpr (BIAS) {
-    for (int q = tid; q < WR; q += G_THREADS) lds[NST * BUF + 512 + q] = bias[nt * WR + q];
-    __syncthreads();
-  }
-  auto epilogue = [&]() {
-    const int64_t m0 = mt * G_TM;
-    const int64_t rows = M - m0 < G_TM ? M - m0 : G_TM;
-    const __amdgpu_buffer_rsrc_t yres = __builtin_amdgcn_make_buffer_rsrc(
-        y + m0 * ldy, 0, static_cast<int>(rows * ldy * 2), 0x00020000);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int tok = wc * 64 + j * 16 + (lane & 15);
-#pragma unroll
-      for (int i = 0; i < I; ++i) {
-        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-        if constexpr (BIAS) {
-          const uint2 bb = *reinterpret_cast<const uint2 *>(lbias + fl + i * 16);
-          v0 += bf16_lo(bb.x), v1 += bf16_hi(bb.x), v2 += bf16_lo(bb.y), v3 += bf16_hi(bb.y);
-        }
-        typedef int v2i __attribute__((ext_vector_type(2)));
-        const v2i q = {static_cast<int>(pack2_bf16(v0, v1)), static_cast<int>(pack2_bf16(v2, v3))};
-        __builtin_amdgcn_raw_buffer_store_b64(q, yres, (tok * static_cast<int>(ldy) + fb + i * 16) * 2, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < I; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
-
-  // prologue: steps 0 .. NST - 1 issued, step 0 (and step 1) retired, step 0's fragments in registers
-  for (int b = 0; b < NST; ++b) {
-    const int src = b < nsteps ? b : nsteps - 1;
-    issue_to(b, src / nk, src % nk);
-  }
-  p_vm_wait<(NST - 2) * PER>();
-  asm volatile("s_barrier" ::: "memory");
-  read(lds);
-  ready();
-  if (wr == 1 && PROBE != 3) asm volatile("s_barrier" ::: "memory");  // the stagger: waves 4-7 one barrier behind
-  for (int st = 0; st < nsteps; ++st) {
-    // MFMA phase
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < I; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_barrier" ::: "memory");
-    // load phase
-    if (++kt == nk) {
-      epilogue();
-      st_epi = st;
-      kt = 0;
-      ++mt;
-    }
-    const bool in_range = st + NST < nsteps;
-    issue_to(st % NST, in_range ? d_tl : static_cast<int>(ntiles) - 1, in_range ? d_kc : nk - 1);
-    if (++d_kc == nk) d_kc = 0, ++d_tl;
-    if (st + 1 < nsteps) read(lds + ((st + 1) % NST) * BUF);
-    // retire DMA(st + 2): NST - 2 younger steps stay in flight (and a recent epilogue's stores, issued
-    // between DMA(st + 2) and this step's DMA when st - st_epi <= NST - 3)
-    if (st - st_epi <= NST - 3) p_vm_wait<VM_EPI>();
-    else p_vm_wait<VM>();
-    ready();
-    asm volatile("s_barrier" ::: "memory");
-  }
-  if (wr == 0 && PROBE != 3) asm volatile("s_barrier" ::: "memory");  // the same barrier count for every wave
-  p_vm_wait<0>();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-// The ping-pong form over 64-deep K-steps (VA_TUNE_LINEAR_TN = 9): every DMA piece reads 8 rows x 128 B
-// (whole cache lines: half the L1 -> L2 requests of the 32-deep steps' 64-B row pieces, whose texture-data
-// path was the measured limit), the token operand through a 3-stage ring and the weight operand (read
-// by the XCD's 8 workgroups of its feature tile in step, mostly L2 hits) through 2 stages: 152 KB of LDS
-// for 224-wide tiles. Load phase st issues W(st + 2), then X(st + 3), then (a tile end) the epilogue's
-// stores, reads step st + 1's fragments and retires W(st + 2) (and with it X(st + 2)) leaving X(st + 3)
-// and the stores in flight.
+// The ping-pong form (VA_TUNE_LINEAR_TN = 2, default for 192 / 224-wide tiles and K >= 192). Per 64-deep
+// K-step each wave alternates an MFMA phase (the step's 56 MFMAs on fragments already in registers) and a
+// load phase (DMA issue, a finished tile's epilogue, the next step's fragments, the waits that retire
+// them), a barrier after each; waves 4-7 — the partners of waves 0-3 on the four SIMDs — run one barrier
+// behind, so each SIMD's matrix pipe alternates between one wave's MFMA phase and the other's (the stagger
+// of the 8-phase template, cdna_hip_programming.md). Every DMA piece reads 8 rows x 128 B, whole cache
+// lines (32-deep steps' 64-B row pieces doubled the L1 -> L2 requests and were texture-data bound:
+// profiles/r06/w-x); the token operand goes through a 3-stage ring (1 of the 4 workgroups sharing a token
+// step misses L2), the weight operand (8 workgroups per XCD share it) through 2 stages: 152 KB of LDS at
+// 224-wide tiles. Load phase st issues W(st + 2) into step st's weight buffer, then X(st + 3) into step
+// st's token buffer, then a finished tile's stores (buffer stores: rows past M dropped by the resource
+// bound), reads step st + 1's fragments, and retires W(st + 2) — with it X(st + 2) — leaving X(st + 3) and
+// the stores in flight. Ordering under the stagger: the barrier that starts a wave's load phase st pairs
+// with the one that ends its partner group's load phase st - 1, so (RAW) step st + 1, retired by every
+// wave at the end of its load phase st - 1, is complete for both groups' reads in load phase st, and (WAR)
+// step st's buffers, read in every wave's load phase st - 1, are free when load phase st refills them.
 constexpr int Q_TK = 64;
 
 __device__ __forceinline__ int q_swz(int row) { return (row >> 1) & 7; }
@@ -620,7 +237,7 @@ __device__ __forceinline__ void linear_tn_pp64_body(const uint16_t *__restrict__
   constexpr int WG8 = WR / 8;                          // 8-row DMA groups of the weight image
   constexpr int NWS = (WG8 + 7) / 8, NXS = 4;          // pieces per wave and step
   constexpr int S = I * 4;
-  constexpr int VM = NXS, VM_EPI = NXS + S < 63 ? NXS + S : 63;
+  constexpr int VM = NXS, VM_EPI = VM + S < 63 ? VM + S : 63;  // X(st + 3)'s pieces (+ the stores)
   __shared__ __attribute__((aligned(16))) uint16_t lds[BIASO + WR];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -711,7 +328,7 @@ __device__ __forceinline__ void linear_tn_pp64_body(const uint16_t *__restrict__
   int st_epi = -8;
   // DMA cursors: W(st + 2) (K-step only: the weight tile is the workgroup's for every tile) and
   // X(st + 3) (tile, K-step)
-  int w_kc = 2 % nk, x_tl = 3 / nk, x_kc = 3 % nk;
+  int w_kc = NWB % nk, x_tl = NXB / nk, x_kc = NXB % nk;
   const int fl = wr * (WR / 2) + (lane >> 4) * 4, fb = static_cast<int>(nt * WR) + fl;
   if constexpr (BIAS) {
     for (int q = tid; q < WR; q += G_THREADS) lds[BIASO + q] = bias[nt * WR + q];
@@ -747,23 +364,19 @@ __device__ __forceinline__ void linear_tn_pp64_body(const uint16_t *__restrict__
     tl = st2 / nk, kc = st2 % nk;
   };
 
-  // prologue: W(0) X(0) W(1) X(1) X(2) issued; all but X(2) retired; step 0's fragments in registers
+  // prologue: W(0) X(0) W(1) X(1) X(2) issued, all but X(2) retired, step 0's fragments in registers
   {
     int tl, kc;
-    issue_w(0, 0);
-    clampx(0, tl, kc), issue_x(0, tl, kc);
-    issue_w(1, 1 % nk);
-    clampx(1, tl, kc), issue_x(1, tl, kc);
-    clampx(2, tl, kc), issue_x(2, tl, kc);
+    auto xs = [&](int st2) { clampx(st2, tl, kc), issue_x(st2, tl, kc); };
+    issue_w(0, 0), xs(0), issue_w(1, 1 % nk), xs(1), xs(2);
   }
-  p_vm_wait<NXS>();
+  p_vm_wait<VM>();
   asm volatile("s_barrier" ::: "memory");
   read(0);
   ready();
   if (wr == 1) asm volatile("s_barrier" ::: "memory");  // the stagger
   for (int st = 0; st < nsteps; ++st) {
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -771,15 +384,19 @@ __device__ __forceinline__ void linear_tn_pp64_body(const uint16_t *__restrict__
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q][i], fbb[q][j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_barrier" ::: "memory");
-    // load phase st
-    const bool w_in = st + 2 < nsteps, x_in = st + 3 < nsteps;
-    issue_w(st % NWB, w_in ? w_kc : nk - 1);
-    if (++w_kc == nk) w_kc = 0;
-    issue_x(st % NXB, x_in ? x_tl : static_cast<int>(ntiles) - 1, x_in ? x_kc : nk - 1);
-    if (++x_kc == nk) x_kc = 0, ++x_tl;
+    // load phase st: the shallow operand's step st + 2, then the deep one's step st + 3
+    const bool w_in = st + NWB < nsteps, x_in = st + NXB < nsteps;
+    auto dw = [&]() {
+      issue_w(st % NWB, w_in ? w_kc : nk - 1);
+      if (++w_kc == nk) w_kc = 0;
+    };
+    auto dx = [&]() {
+      issue_x(st % NXB, x_in ? x_tl : static_cast<int>(ntiles) - 1, x_in ? x_kc : nk - 1);
+      if (++x_kc == nk) x_kc = 0, ++x_tl;
+    };
+    dw(), dx();
     if (++kt == nk) {
       epilogue();
       st_epi = st;
@@ -798,244 +415,12 @@ __device__ __forceinline__ void linear_tn_pp64_body(const uint16_t *__restrict__
 }
 
 template <int I, bool BIAS>
-__device__ __forceinline__ void linear_tn_pp64s_body(const uint16_t *__restrict__ x, int64_t ldx,
-                                                    const uint16_t *__restrict__ w, int64_t ldw,
-                                                    const uint16_t *__restrict__ bias, int64_t M, int K, int64_t N,
-                                                    int per, uint16_t *__restrict__ y, int64_t ldy) {
-  constexpr int WR = 32 * I;
-  constexpr int WIMG = WR * Q_TK, XIMG = G_TM * Q_TK;  // bf16 elements of one stage
-  constexpr int NXB = 3, NWB = 2;                      // ring depths
-  constexpr int XBASE = 0, WBASE = NXB * XIMG, IDLE = WBASE + NWB * WIMG, BIASO = IDLE + 512;
-  constexpr int WG8 = WR / 8;                          // 8-row DMA groups of the weight image
-  constexpr int NWS = WG8 / 4, NXS = 8;                // pieces per loader wave and step
-  static_assert(WG8 % 4 == 0, "whole weight groups per loader wave");
-  constexpr int S = I * 4;
-  __shared__ __attribute__((aligned(16))) uint16_t lds[BIASO + WR];
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-
-  const int64_t n_nt = N / WR, n_mt = (M + G_TM - 1) / G_TM;
-  int64_t L = blockIdx.x;
-  {
-    const int64_t nl = gridDim.x >> 3;
-    L = (L & 7) * nl + (L >> 3);
-  }
-  const int64_t nt = L % n_nt, mt0 = (L / n_nt) * per;
-  const int64_t ntiles = n_mt - mt0 < per ? n_mt - mt0 : per;
-  if (ntiles <= 0) return;
-  const int nk = K / Q_TK;
-  const int nsteps = static_cast<int>(ntiles) * nk;
-
-  uint32_t xoff[NXS], woff[NWS];
-  int xdst[NXS], wdst[NWS];
-  const int lw = wave & 3;  // the wave's index among its group's four loaders
-#pragma unroll
-  for (int s2 = 0; s2 < NXS; ++s2) {
-    const int g = s2 * 4 + lw, row = g * 8 + (lane >> 3);
-    const int lc = (lane & 7) ^ q_swz(row);
-    xoff[s2] = static_cast<uint32_t>((row * ldx + lc * 8) * 2);
-    xdst[s2] = g * 8 * Q_TK;
-  }
-#pragma unroll
-  for (int s2 = 0; s2 < NWS; ++s2) {
-    const int g = s2 * 4 + lw;
-    const int row = g * 8 + (lane >> 3);
-    const int lc = (lane & 7) ^ q_swz(row);
-    woff[s2] = static_cast<uint32_t>((row * ldw + lc * 8) * 2);
-    wdst[s2] = g * 8 * Q_TK;
-  }
-  const __amdgpu_buffer_rsrc_t wres = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t *>(w + nt * WR * ldw), 0, static_cast<int>(WR * ldw * 2), 0x00020000);
-  auto issue_w = [&](int buf, int kc) {
-    uint16_t *img = lds + WBASE + buf * WIMG;
-    const int kb = kc * Q_TK * 2;
-#pragma unroll
-    for (int s2 = 0; s2 < NWS; ++s2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wres, img + wdst[s2], 16, woff[s2], kb, 0, 0);
-  };
-  auto issue_x = [&](int buf, int tl, int kc) {
-    const int64_t m0 = (mt0 + tl) * G_TM;
-    const int64_t rows = M - m0 < G_TM ? M - m0 : G_TM;
-    const __amdgpu_buffer_rsrc_t xres = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t *>(x + m0 * ldx), 0, static_cast<int>(rows * ldx * 2), 0x00020000);
-    uint16_t *img = lds + XBASE + buf * XIMG;
-    const int kb = kc * Q_TK * 2;
-#pragma unroll
-    for (int s2 = 0; s2 < NXS; ++s2) __builtin_amdgcn_raw_ptr_buffer_load_lds(xres, img + xdst[s2], 16, xoff[s2], kb, 0, 0);
-  };
-  bf16x8 fa[2][I], fbb[2][4];
-  auto read = [&](int step) {
-    const uint16_t *iw = lds + WBASE + (step % NWB) * WIMG, *ix = lds + XBASE + (step % NXB) * XIMG;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int c = q * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < I; ++i)
-        fa[q][i] = *reinterpret_cast<const bf16x8 *>(iw + q_img_off(wr * (WR / 2) + i * 16 + (lane & 15), c));
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        fbb[q][j] = *reinterpret_cast<const bf16x8 *>(ix + q_img_off(wc * 64 + j * 16 + (lane & 15), c));
-    }
-  };
-  auto ready = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[0][0]));
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-#pragma unroll
-      for (int i = 0; i < I; ++i) asm volatile("" : "+v"(fa[q][i]));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(fbb[q][j]));
-    }
-  };
-
-  f32x4 acc[I][4];
-#pragma unroll
-  for (int i = 0; i < I; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  int64_t mt = mt0;
-  int kt = 0;
-  // DMA cursors: W(st + 2) (K-step only: the weight tile is the workgroup's for every tile) and
-  // X(st + 3) (tile, K-step)
-  int w_kc = 2 % nk, x_tl = 3 / nk, x_kc = 3 % nk;
-  const int fl = wr * (WR / 2) + (lane >> 4) * 4, fb = static_cast<int>(nt * WR) + fl;
-  if constexpr (BIAS) {
-    for (int q = tid; q < WR; q += G_THREADS) lds[BIASO + q] = bias[nt * WR + q];
-    __syncthreads();
-  }
-  auto epilogue = [&]() {
-    const int64_t m0 = mt * G_TM;
-    const int64_t rows = M - m0 < G_TM ? M - m0 : G_TM;
-    const __amdgpu_buffer_rsrc_t yres = __builtin_amdgcn_make_buffer_rsrc(
-        y + m0 * ldy, 0, static_cast<int>(rows * ldy * 2), 0x00020000);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int tok = wc * 64 + j * 16 + (lane & 15);
-#pragma unroll
-      for (int i = 0; i < I; ++i) {
-        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-        if constexpr (BIAS) {
-          const uint2 bb = *reinterpret_cast<const uint2 *>(lds + BIASO + fl + i * 16);
-          v0 += bf16_lo(bb.x), v1 += bf16_hi(bb.x), v2 += bf16_lo(bb.y), v3 += bf16_hi(bb.y);
-        }
-        typedef int v2i __attribute__((ext_vector_type(2)));
-        const v2i qv = {static_cast<int>(pack2_bf16(v0, v1)), static_cast<int>(pack2_bf16(v2, v3))};
-        __builtin_amdgcn_raw_buffer_store_b64(qv, yres, (tok * static_cast<int>(ldy) + fb + i * 16) * 2, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < I; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
-  auto clampx = [&](int step, int &tl, int &kc) {  // step -> (tile, K-step); past the end: the last step
-    const int st2 = step < nsteps ? step : nsteps - 1;
-    tl = st2 / nk, kc = st2 % nk;
-  };
-
-  // prologue: the weight loaders (waves 4-7) issue W(0), W(1) and retire both; the token loaders (waves
-  // 0-3) X(0), X(1), X(2) and retire all but X(2); step 0's fragments in registers
-  const bool wload = wr == 1;
-  if (wload) {
-    issue_w(0, 0);
-    issue_w(1, 1 % nk);
-    p_vm_wait<0>();
-  } else {
-    int tl, kc;
-    clampx(0, tl, kc), issue_x(0, tl, kc);
-    clampx(1, tl, kc), issue_x(1, tl, kc);
-    clampx(2, tl, kc), issue_x(2, tl, kc);
-    p_vm_wait<NXS>();
-  }
-  asm volatile("s_barrier" ::: "memory");
-  read(0);
-  ready();
-  if (wload) asm volatile("s_barrier" ::: "memory");  // the stagger
-  for (int st = 0; st < nsteps; ++st) {
-    __builtin_amdgcn_sched_barrier(0);
-    // MFMA phase; a weight loader first issues W(st + 2) into step st's weight buffer, free since every
-    // wave's load phase st - 1 (see above)
-    if (wload) {
-      issue_w(st % NWB, st + 2 < nsteps ? w_kc : nk - 1);
-      if (++w_kc == nk) w_kc = 0;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int i = 0; i < I; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[q][i], fbb[q][j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_barrier" ::: "memory");
-    // load phase st: a token loader issues X(st + 3); the epilogue at a tile's end; step st + 1's
-    // fragments; then the token loaders retire X(st + 2) (X(st + 3) and the stores stay in flight), the
-    // weight loaders W(st + 2) (the stores stay in flight)
-    if (!wload) {
-      const bool x_in = st + 3 < nsteps;
-      issue_x(st % NXB, x_in ? x_tl : static_cast<int>(ntiles) - 1, x_in ? x_kc : nk - 1);
-      if (++x_kc == nk) x_kc = 0, ++x_tl;
-    }
-    const bool epi = ++kt == nk;
-    if (epi) {
-      epilogue();
-      kt = 0;
-      ++mt;
-    }
-    if (st + 1 < nsteps) read(st + 1);
-    if (wload) {
-      if (epi) p_vm_wait<S>();
-      else p_vm_wait<0>();
-    } else {
-      if (epi) p_vm_wait<NXS + S>();
-      else p_vm_wait<NXS>();
-    }
-    ready();
-    asm volatile("s_barrier" ::: "memory");
-  }
-  if (!wload) asm volatile("s_barrier" ::: "memory");
-  p_vm_wait<0>();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-template <int I, bool BIAS>
-__global__ __launch_bounds__(G_THREADS, 1) void linear_tn_pp64s_kernel(const uint16_t *__restrict__ x, int64_t ldx,
-                                                                       const uint16_t *__restrict__ w, int64_t ldw,
-                                                                       const uint16_t *__restrict__ bias, int64_t M,
-                                                                       int K, int64_t N, int per,
-                                                                       uint16_t *__restrict__ y, int64_t ldy) {
-  linear_tn_pp64s_body<I, BIAS>(x, ldx, w, ldw, bias, M, K, N, per, y, ldy);
-}
-
-template <int I, bool BIAS>
 __global__ __launch_bounds__(G_THREADS, 1) void linear_tn_pp64_kernel(const uint16_t *__restrict__ x, int64_t ldx,
                                                                       const uint16_t *__restrict__ w, int64_t ldw,
                                                                       const uint16_t *__restrict__ bias, int64_t M,
                                                                       int K, int64_t N, int per,
                                                                       uint16_t *__restrict__ y, int64_t ldy) {
   linear_tn_pp64_body<I, BIAS>(x, ldx, w, ldw, bias, M, K, N, per, y, ldy);
-}
-
-template <int I, int NST, bool BIAS, int PROBE = 0>
-__global__ __launch_bounds__(G_THREADS, 1) void linear_tn_pp_kernel(const uint16_t *__restrict__ x, int64_t ldx,
-                                                                    const uint16_t *__restrict__ w, int64_t ldw,
-                                                                    const uint16_t *__restrict__ bias, int64_t M, int K,
-                                                                    int64_t N, int per, uint16_t *__restrict__ y,
-                                                                    int64_t ldy) {
-  linear_tn_pp_body<I, NST, BIAS, PROBE>(x, ldx, w, ldw, bias, M, K, N, per, y, ldy);
-}
-
-template <int I, int WC, int NST, bool BIAS>
-__global__ __launch_bounds__(128 * WC, 1) void linear_tn_pipe_kernel(const uint16_t *__restrict__ x, int64_t ldx,
-                                                                      const uint16_t *__restrict__ w, int64_t ldw,
-                                                                      const uint16_t *__restrict__ bias, int64_t M,
-                                                                      int K, int64_t N, int per,
-                                                                      uint16_t *__restrict__ y, int64_t ldy) {
-  linear_tn_pipe_body<I, WC, NST, BIAS>(x, ldx, w, ldw, bias, M, K, N, per, y, ldy);
 }
 
 template <int I, bool BIAS, bool REMAP, bool LOCK>
@@ -1063,28 +448,9 @@ int pick_tile(int64_t N, bool pipe) {
 
 using namespace va;
 
-// va_set_tuning(VA_TUNE_LINEAR_TN): 4 = the ping-pong form; 2 / 3 = the pipelined form with a 4 / 5-stage
-// ring; 1 / 0 = the two-buffer form in LOCK / list
+// va_set_tuning(VA_TUNE_LINEAR_TN): 2 = the ping-pong form; 1 / 0 = the two-buffer form in LOCK / list
 // tile order (see linear_tn_body)
 int g_linear_tn = 2;
-
-template <int I, int NST>
-static void launch_tn_pp(bool has_b, int64_t nwg, hipStream_t s, const uint16_t *x, int64_t ldx, const uint16_t *w,
-                         int64_t ldw, const uint16_t *b, int64_t M, int64_t N, int64_t K, int per, uint16_t *y,
-                         int64_t ldy) {
-  const auto kern = has_b ? linear_tn_pp_kernel<I, NST, true> : linear_tn_pp_kernel<I, NST, false>;
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nwg)), dim3(G_THREADS), 0, s, x, ldx, w, ldw, b, M,
-                     static_cast<int>(K), N, per, y, ldy);
-}
-
-template <int I, int WC, int NST>
-static void launch_tn_pipe(bool has_b, int64_t nwg, hipStream_t s, const uint16_t *x, int64_t ldx, const uint16_t *w,
-                           int64_t ldw, const uint16_t *b, int64_t M, int64_t N, int64_t K, int per, uint16_t *y,
-                           int64_t ldy) {
-  const auto kern = has_b ? linear_tn_pipe_kernel<I, WC, NST, true> : linear_tn_pipe_kernel<I, WC, NST, false>;
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nwg)), dim3(128 * WC), 0, s, x, ldx, w, ldw, b, M,
-                     static_cast<int>(K), N, per, y, ldy);
-}
 
 template <int I, bool LOCK>
 static void launch_tn(bool remap, bool has_b, int64_t nwg, hipStream_t s, const uint16_t *x, int64_t ldx,
@@ -1104,13 +470,13 @@ static void launch_tn(bool lock, bool remap, bool has_b, int64_t nwg, hipStream_
   else launch_tn<I, false>(remap, has_b, nwg, s, x, ldx, w, ldw, b, M, N, K, per, y, ldy);
 }
 
-extern "C" int va_linear_tn_tile(int64_t N) { return pick_tile(N, g_linear_tn >= 2); }
+extern "C" int va_linear_tn_tile(int64_t N) { return pick_tile(N, g_linear_tn == 2); }
 
 extern "C" int va_linear_tn(const void *x, int64_t ldx, const void *w, int64_t ldw, const void *bias, int dtype,
                             int64_t M, int64_t N, int64_t K, int tile_n, int per, void *y, int64_t ldy,
                             void *stream) {
   VA_CHECK_ARG(dtype == VA_BF16, "linear_tn: only bf16 is implemented");
-  if (tile_n == 0) tile_n = pick_tile(N, g_linear_tn >= 2);
+  if (tile_n == 0) tile_n = pick_tile(N, g_linear_tn == 2);
   VA_CHECK_ARG(tile_n == 192 || tile_n == 224 || tile_n == 256 || tile_n == 288,
                "linear_tn: no output tile of {192, 224, 256, 288} divides N=%lld", static_cast<long long>(N));
   VA_CHECK_ARG(M >= 0 && N > 0 && N % tile_n == 0 && K > 0 && K % G_TK == 0 && K <= (1 << 20),
@@ -1128,9 +494,8 @@ extern "C" int va_linear_tn(const void *x, int64_t ldx, const void *w, int64_t l
                "linear_tn: 16-byte aligned x / w, 8-byte aligned y / bias required");
   const int64_t n_nt = N / tile_n, n_mt = (M + G_TM - 1) / G_TM;
   const bool lock = g_linear_tn >= 1 && n_nt <= 32;  // (wider outputs: list order, two-buffer form)
-  // the pipelined form needs a K of at least its ring (4 / 5 steps of 32); shorter: the two-buffer form
-  const bool pipe = g_linear_tn >= 2 && lock && K >= (g_linear_tn == 3 || g_linear_tn == 8 ? 5 : 4) * P_TK &&
-                    (g_linear_tn < 9 || K >= 3 * Q_TK);  // (ping-pong: 4)
+  // the ping-pong form needs K >= 3 steps of 64 (its prologue fills the token ring); shorter: two-buffer
+  const bool pipe = g_linear_tn == 2 && lock && K >= 3 * Q_TK;  // (ping-pong: 4)
   // automatic: one round of the 256 CUs (one 512-thread workgroup per CU), tiles spread evenly; in LOCK
   // order whole groups of 8 token ranges (the grid is padded to multiples of 8 n_nt workgroups)
   if (per == 0) {
@@ -1159,36 +524,12 @@ extern "C" int va_linear_tn(const void *x, int64_t ldx, const void *w, int64_t l
   const auto *w16 = static_cast<const uint16_t *>(w);
   const auto *b16 = static_cast<const uint16_t *>(bias);
   auto *y16 = static_cast<uint16_t *>(y);
-  if (pipe && (tile_n == 192 || tile_n == 224)) {  // the two register sets fit these wave tiles only
-    if (g_linear_tn == 10) {  // ping-pong, 64-deep steps, split loaders
-      const auto kern = tile_n == 192 ? (has_b ? linear_tn_pp64s_kernel<6, true> : linear_tn_pp64s_kernel<6, false>)
-                                      : (has_b ? linear_tn_pp64s_kernel<7, true> : linear_tn_pp64s_kernel<7, false>);
-      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nwg)), dim3(G_THREADS), 0, s, x16, ldx, w16, ldw, b16, M,
-                         static_cast<int>(K), N, per, y16, ldy);
-    } else if (g_linear_tn == 9) {  // ping-pong, 64-deep steps
-      const auto kern = tile_n == 192 ? (has_b ? linear_tn_pp64_kernel<6, true> : linear_tn_pp64_kernel<6, false>)
-                                      : (has_b ? linear_tn_pp64_kernel<7, true> : linear_tn_pp64_kernel<7, false>);
-      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nwg)), dim3(G_THREADS), 0, s, x16, ldx, w16, ldw, b16, M,
-                         static_cast<int>(K), N, per, y16, ldy);
-    } else if (g_linear_tn == 8) {  // ping-pong, 5-stage ring
-      if (tile_n == 192) launch_tn_pp<6, 5>(has_b, nwg, s, x16, ldx, w16, ldw, b16, M, N, K, per, y16, ldy);
-      else launch_tn_pp<7, 5>(has_b, nwg, s, x16, ldx, w16, ldw, b16, M, N, K, per, y16, ldy);
-    } else if (g_linear_tn >= 5) {  // timing probes (wrong results): 5 no operand traffic, 6 one token block, 7 no stagger
-      const int pr = g_linear_tn - 4;
-      const auto kern = pr == 1 ? linear_tn_pp_kernel<7, 4, false, 1>
-                                : (pr == 2 ? linear_tn_pp_kernel<7, 4, false, 2> : linear_tn_pp_kernel<7, 4, false, 3>);
-      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nwg)), dim3(G_THREADS), 0, s, x16, ldx, w16, ldw, b16, M,
-                         static_cast<int>(K), N, per, y16, ldy);
-    } else if (g_linear_tn == 4) {  // ping-pong
-      if (tile_n == 192) launch_tn_pp<6, 4>(has_b, nwg, s, x16, ldx, w16, ldw, b16, M, N, K, per, y16, ldy);
-      else launch_tn_pp<7, 4>(has_b, nwg, s, x16, ldx, w16, ldw, b16, M, N, K, per, y16, ldy);
-    } else if (g_linear_tn == 3) {  // 5-stage ring
-      if (tile_n == 192) launch_tn_pipe<6, 4, 5>(has_b, nwg, s, x16, ldx, w16, ldw, b16, M, N, K, per, y16, ldy);
-      else launch_tn_pipe<7, 4, 5>(has_b, nwg, s, x16, ldx, w16, ldw, b16, M, N, K, per, y16, ldy);
-    } else {
-      if (tile_n == 192) launch_tn_pipe<6, 4, 4>(has_b, nwg, s, x16, ldx, w16, ldw, b16, M, N, K, per, y16, ldy);
-      else launch_tn_pipe<7, 4, 4>(has_b, nwg, s, x16, ldx, w16, ldw, b16, M, N, K, per, y16, ldy);
-    }
+  // its registers fit the 192-wide wave tiles and the 224-wide ones without a bias (with one: 9 spills)
+  if (pipe && (tile_n == 192 || (tile_n == 224 && !has_b))) {
+    const auto kern = tile_n == 192 ? (has_b ? linear_tn_pp64_kernel<6, true> : linear_tn_pp64_kernel<6, false>)
+                                    : linear_tn_pp64_kernel<7, false>;
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nwg)), dim3(G_THREADS), 0, s, x16, ldx, w16, ldw, b16, M,
+                       static_cast<int>(K), N, per, y16, ldy);
     return check_launch("linear_tn");
   }
   switch (tile_n) {

@@ -760,8 +760,8 @@ extern "C" int va_set_tuning(int key, int value) {
       g_wgrad_kind = value;
       return VA_OK;
     case VA_TUNE_LINEAR_TN:
-      if (value < 0 || value > 10) {
-        va::set_error("va_set_tuning: VA_TUNE_LINEAR_TN must be 0 .. 10");
+      if (value < 0 || value > 2) {
+        va::set_error("va_set_tuning: VA_TUNE_LINEAR_TN must be 0 .. 2");
         return VA_E_ARG;
       }
       g_linear_tn = value;
