@@ -83,12 +83,12 @@ def _shard_run(hidden, weight, labels, T, tp, g_lp, g_ent):
 
     V = weight.shape[0]
     vs = V // tp
-    parts = [K._linear_logprob_fwd_raw(hidden, weight[r * vs:(r + 1) * vs], labels - r * vs, T, fp32_logits=True)
-             for r in range(tp)]
+    parts = [K._linear_logprob_fwd_raw(hidden, weight[r * vs:(r + 1) * vs], labels - r * vs, T, fp32_logits=True,
+                                       with_label_logit=True) for r in range(tp)]
     m = torch.stack([p[2] for p in parts]).max(0).values
     packed = None
     outs = []
-    for r, (lp_l, ent_l, lse_l) in enumerate(parts):
+    for r, (lp_l, ent_l, lse_l, xl) in enumerate(parts):
         cap = {}
 
         def amax(t):
@@ -97,16 +97,16 @@ def _shard_run(hidden, weight, labels, T, tp, g_lp, g_ent):
         def asum(t, cap=cap):
             cap["t"] = t
 
-        tp_merge(labels, r * vs, vs, V, lp_l, ent_l, lse_l, amax, asum)
+        tp_merge(labels, r * vs, vs, V, lp_l, ent_l, lse_l, amax, asum, label_logit_l=xl)
         packed = cap["t"].clone() if packed is None else packed + cap["t"]
-    for r, (lp_l, ent_l, lse_l) in enumerate(parts):
+    for r, (lp_l, ent_l, lse_l, xl) in enumerate(parts):
         def amax(t):
             t.copy_(m)
 
         def asum(t):
             t.copy_(packed)
 
-        outs.append(tp_merge(labels, r * vs, vs, V, lp_l, ent_l, lse_l, amax, asum))
+        outs.append(tp_merge(labels, r * vs, vs, V, lp_l, ent_l, lse_l, amax, asum, label_logit_l=xl))
     logp, ent, lse = outs[0]
     for o in outs[1:]:
         assert all(torch.equal(a, b) for a, b in zip(o, outs[0]))  # every rank sees the same result

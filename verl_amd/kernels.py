@@ -185,7 +185,10 @@ def _linear_logprob_splits(n_rows: int, vocab: int | None = None) -> int:
 
 
 def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float, fp32_logits: bool = False,
-                            splits: int | None = None):
+                            splits: int | None = None, with_label_logit: bool = False):
+    """(logp, entropy, lse) [N] fp32 by va_linear_logprob_fwd; with_label_logit: also the label's logit
+    x[label] as the kernel saw it (its workspace's label-logit column; written only for rows whose label
+    lies in [0, V) — the tensor-parallel merge reads it for the rows its shard holds)."""
     N, H = hidden.shape
     V = weight.shape[0]
     splits = _linear_logprob_splits(N) if splits is None else int(splits)
@@ -200,6 +203,8 @@ def _linear_logprob_fwd_raw(hidden, weight, labels, temperature: float, fp32_log
            N, H, V, float(temperature), splits, _p(logp), _p(ent), _p(lse), _p(ws), _stream(hidden))
     if ev is not None:  # MFMA-bound: algorithmic flops 2 N V H
         TIMER.stop("linear_logprob_fwd", 2 * N * V * H, torch.cuda.current_stream(hidden.device), ev)
+    if with_label_logit:  # va_linear_logprob_fwd's workspace: [splits][N][3] partial states, then [N] label logits
+        return logp, ent, lse, ws[splits * N * 3: splits * N * 3 + N]
     return logp, ent, lse
 
 

@@ -40,18 +40,18 @@ def _reduction_code(reduction: str) -> int:
 
 
 def tp_merge(labels, vocab_offset: int, vocab_shard: int, vocab_total: int, logp_l, ent_l, lse_l,
-             all_reduce_max, all_reduce_sum):
+             all_reduce_max, all_reduce_sum, label_logit_l=None):
     """Merge one vocabulary shard's per-row (logp, entropy, lse) — the shard's own softmax, labels
     shifted into the shard — into the whole vocabulary's, given the group's MAX / SUM all-reduces:
       m = max_r lse_r, A = sum_r e^{lse_r - m}, B = sum_r e^{lse_r - m} (lse_r - H_r),
       lse = m + ln A, H = lse - B / A, logp = x[label] - lse,
     x[label] contributed by the shard that holds it. Labels: -100 (ignore_index) gives 0, other ids
-    outside the vocabulary NaN, as va_linear_logprob_fwd. Precision note: x[label] is
-    rebuilt as logp_r + lse_r in fp32, so it carries ~ulp(lse_r) of rounding where the reference
-    all-reduces the raw label logit (epilogue_tp); vocab tensor parallelism is outside SURVEY §8
-    (§2 row 17), so this adapter is kept as is rather than widened to return the raw logit."""
+    outside the vocabulary NaN, as va_linear_logprob_fwd. x[label] is the raw label logit of the shard
+    that holds it (``label_logit_l``, the kernel's own value), all-reduced as the reference's epilogue_tp
+    does; without it, rebuilt as logp_r + lse_r in fp32 (~ulp(lse_r) of rounding)."""
     in_shard = (labels >= vocab_offset) & (labels < vocab_offset + vocab_shard)
-    xlab = torch.where(in_shard, logp_l + lse_l, torch.zeros_like(lse_l))
+    xl = logp_l + lse_l if label_logit_l is None else label_logit_l
+    xlab = torch.where(in_shard, xl, torch.zeros_like(lse_l))
     m = lse_l.clone()
     all_reduce_max(m)
     s = torch.exp(lse_l - m)
@@ -92,11 +92,12 @@ class LinearCrossEntropy(torch.autograd.Function):
                 raise ValueError(f"linear_cross_entropy: a vocabulary shard must be a multiple of 4 rows, got {vs}")
             rank, world = dist.get_rank(dist_process_group), dist.get_world_size(dist_process_group)
             off, total = rank * vs, world * vs
-            logp_l, ent_l, lse_l = K._linear_logprob_fwd_raw(h, w, lab - off, temperature, fp32_logits=True)
+            logp_l, ent_l, lse_l, xl = K._linear_logprob_fwd_raw(h, w, lab - off, temperature, fp32_logits=True,
+                                                                 with_label_logit=True)
             logp, ent, lse = tp_merge(
                 lab, off, vs, total, logp_l, ent_l, lse_l,
                 lambda t: dist.all_reduce(t, op=dist.ReduceOp.MAX, group=dist_process_group),
-                lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=dist_process_group))
+                lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=dist_process_group), label_logit_l=xl)
         ctx.save_for_backward(h, w, lab, lse, ent)
         ctx.hidden_shape = shape
         ctx.reduction = red
