@@ -152,37 +152,7 @@ def test_actor_fused_no_grad_logprob_matches_unfused():
 
 
 # ------------------------------------------------------------------ fused backward (va_linear_logprob_bwd)
-@pytest.mark.parametrize("N,H,V", [(300, 64, 1000), (256, 896, 151936), (77, 128, 36), (1, 64, 132)])
-@pytest.mark.parametrize("T", [1.0, 0.7])
-@pytest.mark.parametrize("ent_grad", [False, True])
-def test_fused_backward_dlogits_bitwise_on_exact_logits(N, H, V, T, ent_grad, tile):
-    """the fused backward recomputes the logits inside its MFMA tiles and forms
-    dlogits in registers. On exact-arithmetic data (every GEMM order gives the same logits) its bf16
-    dlogits equal bitwise those of the unfused composition — bf16 logits in HBM, then the streaming
-    va_logprob_entropy_bwd — given the same (lse, entropy) and upstream gradients, including
-    ignore_index / out-of-range labels, rows past a 256-row block and vocab tails."""
-    if tile != 256:
-        pytest.skip("one backward kernel (the forward's tile setting does not apply)")
-    from verl_amd import kernels as K
-
-    h, w = _exact_inputs(N, H, V, seed=N * 3 + V)
-    g = torch.Generator().manual_seed(N + H)
-    labels = torch.randint(0, V, (N,), generator=g)
-    if N > 2:
-        labels[0], labels[1] = -100, V + 3
-    labels[-1] = V - 1
-    logits = (h.float() @ w.float().t()).to(torch.bfloat16).to(DEV)  # exact fp32 sums, one rounding
-    h, w, labels = h.to(DEV), w.to(DEV), labels.to(DEV)
-    _, ent, lse = torch.ops.verl_amd.logprob_entropy_fwd(logits, labels, T, 0)
-    g1 = torch.randn(N, generator=g).to(DEV)
-    g2 = torch.randn(N, generator=g).to(DEV) if ent_grad else None
-    want = torch.ops.verl_amd.logprob_entropy_bwd(g1, g2, logits, labels, lse, ent, T)
-    got = torch.full((N, V + 4), 7.0, dtype=torch.bfloat16, device=DEV)[:, :V]  # row stride > V
-    K._linear_logprob_bwd_raw(h, w, labels, lse, ent, g1, g2, T, False, got)
-    assert torch.equal(torch.isnan(got), torch.isnan(want))
-    assert torch.equal(torch.nan_to_num(got), torch.nan_to_num(want)), (got.float() - want.float()).abs().max()
-
-
+# (the kernel-level backward tests, which no forward tile setting affects: test_linear_logprob_bwd_gpu.py)
 @pytest.mark.parametrize("f32", [False, True])
 @pytest.mark.parametrize("vocab_split", [9504, 40000])
 def test_fused_backward_equals_composition(f32, vocab_split, tile, monkeypatch):
@@ -216,43 +186,6 @@ def test_fused_backward_equals_composition(f32, vocab_split, tile, monkeypatch):
         err = ((a - b).norm() / b.norm()).item()
         assert err < 1e-2, f"{what}: relative L2 error {err:.3e}"
 
-
-
-@pytest.mark.parametrize("N,H,V,bounds", [
-    (300, 64, 1000, [0, 300, 604, 1000]),       # ranges not multiples of the 256-wide tile
-    (256, 896, 151936, list(range(0, 151936, 9504)) + [151936]),  # the reference's vocab_per_split
-    (77, 128, 38, [0, 4, 36, 38]),              # V % 4 != 0: every range but the last is a multiple of 4
-])
-@pytest.mark.parametrize("T", [1.0, 0.7])
-def test_vocab_range_dlogits_equal_the_whole_vocab_launch(N, H, V, bounds, T, tile):
-    """ABI 6: va_linear_logprob_bwd over vocab ranges [v0, v1) writes exactly the columns v0..v1 of
-    the whole-vocabulary launch, bitwise: the labels (ignore_index, out of range, in every range)
-    and the g_logp term of the softmax gradient count against the whole vocabulary. Where V % 4 != 0
-    the whole launch is not allowed, so the last 2 columns are compared with the unfused
-    composition."""
-    if tile != 256:
-        pytest.skip("one backward kernel")
-    from verl_amd import kernels as K
-
-    h, w = _exact_inputs(N, H, V, seed=N + 2 * V)
-    g = torch.Generator().manual_seed(V)
-    labels = torch.randint(0, V, (N,), generator=g)
-    labels[0], labels[1], labels[2] = -100, V + 3, V - 1
-    logits = (h.float() @ w.float().t()).to(torch.bfloat16).to(DEV)
-    h, w, labels = h.to(DEV), w.to(DEV), labels.to(DEV)
-    _, ent, lse = torch.ops.verl_amd.logprob_entropy_fwd(logits, labels, T, 0)
-    g1, g2 = torch.randn(N, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV)
-    want = torch.ops.verl_amd.logprob_entropy_bwd(g1, g2, logits, labels, lse, ent, T)
-    if V % 4 == 0:
-        whole = torch.empty(N, V, dtype=torch.bfloat16, device=DEV)
-        K._linear_logprob_bwd_raw(h, w, labels, lse, ent, g1, g2, T, False, whole)
-        assert torch.equal(torch.nan_to_num(whole), torch.nan_to_num(want))
-    for v0, v1 in zip(bounds[:-1], bounds[1:]):
-        if (v1 - v0) % 4:
-            continue
-        part = torch.full((N, v1 - v0 + 8), 7.0, dtype=torch.bfloat16, device=DEV)[:, : v1 - v0]
-        K._linear_logprob_bwd_raw(h, w, labels, lse, ent, g1, g2, T, False, part, v0, v1)
-        assert torch.equal(torch.nan_to_num(part), torch.nan_to_num(want[:, v0:v1])), (v0, v1)
 
 
 def test_vocab_split_backward_holds_one_range_of_dlogits(monkeypatch):
