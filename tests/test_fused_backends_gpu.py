@@ -61,6 +61,37 @@ def test_linear_cross_entropy_matches_reference_torch(reduction, V):
     torch.testing.assert_close(w1.grad.float(), w2.grad.float(), atol=2e-2, rtol=4e-2)
 
 
+@pytest.mark.parametrize("method", ["_Total_Separate", "_Total_Fuse_MN"])
+def test_backward_methods_give_the_split_dlogits_gradients(method):
+    """kernels.set_backward_method (the reference's kernels.py:112-117): _Total_Separate runs one
+    vocabulary range ([N, V] dlogits), _Total_Fuse_MN the vocabulary-range path; both give the default
+    _Split_Dlogits_N gradients up to fp32 summation order of the d_hidden ranges (here 16 ranges vs 1)."""
+    from verl_amd.utils.kernel import kernels as KK
+    from verl_amd.utils.kernel.linear_cross_entropy import linear_cross_entropy
+
+    hidden, weight, labels = _inputs(N=512, V=151936, seed=5)
+    g = torch.Generator(device=DEV).manual_seed(2)
+    g_lp, g_ent = torch.randn(512, device=DEV, generator=g), torch.randn(512, device=DEV, generator=g)
+    grads = {}
+    try:
+        for m in ("_Split_Dlogits_N", method):
+            KK.set_backward_method(getattr(KK.BackwardEnum, m))
+            h, w = hidden.clone().requires_grad_(True), weight.clone().requires_grad_(True)
+            lp, ent = linear_cross_entropy(h, w, labels, 1.0, "none")
+            torch.autograd.backward([lp, ent], [g_lp, g_ent])
+            grads[m] = (h.grad.float(), w.grad.float())
+        KK.set_backward_method(KK.BackwardEnum._Split_Dlogits_M)
+        h = hidden.clone().requires_grad_(True)
+        lp, ent = linear_cross_entropy(h, weight, labels, 1.0, "none")
+        with pytest.raises(NotImplementedError):
+            lp.sum().backward()
+    finally:
+        KK.set_backward_method(KK.BackwardEnum._Split_Dlogits_N)
+    a, b = grads["_Split_Dlogits_N"], grads[method]
+    assert torch.equal(a[1], b[1])  # d_weight: per vocabulary row, one K-sum either way
+    assert ((a[0] - b[0]).norm() / a[0].norm()).item() < 1e-5
+
+
 def test_linear_cross_entropy_shapes_and_contract():
     from verl_amd.utils.kernel.linear_cross_entropy import linear_cross_entropy
 

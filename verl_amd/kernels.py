@@ -278,7 +278,8 @@ class _LinearLogprob(torch.autograd.Function):
         N, H = hidden.shape
         V = weight.shape[0]
         need_h, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        width = min(V, max(256, _LinearLogprob.VOCAB_PER_SPLIT // 8 * 8))
+        per = getattr(ctx, "vocab_per_split", None) or _LinearLogprob.VOCAB_PER_SPLIT
+        width = min(V, max(256, per // 8 * 8))
         buf, width = _LinearLogprob._range_buffer(N, width, hidden.dtype, hidden.device)
         # dX over a transposed copy of W ("TN", as input_grad); each range is a column slice of it
         wt = transpose16(weight) if need_h and _DGRAD_TN and weight.dtype == torch.bfloat16 else None

@@ -27,6 +27,7 @@ import torch
 import torch.distributed as dist
 
 from ... import kernels as K
+from . import kernels as _cfg
 
 # EntropyReductionEnum (kernels.py:60-70)
 REDUCTIONS = {"none": 0, "sum": 1, "mean": 2}
@@ -129,9 +130,12 @@ class LinearCrossEntropy(torch.autograd.Function):
                                          fp32_logits=True)
             d_hidden, d_weight = K._LinearLogprob._compose_backward(kctx, h, w, lab, lse, ent, g1, g2)
         else:
+            # the dlogits range width of the configured backward method (kernels.set_backward_method)
             kctx = types.SimpleNamespace(needs_input_grad=(need_h, need_w), temperature=ctx.temperature,
                                          fp32_logits=True, vocab_offset=ctx.vocab_offset,
-                                         vocab_total=ctx.vocab_total)
+                                         vocab_total=ctx.vocab_total,
+                                         vocab_per_split=_cfg.backward_vocab_per_split(
+                                             w.shape[0], K._LinearLogprob.VOCAB_PER_SPLIT))
             d_hidden, d_weight = K._LinearLogprob._vocab_split_backward(kctx, h, w, lab, lse, ent, g1, g2)
         if d_hidden is not None:
             d_hidden = d_hidden.view(ctx.hidden_shape)
