@@ -21,6 +21,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CASES = [  # name, K, N, bias, runs per layer and update pass (forwards: no-grad + update)
     ("o_fwd", 896, 896, False, 2), ("qkv_fwd", 896, 1152, True, 2), ("down_fwd", 4864, 896, False, 2),
     ("o_dgrad", 896, 896, False, 1), ("qkv_dgrad", 1152, 896, False, 1), ("gateup_dgrad", 9728, 896, False, 1)]
+# opt-in (--cases): the lm_head's input gradient dH = dlogits W over the transposed weight, 131,072 rows,
+# once per update pass (runs counted per layer: 1 / 24)
+EXTRA = {"lmhead_dgrad": (151936, 896, False, 1 / 24, 131072)}
 
 
 def main():
@@ -44,8 +47,9 @@ def main():
     g = torch.Generator(device=dev).manual_seed(4)
     own_arms = [tuple(int(v) for v in a.split("/")) for a in args.arms.split(",")]
     totals = {"hipblaslt": 0.0, "own_best": 0.0, "mixed_best": 0.0}
-    for name, k, n, has_bias, runs in CASES:
-        if args.cases and name not in args.cases.split(","):
+    cases = [c + (args.tokens,) for c in CASES] + [(nm, *v) for nm, v in EXTRA.items()]
+    for name, k, n, has_bias, runs, T in cases:
+        if (args.cases and name not in args.cases.split(",")) or (not args.cases and name in EXTRA):
             continue
         x = torch.randn(T, k, device=dev, generator=g).to(torch.bfloat16)
         w = (torch.randn(n, k, device=dev, generator=g) * 0.03).to(torch.bfloat16)
@@ -89,7 +93,7 @@ def main():
         fl = 2.0 * T * k * n
         rel = {} if ref is None else {a: float((o.float() - ref).norm() / ref.norm()) for a, o in outs.items()}
         same = {a: bool(torch.equal(o, outs["hipblaslt"])) for a, o in outs.items() if a != "hipblaslt"}
-        per_step = 24 * args.passes * runs
+        per_step = round(24 * args.passes * runs)
         totals["hipblaslt"] += med["hipblaslt"] * per_step / 1e3
         own_med = [v for a, v in med.items() if a != "hipblaslt"]
         if own_med:
