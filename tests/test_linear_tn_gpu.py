@@ -128,3 +128,5 @@ def test_tile_query_and_argument_checks():
         L.call("va_set_tuning", L.VA_TUNE_LINEAR_TN, 3)
     with pytest.raises(RuntimeError, match="strides"):
         L.call("va_linear_tn", K._p(x), 64, K._p(w), 128, None, L.VA_BF16, 64, 224, 128, 0, 0, K._p(y), 224, s)
+    with pytest.raises(RuntimeError, match="strides"):  # the output's 32-bit buffer offsets
+        L.call("va_linear_tn", K._p(x), 128, K._p(w), 128, None, L.VA_BF16, 64, 224, 128, 0, 0, K._p(y), 1 << 22, s)

@@ -483,7 +483,8 @@ extern "C" int va_linear_tn(const void *x, int64_t ldx, const void *w, int64_t l
                "linear_tn: need N %% %d == 0 and K %% 64 == 0 (N=%lld, K=%lld)", tile_n, static_cast<long long>(N),
                static_cast<long long>(K));
   VA_CHECK_ARG(ldx >= K && ldw >= K && ldx % 8 == 0 && ldw % 8 == 0 && ldx < (1 << 22) &&
-                   static_cast<int64_t>(tile_n) * ldw * 2 < (int64_t{1} << 31) && ldy >= N && ldy % 4 == 0,
+                   static_cast<int64_t>(tile_n) * ldw * 2 < (int64_t{1} << 31) && ldy >= N && ldy % 4 == 0 &&
+                   ldy < (1 << 22),
                "linear_tn: strides must be >= K (ldy >= N), %% 8 (ldy %% 4), < 2^22 / tile_n ldw 2 < 2^31 "
                "(32-bit buffer offsets)");
   VA_CHECK_ARG(per >= 0, "linear_tn: negative tiles per workgroup");
