@@ -128,3 +128,37 @@ def test_adamw_flat_rejects_bad_arguments():
     with pytest.raises(RuntimeError, match="aligned"):
         L.call("va_adamw_flat", K._p(t[1:]), K._p(t), K._p(t), K._p(t), 8, 1e-3, 0.9, 0.999, 1e-8, 0.0, K._p(s), None,
                None, 0, K._stream(t))
+
+
+def test_state_dict_round_trip_resumes_bitwise():
+    """A checkpoint of FlatAdamW (torch's Optimizer.state_dict) loaded into a fresh one resumes the
+    same trajectory bit for bit: the loaded moments and step land in the flat buffers the kernel updates."""
+    import copy as _copy
+
+    from verl_amd.workers.grad_sync import FlatAdamW
+
+    (a, ma, oa), (b, mb, _) = _pair()
+    ob = FlatAdamW(mb, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.01)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    xs = [torch.randn(16, 96, device=DEV, generator=g) for _ in range(4)]
+    for x in xs[:2]:
+        _backward(a, ma, x)
+        ma.clip_grad_norm_(1.0)
+        oa.step()
+        ma.after_step()
+    sd = _copy.deepcopy(oa.state_dict())
+    for (fb, _), (fa, _) in zip(mb.flat_buckets(), ma.flat_buckets(), strict=True):
+        fb.copy_(fa)  # the model checkpoint: masters (and the bf16 weights derived from them)
+    mb.after_step()
+    ob.load_state_dict(sd)
+    assert float(ob._step) == 2.0
+    for x in xs[2:]:
+        for model, man, opt in ((a, ma, oa), (b, mb, ob)):
+            _backward(model, man, x)
+            man.clip_grad_norm_(1.0)
+            opt.step()
+            man.after_step()
+    for (fa, _), (fb, _) in zip(ma.flat_buckets(), mb.flat_buckets(), strict=True):
+        assert torch.equal(fa, fb)
+    for ma_, mb_ in zip(oa._m + oa._v, ob._m + ob._v, strict=True):
+        assert torch.equal(ma_, mb_)

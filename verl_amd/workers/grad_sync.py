@@ -543,13 +543,36 @@ class FlatAdamW(torch.optim.Optimizer):
         self._m = [torch.zeros_like(mf) for mf, _ in self._flat]
         self._v = [torch.zeros_like(mf) for mf, _ in self._flat]
         self._step = torch.zeros((), dtype=torch.float32, device=self._flat[0][0].device)
+        self._bind_state(params)
+        self.found_inf = None
+        manager.fold_clip = True
+
+    def _bind_state(self, params):
         for p in params:
-            i, off = manager.flat_index(p)
+            i, off = self.manager.flat_index(p)
             n = p.numel()
             self.state[p] = {"step": self._step, "exp_avg": self._m[i][off : off + n].view_as(p),
                              "exp_avg_sq": self._v[i][off : off + n].view_as(p)}
-        self.found_inf = None
-        manager.fold_clip = True
+
+    def load_state_dict(self, state_dict):
+        """torch.optim.Optimizer.load_state_dict, then the loaded moments and step copied into the flat
+        buffers the kernel updates (the base class would leave the state as separate tensors)."""
+        super().load_state_dict(state_dict)
+        params = self.param_groups[0]["params"]
+        step = None
+        with torch.no_grad():
+            for p in params:
+                st = self.state.get(p, {})
+                if "exp_avg" not in st:
+                    continue
+                i, off = self.manager.flat_index(p)
+                n = p.numel()
+                self._m[i][off : off + n].copy_(st["exp_avg"].reshape(-1))
+                self._v[i][off : off + n].copy_(st["exp_avg_sq"].reshape(-1))
+                step = st["step"]
+            if step is not None:
+                self._step.copy_(torch.as_tensor(step, dtype=torch.float32))
+        self._bind_state(params)
 
     @torch.no_grad()
     def step(self, closure=None):
