@@ -107,6 +107,15 @@ def test_bench_shape_o_projection_bitwise_on_exact_data():
     assert torch.equal(y, torch.nn.functional.linear(x, w))
 
 
+def test_zero_rows_is_a_no_op():
+    from verl_amd import _lib as L
+    from verl_amd import kernels as K
+
+    w = torch.ones(224, 128, dtype=torch.bfloat16, device=DEV)
+    x = torch.ones(1, 128, dtype=torch.bfloat16, device=DEV)
+    L.call("va_linear_tn", K._p(x), 128, K._p(w), 128, None, L.VA_BF16, 0, 224, 128, 0, 0, None, 224, K._stream(w))
+
+
 def test_tile_query_and_argument_checks():
     from verl_amd import _lib as L
     from verl_amd import kernels as K
