@@ -181,6 +181,10 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *     (else 1); 1 = the two-buffer form, each workgroup keeping one feature tile over a range of token blocks,
  *     the workgroups of one token range side by side on one XCD; 0 = the two-buffer form over consecutive
  *     tiles of the (token block, feature tile) list (all bitwise identical).
+ *   VA_TUNE_T256_DEFER (bit flags, default 1): the 256 x 256 sweep runs a finished tile's storing
+ *     epilogue after the step's operand wait, its stores draining during the next step, for
+ *     va_gate_up_swiglu / _save (bit 1) and va_linear_logprob_bwd (bit 2); else before that wait
+ *     (bitwise identical either way).
  *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
 *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order);
  *   VA_TUNE_FLASH_DMA (va_flash_attn_fwd / _bwd): bit 1 = forward K / V blocks staged by LDS-DMA
@@ -210,6 +214,7 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
 #define VA_TUNE_ADAMW_MATH 22
 #define VA_TUNE_WGRAD_KIND 23
 #define VA_TUNE_LINEAR_TN 24
+#define VA_TUNE_T256_DEFER 25
 int va_set_tuning(int key, int value);
 
 /* ---------------------------------------------------------------------------------------

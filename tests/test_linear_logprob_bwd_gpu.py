@@ -79,3 +79,38 @@ def test_vocab_range_dlogits_equal_the_whole_vocab_launch(N, H, V, bounds, T):
         part = torch.full((N, v1 - v0 + 8), 7.0, dtype=torch.bfloat16, device=DEV)[:, : v1 - v0]
         K._linear_logprob_bwd_raw(h, w, labels, lse, ent, g1, g2, T, False, part, v0, v1)
         assert torch.equal(torch.nan_to_num(part), torch.nan_to_num(want[:, v0:v1])), (v0, v1)
+
+
+@pytest.mark.parametrize("defer", [0, 2])
+@pytest.mark.parametrize("N,H,V,ldd", [(300, 896, 151936, 151936), (77, 128, 1000, 1008), (513, 64, 2048, 2052)])
+def test_dlogits_epilogue_placement_bitwise(defer, N, H, V, ldd):
+    """VA_TUNE_T256_DEFER bit 2: the dlogits tile epilogue before or after the step's operand wait
+    (16-byte rows through the scratch, and 8-byte stores when ldd % 8 != 0) writes the unfused
+    composition's dlogits bit for bit on exact data."""
+    from verl_amd import _lib as L
+    from verl_amd import kernels as K
+
+    h, w = _exact_inputs(N, H, V, seed=N + V + ldd)
+    g = torch.Generator().manual_seed(N)
+    labels = torch.randint(0, V, (N,), generator=g)
+    labels[0] = -100
+    logits = (h.float() @ w.float().t()).to(torch.bfloat16).to(DEV)
+    h, w, labels = h.to(DEV), w.to(DEV), labels.to(DEV)
+    _, ent, lse = torch.ops.verl_amd.logprob_entropy_fwd(logits, labels, 1.0, 0)
+    g1, g2 = torch.randn(N, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV)
+    want = torch.ops.verl_amd.logprob_entropy_bwd(g1, g2, logits, labels, lse, ent, 1.0)
+    got = torch.full((N, ldd), 7.0, dtype=torch.bfloat16, device=DEV)
+    try:
+        L.call("va_set_tuning", L.VA_TUNE_T256_DEFER, defer)
+        K._linear_logprob_bwd_raw(h, w, labels, lse, ent, g1, g2, 1.0, False, got[:, :V])
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_T256_DEFER, 1)
+    assert torch.equal(torch.nan_to_num(got[:, :V]), torch.nan_to_num(want))
+    assert (got[:, V:].float() == 7.0).all()
+
+
+def test_epilogue_placement_key_range():
+    from verl_amd import _lib as L
+
+    with pytest.raises(RuntimeError, match="VA_TUNE_T256_DEFER"):
+        L.call("va_set_tuning", L.VA_TUNE_T256_DEFER, 4)

@@ -371,6 +371,27 @@ def test_gate_up_swiglu_save_bitwise_on_exact_data(T, H, F_, ldx):
     assert torch.equal(y, y_want)
 
 
+@pytest.mark.parametrize("defer", [0, 1])
+@pytest.mark.parametrize("T,H,F_,splits", [(1000, 896, 4864, None), (517, 256, 512, 3), (3, 128, 256, 64)])
+def test_gate_up_swiglu_epilogue_placement_bitwise(defer, T, H, F_, splits):
+    """VA_TUNE_T256_DEFER bit 1: the tile epilogue before or after the step's operand wait writes the
+    same y and projection, equal to GEMM + swiglu_merged on exact data."""
+    from verl_amd import _lib as L
+    from verl_amd import kernels as K
+
+    x, w = _exact_operands(T, H, F_, None, seed=5 * T + F_)
+    try:
+        L.call("va_set_tuning", L.VA_TUNE_T256_DEFER, defer)
+        with torch.no_grad():
+            gu_want = x @ w.t()
+            y_want = K.swiglu_merged(gu_want)
+            y, gu = K._gate_up_swiglu_raw(x, w, splits, save=True)
+            y2, _ = K._gate_up_swiglu_raw(x, w, splits, save=False)
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_T256_DEFER, 1)
+    assert torch.equal(gu, gu_want) and torch.equal(y, y_want) and torch.equal(y2, y_want)
+
+
 @pytest.mark.parametrize("T,H,F_", [(1000, 896, 4864), (300, 128, 256)])
 def test_fused_mlp_train_forward_backward_bitwise_on_exact_data(T, H, F_):
     """gate_up_swiglu_train (fused_mlp_train): the activation and the gradients of x and of the gate /

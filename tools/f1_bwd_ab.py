@@ -43,8 +43,14 @@ def main():
     ap.add_argument("--skip-kernel", action="store_true", help="pass level only")
     ap.add_argument("--breakdown", action="store_true",
                     help="also time each component of both passes (HIP events between the launches)")
+    ap.add_argument("--tune", action="append", default=[], help="KEY=VALUE for va_set_tuning (A/B runs)")
     args = ap.parse_args()
+    from verl_amd import _lib as L
     from verl_amd import kernels as K
+
+    for kv in args.tune:
+        key, val = (int(x) for x in kv.split("="))
+        L.call("va_set_tuning", key, val)
 
     dev = torch.device("cuda", 0)
     H, V, N = 896, 151936, args.rows
@@ -53,7 +59,7 @@ def main():
     h = torch.randn(N, H, device=dev, generator=g).to(torch.bfloat16)
     lab = torch.randint(0, V, (N,), device=dev, generator=g)
     g1 = torch.randn(N, device=dev, generator=g)
-    out = {"rows": N, "H": H, "V": V}
+    out = {"rows": N, "H": H, "V": V, "tune": args.tune}
     with torch.no_grad():
         _, ent, lse = torch.ops.verl_amd.logprob_entropy_fwd(h @ w.t(), lab, 1.0, 0)
     flops = 2.0 * N * V * H

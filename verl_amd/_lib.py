@@ -36,7 +36,7 @@ VA_TUNE_FLASH_DKDV_QT, VA_TUNE_FLASH_DQ_KB, VA_TUNE_FLASH_FWD_KB, VA_TUNE_GAE_PA
 VA_TUNE_GAE_NT, VA_TUNE_LOSS_VEC = 13, 14
 VA_TUNE_WHITEN_SLICE_MIN, VA_TUNE_WHITEN_GRID, VA_TUNE_LINEAR_LOGPROB_TILE = 15, 16, 17
 VA_TUNE_WGRAD_REMAINDER, VA_TUNE_FLASH_DMA, VA_TUNE_WGRAD_MFMA, VA_TUNE_WGRAD_TILES = 18, 19, 20, 21
-VA_TUNE_ADAMW_MATH, VA_TUNE_WGRAD_KIND, VA_TUNE_LINEAR_TN = 22, 23, 24
+VA_TUNE_ADAMW_MATH, VA_TUNE_WGRAD_KIND, VA_TUNE_LINEAR_TN, VA_TUNE_T256_DEFER = 22, 23, 24, 25
 # the library's compiled-in flash-attention staging defaults (csrc/attention.hip), for code that
 # changes a setting and restores it
 FLASH_TUNING_DEFAULTS = {VA_TUNE_FLASH_DMA: 7, VA_TUNE_FLASH_DQ_KB: 64, VA_TUNE_FLASH_DKDV_QT: 64,

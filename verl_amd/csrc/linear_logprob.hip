@@ -399,7 +399,10 @@ struct FwdEpilogue {
 // Staging addresses: each lane's 4 hidden rows (clamped at N) and its 4 weight-image rows' offsets
 // within a tile are fixed for the sweep and computed once; per K-step only the scalar tile / chunk
 // base moves (in the last vocab tile, rows past V select row V - 1's address instead).
-template <typename Tile, typename WMap = IdentityRows>
+// DEFER (epilogues that store, VA_TUNE_T256_DEFER): tile() runs after the step's wait + barrier
+// instead of before, so its global stores are in flight during the next step's MFMAs and drain at
+// that step's wait, instead of the wait for the next step's operands also waiting for them.
+template <bool DEFER = false, typename Tile, typename WMap = IdentityRows>
 __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int64_t ldh,
                                            const uint16_t *__restrict__ w, int64_t ldw, int64_t N, int K, int64_t V,
                                            int64_t row0, int64_t vt_begin, int64_t vt_end, uint16_t *lds, int wave,
@@ -484,19 +487,24 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    if (kt == nk - 1) {
+    const bool fin = kt == nk - 1;
+    auto finish = [&] {
       tile(acc, vt);
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    if (!DEFER && fin) finish();
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (DEFER && fin) finish();
+    if (fin) {
       kt = 0;
       ++vt;
     } else {
       ++kt;
     }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
   }
 }
 
@@ -643,7 +651,7 @@ __global__ __launch_bounds__(256) void linear_logprob_merge_kernel(const float *
 // WIDE (dlogits 16-byte aligned, ldd % 8 == 0): the stores go through a wave-private LDS scratch as
 // whole row segments (8 lanes x 16 B per token row, 64 vocab columns at a time), as the fused SwiGLU's;
 // otherwise each lane stores its 4 columns (8 B) directly.
-template <bool SCALE, bool ROUND, bool REMAP, bool WIDE>
+template <bool SCALE, bool ROUND, bool REMAP, bool WIDE, bool DEFER>
 __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
     const uint16_t *__restrict__ hid, int64_t ldh, const uint16_t *__restrict__ w, int64_t ldw,
     const int64_t *__restrict__ labels, const float *__restrict__ lse_in, const float *__restrict__ ent_in,
@@ -693,7 +701,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
       }
     }
   };
-  t256_sweep(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
+  t256_sweep<DEFER>(hid, ldh, w, ldw, N, K, V, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
     const int v0 = static_cast<int>(vt * TB) + wr * 128 + (lane >> 4) * 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -757,7 +765,7 @@ struct GateUpRows {
 // SAVE: also store the projection's g / u (bf16, as the merged GEMM writes them) into gu [T, 2F] for
 // the training forward, whose SwiGLU backward needs them: the GEMM + swiglu_fwd pair without the
 // swiglu_fwd's re-read of the projection.
-template <bool REMAP, bool SAVE>
+template <bool REMAP, bool SAVE, bool DEFER>
 __global__ __launch_bounds__(T_THREADS, 1) void gate_up_swiglu_t256_kernel(
     const uint16_t *__restrict__ x, int64_t ldx, const uint16_t *__restrict__ w, int64_t ldw, int64_t T, int K,
     int64_t F, int splits, int tiles_per_split, uint16_t *__restrict__ y, int64_t ldy, uint16_t *__restrict__ gu,
@@ -787,7 +795,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void gate_up_swiglu_t256_kernel(
       if (t < T) *reinterpret_cast<uint4 *>(out + t * ld + col0 + (lane & 7) * 8) = v;
     }
   };
-  t256_sweep(
+  t256_sweep<DEFER>(
       x, ldx, w, ldw, T, K, 2 * F, row0, vt_begin, vt_end, lds, wave, lane,
       [&](f32x4(&acc)[8][4], int64_t vt) {
         const int64_t c0 = vt * 128 + wr * 64;  // this wave's 64 output features
@@ -917,6 +925,11 @@ using namespace va;
 // va_set_tuning(VA_TUNE_LINEAR_LOGPROB_TILE): 128 (the 128 x 128 register-staged kernel) or 256
 // (the 256 x 256 LDS-DMA kernel above)
 int g_linear_logprob_tile = 256;
+// va_set_tuning(VA_TUNE_T256_DEFER): bit 1 = the gate|up + SwiGLU sweeps, bit 2 = the fused backward's
+// dlogits sweep run their tile epilogue after the step's wait (t256_sweep DEFER), else before it.
+// Default 1: gate|up 2.47 vs 2.52 ms (save form 2.80 vs 2.89) at 151,552 tokens, the dlogits sweep
+// 38.5 vs 38.0 ms at 131,072 rows (profiles/r06/al/)
+int g_t256_defer = 1;
 
 template <bool SC, bool RD>
 static void launch_t256(bool remap, dim3 grid, hipStream_t s, const uint16_t *h16, int64_t ldh, const uint16_t *w16,
@@ -1002,10 +1015,13 @@ static void launch_bwd_t256(bool remap, dim3 grid, hipStream_t s, const uint16_t
                             int64_t V, int64_t V_full, int64_t vbase, int used, int per, float temperature,
                             uint16_t *dlog, int64_t ldd) {
   const bool wide = ldd % 8 == 0 && reinterpret_cast<uintptr_t>(dlog) % 16 == 0;
-  const auto kern = remap ? (wide ? linear_logprob_bwd_t256_kernel<SC, RD, true, true>
-                                  : linear_logprob_bwd_t256_kernel<SC, RD, true, false>)
-                          : (wide ? linear_logprob_bwd_t256_kernel<SC, RD, false, true>
-                                  : linear_logprob_bwd_t256_kernel<SC, RD, false, false>);
+  const bool defer = (g_t256_defer & 2) != 0;
+  const auto kern = remap ? (wide ? (defer ? linear_logprob_bwd_t256_kernel<SC, RD, true, true, true>
+                                           : linear_logprob_bwd_t256_kernel<SC, RD, true, true, false>)
+                                  : linear_logprob_bwd_t256_kernel<SC, RD, true, false, false>)
+                          : (wide ? (defer ? linear_logprob_bwd_t256_kernel<SC, RD, false, true, true>
+                                           : linear_logprob_bwd_t256_kernel<SC, RD, false, true, false>)
+                                  : linear_logprob_bwd_t256_kernel<SC, RD, false, false, false>);
   hipLaunchKernelGGL(kern, grid, dim3(T_THREADS), 0, s, h16, ldh, w16, ldw, labels, lse, ent, g_logp, g_ent, N,
                      static_cast<int>(H), V, V_full, vbase, used, per, temperature, dlog, ldd);
 }
@@ -1091,9 +1107,13 @@ static int gate_up_swiglu_impl(const void *x, int64_t ldx, const void *w_gate_up
   auto *y16 = static_cast<uint16_t *>(y);
   auto *g16 = static_cast<uint16_t *>(gu);
   const bool remap = nwg % 8 == 0;
-  const auto kern = gu != nullptr ? (remap ? gate_up_swiglu_t256_kernel<true, true> : gate_up_swiglu_t256_kernel<false, true>)
-                                  : (remap ? gate_up_swiglu_t256_kernel<true, false>
-                                           : gate_up_swiglu_t256_kernel<false, false>);
+  const bool defer = (g_t256_defer & 1) != 0;
+  const auto kern =
+      gu != nullptr
+          ? (remap ? (defer ? gate_up_swiglu_t256_kernel<true, true, true> : gate_up_swiglu_t256_kernel<true, true, false>)
+                   : (defer ? gate_up_swiglu_t256_kernel<false, true, true> : gate_up_swiglu_t256_kernel<false, true, false>))
+          : (remap ? (defer ? gate_up_swiglu_t256_kernel<true, false, true> : gate_up_swiglu_t256_kernel<true, false, false>)
+                   : (defer ? gate_up_swiglu_t256_kernel<false, false, true> : gate_up_swiglu_t256_kernel<false, false, false>));
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nwg)), dim3(T_THREADS), 0, s, x16, ldx, w16, ldw, T,
                      static_cast<int>(H), F, used, per, y16, ldy, g16, ldgu);
   return check_launch("gate_up_swiglu");

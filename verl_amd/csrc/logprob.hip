@@ -720,6 +720,7 @@ extern int g_wgrad_tiles;          // wgrad.hip
 extern int g_adamw_math;           // optim.hip
 extern int g_wgrad_kind;           // wgrad.hip
 extern int g_linear_tn;            // gemm_tn.hip
+extern int g_t256_defer;           // linear_logprob.hip
 extern int g_whiten_grid;         // advantage.hip
 extern int g_swiglu_variant;      // model_ops.hip
 extern int g_flash_dkdv_qt;       // attention.hip
@@ -758,6 +759,13 @@ extern "C" int va_set_tuning(int key, int value) {
         return VA_E_ARG;
       }
       g_wgrad_kind = value;
+      return VA_OK;
+    case VA_TUNE_T256_DEFER:
+      if (value < 0 || value > 3) {
+        va::set_error("va_set_tuning: VA_TUNE_T256_DEFER must be 0 .. 3");
+        return VA_E_ARG;
+      }
+      g_t256_defer = value;
       return VA_OK;
     case VA_TUNE_LINEAR_TN:
       if (value < 0 || value > 2) {
