@@ -183,8 +183,8 @@ int va_logprob_entropy_bwd(const float *g_logp, const float *g_entropy, const vo
  *     tiles of the (token block, feature tile) list (all bitwise identical).
  *   VA_TUNE_T256_DEFER (bit flags, default 1): the 256 x 256 sweep runs a finished tile's storing
  *     epilogue after the step's operand wait, its stores draining during the next step, for
- *     va_gate_up_swiglu / _save (bit 1) and va_linear_logprob_bwd (bit 2); else before that wait
- *     (bitwise identical either way).
+ *     va_gate_up_swiglu / _save (bit 1), va_linear_logprob_bwd (bit 2) and va_qkv_rope (bit 4); else
+ *     before that wait (bitwise identical either way).
  *   VA_TUNE_LINEAR_LOGPROB_TILE (va_linear_logprob_fwd): 256 (default) = 256 x 256 LDS-DMA tiles,
 *   8 waves; 128 = the 128 x 128 register-staged kernel (same results up to fp32 merge order);
  *   VA_TUNE_FLASH_DMA (va_flash_attn_fwd / _bwd): bit 1 = forward K / V blocks staged by LDS-DMA

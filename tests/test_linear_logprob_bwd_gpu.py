@@ -113,4 +113,4 @@ def test_epilogue_placement_key_range():
     from verl_amd import _lib as L
 
     with pytest.raises(RuntimeError, match="VA_TUNE_T256_DEFER"):
-        L.call("va_set_tuning", L.VA_TUNE_T256_DEFER, 4)
+        L.call("va_set_tuning", L.VA_TUNE_T256_DEFER, 8)

@@ -434,17 +434,23 @@ def _qkv_case(T, H, hq, hk, seed, bias=True):
     return x, w, b, emb.cos().to(torch.bfloat16)[None], emb.sin().to(torch.bfloat16)[None]
 
 
+@pytest.mark.parametrize("defer", [1, 5])  # VA_TUNE_T256_DEFER bit 4: the epilogue after the operand wait
 @pytest.mark.parametrize("T,H,hq,hk,bias", [(1000, 896, 14, 2, True), (300, 128, 4, 2, True), (37, 64, 2, 1, False),
                                             (2048, 896, 14, 2, True)])
-def test_qkv_rope_bitwise_on_exact_data(T, H, hq, hk, bias):
+def test_qkv_rope_bitwise_on_exact_data(defer, T, H, hq, hk, bias):
     """va_qkv_rope (ABI 9) == merged q|k|v GEMM with bias (hipBLASLt) + rope_qkv, bit for bit, on exact
     projections: q / k rotated, v passed through, ragged token tails, a last tile half past the heads."""
+    from verl_amd import _lib as L
     from verl_amd import kernels as K
 
     x, w, b, cos, sin = _qkv_case(T, H, hq, hk, seed=T + hq)
-    with torch.no_grad():
-        want = K.rope_qkv(torch.nn.functional.linear(x, w, b), cos, sin, hq, hk, 64)
-        got = K.qkv_rope(x, w, b, cos, sin, hq, hk, 64, [w], [b] if bias else None)
+    try:
+        L.call("va_set_tuning", L.VA_TUNE_T256_DEFER, defer)
+        with torch.no_grad():
+            want = K.rope_qkv(torch.nn.functional.linear(x, w, b), cos, sin, hq, hk, 64)
+            got = K.qkv_rope(x, w, b, cos, sin, hq, hk, 64, [w], [b] if bias else None)
+    finally:
+        L.call("va_set_tuning", L.VA_TUNE_T256_DEFER, 1)
     for a, e, what in zip(got, want, "qkv"):
         assert torch.equal(a, e), what
 

@@ -833,7 +833,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void gate_up_swiglu_t256_kernel(
 // RoPE is lane-local; per element the arithmetic of F.linear's bias epilogue (bf16(acc + b)) and of
 // rope_qkv_fwd (model_ops.hip: bf16 after each product, then the sum rounded). Stores through the
 // wave-private LDS scratch as whole 128-B head rows. cos / sin [T, D] bf16 (row stride D).
-template <bool REMAP>
+template <bool REMAP, bool DEFER>
 __global__ __launch_bounds__(T_THREADS, 1) void qkv_rope_t256_kernel(
     const uint16_t *__restrict__ x, int64_t ldx, const uint16_t *__restrict__ w, int64_t ldw,
     const uint16_t *__restrict__ bias, const uint16_t *__restrict__ cs, const uint16_t *__restrict__ sn, int64_t T,
@@ -866,7 +866,7 @@ __global__ __launch_bounds__(T_THREADS, 1) void qkv_rope_t256_kernel(
   auto lo = [](uint32_t u) { return __uint_as_float(u << 16); };
   auto hi = [](uint32_t u) { return __uint_as_float(u & 0xffff0000u); };
   auto el = [&](const uint2 &u, int e) { return e == 0 ? lo(u.x) : e == 1 ? hi(u.x) : e == 2 ? lo(u.y) : hi(u.y); };
-  t256_sweep(x, ldx, w, ldw, T, K, NF, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
+  t256_sweep<DEFER>(x, ldx, w, ldw, T, K, NF, row0, vt_begin, vt_end, lds, wave, lane, [&](f32x4(&acc)[8][4], int64_t vt) {
     const int hb = static_cast<int>(vt * 4) + wr * 2;  // this wave-row's two heads
     uint2 bb[8];  // bias of features 16 i + g4 + 0..3 of the two heads (packed bf16)
 #pragma unroll
@@ -926,7 +926,8 @@ using namespace va;
 // (the 256 x 256 LDS-DMA kernel above)
 int g_linear_logprob_tile = 256;
 // va_set_tuning(VA_TUNE_T256_DEFER): bit 1 = the gate|up + SwiGLU sweeps, bit 2 = the fused backward's
-// dlogits sweep run their tile epilogue after the step's wait (t256_sweep DEFER), else before it.
+// dlogits sweep, bit 4 = the q|k|v + RoPE sweep run their tile epilogue after the step's wait
+// (t256_sweep DEFER), else before it.
 // Default 1: gate|up 2.47 vs 2.52 ms (save form 2.80 vs 2.89) at 151,552 tokens, the dlogits sweep
 // 38.5 vs 38.0 ms at 131,072 rows (profiles/r06/al/)
 int g_t256_defer = 1;
@@ -1155,7 +1156,9 @@ extern "C" int va_qkv_rope(const void *x, int64_t ldx, const void *w_qkv, int64_
   const int64_t nwg = ((T + TB - 1) / TB) * used;
   VA_CHECK_ARG(nwg < (int64_t{1} << 31), "qkv_rope: grid too large");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const auto kern = nwg % 8 == 0 ? qkv_rope_t256_kernel<true> : qkv_rope_t256_kernel<false>;
+  const bool defer = (g_t256_defer & 4) != 0;
+  const auto kern = nwg % 8 == 0 ? (defer ? qkv_rope_t256_kernel<true, true> : qkv_rope_t256_kernel<true, false>)
+                                 : (defer ? qkv_rope_t256_kernel<false, true> : qkv_rope_t256_kernel<false, false>);
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(nwg)), dim3(T_THREADS), 0, s, static_cast<const uint16_t *>(x),
                      ldx, static_cast<const uint16_t *>(w_qkv), ldw, static_cast<const uint16_t *>(bias),
                      static_cast<const uint16_t *>(cos), static_cast<const uint16_t *>(sin), T, static_cast<int>(H), Hq,

@@ -761,8 +761,8 @@ extern "C" int va_set_tuning(int key, int value) {
       g_wgrad_kind = value;
       return VA_OK;
     case VA_TUNE_T256_DEFER:
-      if (value < 0 || value > 3) {
-        va::set_error("va_set_tuning: VA_TUNE_T256_DEFER must be 0 .. 3");
+      if (value < 0 || value > 7) {
+        va::set_error("va_set_tuning: VA_TUNE_T256_DEFER must be 0 .. 7");
         return VA_E_ARG;
       }
       g_t256_defer = value;
