@@ -23,6 +23,8 @@
 
 #include <math.h>
 
+#include <type_traits>
+
 #include "va_common.h"
 
 namespace va {
@@ -442,10 +444,6 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
       __builtin_amdgcn_raw_ptr_buffer_load_lds(hres, img + T_TILE + ldsoff[i], 16, hoff[i], kb, 0, 0);
   };
   f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (nsteps > 0) stage(vt_begin, 0, lds);
   __builtin_amdgcn_s_waitcnt(0);
@@ -458,47 +456,49 @@ __device__ __forceinline__ void t256_sweep(const uint16_t *__restrict__ hid, int
     const int buf = static_cast<int>(st & 1);
     const uint16_t *la = lds + buf * 2 * T_TILE;
     const uint16_t *lb = la + T_TILE;
+    // FIRST (a tile's first K-step): the first K-half's MFMAs start from a zero accumulator operand
+    // instead of acc, so a finished tile needs no 128 v_mov to clear acc (round 6)
+    auto kstep = [&](auto first) {
+      constexpr bool FIRST = decltype(first)::value;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      // the next step's images, issued between the two K-halves: hipcc then spreads the address, M0
-      // and DMA issue over the second half's MFMAs instead of running them ahead of the first (30.1 vs
-      // 31.5 ms issued before the step's MFMAs, f1_stage_at_ab.jsonl); the last step re-stages a valid
-      // tile into the free buffer, unread
-      if (q == 1) {
-        const bool last = kt + 1 == nk;
-        int64_t vs = last ? vt + 1 : vt;
-        if (vs >= vt_end) vs = vt_end - 1;
-        stage(vs, last ? 0 : kt + 1, lds + (buf ^ 1) * 2 * T_TILE);
+      for (int q = 0; q < 2; ++q) {
+        // the next step's images, issued between the two K-halves: hipcc then spreads the address, M0
+        // and DMA issue over the second half's MFMAs instead of running them ahead of the first (30.1
+        // vs 31.5 ms issued before the step's MFMAs, f1_stage_at_ab.jsonl); the last step re-stages a
+        // valid tile into the free buffer, unread
+        if (q == 1) {
+          const bool last = kt + 1 == nk;
+          int64_t vs = last ? vt + 1 : vt;
+          if (vs >= vt_end) vs = vt_end - 1;
+          stage(vs, last ? 0 : kt + 1, lds + (buf ^ 1) * 2 * T_TILE);
+        }
+        const int c = q * 4 + (lane >> 4);
+        auto frag_a = [&](int i) {
+          return *reinterpret_cast<const bf16x8 *>(la + t_img_off(wr * 128 + i * 16 + (lane & 15), c));
+        };
+        auto frag_b = [&](int j) {
+          return *reinterpret_cast<const bf16x8 *>(lb + t_img_off(wc * 64 + j * 16 + (lane & 15), c));
+        };
+        bf16x8 fa[8], fb[4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) fa[i] = frag_a(i);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = frag_b(j);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                fa[i], fb[j], (FIRST && q == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j], 0, 0, 0);
       }
-      const int c = q * 4 + (lane >> 4);
-      auto frag_a = [&](int i) {
-        return *reinterpret_cast<const bf16x8 *>(la + t_img_off(wr * 128 + i * 16 + (lane & 15), c));
-      };
-      auto frag_b = [&](int j) {
-        return *reinterpret_cast<const bf16x8 *>(lb + t_img_off(wc * 64 + j * 16 + (lane & 15), c));
-      };
-      bf16x8 fa[8], fb[4];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) fa[i] = frag_a(i);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = frag_b(j);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
-    const bool fin = kt == nk - 1;
-    auto finish = [&] {
-      tile(acc, vt);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    if (!DEFER && fin) finish();
+    if (kt == 0) kstep(std::true_type{});
+    else kstep(std::false_type{});
+    const bool fin = kt == nk - 1;
+    if (!DEFER && fin) tile(acc, vt);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    if (DEFER && fin) finish();
+    if (DEFER && fin) tile(acc, vt);
     if (fin) {
       kt = 0;
       ++vt;
@@ -749,6 +749,23 @@ __global__ __launch_bounds__(T_THREADS, 1) void linear_logprob_bwd_t256_kernel(
 // are the gate and up of one (feature, token) in one lane: the epilogue is elementwise, each lane
 // storing 4 consecutive features of a token (8 bytes) per (i, j). Per element the arithmetic of
 // swiglu_fwd (model_ops.hip), so on exact-arithmetic data the output equals GEMM + swiglu bitwise.
+// bf16(bf16(silu(bf16 g)) * bf16 u) for two (g, u) pairs: va_silu's operations (v_mul by -log2 e,
+// v_exp_f32, + 1, v_rcp_f32, * g) with the multiplies / adds in packed fp32 and each pair rounded to
+// bf16 by one v_cvt_pk_bf16_f32 (the same IEEE results as the scalar form swiglu_fwd uses, ~30 % fewer
+// VALU issues in an epilogue that runs while the MFMA pipe idles)
+__device__ __forceinline__ va_f32x2 unpack2_bf16(uint32_t p) {
+  return va_f32x2{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+}
+__device__ __forceinline__ va_f32x2 swiglu_pair(float g0, float g1, float u0, float u1) {
+  const va_f32x2 g = unpack2_bf16(pack2_bf16(g0, g1));
+  const va_f32x2 u = unpack2_bf16(pack2_bf16(u0, u1));
+  const va_f32x2 a = g * va_f32x2{-kLog2eF, -kLog2eF};
+  const va_f32x2 d = va_f32x2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)} + va_f32x2{1.f, 1.f};
+  const va_f32x2 sg = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  const va_f32x2 sl = g * sg;
+  return unpack2_bf16(pack2_bf16(sl.x, sl.y)) * u;
+}
+
 struct GateUpRows {
   static constexpr int64_t kTileStep = 128;
   int64_t F;
@@ -803,11 +820,9 @@ __global__ __launch_bounds__(T_THREADS, 1) void gate_up_swiglu_t256_kernel(
         for (int j = 0; j < 4; ++j) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              o[e] = round_bf16(va_silu(round_bf16(acc[i][j][e]))) * round_bf16(acc[i + 4][j][e]);
-            put(i, o[0], o[1], o[2], o[3]);
+            const va_f32x2 o01 = swiglu_pair(acc[i][j][0], acc[i][j][1], acc[i + 4][j][0], acc[i + 4][j][1]);
+            const va_f32x2 o23 = swiglu_pair(acc[i][j][2], acc[i][j][3], acc[i + 4][j][2], acc[i + 4][j][3]);
+            put(i, o01.x, o01.y, o23.x, o23.y);
           }
           flush(j, y, ldy, c0);
           if constexpr (SAVE) {
