@@ -70,7 +70,14 @@ def pmc_traffic_f1(flops_per_launch: float):
     (tools/f1_pmc.sh: FETCH_SIZE x2 + WRITE_SIZE) when they were taken at this launch's shape."""
     import glob
 
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_f1_product.json")), reverse=True):
+    def newest_first(path):  # profiles/r<NN>[/<pass>]/pmc_f1_product.json: latest round, then latest pass
+        parts = os.path.relpath(path, os.path.join(ROOT, "profiles")).split(os.sep)[:-1]
+        tag = parts[1] if len(parts) > 1 else ""
+        return (parts[0], len(tag), tag)
+
+    paths = glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_f1_product.json")) + glob.glob(
+        os.path.join(ROOT, "profiles", "r*", "*", "pmc_f1_product.json"))
+    for p in sorted(paths, key=newest_first, reverse=True):
         d = json.load(open(p))
         n, h, v = d["shape"]
         if abs(2.0 * n * v * h - flops_per_launch) <= 1e-6 * flops_per_launch:
