@@ -165,12 +165,15 @@ __global__ __launch_bounds__(256, DMA ? VA_FLASH_FWD_DMA_OCC : 2) void flash_fwd
     if (!(key0 > wave_last_q || qs + wave * 32 >= len || key0 >= kv_end)) {
       const bool t1_live = key0 + 32 <= wave_last_q && key0 + 32 < len;  // second 32-key tile
       // ---- S^T = K Q^T for the block's two 32-key tiles (keys on rows, queries on lanes)
+      // both tiles always: a dead second tile (its keys past every query of the wave or past the
+      // sequence) costs 4 MFMAs on the few blocks that have one, and need_mask then holds and masks
+      // all of its scores to -inf by select below; skipping it instead cost 16 v_mov per block (its
+      // registers cleared for the skip path) in this VALU-bound loop (round 6)
       f32x16 sacc[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) sacc[t][r] = 0.f;
-        if (t == 1 && !t1_live) continue;
         const int krow = t * 32 + ql;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
